@@ -1,0 +1,618 @@
+// abi.hip — extern "C" entry points of libskyline_hip.so (include/skyline_hip.h).
+// Status codes only; no exception crosses the boundary.
+#include "ctx.h"
+
+#include <cstring>
+#include <new>
+#include <string>
+
+namespace sky {
+static thread_local std::string g_err;
+void set_error(const std::string &m) { g_err = m; }
+}  // namespace sky
+
+using namespace sky;
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #expr);   \
+            return SKY_E_HIP;                                                             \
+        }                                                                                 \
+    } while (0)
+#define SKY_TRY(expr)                \
+    do {                             \
+        int r_ = (expr);             \
+        if (r_ != SKY_OK) return r_; \
+    } while (0)
+#define ARG_CHECK(cond, msg)          \
+    do {                              \
+        if (!(cond)) {                \
+            set_error(msg);           \
+            return SKY_E_ARG;         \
+        }                             \
+    } while (0)
+#define GUARD_BEGIN try {
+#define GUARD_END                                             \
+    }                                                         \
+    catch (const std::bad_alloc &) {                          \
+        set_error("host allocation failed");                  \
+        return SKY_E_NOMEM;                                   \
+    }                                                         \
+    catch (...) {                                             \
+        set_error("internal error");                          \
+        return SKY_E_HIP;                                     \
+    }
+
+static int bind(sky_ctx *c) {
+    HIP_TRY(hipSetDevice(c->dev));
+    return SKY_OK;
+}
+
+static void finish_profile(sky_ctx *c) {
+    if (!c->profile) return;
+    hipStreamSynchronize(c->st);
+    for (int i = 0; i < SKY_PHASES; i++) {
+        float ms = 0;
+        c->phase_ms[i] = 0;
+        if (c->pt.marked[i] && c->pt.marked[i + 1] &&
+            hipEventElapsedTime(&ms, c->pt.ev[i], c->pt.ev[i + 1]) == hipSuccess)
+            c->phase_ms[i] = ms;
+    }
+    c->ktimer_collect();
+}
+
+static void store_stats(sky_ctx *c, const Pipe &p) {
+    c->K_last = p.K;
+    c->lsz.assign(p.h_lsz.begin(), p.h_lsz.end());
+    c->surv.assign(p.h_surv.begin(), p.h_surv.end());
+    c->counters[0] = p.n;
+    c->counters[1] = p.m;
+    c->counters[2] = p.mr;
+    c->counters[3] = p.mg;
+    c->counters[4] = p.nout;
+    c->counters[5] = p.sfs_rounds;
+    c->counters[6] = p.sfs_pairs_upper;
+    c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0);
+}
+
+extern "C" {
+
+const char *sky_last_error(void) { return g_err.c_str(); }
+const char *sky_version(void) { return "skyline_hip 0.1 (gfx950)"; }
+
+int sky_ctx_create(const int *devices, int ndev, int dims, int num_partitions, int algo, double domain_max,
+                   sky_ctx **out) {
+    GUARD_BEGIN
+    ARG_CHECK(out != nullptr, "out is null");
+    *out = nullptr;
+    ARG_CHECK(dims >= 1 && dims <= SKY_MAX_DIMS, "dims must be in [1,16]");
+    ARG_CHECK(num_partitions >= 1 && num_partitions <= SKY_MAX_PARTITIONS, "num_partitions must be in [1,256]");
+    ARG_CHECK(algo >= SKY_ALGO_DIM && algo <= SKY_ALGO_ANGLE, "algo must be 0 (dim), 1 (grid) or 2 (angle)");
+    ARG_CHECK(ndev >= 0 && ndev <= 1, "one device per context (run one process per GPU)");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device visible");
+        return SKY_E_NOLIB;
+    }
+    const int dev = (ndev == 1 && devices) ? devices[0] : 0;
+    ARG_CHECK(dev >= 0 && dev < count, "device ordinal out of range");
+    sky_ctx *c = new sky_ctx();
+    c->dev = dev;
+    c->D = dims;
+    c->P = num_partitions;
+    c->algo = algo;
+    c->domain = domain_max;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        set_error("could not bind the HIP device / create a stream");
+        return SKY_E_HIP;
+    }
+    c->st = c->own;
+    *out = c;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_ctx_destroy(sky_ctx *c) {
+    if (!c) return SKY_OK;
+    hipSetDevice(c->dev);
+    hipStreamSynchronize(c->st);
+    c->ktimer_collect();
+    for (hipEvent_t e : c->event_pool) hipEventDestroy(e);
+    if (c->pt.ok) c->pt.destroy();
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+    return SKY_OK;
+}
+
+int sky_ctx_set_semantics(sky_ctx *c, int sem) {
+    ARG_CHECK(c, "ctx is null");
+    ARG_CHECK(sem == SKY_SEM_REFERENCE || sem == SKY_SEM_COMPLETE, "semantics must be 0 or 1");
+    ARG_CHECK(!(sem == SKY_SEM_COMPLETE && c->algo == SKY_ALGO_GRID && c->D > 8),
+              "complete MR-Grid semantics needs 2^dims <= 256 keys");
+    c->sem = sem;
+    return SKY_OK;
+}
+
+int sky_ctx_set_stream(sky_ctx *c, void *s) {
+    ARG_CHECK(c, "ctx is null");
+    c->st = s ? (hipStream_t)s : c->own;
+    return SKY_OK;
+}
+
+int sky_ctx_sync(sky_ctx *c) {
+    ARG_CHECK(c, "ctx is null");
+    SKY_TRY(bind(c));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+}
+
+int sky_partition_keys_dev(sky_ctx *c, const double *d_values, int64_t n, int32_t *d_keys_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || (d_values && d_keys_out)), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0xffffffffLL, "n out of range");
+    SKY_TRY(bind(c));
+    launch_keys(c->D, d_values, (uint32_t)n, c->kp(), d_keys_out, c->st);
+    HIP_TRY(hipGetLastError());
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_partition_keys(sky_ctx *c, const double *values, int64_t n, int32_t *keys_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || (values && keys_out)), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0xffffffffLL, "n out of range");
+    if (n == 0) return SKY_OK;
+    SKY_TRY(bind(c));
+    SKY_TRY(c->h_vals.ensure((size_t)n * c->D * 8));
+    SKY_TRY(c->h_keys.ensure((size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(c->h_vals.p, values, (size_t)n * c->D * 8, hipMemcpyHostToDevice, c->st));
+    launch_keys(c->D, c->h_vals.as<double>(), (uint32_t)n, c->kp(), c->h_keys.as<int32_t>(), c->st);
+    HIP_TRY(hipMemcpyAsync(keys_out, c->h_keys.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
+// ---- fused query -------------------------------------------------------------
+int sky_query_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int64_t n, int64_t *d_ids_out,
+                  int32_t *d_origin_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || d_values), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
+    SKY_TRY(bind(c));
+    if (c->profile) {
+        if (!c->pt.ok) c->pt.init();
+        c->pt.reset();
+    }
+    PipeIn in;
+    in.vals = d_values;
+    in.n = (uint32_t)n;
+    in.ids = d_ids;
+    in.global = true;
+    in.K = c->Kq();
+    c->shard_valid = false;
+    int r = pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr);
+    if (r == SKY_OK) {
+        store_stats(c, c->main);
+        r = pipe_output(*c, c->main, in, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr);
+    }
+    HIP_TRY(hipGetLastError());
+    finish_profile(c);
+    return r;
+    GUARD_END
+}
+
+int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, int64_t *ids_out, int32_t *origin_out,
+              int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || values), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
+    SKY_TRY(bind(c));
+    const size_t nn = (size_t)std::max<int64_t>(n, 1);
+    SKY_TRY(c->h_vals.ensure(nn * c->D * 8));
+    SKY_TRY(c->h_ids.ensure(nn * 8));
+    if (n) HIP_TRY(hipMemcpyAsync(c->h_vals.p, values, (size_t)n * c->D * 8, hipMemcpyHostToDevice, c->st));
+    if (n && ids) HIP_TRY(hipMemcpyAsync(c->h_ids.p, ids, (size_t)n * 8, hipMemcpyHostToDevice, c->st));
+    PipeIn in;
+    in.vals = c->h_vals.as<double>();
+    in.n = (uint32_t)n;
+    in.ids = ids ? c->h_ids.as<int64_t>() : nullptr;
+    in.global = true;
+    in.K = c->Kq();
+    c->shard_valid = false;
+    if (c->profile) {
+        if (!c->pt.ok) c->pt.init();
+        c->pt.reset();
+    }
+    SKY_TRY(pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr));
+    store_stats(c, c->main);
+    const int64_t g = c->main.nout;
+    if (n_out) *n_out = g;
+    if (g > cap && (ids_out || origin_out)) {
+        set_error("output capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    SKY_TRY(c->h_out_ids.ensure((size_t)std::max<int64_t>(g, 1) * 8));
+    SKY_TRY(c->h_out_org.ensure((size_t)std::max<int64_t>(g, 1) * 4));
+    SKY_TRY(pipe_output(*c, c->main, in, false, c->h_out_ids.as<int64_t>(), c->h_out_org.as<int32_t>(), nullptr,
+                        std::max<int64_t>(g, 0), nullptr, nullptr));
+    if (g && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->h_out_ids.p, (size_t)g * 8, hipMemcpyDeviceToHost, c->st));
+    if (g && origin_out)
+        HIP_TRY(hipMemcpyAsync(origin_out, c->h_out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    finish_profile(c);
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_global_stats(sky_ctx *c, int64_t *local_sizes, int64_t *survivors, int32_t *k_out) {
+    ARG_CHECK(c, "ctx is null");
+    if (k_out) *k_out = c->K_last;
+    for (int k = 0; k < c->K_last; k++) {
+        if (local_sizes) local_sizes[k] = c->lsz[k];
+        if (survivors) survivors[k] = c->surv[k];
+    }
+    return SKY_OK;
+}
+
+// ---- global merge of host lists -------------------------------------------------
+int sky_global_merge(sky_ctx *c, int nparts, const int32_t *part_ids, const int64_t *const *ids,
+                     const double *const *values, const int64_t *counts, int64_t *ids_out, int32_t *origin_out,
+                     int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && nparts >= 0 && nparts <= SKY_MAX_PARTITIONS, "bad nparts (<= 256 lists)");
+    ARG_CHECK(nparts == 0 || (counts && values), "null argument");
+    SKY_TRY(bind(c));
+    int64_t n = 0;
+    for (int k = 0; k < nparts; k++) {
+        ARG_CHECK(counts[k] >= 0, "negative count");
+        ARG_CHECK(counts[k] == 0 || values[k], "null values list");
+        n += counts[k];
+    }
+    ARG_CHECK(n < (int64_t)0x7fffffffLL, "too many tuples");
+    const size_t nn = (size_t)std::max<int64_t>(n, 1);
+    SKY_TRY(c->h_vals.ensure(nn * c->D * 8));
+    SKY_TRY(c->h_ids.ensure(nn * 8));
+    SKY_TRY(c->h_origin.ensure(nn * 4));
+    std::vector<int32_t> org((size_t)n);
+    int64_t off = 0;
+    for (int k = 0; k < nparts; k++) {
+        if (counts[k] == 0) continue;
+        HIP_TRY(hipMemcpyAsync(c->h_vals.as<double>() + off * c->D, values[k], (size_t)counts[k] * c->D * 8,
+                               hipMemcpyHostToDevice, c->st));
+        if (ids && ids[k]) {
+            HIP_TRY(hipMemcpyAsync(c->h_ids.as<int64_t>() + off, ids[k], (size_t)counts[k] * 8, hipMemcpyHostToDevice,
+                                   c->st));
+        } else {
+            std::vector<int64_t> seq((size_t)counts[k]);
+            for (int64_t j = 0; j < counts[k]; j++) seq[j] = j;
+            HIP_TRY(hipMemcpy(c->h_ids.as<int64_t>() + off, seq.data(), (size_t)counts[k] * 8, hipMemcpyHostToDevice));
+        }
+        for (int64_t j = 0; j < counts[k]; j++) org[off + j] = k;
+        off += counts[k];
+    }
+    if (n) HIP_TRY(hipMemcpyAsync(c->h_origin.p, org.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->st));
+    PipeIn in;
+    in.vals = c->h_vals.as<double>();
+    in.n = (uint32_t)n;
+    in.ids = c->h_ids.as<int64_t>();
+    in.origin = c->h_origin.as<int32_t>();
+    in.single = true;
+    in.global = false;
+    in.K = std::max(nparts, 1);
+    c->shard_valid = false;
+    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
+    // GlobalSkylineAggregator: localSkylineSizes[k] = incoming list size (:544);
+    // survivors by originPartition (:593-596)
+    c->K_last = nparts;
+    c->lsz.assign(nparts, 0);
+    c->surv.assign(nparts, 0);
+    for (int k = 0; k < nparts; k++) {
+        c->lsz[k] = counts[k];
+        c->surv[k] = (int64_t)c->main.h_lsz[k];
+    }
+    const int64_t g = c->main.nout;
+    if (n_out) *n_out = g;
+    if (g > cap && (ids_out || origin_out)) {
+        set_error("output capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    SKY_TRY(c->h_out_ids.ensure((size_t)std::max<int64_t>(g, 1) * 8));
+    SKY_TRY(c->h_out_org.ensure((size_t)std::max<int64_t>(g, 1) * 4));
+    SKY_TRY(pipe_output(*c, c->main, in, false, c->h_out_ids.as<int64_t>(), c->h_out_org.as<int32_t>(), nullptr, g,
+                        nullptr, nullptr));
+    std::vector<int32_t> o((size_t)std::max<int64_t>(g, 1));
+    if (g && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->h_out_ids.p, (size_t)g * 8, hipMemcpyDeviceToHost, c->st));
+    if (g) HIP_TRY(hipMemcpyAsync(o.data(), c->h_out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (origin_out)
+        for (int64_t j = 0; j < g; j++) origin_out[j] = part_ids ? part_ids[o[j]] : o[j];
+    return SKY_OK;
+    GUARD_END
+}
+
+// ---- local operator state ----------------------------------------------------------
+int sky_part_open(sky_ctx *c, int32_t key, sky_part **out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && out, "null argument");
+    sky_part *p = new sky_part();
+    p->ctx = c;
+    p->key = key;
+    *out = p;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_part_close(sky_part *p) {
+    if (!p) return SKY_OK;
+    hipSetDevice(p->ctx->dev);
+    hipStreamSynchronize(p->ctx->st);
+    delete p;
+    return SKY_OK;
+}
+
+int sky_part_size(sky_part *p, int64_t *n_out) {
+    ARG_CHECK(p && n_out, "null argument");
+    *n_out = p->n;
+    return SKY_OK;
+}
+
+int sky_part_insert(sky_part *p, const int64_t *ids, const double *values, int64_t n) {
+    GUARD_BEGIN
+    ARG_CHECK(p && (n == 0 || (ids && values)), "null argument");
+    ARG_CHECK(n >= 0, "negative n");
+    if (n == 0) return SKY_OK;
+    sky_ctx *c = p->ctx;
+    SKY_TRY(bind(c));
+    const int D = c->D;
+    const int64_t tot = p->n + n;
+    ARG_CHECK(tot < (int64_t)0x7fffffffLL, "partition state too large");
+    SKY_TRY(p->cat_ids.ensure((size_t)tot * 8));
+    SKY_TRY(p->cat_rows.ensure((size_t)tot * D * 8));
+    if (p->n) {
+        HIP_TRY(hipMemcpyAsync(p->cat_ids.p, p->ids.p, (size_t)p->n * 8, hipMemcpyDeviceToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(p->cat_rows.p, p->rows.p, (size_t)p->n * D * 8, hipMemcpyDeviceToDevice, c->st));
+    }
+    HIP_TRY(hipMemcpyAsync(p->cat_ids.as<int64_t>() + p->n, ids, (size_t)n * 8, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(p->cat_rows.as<double>() + p->n * D, values, (size_t)n * D * 8, hipMemcpyHostToDevice,
+                           c->st));
+    PipeIn in;
+    in.vals = p->cat_rows.as<double>();
+    in.n = (uint32_t)tot;
+    in.ids = p->cat_ids.as<int64_t>();
+    in.single = true;
+    in.global = false;
+    in.K = 1;
+    c->shard_valid = false;
+    SKY_TRY(pipe_run(*c, c->aux, in, nullptr));
+    const int64_t g = c->aux.nout;
+    SKY_TRY(p->ids.ensure((size_t)std::max<int64_t>(g, 1) * 8));
+    SKY_TRY(p->rows.ensure((size_t)std::max<int64_t>(g, 1) * D * 8));
+    SKY_TRY(pipe_output(*c, c->aux, in, true, p->ids.as<int64_t>(), nullptr, p->rows.as<double>(), g, nullptr,
+                        nullptr));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    p->n = g;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_part_snapshot(sky_part *p, int64_t *ids_out, double *values_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(p, "null part");
+    if (n_out) *n_out = p->n;
+    if (p->n > cap) {
+        set_error("snapshot capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    if (p->n == 0) return SKY_OK;
+    sky_ctx *c = p->ctx;
+    SKY_TRY(bind(c));
+    if (ids_out) HIP_TRY(hipMemcpyAsync(ids_out, p->ids.p, (size_t)p->n * 8, hipMemcpyDeviceToHost, c->st));
+    if (values_out)
+        HIP_TRY(hipMemcpyAsync(values_out, p->rows.p, (size_t)p->n * c->D * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
+// ---- multi-GPU phases ---------------------------------------------------------------
+int sky_export_local_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int64_t n, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || d_values) && n_out, "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
+    SKY_TRY(bind(c));
+    PipeIn in;
+    in.vals = d_values;
+    in.n = (uint32_t)n;
+    in.ids = d_ids;
+    in.global = false;
+    in.K = c->Kq();
+    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
+    Pipe &p = c->main;
+    // multiplicity of every representative + export order among the alive ones
+    SKY_TRY(p.mult.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 8));
+    SKY_TRY(p.alive_u32.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 4));
+    SKY_TRY(p.alive_scan.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 4));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(p.mr + 1) * 4 + 64));
+    uint32_t ne = 0;
+    if (p.mr) {
+        HIP_TRY(hipMemsetAsync(p.mult.p, 0, (size_t)p.mr * 8, c->st));
+        const uint32_t *perm = nullptr;
+        // the sorted permutation lives in perm or val_alt; rep_of_sorted/slot_rep are per sorted position / slot,
+        // so weigh every slot once through slot_rep instead
+        (void)perm;
+        launch_flag_u8_to_u32(p.alive_l.as<uint8_t>(), p.mr, p.alive_u32.as<uint32_t>(), c->st);
+        scan_excl_u32(p.alive_u32.as<uint32_t>(), p.alive_scan.as<uint32_t>(), p.mr, p.totals.as<uint32_t>() + 4,
+                      p.scratch.as<uint32_t>(), c->st);
+        SKY_TRY(p.perm.ensure((size_t)p.mt * 4));
+        launch_iota(p.perm.as<uint32_t>(), p.mt, c->st);   // identity: slot order
+        launch_rep_mult(p.mt, p.perm.as<uint32_t>(), p.slot_src.as<uint32_t>(), p.slot_rep.as<uint32_t>(),
+                        in.weights, p.dup_cnt.as<uint32_t>(), p.pr_entries.as<int32_t>(),
+                        p.mult.as<unsigned long long>(), c->st);
+        HIP_TRY(hipMemcpyAsync(&ne, p.totals.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
+    }
+    c->shard = in;
+    c->shard_valid = true;
+    c->counters[0] = p.n;
+    c->counters[1] = p.m;
+    c->counters[2] = p.mr;
+    *n_out = ne;
+    c->counters[3] = ne;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_export_copy_dev(sky_ctx *c, double *d_rows_out, int32_t *d_keys_out, int64_t *d_mult_out, int64_t cap) {
+    GUARD_BEGIN
+    ARG_CHECK(c && c->shard_valid, "call sky_export_local_dev first");
+    ARG_CHECK(cap >= c->counters[3], "export capacity too small");
+    SKY_TRY(bind(c));
+    Pipe &p = c->main;
+    launch_export_reps(c->D, p.f64, p.mr, p.rep_rows.p, p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(),
+                       p.alive_scan.as<uint32_t>(), p.mult.as<unsigned long long>(), d_rows_out, d_keys_out,
+                       d_mult_out, c->st);
+    HIP_TRY(hipGetLastError());
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys, const int64_t *d_mult,
+                         int64_t n_union, int64_t self_offset, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
+                         int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && c->shard_valid, "call sky_export_local_dev first");
+    ARG_CHECK(n_union >= 0 && n_union < (int64_t)0x7fffffffLL, "n_union out of range");
+    ARG_CHECK(self_offset >= 0 && self_offset + c->counters[3] <= n_union, "self_offset out of range");
+    SKY_TRY(bind(c));
+    PipeIn u;
+    u.vals = d_rows;
+    u.n = (uint32_t)n_union;
+    u.keys = d_keys;
+    u.weights = d_mult;
+    u.global = true;
+    u.K = c->Kq();
+    SKY_TRY(pipe_run(*c, c->aux, u, nullptr));
+    store_stats(c, c->aux);
+    SKY_TRY(c->h_flags.ensure((size_t)std::max<int64_t>(n_union, 1)));
+    SKY_TRY(pipe_output(*c, c->aux, u, false, nullptr, nullptr, nullptr, 0, nullptr, c->h_flags.as<uint8_t>()));
+    Pipe &p = c->main;
+    launch_import_flags(p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), p.mr, c->h_flags.as<uint8_t>(),
+                        (uint32_t)self_offset, p.alive_g.as<uint8_t>(), c->st);
+    // recount this shard's output with the imported global fates (no stats: those came from the union)
+    {
+        const uint32_t tiles = (p.n + kTile - 1) / kTile;
+        OutArgs oa{};
+        oa.status = p.status.as<uint16_t>();
+        oa.n = p.n;
+        oa.blk_off = p.blk_off.as<uint32_t>();
+        oa.slot_rep = p.slot_rep.as<uint32_t>();
+        oa.m = p.m;
+        oa.pruner_slot = p.pruner_slot.as<int32_t>();
+        oa.M = p.M;
+        oa.alive_l = p.alive_l.as<uint8_t>();
+        oa.alive_g = p.alive_g.as<uint8_t>();
+        oa.K = p.K;
+        oa.out_cnt = p.out_cnt.as<uint32_t>();
+        if (p.n) {
+            launch_out_count(oa, c->st);
+            scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                          p.scratch.as<uint32_t>(), c->st);
+            uint32_t nout = 0;
+            HIP_TRY(hipMemcpyAsync(&nout, p.totals.as<uint32_t>() + 3, 4, hipMemcpyDeviceToHost, c->st));
+            HIP_TRY(hipStreamSynchronize(c->st));
+            p.nout = nout;
+        } else {
+            p.nout = 0;
+        }
+    }
+    SKY_TRY(pipe_output(*c, p, c->shard, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr));
+    HIP_TRY(hipGetLastError());
+    return SKY_OK;
+    GUARD_END
+}
+
+// ---- utilities ------------------------------------------------------------------------
+int sky_synth_dev(sky_ctx *c, int dist, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *d_values,
+                  int64_t *d_ids) {
+    GUARD_BEGIN
+    ARG_CHECK(c && (n == 0 || d_values), "null argument");
+    ARG_CHECK(dist >= 0 && dist <= 4 && dmax >= dmin, "bad distribution arguments");
+    SKY_TRY(bind(c));
+    launch_synth(dist, c->D, dmin, dmax, seed, id0, n, d_values, d_ids, c->st);
+    HIP_TRY(hipGetLastError());
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_synth(int dist, int dims, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *values,
+              int64_t *ids) {
+    ARG_CHECK(dims >= 1 && dims <= SKY_MAX_DIMS && (n == 0 || values), "bad arguments");
+    ARG_CHECK(dist >= 0 && dist <= 4 && dmax >= dmin, "bad distribution arguments");
+    synth_host(dist, dims, dmin, dmax, seed, id0, n, values, ids);
+    return SKY_OK;
+}
+
+int sky_dev_alloc(sky_ctx *c, int64_t bytes, void **d_out) {
+    ARG_CHECK(c && d_out && bytes >= 0, "bad arguments");
+    SKY_TRY(bind(c));
+    HIP_TRY(hipMalloc(d_out, (size_t)std::max<int64_t>(bytes, 1)));
+    return SKY_OK;
+}
+int sky_dev_free(sky_ctx *c, void *d) {
+    ARG_CHECK(c, "ctx is null");
+    SKY_TRY(bind(c));
+    if (d) HIP_TRY(hipFree(d));
+    return SKY_OK;
+}
+int sky_memcpy_h2d(sky_ctx *c, void *d_dst, const void *h_src, int64_t bytes) {
+    ARG_CHECK(c && bytes >= 0, "bad arguments");
+    SKY_TRY(bind(c));
+    if (bytes) HIP_TRY(hipMemcpyAsync(d_dst, h_src, (size_t)bytes, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+}
+int sky_memcpy_d2h(sky_ctx *c, void *h_dst, const void *d_src, int64_t bytes) {
+    ARG_CHECK(c && bytes >= 0, "bad arguments");
+    SKY_TRY(bind(c));
+    if (bytes) HIP_TRY(hipMemcpyAsync(h_dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+}
+
+int sky_profile_enable(sky_ctx *c, int on) {
+    ARG_CHECK(c, "ctx is null");
+    c->profile = on != 0;
+    return SKY_OK;
+}
+int sky_profile_phases(sky_ctx *c, double *ms_out, int64_t *counters_out) {
+    ARG_CHECK(c, "ctx is null");
+    for (int i = 0; i < SKY_PHASES; i++)
+        if (ms_out) ms_out[i] = c->phase_ms[i];
+    for (int i = 0; i < 8; i++)
+        if (counters_out) counters_out[i] = c->counters[i];
+    return SKY_OK;
+}
+int sky_profile_kernel(sky_ctx *c, const char *name, double *total_ms, int64_t *launches, int64_t *units) {
+    ARG_CHECK(c && name, "null argument");
+    c->ktimer_collect();
+    auto it = c->kt.find(name);
+    if (total_ms) *total_ms = it == c->kt.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == c->kt.end() ? 0 : it->second.launches;
+    if (units) *units = it == c->kt.end() ? 0 : it->second.units;
+    return SKY_OK;
+}
+int sky_profile_reset(sky_ctx *c) {
+    ARG_CHECK(c, "ctx is null");
+    c->ktimer_collect();
+    c->kt.clear();
+    for (double &x : c->phase_ms) x = 0;
+    return SKY_OK;
+}
+
+}  // extern "C"

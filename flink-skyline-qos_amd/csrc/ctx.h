@@ -1,0 +1,132 @@
+// ctx.h — the object behind an sky_ctx* handle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <map>
+#include <string>
+#include <vector>
+#include "engine.h"
+
+namespace sky {
+
+// HIP-event timings of the pipeline phases of one query (profiling only)
+struct PhaseTimer {
+    hipEvent_t ev[SKY_PHASES + 1] = {};
+    bool marked[SKY_PHASES + 1] = {};
+    bool ok = false;
+    void init() {
+        ok = true;
+        for (auto &e : ev)
+            if (hipEventCreate(&e) != hipSuccess) ok = false;
+    }
+    void reset() {
+        for (bool &m : marked) m = false;
+    }
+    void mark(int i, hipStream_t st) {
+        if (ok && i >= 0 && i <= SKY_PHASES) {
+            hipEventRecord(ev[i], st);
+            marked[i] = true;
+        }
+    }
+    void destroy() {
+        for (auto &e : ev)
+            if (e) hipEventDestroy(e);
+    }
+};
+
+// accumulated HIP-event time of one kernel family on the launching stream
+struct KTime {
+    double ms = 0;
+    int64_t launches = 0, units = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<int64_t> pending_units;
+};
+
+struct Ctx {
+    int dev = 0, D = 2, P = 8, algo = SKY_ALGO_ANGLE, sem = SKY_SEM_REFERENCE;
+    double domain = 1000.0;
+    hipStream_t own = nullptr, st = nullptr;
+    Pipe main, aux;
+    std::vector<int64_t> lsz, surv;
+    int K_last = 0;
+    bool profile = false;
+    PhaseTimer pt;
+    double phase_ms[SKY_PHASES] = {};
+    int64_t counters[8] = {};
+    std::map<std::string, KTime> kt;
+    std::vector<hipEvent_t> event_pool;
+    // staging for the host-buffer entry points
+    DevBuf h_vals, h_ids, h_keys, h_out_ids, h_out_org, h_origin, h_flags;
+    // multi-GPU phase-1 state (the shard stays caller-owned)
+    PipeIn shard;
+    bool shard_valid = false;
+    DevBuf exp_scan;
+
+    int Kq() const {
+        if (algo == SKY_ALGO_GRID && sem == SKY_SEM_COMPLETE) return std::max(P, 1 << D);
+        return P;
+    }
+    KeyParams kp() const {
+        KeyParams k{};
+        k.algo = algo;
+        k.P = P;
+        k.K = Kq();
+        k.dim_width = domain / (double)P;
+        k.grid_mid = domain / 2.0;
+        return k;
+    }
+    hipEvent_t take_event() {
+        if (!event_pool.empty()) {
+            hipEvent_t e = event_pool.back();
+            event_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        hipEventCreate(&e);
+        return e;
+    }
+    void ktimer_begin(const char *name, hipStream_t s) {
+        if (!profile) return;
+        KTime &k = kt[name];
+        hipEvent_t a = take_event(), b = take_event();
+        hipEventRecord(a, s);
+        k.pending.push_back({a, b});
+        k.pending_units.push_back(0);
+    }
+    void ktimer_end(const char *name, hipStream_t s, int64_t units) {
+        if (!profile) return;
+        KTime &k = kt[name];
+        if (k.pending.empty()) return;
+        hipEventRecord(k.pending.back().second, s);
+        k.pending_units.back() = units;
+    }
+    void ktimer_collect() {
+        for (auto &kv : kt) {
+            KTime &k = kv.second;
+            for (size_t i = 0; i < k.pending.size(); i++) {
+                float ms = 0;
+                hipEventSynchronize(k.pending[i].second);
+                if (hipEventElapsedTime(&ms, k.pending[i].first, k.pending[i].second) == hipSuccess) {
+                    k.ms += ms;
+                    k.launches++;
+                    k.units += k.pending_units[i];
+                }
+                event_pool.push_back(k.pending[i].first);
+                event_pool.push_back(k.pending[i].second);
+            }
+            k.pending.clear();
+            k.pending_units.clear();
+        }
+    }
+};
+
+}  // namespace sky
+
+struct sky_ctx : sky::Ctx {};
+
+struct sky_part {
+    sky_ctx *ctx = nullptr;
+    int32_t key = 0;
+    sky::DevBuf ids, rows;    // current local skyline (device), insertion order
+    int64_t n = 0;
+    sky::DevBuf cat_ids, cat_rows;
+};

@@ -1,0 +1,75 @@
+// engine.h — host-side orchestration of the gfx950 skyline pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string>
+#include <vector>
+#include "sky_internal.h"
+
+namespace sky {
+
+void set_error(const std::string &msg);
+
+// grow-only device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes);
+    void release();
+    template <typename T> T *as() const { return reinterpret_cast<T *>(p); }
+    ~DevBuf() { release(); }
+};
+
+struct PipeIn {
+    const double *vals = nullptr;   // device, n x D f64
+    uint32_t n = 0;
+    const int64_t *ids = nullptr;   // device ids (nullptr: tuple index)
+    const int32_t *keys = nullptr;  // given partition keys (nullptr: computed)
+    const int32_t *origin = nullptr;// given origin tags for stats / output (nullptr: partition key)
+    const int64_t *weights = nullptr;
+    bool single = false;            // one partition (global merge of lists, local state insert)
+    bool global = true;             // run the global merge after the local skylines
+    int K = 1;                      // stats slots
+};
+
+struct PhaseTimer;
+
+// One pipeline instance = its own workspace (a context owns two so that the
+// multi-GPU import can run on the union while the local shard's state is kept).
+struct Pipe {
+    // per tuple / per tile
+    DevBuf status, blk_cnt, blk_off, out_cnt, out_off;
+    // pruners
+    DevBuf skey, ssum, sidx, pruners, npr, dup_cnt, pr_entries, pruner_slot;
+    // candidates (slot order) and sort
+    DevBuf rows, sortkey, slot_src, perm, key_alt, val_alt, rows_sorted;
+    DevBuf runflag, runscan, run_first, repof, repflag, repscan, rep_rows, rep_key, rep_of_sorted, slot_rep;
+    DevBuf alive_l, alive_g, alive_u32, alive_scan, mult;
+    // SFS
+    DevBuf act, act2, keep, keep_scan, conf_rows, nconf, segs, seg_list, tiles, seg_begin, seg_end, segcnt;
+    // global
+    DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
+    DevBuf scratch, flags, totals, orand, lsz, surv;
+    // host-visible pinned staging
+    void *pin = nullptr;
+    size_t pin_cap = 0;
+
+    // results of the last run
+    uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0;
+    int M = 1, Kp = 1, K = 1;
+    bool f64 = false, ties = false;
+    std::vector<uint32_t> h_dup;
+    std::vector<int32_t> h_entries;
+    std::vector<unsigned long long> h_lsz, h_surv;
+    int64_t sfs_rounds = 0, sfs_pairs_upper = 0;
+
+    ~Pipe();
+    int pinned(size_t bytes);
+};
+
+struct Ctx;
+int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
+// stream-ordered output of the tuples selected by the last run
+int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,
+                double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags);
+
+}  // namespace sky

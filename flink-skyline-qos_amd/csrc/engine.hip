@@ -1,0 +1,475 @@
+// engine.hip — host orchestration of one skyline query on one MI355X.
+//
+//   sample + pruners -> k_filter (HBM stream) -> scan -> k_compact<T>
+//   -> radix sort (partition | score | hash) -> duplicate collapse
+//   -> segmented SFS (local skylines L_k) -> SFS over the union of the L_k (G)
+//   -> per-tuple fate pass (|L_k|, survivors_k, stream-ordered ids)
+//
+// Host synchronisations happen only where the host must size the next launch
+// (candidate count, representative count, per-round SFS segment counts).
+#include "engine.h"
+#include "ctx.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace sky {
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #expr);   \
+            return SKY_E_HIP;                                                             \
+        }                                                                                 \
+    } while (0)
+#define SKY_TRY(expr)            \
+    do {                         \
+        int r_ = (expr);         \
+        if (r_ != SKY_OK) return r_; \
+    } while (0)
+
+int DevBuf::ensure(size_t bytes) {
+    if (bytes <= cap && p) return SKY_OK;
+    release();
+    size_t want = std::max<size_t>(bytes, 256);
+    want = (want + 4095) & ~size_t(4095);
+    if (hipMalloc(&p, want) != hipSuccess) {
+        p = nullptr;
+        cap = 0;
+        (void)hipGetLastError();
+        set_error("hipMalloc of " + std::to_string(want) + " bytes failed");
+        return SKY_E_NOMEM;
+    }
+    cap = want;
+    return SKY_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+Pipe::~Pipe() {
+    if (pin) (void)hipHostFree(pin);
+}
+
+int Pipe::pinned(size_t bytes) {
+    if (bytes <= pin_cap && pin) return SKY_OK;
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    if (hipHostMalloc(&pin, want, hipHostMallocDefault) != hipSuccess) {
+        pin = nullptr;
+        pin_cap = 0;
+        set_error("hipHostMalloc failed");
+        return SKY_E_NOMEM;
+    }
+    pin_cap = want;
+    return SKY_OK;
+}
+
+static int choose_B(bool f64, int D) {
+    const int DP = f64 ? padded_dims<double>(D) : padded_dims<float>(D);
+    const int rowb = DP * (f64 ? 8 : 4);
+    int lim = 49152 / rowb;
+    int B = 1024;
+    while (B > lim) B >>= 1;
+    return B < 64 ? 64 : B;
+}
+
+static size_t row_bytes(bool f64, int D) {
+    return f64 ? padded_dims<double>(D) * 8 : padded_dims<float>(D) * 4;
+}
+
+// ---- segmented blocked SFS -------------------------------------------------------
+static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint32_t nrep,
+                   std::vector<uint32_t> begin, std::vector<uint32_t> cnt, bool full, uint8_t *alive) {
+    hipStream_t st = c.st;
+    const int D = c.D;
+    const uint32_t nseg = (uint32_t)begin.size();
+    const int B = choose_B(p.f64, D);
+    const size_t rb = row_bytes(p.f64, D);
+    constexpr uint32_t kTileP = 1024;   // 256 threads x PPT(4)
+    SKY_TRY(p.act.ensure((size_t)nrep * 4));
+    SKY_TRY(p.act2.ensure((size_t)nrep * 4));
+    SKY_TRY(p.keep.ensure((size_t)nrep * 4));
+    SKY_TRY(p.keep_scan.ensure((size_t)nrep * 4));
+    SKY_TRY(p.conf_rows.ensure((size_t)nseg * B * rb));
+    SKY_TRY(p.nconf.ensure((size_t)nseg * 4));
+    SKY_TRY(p.segs.ensure((size_t)nseg * sizeof(SfsSeg)));
+    SKY_TRY(p.seg_list.ensure((size_t)nseg * 4));
+    SKY_TRY(p.segcnt.ensure((size_t)nseg * 4));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(nrep + 1) * 4 + 64));
+    SKY_TRY(p.totals.ensure(64));
+    launch_iota(p.act.as<uint32_t>(), nrep, st);
+    std::vector<SfsSeg> hsegs(nseg);
+    std::vector<uint32_t> work;
+    std::vector<SfsTile> tiles;
+    for (;;) {
+        work.clear();
+        for (uint32_t k = 0; k < nseg; k++) {
+            hsegs[k] = SfsSeg{begin[k], cnt[k]};
+            if (cnt[k]) work.push_back(k);
+        }
+        if (work.empty()) break;
+        p.sfs_rounds++;
+        HIP_TRY(hipMemcpyAsync(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(p.seg_list.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, st));
+        launch_block_sky(D, p.f64, full, p.ties, B, rows, key, p.act.as<uint32_t>(), p.segs.as<SfsSeg>(),
+                         p.seg_list.as<uint32_t>(), (uint32_t)work.size(), alive, p.conf_rows.p,
+                         p.nconf.as<uint32_t>(), st);
+        tiles.clear();
+        uint32_t out = 0;
+        for (uint32_t k : work) {
+            const uint32_t xk = std::min<uint32_t>(B, cnt[k]);
+            const uint32_t rem = cnt[k] - xk;
+            for (uint32_t off = 0; off < rem; off += kTileP) {
+                const uint32_t cn = std::min<uint32_t>(kTileP, rem - off);
+                tiles.push_back(SfsTile{k, begin[k] + xk + off, cn, out});
+                out += cn;
+            }
+            p.sfs_pairs_upper += (int64_t)rem * xk + (int64_t)xk * (xk - 1) / 2;
+        }
+        if (out == 0) break;
+        SKY_TRY(p.tiles.ensure(tiles.size() * sizeof(SfsTile)));
+        HIP_TRY(hipMemcpyAsync(p.tiles.p, tiles.data(), tiles.size() * sizeof(SfsTile), hipMemcpyHostToDevice, st));
+        c.ktimer_begin("sfs_filter", st);
+        launch_filter_rest(D, p.f64, full, B, rows, p.act.as<uint32_t>(), p.tiles.as<SfsTile>(),
+                           (uint32_t)tiles.size(), p.conf_rows.p, p.nconf.as<uint32_t>(), p.keep.as<uint32_t>(), st);
+        c.ktimer_end("sfs_filter", st, out);
+        scan_excl_u32(p.keep.as<uint32_t>(), p.keep_scan.as<uint32_t>(), out, nullptr, p.scratch.as<uint32_t>(), st);
+        HIP_TRY(hipMemsetAsync(p.segcnt.p, 0, nseg * 4, st));
+        launch_act_compact(p.act.as<uint32_t>(), p.keep.as<uint32_t>(), p.keep_scan.as<uint32_t>(),
+                           p.tiles.as<SfsTile>(), (uint32_t)tiles.size(), p.act2.as<uint32_t>(),
+                           p.segcnt.as<uint32_t>(), st);
+        SKY_TRY(p.pinned(nseg * 4));
+        HIP_TRY(hipMemcpyAsync(p.pin, p.segcnt.p, nseg * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const uint32_t *sc = (const uint32_t *)p.pin;
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < nseg; k++) {
+            begin[k] = run;
+            cnt[k] = sc[k];
+            run += sc[k];
+        }
+        std::swap(p.act, p.act2);
+    }
+    return SKY_OK;
+}
+
+static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
+                     std::vector<void *> dsts) {
+    size_t tot = 0;
+    for (auto &s : srcs) tot += (s.second + 15) & ~size_t(15);
+    SKY_TRY(p.pinned(tot));
+    size_t off = 0;
+    for (auto &s : srcs) {
+        if (s.second) HIP_TRY(hipMemcpyAsync((char *)p.pin + off, s.first, s.second, hipMemcpyDeviceToHost, st));
+        off += (s.second + 15) & ~size_t(15);
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    off = 0;
+    for (size_t i = 0; i < srcs.size(); i++) {
+        if (srcs[i].second) memcpy(dsts[i], (char *)p.pin + off, srcs[i].second);
+        off += (srcs[i].second + 15) & ~size_t(15);
+    }
+    return SKY_OK;
+}
+
+int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
+    hipStream_t st = c.st;
+    const int D = c.D;
+    const uint32_t n = in.n;
+    p.n = n;
+    p.K = in.K;
+    p.Kp = in.single ? 1 : c.Kq();
+    p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
+    p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
+    p.sfs_rounds = p.sfs_pairs_upper = 0;
+    p.h_lsz.assign(p.K, 0);
+    p.h_surv.assign(p.K, 0);
+    const uint32_t tiles = (n + kTile - 1) / kTile;
+    SKY_TRY(p.lsz.ensure((size_t)p.K * 8));
+    SKY_TRY(p.surv.ensure((size_t)p.K * 8));
+    SKY_TRY(p.totals.ensure(64));
+    SKY_TRY(p.flags.ensure(64));
+    HIP_TRY(hipMemsetAsync(p.lsz.p, 0, (size_t)p.K * 8, st));
+    HIP_TRY(hipMemsetAsync(p.surv.p, 0, (size_t)p.K * 8, st));
+    if (n == 0) return SKY_OK;
+    KeyParams kp = c.kp();
+    kp.K = p.Kp;
+    if (tm) tm->mark(0, st);
+
+    // ---- pruners from a strided sample
+    const uint32_t S = std::min<uint32_t>(n, 65536);
+    SKY_TRY(p.skey.ensure((size_t)S * 4));
+    SKY_TRY(p.ssum.ensure((size_t)S * 8));
+    SKY_TRY(p.sidx.ensure((size_t)S * 4));
+    SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
+    SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
+    launch_sample(D, in.vals, n, S, kp, in.keys, in.single, p.skey.as<int32_t>(), p.ssum.as<double>(),
+                  p.sidx.as<uint32_t>(), st);
+    launch_select_pruners(D, in.vals, S, p.skey.as<int32_t>(), p.ssum.as<double>(), p.sidx.as<uint32_t>(), p.Kp,
+                          p.M, p.pruners.as<double>(), p.npr.as<int32_t>(), st);
+    if (tm) tm->mark(1, st);
+
+    // ---- the HBM stream: keys + pruner test + status
+    SKY_TRY(p.status.ensure((size_t)n * 2));
+    SKY_TRY(p.blk_cnt.ensure((size_t)tiles * 4));
+    SKY_TRY(p.blk_off.ensure((size_t)tiles * 4));
+    SKY_TRY(p.dup_cnt.ensure((size_t)p.Kp * p.M * 4));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
+    HIP_TRY(hipMemsetAsync(p.dup_cnt.p, 0, (size_t)p.Kp * p.M * 4, st));
+    HIP_TRY(hipMemsetAsync(p.flags.p, 0, 64, st));
+    FilterArgs fa{};
+    fa.vals = in.vals;
+    fa.n = n;
+    fa.kp = kp;
+    fa.given_keys = in.keys;
+    fa.single = in.single;
+    fa.pruners = p.pruners.as<double>();
+    fa.npr = p.npr.as<int32_t>();
+    fa.M = p.M;
+    fa.Kp = p.Kp;
+    fa.status = p.status.as<uint16_t>();
+    fa.blk_cnt = p.blk_cnt.as<uint32_t>();
+    fa.dup_cnt = p.dup_cnt.as<uint32_t>();
+    fa.flags = p.flags.as<uint32_t>();
+    c.ktimer_begin("filter", st);
+    launch_filter(D, fa, st);
+    c.ktimer_end("filter", st, n);
+    scan_excl_u32(p.blk_cnt.as<uint32_t>(), p.blk_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>(),
+                  p.scratch.as<uint32_t>(), st);
+    uint32_t m = 0, flags = 0;
+    p.h_dup.assign((size_t)p.Kp * p.M, 0);
+    SKY_TRY(sync_read(p, st, {{p.totals.p, 4}, {p.flags.p, 4}, {p.dup_cnt.p, p.h_dup.size() * 4}},
+                      {&m, &flags, p.h_dup.data()}));
+    if (tm) tm->mark(2, st);
+    if (flags & kFlagNaN) {
+        set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; rejected");
+        return SKY_E_NAN;
+    }
+    p.m = m;
+    p.f64 = (flags & kFlagNotF32) != 0;
+    p.h_entries.clear();
+    std::vector<int32_t> pslot((size_t)p.Kp * p.M, -1);
+    for (size_t q = 0; q < p.h_dup.size(); q++)
+        if (p.h_dup[q]) {
+            pslot[q] = (int32_t)(m + p.h_entries.size());
+            p.h_entries.push_back((int32_t)q);
+        }
+    p.nps = (uint32_t)p.h_entries.size();
+    p.mt = m + p.nps;
+    SKY_TRY(p.pr_entries.ensure(std::max<size_t>(p.nps, 1) * 4));
+    SKY_TRY(p.pruner_slot.ensure(pslot.size() * 4));
+    if (p.nps) HIP_TRY(hipMemcpyAsync(p.pr_entries.p, p.h_entries.data(), p.nps * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p.pruner_slot.p, pslot.data(), pslot.size() * 4, hipMemcpyHostToDevice, st));
+
+    const uint32_t mt = p.mt;
+    const size_t rb = row_bytes(p.f64, D);
+    SKY_TRY(p.rows.ensure(std::max<size_t>(mt, 1) * rb));
+    SKY_TRY(p.sortkey.ensure(std::max<size_t>(mt, 1) * 8));
+    SKY_TRY(p.slot_src.ensure(std::max<size_t>(mt, 1) * 4));
+    SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
+    SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
+    SKY_TRY(p.alive_g.ensure(std::max<size_t>(mt, 1)));
+    if (mt) {
+        CompactArgs ca{};
+        ca.vals = in.vals;
+        ca.n = n;
+        ca.status = p.status.as<uint16_t>();
+        ca.blk_off = p.blk_off.as<uint32_t>();
+        ca.rows = p.rows.p;
+        ca.sortkey = p.sortkey.as<uint64_t>();
+        ca.slot_src = p.slot_src.as<uint32_t>();
+        ca.flags = p.flags.as<uint32_t>();
+        if (m) launch_compact(D, p.f64, ca, st);
+        launch_append_pruners(D, p.f64, p.pruners.as<double>(), p.M, p.pr_entries.as<int32_t>(), p.nps, m, p.rows.p,
+                              p.sortkey.as<uint64_t>(), p.slot_src.as<uint32_t>(), p.flags.as<uint32_t>(), st);
+        if (tm) tm->mark(3, st);
+
+        // ---- sort the candidates by (partition, score, hash)
+        SKY_TRY(p.perm.ensure((size_t)mt * 4));
+        SKY_TRY(p.key_alt.ensure((size_t)mt * 8));
+        SKY_TRY(p.val_alt.ensure((size_t)mt * 4));
+        SKY_TRY(p.orand.ensure(16));
+        SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mt), scan_scratch_words(mt + 1)) * 4 + 64));
+        launch_iota(p.perm.as<uint32_t>(), mt, st);
+        radix_key_orand(p.sortkey.as<uint64_t>(), mt, p.orand.as<unsigned long long>(), st);
+        unsigned long long orand[2];
+        SKY_TRY(sync_read(p, st, {{p.orand.p, 16}, {p.flags.p, 4}}, {orand, &flags}));
+        p.ties = (flags & kFlagScoreTies) != 0;
+        const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
+                                          p.val_alt.as<uint32_t>(), mt, orand[0] ^ orand[1],
+                                          p.scratch.as<uint32_t>(), st);
+        const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
+        const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
+        if (tm) tm->mark(4, st);
+
+        // ---- collapse exact duplicates: one representative per distinct vector
+        SKY_TRY(p.rows_sorted.ensure((size_t)mt * rb));
+        for (DevBuf *b : {&p.runflag, &p.runscan, &p.run_first, &p.repof, &p.repflag, &p.repscan, &p.rep_of_sorted})
+            SKY_TRY(b->ensure((size_t)mt * 4));
+        SKY_TRY(p.rep_rows.ensure((size_t)mt * rb));
+        SKY_TRY(p.rep_key.ensure((size_t)mt * 8));
+        RepArgs ra{};
+        ra.mt = mt;
+        ra.perm = perm;
+        ra.skey = skey;
+        ra.rows = p.rows.p;
+        ra.rows_sorted = p.rows_sorted.p;
+        ra.runflag = p.runflag.as<uint32_t>();
+        ra.runscan = p.runscan.as<uint32_t>();
+        ra.run_first = p.run_first.as<uint32_t>();
+        ra.repof = p.repof.as<uint32_t>();
+        ra.repflag = p.repflag.as<uint32_t>();
+        ra.repscan = p.repscan.as<uint32_t>();
+        ra.rep_rows = p.rep_rows.p;
+        ra.rep_key = p.rep_key.as<uint64_t>();
+        ra.rep_of_sorted = p.rep_of_sorted.as<uint32_t>();
+        ra.slot_rep = p.slot_rep.as<uint32_t>();
+        launch_gather_runs(D, p.f64, ra, st);
+        scan_excl_u32(ra.runflag, ra.runscan, mt, nullptr, p.scratch.as<uint32_t>(), st);
+        launch_run_first(ra, st);
+        launch_rep_of(D, p.f64, ra, st);
+        scan_excl_u32(ra.repflag, ra.repscan, mt, p.totals.as<uint32_t>() + 1, p.scratch.as<uint32_t>(), st);
+        launch_build_reps(D, p.f64, ra, st);
+        uint32_t mr = 0;
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}}, {&mr}));
+        p.mr = mr;
+        SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
+        SKY_TRY(p.seg_end.ensure((size_t)p.Kp * 4));
+        HIP_TRY(hipMemsetAsync(p.seg_begin.p, 0, (size_t)p.Kp * 4, st));
+        HIP_TRY(hipMemsetAsync(p.seg_end.p, 0, (size_t)p.Kp * 4, st));
+        launch_seg_bounds(p.rep_key.as<uint64_t>(), mr, p.seg_begin.as<uint32_t>(), p.seg_end.as<uint32_t>(), st);
+        std::vector<uint32_t> sb(p.Kp), se(p.Kp);
+        SKY_TRY(sync_read(p, st, {{p.seg_begin.p, (size_t)p.Kp * 4}, {p.seg_end.p, (size_t)p.Kp * 4}},
+                          {sb.data(), se.data()}));
+        for (int k = 0; k < p.Kp; k++) se[k] -= sb[k];
+        if (tm) tm->mark(5, st);
+
+        // ---- local skylines
+        HIP_TRY(hipMemsetAsync(p.alive_l.p, 0, mr, st));
+        SKY_TRY(sfs_run(c, p, p.rep_rows.p, p.rep_key.as<uint64_t>(), mr, sb, se, false, p.alive_l.as<uint8_t>()));
+        if (tm) tm->mark(6, st);
+
+        // ---- global merge over the union of the local skylines
+        if (in.global && !in.single) {
+            SKY_TRY(p.alive_u32.ensure((size_t)mr * 4));
+            SKY_TRY(p.alive_scan.ensure((size_t)mr * 4));
+            launch_flag_u8_to_u32(p.alive_l.as<uint8_t>(), mr, p.alive_u32.as<uint32_t>(), st);
+            scan_excl_u32(p.alive_u32.as<uint32_t>(), p.alive_scan.as<uint32_t>(), mr, p.totals.as<uint32_t>() + 2,
+                          p.scratch.as<uint32_t>(), st);
+            uint32_t mg = 0;
+            SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 2, 4}}, {&mg}));
+            p.mg = mg;
+            HIP_TRY(hipMemsetAsync(p.alive_g.p, 0, mr, st));
+            if (mg) {
+                SKY_TRY(p.gkey.ensure((size_t)mg * 8));
+                SKY_TRY(p.gval.ensure((size_t)mg * 4));
+                SKY_TRY(p.gkey_alt.ensure((size_t)mg * 8));
+                SKY_TRY(p.gval_alt.ensure((size_t)mg * 4));
+                SKY_TRY(p.grows.ensure((size_t)mg * rb));
+                SKY_TRY(p.galive.ensure((size_t)mg));
+                launch_global_keys(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), mr,
+                                   p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(), st);
+                radix_key_orand(p.gkey.as<uint64_t>(), mg, p.orand.as<unsigned long long>(), st);
+                SKY_TRY(sync_read(p, st, {{p.orand.p, 16}}, {orand}));
+                const bool galt = radix_sort_pairs(p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(),
+                                                   p.gkey_alt.as<uint64_t>(), p.gval_alt.as<uint32_t>(), mg,
+                                                   orand[0] ^ orand[1], p.scratch.as<uint32_t>(), st);
+                const uint64_t *gk = galt ? p.gkey_alt.as<uint64_t>() : p.gkey.as<uint64_t>();
+                const uint32_t *gv = galt ? p.gval_alt.as<uint32_t>() : p.gval.as<uint32_t>();
+                launch_gather_rows(D, p.f64, p.rep_rows.p, gv, mg, p.grows.p, st);
+                HIP_TRY(hipMemsetAsync(p.galive.p, 0, mg, st));
+                SKY_TRY(sfs_run(c, p, p.grows.p, gk, mg, {0u}, {mg}, true, p.galive.as<uint8_t>()));
+                launch_scatter_alive(gv, p.galive.as<uint8_t>(), mg, p.alive_g.as<uint8_t>(), st);
+            }
+        } else {
+            HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
+        }
+    }
+    if (tm) tm->mark(7, st);
+
+    // ---- per-tuple fate: stats + output counts
+    SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
+    SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
+    OutArgs oa{};
+    oa.status = p.status.as<uint16_t>();
+    oa.n = n;
+    oa.blk_off = p.blk_off.as<uint32_t>();
+    oa.slot_rep = p.slot_rep.as<uint32_t>();
+    oa.m = p.m;
+    oa.pruner_slot = p.pruner_slot.as<int32_t>();
+    oa.M = p.M;
+    oa.alive_l = p.alive_l.as<uint8_t>();
+    oa.alive_g = p.alive_g.as<uint8_t>();
+    oa.given_origin = in.origin;
+    oa.given_w = in.weights;
+    oa.K = p.K;
+    oa.lsz = p.lsz.as<unsigned long long>();
+    oa.surv = p.surv.as<unsigned long long>();
+    oa.out_cnt = p.out_cnt.as<uint32_t>();
+    oa.select_local = 0;
+    c.ktimer_begin("out", st);
+    launch_out_count(oa, st);
+    scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                  p.scratch.as<uint32_t>(), st);
+    c.ktimer_end("out", st, n);
+    uint32_t nout = 0;
+    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, (size_t)p.K * 8}, {p.surv.p, (size_t)p.K * 8}},
+                      {&nout, p.h_lsz.data(), p.h_surv.data()}));
+    p.nout = nout;
+    if (tm) tm->mark(8, st);
+    return SKY_OK;
+}
+
+int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,
+                double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags) {
+    (void)select_local;
+    if (n_out) *n_out = p.nout;
+    if ((int64_t)p.nout > cap && (d_ids_out || d_origin_out || d_rows_out)) {
+        set_error("output capacity " + std::to_string(cap) + " < skyline size " + std::to_string(p.nout));
+        return SKY_E_CAPACITY;
+    }
+    if (p.n == 0) return SKY_OK;
+    OutArgs oa{};
+    oa.status = p.status.as<uint16_t>();
+    oa.n = p.n;
+    oa.blk_off = p.blk_off.as<uint32_t>();
+    oa.slot_rep = p.slot_rep.as<uint32_t>();
+    oa.m = p.m;
+    oa.pruner_slot = p.pruner_slot.as<int32_t>();
+    oa.M = p.M;
+    oa.alive_l = p.alive_l.as<uint8_t>();
+    oa.alive_g = p.alive_g.as<uint8_t>();
+    oa.given_origin = in.origin;
+    oa.given_w = in.weights;
+    oa.K = p.K;
+    oa.out_cnt = p.out_cnt.as<uint32_t>();
+    oa.out_off = p.out_off.as<uint32_t>();
+    oa.ids = in.ids;
+    oa.vals = in.vals;
+    oa.D = c.D;
+    oa.ids_out = d_ids_out;
+    oa.origin_out = d_origin_out;
+    oa.rows_out = d_rows_out;
+    oa.select_local = 0;
+    if (d_row_flags) {
+        oa.row_flags = d_row_flags;
+        oa.lsz = nullptr;
+        oa.surv = nullptr;
+        launch_out_count(oa, c.st);
+        oa.row_flags = nullptr;
+    }
+    if (d_ids_out || d_origin_out || d_rows_out) {
+        c.ktimer_begin("out", c.st);
+        launch_out_write(oa, c.st);
+        c.ktimer_end("out", c.st, 0);
+    }
+    return SKY_OK;
+}
+
+}  // namespace sky

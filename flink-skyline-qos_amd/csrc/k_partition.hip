@@ -1,0 +1,616 @@
+// k_partition.hip — the HBM-streaming stages of the skyline path on gfx950.
+//
+//   k_keys           getKey for every tuple (FlinkSkyline.java:707-712 / 774-789 / 827-875)
+//   k_sample         strided sample: key + f64 monotone score
+//   k_select_pruners per partition, up to M mutually non-dominated sample tuples, smallest
+//                    score first (pruners never change the result: a tuple they dominate is
+//                    outside its partition's skyline; a tuple EQUAL to one shares its fate)
+//   k_filter         one pass over the f64 rows: key, pruner test, status word, per-tile
+//                    candidate counts (wave-ballot + LDS), NaN / f32-exactness flags
+//   k_compact<T>     order-preserving compaction of the candidates into AoS rows of T
+//                    (f32 when every candidate value is exactly an f32, else f64) with a
+//                    64-bit sort key (partition | score | vector hash)
+//   k_gather_runs / k_run_first / k_rep_of / k_build_reps
+//                    exact-duplicate collapse after the sort: one representative per
+//                    distinct vector of a partition
+//   k_out_count / k_out_write
+//                    per tuple: is it in its local / the global skyline? -> stats
+//                    (|L_k|, survivors_k) and the stream-ordered output ids
+#include "sky_internal.h"
+
+namespace sky {
+
+template <int D>
+__device__ __forceinline__ void load_row(const double *__restrict__ p, double (&v)[D]) {
+    if constexpr (D % 2 == 0) {
+        const double2 *q = reinterpret_cast<const double2 *>(p);
+#pragma unroll
+        for (int d = 0; d < D / 2; d++) {
+            double2 x = q[d];
+            v[2 * d] = x.x;
+            v[2 * d + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; d++) v[d] = p[d];
+    }
+}
+
+template <typename T, int D>
+__device__ __forceinline__ void store_row(T *__restrict__ p, const T (&v)[D]) {
+    constexpr int DP = padded_dims<T>(D);
+    T w[DP];
+#pragma unroll
+    for (int d = 0; d < DP; d++) w[d] = d < D ? v[d] : T(0);
+    if constexpr (sizeof(T) == 4) {
+        float4 *q = reinterpret_cast<float4 *>(p);
+#pragma unroll
+        for (int d = 0; d < DP / 4; d++) q[d] = make_float4(w[4 * d], w[4 * d + 1], w[4 * d + 2], w[4 * d + 3]);
+    } else {
+        double2 *q = reinterpret_cast<double2 *>(p);
+#pragma unroll
+        for (int d = 0; d < DP / 2; d++) q[d] = make_double2(w[2 * d], w[2 * d + 1]);
+    }
+}
+
+template <typename T, int D>
+__device__ __forceinline__ void load_trow(const T *__restrict__ p, T (&v)[D]) {
+    constexpr int DP = padded_dims<T>(D);
+    if constexpr (sizeof(T) == 4) {
+        const float4 *q = reinterpret_cast<const float4 *>(p);
+#pragma unroll
+        for (int d = 0; d < DP / 4; d++) {
+            float4 x = q[d];
+            if (4 * d + 0 < D) v[4 * d + 0] = x.x;
+            if (4 * d + 1 < D) v[4 * d + 1] = x.y;
+            if (4 * d + 2 < D) v[4 * d + 2] = x.z;
+            if (4 * d + 3 < D) v[4 * d + 3] = x.w;
+        }
+    } else {
+        const double2 *q = reinterpret_cast<const double2 *>(p);
+#pragma unroll
+        for (int d = 0; d < DP / 2; d++) {
+            double2 x = q[d];
+            if (2 * d + 0 < D) v[2 * d + 0] = x.x;
+            if (2 * d + 1 < D) v[2 * d + 1] = x.y;
+        }
+    }
+}
+
+// exclusive rank of `flag` in (round, thread) order within the block; `base` carries
+// the running count across rounds.  All threads of the block must call it.
+__device__ __forceinline__ uint32_t block_rank(bool flag, uint32_t *s_w, uint32_t &base) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t b = __ballot(flag);
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t pre = __popcll(b & lt);
+    if (lane == 0) s_w[w] = __popcll(b);
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; i++) {
+        const uint32_t c = s_w[i];
+        wb += i < w ? c : 0u;
+        tot += c;
+    }
+    __syncthreads();
+    const uint32_t r = base + wb + pre;
+    base += tot;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *s_w) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; i++) t += s_w[i];
+    __syncthreads();
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_keys(const double *__restrict__ vals, uint32_t n, KeyParams kp,
+                                                   int32_t *__restrict__ keys) {
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        double v[D];
+        load_row<D>(vals + (size_t)i * D, v);
+        keys[i] = partition_key<D>(v, kp);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_sample(const double *__restrict__ vals, uint32_t n, uint32_t S,
+                                                     KeyParams kp, const int32_t *__restrict__ given_keys,
+                                                     int single, int32_t *__restrict__ skey,
+                                                     double *__restrict__ ssum, uint32_t *__restrict__ sidx) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= S) return;
+    const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
+    double v[D];
+    load_row<D>(vals + (size_t)i * D, v);
+    bool nan = false;
+    double sum = 0.0;
+#pragma unroll
+    for (int d = 0; d < D; d++) { nan |= v[d] != v[d]; sum = sum + v[d]; }
+    int32_t k = single ? 0 : given_keys ? given_keys[i] : partition_key<D>(v, kp);
+    if (nan || k < 0 || k >= kp.K || sum != sum) k = -1;
+    skey[s] = k;
+    ssum[s] = sum;
+    sidx[s] = i;
+}
+
+// one workgroup per partition
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__restrict__ vals, uint32_t S,
+                                                             const int32_t *__restrict__ skey,
+                                                             const double *__restrict__ ssum,
+                                                             const uint32_t *__restrict__ sidx, int M,
+                                                             double *__restrict__ pruners,
+                                                             int32_t *__restrict__ npr) {
+    __shared__ double s_pr[8][D];
+    __shared__ double s_bs[kThreads / 64];
+    __shared__ uint32_t s_bi[kThreads / 64];
+    __shared__ uint32_t s_win;
+    const int k = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int chosen = 0;
+    for (int j = 0; j < M && j < 8; j++) {
+        double best = __builtin_inf();
+        uint32_t bi = 0xffffffffu;
+        for (uint32_t s = threadIdx.x; s < S; s += kThreads) {
+            if (skey[s] != k) continue;
+            const double sc = ssum[s];
+            if (!(sc < best || (sc == best && s < bi))) continue;
+            double v[D];
+            load_row<D>(vals + (size_t)sidx[s] * D, v);
+            bool ok = true;
+            for (int c = 0; c < chosen && ok; c++) {
+                bool le = true, lt = false, eq = true;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    le &= s_pr[c][d] <= v[d];
+                    lt |= s_pr[c][d] < v[d];
+                    eq &= s_pr[c][d] == v[d];
+                }
+                ok = !(le && lt) && !eq;
+            }
+            if (ok) { best = sc; bi = s; }
+        }
+        // block argmin over (best, bi)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const uint32_t oi = __shfl_xor(bi, o, 64);
+            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        if (lane == 0) { s_bs[w] = best; s_bi[w] = bi; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double b = s_bs[0];
+            uint32_t x = s_bi[0];
+            for (int q = 1; q < kThreads / 64; q++)
+                if (s_bs[q] < b || (s_bs[q] == b && s_bi[q] < x)) { b = s_bs[q]; x = s_bi[q]; }
+            s_win = x;
+        }
+        __syncthreads();
+        const uint32_t win = s_win;
+        if (win == 0xffffffffu) break;
+        if (threadIdx.x < D) {
+            const double x = vals[(size_t)sidx[win] * D + threadIdx.x];
+            s_pr[chosen][threadIdx.x] = x;
+            pruners[((size_t)k * M + chosen) * D + threadIdx.x] = x;
+        }
+        chosen++;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) npr[k] = chosen;
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // [Kp*M*D]
+    __shared__ int32_t s_npr[kMaxK];
+    __shared__ uint32_t s_dup[2048];
+    __shared__ uint32_t s_w[kThreads / 64];
+    const int nprw = a.Kp * a.M;
+    for (int q = threadIdx.x; q < nprw * D; q += kThreads) s_pr[q] = a.pruners[q];
+    for (int q = threadIdx.x; q < a.Kp; q += kThreads) s_npr[q] = a.npr[q];
+    for (int q = threadIdx.x; q < nprw; q += kThreads) s_dup[q] = 0;
+    __syncthreads();
+    uint32_t lflags = 0, mycnt = 0;
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 1
+    for (int r = 0; r < kItems; r++) {
+        const uint32_t i = base + r * kThreads + threadIdx.x;
+        if (i >= a.n) break;
+        double v[D];
+        load_row<D>(a.vals + (size_t)i * D, v);
+        bool nan = false;
+#pragma unroll
+        for (int d = 0; d < D; d++) nan |= v[d] != v[d];
+        int32_t k = a.single ? 0 : a.given_keys ? a.given_keys[i] : partition_key<D>(v, a.kp);
+        uint16_t code = kCodeCandidate;
+        if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
+        else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
+        else {
+            const int np = s_npr[k];
+            const double *pr = s_pr + (size_t)k * a.M * D;
+            for (int j = 0; j < np; j++) {
+                bool le = true, lt = false, eq = true;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    const double p = pr[j * D + d];
+                    le &= p <= v[d];
+                    lt |= p < v[d];
+                    eq &= p == v[d];
+                }
+                if (le && lt) { code = kCodeDropped; break; }
+                if (eq) { code = (uint16_t)(1 + j); atomicAdd(&s_dup[k * a.M + j], 1u); break; }
+            }
+            if (code == kCodeCandidate) {
+                mycnt++;
+#pragma unroll
+                for (int d = 0; d < D; d++)
+                    if ((double)(float)v[d] != v[d]) lflags |= kFlagNotF32;
+            }
+        }
+        a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+    }
+    const uint32_t tot = block_sum(mycnt, s_w);
+    if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = tot;
+    for (int q = threadIdx.x; q < nprw; q += kThreads)
+        if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
+    if (lflags) atomicOr(a.flags, lflags);
+}
+
+// score = f64 sum of the (exact) T values in dimension order; a tie-free key needs
+// the sum to be exact and exactly an f32 -> otherwise flag kFlagScoreTies.
+template <typename T, int D>
+__device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part, uint32_t &lflags) {
+    double s = 0.0;
+    bool inexact = false;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        const double x = (double)tv[d];
+        const double sn = s + x;
+        const double bb = sn - s;
+        const double err = (s - (sn - bb)) + (x - bb);
+        inexact |= err != 0.0;
+        s = sn;
+    }
+    const float f = (float)s;
+    inexact |= (double)f != s;
+    if (inexact) lflags |= kFlagScoreTies;
+    uint32_t h = 0x9e3779b9u;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        uint64_t bits;
+        if constexpr (sizeof(T) == 4) bits = __float_as_uint(tv[d] == T(0) ? T(0) : tv[d]);
+        else bits = (uint64_t)__double_as_longlong(tv[d] == T(0) ? T(0) : tv[d]);
+        h = mix32(h ^ (uint32_t)bits ^ (uint32_t)(bits >> 32) * 0x85ebca6bu);
+    }
+    return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffffu);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_compact(CompactArgs a) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    constexpr int DP = padded_dims<T>(D);
+    T *rows = reinterpret_cast<T *>(a.rows);
+    uint32_t lflags = 0;
+    uint32_t run = a.blk_off[blockIdx.x];
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 1
+    for (int r = 0; r < kItems; r++) {
+        if (base + r * kThreads >= a.n) break;                       // block-uniform
+        const uint32_t i = base + r * kThreads + threadIdx.x;
+        const uint16_t st = i < a.n ? a.status[i] : 0;
+        const bool cand = i < a.n && (st & 0xff) == kCodeCandidate;
+        const uint32_t slot = block_rank(cand, s_w, run);
+        if (cand) {
+            double v[D];
+            load_row<D>(a.vals + (size_t)i * D, v);
+            T tv[D];
+#pragma unroll
+            for (int d = 0; d < D; d++) tv[d] = (T)v[d];
+            store_row<T, D>(rows + (size_t)slot * DP, tv);
+            a.sortkey[slot] = make_sortkey<T, D>(tv, st >> 8, lflags);
+            a.slot_src[slot] = i;
+        }
+    }
+    if (lflags) atomicOr(a.flags, lflags);
+}
+
+template <typename T, int D>
+__global__ void k_append_pruners(const double *__restrict__ pruners, int M, const int32_t *__restrict__ entries,
+                                 uint32_t nps, uint32_t m, T *__restrict__ rows, uint64_t *__restrict__ sortkey,
+                                 uint32_t *__restrict__ slot_src, uint32_t *__restrict__ flags) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nps) return;
+    constexpr int DP = padded_dims<T>(D);
+    const int32_t kj = entries[e];
+    const int k = kj / M;
+    T tv[D];
+#pragma unroll
+    for (int d = 0; d < D; d++) tv[d] = (T)pruners[(size_t)kj * D + d];
+    uint32_t lflags = 0;
+    store_row<T, D>(rows + (size_t)(m + e) * DP, tv);
+    sortkey[m + e] = make_sortkey<T, D>(tv, (uint32_t)k, lflags);
+    slot_src[m + e] = 0x80000000u | e;
+    if (lflags) atomicOr(flags, lflags);
+}
+
+// ---- duplicate collapse after the sort --------------------------------------
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_gather_runs(RepArgs a) {
+    constexpr int DP = padded_dims<T>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.mt) return;
+    const T *src = reinterpret_cast<const T *>(a.rows) + (size_t)a.perm[j] * DP;
+    T *dst = reinterpret_cast<T *>(a.rows_sorted) + (size_t)j * DP;
+    T v[D];
+    load_trow<T, D>(src, v);
+    store_row<T, D>(dst, v);
+    a.runflag[j] = (j == 0 || a.skey[j] != a.skey[j - 1]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kThreads) void k_run_first(RepArgs a) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.mt) return;
+    if (a.runflag[j]) a.run_first[a.runscan[j]] = j;
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_rep_of(RepArgs a) {
+    constexpr int DP = padded_dims<T>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.mt) return;
+    const T *rs = reinterpret_cast<const T *>(a.rows_sorted);
+    T v[D];
+    load_trow<T, D>(rs + (size_t)j * DP, v);
+    const uint32_t s0 = a.run_first[a.runscan[j] + a.runflag[j] - 1];
+    uint32_t q = s0;
+    for (; q < j; q++) {
+        T u[D];
+        load_trow<T, D>(rs + (size_t)q * DP, u);
+        if (rows_equal<D, T>(u, v)) break;
+    }
+    a.repof[j] = q;
+    a.repflag[j] = q == j ? 1u : 0u;
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_build_reps(RepArgs a) {
+    constexpr int DP = padded_dims<T>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= a.mt) return;
+    const uint32_t r = a.repscan[a.repof[j]];
+    a.rep_of_sorted[j] = r;
+    a.slot_rep[a.perm[j]] = r;
+    if (a.repflag[j]) {
+        T v[D];
+        load_trow<T, D>(reinterpret_cast<const T *>(a.rows_sorted) + (size_t)j * DP, v);
+        store_row<T, D>(reinterpret_cast<T *>(a.rep_rows) + (size_t)r * DP, v);
+        a.rep_key[r] = a.skey[j];
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_seg_bounds(const uint64_t *__restrict__ rep_key, uint32_t mr,
+                                                         uint32_t *__restrict__ seg_begin,
+                                                         uint32_t *__restrict__ seg_end) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= mr) return;
+    const uint32_t p = (uint32_t)(rep_key[r] >> 56);
+    if (r == 0 || (uint32_t)(rep_key[r - 1] >> 56) != p) seg_begin[p] = r;
+    if (r == mr - 1 || (uint32_t)(rep_key[r + 1] >> 56) != p) seg_end[p] = r + 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_rep_mult(uint32_t mt, const uint32_t *__restrict__ perm,
+                                                       const uint32_t *__restrict__ slot_src,
+                                                       const uint32_t *__restrict__ rep_of_sorted,
+                                                       const int64_t *__restrict__ given_w,
+                                                       const uint32_t *__restrict__ dup_cnt,
+                                                       const int32_t *__restrict__ pr_entries,
+                                                       unsigned long long *__restrict__ mult) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= mt) return;
+    const uint32_t src = slot_src[perm[j]];
+    unsigned long long w;
+    if (src & 0x80000000u) w = dup_cnt[pr_entries[src & 0x7fffffffu]];
+    else w = given_w ? (unsigned long long)given_w[src] : 1ull;
+    atomicAdd(&mult[rep_of_sorted[j]], w);
+}
+
+// ---- output: per tuple local / global membership ------------------------------
+struct OutLds {
+    unsigned long long lsz[kMaxK];
+    unsigned long long surv[kMaxK];
+    uint32_t w[kThreads / 64];
+};
+
+__device__ __forceinline__ void tuple_fate(const OutArgs &a, uint32_t i, uint16_t st, uint32_t cand_slot,
+                                           bool &inl, bool &ing) {
+    const uint32_t code = st & 0xff;
+    inl = ing = false;
+    if (code == kCodeDropped) return;
+    uint32_t rep;
+    if (code == kCodeCandidate) rep = a.slot_rep[cand_slot];
+    else {
+        const int32_t ps = a.pruner_slot[(st >> 8) * a.M + (code - 1)];
+        rep = a.slot_rep[ps];
+    }
+    inl = a.alive_l[rep] != 0;
+    ing = a.alive_g[rep] != 0;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
+    __shared__ OutLds s;
+    const bool stats = !WRITE && a.lsz != nullptr;
+    if (stats)
+        for (int q = threadIdx.x; q < a.K; q += kThreads) { s.lsz[q] = 0; s.surv[q] = 0; }
+    __syncthreads();
+    uint32_t cand_run = a.blk_off[blockIdx.x];
+    uint32_t out_run = WRITE ? a.out_off[blockIdx.x] : 0u;
+    uint32_t mycnt = 0;
+    const uint32_t base = blockIdx.x * kTile;
+#pragma unroll 1
+    for (int r = 0; r < kItems; r++) {
+        if (base + r * kThreads >= a.n) break;
+        const uint32_t i = base + r * kThreads + threadIdx.x;
+        const uint16_t st = i < a.n ? a.status[i] : 0;
+        const bool cand = i < a.n && (st & 0xff) == kCodeCandidate;
+        const uint32_t slot = block_rank(cand, s.w, cand_run);
+        bool inl = false, ing = false;
+        if (i < a.n) tuple_fate(a, i, st, slot, inl, ing);
+        const bool sel = a.select_local ? inl : ing;
+        if (!WRITE) {
+            mycnt += sel;
+            if (stats && inl) {
+                const int o = a.given_origin ? a.given_origin[i] : (st >> 8);
+                const unsigned long long w = a.given_w ? (unsigned long long)a.given_w[i] : 1ull;
+                atomicAdd(&s.lsz[o], w);
+                if (ing) atomicAdd(&s.surv[o], w);
+            }
+            if (a.row_flags && i < a.n) a.row_flags[i] = (uint8_t)((inl ? 1 : 0) | (ing ? 2 : 0));
+        } else {
+            const uint32_t pos = block_rank(sel, s.w, out_run);
+            if (sel) {
+                if (a.ids_out) a.ids_out[pos] = a.ids ? a.ids[i] : (int64_t)i;
+                if (a.origin_out) a.origin_out[pos] = a.given_origin ? a.given_origin[i] : (int32_t)(st >> 8);
+                if (a.rows_out)
+                    for (int d = 0; d < a.D; d++) a.rows_out[(size_t)pos * a.D + d] = a.vals[(size_t)i * a.D + d];
+            }
+        }
+    }
+    if (!WRITE) {
+        const uint32_t tot = block_sum(mycnt, s.w);
+        if (threadIdx.x == 0) a.out_cnt[blockIdx.x] = tot;
+        if (stats) {
+            __syncthreads();
+            for (int q = threadIdx.x; q < a.K; q += kThreads) {
+                if (s.lsz[q]) atomicAdd(&a.lsz[q], s.lsz[q]);
+                if (s.surv[q]) atomicAdd(&a.surv[q], s.surv[q]);
+            }
+        }
+    }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_export_reps(uint32_t mr, const T *__restrict__ rep_rows,
+                                                          const uint64_t *__restrict__ rep_key,
+                                                          const uint8_t *__restrict__ alive_l,
+                                                          const uint32_t *__restrict__ alive_scan,
+                                                          const unsigned long long *__restrict__ mult,
+                                                          double *__restrict__ rows_out,
+                                                          int32_t *__restrict__ keys_out,
+                                                          int64_t *__restrict__ mult_out) {
+    constexpr int DP = padded_dims<T>(D);
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= mr || !alive_l[r]) return;
+    const uint32_t e = alive_scan[r];
+    T v[D];
+    load_trow<T, D>(rep_rows + (size_t)r * DP, v);
+#pragma unroll
+    for (int d = 0; d < D; d++) rows_out[(size_t)e * D + d] = (double)v[d];
+    keys_out[e] = (int32_t)(rep_key[r] >> 56);
+    mult_out[e] = (int64_t)mult[r];
+}
+
+// ---- host launchers -----------------------------------------------------------
+static inline unsigned nblk(size_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st) {
+    unsigned g = nblk(n, kThreads);
+    if (g > 4096) g = 4096;
+    if (g == 0) return;
+    SKY_DISPATCH_D(D, (k_keys<DD><<<g, kThreads, 0, st>>>(vals, n, kp, keys)));
+}
+
+void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
+                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, uint32_t *sidx,
+                   hipStream_t st) {
+    if (S == 0) return;
+    SKY_DISPATCH_D(D, (k_sample<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
+                                                                             skey, ssum, sidx)));
+}
+
+void launch_select_pruners(int D, const double *vals, uint32_t S, const int32_t *skey, const double *ssum,
+                           const uint32_t *sidx, int Kp, int M, double *pruners, int32_t *npr, hipStream_t st) {
+    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, kThreads, 0, st>>>(vals, S, skey, ssum, sidx, M, pruners, npr)));
+}
+
+void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double);
+    SKY_DISPATCH_D(D, (k_filter<DD><<<nblk(a.n, kTile), kThreads, lds, st>>>(a)));
+}
+
+void launch_compact(int D, bool f64, const CompactArgs &a, hipStream_t st) {
+    if (f64) { SKY_DISPATCH_D(D, (k_compact<double, DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
+    else { SKY_DISPATCH_D(D, (k_compact<float, DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
+}
+
+void launch_append_pruners(int D, bool f64, const double *pruners, int M, const int32_t *entries, uint32_t nps,
+                           uint32_t m, void *rows, uint64_t *sortkey, uint32_t *slot_src, uint32_t *flags,
+                           hipStream_t st) {
+    if (nps == 0) return;
+    if (f64) {
+        SKY_DISPATCH_D(D, (k_append_pruners<double, DD><<<nblk(nps, 64), 64, 0, st>>>(
+                              pruners, M, entries, nps, m, (double *)rows, sortkey, slot_src, flags)));
+    } else {
+        SKY_DISPATCH_D(D, (k_append_pruners<float, DD><<<nblk(nps, 64), 64, 0, st>>>(
+                              pruners, M, entries, nps, m, (float *)rows, sortkey, slot_src, flags)));
+    }
+}
+
+void launch_gather_runs(int D, bool f64, const RepArgs &a, hipStream_t st) {
+    if (f64) { SKY_DISPATCH_D(D, (k_gather_runs<double, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+    else { SKY_DISPATCH_D(D, (k_gather_runs<float, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+}
+void launch_run_first(const RepArgs &a, hipStream_t st) {
+    k_run_first<<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a);
+}
+void launch_rep_of(int D, bool f64, const RepArgs &a, hipStream_t st) {
+    if (f64) { SKY_DISPATCH_D(D, (k_rep_of<double, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+    else { SKY_DISPATCH_D(D, (k_rep_of<float, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+}
+void launch_build_reps(int D, bool f64, const RepArgs &a, hipStream_t st) {
+    if (f64) { SKY_DISPATCH_D(D, (k_build_reps<double, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+    else { SKY_DISPATCH_D(D, (k_build_reps<float, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
+}
+void launch_seg_bounds(const uint64_t *rep_key, uint32_t mr, uint32_t *seg_begin, uint32_t *seg_end,
+                       hipStream_t st) {
+    if (mr) k_seg_bounds<<<nblk(mr, kThreads), kThreads, 0, st>>>(rep_key, mr, seg_begin, seg_end);
+}
+void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src, const uint32_t *rep_of_sorted,
+                     const int64_t *given_w, const uint32_t *dup_cnt, const int32_t *pr_entries,
+                     unsigned long long *mult, hipStream_t st) {
+    if (mt) k_rep_mult<<<nblk(mt, kThreads), kThreads, 0, st>>>(mt, perm, slot_src, rep_of_sorted, given_w, dup_cnt,
+                                                                pr_entries, mult);
+}
+void launch_out_count(const OutArgs &a, hipStream_t st) {
+    if (a.n) k_out<false><<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
+}
+void launch_out_write(const OutArgs &a, hipStream_t st) {
+    if (a.n) k_out<true><<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
+}
+void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
+                        const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,
+                        double *rows_out, int32_t *keys_out, int64_t *mult_out, hipStream_t st) {
+    if (!mr) return;
+    if (f64) {
+        SKY_DISPATCH_D(D, (k_export_reps<double, DD><<<nblk(mr, kThreads), kThreads, 0, st>>>(
+                              mr, (const double *)rep_rows, rep_key, alive_l, alive_scan, mult, rows_out, keys_out,
+                              mult_out)));
+    } else {
+        SKY_DISPATCH_D(D, (k_export_reps<float, DD><<<nblk(mr, kThreads), kThreads, 0, st>>>(
+                              mr, (const float *)rep_rows, rep_key, alive_l, alive_scan, mult, rows_out, keys_out,
+                              mult_out)));
+    }
+}
+
+}  // namespace sky

@@ -1,0 +1,121 @@
+// k_scan.hip — device-wide exclusive prefix sums (u32), reduce-then-scan.
+// Used for order-preserving stream compaction (candidate slots, output ids)
+// and for the radix-sort digit offsets.  Wave64 scans via __shfl_up.
+#include "sky_internal.h"
+
+namespace sky {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;   // 4096
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// exclusive scan of one value per thread across a 256-thread block
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kScanThreads / 64; i++) {
+        uint32_t c = s_w[i];
+        wbase += i < w ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return wbase + inc - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t *__restrict__ in, size_t n,
+                                                              uint32_t *__restrict__ partial) {
+    __shared__ uint32_t s_w[4];
+    const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) s += base + i < n ? in[base + i] : 0u;
+    uint32_t total;
+    block_excl_scan(s, s_w, total);
+    if (threadIdx.x == 0) partial[blockIdx.x] = total;
+}
+
+// scans `n` items of one tile per block, adding offs[blockIdx.x] (if given)
+__global__ __launch_bounds__(kScanThreads) void k_scan_tile(const uint32_t *__restrict__ in, size_t n,
+                                                            uint32_t *__restrict__ out,
+                                                            const uint32_t *__restrict__ offs,
+                                                            uint32_t *__restrict__ total_out) {
+    __shared__ uint32_t s_w[4];
+    const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) { v[i] = base + i < n ? in[base + i] : 0u; s += v[i]; }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, s_w, total) + (offs ? offs[blockIdx.x] : 0u);
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+    if (total_out && threadIdx.x == kScanThreads - 1 && gridDim.x == 1) *total_out = run;
+}
+
+// single-block scan of a short array (the per-tile partials), in place, writes total
+__global__ __launch_bounds__(1024) void k_scan_small(uint32_t *__restrict__ a, size_t n,
+                                                     uint32_t *__restrict__ total_out) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (size_t base = 0; base < n; base += 1024) {
+        const size_t i = base + threadIdx.x;
+        const uint32_t v = i < n ? a[i] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        uint32_t wbase = 0, tot = 0;
+        for (int k = 0; k < 16; k++) { wbase += k < w ? s_w[k] : 0u; tot += s_w[k]; }
+        const uint32_t carry = s_carry;
+        if (i < n) a[i] = carry + wbase + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = carry + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = s_carry;
+}
+
+// out[i] = sum(in[0..i)), *d_total = sum(in) ; `scratch` needs scan_scratch_words(n) words
+size_t scan_scratch_words(size_t n) {
+    size_t tiles = (n + kScanTile - 1) / kScanTile;
+    return tiles + 64;
+}
+
+void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, uint32_t *scratch,
+                   hipStream_t st) {
+    if (n == 0) {
+        if (d_total) hipMemsetAsync(d_total, 0, 4, st);
+        return;
+    }
+    const size_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles == 1) {
+        k_scan_tile<<<1, kScanThreads, 0, st>>>(in, n, out, nullptr, d_total);
+        return;
+    }
+    uint32_t *partial = scratch;
+    k_scan_reduce<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, partial);
+    k_scan_small<<<1, 1024, 0, st>>>(partial, tiles, d_total);
+    k_scan_tile<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, out, partial, nullptr);
+}
+
+}  // namespace sky

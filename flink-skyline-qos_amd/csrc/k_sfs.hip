@@ -1,0 +1,335 @@
+// k_sfs.hip — the dominance-compare-bound stage: a blocked, segmented SFS.
+//
+// Input: the distinct vectors (representatives) of every partition, sorted by
+// (partition, monotone score).  A dominator always precedes what it dominates
+// in that order (strict score when kFlagScoreTies is clear; equal-score runs are
+// checked both ways otherwise), so per round and per partition:
+//   k_block_sky    the next B candidates X are staged in LDS; each lane tests its
+//                  candidate against the EARLIER ones of X (LDS broadcast reads,
+//                  scalar VALU compares, wave-ballot early exit).  Survivors X' are
+//                  confirmed skyline members.
+//   k_filter_rest  every remaining candidate of the partition is tested against X'
+//                  (X' in LDS, PPT candidates per lane in registers).
+//   k_act_compact  order-preserving compaction of the survivors for the next round.
+// The work is Σ_rounds |R|·|X'| pair tests of D compares each.
+#include "sky_internal.h"
+
+namespace sky {
+
+template <typename T>
+__device__ __forceinline__ uint32_t key_score(uint64_t k) { return (uint32_t)(k >> 24); }
+
+template <typename T, int D, bool FULL>
+__device__ __forceinline__ bool dom_test(const T *x, const T *y) {
+    if constexpr (FULL) return dominates_full<D, T>(x, y);
+    else return dominates_distinct<D, T>(x, y);
+}
+
+template <typename T, int D>
+__device__ __forceinline__ void lds_row(const T *s, T (&v)[D]) {
+#pragma unroll
+    for (int d = 0; d < D; d++) v[d] = s[d];
+}
+
+template <typename T, int D, bool FULL, bool TIES>
+__global__ __launch_bounds__(kThreads) void k_block_sky(const T *__restrict__ rows, const uint64_t *__restrict__ key,
+                                                        const uint32_t *__restrict__ act,
+                                                        const SfsSeg *__restrict__ segs,
+                                                        const uint32_t *__restrict__ seg_list, int B,
+                                                        uint8_t *__restrict__ alive, T *__restrict__ conf_rows,
+                                                        uint32_t *__restrict__ nconf) {
+    constexpr int DP = padded_dims<T>(D);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *s_x = reinterpret_cast<T *>(smem);                               // [B][DP]
+    uint32_t *s_sc = reinterpret_cast<uint32_t *>(s_x + (size_t)B * DP);  // [B]
+    uint32_t *s_keep = s_sc + B;                                         // [B]
+    __shared__ uint32_t s_w[kThreads / 64];
+    const uint32_t k = seg_list[blockIdx.x];
+    const SfsSeg sg = segs[k];
+    const uint32_t xk = sg.count < (uint32_t)B ? sg.count : (uint32_t)B;
+    for (uint32_t q = threadIdx.x; q < xk; q += kThreads) {
+        const uint32_t r = act[sg.begin + q];
+        const T *src = rows + (size_t)r * DP;
+#pragma unroll
+        for (int d = 0; d < DP; d++) s_x[(size_t)q * DP + d] = src[d];
+        s_sc[q] = key_score<T>(key[r]);
+    }
+    __syncthreads();
+    const bool has_rest = sg.count > xk;
+    const uint32_t rest_score = (TIES && has_rest) ? key_score<T>(key[act[sg.begin + xk]]) : 0u;
+    for (uint32_t j0 = 0; j0 < xk; j0 += kThreads) {
+        const uint32_t j = j0 + threadIdx.x;
+        const bool valid = j < xk;
+        T y[D];
+        if (valid) lds_row<T, D>(s_x + (size_t)j * DP, y);
+        else {
+#pragma unroll
+            for (int d = 0; d < D; d++) y[d] = T(0);
+        }
+        bool dom = false;
+        // wave-uniform bound: the largest j of this wave
+        const uint32_t wlast = j0 + (threadIdx.x | 63u);
+        const uint32_t iend = wlast < xk ? wlast : xk - 1;
+        for (uint32_t i = 0; i < iend; i++) {
+            T x[D];
+            lds_row<T, D>(s_x + (size_t)i * DP, x);
+            dom |= (i < j) && dom_test<T, D, FULL>(x, y);
+            if ((i & 15u) == 15u && __ballot(valid && !dom) == 0ull) break;
+        }
+        if constexpr (TIES) {
+            if (valid && !dom) {
+                const uint32_t sj = s_sc[j];
+                for (uint32_t i = j + 1; i < xk && s_sc[i] == sj && !dom; i++) {
+                    T x[D];
+                    lds_row<T, D>(s_x + (size_t)i * DP, x);
+                    dom = dom_test<T, D, true>(x, y);
+                }
+                if (has_rest && sj == rest_score) {
+                    for (uint32_t q = xk; q < sg.count && !dom; q++) {
+                        const uint32_t r = act[sg.begin + q];
+                        if (key_score<T>(key[r]) != sj) break;
+                        T x[D];
+#pragma unroll
+                        for (int d = 0; d < D; d++) x[d] = rows[(size_t)r * DP + d];
+                        dom = dom_test<T, D, true>(x, y);
+                    }
+                }
+            }
+        }
+        if (valid) s_keep[j] = dom ? 0u : 1u;
+    }
+    __syncthreads();
+    // order-preserving compaction of X' into conf_rows[k]
+    uint32_t run = 0;
+    T *conf = conf_rows + (size_t)k * B * DP;
+    for (uint32_t j0 = 0; j0 < xk; j0 += kThreads) {
+        const uint32_t j = j0 + threadIdx.x;
+        const bool keep = j < xk && s_keep[j];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const uint64_t b = __ballot(keep);
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+        if (lane == 0) s_w[w] = __popcll(b);
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+        for (int q = 0; q < kThreads / 64; q++) { wb += q < w ? s_w[q] : 0u; tot += s_w[q]; }
+        __syncthreads();
+        if (keep) {
+            const uint32_t pos = run + wb + __popcll(b & lt);
+#pragma unroll
+            for (int d = 0; d < DP; d++) conf[(size_t)pos * DP + d] = s_x[(size_t)j * DP + d];
+            alive[act[sg.begin + j]] = 1;
+        }
+        run += tot;
+    }
+    if (threadIdx.x == 0) nconf[k] = run;
+}
+
+template <typename T, int D, bool FULL, int PPT>
+__global__ __launch_bounds__(kThreads) void k_filter_rest(const T *__restrict__ rows, const uint32_t *__restrict__ act,
+                                                          const SfsTile *__restrict__ tiles,
+                                                          const T *__restrict__ conf_rows,
+                                                          const uint32_t *__restrict__ nconf, int B,
+                                                          uint32_t *__restrict__ keep) {
+    constexpr int DP = padded_dims<T>(D);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *s_c = reinterpret_cast<T *>(smem);
+    const SfsTile tl = tiles[blockIdx.x];
+    const uint32_t nc = nconf[tl.seg];
+    const T *conf = conf_rows + (size_t)tl.seg * B * DP;
+    for (uint32_t q = threadIdx.x; q < nc * DP; q += kThreads) s_c[q] = conf[q];
+    T y[PPT][D];
+    bool valid[PPT], dom[PPT];
+#pragma unroll
+    for (int p = 0; p < PPT; p++) {
+        const uint32_t e = threadIdx.x + p * kThreads;
+        valid[p] = e < tl.count;
+        dom[p] = false;
+        if (valid[p]) {
+            const T *src = rows + (size_t)act[tl.start + e] * DP;
+#pragma unroll
+            for (int d = 0; d < D; d++) y[p][d] = src[d];
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; d++) y[p][d] = T(0);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < nc; i++) {
+        T x[D];
+        lds_row<T, D>(s_c + (size_t)i * DP, x);
+#pragma unroll
+        for (int p = 0; p < PPT; p++) dom[p] |= dom_test<T, D, FULL>(x, y[p]);
+        if ((i & 7u) == 7u) {
+            bool live = false;
+#pragma unroll
+            for (int p = 0; p < PPT; p++) live |= valid[p] && !dom[p];
+            if (__ballot(live) == 0ull) break;
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < PPT; p++) {
+        const uint32_t e = threadIdx.x + p * kThreads;
+        if (valid[p]) keep[tl.out + e] = dom[p] ? 0u : 1u;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_act_compact(const uint32_t *__restrict__ act_old,
+                                                          const uint32_t *__restrict__ keep,
+                                                          const uint32_t *__restrict__ keep_scan,
+                                                          const SfsTile *__restrict__ tiles,
+                                                          uint32_t *__restrict__ act_new,
+                                                          uint32_t *__restrict__ segcnt) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    const SfsTile tl = tiles[blockIdx.x];
+    uint32_t c = 0;
+    for (uint32_t e = threadIdx.x; e < tl.count; e += kThreads)
+        if (keep[tl.out + e]) { act_new[keep_scan[tl.out + e]] = act_old[tl.start + e]; c++; }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) c += __shfl_xor(c, s, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < kThreads / 64; i++) t += s_w[i];
+        if (t) atomicAdd(&segcnt[tl.seg], t);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_iota(uint32_t *__restrict__ a, uint32_t n) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j < n) a[j] = j;
+}
+
+// global merge ordering: (score | rep index) for the alive local representatives
+__global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__restrict__ rep_key,
+                                                          const uint8_t *__restrict__ alive_l,
+                                                          const uint32_t *__restrict__ alive_scan, uint32_t mr,
+                                                          uint64_t *__restrict__ gkey, uint32_t *__restrict__ gval) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= mr || !alive_l[r]) return;
+    const uint32_t e = alive_scan[r];
+    gkey[e] = rep_key[r] & 0x00ffffffff000000ull;   // score field only (same layout as rep_key)
+    gval[e] = r;
+}
+
+__global__ __launch_bounds__(kThreads) void k_import_flags(const uint8_t *__restrict__ alive_l,
+                                                           const uint32_t *__restrict__ alive_scan, uint32_t mr,
+                                                           const uint8_t *__restrict__ union_flags,
+                                                           uint32_t self_offset, uint8_t *__restrict__ alive_g) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= mr) return;
+    alive_g[r] = alive_l[r] ? ((union_flags[self_offset + alive_scan[r]] & 2u) ? 1 : 0) : 0;
+}
+
+void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
+                         uint32_t self_offset, uint8_t *alive_g, hipStream_t st) {
+    if (mr) k_import_flags<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(alive_l, alive_scan, mr, union_flags,
+                                                                                self_offset, alive_g);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_gather_rows(const T *__restrict__ src, const uint32_t *__restrict__ idx,
+                                                          uint32_t m, T *__restrict__ dst) {
+    constexpr int DP = padded_dims<T>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= m) return;
+    const T *s = src + (size_t)idx[j] * DP;
+    T *o = dst + (size_t)j * DP;
+#pragma unroll
+    for (int d = 0; d < DP; d++) o[d] = s[d];
+}
+
+__global__ __launch_bounds__(kThreads) void k_scatter_alive(const uint32_t *__restrict__ gval,
+                                                            const uint8_t *__restrict__ galive, uint32_t mg,
+                                                            uint8_t *__restrict__ alive_g) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j < mg) alive_g[gval[j]] = galive[j];
+}
+
+__global__ __launch_bounds__(kThreads) void k_u8_to_u32(const uint8_t *__restrict__ in, uint32_t n,
+                                                        uint32_t *__restrict__ out) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j < n) out[j] = in[j] ? 1u : 0u;
+}
+
+// ---- launchers ------------------------------------------------------------------
+static inline unsigned nb(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
+
+template <typename T, int D>
+static void block_sky_t(bool full, bool ties, int B, const void *rows, const uint64_t *key, const uint32_t *act,
+                        const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work, uint8_t *alive,
+                        void *conf_rows, uint32_t *nconf, hipStream_t st) {
+    constexpr int DP = padded_dims<T>(D);
+    const size_t lds = (size_t)B * DP * sizeof(T) + 2 * (size_t)B * sizeof(uint32_t);
+    const T *r = (const T *)rows;
+    T *c = (T *)conf_rows;
+    if (full) {
+        if (ties) k_block_sky<T, D, true, true><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+        else k_block_sky<T, D, true, false><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+    } else {
+        if (ties) k_block_sky<T, D, false, true><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+        else k_block_sky<T, D, false, false><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+    }
+}
+
+void launch_block_sky(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+                      const uint32_t *act, const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work,
+                      uint8_t *alive, void *conf_rows, uint32_t *nconf, hipStream_t st) {
+    if (!nseg_work) return;
+    if (f64) { SKY_DISPATCH_D(D, (block_sky_t<double, DD>(full, ties, B, rows, key, act, segs, seg_list, nseg_work, alive, conf_rows, nconf, st))); }
+    else { SKY_DISPATCH_D(D, (block_sky_t<float, DD>(full, ties, B, rows, key, act, segs, seg_list, nseg_work, alive, conf_rows, nconf, st))); }
+}
+
+constexpr int kPPT = 4;
+
+template <typename T, int D>
+static void filter_rest_t(bool full, int B, const void *rows, const uint32_t *act, const SfsTile *tiles,
+                          uint32_t ntiles, const void *conf_rows, const uint32_t *nconf, uint32_t *keep,
+                          hipStream_t st) {
+    constexpr int DP = padded_dims<T>(D);
+    const size_t lds = (size_t)B * DP * sizeof(T);
+    if (full)
+        k_filter_rest<T, D, true, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, (const T *)conf_rows, nconf, B, keep);
+    else
+        k_filter_rest<T, D, false, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, (const T *)conf_rows, nconf, B, keep);
+}
+
+void launch_filter_rest(int D, bool f64, bool full, int B, const void *rows, const uint32_t *act,
+                        const SfsTile *tiles, uint32_t ntiles, const void *conf_rows, const uint32_t *nconf,
+                        uint32_t *keep, hipStream_t st) {
+    if (!ntiles) return;
+    if (f64) { SKY_DISPATCH_D(D, (filter_rest_t<double, DD>(full, B, rows, act, tiles, ntiles, conf_rows, nconf, keep, st))); }
+    else { SKY_DISPATCH_D(D, (filter_rest_t<float, DD>(full, B, rows, act, tiles, ntiles, conf_rows, nconf, keep, st))); }
+}
+
+void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uint32_t *keep_scan,
+                        const SfsTile *tiles, uint32_t ntiles, uint32_t *act_new, uint32_t *segcnt, hipStream_t st) {
+    if (ntiles) k_act_compact<<<ntiles, kThreads, 0, st>>>(act_old, keep, keep_scan, tiles, act_new, segcnt);
+}
+
+void launch_iota(uint32_t *a, uint32_t n, hipStream_t st) {
+    if (n) k_iota<<<nb(n), kThreads, 0, st>>>(a, n);
+}
+
+void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
+                        uint64_t *gkey, uint32_t *gval, hipStream_t st) {
+    if (mr) k_global_keys<<<nb(mr), kThreads, 0, st>>>(rep_key, alive_l, alive_scan, mr, gkey, gval);
+}
+
+void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, uint32_t m, void *dst,
+                        hipStream_t st) {
+    if (!m) return;
+    if (f64) { SKY_DISPATCH_D(D, (k_gather_rows<double, DD><<<nb(m), kThreads, 0, st>>>((const double *)src, idx, m, (double *)dst))); }
+    else { SKY_DISPATCH_D(D, (k_gather_rows<float, DD><<<nb(m), kThreads, 0, st>>>((const float *)src, idx, m, (float *)dst))); }
+}
+
+void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t mg, uint8_t *alive_g,
+                          hipStream_t st) {
+    if (mg) k_scatter_alive<<<nb(mg), kThreads, 0, st>>>(gval, galive, mg, alive_g);
+}
+
+void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st) {
+    if (n) k_u8_to_u32<<<nb(n), kThreads, 0, st>>>(in, n, out);
+}
+
+}  // namespace sky

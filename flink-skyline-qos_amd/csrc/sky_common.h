@@ -1,0 +1,28 @@
+// sky_common.h — constants shared by host orchestration and gfx950 kernels.
+#pragma once
+#include <stdint.h>
+#include "../../include/skyline_hip.h"
+
+namespace sky {
+
+constexpr int kMaxD = SKY_MAX_DIMS;
+constexpr int kMaxK = SKY_MAX_PARTITIONS;
+constexpr int kThreads = 256;                 // 4 waves of 64
+constexpr int kItems = 8;                     // tuples per thread per tile
+constexpr int kTile = kThreads * kItems;      // 2048 tuples per workgroup tile
+
+// per-tuple status word (u16): high byte = partition key, low byte = code
+constexpr uint16_t kCodeDropped = 0;          // dominated by a pruner / key never queried
+constexpr uint16_t kCodeCandidate = 255;      // goes to sort + SFS
+// codes 1..254: exact duplicate of pruner (code-1) of its partition
+
+// flag bits (device u32)
+constexpr uint32_t kFlagNotF32 = 1u;          // some candidate value is not exactly an f32
+constexpr uint32_t kFlagNaN = 2u;             // a NaN was seen
+constexpr uint32_t kFlagScoreTies = 4u;       // score key is not strictly monotone
+
+// padded row width in elements so every row starts 16-byte aligned
+template <typename T>
+constexpr int padded_dims(int D) { return sizeof(T) == 4 ? (D + 3) & ~3 : (D + 1) & ~1; }
+
+}  // namespace sky

@@ -1,0 +1,192 @@
+// sky_device.h — device-side building blocks shared by the gfx950 kernels.
+//
+// * Java narrowing (int) of a double (JLS 5.1.3)
+// * fdlibm 5.3 atan / atan2 (what java.lang.Math.atan2 delegates to in JDK 11)
+// * the three partitioner key functions, bit-exact with
+//   /root/reference/java/org.main/FlinkSkyline.java (Dim :707-712, Grid :774-789,
+//   Angle :827-875).  Built with -ffp-contract=off: Java never fuses a*b+c.
+// * dominance (ServiceTuple.java:67-77)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sky_common.h"
+
+namespace sky {
+
+__device__ __forceinline__ int32_t java_d2i(double x) {
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return 2147483647;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
+// ---- fdlibm s_atan.c / e_atan2.c ------------------------------------------
+__device__ __forceinline__ double fd_atan(double x) {
+    constexpr double hi0 = 4.63647609000806093515e-01, hi1 = 7.85398163397448278999e-01,
+                     hi2 = 9.82793723247329054082e-01, hi3 = 1.57079632679489655800e+00;
+    constexpr double lo0 = 2.26987774529616870924e-17, lo1 = 3.06161699786838301793e-17,
+                     lo2 = 1.39033110312309984516e-17, lo3 = 6.12323399573676603587e-17;
+    constexpr double a0 = 3.33333333333329318027e-01, a1 = -1.99999999998764832476e-01,
+                     a2 = 1.42857142725034663711e-01, a3 = -1.11111104054623557880e-01,
+                     a4 = 9.09088713343650656196e-02, a5 = -7.69187620504482999495e-02,
+                     a6 = 6.66107313738753120669e-02, a7 = -5.83357013379057348645e-02,
+                     a8 = 4.97687799461593236017e-02, a9 = -3.65315727442169155270e-02,
+                     a10 = 1.62858201153657823623e-02;
+    const int32_t hx = __double2hiint(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) {                              // |x| >= 2^66
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && __double2loint(x) != 0)) return x + x;
+        return hx > 0 ? hi3 + lo3 : -hi3 - lo3;
+    }
+    if (ix < 0x3fdc0000) {                               // |x| < 0.4375
+        if (ix < 0x3e200000) return x;                   // |x| < 2^-29 (inexact flag ignored)
+        id = -1;
+    } else {
+        x = fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+            else                 { id = 1; x = (x - 1.0) / (x + 1.0); }
+        } else {
+            if (ix < 0x40038000) { id = 2; x = (x - 1.5) / (1.0 + 1.5 * x); }
+            else                 { id = 3; x = -1.0 / x; }
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (a0 + w * (a2 + w * (a4 + w * (a6 + w * (a8 + w * a10)))));
+    const double s2 = w * (a1 + w * (a3 + w * (a5 + w * (a7 + w * a9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double hi = id == 0 ? hi0 : id == 1 ? hi1 : id == 2 ? hi2 : hi3;
+    const double lo = id == 0 ? lo0 : id == 1 ? lo1 : id == 2 ? lo2 : lo3;
+    const double r = hi - ((x * (s1 + s2) - lo) - x);
+    return hx < 0 ? -r : r;
+}
+
+__device__ __forceinline__ double fd_atan2(double y, double x) {
+    constexpr double tiny = 1.0e-300;
+    constexpr double pi_o_4 = 7.8539816339744827900E-01, pi_o_2 = 1.5707963267948965580E+00,
+                     pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    const int32_t hx = __double2hiint(x), ix = hx & 0x7fffffff;
+    const uint32_t lx = (uint32_t)__double2loint(x);
+    const int32_t hy = __double2hiint(y), iy = hy & 0x7fffffff;
+    const uint32_t ly = (uint32_t)__double2loint(y);
+    if (((uint32_t)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u ||
+        ((uint32_t)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
+        return x + y;
+    if (((hx - 0x3ff00000) | (int32_t)lx) == 0) return fd_atan(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if ((iy | (int32_t)ly) == 0) {
+        if (m <= 1) return y;
+        return m == 2 ? pi + tiny : -pi - tiny;
+    }
+    if ((ix | (int32_t)lx) == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7ff00000) {
+        if (iy == 0x7ff00000) {
+            switch (m) {
+                case 0: return pi_o_4 + tiny;
+                case 1: return -pi_o_4 - tiny;
+                case 2: return 3.0 * pi_o_4 + tiny;
+                default: return -3.0 * pi_o_4 - tiny;
+            }
+        }
+        switch (m) {
+            case 0: return 0.0;
+            case 1: return -0.0;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7ff00000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = pi_o_2 + 0.5 * pi_lo;               // original fdlibm (JDK): no m &= 1
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = fd_atan(fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// ---- partition keys ----------------------------------------------------------
+struct KeyParams {
+    int algo;          // SKY_ALGO_*
+    int P;             // partitions
+    int K;             // queried key space: keys >= K are dropped (reference MR-Grid)
+    double dim_width;  // maxVal / partitions  (:710)
+    double grid_mid;   // maxVal / 2.0          (:756)
+};
+
+template <int D>
+__device__ __forceinline__ int32_t partition_key(const double (&v)[D], const KeyParams &kp) {
+    if (kp.algo == SKY_ALGO_DIM) {
+        int32_t p = java_d2i(v[0] / kp.dim_width);
+        p = p > kp.P - 1 ? kp.P - 1 : p;
+        return p < 0 ? 0 : p;
+    }
+    if (kp.algo == SKY_ALGO_GRID) {
+        uint32_t mask = 0;
+#pragma unroll
+        for (int i = 0; i < D; i++)
+            if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
+        return (int32_t)mask;
+    }
+    if (D < 2) return 0;
+    constexpr double max_angle = 3.141592653589793 / 2.0;
+    double normalized = 0.0;
+#pragma unroll
+    for (int i = 0; i < D - 1; i++) {
+        double s = 0.0;
+#pragma unroll
+        for (int j = i + 1; j < D; j++) s = s + v[j] * v[j];   // ascending j, no FMA
+        const double hyp = sqrt(s);
+        normalized = normalized + fd_atan2(hyp, v[i]) / max_angle;
+    }
+    const double avg = normalized / (double)(D - 1);
+    int32_t p = java_d2i(avg * (double)kp.P);
+    p = p > kp.P - 1 ? kp.P - 1 : p;
+    return p < 0 ? 0 : p;
+}
+
+// ---- dominance ----------------------------------------------------------------
+// a dominates b (ServiceTuple.java:67-77): all a<=b and some a<b.  With NaN-free
+// rows the early-exit loop and this branch-free form agree.
+template <int D, typename T>
+__device__ __forceinline__ bool dominates_full(const T *a, const T *b) {
+    bool le = true, lt = false;
+#pragma unroll
+    for (int d = 0; d < D; d++) { le &= a[d] <= b[d]; lt |= a[d] < b[d]; }
+    return le && lt;
+}
+// For rows known to be DISTINCT vectors (representatives of one partition),
+// "all a <= b" already implies some a < b: D compares per pair.
+template <int D, typename T>
+__device__ __forceinline__ bool dominates_distinct(const T *a, const T *b) {
+    bool le = true;
+#pragma unroll
+    for (int d = 0; d < D; d++) le &= a[d] <= b[d];
+    return le;
+}
+template <int D, typename T>
+__device__ __forceinline__ bool rows_equal(const T *a, const T *b) {
+    bool eq = true;
+#pragma unroll
+    for (int d = 0; d < D; d++) eq &= a[d] == b[d];
+    return eq;
+}
+
+// order-preserving map f32 -> u32 (-0.0 canonicalised to +0.0)
+__device__ __forceinline__ uint32_t f32_order_key(float f) {
+    uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+    return h;
+}
+
+}  // namespace sky

@@ -1,0 +1,163 @@
+// sky_internal.h — host-side declarations shared by the kernel translation units
+// and the engine.  Nothing here is part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "sky_common.h"
+#include "sky_device.h"
+
+#define SKY_DISPATCH_D(D, BODY)                                                    \
+    switch (D) {                                                                   \
+        case 1: { constexpr int DD = 1; BODY; } break;                             \
+        case 2: { constexpr int DD = 2; BODY; } break;                             \
+        case 3: { constexpr int DD = 3; BODY; } break;                             \
+        case 4: { constexpr int DD = 4; BODY; } break;                             \
+        case 5: { constexpr int DD = 5; BODY; } break;                             \
+        case 6: { constexpr int DD = 6; BODY; } break;                             \
+        case 7: { constexpr int DD = 7; BODY; } break;                             \
+        case 8: { constexpr int DD = 8; BODY; } break;                             \
+        case 9: { constexpr int DD = 9; BODY; } break;                             \
+        case 10: { constexpr int DD = 10; BODY; } break;                           \
+        case 11: { constexpr int DD = 11; BODY; } break;                           \
+        case 12: { constexpr int DD = 12; BODY; } break;                           \
+        case 13: { constexpr int DD = 13; BODY; } break;                           \
+        case 14: { constexpr int DD = 14; BODY; } break;                           \
+        case 15: { constexpr int DD = 15; BODY; } break;                           \
+        case 16: { constexpr int DD = 16; BODY; } break;                           \
+        default: break;                                                            \
+    }
+
+namespace sky {
+
+// ---- k_scan.hip ----
+size_t scan_scratch_words(size_t n);
+void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, uint32_t *scratch,
+                   hipStream_t st);
+
+// ---- k_radix.hip ----
+size_t radix_scratch_words(size_t m);
+bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
+                      uint64_t varying_bits, uint32_t *scratch, hipStream_t st);
+void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st);
+
+// ---- k_partition.hip ----
+struct FilterArgs {
+    const double *vals;           // n x D row-major f64 (the boundary format)
+    uint32_t n;
+    KeyParams kp;
+    const int32_t *given_keys;    // partition key per tuple (nullptr: computed by kp.algo)
+    int single;                   // 1: every tuple is partition 0 (merge / part state)
+    const double *pruners;        // [Kp][M][D]
+    const int32_t *npr;           // [Kp]
+    int M, Kp;
+    uint16_t *status;             // [n]
+    uint32_t *blk_cnt;            // [tiles] candidates per tile
+    uint32_t *dup_cnt;            // [Kp*M]
+    uint32_t *flags;              // kFlag*
+};
+void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
+void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
+                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, uint32_t *sidx,
+                   hipStream_t st);
+void launch_select_pruners(int D, const double *vals, uint32_t S, const int32_t *skey, const double *ssum,
+                           const uint32_t *sidx, int Kp, int M, double *pruners, int32_t *npr, hipStream_t st);
+void launch_filter(int D, const FilterArgs &a, hipStream_t st);
+
+struct CompactArgs {
+    const double *vals;
+    uint32_t n;
+    const uint16_t *status;
+    const uint32_t *blk_off;      // exclusive scan of blk_cnt
+    void *rows;                   // [mt][DP] T
+    uint64_t *sortkey;            // [mt]
+    uint32_t *slot_src;           // [mt] source tuple index (bit31: pruner entry)
+    uint32_t *flags;
+};
+void launch_compact(int D, bool f64, const CompactArgs &a, hipStream_t st);
+void launch_append_pruners(int D, bool f64, const double *pruners, int M, const int32_t *entries /*k*M+j*/,
+                           uint32_t nps, uint32_t m, void *rows, uint64_t *sortkey, uint32_t *slot_src,
+                           uint32_t *flags, hipStream_t st);
+
+struct RepArgs {
+    uint32_t mt;                  // sorted slots
+    const uint32_t *perm;         // sorted position -> slot
+    const uint64_t *skey;         // sorted keys
+    const void *rows;             // [mt][DP] by slot
+    void *rows_sorted;            // [mt][DP] by sorted position
+    uint32_t *runflag, *runscan, *run_first, *repof, *repflag, *repscan;
+    void *rep_rows;               // [mr][DP]
+    uint64_t *rep_key;            // [mr]
+    uint32_t *rep_of_sorted;      // [mt]
+    uint32_t *slot_rep;           // [mt]
+};
+void launch_gather_runs(int D, bool f64, const RepArgs &a, hipStream_t st);
+void launch_run_first(const RepArgs &a, hipStream_t st);
+void launch_rep_of(int D, bool f64, const RepArgs &a, hipStream_t st);
+void launch_build_reps(int D, bool f64, const RepArgs &a, hipStream_t st);
+void launch_seg_bounds(const uint64_t *rep_key, uint32_t mr, uint32_t *seg_begin, uint32_t *seg_end,
+                       hipStream_t st);
+void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src, const uint32_t *rep_of_sorted,
+                     const int64_t *given_w, const uint32_t *dup_cnt, const int32_t *pr_entries,
+                     unsigned long long *mult, hipStream_t st);
+
+struct OutArgs {
+    const uint16_t *status;
+    uint32_t n;
+    const uint32_t *blk_off;      // candidate slot base per tile
+    const uint32_t *slot_rep;     // [m + nps]
+    uint32_t m;
+    const int32_t *pruner_slot;   // [Kp*M] -> slot index (m + e) or -1
+    int M;
+    const uint8_t *alive_l, *alive_g;   // per rep
+    const int32_t *given_origin;  // per tuple origin (nullptr: partition key)
+    const int64_t *given_w;       // per tuple weight (nullptr: 1)
+    int K;                        // stats slots
+    unsigned long long *lsz, *surv;   // [K]
+    uint32_t *out_cnt;            // [tiles]
+    const uint32_t *out_off;      // [tiles] (write pass)
+    const int64_t *ids;           // nullptr: ids are the tuple index
+    const double *vals;           // for rows_out
+    int D;
+    int64_t *ids_out;
+    int32_t *origin_out;
+    double *rows_out;
+    uint8_t *row_flags;           // optional per tuple: bit0 inL, bit1 inG
+    int select_local;             // output tuples in L instead of G
+};
+void launch_out_count(const OutArgs &a, hipStream_t st);
+void launch_out_write(const OutArgs &a, hipStream_t st);
+void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
+                        const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,
+                        double *rows_out, int32_t *keys_out, int64_t *mult_out, hipStream_t st);
+
+// ---- k_sfs.hip ----
+struct SfsSeg { uint32_t begin, count; };
+struct SfsTile { uint32_t seg, start, count, out; };
+void launch_block_sky(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+                      const uint32_t *act, const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work,
+                      uint8_t *alive, void *conf_rows, uint32_t *nconf, hipStream_t st);
+void launch_filter_rest(int D, bool f64, bool full, int B, const void *rows, const uint32_t *act,
+                        const SfsTile *tiles, uint32_t ntiles, const void *conf_rows, const uint32_t *nconf,
+                        uint32_t *keep, hipStream_t st);
+void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uint32_t *keep_scan,
+                        const SfsTile *tiles, uint32_t ntiles, uint32_t *act_new, uint32_t *segcnt,
+                        hipStream_t st);
+void launch_iota(uint32_t *a, uint32_t n, hipStream_t st);
+void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
+                         uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
+void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
+                        uint64_t *gkey, uint32_t *gval, hipStream_t st);
+void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, uint32_t m, void *dst,
+                        hipStream_t st);
+void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t mg, uint8_t *alive_g,
+                          hipStream_t st);
+void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
+
+// ---- k_synth.hip ----
+void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
+                  int64_t *ids, hipStream_t st);
+void synth_host(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
+                int64_t *ids);
+
+}  // namespace sky

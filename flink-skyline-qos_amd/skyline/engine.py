@@ -1,0 +1,170 @@
+"""Python handle over one sky_ctx (one MI355X).
+
+Host-buffer methods take numpy arrays; `*_dev` methods take torch CUDA tensors
+(HBM-resident) and pass their data pointers through the C ABI.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _tptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class SkylineEngine:
+    """One context = one device, D dims, P partitions, one partitioner.
+
+    Mirrors the job-level knobs of FlinkSkyline.main (FlinkSkyline.java:66-76):
+    algo (--algo), domain (--domain), dims (--dims), num_partitions = 2 x parallelism.
+    """
+
+    def __init__(self, dims, num_partitions, algo="mr-angle", domain=1000.0, device=0,
+                 semantics="reference"):
+        if isinstance(algo, str):
+            algo = _abi.ALGOS.get(algo.lower(), _abi.ALGO_ANGLE)  # reference default branch (:129-133)
+        self.dims = int(dims)
+        self.P = int(num_partitions)
+        self.algo = int(algo)
+        self.domain = float(domain)
+        h = ctypes.c_void_p()
+        dev = (ctypes.c_int32 * 1)(device)
+        check(lib().sky_ctx_create(dev, 1, self.dims, self.P, self.algo, self.domain, ctypes.byref(h)))
+        self.h = h
+        if semantics != "reference":
+            check(lib().sky_ctx_set_semantics(self.h, _abi.SEM_COMPLETE))
+        self.K = self.P if not (self.algo == _abi.ALGO_GRID and semantics == "complete") else max(self.P, 1 << self.dims)
+
+    def close(self):
+        if self.h:
+            lib().sky_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- partitioners ----------------------------------------------------------
+    def partition_keys(self, values):
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.dims)
+        out = np.empty(len(v), np.int32)
+        check(lib().sky_partition_keys(self.h, _ptr(v), len(v), _ptr(out)))
+        return out
+
+    def partition_keys_dev(self, d_values, d_keys_out):
+        n = d_values.numel() // self.dims
+        check(lib().sky_partition_keys_dev(self.h, _tptr(d_values), n, _tptr(d_keys_out)))
+
+    # ---- fused query ---------------------------------------------------------------
+    def query(self, values, ids=None):
+        """Global skyline of the whole stream (trigger after the last tuple).
+        Returns (ids, origin) in stream order."""
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.dims)
+        n = len(v)
+        idv = None if ids is None else np.ascontiguousarray(ids, dtype=np.int64)
+        cnt = ctypes.c_int64(0)
+        out_ids = np.empty(max(n, 1), np.int64)
+        out_org = np.empty(max(n, 1), np.int32)
+        check(lib().sky_query(self.h, _ptr(idv), _ptr(v), n, _ptr(out_ids), _ptr(out_org), n, ctypes.byref(cnt)))
+        g = cnt.value
+        return out_ids[:g].copy(), out_org[:g].copy()
+
+    def query_dev(self, d_ids, d_values, d_ids_out, d_origin_out, cap):
+        n = d_values.numel() // self.dims
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_query_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_ids_out),
+                                  _tptr(d_origin_out), cap, ctypes.byref(cnt)))
+        return cnt.value
+
+    def stats(self):
+        """(local_sizes[K], survivors[K]) of the last query/merge (FlinkSkyline.java:593-608)."""
+        k = ctypes.c_int32(0)
+        check(lib().sky_global_stats(self.h, None, None, ctypes.byref(k)))
+        ls = np.zeros(max(k.value, 1), np.int64)
+        sv = np.zeros(max(k.value, 1), np.int64)
+        check(lib().sky_global_stats(self.h, _ptr(ls), _ptr(sv), ctypes.byref(k)))
+        return ls[:k.value], sv[:k.value]
+
+    # ---- global merge of local lists ------------------------------------------------
+    def global_merge(self, part_ids, ids_lists, values_lists):
+        n = len(part_ids)
+        vals = [np.ascontiguousarray(v, dtype=np.float64).reshape(-1, self.dims) for v in values_lists]
+        idl = [np.ascontiguousarray(i, dtype=np.int64) for i in ids_lists]
+        counts = np.array([len(v) for v in vals], np.int64)
+        pids = np.ascontiguousarray(part_ids, dtype=np.int32)
+        vp = (ctypes.c_void_p * max(n, 1))(*[v.ctypes.data for v in vals])
+        ip = (ctypes.c_void_p * max(n, 1))(*[i.ctypes.data for i in idl])
+        tot = int(counts.sum())
+        out_ids = np.empty(max(tot, 1), np.int64)
+        out_org = np.empty(max(tot, 1), np.int32)
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_global_merge(self.h, n, _ptr(pids), ip, vp, _ptr(counts), _ptr(out_ids), _ptr(out_org),
+                                     tot, ctypes.byref(cnt)))
+        g = cnt.value
+        return out_ids[:g].copy(), out_org[:g].copy()
+
+    # ---- multi-GPU phases ----------------------------------------------------------------
+    def export_local_dev(self, d_ids, d_values):
+        n = d_values.numel() // self.dims
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_export_local_dev(self.h, _tptr(d_ids), _tptr(d_values), n, ctypes.byref(cnt)))
+        return cnt.value
+
+    def export_copy_dev(self, d_rows, d_keys, d_mult, cap):
+        check(lib().sky_export_copy_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), cap))
+
+    def import_union_dev(self, d_rows, d_keys, d_mult, n_union, self_offset, d_ids_out, d_origin_out, cap):
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_import_union_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), n_union, self_offset,
+                                         _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(cnt)))
+        return cnt.value
+
+    # ---- utilities -----------------------------------------------------------------------
+    def synth_dev(self, dist, n, d_values, d_ids=None, seed=1234, id0=0, dmin=0, dmax=1000):
+        if isinstance(dist, str):
+            dist = _abi.DISTS[dist]
+        check(lib().sky_synth_dev(self.h, dist, dmin, dmax, seed, id0, n, _tptr(d_values), _tptr(d_ids)))
+
+    def set_stream(self, stream_ptr):
+        check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def sync(self):
+        check(lib().sky_ctx_sync(self.h))
+
+    def profile(self, on=True):
+        check(lib().sky_profile_enable(self.h, 1 if on else 0))
+
+    def profile_reset(self):
+        check(lib().sky_profile_reset(self.h))
+
+    def phases(self):
+        ms = np.zeros(8, np.float64)
+        cnt = np.zeros(8, np.int64)
+        check(lib().sky_profile_phases(self.h, _ptr(ms), _ptr(cnt)))
+        return dict(zip(_abi.PHASES, ms.tolist())), cnt
+
+    def kernel_time(self, name):
+        ms = ctypes.c_double(0)
+        la = ctypes.c_int64(0)
+        un = ctypes.c_int64(0)
+        check(lib().sky_profile_kernel(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(la), ctypes.byref(un)))
+        return ms.value, la.value, un.value
+
+
+def synth_host(dist, dims, n, seed=1234, id0=0, dmin=0, dmax=1000):
+    """Host copy of the device generator (same values bit for bit)."""
+    if isinstance(dist, str):
+        dist = _abi.DISTS[dist]
+    v = np.empty((n, dims), np.float64)
+    ids = np.empty(n, np.int64)
+    check(lib().sky_synth(dist, dims, dmin, dmax, seed, id0, n, _ptr(v), _ptr(ids)))
+    return v, ids

@@ -1,0 +1,358 @@
+"""Host-side mirror of the reference's operator surface, running on libskyline_hip.
+
+Same class and method names, argument meaning and error behaviour as
+/root/reference/java/org.main/FlinkSkyline.java and ServiceTuple.java, so that a
+caller of the Java operators finds the same API.  The dominance work (BNL in the
+reference) always runs in the library on the GPU; this module only keeps the
+operator protocol: buffering, the id barrier, the trigger fan-out, the arrival
+count and the JSON payload.
+
+Deliberate, documented differences:
+  * the input buffer is per key (the reference's is shared by every key of a
+    subtask, FlinkSkyline.java:223,244 — it moves tuples between keys);
+  * the JSON carries "query_latency_ms" (computed but never emitted by the
+    reference, :588 vs :632-641);
+  * NaN values raise (the reference's BNL result is order-dependent for NaN).
+"""
+import ctypes
+import decimal
+import time
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, lib
+from .engine import SkylineEngine
+
+
+def now_ms():
+    return int(time.time() * 1000)
+
+
+def java_format_4f(x):
+    """String.format(Locale.US, "%.4f", x): Java rounds HALF_UP on the shortest
+    decimal representation of the double (FormattedFloatingDecimal)."""
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Infinity" if x > 0 else "-Infinity"
+    d = decimal.Decimal(repr(float(x)))
+    return str(d.quantize(decimal.Decimal("0.0001"), rounding=decimal.ROUND_HALF_UP))
+
+
+class ServiceTuple:
+    """ServiceTuple.java:15-115 (data model; dominance is evaluated on the device)."""
+
+    __slots__ = ("id", "values", "originPartition")
+
+    def __init__(self, id=None, values=None):
+        self.id = id
+        self.values = values
+        self.originPartition = -1
+
+    @staticmethod
+    def fromString(s):
+        """ServiceTuple.fromString (:89-104): "id,v1,...,vD" -> tuple, None if malformed."""
+        try:
+            p = s.split(",")
+            if len(p) < 2:
+                return None
+            return ServiceTuple(p[0], [_java_parse_double(x) for x in p[1:]])
+        except Exception:
+            return None
+
+    def __repr__(self):
+        return "ID:" + str(self.id) + " " + str(self.values)
+
+
+def _java_parse_double(s):
+    t = s.strip()
+    if t in ("NaN", "+NaN", "-NaN"):
+        return float("nan")
+    if t.endswith(("d", "D", "f", "F")):
+        t = t[:-1]
+    if t.lower() in ("inf", "+inf", "-inf", "infinity", "+infinity", "-infinity", "nan"):
+        if t in ("Infinity", "+Infinity"):
+            return float("inf")
+        if t == "-Infinity":
+            return float("-inf")
+        raise ValueError(s)
+    return float(t)
+
+
+class PartitioningLogic:
+    """FlinkSkyline.PartitioningLogic (:669-877).  getKey runs the bit-exact device
+    key function; getKeys batches a whole array (the form the operators use)."""
+
+    class SkylinePartitioner:
+        algo = _abi.ALGO_ANGLE
+
+        def __init__(self, partitions, dims, maxVal=1000.0, device=0):
+            self.partitions = int(partitions)
+            self.dims = int(dims)
+            self.engine = SkylineEngine(dims, partitions, self.algo, maxVal, device)
+
+        def getKey(self, t):
+            if len(t.values) != self.dims:
+                raise IndexError("tuple has %d values, partitioner expects %d" % (len(t.values), self.dims))
+            return int(self.engine.partition_keys(np.asarray(t.values, np.float64))[0])
+
+        def getKeys(self, values):
+            return self.engine.partition_keys(values)
+
+    class DimPartitioner(SkylinePartitioner):
+        algo = _abi.ALGO_DIM
+
+        def __init__(self, partitions, maxVal, dims=1, device=0):
+            super().__init__(partitions, dims, maxVal, device)
+
+    class GridPartitioner(SkylinePartitioner):
+        algo = _abi.ALGO_GRID
+
+        def __init__(self, partitions, maxVal, dims, device=0):
+            super().__init__(partitions, dims, maxVal, device)
+
+    class AnglePartitioner(SkylinePartitioner):
+        algo = _abi.ALGO_ANGLE
+
+        def __init__(self, partitions, dims, device=0):
+            super().__init__(partitions, dims, 1000.0, device)
+
+
+def make_partitioner(algo, num_partitions, domain, dims, device=0):
+    """The --algo switch of FlinkSkyline.main (:112-134); unknown names fall back to MR-Angle."""
+    a = algo.lower()
+    if a == "mr-dim":
+        return PartitioningLogic.DimPartitioner(num_partitions, domain, dims, device)
+    if a == "mr-grid":
+        return PartitioningLogic.GridPartitioner(num_partitions, domain, dims, device)
+    return PartitioningLogic.AnglePartitioner(num_partitions, dims, device)
+
+
+class _LocalPart:
+    def __init__(self, engine, key):
+        h = ctypes.c_void_p()
+        check(lib().sky_part_open(engine.h, key, ctypes.byref(h)))
+        self.h = h
+        self.dims = engine.dims
+
+    def insert(self, ids, vals):
+        ids = np.ascontiguousarray(ids, np.int64)
+        vals = np.ascontiguousarray(vals, np.float64)
+        check(lib().sky_part_insert(self.h, ids.ctypes.data_as(ctypes.c_void_p),
+                                    vals.ctypes.data_as(ctypes.c_void_p), len(ids)))
+
+    def snapshot(self):
+        n = ctypes.c_int64(0)
+        check(lib().sky_part_size(self.h, ctypes.byref(n)))
+        ids = np.empty(max(n.value, 1), np.int64)
+        vals = np.empty((max(n.value, 1), self.dims), np.float64)
+        check(lib().sky_part_snapshot(self.h, ids.ctypes.data_as(ctypes.c_void_p),
+                                      vals.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
+        return ids[:n.value].copy(), vals[:n.value].copy()
+
+    def close(self):
+        if self.h:
+            lib().sky_part_close(self.h)
+            self.h = None
+
+
+class SkylineLocalProcessor:
+    """FlinkSkyline.SkylineLocalProcessor (:214-445) over sky_part_* state.
+
+    processElement1(point, key, out)   data input (:265-316)
+    processElement2(trigger, out)      trigger input, trigger = (partitionId, payload, dispatchMs) (:330-356)
+    Emits Tuple6 = (partitionId, payload, dispatchMs, partitionStartMs, localSkyline, cpuMillis) (:396-403),
+    the local skyline as (ids ndarray, values ndarray).
+    """
+
+    BUFFER_SIZE = 5000   # :232
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.localSkylineState = {}      # key -> _LocalPart
+        self.inputBuffer = {}            # key -> list of (id, values)
+        self.maxSeenIdState = {}
+        self.pendingQueriesState = {}
+        self.startTimeState = {}
+        self.accumulatedCpuNanosState = {}
+
+    def _state(self, key):
+        if key not in self.localSkylineState:
+            self.localSkylineState[key] = _LocalPart(self.engine, key)
+            self.inputBuffer[key] = []
+        return self.localSkylineState[key]
+
+    def processElement1(self, point, key, out):
+        start = time.perf_counter_ns()
+        self._state(key)
+        if key not in self.startTimeState:
+            self.startTimeState[key] = now_ms()
+        current_id = int(point.id)                                   # Long.parseLong (:276)
+        max_id = self.maxSeenIdState.get(key, -1)
+        if current_id > max_id:
+            self.maxSeenIdState[key] = current_id
+            max_id = current_id
+        buf = self.inputBuffer[key]
+        buf.append((current_id, point.values))
+        if len(buf) >= self.BUFFER_SIZE:
+            self.processBuffer(key)
+        self.accumulatedCpuNanosState[key] = self.accumulatedCpuNanosState.get(key, 0) + \
+            (time.perf_counter_ns() - start)
+        pending = self.pendingQueriesState.get(key)
+        if pending:
+            remaining = []
+            processed = False
+            for q in pending:
+                parts = q[1].split(",")
+                required = int(parts[1]) if len(parts) > 1 else 0
+                if max_id >= required:
+                    self.processQuery(q, key, out)
+                    processed = True
+                else:
+                    remaining.append(q)
+            if processed:
+                self.pendingQueriesState[key] = remaining
+
+    def processElement2(self, trigger, out):
+        key = trigger[0]
+        parts = trigger[1].split(",")
+        required = int(parts[1]) if len(parts) > 1 else 0
+        current = self.maxSeenIdState.get(key, -1)
+        if current >= required or current == -1:
+            self.processQuery(trigger, key, out)
+        else:
+            self.pendingQueriesState.setdefault(key, []).append(trigger)
+
+    def processQuery(self, trigger, key, out):
+        start = time.perf_counter_ns()
+        self._state(key)
+        if self.inputBuffer[key]:
+            self.processBuffer(key)
+        total = self.accumulatedCpuNanosState.get(key, 0) + (time.perf_counter_ns() - start)
+        self.accumulatedCpuNanosState[key] = total
+        part_start = self.startTimeState.get(key, now_ms())
+        ids, vals = self.localSkylineState[key].snapshot()
+        out.append((trigger[0], trigger[1], trigger[2], part_start, (ids, vals), total // 1_000_000))
+
+    def processBuffer(self, key):
+        """S <- SKY(S u buffer) on the device (the BNL of :417-444)."""
+        buf = self.inputBuffer[key]
+        if not buf:
+            return
+        ids = np.fromiter((b[0] for b in buf), np.int64, len(buf))
+        vals = np.asarray([b[1] for b in buf], np.float64).reshape(len(buf), self.engine.dims)
+        self.localSkylineState[key].insert(ids, vals)
+        buf.clear()
+
+    def close(self):
+        for p in self.localSkylineState.values():
+            p.close()
+        self.localSkylineState.clear()
+
+
+class GlobalSkylineAggregator:
+    """FlinkSkyline.GlobalSkylineAggregator (:460-660).  Collects the P local
+    skylines of one query key and, on the last arrival, merges them on the
+    device (sky_global_merge) and emits the JSON payload (:631-648)."""
+
+    def __init__(self, engine, totalPartitions):
+        self.engine = engine
+        self.totalPartitions = int(totalPartitions)
+        self.state = {}
+
+    def processElement(self, inp, out):
+        pid, payload, dispatch_ms, pstart, (ids, vals), cpu_ms = inp
+        st = self.state.setdefault(payload, {"lists": [], "count": 0, "minStart": None, "lastArr": None,
+                                             "maxCpu": None})
+        if st["minStart"] is None or (pstart is not None and pstart < st["minStart"]):
+            st["minStart"] = pstart
+        st["lastArr"] = now_ms()
+        if st["maxCpu"] is None or cpu_ms > st["maxCpu"]:
+            st["maxCpu"] = cpu_ms
+        st["lists"].append((pid, ids, vals))
+        st["count"] += 1
+        if st["count"] >= self.totalPartitions:
+            lists = st["lists"]
+            gids, gorg = self.engine.global_merge([l[0] for l in lists], [l[1] for l in lists],
+                                                  [l[2] for l in lists])
+            finish = now_ms()
+            job_start = st["minStart"]
+            map_finish = st["lastArr"]
+            map_wall = (map_finish - job_start) if job_start is not None else 0
+            local_t = st["maxCpu"] or 0
+            ingest = max(0, map_wall - local_t)
+            global_t = finish - map_finish
+            total_t = (finish - job_start) if job_start is not None else 0
+            latency = finish - dispatch_ms
+            # optimality (:593-608): the local size of partition i is its list size
+            sizes = {}
+            for l in lists:
+                sizes[l[0]] = len(l[1])
+            surv = {}
+            for o in gorg.tolist():
+                surv[o] = surv.get(o, 0) + 1
+            s = 0.0
+            for i in range(self.totalPartitions):
+                if i in sizes and sizes[i] > 0:
+                    s += surv.get(i, 0) / sizes[i]
+            optimality = s / self.totalPartitions
+            parts = payload.split(",")
+            qid = parts[0]
+            rec = parts[1] if len(parts) > 1 else "unknown"
+            js = ('{"query_id": "%s", "record_count": %s, "skyline_size": %d, "optimality": %s, '
+                  '"ingestion_time_ms": %d, "local_processing_time_ms": %d, "global_processing_time_ms": %d, '
+                  '"total_processing_time_ms": %d, "query_latency_ms": %d}') % (
+                qid, rec, len(gids), java_format_4f(optimality), ingest, local_t, global_t, total_t, latency)
+            out.append(js)
+            st["result_ids"] = gids
+            del self.state[payload]
+            self.last_result = (gids, gorg)
+
+
+def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=1000.0, device=0):
+    """Single-process rendition of the topology of FlinkSkyline.main (:61-186):
+    parse -> keyBy(partitioner) -> SkylineLocalProcessor <- broadcast triggers
+    -> keyBy(payload) -> GlobalSkylineAggregator.  `triggers` is a list of
+    (position, payload): the trigger is injected after that many input lines,
+    like unified_producer.py:177-185.  Returns the emitted JSON strings and the
+    result ids of the last query."""
+    P = 2 * parallelism
+    part = make_partitioner(algo, P, domain, dims, device)
+    eng = part.engine
+    local = SkylineLocalProcessor(eng)
+    glob = GlobalSkylineAggregator(eng, P)
+    emitted, results = [], []
+    tuples = [ServiceTuple.fromString(s) for s in csv_lines]
+    valid = [t for t in tuples if t is not None]
+    keys = part.getKeys(np.asarray([t.values for t in valid], np.float64)) if valid else []
+    trig = sorted(triggers)
+    ti = 0
+    pos = 0
+
+    def fire(payload):
+        start = now_ms()
+        for i in range(P):                                            # broadcast (:152-154)
+            local.processElement2((i, payload, start), emitted)
+        drain()
+
+    def drain():
+        while emitted:
+            glob.processElement(emitted.pop(0), results)
+
+    vi = 0
+    for t in tuples:
+        while ti < len(trig) and trig[ti][0] <= pos:
+            fire(trig[ti][1])
+            ti += 1
+        if t is not None:
+            local.processElement1(t, int(keys[vi]), emitted)
+            vi += 1
+            drain()
+        pos += 1
+    while ti < len(trig):
+        fire(trig[ti][1])
+        ti += 1
+    last = getattr(glob, "last_result", None)
+    local.close()
+    return results, last

@@ -1,0 +1,162 @@
+/*
+ * skyline_hip.h — C ABI of libskyline_hip.so, the MI355X-native engine behind the
+ * reference's Flink skyline operators (Asterinos1/Flink-Skyline-QoS).
+ *
+ * Plain C types only (JNI / Panama-FFM / ctypes friendly).  Every entry point
+ * returns an int status: SKY_OK (0) or a negative SKY_E_* code; the message of
+ * the last failure on the calling thread is in sky_last_error().  No C++
+ * exception crosses this boundary.
+ *
+ * Threading: calls on one handle must not run concurrently (Flink's mailbox
+ * model gives one thread per operator subtask); distinct handles may be used
+ * from distinct threads.  Each entry point binds its context's device.
+ *
+ * Buffers: `*_dev` entry points take device pointers (HBM-resident inputs and
+ * outputs, for callers that already hold device memory); the others take
+ * caller-owned host buffers that are only read/written during the call.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/java/org.main/):
+ *   sky_partition_keys   <- PartitioningLogic.SkylinePartitioner.getKey
+ *                           (FlinkSkyline.java:675; Dim :707-712, Grid :774-789, Angle :827-875)
+ *   sky_part_*           <- SkylineLocalProcessor keyed state + processBuffer BNL
+ *                           (FlinkSkyline.java:214-445; BNL :417-444; snapshot :387-392)
+ *   sky_global_merge     <- GlobalSkylineAggregator.processElement merge (FlinkSkyline.java:515-569)
+ *   sky_global_stats     <- optimality integers (FlinkSkyline.java:593-608)
+ *   sky_query[_dev]      <- the whole keyBy -> local -> global path for a trigger that arrives
+ *                           after the last tuple (FlinkSkyline.java:138-174)
+ *   dominance            <- ServiceTuple.dominates (ServiceTuple.java:67-77)
+ */
+#ifndef SKYLINE_HIP_H
+#define SKYLINE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define SKY_OK          0
+#define SKY_E_ARG      -1   /* invalid argument (null pointer, dims out of range, ...) */
+#define SKY_E_HIP      -2   /* HIP runtime failure (message in sky_last_error) */
+#define SKY_E_CAPACITY -3   /* output buffer too small; *n_out holds the required count */
+#define SKY_E_NAN      -4   /* a value is NaN: the reference BNL result is order-dependent for NaN */
+#define SKY_E_NOMEM    -5   /* device allocation failed */
+#define SKY_E_NOLIB    -6   /* no HIP device / code object for gfx950 */
+
+/* partitioners (FlinkSkyline.java:112-134, flag --algo) */
+#define SKY_ALGO_DIM    0   /* "mr-dim"   */
+#define SKY_ALGO_GRID   1   /* "mr-grid"  */
+#define SKY_ALGO_ANGLE  2   /* "mr-angle" (the reference default) */
+
+/* query semantics */
+#define SKY_SEM_REFERENCE 0 /* only keys 0..P-1 are queried (FlinkSkyline.java:152-154): MR-Grid
+                               tuples with key >= P never reach the global merge */
+#define SKY_SEM_COMPLETE  1 /* every key in [0, 2^D) of MR-Grid is queried (D <= 8) */
+
+/* synthetic streams (restating python/unified_producer.py:50-123 with a counter RNG) */
+#define SKY_DIST_UNIFORM    0
+#define SKY_DIST_CORRELATED 1
+#define SKY_DIST_ANTI       2   /* reference anti-correlated formula */
+#define SKY_DIST_STD_ANTI   3   /* Borzsonyi-style anti-correlated band (extension, labelled) */
+#define SKY_DIST_MIXED      4   /* 65536-tuple blocks cycling 0,1,2 (extension for config C5) */
+
+#define SKY_MAX_DIMS       16
+#define SKY_MAX_PARTITIONS 256
+
+typedef struct sky_ctx sky_ctx;
+typedef struct sky_part sky_part;
+
+/* ---- context ------------------------------------------------------------ */
+/* devices/ndev: HIP device ordinals; one process drives one device (ndev == 1),
+ * multi-GPU runs one process per GPU (see sky_export_local / sky_import_union).
+ * dims in [1,16]; num_partitions P in [1,256] (= 2 x Flink parallelism, :76);
+ * domain_max = --domain (default 1000.0, :71). */
+int sky_ctx_create(const int *devices, int ndev, int dims, int num_partitions, int algo,
+                   double domain_max, sky_ctx **out);
+int sky_ctx_destroy(sky_ctx *ctx);
+int sky_ctx_set_semantics(sky_ctx *ctx, int semantics);
+/* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL returns to the context's own stream. */
+int sky_ctx_set_stream(sky_ctx *ctx, void *hip_stream);
+int sky_ctx_sync(sky_ctx *ctx);
+const char *sky_last_error(void);
+const char *sky_version(void);
+
+/* ---- partitioners --------------------------------------------------------- */
+/* keys_out[i] = getKey(tuple i), bit-exact with Java (fdlibm atan2, no FMA);
+ * MR-Grid keys are the unclamped mask in [0, 2^D). values: n x dims row-major. */
+int sky_partition_keys(sky_ctx *ctx, const double *values, int64_t n, int32_t *keys_out);
+int sky_partition_keys_dev(sky_ctx *ctx, const double *d_values, int64_t n, int32_t *d_keys_out);
+
+/* ---- local operator state (one per Flink key) ----------------------------- */
+int sky_part_open(sky_ctx *ctx, int32_t key, sky_part **out);
+int sky_part_close(sky_part *part);
+/* S <- SKY(S u batch)  (processBuffer, FlinkSkyline.java:417-444); duplicates kept */
+int sky_part_insert(sky_part *part, const int64_t *ids, const double *values, int64_t n);
+int sky_part_size(sky_part *part, int64_t *n_out);
+/* copy of the current local skyline (ids + values), order = ascending insertion order;
+ * SKY_E_CAPACITY with *n_out set if cap is too small */
+int sky_part_snapshot(sky_part *part, int64_t *ids_out, double *values_out, int64_t cap,
+                      int64_t *n_out);
+
+/* ---- global merge ---------------------------------------------------------- */
+/* G = SKY(u_k list_k) for the nparts local skylines; origin_out[j] = part_ids[k] of
+ * the list that supplied ids_out[j].  Output order: list order, then position. */
+int sky_global_merge(sky_ctx *ctx, int nparts, const int32_t *part_ids,
+                     const int64_t *const *ids, const double *const *values,
+                     const int64_t *counts, int64_t *ids_out, int32_t *origin_out,
+                     int64_t cap, int64_t *n_out);
+/* integers behind the optimality metric of the last merge / query:
+ * local_sizes[k] = |L_k|, survivors[k] = |G n L_k| for k < K
+ * (K = P, or max(P, 2^D) for MR-Grid with SKY_SEM_COMPLETE). */
+int sky_global_stats(sky_ctx *ctx, int64_t *local_sizes, int64_t *survivors, int32_t *k_out);
+
+/* ---- fused whole-stream query --------------------------------------------- */
+/* keyBy -> per-key local skylines -> global merge, the trigger arriving after
+ * the last tuple.  ids_out/origin_out: the global skyline in stream order. */
+int sky_query(sky_ctx *ctx, const int64_t *ids, const double *values, int64_t n,
+              int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
+int sky_query_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
+                  int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);
+
+/* ---- multi-GPU (one process per GPU; the caller moves bytes with RCCL) ------ */
+/* Phase 1 on each rank: local skylines of this rank's shard; export their
+ * distinct vectors: rows (f64, dims wide) + origin key + multiplicity.  Returns the
+ * count in *n_out; call with cap = 0 first to size the buffers. */
+int sky_export_local_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
+                         int64_t *n_out);
+int sky_export_copy_dev(sky_ctx *ctx, double *d_rows_out, int32_t *d_keys_out,
+                        int64_t *d_mult_out, int64_t cap);
+/* Phase 2: the all-gathered union of every rank's exported vectors (this rank's
+ * own export starts at row self_offset); computes L_k (for stats) and G over the
+ * union; writes this rank's global-skyline ids (stream order).  The shard buffers
+ * passed to sky_export_local_dev must still be valid. */
+int sky_import_union_dev(sky_ctx *ctx, const double *d_rows, const int32_t *d_keys,
+                         const int64_t *d_mult, int64_t n_union, int64_t self_offset,
+                         int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);
+
+/* ---- utilities ------------------------------------------------------------- */
+int sky_synth_dev(sky_ctx *ctx, int dist, int dmin, int dmax, uint64_t seed, int64_t id0,
+                  int64_t n, double *d_values, int64_t *d_ids);
+int sky_synth(int dist, int dims, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n,
+              double *values, int64_t *ids);   /* host copy of the generator (no device) */
+/* device memory helpers for callers without a HIP runtime binding of their own */
+int sky_dev_alloc(sky_ctx *ctx, int64_t bytes, void **d_out);
+int sky_dev_free(sky_ctx *ctx, void *d_ptr);
+int sky_memcpy_h2d(sky_ctx *ctx, void *d_dst, const void *h_src, int64_t bytes);
+int sky_memcpy_d2h(sky_ctx *ctx, void *h_dst, const void *d_src, int64_t bytes);
+
+/* profiling: HIP-event timings (ms) of the last query, per phase, and the
+ * dominant streaming kernel's accumulated time / launch count since reset */
+#define SKY_PHASES 8
+int sky_profile_enable(sky_ctx *ctx, int on);
+int sky_profile_phases(sky_ctx *ctx, double *ms_out /* SKY_PHASES */, int64_t *counters_out /* 8 */);
+int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
+                       int64_t *units);
+int sky_profile_reset(sky_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKYLINE_HIP_H */

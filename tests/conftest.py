@@ -1,0 +1,140 @@
+"""Shared fixtures.  The oracle (oracle/) is TEST INFRASTRUCTURE: it is only the
+checker here, never the thing under test."""
+import ctypes
+import glob
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "flink-skyline-qos_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libskyline_hip.so)")
+
+
+_ORACLE = None
+
+
+def load_oracle():
+    global _ORACLE
+    if _ORACLE is None:
+        so = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+        if not os.path.exists(so):
+            subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+        L = ctypes.CDLL(so)
+        dp = ctypes.c_void_p
+        L.orc_fdlibm_atan2.restype = ctypes.c_double
+        L.orc_fdlibm_atan2.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.orc_fdlibm_table.restype = ctypes.POINTER(ctypes.c_double)
+        L.orc_fdlibm_table.argtypes = [ctypes.c_int]
+        L.orc_dominates.argtypes = [dp, dp, ctypes.c_int]
+        L.orc_keys.argtypes = [ctypes.c_int, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double, dp]
+        L.orc_query_bnl.restype = ctypes.c_int64
+        L.orc_query_bnl.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_double, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.c_int64, dp, dp]
+        L.orc_query_sfs.restype = ctypes.c_int64
+        L.orc_query_sfs.argtypes = [ctypes.c_int, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_int, dp, dp, dp, dp, dp]
+        L.orc_skyline_brute.argtypes = [dp, ctypes.c_int64, ctypes.c_int, dp]
+        L.orc_synth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                ctypes.c_int64, ctypes.c_int64, dp]
+        _ORACLE = L
+    return _ORACLE
+
+
+def P(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Oracle:
+    """numpy-friendly wrapper over oracle/_build/liboracle.so."""
+    ALGO = {"dim": 0, "grid": 1, "angle": 2, "mr-dim": 0, "mr-grid": 1, "mr-angle": 2}
+
+    def __init__(self):
+        self.L = load_oracle()
+
+    def keys(self, algo, vals, P_, domain=1000.0):
+        v = np.ascontiguousarray(vals, np.float64)
+        out = np.zeros(len(v), np.int32)
+        self.L.orc_keys(self.ALGO[algo], P(v), len(v), v.shape[1], P_, domain, P(out))
+        return out
+
+    def query_bnl(self, algo, vals, ids, P_, domain=1000.0, sem=0, buffer_size=5000):
+        v = np.ascontiguousarray(vals, np.float64)
+        ids = np.ascontiguousarray(ids, np.int64)
+        n, D = v.shape
+        K = P_ if not (self.ALGO[algo] == 1 and sem == 1) else max(P_, 1 << D)
+        oi = np.zeros(max(n, 1), np.int64)
+        oo = np.zeros(max(n, 1), np.int32)
+        ls = np.zeros(K, np.int64)
+        sv = np.zeros(K, np.int64)
+        g = self.L.orc_query_bnl(self.ALGO[algo], P(v), P(ids), n, D, P_, domain, buffer_size, sem, P(oi), P(oo),
+                                 n, P(ls), P(sv))
+        assert g >= 0
+        return oi[:g], oo[:g], ls, sv
+
+    def query_sfs(self, algo, vals, P_, domain=1000.0, sem=0):
+        v = np.ascontiguousarray(vals, np.float64)
+        n, D = v.shape
+        K = P_ if not (self.ALGO[algo] == 1 and sem == 1) else max(P_, 1 << D)
+        keys = np.zeros(max(n, 1), np.int32)
+        inl = np.zeros(max(n, 1), np.uint8)
+        ing = np.zeros(max(n, 1), np.uint8)
+        ls = np.zeros(K, np.int64)
+        sv = np.zeros(K, np.int64)
+        g = self.L.orc_query_sfs(self.ALGO[algo], P(v), n, D, P_, domain, sem, P(keys), P(inl), P(ing), P(ls), P(sv))
+        assert g >= 0
+        return np.nonzero(ing[:n])[0], keys[:n], ls, sv
+
+    def brute(self, vals):
+        v = np.ascontiguousarray(vals, np.float64)
+        out = np.zeros(max(len(v), 1), np.uint8)
+        self.L.orc_skyline_brute(P(v), len(v), v.shape[1], P(out))
+        return np.nonzero(out[:len(v)])[0]
+
+    def synth(self, dist, D, n, seed=1234, id0=0, dmin=0, dmax=1000):
+        out = np.zeros((n, D), np.float64)
+        self.L.orc_synth(dist, D, dmin, dmax, seed, id0, n, P(out))
+        return out
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return Oracle()
+
+
+def golden_streams():
+    return sorted(glob.glob(os.path.join(GOLDEN, "stream_*.npz")))
+
+
+def load_golden(path):
+    z = np.load(path)   # allow_pickle stays False
+    d = {k: z[k] for k in z.files}
+    d["values"] = d["values"].astype(np.float64)
+    return d
+
+
+@pytest.fixture(scope="session")
+def gpu_engine_factory():
+    """Builds SkylineEngine objects; skips cleanly when no GPU is visible (CPU runs)."""
+    import skyline
+    from skyline._abi import SkylineError
+
+    def make(dims, P_, algo="mr-angle", domain=1000.0, semantics="reference"):
+        try:
+            return skyline.SkylineEngine(dims, P_, algo, domain, 0, semantics)
+        except SkylineError as e:
+            if e.code == -6:
+                pytest.fail("no HIP device visible for a gpu-marked test: " + str(e))
+            raise
+    return make
