@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""bench.py — skyline tuples/sec (+ p50 query latency) on MI355X.
+
+Workload (BASELINE.json metric, config C4 on one GPU per rank): MR-Angle, 8D,
+anti-correlated stream (the reference producer's formula,
+python/unified_producer.py:89-123, counter RNG), P = 16 partitions, domain
+[0,1000], N tuples per rank (default 100M) generated directly in HBM.
+
+A step = one query over the whole landmark window (every tuple of the rank's
+shard): partition keys -> local skylines of the P partitions -> global merge ->
+stream-ordered skyline ids, with inputs already resident in HBM.  With N GPUs
+(one process per GPU, launched by torch.distributed.run) every rank holds its
+own N-tuple shard (weak scaling) and the ranks exchange their local skylines'
+distinct vectors with one RCCL all-gather (skyline/dist.py).
+
+Extra fields: "roofline" for the dominant kernel (k_filter, HBM-bound), timed
+with HIP events on the stream it is launched on; "cpu_baseline" = the C
+restatement of the reference BNL operators (oracle/, 1 thread) timed on a
+bounded prefix of the same stream (rank 0, N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "flink-skyline-qos_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import skyline  # noqa: E402
+from skyline import _abi  # noqa: E402
+from skyline.dist import distributed_query  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
+
+
+def cpu_baseline(d, P, dist_name, seed, sample, domain):
+    """Reference algorithm restated in C (per-key BNL, buffer 5000, single-threaded
+    global BNL), one thread, on the first `sample` tuples of the same stream."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import Oracle   # test infrastructure: the checker / CPU baseline only
+    orc = Oracle()
+    vals = orc.synth(_abi.DISTS[dist_name], d, sample, seed=seed)
+    ids = np.arange(sample, dtype=np.int64)
+    t0 = time.perf_counter()
+    g, _, _, _ = orc.query_bnl("angle", vals, ids, P, domain)
+    dt = time.perf_counter() - t0
+    return sample / dt, dt, len(g)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=100_000_000, help="tuples per rank")
+    ap.add_argument("--dims", type=int, default=8)
+    ap.add_argument("--partitions", type=int, default=16)
+    ap.add_argument("--dist", default="anti_correlated")
+    ap.add_argument("--seed", type=int, default=1242)
+    ap.add_argument("--cpu-sample", type=int, default=60000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    D, P, n = args.dims, args.partitions, args.n
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, local_rank)
+    vals = torch.empty((n, D), dtype=torch.float64, device=dev)
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.synth_dev(args.dist, n, vals, ids, seed=args.seed, id0=rank * n)
+    eng.sync()
+    out_ids = torch.empty(n, dtype=torch.int64, device=dev)
+    out_org = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def step():
+        if distributed:
+            return distributed_query(eng, ids, vals, out_ids, out_org, n)
+        return eng.query_dev(ids, vals, out_ids, out_org, n)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    eng.profile_reset()
+    step_ms = []
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = 0
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        g = step()
+        eng.sync()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.profile(False)
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gt = torch.tensor([g], dtype=torch.int64, device=dev)
+        dist.all_reduce(gt)
+        g = int(gt.item())
+    phases, counters = eng.phases()
+    f_ms, f_launch, f_units = eng.kernel_time("filter")
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        total = n * world
+        value = total / (ms_per_step / 1e3)
+        bytes_per_tuple = D * 8 + 2            # read the f64 row once, write the u16 status word
+        avg_ms = f_ms / max(f_launch, 1)
+        achieved = (bytes_per_tuple * (f_units / max(f_launch, 1))) / (avg_ms / 1e3) / 1e9 if f_launch else 0.0
+        traffic = None
+        tf = os.path.join(REPO, "profiles", "traffic_filter.json")
+        if os.path.exists(tf):
+            try:
+                tj = json.load(open(tf))
+                if tj.get("n") == n and tj.get("dims") == D and tj.get("dist") == args.dist:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            rate, dt, gs = cpu_baseline(D, P, args.dist, args.seed, args.cpu_sample, 1000.0)
+            cpu = {"value": rate, "unit": "tuples/s", "cores": 1, "kind": "port",
+                   "sample": f"first {args.cpu_sample} tuples of the same stream, oracle/ C restatement of the "
+                             f"reference per-key BNL (buffer 5000) + single-threaded global BNL, "
+                             f"{dt:.1f} s, skyline {gs}"}
+        line = {
+            "metric": "skyline tuples/sec + p50 query latency, 8D anti-corr, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "tuples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "p50_query_latency_ms": statistics.median(step_ms),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (reference anti-correlated formula, counter RNG, generated in HBM)",
+            "config": {"workload": "C4: MR-Angle 8D anti-correlated, P=16, landmark-window query",
+                       "tuples_per_gpu": n, "dims": D, "partitions": P, "algo": "mr-angle",
+                       "dist": args.dist, "domain": [0, 1000], "compare_dtype": "f32 (values exact)",
+                       "parallelism": f"shards{world}", "skyline_size": g},
+            "roofline": {"bound": "hbm", "kernel": "k_filter", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_unit": bytes_per_tuple, "units_per_launch": f_units / max(f_launch, 1),
+                         "avg_launch_ms": avg_ms, "launches": f_launch},
+            "phases_ms_last_step": phases,
+            "counters_last_step": {"n": int(counters[0]), "candidates": int(counters[1]),
+                                   "distinct_reps": int(counters[2]), "global_candidates": int(counters[3]),
+                                   "output": int(counters[4]), "sfs_rounds": int(counters[5])},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,6 +46,9 @@ using namespace sky;
     }
 
 static int bind(sky_ctx *c) {
+    // hipGetLastError() is per thread and sticky: drop whatever another library
+    // (e.g. torch) left behind so our launch checks only see our own failures
+    (void)hipGetLastError();
     HIP_TRY(hipSetDevice(c->dev));
     return SKY_OK;
 }

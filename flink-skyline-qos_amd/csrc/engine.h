@@ -13,6 +13,20 @@ void set_error(const std::string &msg);
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p;
+            cap = o.cap;
+            o.p = nullptr;
+            o.cap = 0;
+        }
+        return *this;
+    }
     int ensure(size_t bytes);
     void release();
     template <typename T> T *as() const { return reinterpret_cast<T *>(p); }
@@ -39,7 +53,7 @@ struct Pipe {
     // per tuple / per tile
     DevBuf status, blk_cnt, blk_off, out_cnt, out_off;
     // pruners
-    DevBuf skey, ssum, sidx, pruners, npr, dup_cnt, pr_entries, pruner_slot;
+    DevBuf skey, ssum, sidx, sorder, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     // candidates (slot order) and sort
     DevBuf rows, sortkey, slot_src, perm, key_alt, val_alt, rows_sorted;
     DevBuf runflag, runscan, run_first, repof, repflag, repscan, rep_rows, rep_key, rep_of_sorted, slot_rep;

@@ -11,6 +11,7 @@
 #include "ctx.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace sky {
@@ -70,6 +71,28 @@ int Pipe::pinned(size_t bytes) {
     return SKY_OK;
 }
 
+// SKY_DEBUG=1: synchronise and check after every stage, naming the stage
+static int debug_level() {
+    static int lvl = [] {
+        const char *e = getenv("SKY_DEBUG");
+        return e ? atoi(e) : 0;
+    }();
+    return lvl;
+}
+static int stage_check(hipStream_t st, const char *where) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug_level()) {
+        e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("HIP error ") + hipGetErrorString(e) + " in stage " + where);
+        return SKY_E_HIP;
+    }
+    return SKY_OK;
+}
+#define STAGE(st, name) SKY_TRY(stage_check(st, name))
+
 static int choose_B(bool f64, int D) {
     const int DP = f64 ? padded_dims<double>(D) : padded_dims<float>(D);
     const int rowb = DP * (f64 ? 8 : 4);
@@ -120,6 +143,7 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         launch_block_sky(D, p.f64, full, p.ties, B, rows, key, p.act.as<uint32_t>(), p.segs.as<SfsSeg>(),
                          p.seg_list.as<uint32_t>(), (uint32_t)work.size(), alive, p.conf_rows.p,
                          p.nconf.as<uint32_t>(), st);
+        STAGE(st, "block_sky");
         tiles.clear();
         uint32_t out = 0;
         for (uint32_t k : work) {
@@ -139,11 +163,13 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         launch_filter_rest(D, p.f64, full, B, rows, p.act.as<uint32_t>(), p.tiles.as<SfsTile>(),
                            (uint32_t)tiles.size(), p.conf_rows.p, p.nconf.as<uint32_t>(), p.keep.as<uint32_t>(), st);
         c.ktimer_end("sfs_filter", st, out);
+        STAGE(st, "sfs_filter");
         scan_excl_u32(p.keep.as<uint32_t>(), p.keep_scan.as<uint32_t>(), out, nullptr, p.scratch.as<uint32_t>(), st);
         HIP_TRY(hipMemsetAsync(p.segcnt.p, 0, nseg * 4, st));
         launch_act_compact(p.act.as<uint32_t>(), p.keep.as<uint32_t>(), p.keep_scan.as<uint32_t>(),
                            p.tiles.as<SfsTile>(), (uint32_t)tiles.size(), p.act2.as<uint32_t>(),
                            p.segcnt.as<uint32_t>(), st);
+        STAGE(st, "act_compact");
         SKY_TRY(p.pinned(nseg * 4));
         HIP_TRY(hipMemcpyAsync(p.pin, p.segcnt.p, nseg * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
@@ -206,13 +232,16 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const uint32_t S = std::min<uint32_t>(n, 65536);
     SKY_TRY(p.skey.ensure((size_t)S * 4));
     SKY_TRY(p.ssum.ensure((size_t)S * 8));
-    SKY_TRY(p.sidx.ensure((size_t)S * 4));
+    SKY_TRY(p.sidx.ensure((size_t)S * D * 8));          // sample rows
+    SKY_TRY(p.sorder.ensure((size_t)S * 4 + ((size_t)p.Kp + 1) * 4));
     SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
     launch_sample(D, in.vals, n, S, kp, in.keys, in.single, p.skey.as<int32_t>(), p.ssum.as<double>(),
-                  p.sidx.as<uint32_t>(), st);
-    launch_select_pruners(D, in.vals, S, p.skey.as<int32_t>(), p.ssum.as<double>(), p.sidx.as<uint32_t>(), p.Kp,
-                          p.M, p.pruners.as<double>(), p.npr.as<int32_t>(), st);
+                  p.sidx.as<double>(), st);
+    launch_select_pruners(D, p.sidx.as<double>(), S, p.skey.as<int32_t>(), p.ssum.as<double>(),
+                          p.sorder.as<uint32_t>() + S, p.sorder.as<uint32_t>(), p.Kp, p.M, p.pruners.as<double>(),
+                          p.npr.as<int32_t>(), st);
+    STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
     // ---- the HBM stream: keys + pruner test + status
@@ -240,6 +269,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     c.ktimer_begin("filter", st);
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
+    STAGE(st, "filter");
     scan_excl_u32(p.blk_cnt.as<uint32_t>(), p.blk_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>(),
                   p.scratch.as<uint32_t>(), st);
     uint32_t m = 0, flags = 0;
@@ -288,6 +318,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         if (m) launch_compact(D, p.f64, ca, st);
         launch_append_pruners(D, p.f64, p.pruners.as<double>(), p.M, p.pr_entries.as<int32_t>(), p.nps, m, p.rows.p,
                               p.sortkey.as<uint64_t>(), p.slot_src.as<uint32_t>(), p.flags.as<uint32_t>(), st);
+        STAGE(st, "compact");
         if (tm) tm->mark(3, st);
 
         // ---- sort the candidates by (partition, score, hash)
@@ -304,6 +335,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
                                           p.val_alt.as<uint32_t>(), mt, orand[0] ^ orand[1],
                                           p.scratch.as<uint32_t>(), st);
+        STAGE(st, "sort");
         const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
         const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
         if (tm) tm->mark(4, st);
@@ -336,6 +368,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_rep_of(D, p.f64, ra, st);
         scan_excl_u32(ra.repflag, ra.repscan, mt, p.totals.as<uint32_t>() + 1, p.scratch.as<uint32_t>(), st);
         launch_build_reps(D, p.f64, ra, st);
+        STAGE(st, "dedup");
         uint32_t mr = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}}, {&mr}));
         p.mr = mr;
@@ -386,6 +419,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 HIP_TRY(hipMemsetAsync(p.galive.p, 0, mg, st));
                 SKY_TRY(sfs_run(c, p, p.grows.p, gk, mg, {0u}, {mg}, true, p.galive.as<uint8_t>()));
                 launch_scatter_alive(gv, p.galive.as<uint8_t>(), mg, p.alive_g.as<uint8_t>(), st);
+                STAGE(st, "global");
             }
         } else {
             HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
@@ -418,6 +452,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
                   p.scratch.as<uint32_t>(), st);
     c.ktimer_end("out", st, n);
+    STAGE(st, "fate");
     uint32_t nout = 0;
     SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, (size_t)p.K * 8}, {p.surv.p, (size_t)p.K * 8}},
                       {&nout, p.h_lsz.data(), p.h_surv.data()}));

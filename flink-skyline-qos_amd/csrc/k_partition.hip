@@ -122,11 +122,12 @@ __global__ __launch_bounds__(kThreads) void k_keys(const double *__restrict__ va
     }
 }
 
+// strided sample: key, f64 score and a private copy of the row (contiguous)
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_sample(const double *__restrict__ vals, uint32_t n, uint32_t S,
                                                      KeyParams kp, const int32_t *__restrict__ given_keys,
                                                      int single, int32_t *__restrict__ skey,
-                                                     double *__restrict__ ssum, uint32_t *__restrict__ sidx) {
+                                                     double *__restrict__ ssum, double *__restrict__ srow) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= S) return;
     const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
@@ -135,20 +136,44 @@ __global__ __launch_bounds__(kThreads) void k_sample(const double *__restrict__ 
     bool nan = false;
     double sum = 0.0;
 #pragma unroll
-    for (int d = 0; d < D; d++) { nan |= v[d] != v[d]; sum = sum + v[d]; }
+    for (int d = 0; d < D; d++) { nan |= v[d] != v[d]; sum = sum + v[d]; srow[(size_t)s * D + d] = v[d]; }
     int32_t k = single ? 0 : given_keys ? given_keys[i] : partition_key<D>(v, kp);
     if (nan || k < 0 || k >= kp.K || sum != sum) k = -1;
     skey[s] = k;
     ssum[s] = sum;
-    sidx[s] = i;
 }
 
-// one workgroup per partition
+// one workgroup: counting sort of the sample ids by partition -> boff[Kp+1], order[S]
+__global__ __launch_bounds__(1024) void k_bucket_samples(const int32_t *__restrict__ skey, uint32_t S, int Kp,
+                                                         uint32_t *__restrict__ boff, uint32_t *__restrict__ order) {
+    __shared__ uint32_t s_cnt[kMaxK + 1];
+    __shared__ uint32_t s_cur[kMaxK + 1];
+    for (int q = threadIdx.x; q <= Kp; q += 1024) s_cnt[q] = 0;
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < S; s += 1024) {
+        const int32_t k = skey[s];
+        if (k >= 0) atomicAdd(&s_cnt[k], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int q = 0; q < Kp; q++) { s_cur[q] = run; boff[q] = run; run += s_cnt[q]; }
+        boff[Kp] = run;
+    }
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < S; s += 1024) {
+        const int32_t k = skey[s];
+        if (k >= 0) order[atomicAdd(&s_cur[k], 1u)] = s;
+    }
+}
+
+// one workgroup per partition: up to M mutually non-dominated, non-equal sample
+// tuples, smallest (score, sample id) first
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__restrict__ vals, uint32_t S,
-                                                             const int32_t *__restrict__ skey,
-                                                             const double *__restrict__ ssum,
-                                                             const uint32_t *__restrict__ sidx, int M,
+__global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__restrict__ srow,
+                                                             const uint32_t *__restrict__ boff,
+                                                             const uint32_t *__restrict__ order,
+                                                             const double *__restrict__ ssum, int M,
                                                              double *__restrict__ pruners,
                                                              int32_t *__restrict__ npr) {
     __shared__ double s_pr[8][D];
@@ -157,16 +182,17 @@ __global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__res
     __shared__ uint32_t s_win;
     const int k = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t b0 = boff[k], b1 = boff[k + 1];
     int chosen = 0;
     for (int j = 0; j < M && j < 8; j++) {
         double best = __builtin_inf();
         uint32_t bi = 0xffffffffu;
-        for (uint32_t s = threadIdx.x; s < S; s += kThreads) {
-            if (skey[s] != k) continue;
+        for (uint32_t q = b0 + threadIdx.x; q < b1; q += kThreads) {
+            const uint32_t s = order[q];
             const double sc = ssum[s];
             if (!(sc < best || (sc == best && s < bi))) continue;
             double v[D];
-            load_row<D>(vals + (size_t)sidx[s] * D, v);
+            load_row<D>(srow + (size_t)s * D, v);
             bool ok = true;
             for (int c = 0; c < chosen && ok; c++) {
                 bool le = true, lt = false, eq = true;
@@ -200,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__res
         const uint32_t win = s_win;
         if (win == 0xffffffffu) break;
         if (threadIdx.x < D) {
-            const double x = vals[(size_t)sidx[win] * D + threadIdx.x];
+            const double x = srow[(size_t)win * D + threadIdx.x];
             s_pr[chosen][threadIdx.x] = x;
             pruners[((size_t)k * M + chosen) * D + threadIdx.x] = x;
         }
@@ -267,15 +293,19 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
     if (lflags) atomicOr(a.flags, lflags);
 }
 
-// score = f64 sum of the (exact) T values in dimension order; a tie-free key needs
-// the sum to be exact and exactly an f32 -> otherwise flag kFlagScoreTies.
+// score = f64 sum of the (exact) T values in dimension order, each clamped to
+// [-1e300, 1e300] so that +inf and -inf never meet (the clamp is monotone, so the
+// score stays a linear extension of dominance).  A tie-free key needs no clamp, an
+// exact sum and an exact f32 of it -> otherwise flag kFlagScoreTies.
 template <typename T, int D>
 __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part, uint32_t &lflags) {
     double s = 0.0;
     bool inexact = false;
 #pragma unroll
     for (int d = 0; d < D; d++) {
-        const double x = (double)tv[d];
+        const double raw = (double)tv[d];
+        const double x = raw > 1e300 ? 1e300 : (raw < -1e300 ? -1e300 : raw);
+        inexact |= x != raw;
         const double sn = s + x;
         const double bb = sn - s;
         const double err = (s - (sn - bb)) + (x - bb);
@@ -470,11 +500,31 @@ __global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
         const bool sel = a.select_local ? inl : ing;
         if (!WRITE) {
             mycnt += sel;
-            if (stats && inl) {
-                const int o = a.given_origin ? a.given_origin[i] : (st >> 8);
-                const unsigned long long w = a.given_w ? (unsigned long long)a.given_w[i] : 1ull;
-                atomicAdd(&s.lsz[o], w);
-                if (ing) atomicAdd(&s.surv[o], w);
+            if (stats) {
+                // wave-aggregate when every member lane shares one origin (the common
+                // case: duplicates of one vector), else per-lane LDS atomics
+                const int o = i < a.n ? (a.given_origin ? a.given_origin[i] : (st >> 8)) : 0;
+                const unsigned long long w = inl ? (a.given_w ? (unsigned long long)a.given_w[i] : 1ull) : 0ull;
+                const unsigned long long wg = ing ? w : 0ull;
+                const uint64_t act = __ballot(inl);
+                if (act) {
+                    const int o0 = __shfl(o, __ffsll((unsigned long long)act) - 1, 64);
+                    if (__ballot(inl && o != o0) == 0ull) {
+                        unsigned long long a1 = w, a2 = wg;
+#pragma unroll
+                        for (int sh = 32; sh >= 1; sh >>= 1) {
+                            a1 += __shfl_xor(a1, sh, 64);
+                            a2 += __shfl_xor(a2, sh, 64);
+                        }
+                        if ((threadIdx.x & 63) == 0) {
+                            atomicAdd(&s.lsz[o0], a1);
+                            if (a2) atomicAdd(&s.surv[o0], a2);
+                        }
+                    } else if (inl) {
+                        atomicAdd(&s.lsz[o], w);
+                        if (ing) atomicAdd(&s.surv[o], w);
+                    }
+                }
             }
             if (a.row_flags && i < a.n) a.row_flags[i] = (uint8_t)((inl ? 1 : 0) | (ing ? 2 : 0));
         } else {
@@ -532,16 +582,18 @@ void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int
 }
 
 void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
-                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, uint32_t *sidx,
+                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, double *srow,
                    hipStream_t st) {
     if (S == 0) return;
     SKY_DISPATCH_D(D, (k_sample<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
-                                                                             skey, ssum, sidx)));
+                                                                             skey, ssum, srow)));
 }
 
-void launch_select_pruners(int D, const double *vals, uint32_t S, const int32_t *skey, const double *ssum,
-                           const uint32_t *sidx, int Kp, int M, double *pruners, int32_t *npr, hipStream_t st) {
-    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, kThreads, 0, st>>>(vals, S, skey, ssum, sidx, M, pruners, npr)));
+void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
+                           uint32_t *boff, uint32_t *order, int Kp, int M, double *pruners, int32_t *npr,
+                           hipStream_t st) {
+    k_bucket_samples<<<1, 1024, 0, st>>>(skey, S, Kp, boff, order);
+    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, kThreads, 0, st>>>(srow, boff, order, ssum, M, pruners, npr)));
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {

@@ -120,13 +120,84 @@ struct KeyParams {
     double grid_mid;   // maxVal / 2.0          (:756)
 };
 
+__device__ __forceinline__ int32_t clamp_key(int32_t p, int P) {
+    p = p > P - 1 ? P - 1 : p;
+    return p < 0 ? 0 : p;
+}
+
+// The reference's AnglePartitioner.getKey, operation for operation in f64.
+template <int D>
+__device__ __noinline__ int32_t angle_key_exact(const double *v, int P) {
+    constexpr double max_angle = 3.141592653589793 / 2.0;
+    double normalized = 0.0;
+    for (int i = 0; i < D - 1; i++) {
+        double s = 0.0;
+        for (int j = i + 1; j < D; j++) s = s + v[j] * v[j];   // ascending j, no FMA
+        const double hyp = sqrt(s);
+        normalized = normalized + fd_atan2(hyp, v[i]) / max_angle;
+    }
+    const double avg = normalized / (double)(D - 1);
+    return clamp_key(java_d2i(avg * (double)P), P);
+}
+
+// MR-Angle key with a certified fast path (a "filtered predicate"):
+//  1. exact special case: every angle is atan2(+0, x) or atan2(y>0, ±0), i.e. exactly
+//     0, pi (x negative/-0) or pi/2 -> normalized 0, 2, 1 exactly; the remaining
+//     f64 ops are replayed as the reference does them (all-zero tuples land here);
+//  2. f32 estimate of sum(atan2/(pi/2)); if t = avg*P is farther than kKeyMargin
+//     from an integer, floor(t) IS the exact key (f32 error is < 1e-5 in t for
+//     inputs with nonzero magnitudes in [1e-15, 1e15]);
+//  3. otherwise the exact fdlibm path.
+constexpr double kKeyMargin = 2e-3;
+
+template <int D>
+__device__ __forceinline__ int32_t angle_key(const double (&v)[D], int P) {
+    if (D < 2) return 0;
+    double s[D > 1 ? D - 1 : 1];
+    bool special = true, ranged = true;
+#pragma unroll
+    for (int i = 0; i < D; i++) special &= v[i] == v[i];    // NaN -> exact path
+#pragma unroll
+    for (int i = 0; i < D - 1; i++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = i + 1; j < D; j++) acc = acc + v[j] * v[j];
+        s[i] = acc;
+        special &= (acc == 0.0) | (v[i] == 0.0);
+    }
+#pragma unroll
+    for (int i = 0; i < D; i++) {
+        const double a = fabs(v[i]);
+        ranged &= (a == 0.0) | ((a >= 1e-15) & (a <= 1e15));
+    }
+    if (special) {
+        double normalized = 0.0;
+#pragma unroll
+        for (int i = 0; i < D - 1; i++) {
+            const double nrm = s[i] == 0.0 ? (signbit(v[i]) ? 2.0 : 0.0) : 1.0;
+            normalized = normalized + nrm;
+        }
+        const double avg = normalized / (double)(D - 1);
+        return clamp_key(java_d2i(avg * (double)P), P);
+    }
+    if (ranged) {
+        double est = 0.0;
+#pragma unroll
+        for (int i = 0; i < D - 1; i++) {
+            const float h = sqrtf((float)s[i]);
+            est += (double)atan2f(h, (float)v[i]);
+        }
+        const double t = est * (2.0 / 3.141592653589793) / (double)(D - 1) * (double)P;
+        const double fl = floor(t);
+        const double fr = t - fl;
+        if (fr > kKeyMargin && fr < 1.0 - kKeyMargin) return clamp_key((int32_t)fl, P);
+    }
+    return angle_key_exact<D>(v, P);
+}
+
 template <int D>
 __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const KeyParams &kp) {
-    if (kp.algo == SKY_ALGO_DIM) {
-        int32_t p = java_d2i(v[0] / kp.dim_width);
-        p = p > kp.P - 1 ? kp.P - 1 : p;
-        return p < 0 ? 0 : p;
-    }
+    if (kp.algo == SKY_ALGO_DIM) return clamp_key(java_d2i(v[0] / kp.dim_width), kp.P);
     if (kp.algo == SKY_ALGO_GRID) {
         uint32_t mask = 0;
 #pragma unroll
@@ -134,21 +205,7 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
             if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
         return (int32_t)mask;
     }
-    if (D < 2) return 0;
-    constexpr double max_angle = 3.141592653589793 / 2.0;
-    double normalized = 0.0;
-#pragma unroll
-    for (int i = 0; i < D - 1; i++) {
-        double s = 0.0;
-#pragma unroll
-        for (int j = i + 1; j < D; j++) s = s + v[j] * v[j];   // ascending j, no FMA
-        const double hyp = sqrt(s);
-        normalized = normalized + fd_atan2(hyp, v[i]) / max_angle;
-    }
-    const double avg = normalized / (double)(D - 1);
-    int32_t p = java_d2i(avg * (double)kp.P);
-    p = p > kp.P - 1 ? kp.P - 1 : p;
-    return p < 0 ? 0 : p;
+    return angle_key<D>(v, kp.P);
 }
 
 // ---- dominance ----------------------------------------------------------------

@@ -58,10 +58,11 @@ struct FilterArgs {
 };
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
 void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
-                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, uint32_t *sidx,
+                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, double *srow,
                    hipStream_t st);
-void launch_select_pruners(int D, const double *vals, uint32_t S, const int32_t *skey, const double *ssum,
-                           const uint32_t *sidx, int Kp, int M, double *pruners, int32_t *npr, hipStream_t st);
+void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
+                           uint32_t *boff, uint32_t *order, int Kp, int M, double *pruners, int32_t *npr,
+                           hipStream_t st);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
 struct CompactArgs {

@@ -235,8 +235,8 @@ static void sfs_subset(const double *vals, int D, const int64_t *idx, int64_t m,
     sfs_item *it = (sfs_item *)malloc((size_t)(m > 0 ? m : 1) * sizeof(sfs_item));
     for (int64_t j = 0; j < m; j++) {
         const double *v = vals + idx[j] * D;
-        double s = 0.0;
-        for (int d = 0; d < D; d++) s += v[d];
+        double s = 0.0;   /* clamped: +inf and -inf never meet, the sum stays monotone */
+        for (int d = 0; d < D; d++) s += v[d] > 1e300 ? 1e300 : (v[d] < -1e300 ? -1e300 : v[d]);
         it[j].s = s; it[j].i = idx[j];
     }
     g_sfs_vals = vals; g_sfs_D = D;

@@ -1,0 +1,212 @@
+"""HIP path vs oracle beyond the golden fixtures: seeded synthetic streams at
+larger N (device generator), all partitioners, edge cases the reference's
+semantics reach (empty, single tuple, all duplicates, P=1, D=1, NaN, infinities,
+non-f32 values -> f64 path, score ties, ±0), repeated queries on one context."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import Oracle
+
+pytestmark = pytest.mark.gpu
+
+DISTS = {"uniform": 0, "correlated": 1, "anti_correlated": 2, "std_anti": 3, "mixed": 4}
+
+
+def run_query(make, vals, P, algo, ids=None, sem="reference"):
+    eng = make(vals.shape[1], P, algo, semantics=sem)
+    out = eng.query(vals, ids)
+    st = eng.stats()
+    eng.close()
+    return out, st
+
+
+def check_vs_oracle(make, orc, vals, P, algo, sem=0):
+    (ids, org), (ls, sv) = run_query(make, vals, P, algo, sem="complete" if sem else "reference")
+    exp, keys, els, esv = orc.query_sfs(algo, vals, P, 1000.0, sem)
+    np.testing.assert_array_equal(ids, exp)
+    np.testing.assert_array_equal(org, keys[exp])
+    np.testing.assert_array_equal(ls, els)
+    np.testing.assert_array_equal(sv, esv)
+    return len(ids)
+
+
+@pytest.mark.parametrize("dist", list(DISTS))
+@pytest.mark.parametrize("D", [2, 3, 5, 8])
+def test_synth_streams_vs_oracle(dist, D, gpu_engine_factory, oracle):
+    n = 60000 if dist != "std_anti" else 20000
+    vals = oracle.synth(DISTS[dist], D, n, seed=100 + D)
+    for algo, P in (("mr-angle", 16), ("mr-dim", 8), ("mr-grid", 8)):
+        check_vs_oracle(gpu_engine_factory, oracle, vals, P, algo)
+
+
+def test_device_generator_matches_host(gpu_engine_factory, oracle):
+    import skyline
+    for dist in DISTS.values():
+        for D in (1, 2, 4, 7, 8, 16):
+            n = 5000
+            eng = gpu_engine_factory(D, 4)
+            dv = torch.empty((n, D), dtype=torch.float64, device="cuda")
+            di = torch.empty(n, dtype=torch.int64, device="cuda")
+            eng.synth_dev(dist, n, dv, di, seed=99, id0=12345)
+            eng.sync()
+            hv, hi = skyline.synth_host(dist, D, n, seed=99, id0=12345)
+            ov = oracle.synth(dist, D, n, seed=99, id0=12345)
+            np.testing.assert_array_equal(dv.cpu().numpy(), hv)
+            np.testing.assert_array_equal(hv, ov)
+            np.testing.assert_array_equal(di.cpu().numpy(), hi)
+            eng.close()
+
+
+def test_repeated_queries_one_context(gpu_engine_factory, oracle):
+    eng = gpu_engine_factory(4, 8, "mr-angle")
+    for seed in range(4):
+        for n in (100000, 3000, 0, 50000):
+            vals = oracle.synth(seed % 4, 4, n, seed=seed)
+            ids, _ = eng.query(vals)
+            exp, _, els, esv = oracle.query_sfs("angle", vals, 8)
+            np.testing.assert_array_equal(ids, exp)
+            ls, sv = eng.stats()
+            np.testing.assert_array_equal(ls, els)
+            np.testing.assert_array_equal(sv, esv)
+    eng.close()
+
+
+def test_edge_empty_and_single(gpu_engine_factory):
+    eng = gpu_engine_factory(3, 4)
+    ids, org = eng.query(np.zeros((0, 3)))
+    assert len(ids) == 0
+    ids, org = eng.query(np.array([[5.0, 1.0, 2.0]]), np.array([42]))
+    assert ids.tolist() == [42]
+    ls, sv = eng.stats()
+    assert ls.sum() == 1 and sv.sum() == 1
+    eng.close()
+
+
+def test_all_duplicates_survive(gpu_engine_factory):
+    vals = np.tile(np.array([[3.0, 4.0, 5.0, 6.0]]), (70000, 1))
+    (ids, _), (ls, sv) = run_query(gpu_engine_factory, vals, 8, "mr-angle")
+    assert len(ids) == 70000          # equal vectors never dominate each other
+    assert ls.sum() == 70000 and sv.sum() == 70000
+
+
+def test_one_partition_and_one_dim(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(5)
+    vals = rng.integers(0, 50, size=(30000, 1)).astype(np.float64)
+    check_vs_oracle(gpu_engine_factory, oracle, vals, 1, "mr-angle")
+    check_vs_oracle(gpu_engine_factory, oracle, vals, 8, "mr-dim")
+    vals = rng.integers(0, 1000, size=(30000, 6)).astype(np.float64)
+    check_vs_oracle(gpu_engine_factory, oracle, vals, 1, "mr-grid")
+
+
+def test_nan_is_rejected(gpu_engine_factory):
+    from skyline._abi import SkylineError
+    vals = np.ones((100, 2))
+    vals[37, 1] = np.nan
+    eng = gpu_engine_factory(2, 4)
+    with pytest.raises(SkylineError) as e:
+        eng.query(vals)
+    assert e.value.code == -4
+    eng.close()
+
+
+def test_f64_path_and_score_ties(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(11)
+    # not representable in f32 -> f64 rows; sums inexact -> tie-safe SFS
+    vals = rng.random((40000, 4)) * 1000.0
+    check_vs_oracle(gpu_engine_factory, oracle, vals, 8, "mr-angle")
+    # equal-sum, mutually dominating-by-rounding data: huge and tiny magnitudes mixed
+    base = rng.integers(0, 4, size=(20000, 3)).astype(np.float64)
+    base[:, 0] *= 1e17
+    base[:, 1] += rng.integers(0, 3, size=20000)
+    check_vs_oracle(gpu_engine_factory, oracle, base, 4, "mr-dim")
+    check_vs_oracle(gpu_engine_factory, oracle, base, 4, "mr-angle")
+
+
+def test_infinities_and_signed_zero(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(3)
+    vals = rng.integers(0, 20, size=(20000, 3)).astype(np.float64)
+    vals[rng.random(20000) < 0.05, 1] = np.inf
+    vals[rng.random(20000) < 0.05, 2] = -np.inf
+    vals[rng.random(20000) < 0.2, 0] = -0.0
+    for algo in ("mr-angle", "mr-dim", "mr-grid"):
+        n = check_vs_oracle(gpu_engine_factory, oracle, vals, 8, algo)
+        bnl, _, _, _ = oracle.query_bnl(algo[3:], vals, np.arange(len(vals)), 8)
+        assert n == len(bnl)
+
+
+def test_negative_values(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(8)
+    vals = rng.integers(-500, 500, size=(50000, 4)).astype(np.float64)
+    for algo in ("mr-angle", "mr-dim", "mr-grid"):
+        check_vs_oracle(gpu_engine_factory, oracle, vals, 8, algo)
+
+
+def test_grid_complete_semantics(gpu_engine_factory, oracle):
+    vals = oracle.synth(0, 4, 50000, seed=3)
+    n_ref = check_vs_oracle(gpu_engine_factory, oracle, vals, 8, "mr-grid", sem=0)
+    n_all = check_vs_oracle(gpu_engine_factory, oracle, vals, 8, "mr-grid", sem=1)
+    assert n_all >= n_ref
+    assert len(oracle.brute(vals[:3000])) >= 0
+
+
+def test_keys_random_f64_bit_exact(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(21)
+    for D in (2, 3, 4, 8, 13, 16):
+        v = rng.random((20000, D)) * rng.choice([1e-3, 1.0, 1e3, 1e6], size=(20000, 1))
+        v[::7] = np.floor(v[::7])
+        v[::11, 0] = 0.0
+        for algo, name in ((0, "dim"), (1, "grid"), (2, "angle")):
+            for P in (1, 7, 16, 256):
+                eng = gpu_engine_factory(D, P, ["mr-dim", "mr-grid", "mr-angle"][algo], 1000.0)
+                np.testing.assert_array_equal(eng.partition_keys(v), oracle.keys(name, v, P), err_msg=f"{name} D={D} P={P}")
+                eng.close()
+
+
+def test_angle_keys_near_partition_boundaries(gpu_engine_factory, oracle):
+    """Tuples whose exact avg*P sits on / next to an integer force the exact fdlibm
+    fallback of the filtered MR-Angle key; all must match the oracle bit for bit."""
+    rng = np.random.default_rng(4)
+    for D, P in ((2, 8), (2, 16), (3, 16), (4, 8), (8, 16), (8, 256)):
+        rows = []
+        for k in range(P + 1):
+            for eps in (0.0, 1e-12, -1e-12, 1e-7, -1e-7, 1e-4, -1e-4):
+                th = (k / P + eps) * (np.pi / 2)
+                r = rng.random() * 1000 + 1
+                v = np.zeros(D)
+                v[0] = r * np.cos(th)
+                v[1:] = r * np.sin(th) / np.sqrt(D - 1)
+                rows.append(v)
+                rows.append(np.round(v))
+        v = np.asarray(rows)
+        v = np.concatenate([v, -v[:20], np.abs(v) * 1e-16, np.abs(v) * 1e17])
+        eng = gpu_engine_factory(D, P, "mr-angle")
+        np.testing.assert_array_equal(eng.partition_keys(v), oracle.keys("angle", v, P), err_msg=f"D={D} P={P}")
+        eng.close()
+
+
+def test_angle_keys_many_random(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(12)
+    for D in (2, 4, 8):
+        v = rng.integers(0, 1001, size=(400000, D)).astype(np.float64)
+        v[rng.random(len(v)) < 0.3] = 0.0
+        v[rng.random(len(v)) < 0.1, 0] = 0.0
+        eng = gpu_engine_factory(D, 16, "mr-angle")
+        np.testing.assert_array_equal(eng.partition_keys(v), oracle.keys("angle", v, 16))
+        eng.close()
+
+
+def test_device_query_matches_host_query(gpu_engine_factory, oracle):
+    n, D = 200000, 8
+    vals = oracle.synth(2, D, n, seed=77)
+    eng = gpu_engine_factory(D, 16)
+    hid, horg = eng.query(vals, np.arange(n) + 10)
+    dv = torch.from_numpy(vals).cuda()
+    di = torch.arange(n, dtype=torch.int64, device="cuda") + 10
+    oi = torch.empty(n, dtype=torch.int64, device="cuda")
+    oo = torch.empty(n, dtype=torch.int32, device="cuda")
+    g = eng.query_dev(di, dv, oi, oo, n)
+    eng.sync()
+    np.testing.assert_array_equal(oi[:g].cpu().numpy(), hid)
+    np.testing.assert_array_equal(oo[:g].cpu().numpy(), horg)
+    eng.close()

@@ -1,0 +1,138 @@
+"""Operator-level behaviour on the GPU: local state inserts (processBuffer),
+global merge (GlobalSkylineAggregator), the whole single-process topology with
+its JSON payload, and the multi-GPU export/import decomposition (emulated with
+several contexts on one device)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_streams, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_part_insert_equals_one_shot(gpu_engine_factory, oracle):
+    from skyline.operators import _LocalPart
+    eng = gpu_engine_factory(4, 8)
+    vals = oracle.synth(2, 4, 23000, seed=5)
+    ids = np.arange(len(vals), dtype=np.int64) + 7
+    part = _LocalPart(eng, 3)
+    for s in range(0, len(vals), 5000):                     # flush every BUFFER_SIZE tuples (:232)
+        part.insert(ids[s:s + 5000], vals[s:s + 5000])
+        got_ids, got_vals = part.snapshot()
+        exp, _, _, _ = oracle.query_sfs("dim", vals[:s + 5000], 1)
+        np.testing.assert_array_equal(got_ids, ids[exp])    # insertion order
+        np.testing.assert_array_equal(got_vals, vals[exp])
+    part.close()
+    eng.close()
+
+
+def test_global_merge_lists(gpu_engine_factory, oracle):
+    rng = np.random.default_rng(2)
+    eng = gpu_engine_factory(3, 8)
+    lists_v, lists_i, pids = [], [], []
+    off = 0
+    for k in range(6):
+        n = int(rng.integers(0, 4000))
+        v = rng.integers(0, 300, size=(n, 3)).astype(np.float64)
+        lists_v.append(v)
+        lists_i.append(np.arange(off, off + n, dtype=np.int64))
+        pids.append(10 + k)
+        off += n
+    gids, gorg = eng.global_merge(pids, lists_i, lists_v)
+    allv = np.concatenate(lists_v)
+    exp = oracle.brute(allv)
+    np.testing.assert_array_equal(np.sort(gids), exp)
+    owner = np.concatenate([np.full(len(v), p) for v, p in zip(lists_v, pids)])
+    np.testing.assert_array_equal(gorg, owner[gids])
+    ls, sv = eng.stats()
+    np.testing.assert_array_equal(ls, [len(v) for v in lists_v])
+    np.testing.assert_array_equal(sv, [np.sum(owner[gids] == p) for p in pids])
+    eng.close()
+
+
+@pytest.mark.parametrize("path", [p for p in golden_streams() if "_4d" in p or "_2d" in p],
+                         ids=lambda p: os.path.basename(p)[7:-4])
+def test_run_job_json(path, oracle):
+    from skyline.operators import run_job, java_format_4f
+    g = load_golden(path)
+    vals = g["values"]
+    D = vals.shape[1]
+    lines = [f"{i}," + ",".join(str(int(x)) for x in row) for i, row in enumerate(vals)]
+    lines.insert(17, "garbage")                       # malformed CSV is dropped (:104)
+    for algo, P in (("mr-angle", 8), ("mr-dim", 8), ("mr-grid", 8)):
+        out, last = run_job(lines, [(len(lines), "1")], algo=algo, parallelism=P // 2, dims=D)
+        assert len(out) == 1
+        js = json.loads(out[0])
+        short = algo[3:]
+        exp_ids = g[f"gsky_{short}_{P}"]
+        assert js["query_id"] == "1" and js["skyline_size"] == len(exp_ids)
+        np.testing.assert_array_equal(np.sort(last[0]), exp_ids)
+        lsz, surv = g[f"lsz_{short}_{P}"], g[f"surv_{short}_{P}"]
+        opt = sum(surv[i] / lsz[i] for i in range(P) if lsz[i] > 0) / P
+        assert js["optimality"] == float(java_format_4f(opt))
+        assert "query_latency_ms" in js
+        assert '"record_count": unknown' in out[0]         # no comma in the payload (:629)
+
+
+def test_run_job_barrier_triggers(oracle):
+    """Triggers 'q,R' after R tuples: the per-key max-id barrier (:306,:351)."""
+    from skyline.operators import run_job
+    vals = oracle.synth(0, 2, 12000, seed=9)
+    lines = [f"{i}," + ",".join(str(int(x)) for x in row) for i, row in enumerate(vals)]
+    out, last = run_job(lines, [(6000, "1,5999"), (12000, "2,0")], algo="mr-angle", parallelism=2, dims=2)
+    assert len(out) == 2
+    res = [json.loads(o) for o in out]
+    assert {r["query_id"] for r in res} == {"1", "2"}
+    final = [r for r in res if r["query_id"] == "2"][0]
+    exp, _, _, _ = oracle.query_sfs("angle", vals, 4)
+    assert final["skyline_size"] == len(exp)
+
+
+def test_multi_rank_decomposition(gpu_engine_factory, oracle):
+    """Export/import of 3 shards == one query over the whole stream (ids, stats)."""
+    n, D, P, W = 90000, 6, 16, 3
+    vals = oracle.synth(2, D, n, seed=31)
+    ids = np.arange(n, dtype=np.int64)
+    single = gpu_engine_factory(D, P)
+    exp_ids, exp_org = single.query(vals, ids)
+    exp_ls, exp_sv = single.stats()
+    single.close()
+    engs = [gpu_engine_factory(D, P) for _ in range(W)]
+    shards = np.array_split(np.arange(n), W)
+    dv = [torch.from_numpy(vals[s]).cuda() for s in shards]
+    di = [torch.from_numpy(ids[s]).cuda() for s in shards]
+    exports = []
+    for e, v, i in zip(engs, dv, di):
+        ne = e.export_local_dev(i, v)
+        rows = torch.empty((max(ne, 1), D), dtype=torch.float64, device="cuda")
+        keys = torch.empty(max(ne, 1), dtype=torch.int32, device="cuda")
+        mult = torch.empty(max(ne, 1), dtype=torch.int64, device="cuda")
+        e.export_copy_dev(rows, keys, mult, ne)
+        e.sync()
+        exports.append((rows[:ne], keys[:ne], mult[:ne]))
+    urows = torch.cat([x[0] for x in exports]).contiguous()
+    ukeys = torch.cat([x[1] for x in exports]).contiguous()
+    umult = torch.cat([x[2] for x in exports]).contiguous()
+    assert int(umult.sum()) <= n
+    got = []
+    off = 0
+    for r, (e, s) in enumerate(zip(engs, shards)):
+        oi = torch.empty(len(s), dtype=torch.int64, device="cuda")
+        oo = torch.empty(len(s), dtype=torch.int32, device="cuda")
+        g = e.import_union_dev(urows, ukeys, umult, urows.shape[0], off, oi, oo, len(s))
+        e.sync()
+        got.append((oi[:g].cpu().numpy(), oo[:g].cpu().numpy()))
+        off += exports[r][0].shape[0]
+        ls, sv = e.stats()
+        np.testing.assert_array_equal(ls, exp_ls)
+        np.testing.assert_array_equal(sv, exp_sv)
+    gi = np.concatenate([x[0] for x in got])
+    go = np.concatenate([x[1] for x in got])
+    np.testing.assert_array_equal(gi, exp_ids)
+    np.testing.assert_array_equal(go, exp_org)
+    for e in engs:
+        e.close()
