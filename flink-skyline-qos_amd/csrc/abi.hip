@@ -510,16 +510,17 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
     // recount this shard's output with the imported global fates (no stats: those came from the union)
     {
         const uint32_t tiles = (p.n + kTile - 1) / kTile;
+        launch_fate_tables(p.mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
+                           p.Kp * p.M, p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(),
+                           p.pruner_fate.as<uint8_t>(), c->st);
         OutArgs oa{};
         oa.status = p.status.as<uint16_t>();
         oa.n = p.n;
         oa.blk_off = p.blk_off.as<uint32_t>();
-        oa.slot_rep = p.slot_rep.as<uint32_t>();
-        oa.m = p.m;
-        oa.pruner_slot = p.pruner_slot.as<int32_t>();
+        oa.slot_fate = p.slot_fate.as<uint8_t>();
+        oa.pruner_fate = p.pruner_fate.as<uint8_t>();
         oa.M = p.M;
-        oa.alive_l = p.alive_l.as<uint8_t>();
-        oa.alive_g = p.alive_g.as<uint8_t>();
+        oa.KM = p.Kp * p.M;
         oa.K = p.K;
         oa.out_cnt = p.out_cnt.as<uint32_t>();
         if (p.n) {

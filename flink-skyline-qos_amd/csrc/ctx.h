@@ -72,6 +72,7 @@ struct Ctx {
         k.K = Kq();
         k.dim_width = domain / (double)P;
         k.grid_mid = domain / 2.0;
+        k.margin = angle_margin(P);
         return k;
     }
     hipEvent_t take_event() {

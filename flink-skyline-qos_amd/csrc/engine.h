@@ -60,6 +60,7 @@ struct Pipe {
     DevBuf alive_l, alive_g, alive_u32, alive_scan, mult;
     // SFS
     DevBuf act, act2, keep, keep_scan, conf_rows, nconf, segs, seg_list, tiles, seg_begin, seg_end, segcnt;
+    DevBuf conf_small, seg_small, slot_fate, pruner_fate;
     // global
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     DevBuf scratch, flags, totals, orand, lsz, surv;
@@ -76,8 +77,14 @@ struct Pipe {
     std::vector<unsigned long long> h_lsz, h_surv;
     int64_t sfs_rounds = 0, sfs_pairs_upper = 0;
 
+    // pinned bump buffer for small host->device uploads (segment tables, tile lists):
+    // asynchronous, no implicit synchronisation of the stream
+    void *up = nullptr;
+    size_t up_cap = 0, up_used = 0;
+
     ~Pipe();
     int pinned(size_t bytes);
+    int upload(void *dst, const void *src, size_t bytes, hipStream_t st);
 };
 
 struct Ctx;

@@ -54,6 +54,39 @@ void DevBuf::release() {
 
 Pipe::~Pipe() {
     if (pin) (void)hipHostFree(pin);
+    if (up) (void)hipHostFree(up);
+}
+
+int Pipe::upload(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    if (!bytes) return SKY_OK;
+    const size_t need = (bytes + 255) & ~size_t(255);
+    if (up_used + need > up_cap) {
+        // wrap: every earlier upload must have been consumed before the area is reused
+        if (hipStreamSynchronize(st) != hipSuccess) {
+            set_error("stream synchronisation failed");
+            return SKY_E_HIP;
+        }
+        up_used = 0;
+        if (need > up_cap) {
+            if (up) (void)hipHostFree(up);
+            up = nullptr;
+            up_cap = std::max<size_t>(need, size_t(4) << 20);
+            if (hipHostMalloc(&up, up_cap, hipHostMallocDefault) != hipSuccess) {
+                up = nullptr;
+                up_cap = 0;
+                set_error("hipHostMalloc failed");
+                return SKY_E_NOMEM;
+            }
+        }
+    }
+    char *slot = (char *)up + up_used;
+    memcpy(slot, src, bytes);
+    up_used += need;
+    if (hipMemcpyAsync(dst, slot, bytes, hipMemcpyHostToDevice, st) != hipSuccess) {
+        set_error("upload failed");
+        return SKY_E_HIP;
+    }
+    return SKY_OK;
 }
 
 int Pipe::pinned(size_t bytes) {
@@ -126,10 +159,35 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
     SKY_TRY(p.segcnt.ensure((size_t)nseg * 4));
     SKY_TRY(p.scratch.ensure(scan_scratch_words(nrep + 1) * 4 + 64));
     SKY_TRY(p.totals.ensure(64));
-    launch_iota(p.act.as<uint32_t>(), nrep, st);
     std::vector<SfsSeg> hsegs(nseg);
     std::vector<uint32_t> work;
     std::vector<SfsTile> tiles;
+    // small partitions: the whole SFS in one workgroup each, one launch, no host sync
+    {
+        constexpr uint32_t kSmallSeg = 16384;
+        std::vector<uint32_t> small;
+        for (uint32_t k = 0; k < nseg; k++) {
+            hsegs[k] = SfsSeg{begin[k], cnt[k]};
+            if (cnt[k] && cnt[k] <= kSmallSeg) small.push_back(k);
+        }
+        if (!small.empty()) {
+            SKY_TRY(p.conf_small.ensure((size_t)nrep * rb));
+            SKY_TRY(p.seg_small.ensure(small.size() * 4));
+            SKY_TRY(p.upload(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), st));
+            SKY_TRY(p.upload(p.seg_small.p, small.data(), small.size() * 4, st));
+            c.ktimer_begin("sfs_small", st);
+            launch_sfs_small(D, p.f64, full, p.ties, std::min(512, B / 2), rows, key, p.segs.as<SfsSeg>(),
+                             p.seg_small.as<uint32_t>(), (uint32_t)small.size(), alive, p.conf_small.p, st);
+            c.ktimer_end("sfs_small", st, 0);
+            STAGE(st, "sfs_small");
+            for (uint32_t k : small) cnt[k] = 0;
+            p.sfs_rounds++;
+        }
+    }
+    bool any_big = false;
+    for (uint32_t k = 0; k < nseg; k++) any_big |= cnt[k] != 0;
+    if (!any_big) return SKY_OK;
+    launch_iota(p.act.as<uint32_t>(), nrep, st);
     for (;;) {
         work.clear();
         for (uint32_t k = 0; k < nseg; k++) {
@@ -138,8 +196,8 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         }
         if (work.empty()) break;
         p.sfs_rounds++;
-        HIP_TRY(hipMemcpyAsync(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(p.seg_list.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, st));
+        SKY_TRY(p.upload(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), st));
+        SKY_TRY(p.upload(p.seg_list.p, work.data(), work.size() * 4, st));
         launch_block_sky(D, p.f64, full, p.ties, B, rows, key, p.act.as<uint32_t>(), p.segs.as<SfsSeg>(),
                          p.seg_list.as<uint32_t>(), (uint32_t)work.size(), alive, p.conf_rows.p,
                          p.nconf.as<uint32_t>(), st);
@@ -158,7 +216,7 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         }
         if (out == 0) break;
         SKY_TRY(p.tiles.ensure(tiles.size() * sizeof(SfsTile)));
-        HIP_TRY(hipMemcpyAsync(p.tiles.p, tiles.data(), tiles.size() * sizeof(SfsTile), hipMemcpyHostToDevice, st));
+        SKY_TRY(p.upload(p.tiles.p, tiles.data(), tiles.size() * sizeof(SfsTile), st));
         c.ktimer_begin("sfs_filter", st);
         launch_filter_rest(D, p.f64, full, B, rows, p.act.as<uint32_t>(), p.tiles.as<SfsTile>(),
                            (uint32_t)tiles.size(), p.conf_rows.p, p.nconf.as<uint32_t>(), p.keep.as<uint32_t>(), st);
@@ -173,6 +231,7 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         SKY_TRY(p.pinned(nseg * 4));
         HIP_TRY(hipMemcpyAsync(p.pin, p.segcnt.p, nseg * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        p.up_used = 0;
         const uint32_t *sc = (const uint32_t *)p.pin;
         uint32_t run = 0;
         for (uint32_t k = 0; k < nseg; k++) {
@@ -196,6 +255,7 @@ static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const 
         off += (s.second + 15) & ~size_t(15);
     }
     HIP_TRY(hipStreamSynchronize(st));
+    p.up_used = 0;
     off = 0;
     for (size_t i = 0; i < srcs.size(); i++) {
         if (srcs[i].second) memcpy(dsts[i], (char *)p.pin + off, srcs[i].second);
@@ -272,66 +332,78 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     STAGE(st, "filter");
     scan_excl_u32(p.blk_cnt.as<uint32_t>(), p.blk_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>(),
                   p.scratch.as<uint32_t>(), st);
-    uint32_t m = 0, flags = 0;
-    p.h_dup.assign((size_t)p.Kp * p.M, 0);
-    SKY_TRY(sync_read(p, st, {{p.totals.p, 4}, {p.flags.p, 4}, {p.dup_cnt.p, p.h_dup.size() * 4}},
-                      {&m, &flags, p.h_dup.data()}));
     if (tm) tm->mark(2, st);
+
+    // ---- compaction into candidate slots + one slot per duplicated pruner; the row
+    //      type (f32/f64), the OR/AND of the sort keys and the slot count are all
+    //      produced on the device and read back in ONE synchronisation
+    const int KM = p.Kp * p.M;
+    const size_t rb64 = row_bytes(true, D);
+    const size_t cap = (size_t)n + KM;
+    SKY_TRY(p.rows.ensure(cap * rb64));
+    SKY_TRY(p.sortkey.ensure(cap * 8));
+    SKY_TRY(p.slot_src.ensure(cap * 4));
+    SKY_TRY(p.pr_entries.ensure((size_t)KM * 4));
+    SKY_TRY(p.pruner_slot.ensure((size_t)KM * 4));
+    SKY_TRY(p.orand.ensure(16));
+    HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
+        HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
+    CompactArgs ca{};
+    ca.vals = in.vals;
+    ca.n = n;
+    ca.status = p.status.as<uint16_t>();
+    ca.blk_off = p.blk_off.as<uint32_t>();
+    ca.rows = p.rows.p;
+    ca.sortkey = p.sortkey.as<uint64_t>();
+    ca.slot_src = p.slot_src.as<uint32_t>();
+    ca.flags = p.flags.as<uint32_t>();
+    ca.orand = p.orand.as<unsigned long long>();
+    launch_compact(D, ca, st);
+    AppendArgs aa{};
+    aa.pruners = p.pruners.as<double>();
+    aa.dup_cnt = p.dup_cnt.as<uint32_t>();
+    aa.Kp = p.Kp;
+    aa.M = p.M;
+    aa.m_total = p.totals.as<uint32_t>();
+    aa.nps_total = p.totals.as<uint32_t>() + 5;
+    aa.entries = p.pr_entries.as<int32_t>();
+    aa.pruner_slot = p.pruner_slot.as<int32_t>();
+    aa.rows = p.rows.p;
+    aa.sortkey = p.sortkey.as<uint64_t>();
+    aa.slot_src = p.slot_src.as<uint32_t>();
+    aa.flags = p.flags.as<uint32_t>();
+    aa.orand = p.orand.as<unsigned long long>();
+    launch_append_pruners(D, aa, st);
+    STAGE(st, "compact");
+    uint32_t m = 0, nps = 0, flags = 0;
+    unsigned long long orand[2] = {0ull, 0ull};
+    SKY_TRY(sync_read(p, st, {{p.totals.p, 4}, {p.totals.as<uint32_t>() + 5, 4}, {p.flags.p, 4}, {p.orand.p, 16}},
+                      {&m, &nps, &flags, orand}));
+    if (tm) tm->mark(3, st);
     if (flags & kFlagNaN) {
         set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; rejected");
         return SKY_E_NAN;
     }
     p.m = m;
+    p.nps = nps;
     p.f64 = (flags & kFlagNotF32) != 0;
-    p.h_entries.clear();
-    std::vector<int32_t> pslot((size_t)p.Kp * p.M, -1);
-    for (size_t q = 0; q < p.h_dup.size(); q++)
-        if (p.h_dup[q]) {
-            pslot[q] = (int32_t)(m + p.h_entries.size());
-            p.h_entries.push_back((int32_t)q);
-        }
-    p.nps = (uint32_t)p.h_entries.size();
-    p.mt = m + p.nps;
-    SKY_TRY(p.pr_entries.ensure(std::max<size_t>(p.nps, 1) * 4));
-    SKY_TRY(p.pruner_slot.ensure(pslot.size() * 4));
-    if (p.nps) HIP_TRY(hipMemcpyAsync(p.pr_entries.p, p.h_entries.data(), p.nps * 4, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(p.pruner_slot.p, pslot.data(), pslot.size() * 4, hipMemcpyHostToDevice, st));
-
+    p.ties = (flags & kFlagScoreTies) != 0;
+    p.mt = m + nps;
     const uint32_t mt = p.mt;
     const size_t rb = row_bytes(p.f64, D);
-    SKY_TRY(p.rows.ensure(std::max<size_t>(mt, 1) * rb));
-    SKY_TRY(p.sortkey.ensure(std::max<size_t>(mt, 1) * 8));
-    SKY_TRY(p.slot_src.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
     SKY_TRY(p.alive_g.ensure(std::max<size_t>(mt, 1)));
+    SKY_TRY(p.slot_fate.ensure(std::max<size_t>(mt, 1)));
+    SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
+    uint32_t mr = 0;
     if (mt) {
-        CompactArgs ca{};
-        ca.vals = in.vals;
-        ca.n = n;
-        ca.status = p.status.as<uint16_t>();
-        ca.blk_off = p.blk_off.as<uint32_t>();
-        ca.rows = p.rows.p;
-        ca.sortkey = p.sortkey.as<uint64_t>();
-        ca.slot_src = p.slot_src.as<uint32_t>();
-        ca.flags = p.flags.as<uint32_t>();
-        if (m) launch_compact(D, p.f64, ca, st);
-        launch_append_pruners(D, p.f64, p.pruners.as<double>(), p.M, p.pr_entries.as<int32_t>(), p.nps, m, p.rows.p,
-                              p.sortkey.as<uint64_t>(), p.slot_src.as<uint32_t>(), p.flags.as<uint32_t>(), st);
-        STAGE(st, "compact");
-        if (tm) tm->mark(3, st);
-
         // ---- sort the candidates by (partition, score, hash)
         SKY_TRY(p.perm.ensure((size_t)mt * 4));
         SKY_TRY(p.key_alt.ensure((size_t)mt * 8));
         SKY_TRY(p.val_alt.ensure((size_t)mt * 4));
-        SKY_TRY(p.orand.ensure(16));
         SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mt), scan_scratch_words(mt + 1)) * 4 + 64));
         launch_iota(p.perm.as<uint32_t>(), mt, st);
-        radix_key_orand(p.sortkey.as<uint64_t>(), mt, p.orand.as<unsigned long long>(), st);
-        unsigned long long orand[2];
-        SKY_TRY(sync_read(p, st, {{p.orand.p, 16}, {p.flags.p, 4}}, {orand, &flags}));
-        p.ties = (flags & kFlagScoreTies) != 0;
         const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
                                           p.val_alt.as<uint32_t>(), mt, orand[0] ^ orand[1],
                                           p.scratch.as<uint32_t>(), st);
@@ -368,18 +440,18 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_rep_of(D, p.f64, ra, st);
         scan_excl_u32(ra.repflag, ra.repscan, mt, p.totals.as<uint32_t>() + 1, p.scratch.as<uint32_t>(), st);
         launch_build_reps(D, p.f64, ra, st);
-        STAGE(st, "dedup");
-        uint32_t mr = 0;
-        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}}, {&mr}));
-        p.mr = mr;
         SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
         SKY_TRY(p.seg_end.ensure((size_t)p.Kp * 4));
         HIP_TRY(hipMemsetAsync(p.seg_begin.p, 0, (size_t)p.Kp * 4, st));
         HIP_TRY(hipMemsetAsync(p.seg_end.p, 0, (size_t)p.Kp * 4, st));
-        launch_seg_bounds(p.rep_key.as<uint64_t>(), mr, p.seg_begin.as<uint32_t>(), p.seg_end.as<uint32_t>(), st);
+        launch_seg_bounds(p.rep_key.as<uint64_t>(), mt, p.totals.as<uint32_t>() + 1, p.seg_begin.as<uint32_t>(),
+                          p.seg_end.as<uint32_t>(), st);
+        STAGE(st, "dedup");
         std::vector<uint32_t> sb(p.Kp), se(p.Kp);
-        SKY_TRY(sync_read(p, st, {{p.seg_begin.p, (size_t)p.Kp * 4}, {p.seg_end.p, (size_t)p.Kp * 4}},
-                          {sb.data(), se.data()}));
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
+                                  {p.seg_end.p, (size_t)p.Kp * 4}},
+                          {&mr, sb.data(), se.data()}));
+        p.mr = mr;
         for (int k = 0; k < p.Kp; k++) se[k] -= sb[k];
         if (tm) tm->mark(5, st);
 
@@ -392,24 +464,24 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         if (in.global && !in.single) {
             SKY_TRY(p.alive_u32.ensure((size_t)mr * 4));
             SKY_TRY(p.alive_scan.ensure((size_t)mr * 4));
+            SKY_TRY(p.gkey.ensure((size_t)mr * 8));
+            SKY_TRY(p.gval.ensure((size_t)mr * 4));
             launch_flag_u8_to_u32(p.alive_l.as<uint8_t>(), mr, p.alive_u32.as<uint32_t>(), st);
             scan_excl_u32(p.alive_u32.as<uint32_t>(), p.alive_scan.as<uint32_t>(), mr, p.totals.as<uint32_t>() + 2,
                           p.scratch.as<uint32_t>(), st);
+            HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
+                HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
+            launch_global_keys(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), mr,
+                               p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(), p.orand.as<unsigned long long>(), st);
             uint32_t mg = 0;
-            SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 2, 4}}, {&mg}));
+            SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 2, 4}, {p.orand.p, 16}}, {&mg, orand}));
             p.mg = mg;
             HIP_TRY(hipMemsetAsync(p.alive_g.p, 0, mr, st));
             if (mg) {
-                SKY_TRY(p.gkey.ensure((size_t)mg * 8));
-                SKY_TRY(p.gval.ensure((size_t)mg * 4));
                 SKY_TRY(p.gkey_alt.ensure((size_t)mg * 8));
                 SKY_TRY(p.gval_alt.ensure((size_t)mg * 4));
                 SKY_TRY(p.grows.ensure((size_t)mg * rb));
                 SKY_TRY(p.galive.ensure((size_t)mg));
-                launch_global_keys(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), mr,
-                                   p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(), st);
-                radix_key_orand(p.gkey.as<uint64_t>(), mg, p.orand.as<unsigned long long>(), st);
-                SKY_TRY(sync_read(p, st, {{p.orand.p, 16}}, {orand}));
                 const bool galt = radix_sort_pairs(p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(),
                                                    p.gkey_alt.as<uint64_t>(), p.gval_alt.as<uint32_t>(), mg,
                                                    orand[0] ^ orand[1], p.scratch.as<uint32_t>(), st);
@@ -425,6 +497,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
         }
     }
+    launch_fate_tables(mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(), KM,
+                       p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(), p.pruner_fate.as<uint8_t>(), st);
     if (tm) tm->mark(7, st);
 
     // ---- per-tuple fate: stats + output counts
@@ -434,12 +508,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     oa.status = p.status.as<uint16_t>();
     oa.n = n;
     oa.blk_off = p.blk_off.as<uint32_t>();
-    oa.slot_rep = p.slot_rep.as<uint32_t>();
-    oa.m = p.m;
-    oa.pruner_slot = p.pruner_slot.as<int32_t>();
+    oa.slot_fate = p.slot_fate.as<uint8_t>();
+    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;
-    oa.alive_l = p.alive_l.as<uint8_t>();
-    oa.alive_g = p.alive_g.as<uint8_t>();
+    oa.KM = p.Kp * p.M;
     oa.given_origin = in.origin;
     oa.given_w = in.weights;
     oa.K = p.K;
@@ -474,12 +546,10 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     oa.status = p.status.as<uint16_t>();
     oa.n = p.n;
     oa.blk_off = p.blk_off.as<uint32_t>();
-    oa.slot_rep = p.slot_rep.as<uint32_t>();
-    oa.m = p.m;
-    oa.pruner_slot = p.pruner_slot.as<int32_t>();
+    oa.slot_fate = p.slot_fate.as<uint8_t>();
+    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;
-    oa.alive_l = p.alive_l.as<uint8_t>();
-    oa.alive_g = p.alive_g.as<uint8_t>();
+    oa.KM = p.Kp * p.M;
     oa.given_origin = in.origin;
     oa.given_w = in.weights;
     oa.K = p.K;

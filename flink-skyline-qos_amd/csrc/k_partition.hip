@@ -326,52 +326,158 @@ __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part
     return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffffu);
 }
 
+// Blocked tile layout for the status-word passes: thread t of tile b owns the
+// kItems CONSECUTIVE tuples b*kTile + t*kItems ...; its 8 status words are one
+// 16-byte load, and index order inside the tile is (thread, item) order, so one
+// block-wide exclusive scan per tile gives order-preserving ranks.
+__device__ __forceinline__ void load_status8(const uint16_t *__restrict__ status, uint32_t n, uint32_t i0,
+                                             uint16_t (&st)[kItems]) {
+    if (i0 + kItems <= n) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(status + i0);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            st[2 * k] = (uint16_t)(w[k] & 0xffffu);
+            st[2 * k + 1] = (uint16_t)(w[k] >> 16);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) st[k] = i0 + k < n ? status[i0 + k] : (uint16_t)0;
+    }
+}
+
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_w, uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; i++) {
+        const uint32_t c = s_w[i];
+        wb += i < w ? c : 0u;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return wb + inc - v;
+}
+
 template <typename T, int D>
+__device__ __forceinline__ uint64_t emit_candidate(const double *__restrict__ vals, uint32_t i, uint32_t part,
+                                                   T *rows, uint32_t slot, uint64_t *sortkey, uint32_t &lflags) {
+    constexpr int DP = padded_dims<T>(D);
+    double v[D];
+    load_row<D>(vals + (size_t)i * D, v);
+    T tv[D];
+#pragma unroll
+    for (int d = 0; d < D; d++) tv[d] = (T)v[d];
+    store_row<T, D>(rows + (size_t)slot * DP, tv);
+    const uint64_t key = make_sortkey<T, D>(tv, part, lflags);
+    sortkey[slot] = key;
+    return key;
+}
+
+// Order-preserving compaction of the candidates.  The row type is chosen on the
+// device: f32 unless the filter saw a candidate value that is not exactly an f32.
+template <int D>
 __global__ __launch_bounds__(kThreads) void k_compact(CompactArgs a) {
     __shared__ uint32_t s_w[kThreads / 64];
-    constexpr int DP = padded_dims<T>(D);
-    T *rows = reinterpret_cast<T *>(a.rows);
+    const bool f64 = (*a.flags & kFlagNotF32) != 0;
     uint32_t lflags = 0;
-    uint32_t run = a.blk_off[blockIdx.x];
-    const uint32_t base = blockIdx.x * kTile;
-#pragma unroll 1
-    for (int r = 0; r < kItems; r++) {
-        if (base + r * kThreads >= a.n) break;                       // block-uniform
-        const uint32_t i = base + r * kThreads + threadIdx.x;
-        const uint16_t st = i < a.n ? a.status[i] : 0;
-        const bool cand = i < a.n && (st & 0xff) == kCodeCandidate;
-        const uint32_t slot = block_rank(cand, s_w, run);
-        if (cand) {
-            double v[D];
-            load_row<D>(a.vals + (size_t)i * D, v);
-            T tv[D];
+    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kItems;
+    uint16_t st[kItems];
+    load_status8(a.status, a.n, i0, st);
+    uint32_t c = 0;
 #pragma unroll
-            for (int d = 0; d < D; d++) tv[d] = (T)v[d];
-            store_row<T, D>(rows + (size_t)slot * DP, tv);
-            a.sortkey[slot] = make_sortkey<T, D>(tv, st >> 8, lflags);
-            a.slot_src[slot] = i;
-        }
+    for (int k = 0; k < kItems; k++) c += (i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate) ? 1u : 0u;
+    uint32_t tot;
+    uint32_t slot = a.blk_off[blockIdx.x] + block_scan_excl(c, s_w, tot);
+    uint64_t o = 0, an = ~0ull;
+    for (int k = 0; k < kItems; k++) {
+        if (!(i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate)) continue;
+        const uint32_t i = i0 + k;
+        const uint64_t key =
+            f64 ? emit_candidate<double, D>(a.vals, i, st[k] >> 8, (double *)a.rows, slot, a.sortkey, lflags)
+                : emit_candidate<float, D>(a.vals, i, st[k] >> 8, (float *)a.rows, slot, a.sortkey, lflags);
+        a.slot_src[slot] = i;
+        o |= key;
+        an &= key;
+        slot++;
+    }
+    // OR / AND of the sort keys (which key bytes vary -> radix passes), wave-reduced
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        o |= __shfl_xor(o, s, 64);
+        an &= __shfl_xor(an, s, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && tot) {
+        atomicOr(&a.orand[0], (unsigned long long)o);
+        atomicAnd(&a.orand[1], (unsigned long long)an);
     }
     if (lflags) atomicOr(a.flags, lflags);
 }
 
+// One workgroup: every pruner that some tuple duplicates becomes one more candidate
+// slot (m + e) carrying that duplicate group; builds entries[e] = k*M+j and
+// pruner_slot[k*M+j] on the device (no host round trip).
 template <typename T, int D>
-__global__ void k_append_pruners(const double *__restrict__ pruners, int M, const int32_t *__restrict__ entries,
-                                 uint32_t nps, uint32_t m, T *__restrict__ rows, uint64_t *__restrict__ sortkey,
-                                 uint32_t *__restrict__ slot_src, uint32_t *__restrict__ flags) {
-    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= nps) return;
+__device__ __forceinline__ uint64_t emit_pruner(const double *pr, uint32_t part, T *rows_t, uint32_t slot,
+                                                uint64_t *sortkey, uint32_t &lflags) {
     constexpr int DP = padded_dims<T>(D);
-    const int32_t kj = entries[e];
-    const int k = kj / M;
     T tv[D];
 #pragma unroll
-    for (int d = 0; d < D; d++) tv[d] = (T)pruners[(size_t)kj * D + d];
-    uint32_t lflags = 0;
-    store_row<T, D>(rows + (size_t)(m + e) * DP, tv);
-    sortkey[m + e] = make_sortkey<T, D>(tv, (uint32_t)k, lflags);
-    slot_src[m + e] = 0x80000000u | e;
-    if (lflags) atomicOr(flags, lflags);
+    for (int d = 0; d < D; d++) tv[d] = (T)pr[d];
+    store_row<T, D>(rows_t + (size_t)slot * DP, tv);
+    const uint64_t key = make_sortkey<T, D>(tv, part, lflags);
+    sortkey[slot] = key;
+    return key;
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
+    __shared__ uint32_t s_w[kThreads / 64];
+    const bool f64 = (*a.flags & kFlagNotF32) != 0;
+    const uint32_t m = *a.m_total;
+    const int KM = a.Kp * a.M;
+    uint32_t run = 0, lflags = 0;
+    uint64_t o = 0, an = ~0ull;
+    for (int q0 = 0; q0 < KM; q0 += kThreads) {
+        const int q = q0 + threadIdx.x;
+        const bool has = q < KM && a.dup_cnt[q] > 0;
+        uint32_t tot;
+        const uint32_t e = run + block_scan_excl(has ? 1u : 0u, s_w, tot);
+        if (has) {
+            const uint32_t slot = m + e;
+            a.entries[e] = q;
+            a.pruner_slot[q] = (int32_t)slot;
+            a.slot_src[slot] = 0x80000000u | e;
+            const double *pr = a.pruners + (size_t)q * D;
+            const uint64_t key = f64 ? emit_pruner<double, D>(pr, q / a.M, (double *)a.rows, slot, a.sortkey, lflags)
+                                     : emit_pruner<float, D>(pr, q / a.M, (float *)a.rows, slot, a.sortkey, lflags);
+            o |= key;
+            an &= key;
+        } else if (q < KM) {
+            a.pruner_slot[q] = -1;
+        }
+        run += tot;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        o |= __shfl_xor(o, s, 64);
+        an &= __shfl_xor(an, s, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && run) {
+        atomicOr(&a.orand[0], (unsigned long long)o);
+        atomicAnd(&a.orand[1], (unsigned long long)an);
+    }
+    if (lflags) atomicOr(a.flags, lflags);
+    if (threadIdx.x == 0) *a.nps_total = run;
 }
 
 // ---- duplicate collapse after the sort --------------------------------------
@@ -429,10 +535,12 @@ __global__ __launch_bounds__(kThreads) void k_build_reps(RepArgs a) {
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_seg_bounds(const uint64_t *__restrict__ rep_key, uint32_t mr,
+__global__ __launch_bounds__(kThreads) void k_seg_bounds(const uint64_t *__restrict__ rep_key,
+                                                         const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ seg_begin,
                                                          uint32_t *__restrict__ seg_end) {
     const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t mr = *d_mr;
     if (r >= mr) return;
     const uint32_t p = (uint32_t)(rep_key[r] >> 56);
     if (r == 0 || (uint32_t)(rep_key[r - 1] >> 56) != p) seg_begin[p] = r;
@@ -456,96 +564,129 @@ __global__ __launch_bounds__(kThreads) void k_rep_mult(uint32_t mt, const uint32
 }
 
 // ---- output: per tuple local / global membership ------------------------------
-struct OutLds {
-    unsigned long long lsz[kMaxK];
-    unsigned long long surv[kMaxK];
-    uint32_t w[kThreads / 64];
-};
-
-__device__ __forceinline__ void tuple_fate(const OutArgs &a, uint32_t i, uint16_t st, uint32_t cand_slot,
-                                           bool &inl, bool &ing) {
-    const uint32_t code = st & 0xff;
-    inl = ing = false;
-    if (code == kCodeDropped) return;
-    uint32_t rep;
-    if (code == kCodeCandidate) rep = a.slot_rep[cand_slot];
-    else {
-        const int32_t ps = a.pruner_slot[(st >> 8) * a.M + (code - 1)];
-        rep = a.slot_rep[ps];
+// fate byte = inL | inG << 1, precomputed per candidate slot and per (partition,
+// pruner) duplicate group, so the per-tuple pass does at most one lookup.
+__global__ __launch_bounds__(kThreads) void k_fate_tables(uint32_t mt, const uint32_t *__restrict__ slot_rep,
+                                                          const uint8_t *__restrict__ alive_l,
+                                                          const uint8_t *__restrict__ alive_g, int KM,
+                                                          const int32_t *__restrict__ pruner_slot,
+                                                          uint8_t *__restrict__ slot_fate,
+                                                          uint8_t *__restrict__ pruner_fate) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j < mt) {
+        const uint32_t r = slot_rep[j];
+        slot_fate[j] = (uint8_t)((alive_l[r] ? 1 : 0) | (alive_g[r] ? 2 : 0));
+    } else if (j - mt < (uint32_t)KM) {
+        const uint32_t q = j - mt;
+        const int32_t ps = pruner_slot[q];
+        uint8_t f = 0;
+        if (ps >= 0) {
+            const uint32_t r = slot_rep[ps];
+            f = (uint8_t)((alive_l[r] ? 1 : 0) | (alive_g[r] ? 2 : 0));
+        }
+        pruner_fate[q] = f;
     }
-    inl = a.alive_l[rep] != 0;
-    ing = a.alive_g[rep] != 0;
 }
 
 template <bool WRITE>
 __global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
-    __shared__ OutLds s;
+    __shared__ unsigned long long s_lsz[kMaxK];
+    __shared__ unsigned long long s_surv[kMaxK];
+    __shared__ uint8_t s_pf[2048];
+    __shared__ uint32_t s_w[kThreads / 64];
     const bool stats = !WRITE && a.lsz != nullptr;
     if (stats)
-        for (int q = threadIdx.x; q < a.K; q += kThreads) { s.lsz[q] = 0; s.surv[q] = 0; }
+        for (int q = threadIdx.x; q < a.K; q += kThreads) { s_lsz[q] = 0; s_surv[q] = 0; }
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     __syncthreads();
-    uint32_t cand_run = a.blk_off[blockIdx.x];
-    uint32_t out_run = WRITE ? a.out_off[blockIdx.x] : 0u;
-    uint32_t mycnt = 0;
-    const uint32_t base = blockIdx.x * kTile;
-#pragma unroll 1
-    for (int r = 0; r < kItems; r++) {
-        if (base + r * kThreads >= a.n) break;
-        const uint32_t i = base + r * kThreads + threadIdx.x;
-        const uint16_t st = i < a.n ? a.status[i] : 0;
-        const bool cand = i < a.n && (st & 0xff) == kCodeCandidate;
-        const uint32_t slot = block_rank(cand, s.w, cand_run);
-        bool inl = false, ing = false;
-        if (i < a.n) tuple_fate(a, i, st, slot, inl, ing);
-        const bool sel = a.select_local ? inl : ing;
-        if (!WRITE) {
-            mycnt += sel;
-            if (stats) {
-                // wave-aggregate when every member lane shares one origin (the common
-                // case: duplicates of one vector), else per-lane LDS atomics
-                const int o = i < a.n ? (a.given_origin ? a.given_origin[i] : (st >> 8)) : 0;
-                const unsigned long long w = inl ? (a.given_w ? (unsigned long long)a.given_w[i] : 1ull) : 0ull;
-                const unsigned long long wg = ing ? w : 0ull;
-                const uint64_t act = __ballot(inl);
-                if (act) {
-                    const int o0 = __shfl(o, __ffsll((unsigned long long)act) - 1, 64);
-                    if (__ballot(inl && o != o0) == 0ull) {
-                        unsigned long long a1 = w, a2 = wg;
+    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kItems;
+    uint16_t st[kItems];
+    load_status8(a.status, a.n, i0, st);
+    uint32_t c = 0;
 #pragma unroll
-                        for (int sh = 32; sh >= 1; sh >>= 1) {
-                            a1 += __shfl_xor(a1, sh, 64);
-                            a2 += __shfl_xor(a2, sh, 64);
-                        }
-                        if ((threadIdx.x & 63) == 0) {
-                            atomicAdd(&s.lsz[o0], a1);
-                            if (a2) atomicAdd(&s.surv[o0], a2);
-                        }
-                    } else if (inl) {
-                        atomicAdd(&s.lsz[o], w);
-                        if (ing) atomicAdd(&s.surv[o], w);
-                    }
-                }
-            }
-            if (a.row_flags && i < a.n) a.row_flags[i] = (uint8_t)((inl ? 1 : 0) | (ing ? 2 : 0));
-        } else {
-            const uint32_t pos = block_rank(sel, s.w, out_run);
-            if (sel) {
-                if (a.ids_out) a.ids_out[pos] = a.ids ? a.ids[i] : (int64_t)i;
-                if (a.origin_out) a.origin_out[pos] = a.given_origin ? a.given_origin[i] : (int32_t)(st >> 8);
-                if (a.rows_out)
-                    for (int d = 0; d < a.D; d++) a.rows_out[(size_t)pos * a.D + d] = a.vals[(size_t)i * a.D + d];
-            }
+    for (int k = 0; k < kItems; k++) c += (i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate) ? 1u : 0u;
+    uint32_t tot;
+    uint32_t slot = a.blk_off[blockIdx.x] + block_scan_excl(c, s_w, tot);
+    uint8_t fate[kItems];
+    uint32_t nsel = 0;
+    const int shift = a.select_local ? 0 : 1;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        const uint32_t code = st[k] & 0xff;
+        uint8_t f = 0;
+        if (i0 + k < a.n) {
+            if (code == kCodeCandidate) f = a.slot_fate[slot++];
+            else if (code != kCodeDropped) f = s_pf[(st[k] >> 8) * a.M + (code - 1)];
         }
+        fate[k] = f;
+        nsel += (f >> shift) & 1u;
     }
     if (!WRITE) {
-        const uint32_t tot = block_sum(mycnt, s.w);
-        if (threadIdx.x == 0) a.out_cnt[blockIdx.x] = tot;
+        uint32_t bt;
+        (void)block_scan_excl(nsel, s_w, bt);
+        if (threadIdx.x == 0) a.out_cnt[blockIdx.x] = bt;
+        if (a.row_flags) {
+#pragma unroll
+            for (int k = 0; k < kItems; k++)
+                if (i0 + k < a.n) a.row_flags[i0 + k] = fate[k];
+        }
         if (stats) {
+            // per thread: one (origin, |L| weight, |G| weight) triple when its tuples share
+            // an origin (else per-tuple LDS atomics); per wave: one add when uniform
+            int o1 = -1;
+            bool mixed = false;
+            unsigned long long wl = 0, wg = 0;
+            for (int k = 0; k < kItems; k++) {
+                if (!(fate[k] & 1)) continue;
+                const uint32_t i = i0 + k;
+                const int o = a.given_origin ? a.given_origin[i] : (int)(st[k] >> 8);
+                const unsigned long long w = a.given_w ? (unsigned long long)a.given_w[i] : 1ull;
+                if (o1 < 0) o1 = o;
+                if (o == o1 && !mixed) {
+                    wl += w;
+                    if (fate[k] & 2) wg += w;
+                } else {
+                    mixed = true;
+                    atomicAdd(&s_lsz[o], w);
+                    if (fate[k] & 2) atomicAdd(&s_surv[o], w);
+                }
+            }
+            const bool has = o1 >= 0;
+            const uint64_t act = __ballot(has);
+            if (act) {
+                const int o0 = __shfl(o1, __ffsll((unsigned long long)act) - 1, 64);
+                if (__ballot(has && o1 != o0) == 0ull) {
+#pragma unroll
+                    for (int sh = 32; sh >= 1; sh >>= 1) {
+                        wl += __shfl_xor(wl, sh, 64);
+                        wg += __shfl_xor(wg, sh, 64);
+                    }
+                    if ((threadIdx.x & 63) == 0) {
+                        atomicAdd(&s_lsz[o0], wl);
+                        if (wg) atomicAdd(&s_surv[o0], wg);
+                    }
+                } else if (has) {
+                    atomicAdd(&s_lsz[o1], wl);
+                    if (wg) atomicAdd(&s_surv[o1], wg);
+                }
+            }
             __syncthreads();
             for (int q = threadIdx.x; q < a.K; q += kThreads) {
-                if (s.lsz[q]) atomicAdd(&a.lsz[q], s.lsz[q]);
-                if (s.surv[q]) atomicAdd(&a.surv[q], s.surv[q]);
+                if (s_lsz[q]) atomicAdd(&a.lsz[q], s_lsz[q]);
+                if (s_surv[q]) atomicAdd(&a.surv[q], s_surv[q]);
             }
+        }
+    } else {
+        uint32_t bt;
+        uint32_t pos = a.out_off[blockIdx.x] + block_scan_excl(nsel, s_w, bt);
+        for (int k = 0; k < kItems; k++) {
+            if (!((fate[k] >> shift) & 1)) continue;
+            const uint32_t i = i0 + k;
+            if (a.ids_out) a.ids_out[pos] = a.ids ? a.ids[i] : (int64_t)i;
+            if (a.origin_out) a.origin_out[pos] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
+            if (a.rows_out)
+                for (int d = 0; d < a.D; d++) a.rows_out[(size_t)pos * a.D + d] = a.vals[(size_t)i * a.D + d];
+            pos++;
         }
     }
 }
@@ -601,22 +742,19 @@ void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
     SKY_DISPATCH_D(D, (k_filter<DD><<<nblk(a.n, kTile), kThreads, lds, st>>>(a)));
 }
 
-void launch_compact(int D, bool f64, const CompactArgs &a, hipStream_t st) {
-    if (f64) { SKY_DISPATCH_D(D, (k_compact<double, DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
-    else { SKY_DISPATCH_D(D, (k_compact<float, DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
+void launch_compact(int D, const CompactArgs &a, hipStream_t st) {
+    if (a.n) { SKY_DISPATCH_D(D, (k_compact<DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
 }
 
-void launch_append_pruners(int D, bool f64, const double *pruners, int M, const int32_t *entries, uint32_t nps,
-                           uint32_t m, void *rows, uint64_t *sortkey, uint32_t *slot_src, uint32_t *flags,
-                           hipStream_t st) {
-    if (nps == 0) return;
-    if (f64) {
-        SKY_DISPATCH_D(D, (k_append_pruners<double, DD><<<nblk(nps, 64), 64, 0, st>>>(
-                              pruners, M, entries, nps, m, (double *)rows, sortkey, slot_src, flags)));
-    } else {
-        SKY_DISPATCH_D(D, (k_append_pruners<float, DD><<<nblk(nps, 64), 64, 0, st>>>(
-                              pruners, M, entries, nps, m, (float *)rows, sortkey, slot_src, flags)));
-    }
+void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
+    SKY_DISPATCH_D(D, (k_append_pruners<DD><<<1, kThreads, 0, st>>>(a)));
+}
+
+void launch_fate_tables(uint32_t mt, const uint32_t *slot_rep, const uint8_t *alive_l, const uint8_t *alive_g, int KM,
+                        const int32_t *pruner_slot, uint8_t *slot_fate, uint8_t *pruner_fate, hipStream_t st) {
+    const size_t tot = (size_t)mt + KM;
+    if (tot) k_fate_tables<<<nblk(tot, kThreads), kThreads, 0, st>>>(mt, slot_rep, alive_l, alive_g, KM, pruner_slot,
+                                                                     slot_fate, pruner_fate);
 }
 
 void launch_gather_runs(int D, bool f64, const RepArgs &a, hipStream_t st) {
@@ -634,9 +772,9 @@ void launch_build_reps(int D, bool f64, const RepArgs &a, hipStream_t st) {
     if (f64) { SKY_DISPATCH_D(D, (k_build_reps<double, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
     else { SKY_DISPATCH_D(D, (k_build_reps<float, DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a))); }
 }
-void launch_seg_bounds(const uint64_t *rep_key, uint32_t mr, uint32_t *seg_begin, uint32_t *seg_end,
-                       hipStream_t st) {
-    if (mr) k_seg_bounds<<<nblk(mr, kThreads), kThreads, 0, st>>>(rep_key, mr, seg_begin, seg_end);
+void launch_seg_bounds(const uint64_t *rep_key, uint32_t mt, const uint32_t *d_mr, uint32_t *seg_begin,
+                       uint32_t *seg_end, hipStream_t st) {
+    if (mt) k_seg_bounds<<<nblk(mt, kThreads), kThreads, 0, st>>>(rep_key, d_mr, seg_begin, seg_end);
 }
 void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src, const uint32_t *rep_of_sorted,
                      const int64_t *given_w, const uint32_t *dup_cnt, const int32_t *pr_entries,

@@ -124,6 +124,125 @@ __global__ __launch_bounds__(kThreads) void k_block_sky(const T *__restrict__ ro
     if (threadIdx.x == 0) nconf[k] = run;
 }
 
+// Whole SFS of one small partition in ONE workgroup, no host round trips: the
+// partition's representatives are consumed in chunks X of B (sorted order); each
+// chunk is tested against the confirmed skyline C so far (streamed through LDS in
+// tiles of B) and against its own earlier members; survivors are appended to C
+// (a per-partition region of `conf`).  Same result as the round-based path.
+template <typename T, int D, bool FULL, bool TIES>
+__global__ __launch_bounds__(kThreads) void k_sfs_small(const T *__restrict__ rows, const uint64_t *__restrict__ key,
+                                                        const SfsSeg *__restrict__ segs,
+                                                        const uint32_t *__restrict__ seg_list, int B,
+                                                        uint8_t *__restrict__ alive, T *__restrict__ conf) {
+    constexpr int DP = padded_dims<T>(D);
+    constexpr int PPT = 2;                                              // B <= 512 = 256 x 2
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T *s_x = reinterpret_cast<T *>(smem);                               // [B][DP]
+    T *s_c = s_x + (size_t)B * DP;                                      // [B][DP]
+    uint32_t *s_sc = reinterpret_cast<uint32_t *>(s_c + (size_t)B * DP);  // [B]
+    uint32_t *s_keep = s_sc + B;                                         // [B]
+    __shared__ uint32_t s_w[kThreads / 64];
+    const SfsSeg sg = segs[seg_list[blockIdx.x]];
+    const uint32_t base = sg.begin, cnt = sg.count;
+    T *C = conf + (size_t)base * DP;
+    uint32_t nconf = 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t x0 = 0; x0 < cnt; x0 += B) {
+        const uint32_t xk = cnt - x0 < (uint32_t)B ? cnt - x0 : (uint32_t)B;
+        const T *src = rows + (size_t)(base + x0) * DP;
+        for (uint32_t q = threadIdx.x; q < xk * DP; q += kThreads) s_x[q] = src[q];
+        for (uint32_t q = threadIdx.x; q < xk; q += kThreads) s_sc[q] = key_score<T>(key[base + x0 + q]);
+        __syncthreads();
+        T y[PPT][D];
+        bool valid[PPT], dom[PPT];
+#pragma unroll
+        for (int p = 0; p < PPT; p++) {
+            const uint32_t j = threadIdx.x + p * kThreads;
+            valid[p] = j < xk;
+            dom[p] = false;
+#pragma unroll
+            for (int d = 0; d < D; d++) y[p][d] = valid[p] ? s_x[(size_t)j * DP + d] : T(0);
+        }
+        // 1) against the confirmed skyline, tile by tile
+        for (uint32_t c0 = 0; c0 < nconf; c0 += B) {
+            const uint32_t ck = nconf - c0 < (uint32_t)B ? nconf - c0 : (uint32_t)B;
+            for (uint32_t q = threadIdx.x; q < ck * DP; q += kThreads) s_c[q] = C[(size_t)c0 * DP + q];
+            __syncthreads();
+            bool live = false;
+#pragma unroll
+            for (int p = 0; p < PPT; p++) live |= valid[p] && !dom[p];
+            if (__ballot(live) != 0ull) {
+                for (uint32_t i = 0; i < ck; i++) {
+                    T x[D];
+                    lds_row<T, D>(s_c + (size_t)i * DP, x);
+#pragma unroll
+                    for (int p = 0; p < PPT; p++) dom[p] |= dom_test<T, D, FULL>(x, y[p]);
+                    if ((i & 7u) == 7u) {
+                        bool lv = false;
+#pragma unroll
+                        for (int p = 0; p < PPT; p++) lv |= valid[p] && !dom[p];
+                        if (__ballot(lv) == 0ull) break;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // 2) against the earlier members of the chunk (and equal-score ones when TIES)
+#pragma unroll
+        for (int p = 0; p < PPT; p++) {
+            const uint32_t j = threadIdx.x + p * kThreads;
+            const uint32_t wlast = p * kThreads + (threadIdx.x | 63u);
+            const uint32_t iend = xk == 0 ? 0 : (wlast < xk ? wlast : xk - 1);
+            bool dm = dom[p];
+            for (uint32_t i = 0; i < iend; i++) {
+                if ((i & 15u) == 0u && __ballot(valid[p] && !dm) == 0ull) break;
+                T x[D];
+                lds_row<T, D>(s_x + (size_t)i * DP, x);
+                dm |= (i < j) && dom_test<T, D, FULL>(x, y[p]);
+            }
+            if constexpr (TIES) {
+                if (valid[p] && !dm) {
+                    const uint32_t sj = s_sc[j];
+                    for (uint32_t i = j + 1; i < xk && s_sc[i] == sj && !dm; i++) {
+                        T x[D];
+                        lds_row<T, D>(s_x + (size_t)i * DP, x);
+                        dm = dom_test<T, D, true>(x, y[p]);
+                    }
+                    for (uint32_t q = x0 + xk; q < cnt && !dm; q++) {
+                        if (key_score<T>(key[base + q]) != sj) break;
+                        T x[D];
+#pragma unroll
+                        for (int d = 0; d < D; d++) x[d] = rows[(size_t)(base + q) * DP + d];
+                        dm = dom_test<T, D, true>(x, y[p]);
+                    }
+                }
+            }
+            if (valid[p]) s_keep[j] = dm ? 0u : 1u;
+        }
+        __syncthreads();
+        // 3) append the chunk's survivors to C, in order
+        for (uint32_t j0 = 0; j0 < xk; j0 += kThreads) {
+            const uint32_t j = j0 + threadIdx.x;
+            const bool keep = j < xk && s_keep[j];
+            const uint64_t b = __ballot(keep);
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            if (lane == 0) s_w[w] = __popcll(b);
+            __syncthreads();
+            uint32_t wb = 0, tot = 0;
+            for (int q = 0; q < kThreads / 64; q++) { wb += q < w ? s_w[q] : 0u; tot += s_w[q]; }
+            __syncthreads();
+            if (keep) {
+                const uint32_t pos = nconf + wb + __popcll(b & lt);
+#pragma unroll
+                for (int d = 0; d < DP; d++) C[(size_t)pos * DP + d] = s_x[(size_t)j * DP + d];
+                alive[base + x0 + j] = 1;
+            }
+            nconf += tot;
+        }
+        __syncthreads();   // C's new rows (global, written by this workgroup) are read next chunk
+    }
+}
+
 template <typename T, int D, bool FULL, int PPT>
 __global__ __launch_bounds__(kThreads) void k_filter_rest(const T *__restrict__ rows, const uint32_t *__restrict__ act,
                                                           const SfsTile *__restrict__ tiles,
@@ -204,12 +323,28 @@ __global__ __launch_bounds__(kThreads) void k_iota(uint32_t *__restrict__ a, uin
 __global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__restrict__ rep_key,
                                                           const uint8_t *__restrict__ alive_l,
                                                           const uint32_t *__restrict__ alive_scan, uint32_t mr,
-                                                          uint64_t *__restrict__ gkey, uint32_t *__restrict__ gval) {
+                                                          uint64_t *__restrict__ gkey, uint32_t *__restrict__ gval,
+                                                          unsigned long long *__restrict__ orand) {
     const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
-    if (r >= mr || !alive_l[r]) return;
-    const uint32_t e = alive_scan[r];
-    gkey[e] = rep_key[r] & 0x00ffffffff000000ull;   // score field only (same layout as rep_key)
-    gval[e] = r;
+    uint64_t o = 0, an = ~0ull;
+    const bool any = __ballot(r < mr && alive_l[r]) != 0ull;
+    if (r < mr && alive_l[r]) {
+        const uint32_t e = alive_scan[r];
+        const uint64_t k = rep_key[r] & 0x00ffffffff000000ull;   // score field only (same layout as rep_key)
+        gkey[e] = k;
+        gval[e] = r;
+        o = k;
+        an = k;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        o |= __shfl_xor(o, s, 64);
+        an &= __shfl_xor(an, s, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && any) {
+        atomicOr(&orand[0], (unsigned long long)o);
+        atomicAnd(&orand[1], (unsigned long long)an);
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_import_flags(const uint8_t *__restrict__ alive_l,
@@ -280,6 +415,30 @@ void launch_block_sky(int D, bool f64, bool full, bool ties, int B, const void *
     else { SKY_DISPATCH_D(D, (block_sky_t<float, DD>(full, ties, B, rows, key, act, segs, seg_list, nseg_work, alive, conf_rows, nconf, st))); }
 }
 
+template <typename T, int D>
+static void sfs_small_t(bool full, bool ties, int B, const void *rows, const uint64_t *key, const SfsSeg *segs,
+                        const uint32_t *seg_list, uint32_t nwork, uint8_t *alive, void *conf, hipStream_t st) {
+    constexpr int DP = padded_dims<T>(D);
+    const size_t lds = 2 * (size_t)B * DP * sizeof(T) + 2 * (size_t)B * sizeof(uint32_t);
+    const T *r = (const T *)rows;
+    T *c = (T *)conf;
+    if (full) {
+        if (ties) k_sfs_small<T, D, true, true><<<nwork, kThreads, lds, st>>>(r, key, segs, seg_list, B, alive, c);
+        else k_sfs_small<T, D, true, false><<<nwork, kThreads, lds, st>>>(r, key, segs, seg_list, B, alive, c);
+    } else {
+        if (ties) k_sfs_small<T, D, false, true><<<nwork, kThreads, lds, st>>>(r, key, segs, seg_list, B, alive, c);
+        else k_sfs_small<T, D, false, false><<<nwork, kThreads, lds, st>>>(r, key, segs, seg_list, B, alive, c);
+    }
+}
+
+void launch_sfs_small(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+                      const SfsSeg *segs, const uint32_t *seg_list, uint32_t nwork, uint8_t *alive, void *conf,
+                      hipStream_t st) {
+    if (!nwork) return;
+    if (f64) { SKY_DISPATCH_D(D, (sfs_small_t<double, DD>(full, ties, B, rows, key, segs, seg_list, nwork, alive, conf, st))); }
+    else { SKY_DISPATCH_D(D, (sfs_small_t<float, DD>(full, ties, B, rows, key, segs, seg_list, nwork, alive, conf, st))); }
+}
+
 constexpr int kPPT = 4;
 
 template <typename T, int D>
@@ -312,8 +471,8 @@ void launch_iota(uint32_t *a, uint32_t n, hipStream_t st) {
 }
 
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
-                        uint64_t *gkey, uint32_t *gval, hipStream_t st) {
-    if (mr) k_global_keys<<<nb(mr), kThreads, 0, st>>>(rep_key, alive_l, alive_scan, mr, gkey, gval);
+                        uint64_t *gkey, uint32_t *gval, unsigned long long *orand, hipStream_t st) {
+    if (mr) k_global_keys<<<nb(mr), kThreads, 0, st>>>(rep_key, alive_l, alive_scan, mr, gkey, gval, orand);
 }
 
 void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, uint32_t m, void *dst,

@@ -118,7 +118,15 @@ struct KeyParams {
     int K;             // queried key space: keys >= K are dropped (reference MR-Grid)
     double dim_width;  // maxVal / partitions  (:710)
     double grid_mid;   // maxVal / 2.0          (:756)
+    double margin;     // MR-Angle fast path: distance of avg*P from an integer that is certain
 };
+
+// Error budget of the f32 estimate in t = avg*P (inputs with nonzero magnitudes in
+// [1e-15, 1e15]): per angle, input rounding (<= 2^-24 relative each for x and
+// hyp, plus sqrtf's 1 ulp) moves the angle by < 2e-7 rad and atan2f itself errs by
+// <= 6 ulp (OpenCL bound) < 1.5e-6 rad; normalised by pi/2 that is < 1.1e-6 per
+// angle, so |t_est - t| < 1.1e-6 * P.  The margin keeps a 3.5x safety factor.
+inline double angle_margin(int P) { return 1e-5 + 4e-6 * (double)P; }
 
 __device__ __forceinline__ int32_t clamp_key(int32_t p, int P) {
     p = p > P - 1 ? P - 1 : p;
@@ -144,14 +152,12 @@ __device__ __noinline__ int32_t angle_key_exact(const double *v, int P) {
 //  1. exact special case: every angle is atan2(+0, x) or atan2(y>0, ±0), i.e. exactly
 //     0, pi (x negative/-0) or pi/2 -> normalized 0, 2, 1 exactly; the remaining
 //     f64 ops are replayed as the reference does them (all-zero tuples land here);
-//  2. f32 estimate of sum(atan2/(pi/2)); if t = avg*P is farther than kKeyMargin
-//     from an integer, floor(t) IS the exact key (f32 error is < 1e-5 in t for
-//     inputs with nonzero magnitudes in [1e-15, 1e15]);
-//  3. otherwise the exact fdlibm path.
-constexpr double kKeyMargin = 2e-3;
+//  2. f32 estimate of sum(atan2/(pi/2)); if t = avg*P is farther than `margin`
+//     (angle_margin) from an integer, floor(t) IS the exact key;
+//  3. otherwise the exact fdlibm path (~1e-4 of the reference-formula tuples).
 
 template <int D>
-__device__ __forceinline__ int32_t angle_key(const double (&v)[D], int P) {
+__device__ __forceinline__ int32_t angle_key(const double (&v)[D], int P, double margin) {
     if (D < 2) return 0;
     double s[D > 1 ? D - 1 : 1];
     bool special = true, ranged = true;
@@ -190,7 +196,7 @@ __device__ __forceinline__ int32_t angle_key(const double (&v)[D], int P) {
         const double t = est * (2.0 / 3.141592653589793) / (double)(D - 1) * (double)P;
         const double fl = floor(t);
         const double fr = t - fl;
-        if (fr > kKeyMargin && fr < 1.0 - kKeyMargin) return clamp_key((int32_t)fl, P);
+        if (fr > margin && fr < 1.0 - margin) return clamp_key((int32_t)fl, P);
     }
     return angle_key_exact<D>(v, P);
 }
@@ -205,7 +211,7 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
             if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
         return (int32_t)mask;
     }
-    return angle_key<D>(v, kp.P);
+    return angle_key<D>(v, kp.P, kp.margin);
 }
 
 // ---- dominance ----------------------------------------------------------------

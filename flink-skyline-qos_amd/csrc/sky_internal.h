@@ -70,15 +70,30 @@ struct CompactArgs {
     uint32_t n;
     const uint16_t *status;
     const uint32_t *blk_off;      // exclusive scan of blk_cnt
-    void *rows;                   // [mt][DP] T
+    void *rows;                   // [mt][DP] f32 or f64 (chosen on the device from flags)
     uint64_t *sortkey;            // [mt]
     uint32_t *slot_src;           // [mt] source tuple index (bit31: pruner entry)
     uint32_t *flags;
+    unsigned long long *orand;    // {OR, AND} of all sort keys
 };
-void launch_compact(int D, bool f64, const CompactArgs &a, hipStream_t st);
-void launch_append_pruners(int D, bool f64, const double *pruners, int M, const int32_t *entries /*k*M+j*/,
-                           uint32_t nps, uint32_t m, void *rows, uint64_t *sortkey, uint32_t *slot_src,
-                           uint32_t *flags, hipStream_t st);
+void launch_compact(int D, const CompactArgs &a, hipStream_t st);
+struct AppendArgs {
+    const double *pruners;        // [Kp][M][D]
+    const uint32_t *dup_cnt;      // [Kp*M]
+    int Kp, M;
+    const uint32_t *m_total;      // device: number of compacted candidates
+    uint32_t *nps_total;          // device out: number of pruner slots
+    int32_t *entries;             // [nps] -> k*M+j
+    int32_t *pruner_slot;         // [Kp*M] -> slot or -1
+    void *rows;
+    uint64_t *sortkey;
+    uint32_t *slot_src;
+    uint32_t *flags;
+    unsigned long long *orand;
+};
+void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st);
+void launch_fate_tables(uint32_t mt, const uint32_t *slot_rep, const uint8_t *alive_l, const uint8_t *alive_g, int KM,
+                        const int32_t *pruner_slot, uint8_t *slot_fate, uint8_t *pruner_fate, hipStream_t st);
 
 struct RepArgs {
     uint32_t mt;                  // sorted slots
@@ -96,8 +111,8 @@ void launch_gather_runs(int D, bool f64, const RepArgs &a, hipStream_t st);
 void launch_run_first(const RepArgs &a, hipStream_t st);
 void launch_rep_of(int D, bool f64, const RepArgs &a, hipStream_t st);
 void launch_build_reps(int D, bool f64, const RepArgs &a, hipStream_t st);
-void launch_seg_bounds(const uint64_t *rep_key, uint32_t mr, uint32_t *seg_begin, uint32_t *seg_end,
-                       hipStream_t st);
+void launch_seg_bounds(const uint64_t *rep_key, uint32_t mt, const uint32_t *d_mr, uint32_t *seg_begin,
+                       uint32_t *seg_end, hipStream_t st);
 void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src, const uint32_t *rep_of_sorted,
                      const int64_t *given_w, const uint32_t *dup_cnt, const int32_t *pr_entries,
                      unsigned long long *mult, hipStream_t st);
@@ -106,11 +121,9 @@ struct OutArgs {
     const uint16_t *status;
     uint32_t n;
     const uint32_t *blk_off;      // candidate slot base per tile
-    const uint32_t *slot_rep;     // [m + nps]
-    uint32_t m;
-    const int32_t *pruner_slot;   // [Kp*M] -> slot index (m + e) or -1
-    int M;
-    const uint8_t *alive_l, *alive_g;   // per rep
+    const uint8_t *slot_fate;     // [mt] inL | inG << 1
+    const uint8_t *pruner_fate;   // [Kp*M]
+    int M, KM;
     const int32_t *given_origin;  // per tuple origin (nullptr: partition key)
     const int64_t *given_w;       // per tuple weight (nullptr: 1)
     int K;                        // stats slots
@@ -148,7 +161,10 @@ void launch_iota(uint32_t *a, uint32_t n, hipStream_t st);
 void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
                          uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
-                        uint64_t *gkey, uint32_t *gval, hipStream_t st);
+                        uint64_t *gkey, uint32_t *gval, unsigned long long *orand, hipStream_t st);
+void launch_sfs_small(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+                      const SfsSeg *segs, const uint32_t *seg_list, uint32_t nwork, uint8_t *alive, void *conf,
+                      hipStream_t st);
 void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, uint32_t m, void *dst,
                         hipStream_t st);
 void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t mg, uint8_t *alive_g,
