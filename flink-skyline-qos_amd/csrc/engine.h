@@ -53,14 +53,14 @@ struct Pipe {
     // per tuple / per tile
     DevBuf status, blk_cnt, blk_off, out_cnt, out_off;
     // pruners
-    DevBuf skey, ssum, sidx, sorder, pruners, npr, dup_cnt, pr_entries, pruner_slot;
+    DevBuf skey, ssum, sidx, sorder, ssorted, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     // candidates (slot order) and sort
     DevBuf rows, sortkey, slot_src, perm, key_alt, val_alt, rows_sorted;
     DevBuf runflag, runscan, run_first, repof, repflag, repscan, rep_rows, rep_key, rep_of_sorted, slot_rep;
     DevBuf alive_l, alive_g, alive_u32, alive_scan, mult;
     // SFS
     DevBuf act, act2, keep, keep_scan, conf_rows, nconf, segs, seg_list, tiles, seg_begin, seg_end, segcnt;
-    DevBuf conf_small, seg_small, slot_fate, pruner_fate;
+    DevBuf conf_small, seg_small, slot_fate, pruner_fate, defer, tile_orand, xkeep;
     // global
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     DevBuf scratch, flags, totals, orand, lsz, surv;

@@ -152,8 +152,10 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
     SKY_TRY(p.act2.ensure((size_t)nrep * 4));
     SKY_TRY(p.keep.ensure((size_t)nrep * 4));
     SKY_TRY(p.keep_scan.ensure((size_t)nrep * 4));
-    SKY_TRY(p.conf_rows.ensure((size_t)nseg * B * rb));
-    SKY_TRY(p.nconf.ensure((size_t)nseg * 4));
+    // large partitions: rounds of BB candidates; X streamed through LDS in tiles of TB rows
+    const int TB = std::min(512, B);
+    const int BB = 4096;
+    SKY_TRY(p.xkeep.ensure((size_t)nseg * BB));
     SKY_TRY(p.segs.ensure((size_t)nseg * sizeof(SfsSeg)));
     SKY_TRY(p.seg_list.ensure((size_t)nseg * 4));
     SKY_TRY(p.segcnt.ensure((size_t)nseg * 4));
@@ -164,7 +166,7 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
     std::vector<SfsTile> tiles;
     // small partitions: the whole SFS in one workgroup each, one launch, no host sync
     {
-        constexpr uint32_t kSmallSeg = 16384;
+        constexpr uint32_t kSmallSeg = 2048;
         std::vector<uint32_t> small;
         for (uint32_t k = 0; k < nseg; k++) {
             hsegs[k] = SfsSeg{begin[k], cnt[k]};
@@ -198,14 +200,15 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         p.sfs_rounds++;
         SKY_TRY(p.upload(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), st));
         SKY_TRY(p.upload(p.seg_list.p, work.data(), work.size() * 4, st));
-        launch_block_sky(D, p.f64, full, p.ties, B, rows, key, p.act.as<uint32_t>(), p.segs.as<SfsSeg>(),
-                         p.seg_list.as<uint32_t>(), (uint32_t)work.size(), alive, p.conf_rows.p,
-                         p.nconf.as<uint32_t>(), st);
+        c.ktimer_begin("block_sky", st);
+        launch_block_sky(D, p.f64, full, p.ties, BB, TB, rows, key, p.act.as<uint32_t>(), p.segs.as<SfsSeg>(),
+                         p.seg_list.as<uint32_t>(), (uint32_t)work.size(), alive, p.xkeep.as<uint8_t>(), st);
+        c.ktimer_end("block_sky", st, 0);
         STAGE(st, "block_sky");
         tiles.clear();
         uint32_t out = 0;
         for (uint32_t k : work) {
-            const uint32_t xk = std::min<uint32_t>(B, cnt[k]);
+            const uint32_t xk = std::min<uint32_t>(BB, cnt[k]);
             const uint32_t rem = cnt[k] - xk;
             for (uint32_t off = 0; off < rem; off += kTileP) {
                 const uint32_t cn = std::min<uint32_t>(kTileP, rem - off);
@@ -218,8 +221,9 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         SKY_TRY(p.tiles.ensure(tiles.size() * sizeof(SfsTile)));
         SKY_TRY(p.upload(p.tiles.p, tiles.data(), tiles.size() * sizeof(SfsTile), st));
         c.ktimer_begin("sfs_filter", st);
-        launch_filter_rest(D, p.f64, full, B, rows, p.act.as<uint32_t>(), p.tiles.as<SfsTile>(),
-                           (uint32_t)tiles.size(), p.conf_rows.p, p.nconf.as<uint32_t>(), p.keep.as<uint32_t>(), st);
+        launch_filter_rest(D, p.f64, full, BB, TB, rows, p.act.as<uint32_t>(), p.tiles.as<SfsTile>(),
+                           (uint32_t)tiles.size(), p.segs.as<SfsSeg>(), p.xkeep.as<uint8_t>(), p.keep.as<uint32_t>(),
+                           st);
         c.ktimer_end("sfs_filter", st, out);
         STAGE(st, "sfs_filter");
         scan_excl_u32(p.keep.as<uint32_t>(), p.keep_scan.as<uint32_t>(), out, nullptr, p.scratch.as<uint32_t>(), st);
@@ -277,12 +281,13 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.h_lsz.assign(p.K, 0);
     p.h_surv.assign(p.K, 0);
     const uint32_t tiles = (n + kTile - 1) / kTile;
-    SKY_TRY(p.lsz.ensure((size_t)p.K * 8));
-    SKY_TRY(p.surv.ensure((size_t)p.K * 8));
+    const size_t stat_bytes = (size_t)kStatShards * p.K * 8;
+    SKY_TRY(p.lsz.ensure(stat_bytes));
+    SKY_TRY(p.surv.ensure(stat_bytes));
     SKY_TRY(p.totals.ensure(64));
     SKY_TRY(p.flags.ensure(64));
-    HIP_TRY(hipMemsetAsync(p.lsz.p, 0, (size_t)p.K * 8, st));
-    HIP_TRY(hipMemsetAsync(p.surv.p, 0, (size_t)p.K * 8, st));
+    HIP_TRY(hipMemsetAsync(p.lsz.p, 0, stat_bytes, st));
+    HIP_TRY(hipMemsetAsync(p.surv.p, 0, stat_bytes, st));
     if (n == 0) return SKY_OK;
     KeyParams kp = c.kp();
     kp.K = p.Kp;
@@ -293,14 +298,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.skey.ensure((size_t)S * 4));
     SKY_TRY(p.ssum.ensure((size_t)S * 8));
     SKY_TRY(p.sidx.ensure((size_t)S * D * 8));          // sample rows
-    SKY_TRY(p.sorder.ensure((size_t)S * 4 + ((size_t)p.Kp + 1) * 4));
+    SKY_TRY(p.sorder.ensure(((size_t)S + p.Kp + 1) * 4));
+    SKY_TRY(p.ssorted.ensure((size_t)S * 8 + (size_t)S * D * 8));
     SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
     launch_sample(D, in.vals, n, S, kp, in.keys, in.single, p.skey.as<int32_t>(), p.ssum.as<double>(),
                   p.sidx.as<double>(), st);
     launch_select_pruners(D, p.sidx.as<double>(), S, p.skey.as<int32_t>(), p.ssum.as<double>(),
-                          p.sorder.as<uint32_t>() + S, p.sorder.as<uint32_t>(), p.Kp, p.M, p.pruners.as<double>(),
-                          p.npr.as<int32_t>(), st);
+                          p.sorder.as<uint32_t>() + S, p.ssorted.as<double>(), p.sorder.as<uint32_t>(),
+                          p.ssorted.as<double>() + S, p.Kp, p.M, p.pruners.as<double>(), p.npr.as<int32_t>(), st);
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
@@ -326,9 +332,17 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.blk_cnt = p.blk_cnt.as<uint32_t>();
     fa.dup_cnt = p.dup_cnt.as<uint32_t>();
     fa.flags = p.flags.as<uint32_t>();
+    const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;
+    if (angle_keys) {
+        SKY_TRY(p.defer.ensure((size_t)n * 4));
+        fa.defer_list = p.defer.as<uint32_t>();
+        fa.defer_cnt = p.totals.as<uint32_t>() + 6;
+        HIP_TRY(hipMemsetAsync(fa.defer_cnt, 0, 4, st));
+    }
     c.ktimer_begin("filter", st);
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
+    if (angle_keys) launch_filter_deferred(D, fa, st);
     STAGE(st, "filter");
     scan_excl_u32(p.blk_cnt.as<uint32_t>(), p.blk_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>(),
                   p.scratch.as<uint32_t>(), st);
@@ -357,8 +371,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     ca.sortkey = p.sortkey.as<uint64_t>();
     ca.slot_src = p.slot_src.as<uint32_t>();
     ca.flags = p.flags.as<uint32_t>();
-    ca.orand = p.orand.as<unsigned long long>();
+    SKY_TRY(p.tile_orand.ensure((size_t)tiles * 16));
+    ca.tile_orand = p.tile_orand.as<unsigned long long>();
     launch_compact(D, ca, st);
+    launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
     AppendArgs aa{};
     aa.pruners = p.pruners.as<double>();
     aa.dup_cnt = p.dup_cnt.as<uint32_t>();
@@ -526,8 +542,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     c.ktimer_end("out", st, n);
     STAGE(st, "fate");
     uint32_t nout = 0;
-    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, (size_t)p.K * 8}, {p.surv.p, (size_t)p.K * 8}},
-                      {&nout, p.h_lsz.data(), p.h_surv.data()}));
+    std::vector<unsigned long long> sh_l((size_t)kStatShards * p.K), sh_s((size_t)kStatShards * p.K);
+    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, stat_bytes}, {p.surv.p, stat_bytes}},
+                      {&nout, sh_l.data(), sh_s.data()}));
+    for (int sh = 0; sh < kStatShards; sh++)
+        for (int k = 0; k < p.K; k++) {
+            p.h_lsz[k] += sh_l[(size_t)sh * p.K + k];
+            p.h_surv[k] += sh_s[(size_t)sh * p.K + k];
+        }
     p.nout = nout;
     if (tm) tm->mark(8, st);
     return SKY_OK;

@@ -143,16 +143,37 @@ __global__ __launch_bounds__(kThreads) void k_sample(const double *__restrict__ 
     ssum[s] = sum;
 }
 
-// one workgroup: counting sort of the sample ids by partition -> boff[Kp+1], order[S]
-__global__ __launch_bounds__(1024) void k_bucket_samples(const int32_t *__restrict__ skey, uint32_t S, int Kp,
-                                                         uint32_t *__restrict__ boff, uint32_t *__restrict__ order) {
+// lanes of this wave whose (active, 8-bit) key equals mine
+__device__ __forceinline__ uint64_t wave_peers_u8(bool active, uint32_t key) {
+    uint64_t peers = __ballot(active);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    return peers;
+}
+
+// one workgroup: counting sort of the sample by partition into contiguous copies
+// (score, sample id, row) so the pruner scan reads sequential memory
+template <int D>
+__global__ __launch_bounds__(1024) void k_bucket_samples(const int32_t *__restrict__ skey,
+                                                         const double *__restrict__ ssum,
+                                                         const double *__restrict__ srow, uint32_t S, int Kp,
+                                                         uint32_t *__restrict__ boff, double *__restrict__ osum,
+                                                         uint32_t *__restrict__ oid, double *__restrict__ orow) {
     __shared__ uint32_t s_cnt[kMaxK + 1];
     __shared__ uint32_t s_cur[kMaxK + 1];
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     for (int q = threadIdx.x; q <= Kp; q += 1024) s_cnt[q] = 0;
     __syncthreads();
-    for (uint32_t s = threadIdx.x; s < S; s += 1024) {
-        const int32_t k = skey[s];
-        if (k >= 0) atomicAdd(&s_cnt[k], 1u);
+    for (uint32_t s0 = 0; s0 < S; s0 += 1024) {
+        const uint32_t s = s0 + threadIdx.x;
+        const int32_t k = s < S ? skey[s] : -1;
+        const uint64_t peers = wave_peers_u8(k >= 0, (uint32_t)k);
+        if (k >= 0 && __popcll(peers & lt) == 0) atomicAdd(&s_cnt[k], (uint32_t)__popcll(peers));
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -161,24 +182,36 @@ __global__ __launch_bounds__(1024) void k_bucket_samples(const int32_t *__restri
         boff[Kp] = run;
     }
     __syncthreads();
-    for (uint32_t s = threadIdx.x; s < S; s += 1024) {
-        const int32_t k = skey[s];
-        if (k >= 0) order[atomicAdd(&s_cur[k], 1u)] = s;
+    for (uint32_t s0 = 0; s0 < S; s0 += 1024) {
+        const uint32_t s = s0 + threadIdx.x;
+        const int32_t k = s < S ? skey[s] : -1;
+        const uint64_t peers = wave_peers_u8(k >= 0, (uint32_t)k);
+        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)peers) - 1);
+        uint32_t base = 0;
+        if (k >= 0 && lane == (int)leader) base = atomicAdd(&s_cur[k], (uint32_t)__popcll(peers));
+        base = __shfl(base, (int)(k >= 0 ? leader : 0), 64);
+        if (k >= 0) {
+            const uint32_t pos = base + __popcll(peers & lt);
+            osum[pos] = ssum[s];
+            oid[pos] = s;
+#pragma unroll
+            for (int d = 0; d < D; d++) orow[(size_t)pos * D + d] = srow[(size_t)s * D + d];
+        }
     }
 }
 
 // one workgroup per partition: up to M mutually non-dominated, non-equal sample
 // tuples, smallest (score, sample id) first
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__restrict__ srow,
-                                                             const uint32_t *__restrict__ boff,
-                                                             const uint32_t *__restrict__ order,
-                                                             const double *__restrict__ ssum, int M,
-                                                             double *__restrict__ pruners,
-                                                             int32_t *__restrict__ npr) {
+__global__ __launch_bounds__(1024) void k_select_pruners(const double *__restrict__ orow,
+                                                         const uint32_t *__restrict__ boff,
+                                                         const uint32_t *__restrict__ oid,
+                                                         const double *__restrict__ osum, int M,
+                                                         double *__restrict__ pruners, int32_t *__restrict__ npr) {
+    constexpr int NW = 1024 / 64;
     __shared__ double s_pr[8][D];
-    __shared__ double s_bs[kThreads / 64];
-    __shared__ uint32_t s_bi[kThreads / 64];
+    __shared__ double s_bs[NW];
+    __shared__ uint32_t s_bi[NW], s_bq[NW];
     __shared__ uint32_t s_win;
     const int k = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -186,47 +219,49 @@ __global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__res
     int chosen = 0;
     for (int j = 0; j < M && j < 8; j++) {
         double best = __builtin_inf();
-        uint32_t bi = 0xffffffffu;
-        for (uint32_t q = b0 + threadIdx.x; q < b1; q += kThreads) {
-            const uint32_t s = order[q];
-            const double sc = ssum[s];
+        uint32_t bi = 0xffffffffu, bq = 0;
+        for (uint32_t q = b0 + threadIdx.x; q < b1; q += 1024) {
+            const double sc = osum[q];
+            const uint32_t s = oid[q];
             if (!(sc < best || (sc == best && s < bi))) continue;
-            double v[D];
-            load_row<D>(srow + (size_t)s * D, v);
             bool ok = true;
-            for (int c = 0; c < chosen && ok; c++) {
-                bool le = true, lt = false, eq = true;
+            if (chosen) {
+                double v[D];
+                load_row<D>(orow + (size_t)q * D, v);
+                for (int c = 0; c < chosen && ok; c++) {
+                    bool le = true, lt = false, eq = true;
 #pragma unroll
-                for (int d = 0; d < D; d++) {
-                    le &= s_pr[c][d] <= v[d];
-                    lt |= s_pr[c][d] < v[d];
-                    eq &= s_pr[c][d] == v[d];
+                    for (int d = 0; d < D; d++) {
+                        le &= s_pr[c][d] <= v[d];
+                        lt |= s_pr[c][d] < v[d];
+                        eq &= s_pr[c][d] == v[d];
+                    }
+                    ok = !(le && lt) && !eq;
                 }
-                ok = !(le && lt) && !eq;
             }
-            if (ok) { best = sc; bi = s; }
+            if (ok) { best = sc; bi = s; bq = q; }
         }
-        // block argmin over (best, bi)
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             const double ob = __shfl_xor(best, o, 64);
             const uint32_t oi = __shfl_xor(bi, o, 64);
-            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+            const uint32_t oq = __shfl_xor(bq, o, 64);
+            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; bq = oq; }
         }
-        if (lane == 0) { s_bs[w] = best; s_bi[w] = bi; }
+        if (lane == 0) { s_bs[w] = best; s_bi[w] = bi; s_bq[w] = bq; }
         __syncthreads();
         if (threadIdx.x == 0) {
             double b = s_bs[0];
-            uint32_t x = s_bi[0];
-            for (int q = 1; q < kThreads / 64; q++)
-                if (s_bs[q] < b || (s_bs[q] == b && s_bi[q] < x)) { b = s_bs[q]; x = s_bi[q]; }
-            s_win = x;
+            uint32_t x = s_bi[0], xq = s_bq[0];
+            for (int q = 1; q < NW; q++)
+                if (s_bs[q] < b || (s_bs[q] == b && s_bi[q] < x)) { b = s_bs[q]; x = s_bi[q]; xq = s_bq[q]; }
+            s_win = x == 0xffffffffu ? 0xffffffffu : xq;
         }
         __syncthreads();
         const uint32_t win = s_win;
         if (win == 0xffffffffu) break;
         if (threadIdx.x < D) {
-            const double x = srow[(size_t)win * D + threadIdx.x];
+            const double x = orow[(size_t)win * D + threadIdx.x];
             s_pr[chosen][threadIdx.x] = x;
             pruners[((size_t)k * M + chosen) * D + threadIdx.x] = x;
         }
@@ -236,59 +271,120 @@ __global__ __launch_bounds__(kThreads) void k_select_pruners(const double *__res
     if (threadIdx.x == 0) npr[k] = chosen;
 }
 
+// Classify one tuple of partition k: dropped (dominated by a pruner of k), exact
+// duplicate of pruner j (code 1+j), or candidate.  Pruners are tested in f64.
+template <int D>
+__device__ __forceinline__ uint16_t classify(const double (&v)[D], int32_t k, const double *s_pr, const int32_t *s_npr,
+                                             uint32_t *s_dup, int M, uint32_t &lflags) {
+    uint16_t code = kCodeCandidate;
+    const int np = s_npr[k];
+    const double *pr = s_pr + (size_t)k * M * D;
+    for (int j = 0; j < np; j++) {
+        bool le = true, lt = false, eq = true;
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const double p = pr[j * D + d];
+            le &= p <= v[d];
+            lt |= p < v[d];
+            eq &= p == v[d];
+        }
+        if (le && lt) { code = kCodeDropped; break; }
+        if (eq) { code = (uint16_t)(1 + j); atomicAdd(&s_dup[k * M + j], 1u); break; }
+    }
+    if (code == kCodeCandidate) {
+#pragma unroll
+        for (int d = 0; d < D; d++)
+            if ((double)(float)v[d] != v[d]) lflags |= kFlagNotF32;
+    }
+    return code;
+}
+
+template <int D>
+__device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_pr, int32_t *s_npr, uint32_t *s_dup) {
+    const int nprw = a.Kp * a.M;
+    for (int q = threadIdx.x; q < nprw * D; q += kThreads) s_pr[q] = a.pruners[q];
+    for (int q = threadIdx.x; q < a.Kp; q += kThreads) s_npr[q] = a.npr[q];
+    for (int q = threadIdx.x; q < nprw; q += kThreads) s_dup[q] = 0;
+    __syncthreads();
+}
+
+// The HBM stream.  MR-Angle keys the fast path cannot certify are appended to a
+// deferred list (wave-aggregated atomics) and finished by k_filter_deferred, so
+// this kernel carries no exact-fdlibm code (no call, no scratch, fewer VGPRs).
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
     extern __shared__ __attribute__((aligned(16))) double s_pr[];   // [Kp*M*D]
     __shared__ int32_t s_npr[kMaxK];
     __shared__ uint32_t s_dup[2048];
     __shared__ uint32_t s_w[kThreads / 64];
-    const int nprw = a.Kp * a.M;
-    for (int q = threadIdx.x; q < nprw * D; q += kThreads) s_pr[q] = a.pruners[q];
-    for (int q = threadIdx.x; q < a.Kp; q += kThreads) s_npr[q] = a.npr[q];
-    for (int q = threadIdx.x; q < nprw; q += kThreads) s_dup[q] = 0;
-    __syncthreads();
+    load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
     uint32_t lflags = 0, mycnt = 0;
     const uint32_t base = blockIdx.x * kTile;
+    const int lane = threadIdx.x & 63;
 #pragma unroll 1
     for (int r = 0; r < kItems; r++) {
         const uint32_t i = base + r * kThreads + threadIdx.x;
-        if (i >= a.n) break;
+        if (base + r * kThreads >= a.n) break;                       // block-uniform
+        const bool valid = i < a.n;
         double v[D];
-        load_row<D>(a.vals + (size_t)i * D, v);
+        if (valid) load_row<D>(a.vals + (size_t)i * D, v);
+        else {
+#pragma unroll
+            for (int d = 0; d < D; d++) v[d] = 0.0;
+        }
         bool nan = false;
 #pragma unroll
         for (int d = 0; d < D; d++) nan |= v[d] != v[d];
-        int32_t k = a.single ? 0 : a.given_keys ? a.given_keys[i] : partition_key<D>(v, a.kp);
+        int32_t k = a.single ? 0 : a.given_keys ? (valid ? a.given_keys[i] : 0) : partition_key_fast<D>(v, a.kp);
+        const bool defer = valid && !nan && !a.single && !a.given_keys && k == kAngleUndecided;
+        const uint64_t dm = __ballot(defer);
+        if (dm) {
+            uint32_t wbase = 0;
+            if (lane == __ffsll((unsigned long long)dm) - 1) wbase = atomicAdd(a.defer_cnt, (uint32_t)__popcll(dm));
+            wbase = __shfl(wbase, __ffsll((unsigned long long)dm) - 1, 64);
+            if (defer) {
+                const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+                a.defer_list[wbase + __popcll(dm & lt)] = i;
+            }
+        }
+        if (!valid || defer) continue;
         uint16_t code = kCodeCandidate;
         if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
         else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-        else {
-            const int np = s_npr[k];
-            const double *pr = s_pr + (size_t)k * a.M * D;
-            for (int j = 0; j < np; j++) {
-                bool le = true, lt = false, eq = true;
-#pragma unroll
-                for (int d = 0; d < D; d++) {
-                    const double p = pr[j * D + d];
-                    le &= p <= v[d];
-                    lt |= p < v[d];
-                    eq &= p == v[d];
-                }
-                if (le && lt) { code = kCodeDropped; break; }
-                if (eq) { code = (uint16_t)(1 + j); atomicAdd(&s_dup[k * a.M + j], 1u); break; }
-            }
-            if (code == kCodeCandidate) {
-                mycnt++;
-#pragma unroll
-                for (int d = 0; d < D; d++)
-                    if ((double)(float)v[d] != v[d]) lflags |= kFlagNotF32;
-            }
-        }
+        else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+        mycnt += code == kCodeCandidate;
         a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
     }
     const uint32_t tot = block_sum(mycnt, s_w);
     if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = tot;
-    for (int q = threadIdx.x; q < nprw; q += kThreads)
+    for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads)
+        if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
+    if (lflags) atomicOr(a.flags, lflags);
+}
+
+// The deferred MR-Angle tuples: exact fdlibm key, then the same classification;
+// per-tile candidate counts are added atomically (before the scan).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double s_pr[];
+    __shared__ int32_t s_npr[kMaxK];
+    __shared__ uint32_t s_dup[2048];
+    load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
+    const uint32_t cnt = *a.defer_cnt;
+    uint32_t lflags = 0;
+    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < cnt; q += gridDim.x * kThreads) {
+        const uint32_t i = a.defer_list[q];
+        double v[D];
+        load_row<D>(a.vals + (size_t)i * D, v);
+        int32_t k = angle_key_exact<D>(v, a.kp.P);
+        uint16_t code;
+        if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
+        else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+        if (code == kCodeCandidate) atomicAdd(&a.blk_cnt[i / kTile], 1u);
+        a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads)
         if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
     if (lflags) atomicOr(a.flags, lflags);
 }
@@ -410,17 +506,52 @@ __global__ __launch_bounds__(kThreads) void k_compact(CompactArgs a) {
         an &= key;
         slot++;
     }
-    // OR / AND of the sort keys (which key bytes vary -> radix passes), wave-reduced
+    // OR / AND of the sort keys (which key bytes vary -> radix passes): one partial
+    // per tile (plain stores; one global address hit by every tile would serialise)
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) {
         o |= __shfl_xor(o, s, 64);
         an &= __shfl_xor(an, s, 64);
     }
-    if ((threadIdx.x & 63) == 0 && tot) {
-        atomicOr(&a.orand[0], (unsigned long long)o);
-        atomicAnd(&a.orand[1], (unsigned long long)an);
+    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bo = 0, ba = ~0ull;
+        for (int q = 0; q < kThreads / 64; q++) { bo |= s_o[q]; ba &= s_a[q]; }
+        a.tile_orand[2 * blockIdx.x] = bo;
+        a.tile_orand[2 * blockIdx.x + 1] = ba;
     }
     if (lflags) atomicOr(a.flags, lflags);
+}
+
+__global__ __launch_bounds__(kThreads) void k_orand_reduce(const unsigned long long *__restrict__ part, uint32_t np,
+                                                           unsigned long long *__restrict__ orand) {
+    unsigned long long o = 0, an = ~0ull;
+    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < np; q += gridDim.x * kThreads) {
+        o |= part[2 * q];
+        an &= part[2 * q + 1];
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+        o |= __shfl_xor(o, s, 64);
+        an &= __shfl_xor(an, s, 64);
+    }
+    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < kThreads / 64; q++) { s_o[0] |= s_o[q]; s_a[0] &= s_a[q]; }
+        atomicOr(&orand[0], s_o[0]);
+        atomicAnd(&orand[1], s_a[0]);
+    }
+}
+
+void launch_orand_reduce(const unsigned long long *part, uint32_t np, unsigned long long *orand, hipStream_t st) {
+    if (!np) return;
+    unsigned g = (np + kThreads - 1) / kThreads;
+    if (g > 128) g = 128;
+    k_orand_reduce<<<g, kThreads, 0, st>>>(part, np, orand);
 }
 
 // One workgroup: every pruner that some tuple duplicates becomes one more candidate
@@ -671,22 +802,49 @@ __global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
                 }
             }
             __syncthreads();
+            // sharded accumulators: one global address per (shard, origin), summed by the host
+            const size_t sh = (size_t)(blockIdx.x % kStatShards) * a.K;
             for (int q = threadIdx.x; q < a.K; q += kThreads) {
-                if (s_lsz[q]) atomicAdd(&a.lsz[q], s_lsz[q]);
-                if (s_surv[q]) atomicAdd(&a.surv[q], s_surv[q]);
+                if (s_lsz[q]) atomicAdd(&a.lsz[sh + q], s_lsz[q]);
+                if (s_surv[q]) atomicAdd(&a.surv[sh + q], s_surv[q]);
             }
         }
     } else {
+        // the tile's selected ids / origins are staged in LDS in stream order, then
+        // written out as one contiguous, coalesced run per tile
+        __shared__ int64_t s_oid[kTile];
+        __shared__ int32_t s_oorg[kTile];
         uint32_t bt;
-        uint32_t pos = a.out_off[blockIdx.x] + block_scan_excl(nsel, s_w, bt);
+        uint32_t pl = block_scan_excl(nsel, s_w, bt);
+        const uint32_t base = a.out_off[blockIdx.x];
+        int64_t idv[kItems];
+        if (nsel && a.ids && i0 + kItems <= a.n) {
+            const longlong2 *q = reinterpret_cast<const longlong2 *>(a.ids + i0);
+#pragma unroll
+            for (int k = 0; k < kItems / 2; k++) {
+                const longlong2 x = q[k];
+                idv[2 * k] = x.x;
+                idv[2 * k + 1] = x.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kItems; k++)
+                idv[k] = (nsel && i0 + k < a.n) ? (a.ids ? a.ids[i0 + k] : (int64_t)(i0 + k)) : 0;
+        }
+#pragma unroll
         for (int k = 0; k < kItems; k++) {
             if (!((fate[k] >> shift) & 1)) continue;
             const uint32_t i = i0 + k;
-            if (a.ids_out) a.ids_out[pos] = a.ids ? a.ids[i] : (int64_t)i;
-            if (a.origin_out) a.origin_out[pos] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
+            s_oid[pl] = idv[k];
+            s_oorg[pl] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
             if (a.rows_out)
-                for (int d = 0; d < a.D; d++) a.rows_out[(size_t)pos * a.D + d] = a.vals[(size_t)i * a.D + d];
-            pos++;
+                for (int d = 0; d < a.D; d++) a.rows_out[(size_t)(base + pl) * a.D + d] = a.vals[(size_t)i * a.D + d];
+            pl++;
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
+            if (a.ids_out) a.ids_out[base + q] = s_oid[q];
+            if (a.origin_out) a.origin_out[base + q] = s_oorg[q];
         }
     }
 }
@@ -731,15 +889,20 @@ void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyP
 }
 
 void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
-                           uint32_t *boff, uint32_t *order, int Kp, int M, double *pruners, int32_t *npr,
-                           hipStream_t st) {
-    k_bucket_samples<<<1, 1024, 0, st>>>(skey, S, Kp, boff, order);
-    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, kThreads, 0, st>>>(srow, boff, order, ssum, M, pruners, npr)));
+                           uint32_t *boff, double *osum, uint32_t *oid, double *orow, int Kp, int M, double *pruners,
+                           int32_t *npr, hipStream_t st) {
+    SKY_DISPATCH_D(D, (k_bucket_samples<DD><<<1, 1024, 0, st>>>(skey, ssum, srow, S, Kp, boff, osum, oid, orow)));
+    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, 1024, 0, st>>>(orow, boff, oid, osum, M, pruners, npr)));
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double);
     SKY_DISPATCH_D(D, (k_filter<DD><<<nblk(a.n, kTile), kThreads, lds, st>>>(a)));
+}
+
+void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
+    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double);
+    SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<256, kThreads, lds, st>>>(a)));
 }
 
 void launch_compact(int D, const CompactArgs &a, hipStream_t st) {

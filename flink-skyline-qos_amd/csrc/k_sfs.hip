@@ -31,97 +31,68 @@ __device__ __forceinline__ void lds_row(const T *s, T (&v)[D]) {
     for (int d = 0; d < D; d++) v[d] = s[d];
 }
 
+// Round step 1, in parallel over (partition, slice of 256 candidates): the next
+// B candidates X of each large partition are tested against their predecessors in
+// X, streamed through LDS in tiles of TB rows; survivors are confirmed skyline
+// members (alive) and flagged in xkeep for the filter step.
 template <typename T, int D, bool FULL, bool TIES>
 __global__ __launch_bounds__(kThreads) void k_block_sky(const T *__restrict__ rows, const uint64_t *__restrict__ key,
                                                         const uint32_t *__restrict__ act,
                                                         const SfsSeg *__restrict__ segs,
-                                                        const uint32_t *__restrict__ seg_list, int B,
-                                                        uint8_t *__restrict__ alive, T *__restrict__ conf_rows,
-                                                        uint32_t *__restrict__ nconf) {
+                                                        const uint32_t *__restrict__ seg_list, int B, int TB,
+                                                        uint8_t *__restrict__ alive, uint8_t *__restrict__ xkeep) {
     constexpr int DP = padded_dims<T>(D);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    T *s_x = reinterpret_cast<T *>(smem);                               // [B][DP]
-    uint32_t *s_sc = reinterpret_cast<uint32_t *>(s_x + (size_t)B * DP);  // [B]
-    uint32_t *s_keep = s_sc + B;                                         // [B]
-    __shared__ uint32_t s_w[kThreads / 64];
+    T *s_x = reinterpret_cast<T *>(smem);                               // [TB][DP]
     const uint32_t k = seg_list[blockIdx.x];
     const SfsSeg sg = segs[k];
     const uint32_t xk = sg.count < (uint32_t)B ? sg.count : (uint32_t)B;
-    for (uint32_t q = threadIdx.x; q < xk; q += kThreads) {
-        const uint32_t r = act[sg.begin + q];
-        const T *src = rows + (size_t)r * DP;
+    const uint32_t jlo = blockIdx.y * kThreads;
+    if (jlo >= xk) return;                                               // block-uniform
+    const uint32_t jhi = xk - jlo < (uint32_t)kThreads ? xk : jlo + kThreads;
+    const uint32_t j = jlo + threadIdx.x;
+    const bool valid = j < jhi;
+    T y[D];
+    const uint32_t rj = valid ? act[sg.begin + j] : 0u;
 #pragma unroll
-        for (int d = 0; d < DP; d++) s_x[(size_t)q * DP + d] = src[d];
-        s_sc[q] = key_score<T>(key[r]);
-    }
-    __syncthreads();
-    const bool has_rest = sg.count > xk;
-    const uint32_t rest_score = (TIES && has_rest) ? key_score<T>(key[act[sg.begin + xk]]) : 0u;
-    for (uint32_t j0 = 0; j0 < xk; j0 += kThreads) {
-        const uint32_t j = j0 + threadIdx.x;
-        const bool valid = j < xk;
-        T y[D];
-        if (valid) lds_row<T, D>(s_x + (size_t)j * DP, y);
-        else {
-#pragma unroll
-            for (int d = 0; d < D; d++) y[d] = T(0);
+    for (int d = 0; d < D; d++) y[d] = valid ? rows[(size_t)rj * DP + d] : T(0);
+    bool dom = false;
+    const uint32_t wlast = jlo + (threadIdx.x | 63u);                  // largest j of this wave
+    for (uint32_t c0 = 0; c0 < jhi; c0 += TB) {
+        const uint32_t cn = jhi - c0 < (uint32_t)TB ? jhi - c0 : (uint32_t)TB;
+        for (uint32_t q = threadIdx.x; q < cn * DP; q += kThreads) {
+            const uint32_t row = q / DP, d = q - row * DP;
+            s_x[q] = rows[(size_t)act[sg.begin + c0 + row] * DP + d];
         }
-        bool dom = false;
-        // wave-uniform bound: the largest j of this wave
-        const uint32_t wlast = j0 + (threadIdx.x | 63u);
-        const uint32_t iend = wlast < xk ? wlast : xk - 1;
+        __syncthreads();
+        const uint32_t iend = wlast < c0 + cn ? (wlast > c0 ? wlast - c0 : 0u) : cn;
         for (uint32_t i = 0; i < iend; i++) {
+            if ((i & 15u) == 0u && __ballot(valid && !dom) == 0ull) break;
             T x[D];
             lds_row<T, D>(s_x + (size_t)i * DP, x);
-            dom |= (i < j) && dom_test<T, D, FULL>(x, y);
-            if ((i & 15u) == 15u && __ballot(valid && !dom) == 0ull) break;
+            dom |= (c0 + i < j) && dom_test<T, D, FULL>(x, y);
         }
-        if constexpr (TIES) {
-            if (valid && !dom) {
-                const uint32_t sj = s_sc[j];
-                for (uint32_t i = j + 1; i < xk && s_sc[i] == sj && !dom; i++) {
-                    T x[D];
-                    lds_row<T, D>(s_x + (size_t)i * DP, x);
-                    dom = dom_test<T, D, true>(x, y);
-                }
-                if (has_rest && sj == rest_score) {
-                    for (uint32_t q = xk; q < sg.count && !dom; q++) {
-                        const uint32_t r = act[sg.begin + q];
-                        if (key_score<T>(key[r]) != sj) break;
-                        T x[D];
+        if (!__syncthreads_or(valid && !dom)) break;
+    }
+    if constexpr (TIES) {
+        // equal scores can dominate either way: also test later members of X with the
+        // same score and, at the chunk's end, the head of the remaining candidates
+        if (valid && !dom) {
+            const uint32_t sj = key_score<T>(key[rj]);
+            for (uint32_t q = j + 1; q < sg.count && !dom; q++) {
+                const uint32_t r = act[sg.begin + q];
+                if (key_score<T>(key[r]) != sj) break;
+                T x[D];
 #pragma unroll
-                        for (int d = 0; d < D; d++) x[d] = rows[(size_t)r * DP + d];
-                        dom = dom_test<T, D, true>(x, y);
-                    }
-                }
+                for (int d = 0; d < D; d++) x[d] = rows[(size_t)r * DP + d];
+                dom = dom_test<T, D, true>(x, y);
             }
         }
-        if (valid) s_keep[j] = dom ? 0u : 1u;
     }
-    __syncthreads();
-    // order-preserving compaction of X' into conf_rows[k]
-    uint32_t run = 0;
-    T *conf = conf_rows + (size_t)k * B * DP;
-    for (uint32_t j0 = 0; j0 < xk; j0 += kThreads) {
-        const uint32_t j = j0 + threadIdx.x;
-        const bool keep = j < xk && s_keep[j];
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        const uint64_t b = __ballot(keep);
-        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-        if (lane == 0) s_w[w] = __popcll(b);
-        __syncthreads();
-        uint32_t wb = 0, tot = 0;
-        for (int q = 0; q < kThreads / 64; q++) { wb += q < w ? s_w[q] : 0u; tot += s_w[q]; }
-        __syncthreads();
-        if (keep) {
-            const uint32_t pos = run + wb + __popcll(b & lt);
-#pragma unroll
-            for (int d = 0; d < DP; d++) conf[(size_t)pos * DP + d] = s_x[(size_t)j * DP + d];
-            alive[act[sg.begin + j]] = 1;
-        }
-        run += tot;
+    if (valid) {
+        xkeep[(size_t)k * B + j] = dom ? 0 : 1;
+        if (!dom) alive[rj] = 1;
     }
-    if (threadIdx.x == 0) nconf[k] = run;
 }
 
 // Whole SFS of one small partition in ONE workgroup, no host round trips: the
@@ -243,19 +214,22 @@ __global__ __launch_bounds__(kThreads) void k_sfs_small(const T *__restrict__ ro
     }
 }
 
+// Round step 2: every remaining candidate of a large partition is tested against
+// the confirmed X' of its partition (kept rows of X packed into LDS tile by tile).
 template <typename T, int D, bool FULL, int PPT>
 __global__ __launch_bounds__(kThreads) void k_filter_rest(const T *__restrict__ rows, const uint32_t *__restrict__ act,
                                                           const SfsTile *__restrict__ tiles,
-                                                          const T *__restrict__ conf_rows,
-                                                          const uint32_t *__restrict__ nconf, int B,
+                                                          const SfsSeg *__restrict__ segs, int B, int TB,
+                                                          const uint8_t *__restrict__ xkeep,
                                                           uint32_t *__restrict__ keep) {
     constexpr int DP = padded_dims<T>(D);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T *s_c = reinterpret_cast<T *>(smem);
+    __shared__ uint32_t s_n;
     const SfsTile tl = tiles[blockIdx.x];
-    const uint32_t nc = nconf[tl.seg];
-    const T *conf = conf_rows + (size_t)tl.seg * B * DP;
-    for (uint32_t q = threadIdx.x; q < nc * DP; q += kThreads) s_c[q] = conf[q];
+    const SfsSeg sg = segs[tl.seg];
+    const uint32_t xk = sg.count < (uint32_t)B ? sg.count : (uint32_t)B;
+    const uint8_t *xk_flags = xkeep + (size_t)tl.seg * B;
     T y[PPT][D];
     bool valid[PPT], dom[PPT];
 #pragma unroll
@@ -263,27 +237,39 @@ __global__ __launch_bounds__(kThreads) void k_filter_rest(const T *__restrict__ 
         const uint32_t e = threadIdx.x + p * kThreads;
         valid[p] = e < tl.count;
         dom[p] = false;
-        if (valid[p]) {
-            const T *src = rows + (size_t)act[tl.start + e] * DP;
+        const uint32_t r = valid[p] ? act[tl.start + e] : 0u;
 #pragma unroll
-            for (int d = 0; d < D; d++) y[p][d] = src[d];
-        } else {
-#pragma unroll
-            for (int d = 0; d < D; d++) y[p][d] = T(0);
-        }
+        for (int d = 0; d < D; d++) y[p][d] = valid[p] ? rows[(size_t)r * DP + d] : T(0);
     }
-    __syncthreads();
-    for (uint32_t i = 0; i < nc; i++) {
-        T x[D];
-        lds_row<T, D>(s_c + (size_t)i * DP, x);
+    for (uint32_t c0 = 0; c0 < xk; c0 += TB) {
+        const uint32_t cn = xk - c0 < (uint32_t)TB ? xk - c0 : (uint32_t)TB;
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < cn; q += kThreads) {
+            if (!xk_flags[c0 + q]) continue;
+            const uint32_t pos = atomicAdd(&s_n, 1u);          // order inside X' is irrelevant
+            const T *src = rows + (size_t)act[sg.begin + c0 + q] * DP;
 #pragma unroll
-        for (int p = 0; p < PPT; p++) dom[p] |= dom_test<T, D, FULL>(x, y[p]);
-        if ((i & 7u) == 7u) {
-            bool live = false;
-#pragma unroll
-            for (int p = 0; p < PPT; p++) live |= valid[p] && !dom[p];
-            if (__ballot(live) == 0ull) break;
+            for (int d = 0; d < DP; d++) s_c[(size_t)pos * DP + d] = src[d];
         }
+        __syncthreads();
+        const uint32_t nc = s_n;
+        for (uint32_t i = 0; i < nc; i++) {
+            T x[D];
+            lds_row<T, D>(s_c + (size_t)i * DP, x);
+#pragma unroll
+            for (int p = 0; p < PPT; p++) dom[p] |= dom_test<T, D, FULL>(x, y[p]);
+            if ((i & 7u) == 7u) {
+                bool live = false;
+#pragma unroll
+                for (int p = 0; p < PPT; p++) live |= valid[p] && !dom[p];
+                if (__ballot(live) == 0ull) break;
+            }
+        }
+        bool live = false;
+#pragma unroll
+        for (int p = 0; p < PPT; p++) live |= valid[p] && !dom[p];
+        if (!__syncthreads_or(live)) break;
     }
 #pragma unroll
     for (int p = 0; p < PPT; p++) {
@@ -391,28 +377,28 @@ __global__ __launch_bounds__(kThreads) void k_u8_to_u32(const uint8_t *__restric
 static inline unsigned nb(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
 template <typename T, int D>
-static void block_sky_t(bool full, bool ties, int B, const void *rows, const uint64_t *key, const uint32_t *act,
+static void block_sky_t(bool full, bool ties, int B, int TB, const void *rows, const uint64_t *key, const uint32_t *act,
                         const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work, uint8_t *alive,
-                        void *conf_rows, uint32_t *nconf, hipStream_t st) {
+                        uint8_t *xkeep, hipStream_t st) {
     constexpr int DP = padded_dims<T>(D);
-    const size_t lds = (size_t)B * DP * sizeof(T) + 2 * (size_t)B * sizeof(uint32_t);
+    const size_t lds = (size_t)TB * DP * sizeof(T);
+    const dim3 grid(nseg_work, (B + kThreads - 1) / kThreads);
     const T *r = (const T *)rows;
-    T *c = (T *)conf_rows;
     if (full) {
-        if (ties) k_block_sky<T, D, true, true><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
-        else k_block_sky<T, D, true, false><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+        if (ties) k_block_sky<T, D, true, true><<<grid, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, TB, alive, xkeep);
+        else k_block_sky<T, D, true, false><<<grid, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, TB, alive, xkeep);
     } else {
-        if (ties) k_block_sky<T, D, false, true><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
-        else k_block_sky<T, D, false, false><<<nseg_work, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, alive, c, nconf);
+        if (ties) k_block_sky<T, D, false, true><<<grid, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, TB, alive, xkeep);
+        else k_block_sky<T, D, false, false><<<grid, kThreads, lds, st>>>(r, key, act, segs, seg_list, B, TB, alive, xkeep);
     }
 }
 
-void launch_block_sky(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+void launch_block_sky(int D, bool f64, bool full, bool ties, int B, int TB, const void *rows, const uint64_t *key,
                       const uint32_t *act, const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work,
-                      uint8_t *alive, void *conf_rows, uint32_t *nconf, hipStream_t st) {
+                      uint8_t *alive, uint8_t *xkeep, hipStream_t st) {
     if (!nseg_work) return;
-    if (f64) { SKY_DISPATCH_D(D, (block_sky_t<double, DD>(full, ties, B, rows, key, act, segs, seg_list, nseg_work, alive, conf_rows, nconf, st))); }
-    else { SKY_DISPATCH_D(D, (block_sky_t<float, DD>(full, ties, B, rows, key, act, segs, seg_list, nseg_work, alive, conf_rows, nconf, st))); }
+    if (f64) { SKY_DISPATCH_D(D, (block_sky_t<double, DD>(full, ties, B, TB, rows, key, act, segs, seg_list, nseg_work, alive, xkeep, st))); }
+    else { SKY_DISPATCH_D(D, (block_sky_t<float, DD>(full, ties, B, TB, rows, key, act, segs, seg_list, nseg_work, alive, xkeep, st))); }
 }
 
 template <typename T, int D>
@@ -442,23 +428,22 @@ void launch_sfs_small(int D, bool f64, bool full, bool ties, int B, const void *
 constexpr int kPPT = 4;
 
 template <typename T, int D>
-static void filter_rest_t(bool full, int B, const void *rows, const uint32_t *act, const SfsTile *tiles,
-                          uint32_t ntiles, const void *conf_rows, const uint32_t *nconf, uint32_t *keep,
-                          hipStream_t st) {
+static void filter_rest_t(bool full, int B, int TB, const void *rows, const uint32_t *act, const SfsTile *tiles,
+                          uint32_t ntiles, const SfsSeg *segs, const uint8_t *xkeep, uint32_t *keep, hipStream_t st) {
     constexpr int DP = padded_dims<T>(D);
-    const size_t lds = (size_t)B * DP * sizeof(T);
+    const size_t lds = (size_t)TB * DP * sizeof(T);
     if (full)
-        k_filter_rest<T, D, true, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, (const T *)conf_rows, nconf, B, keep);
+        k_filter_rest<T, D, true, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, segs, B, TB, xkeep, keep);
     else
-        k_filter_rest<T, D, false, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, (const T *)conf_rows, nconf, B, keep);
+        k_filter_rest<T, D, false, kPPT><<<ntiles, kThreads, lds, st>>>((const T *)rows, act, tiles, segs, B, TB, xkeep, keep);
 }
 
-void launch_filter_rest(int D, bool f64, bool full, int B, const void *rows, const uint32_t *act,
-                        const SfsTile *tiles, uint32_t ntiles, const void *conf_rows, const uint32_t *nconf,
+void launch_filter_rest(int D, bool f64, bool full, int B, int TB, const void *rows, const uint32_t *act,
+                        const SfsTile *tiles, uint32_t ntiles, const SfsSeg *segs, const uint8_t *xkeep,
                         uint32_t *keep, hipStream_t st) {
     if (!ntiles) return;
-    if (f64) { SKY_DISPATCH_D(D, (filter_rest_t<double, DD>(full, B, rows, act, tiles, ntiles, conf_rows, nconf, keep, st))); }
-    else { SKY_DISPATCH_D(D, (filter_rest_t<float, DD>(full, B, rows, act, tiles, ntiles, conf_rows, nconf, keep, st))); }
+    if (f64) { SKY_DISPATCH_D(D, (filter_rest_t<double, DD>(full, B, TB, rows, act, tiles, ntiles, segs, xkeep, keep, st))); }
+    else { SKY_DISPATCH_D(D, (filter_rest_t<float, DD>(full, B, TB, rows, act, tiles, ntiles, segs, xkeep, keep, st))); }
 }
 
 void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uint32_t *keep_scan,

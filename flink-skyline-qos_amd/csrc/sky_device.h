@@ -122,10 +122,12 @@ struct KeyParams {
 };
 
 // Error budget of the f32 estimate in t = avg*P (inputs with nonzero magnitudes in
-// [1e-15, 1e15]): per angle, input rounding (<= 2^-24 relative each for x and
-// hyp, plus sqrtf's 1 ulp) moves the angle by < 2e-7 rad and atan2f itself errs by
-// <= 6 ulp (OpenCL bound) < 1.5e-6 rad; normalised by pi/2 that is < 1.1e-6 per
-// angle, so |t_est - t| < 1.1e-6 * P.  The margin keeps a 3.5x safety factor.
+// [1e-15, 1e15]): per angle, the f32 inputs and the f32 sum of <= 15 squares are
+// within 16*2^-24 relative, sqrtf within 1 ulp, so the angle moves by < 6e-7 rad;
+// atan2f errs by <= 6 ulp (OpenCL bound) < 1.5e-6 rad; the angles are summed in
+// f64.  Per angle < 2.1e-6 rad, normalised by pi/2 and averaged over the angles:
+// |t_est - t| < 1.4e-6 * P.  The margin 1e-5 + 4e-6*P keeps a ~3x safety factor
+// (the exact fallback runs whenever t_est is closer than that to an integer).
 inline double angle_margin(int P) { return 1e-5 + 4e-6 * (double)P; }
 
 __device__ __forceinline__ int32_t clamp_key(int32_t p, int P) {
@@ -135,7 +137,7 @@ __device__ __forceinline__ int32_t clamp_key(int32_t p, int P) {
 
 // The reference's AnglePartitioner.getKey, operation for operation in f64.
 template <int D>
-__device__ __noinline__ int32_t angle_key_exact(const double *v, int P) {
+__device__ __forceinline__ int32_t angle_key_exact(const double (&v)[D], int P) {
     constexpr double max_angle = 3.141592653589793 / 2.0;
     double normalized = 0.0;
     for (int i = 0; i < D - 1; i++) {
@@ -156,49 +158,71 @@ __device__ __noinline__ int32_t angle_key_exact(const double *v, int P) {
 //     (angle_margin) from an integer, floor(t) IS the exact key;
 //  3. otherwise the exact fdlibm path (~1e-4 of the reference-formula tuples).
 
+// kAngleUndecided: the fast path could not certify the key (non-ranged input or
+// t within `margin` of an integer); the caller runs angle_key_exact.
+constexpr int32_t kAngleUndecided = -1;
+
 template <int D>
-__device__ __forceinline__ int32_t angle_key(const double (&v)[D], int P, double margin) {
+__device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, double margin) {
     if (D < 2) return 0;
-    double s[D > 1 ? D - 1 : 1];
-    bool special = true, ranged = true;
-#pragma unroll
-    for (int i = 0; i < D; i++) special &= v[i] == v[i];    // NaN -> exact path
-#pragma unroll
-    for (int i = 0; i < D - 1; i++) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = i + 1; j < D; j++) acc = acc + v[j] * v[j];
-        s[i] = acc;
-        special &= (acc == 0.0) | (v[i] == 0.0);
-    }
+    // every value 0 or of magnitude in [1e-15, 1e15] (NaN and inf fail): then no
+    // square underflows, so the reference's f64 s_i is 0 exactly when v_j == 0 for
+    // every j > i, and f32 holds every s_i without overflow
+    bool ranged = true;
 #pragma unroll
     for (int i = 0; i < D; i++) {
         const double a = fabs(v[i]);
         ranged &= (a == 0.0) | ((a >= 1e-15) & (a <= 1e15));
     }
-    if (special) {
-        double normalized = 0.0;
-#pragma unroll
-        for (int i = 0; i < D - 1; i++) {
-            const double nrm = s[i] == 0.0 ? (signbit(v[i]) ? 2.0 : 0.0) : 1.0;
-            normalized = normalized + nrm;
-        }
-        const double avg = normalized / (double)(D - 1);
-        return clamp_key(java_d2i(avg * (double)P), P);
-    }
     if (ranged) {
+        bool zero_after[D > 1 ? D - 1 : 1];
+        bool z = true, special = true;
+#pragma unroll
+        for (int i = D - 2; i >= 0; i--) {
+            z &= v[i + 1] == 0.0;
+            zero_after[i] = z;
+            special &= z | (v[i] == 0.0);
+        }
+        if (special) {
+            double normalized = 0.0;
+#pragma unroll
+            for (int i = 0; i < D - 1; i++) {
+                const double nrm = zero_after[i] ? (signbit(v[i]) ? 2.0 : 0.0) : 1.0;
+                normalized = normalized + nrm;
+            }
+            const double avg = normalized / (double)(D - 1);
+            return clamp_key(java_d2i(avg * (double)P), P);
+        }
+        float f[D];
+#pragma unroll
+        for (int i = 0; i < D; i++) f[i] = (float)v[i];
+        float s = 0.0f;
         double est = 0.0;
 #pragma unroll
-        for (int i = 0; i < D - 1; i++) {
-            const float h = sqrtf((float)s[i]);
-            est += (double)atan2f(h, (float)v[i]);
+        for (int i = D - 2; i >= 0; i--) {
+            s += f[i + 1] * f[i + 1];
+            est += (double)atan2f(sqrtf(s), f[i]);
         }
-        const double t = est * (2.0 / 3.141592653589793) / (double)(D - 1) * (double)P;
+        const double t = (double)est * (2.0 / 3.141592653589793) / (double)(D - 1) * (double)P;
         const double fl = floor(t);
         const double fr = t - fl;
         if (fr > margin && fr < 1.0 - margin) return clamp_key((int32_t)fl, P);
     }
-    return angle_key_exact<D>(v, P);
+    return kAngleUndecided;
+}
+
+// Dim and Grid keys are exact; the Angle key may be kAngleUndecided.
+template <int D>
+__device__ __forceinline__ int32_t partition_key_fast(const double (&v)[D], const KeyParams &kp) {
+    if (kp.algo == SKY_ALGO_DIM) return clamp_key(java_d2i(v[0] / kp.dim_width), kp.P);
+    if (kp.algo == SKY_ALGO_GRID) {
+        uint32_t mask = 0;
+#pragma unroll
+        for (int i = 0; i < D; i++)
+            if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
+        return (int32_t)mask;
+    }
+    return angle_key_fast<D>(v, kp.P, kp.margin);
 }
 
 template <int D>
@@ -211,7 +235,8 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
             if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
         return (int32_t)mask;
     }
-    return angle_key<D>(v, kp.P, kp.margin);
+    const int32_t k = angle_key_fast<D>(v, kp.P, kp.margin);
+    return k != kAngleUndecided ? k : angle_key_exact<D>(v, kp.P);
 }
 
 // ---- dominance ----------------------------------------------------------------

@@ -55,14 +55,17 @@ struct FilterArgs {
     uint32_t *blk_cnt;            // [tiles] candidates per tile
     uint32_t *dup_cnt;            // [Kp*M]
     uint32_t *flags;              // kFlag*
+    uint32_t *defer_list;         // [n] MR-Angle tuples whose key needs the exact path
+    uint32_t *defer_cnt;
 };
+void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
 void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                    const int32_t *given_keys, int single, int32_t *skey, double *ssum, double *srow,
                    hipStream_t st);
 void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
-                           uint32_t *boff, uint32_t *order, int Kp, int M, double *pruners, int32_t *npr,
-                           hipStream_t st);
+                           uint32_t *boff, double *osum, uint32_t *oid, double *orow, int Kp, int M, double *pruners,
+                           int32_t *npr, hipStream_t st);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
 struct CompactArgs {
@@ -74,9 +77,10 @@ struct CompactArgs {
     uint64_t *sortkey;            // [mt]
     uint32_t *slot_src;           // [mt] source tuple index (bit31: pruner entry)
     uint32_t *flags;
-    unsigned long long *orand;    // {OR, AND} of all sort keys
+    unsigned long long *tile_orand;   // [tiles][2] per-tile {OR, AND} of the sort keys
 };
 void launch_compact(int D, const CompactArgs &a, hipStream_t st);
+void launch_orand_reduce(const unsigned long long *part, uint32_t np, unsigned long long *orand, hipStream_t st);
 struct AppendArgs {
     const double *pruners;        // [Kp][M][D]
     const uint32_t *dup_cnt;      // [Kp*M]
@@ -148,11 +152,11 @@ void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, cons
 // ---- k_sfs.hip ----
 struct SfsSeg { uint32_t begin, count; };
 struct SfsTile { uint32_t seg, start, count, out; };
-void launch_block_sky(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
+void launch_block_sky(int D, bool f64, bool full, bool ties, int B, int TB, const void *rows, const uint64_t *key,
                       const uint32_t *act, const SfsSeg *segs, const uint32_t *seg_list, uint32_t nseg_work,
-                      uint8_t *alive, void *conf_rows, uint32_t *nconf, hipStream_t st);
-void launch_filter_rest(int D, bool f64, bool full, int B, const void *rows, const uint32_t *act,
-                        const SfsTile *tiles, uint32_t ntiles, const void *conf_rows, const uint32_t *nconf,
+                      uint8_t *alive, uint8_t *xkeep, hipStream_t st);
+void launch_filter_rest(int D, bool f64, bool full, int B, int TB, const void *rows, const uint32_t *act,
+                        const SfsTile *tiles, uint32_t ntiles, const SfsSeg *segs, const uint8_t *xkeep,
                         uint32_t *keep, hipStream_t st);
 void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uint32_t *keep_scan,
                         const SfsTile *tiles, uint32_t ntiles, uint32_t *act_new, uint32_t *segcnt,

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output for the skyline kernels.
+
+  kernel-trace:  python tools/prof_summary.py trace <dir>            -> per-kernel stats (avg/total us)
+  counters:      python tools/prof_summary.py pmc <dir> <kernel-substr> [--n N --dims D --dist X]
+                 -> per-launch counter averages; with FETCH_SIZE / WRITE_SIZE it writes
+                    profiles/traffic_filter.json (HBM bytes per launch)
+
+gfx950 corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): FETCH_SIZE
+counts 64 B per 128-B request of a wide coalesced stream, i.e. HALF the bytes read,
+so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Both are reported by
+rocprofv3 in KiB.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _rows(d, pattern):
+    files = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    for f in files:
+        with open(f, newline="") as fh:
+            for r in csv.DictReader(fh):
+                yield r
+
+
+def trace(d):
+    agg = defaultdict(lambda: [0, 0.0])
+    for r in _rows(d, "*kernel_trace.csv"):
+        name = r.get("Kernel_Name", "?")
+        dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+        agg[name][0] += 1
+        agg[name][1] += dt
+    out = sorted(((v[1], k, v[0]) for k, v in agg.items()), reverse=True)
+    tot = sum(v[0] for v in out) or 1.0
+    print(f"{'total_us':>12} {'calls':>6} {'avg_us':>10} {'pct':>6}  kernel")
+    for t, k, c in out[:40]:
+        print(f"{t:12.1f} {c:6d} {t / c:10.2f} {100 * t / tot:6.1f}  {k[:110]}")
+    return out
+
+
+def pmc(d, sub, meta):
+    per = defaultdict(lambda: defaultdict(float))
+    for r in _rows(d, "*counter_collection.csv"):
+        if sub not in r.get("Kernel_Name", ""):
+            continue
+        per[r.get("Dispatch_Id", r.get("Correlation_Id", "?"))][r["Counter_Name"]] += float(r["Counter_Value"])
+    if not per:
+        print("no dispatches matched", sub)
+        return None
+    names = sorted({c for v in per.values() for c in v})
+    avg = {c: sum(v.get(c, 0.0) for v in per.values()) / len(per) for c in names}
+    print(f"{len(per)} dispatches of *{sub}*")
+    for c in names:
+        print(f"  {c:28s} {avg[c]:.6g}")
+    res = {"kernel_substr": sub, "dispatches": len(per), "avg": avg}
+    res.update(meta)
+    return res
+
+
+def main():
+    mode, d = sys.argv[1], sys.argv[2]
+    if mode == "trace":
+        trace(d)
+        return
+    sub = sys.argv[3]
+    meta = {}
+    args = sys.argv[4:]
+    for i in range(0, len(args), 2):
+        k = args[i].lstrip("-")
+        meta[k] = int(args[i + 1]) if args[i + 1].isdigit() else args[i + 1]
+    res = pmc(d, sub, meta)
+    if res is None:
+        return
+    out = os.path.join(REPO, "profiles", "traffic_filter.json")
+    old = json.load(open(out)) if os.path.exists(out) else {}
+    old.update({k: v for k, v in res.items() if k != "avg"})
+    old.setdefault("counters", {}).update(res["avg"])
+    c = old["counters"]
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rd = 2.0 * c["FETCH_SIZE"] * 1024.0      # gfx950: FETCH_SIZE reads half of a wide stream
+        wr = c["WRITE_SIZE"] * 1024.0
+        old["hbm_read_bytes_per_launch"] = rd
+        old["hbm_write_bytes_per_launch"] = wr
+        old["hbm_bytes_per_launch"] = rd + wr
+        old["correction"] = "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB"
+    json.dump(old, open(out, "w"), indent=1)
+    print("wrote", out)
+
+
+if __name__ == "__main__":
+    main()
