@@ -29,6 +29,18 @@ def _rows(d, pattern):
                 yield r
 
 
+def _db_kernels(d):
+    """(name, duration_ns) of every dispatch in rocprofv3's rocpd SQLite output."""
+    import sqlite3
+    for f in sorted(glob.glob(os.path.join(d, "**", "*.db"), recursive=True)):
+        con = sqlite3.connect(f)
+        try:
+            for name, dur in con.execute("select name, duration from kernels"):
+                yield name, int(dur)
+        finally:
+            con.close()
+
+
 def trace(d):
     agg = defaultdict(lambda: [0, 0.0])
     for r in _rows(d, "*kernel_trace.csv"):
@@ -36,6 +48,10 @@ def trace(d):
         dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
         agg[name][0] += 1
         agg[name][1] += dt
+    if not agg:
+        for name, dur in _db_kernels(d):
+            agg[name][0] += 1
+            agg[name][1] += dur / 1000.0
     out = sorted(((v[1], k, v[0]) for k, v in agg.items()), reverse=True)
     tot = sum(v[0] for v in out) or 1.0
     print(f"{'total_us':>12} {'calls':>6} {'avg_us':>10} {'pct':>6}  kernel")
