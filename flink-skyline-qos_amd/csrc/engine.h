@@ -53,7 +53,7 @@ struct Pipe {
     // per tuple / per tile
     DevBuf status, blk_cnt, blk_off, out_cnt, out_off;
     // pruners
-    DevBuf skey, ssum, sidx, sorder, ssorted, pruners, npr, dup_cnt, pr_entries, pruner_slot;
+    DevBuf pmin, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     // candidates (slot order) and sort
     DevBuf rows, sortkey, slot_src, perm, key_alt, val_alt, rows_sorted;
     DevBuf runflag, runscan, run_first, repof, repflag, repscan, rep_rows, rep_key, rep_of_sorted, slot_rep;

@@ -295,18 +295,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
 
     // ---- pruners from a strided sample
     const uint32_t S = std::min<uint32_t>(n, 65536);
-    SKY_TRY(p.skey.ensure((size_t)S * 4));
-    SKY_TRY(p.ssum.ensure((size_t)S * 8));
-    SKY_TRY(p.sidx.ensure((size_t)S * D * 8));          // sample rows
-    SKY_TRY(p.sorder.ensure(((size_t)S + p.Kp + 1) * 4));
-    SKY_TRY(p.ssorted.ensure((size_t)S * 8 + (size_t)S * D * 8));
+    SKY_TRY(p.pmin.ensure((size_t)p.Kp * p.M * 8));
     SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
-    launch_sample(D, in.vals, n, S, kp, in.keys, in.single, p.skey.as<int32_t>(), p.ssum.as<double>(),
-                  p.sidx.as<double>(), st);
-    launch_select_pruners(D, p.sidx.as<double>(), S, p.skey.as<int32_t>(), p.ssum.as<double>(),
-                          p.sorder.as<uint32_t>() + S, p.ssorted.as<double>(), p.sorder.as<uint32_t>(),
-                          p.ssorted.as<double>() + S, p.Kp, p.M, p.pruners.as<double>(), p.npr.as<int32_t>(), st);
+    launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
+                          p.pruners.as<double>(), p.npr.as<int32_t>(), st);
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 

@@ -122,153 +122,95 @@ __global__ __launch_bounds__(kThreads) void k_keys(const double *__restrict__ va
     }
 }
 
-// strided sample: key, f64 score and a private copy of the row (contiguous)
+// ---- pruners ------------------------------------------------------------------
+// A pruner of partition k is a tuple of k; any tuple of k it dominates is outside
+// L_k, and a tuple EQUAL to it shares its fate, so the choice only affects speed.
+// Pruner j of k is the sample tuple of k minimising the positive-weight linear
+// criterion c_j (j = 0: the plain sum, i.e. the SFS score; j >= 1: the sum with
+// dimension (j-1) mod D weighted 4x, pulling the winner towards another corner of
+// the front): a minimiser of a positive-weight sum is never
+// dominated within the sample, so the winners are (up to f32 rounding of c_j,
+// checked exactly in k_pick_pruners) skyline points of the sample.  One parallel
+// pass: per-(k, j) packed (order-key(c_j) << 32 | sample id) minima, LDS atomics
+// per workgroup, one global atomicMin per workgroup and slot.
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_sample(const double *__restrict__ vals, uint32_t n, uint32_t S,
-                                                     KeyParams kp, const int32_t *__restrict__ given_keys,
-                                                     int single, int32_t *__restrict__ skey,
-                                                     double *__restrict__ ssum, double *__restrict__ srow) {
+__global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restrict__ vals, uint32_t n, uint32_t S,
+                                                         KeyParams kp, const int32_t *__restrict__ given_keys,
+                                                         int single, int Kp, int M,
+                                                         unsigned long long *__restrict__ gmin) {
+    __shared__ unsigned long long s_min[2048];
+    const int KM = Kp * M;
+    for (int q = threadIdx.x; q < KM; q += kThreads) s_min[q] = ~0ull;
+    __syncthreads();
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
-    if (s >= S) return;
-    const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
-    double v[D];
-    load_row<D>(vals + (size_t)i * D, v);
-    bool nan = false;
-    double sum = 0.0;
+    if (s < S) {
+        const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
+        double v[D];
+        load_row<D>(vals + (size_t)i * D, v);
+        bool nan = false;
 #pragma unroll
-    for (int d = 0; d < D; d++) { nan |= v[d] != v[d]; sum = sum + v[d]; srow[(size_t)s * D + d] = v[d]; }
-    int32_t k = single ? 0 : given_keys ? given_keys[i] : partition_key<D>(v, kp);
-    if (nan || k < 0 || k >= kp.K || sum != sum) k = -1;
-    skey[s] = k;
-    ssum[s] = sum;
-}
-
-// lanes of this wave whose (active, 8-bit) key equals mine
-__device__ __forceinline__ uint64_t wave_peers_u8(bool active, uint32_t key) {
-    uint64_t peers = __ballot(active);
+        for (int d = 0; d < D; d++) nan |= v[d] != v[d];
+        const int32_t k = single ? 0 : given_keys ? given_keys[i] : (nan ? -1 : partition_key<D>(v, kp));
+        if (!nan && k >= 0 && k < Kp) {
+            float f[D];
+            float sum = 0.0f;
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
-        const bool bit = (key >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        peers &= bit ? bb : ~bb;
-    }
-    return peers;
-}
-
-// one workgroup: counting sort of the sample by partition into contiguous copies
-// (score, sample id, row) so the pruner scan reads sequential memory
-template <int D>
-__global__ __launch_bounds__(1024) void k_bucket_samples(const int32_t *__restrict__ skey,
-                                                         const double *__restrict__ ssum,
-                                                         const double *__restrict__ srow, uint32_t S, int Kp,
-                                                         uint32_t *__restrict__ boff, double *__restrict__ osum,
-                                                         uint32_t *__restrict__ oid, double *__restrict__ orow) {
-    __shared__ uint32_t s_cnt[kMaxK + 1];
-    __shared__ uint32_t s_cur[kMaxK + 1];
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int q = threadIdx.x; q <= Kp; q += 1024) s_cnt[q] = 0;
-    __syncthreads();
-    for (uint32_t s0 = 0; s0 < S; s0 += 1024) {
-        const uint32_t s = s0 + threadIdx.x;
-        const int32_t k = s < S ? skey[s] : -1;
-        const uint64_t peers = wave_peers_u8(k >= 0, (uint32_t)k);
-        if (k >= 0 && __popcll(peers & lt) == 0) atomicAdd(&s_cnt[k], (uint32_t)__popcll(peers));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int q = 0; q < Kp; q++) { s_cur[q] = run; boff[q] = run; run += s_cnt[q]; }
-        boff[Kp] = run;
-    }
-    __syncthreads();
-    for (uint32_t s0 = 0; s0 < S; s0 += 1024) {
-        const uint32_t s = s0 + threadIdx.x;
-        const int32_t k = s < S ? skey[s] : -1;
-        const uint64_t peers = wave_peers_u8(k >= 0, (uint32_t)k);
-        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)peers) - 1);
-        uint32_t base = 0;
-        if (k >= 0 && lane == (int)leader) base = atomicAdd(&s_cur[k], (uint32_t)__popcll(peers));
-        base = __shfl(base, (int)(k >= 0 ? leader : 0), 64);
-        if (k >= 0) {
-            const uint32_t pos = base + __popcll(peers & lt);
-            osum[pos] = ssum[s];
-            oid[pos] = s;
+            for (int d = 0; d < D; d++) { f[d] = (float)v[d]; sum += f[d]; }
 #pragma unroll
-            for (int d = 0; d < D; d++) orow[(size_t)pos * D + d] = srow[(size_t)s * D + d];
-        }
-    }
-}
-
-// one workgroup per partition: up to M mutually non-dominated, non-equal sample
-// tuples, smallest (score, sample id) first
-template <int D>
-__global__ __launch_bounds__(1024) void k_select_pruners(const double *__restrict__ orow,
-                                                         const uint32_t *__restrict__ boff,
-                                                         const uint32_t *__restrict__ oid,
-                                                         const double *__restrict__ osum, int M,
-                                                         double *__restrict__ pruners, int32_t *__restrict__ npr) {
-    constexpr int NW = 1024 / 64;
-    __shared__ double s_pr[8][D];
-    __shared__ double s_bs[NW];
-    __shared__ uint32_t s_bi[NW], s_bq[NW];
-    __shared__ uint32_t s_win;
-    const int k = blockIdx.x;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t b0 = boff[k], b1 = boff[k + 1];
-    int chosen = 0;
-    for (int j = 0; j < M && j < 8; j++) {
-        double best = __builtin_inf();
-        uint32_t bi = 0xffffffffu, bq = 0;
-        for (uint32_t q = b0 + threadIdx.x; q < b1; q += 1024) {
-            const double sc = osum[q];
-            const uint32_t s = oid[q];
-            if (!(sc < best || (sc == best && s < bi))) continue;
-            bool ok = true;
-            if (chosen) {
-                double v[D];
-                load_row<D>(orow + (size_t)q * D, v);
-                for (int c = 0; c < chosen && ok; c++) {
-                    bool le = true, lt = false, eq = true;
-#pragma unroll
-                    for (int d = 0; d < D; d++) {
-                        le &= s_pr[c][d] <= v[d];
-                        lt |= s_pr[c][d] < v[d];
-                        eq &= s_pr[c][d] == v[d];
-                    }
-                    ok = !(le && lt) && !eq;
-                }
+            for (int j = 0; j < 8; j++) {
+                if (j >= M) break;
+                const float c = j == 0 ? sum : sum + 3.0f * f[(j - 1) % D];
+                if (c != c) continue;
+                atomicMin(&s_min[k * M + j], ((unsigned long long)f32_order_key(c) << 32) | s);
             }
-            if (ok) { best = sc; bi = s; bq = q; }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const double ob = __shfl_xor(best, o, 64);
-            const uint32_t oi = __shfl_xor(bi, o, 64);
-            const uint32_t oq = __shfl_xor(bq, o, 64);
-            if (ob < best || (ob == best && oi < bi)) { best = ob; bi = oi; bq = oq; }
-        }
-        if (lane == 0) { s_bs[w] = best; s_bi[w] = bi; s_bq[w] = bq; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double b = s_bs[0];
-            uint32_t x = s_bi[0], xq = s_bq[0];
-            for (int q = 1; q < NW; q++)
-                if (s_bs[q] < b || (s_bs[q] == b && s_bi[q] < x)) { b = s_bs[q]; x = s_bi[q]; xq = s_bq[q]; }
-            s_win = x == 0xffffffffu ? 0xffffffffu : xq;
-        }
-        __syncthreads();
-        const uint32_t win = s_win;
-        if (win == 0xffffffffu) break;
-        if (threadIdx.x < D) {
-            const double x = orow[(size_t)win * D + threadIdx.x];
-            s_pr[chosen][threadIdx.x] = x;
-            pruners[((size_t)k * M + chosen) * D + threadIdx.x] = x;
-        }
-        chosen++;
-        __syncthreads();
     }
-    if (threadIdx.x == 0) npr[k] = chosen;
+    __syncthreads();
+    for (int q = threadIdx.x; q < KM; q += kThreads)
+        if (s_min[q] != ~0ull) atomicMin(&gmin[q], s_min[q]);
+}
+
+// One workgroup per partition: the (<= M) winners are deduplicated (equal rows keep
+// the first) and every winner another winner dominates is dropped (exact f64 test),
+// so the pruners of k are distinct and mutually non-dominated.  Order: criterion j.
+template <int D>
+__global__ __launch_bounds__(64) void k_pick_pruners(const double *__restrict__ vals, uint32_t n, uint32_t S,
+                                                     const unsigned long long *__restrict__ gmin, int M,
+                                                     double *__restrict__ pruners, int32_t *__restrict__ npr) {
+    __shared__ double s_c[64][D];
+    __shared__ int s_ok[64];
+    const int k = blockIdx.x, j = threadIdx.x;
+    const unsigned long long w = j < M ? gmin[k * M + j] : ~0ull;
+    const bool has = w != ~0ull;
+    if (has) {
+        const uint32_t s = (uint32_t)(w & 0xffffffffu);
+        const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
+#pragma unroll
+        for (int d = 0; d < D; d++) s_c[j][d] = vals[(size_t)i * D + d];
+    }
+    s_ok[j] = has ? 1 : 0;
+    __syncthreads();
+    bool ok = has;
+    if (ok) {
+        for (int q = 0; q < M && ok; q++) {
+            if (q == j || !s_ok[q]) continue;
+            bool le = true, lt = false, eq = true;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                le &= s_c[q][d] <= s_c[j][d];
+                lt |= s_c[q][d] < s_c[j][d];
+                eq &= s_c[q][d] == s_c[j][d];
+            }
+            if ((le && lt) || (eq && q < j)) ok = false;
+        }
+    }
+    const uint64_t b = __ballot(ok);
+    if (ok) {
+        const int pos = __popcll(b & (j == 0 ? 0ull : (~0ull >> (64 - j))));
+#pragma unroll
+        for (int d = 0; d < D; d++) pruners[((size_t)k * M + pos) * D + d] = s_c[j][d];
+    }
+    if (j == 0) npr[k] = __popcll(b);
 }
 
 // Classify one tuple of partition k: dropped (dominated by a pruner of k), exact
@@ -321,16 +263,27 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
     uint32_t lflags = 0, mycnt = 0;
     const uint32_t base = blockIdx.x * kTile;
     const int lane = threadIdx.x & 63;
+    // software pipeline: the row of item r+1 is in flight while item r is classified
+    double vn[D];
+    {
+        const uint32_t i = base + threadIdx.x;
+        if (i < a.n) load_row<D>(a.vals + (size_t)i * D, vn);
+        else {
+#pragma unroll
+            for (int d = 0; d < D; d++) vn[d] = 0.0;
+        }
+    }
 #pragma unroll 1
     for (int r = 0; r < kItems; r++) {
         const uint32_t i = base + r * kThreads + threadIdx.x;
         if (base + r * kThreads >= a.n) break;                       // block-uniform
         const bool valid = i < a.n;
         double v[D];
-        if (valid) load_row<D>(a.vals + (size_t)i * D, v);
-        else {
 #pragma unroll
-            for (int d = 0; d < D; d++) v[d] = 0.0;
+        for (int d = 0; d < D; d++) v[d] = vn[d];
+        if (r + 1 < kItems) {
+            const uint32_t i2 = i + kThreads;
+            if (i2 < a.n) load_row<D>(a.vals + (size_t)i2 * D, vn);
         }
         bool nan = false;
 #pragma unroll
@@ -880,19 +833,14 @@ void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int
     SKY_DISPATCH_D(D, (k_keys<DD><<<g, kThreads, 0, st>>>(vals, n, kp, keys)));
 }
 
-void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
-                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, double *srow,
-                   hipStream_t st) {
+void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
+                           const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
+                           double *pruners, int32_t *npr, hipStream_t st) {
     if (S == 0) return;
-    SKY_DISPATCH_D(D, (k_sample<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
-                                                                             skey, ssum, srow)));
-}
-
-void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
-                           uint32_t *boff, double *osum, uint32_t *oid, double *orow, int Kp, int M, double *pruners,
-                           int32_t *npr, hipStream_t st) {
-    SKY_DISPATCH_D(D, (k_bucket_samples<DD><<<1, 1024, 0, st>>>(skey, ssum, srow, S, Kp, boff, osum, oid, orow)));
-    SKY_DISPATCH_D(D, (k_select_pruners<DD><<<Kp, 1024, 0, st>>>(orow, boff, oid, osum, M, pruners, npr)));
+    (void)hipMemsetAsync(gmin, 0xff, (size_t)Kp * M * 8, st);
+    SKY_DISPATCH_D(D, (k_sample_min<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
+                                                                                 Kp, M, gmin)));
+    SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {

@@ -122,13 +122,43 @@ struct KeyParams {
 };
 
 // Error budget of the f32 estimate in t = avg*P (inputs with nonzero magnitudes in
-// [1e-15, 1e15]): per angle, the f32 inputs and the f32 sum of <= 15 squares are
-// within 16*2^-24 relative, sqrtf within 1 ulp, so the angle moves by < 6e-7 rad;
-// atan2f errs by <= 6 ulp (OpenCL bound) < 1.5e-6 rad; the angles are summed in
-// f64.  Per angle < 2.1e-6 rad, normalised by pi/2 and averaged over the angles:
-// |t_est - t| < 1.4e-6 * P.  The margin 1e-5 + 4e-6*P keeps a ~3x safety factor
-// (the exact fallback runs whenever t_est is closer than that to an integer).
-inline double angle_margin(int P) { return 1e-5 + 4e-6 * (double)P; }
+// [1e-15, 1e15], so no f32 square over- or underflows):
+//   * inputs and the f32 FMA sum of <= 15 squares: relative <= 1.1e-6; v_sqrt_f32
+//     (1 ulp) -> hyp relative <= 7e-7; the ratio a = min/max via v_rcp_f32 (1 ulp)
+//     -> relative <= 1e-6 -> angle error <= 1e-6 rad (d atan(a) <= da);
+//   * atan on [0,1] by the 7-term odd polynomial atan_poly: <= 2.5e-7 rad, plus f32
+//     evaluation and the pi/2 - r, pi - r reflections: <= 1e-6 rad;
+//   so <= 2.2e-6 rad per angle; the f32 sum of <= 15 angles (each partial <= 15 pi)
+//   adds <= 14 x 1.9e-6 rad; t = sum * (2/pi)/(D-1) * P then errs by <= 2.5e-6 * P
+//   for every D in [2,16] (plus 1e-6 for the f32 scale).
+// The margin 1e-5 + 8e-6*P keeps a >= 3x safety factor; the exact fdlibm fallback
+// runs whenever t_est is closer than that to an integer.
+inline double angle_margin(int P) { return 1e-5 + 8e-6 * (double)P; }
+
+// atan(a) for a in [0,1]: a * poly(a^2), 7 terms, |error| <= 2.5e-7 (Lawson-refined
+// least squares on Chebyshev nodes; the constants are what the bound was measured for)
+__device__ __forceinline__ float atan_poly01(float a) {
+    const float z = a * a;
+    float p = 0.006811792604364258f;
+    p = fmaf(p, z, -0.03360421913563544f);
+    p = fmaf(p, z, 0.07962367186607752f);
+    p = fmaf(p, z, -0.1323334216932318f);
+    p = fmaf(p, z, 0.19807815630001427f);
+    p = fmaf(p, z, -0.33317368071637243f);
+    p = fmaf(p, z, 0.999996111561908f);
+    return a * p;
+}
+
+// estimate of atan2(h, x) for h >= 0 (the reference's hyp): first-quadrant
+// polynomial, then reflections; atan2(+0, -0) = pi and atan2(h>0, -0) = pi/2 as Java
+__device__ __forceinline__ float atan2_est(float h, float x) {
+    const float ax = fabsf(x);
+    const float mn = fminf(h, ax), mx = fmaxf(h, ax);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    float r = atan_poly01(a > 1.0f ? 1.0f : a);
+    r = h > ax ? 1.57079632679489662f - r : r;
+    return signbit(x) ? 3.14159265358979324f - r : r;
+}
 
 __device__ __forceinline__ int32_t clamp_key(int32_t p, int P) {
     p = p > P - 1 ? P - 1 : p;
@@ -196,17 +226,16 @@ __device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, d
         float f[D];
 #pragma unroll
         for (int i = 0; i < D; i++) f[i] = (float)v[i];
-        float s = 0.0f;
-        double est = 0.0;
+        float s = 0.0f, est = 0.0f;
 #pragma unroll
         for (int i = D - 2; i >= 0; i--) {
-            s += f[i + 1] * f[i + 1];
-            est += (double)atan2f(sqrtf(s), f[i]);
+            s = fmaf(f[i + 1], f[i + 1], s);
+            est += atan2_est(__builtin_amdgcn_sqrtf(s), f[i]);
         }
-        const double t = (double)est * (2.0 / 3.141592653589793) / (double)(D - 1) * (double)P;
-        const double fl = floor(t);
-        const double fr = t - fl;
-        if (fr > margin && fr < 1.0 - margin) return clamp_key((int32_t)fl, P);
+        const float t = est * (float)((2.0 / 3.141592653589793) / (double)(D - 1) * (double)P);
+        const float fl = floorf(t);
+        const float fr = t - fl;
+        if (fr > (float)margin && fr < (float)(1.0 - margin)) return clamp_key((int32_t)fl, P);
     }
     return kAngleUndecided;
 }

@@ -60,12 +60,10 @@ struct FilterArgs {
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
-void launch_sample(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
-                   const int32_t *given_keys, int single, int32_t *skey, double *ssum, double *srow,
-                   hipStream_t st);
-void launch_select_pruners(int D, const double *srow, uint32_t S, const int32_t *skey, const double *ssum,
-                           uint32_t *boff, double *osum, uint32_t *oid, double *orow, int Kp, int M, double *pruners,
-                           int32_t *npr, hipStream_t st);
+// pruners: per partition up to M (<= 64) distinct, mutually non-dominated sample tuples
+void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
+                           const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
+                           double *pruners, int32_t *npr, hipStream_t st);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
 struct CompactArgs {

@@ -84,6 +84,26 @@ def main():
     if mode == "trace":
         trace(d)
         return
+    if mode == "pmcshow":      # print per-launch averages only (no traffic file)
+        import re
+        rx = re.compile(sys.argv[3])
+        per = defaultdict(lambda: defaultdict(float))
+        names = {}
+        for r in _rows(d, "*counter_collection.csv"):
+            if not rx.search(r.get("Kernel_Name", "")):
+                continue
+            key = r.get("Dispatch_Id", "?")
+            names[key] = r["Kernel_Name"]
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+        by_k = defaultdict(list)
+        for key, c in per.items():
+            by_k[names[key]].append(c)
+        for kname, lst in by_k.items():
+            cs = sorted({c for v in lst for c in v})
+            print(f"{len(lst)} dispatches of {kname[:90]}")
+            for c in cs:
+                print(f"  {c:28s} {sum(v.get(c, 0.0) for v in lst) / len(lst):.6g}")
+        return
     sub = sys.argv[3]
     meta = {}
     args = sys.argv[4:]
