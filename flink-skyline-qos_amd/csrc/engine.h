@@ -63,6 +63,8 @@ struct Pipe {
     DevBuf conf_small, seg_small, slot_fate, pruner_fate, defer, tile_orand, xkeep;
     // global
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
+    // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers
+    DevBuf r16, r16g, r16a, r16b, i16a, i16b, dead16, keep16, scan16, xbuf16, xcnt16, xseg16, items16, at16, atv16;
     DevBuf scratch, flags, totals, orand, lsz, surv;
     // host-visible pinned staging
     void *pin = nullptr;
@@ -71,7 +73,7 @@ struct Pipe {
     // results of the last run
     uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0;
     int M = 1, Kp = 1, K = 1;
-    bool f64 = false, ties = false;
+    bool f64 = false, ties = false, u16 = false;
     std::vector<uint32_t> h_dup;
     std::vector<int32_t> h_entries;
     std::vector<unsigned long long> h_lsz, h_surv;

@@ -11,6 +11,7 @@
 #include "ctx.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -112,6 +113,14 @@ static int debug_level() {
     }();
     return lvl;
 }
+// SKY_SFS16=0 forces the generic f32/f64 SFS (used by the tests to cover both paths)
+static bool sfs16_disabled() {
+    static bool off = [] {
+        const char *e = getenv("SKY_SFS16");
+        return e && atoi(e) == 0;
+    }();
+    return off;
+}
 static int stage_check(hipStream_t st, const char *where) {
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && debug_level()) {
@@ -172,6 +181,11 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
             hsegs[k] = SfsSeg{begin[k], cnt[k]};
             if (cnt[k] && cnt[k] <= kSmallSeg) small.push_back(k);
         }
+        if (debug_level() >= 2) {
+            fprintf(stderr, "[sky] sfs nrep=%u nseg=%u small=%zu full=%d:", nrep, nseg, small.size(), (int)full);
+            for (uint32_t k = 0; k < nseg; k++) fprintf(stderr, " %u", cnt[k]);
+            fprintf(stderr, "\n");
+        }
         if (!small.empty()) {
             SKY_TRY(p.conf_small.ensure((size_t)nrep * rb));
             SKY_TRY(p.seg_small.ensure(small.size() * 4));
@@ -198,6 +212,11 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         }
         if (work.empty()) break;
         p.sfs_rounds++;
+        if (debug_level() >= 2) {
+            fprintf(stderr, "[sky] sfs round %lld full=%d segs:", (long long)p.sfs_rounds, (int)full);
+            for (uint32_t k : work) fprintf(stderr, " %u:%u", k, cnt[k]);
+            fprintf(stderr, "\n");
+        }
         SKY_TRY(p.upload(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), st));
         SKY_TRY(p.upload(p.seg_list.p, work.data(), work.size() * 4, st));
         c.ktimer_begin("block_sky", st);
@@ -244,6 +263,127 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
             run += sc[k];
         }
         std::swap(p.act, p.act2);
+    }
+    return SKY_OK;
+}
+
+static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
+                     std::vector<void *> dsts);
+// ---- segmented SFS for integer-valued rows (k_dom16.hip) ---------------------------
+// rows16: packed rows by position; segments [begin[k], begin[k]+cnt[k]) sorted by a
+// strictly monotone score.  alive[position of round 0] = 1 for skyline members.
+static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std::vector<uint32_t> begin,
+                     std::vector<uint32_t> cnt, uint8_t *alive, int W) {
+    hipStream_t st = c.st;
+    const uint32_t nseg = (uint32_t)begin.size();
+    if (nrep == 0 || nseg == 0) return SKY_OK;
+    uint32_t maxc = 0;
+    for (uint32_t k = 0; k < nseg; k++) maxc = std::max(maxc, cnt[k]);
+    const uint32_t B = maxc > 65536 ? 16384u : 4096u;     // X per round
+    const size_t rowb = (size_t)W * 4;
+    SKY_TRY(p.dead16.ensure((size_t)nrep * 4));
+    SKY_TRY(p.keep16.ensure(((size_t)nrep + 1) * 4));
+    SKY_TRY(p.scan16.ensure(((size_t)nrep + 1) * 4));
+    SKY_TRY(p.r16a.ensure((size_t)nrep * rowb));
+    SKY_TRY(p.r16b.ensure((size_t)nrep * rowb));
+    SKY_TRY(p.i16a.ensure((size_t)nrep * 4));
+    SKY_TRY(p.i16b.ensure((size_t)nrep * 4));
+    SKY_TRY(p.xbuf16.ensure((size_t)nseg * B * rowb));
+    SKY_TRY(p.xcnt16.ensure((size_t)nseg * 4));
+    SKY_TRY(p.xseg16.ensure((size_t)nseg * sizeof(SfsSeg)));
+    SKY_TRY(p.at16.ensure((size_t)nseg * 8));
+    SKY_TRY(p.atv16.ensure((size_t)nseg * 8));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(nrep + 1) * 4 + 64));
+    const uint32_t *cur_rows = rows16;
+    const uint32_t *cur_idx = nullptr;                     // round 0: identity
+    uint32_t npos = 0;
+    for (uint32_t k = 0; k < nseg; k++) npos = std::max(npos, begin[k] + cnt[k]);
+    int flip = 0;
+    std::vector<uint32_t> work;
+    std::vector<SfsSeg> xseg;
+    std::vector<DomItem> tri, rest;
+    std::vector<uint32_t> at;
+    for (;;) {
+        work.clear();
+        for (uint32_t k = 0; k < nseg; k++)
+            if (cnt[k]) work.push_back(k);
+        if (work.empty()) break;
+        p.sfs_rounds++;
+        if (debug_level() >= 2) {
+            fprintf(stderr, "[sky] sfs16 round %lld B=%u segs:", (long long)p.sfs_rounds, B);
+            for (uint32_t k : work) fprintf(stderr, " %u:%u", k, cnt[k]);
+            fprintf(stderr, "\n");
+        }
+        xseg.clear();
+        tri.clear();
+        rest.clear();
+        bool more = false;
+        uint32_t maxch = 0;
+        for (uint32_t s = 0; s < (uint32_t)work.size(); s++) {
+            const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
+            xseg.push_back(SfsSeg{b, xk});
+            more |= cnt[k] > xk;
+            maxch = std::max(maxch, (xk + kDomTx - 1) / kDomTx);
+        }
+        // items ordered by x chunk, so the first chunks (most dominating rows) run first
+        for (uint32_t cx = 0; cx < maxch; cx++)
+            for (uint32_t s = 0; s < (uint32_t)work.size(); s++) {
+                const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
+                if (cx * kDomTx >= xk) continue;
+                const uint32_t x0 = b + cx * kDomTx, nx = std::min(kDomTx, xk - cx * kDomTx);
+                for (uint32_t y = 0; y < xk; y += kDomTy) {
+                    const uint32_t y0 = b + y, ny = std::min(kDomTy, xk - y);
+                    if (x0 >= y0 + ny) continue;                 // every x after every y
+                    tri.push_back(DomItem{s, y0, ny, x0, nx, x0 + nx > y0 ? kDomDiag : 0u});
+                    p.sfs_pairs_upper += (int64_t)ny * nx;
+                }
+                for (uint32_t y = xk; y < cnt[k]; y += kDomTy) {
+                    const uint32_t ny = std::min(kDomTy, cnt[k] - y);
+                    rest.push_back(DomItem{s, b + y, ny, cx * kDomTx, nx, kDomRest});
+                    p.sfs_pairs_upper += (int64_t)ny * nx;
+                }
+            }
+        HIP_TRY(hipMemsetAsync(p.dead16.p, 0, (size_t)npos * 4, st));
+        SKY_TRY(p.items16.ensure((tri.size() + rest.size()) * sizeof(DomItem)));
+        SKY_TRY(p.upload(p.items16.p, tri.data(), tri.size() * sizeof(DomItem), st));
+        if (!rest.empty())
+            SKY_TRY(p.upload(p.items16.as<DomItem>() + tri.size(), rest.data(), rest.size() * sizeof(DomItem), st));
+        SKY_TRY(p.upload(p.xseg16.p, xseg.data(), xseg.size() * sizeof(SfsSeg), st));
+        c.ktimer_begin("dom", st);
+        launch_dom16(W, cur_rows, nullptr, nullptr, p.items16.as<DomItem>(), (uint32_t)tri.size(), 0,
+                     p.dead16.as<uint32_t>(), st);
+        launch_xcompact16(W, cur_rows, cur_idx, p.xseg16.as<SfsSeg>(), (uint32_t)work.size(), B,
+                          p.dead16.as<uint32_t>(), p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), alive, st);
+        launch_dom16(W, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(),
+                     p.items16.as<DomItem>() + tri.size(), (uint32_t)rest.size(), B, p.dead16.as<uint32_t>(), st);
+        c.ktimer_end("dom", st, 0);
+        STAGE(st, "dom16");
+        if (!more) break;
+        // next layout: the live rest of every segment, segments kept in order
+        launch_keep16(p.dead16.as<uint32_t>(), npos, p.keep16.as<uint32_t>(), st);
+        scan_excl_u32(p.keep16.as<uint32_t>(), p.scan16.as<uint32_t>(), npos, p.scan16.as<uint32_t>() + npos,
+                      p.scratch.as<uint32_t>(), st);
+        uint32_t *nrows = flip ? p.r16a.as<uint32_t>() : p.r16b.as<uint32_t>();
+        uint32_t *nidx = flip ? p.i16a.as<uint32_t>() : p.i16b.as<uint32_t>();
+        launch_move16(W, p.keep16.as<uint32_t>(), p.scan16.as<uint32_t>(), npos, cur_idx, cur_rows, nidx, nrows, st);
+        at.clear();
+        for (uint32_t k : work) { at.push_back(begin[k]); at.push_back(begin[k] + cnt[k]); }
+        SKY_TRY(p.upload(p.at16.p, at.data(), at.size() * 4, st));
+        launch_gather_u32(p.scan16.as<uint32_t>(), p.at16.as<uint32_t>(), (uint32_t)at.size(), p.atv16.as<uint32_t>(),
+                          st);
+        STAGE(st, "dom16_next");
+        std::vector<uint32_t> atv(at.size());
+        SKY_TRY(sync_read(p, st, {{p.atv16.p, at.size() * 4}}, {atv.data()}));
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        npos = 0;
+        for (size_t s = 0; s < work.size(); s++) {
+            begin[work[s]] = atv[2 * s];
+            cnt[work[s]] = atv[2 * s + 1] - atv[2 * s];
+            npos = std::max(npos, atv[2 * s + 1]);
+        }
+        cur_rows = nrows;
+        cur_idx = nidx;
+        flip ^= 1;
     }
     return SKY_OK;
 }
@@ -397,6 +537,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.nps = nps;
     p.f64 = (flags & kFlagNotF32) != 0;
     p.ties = (flags & kFlagScoreTies) != 0;
+    p.u16 = !p.f64 && !p.ties && (flags & kFlagNotU16) == 0 && !sfs16_disabled();
     p.mt = m + nps;
     const uint32_t mt = p.mt;
     const size_t rb = row_bytes(p.f64, D);
@@ -466,7 +607,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
 
         // ---- local skylines
         HIP_TRY(hipMemsetAsync(p.alive_l.p, 0, mr, st));
-        SKY_TRY(sfs_run(c, p, p.rep_rows.p, p.rep_key.as<uint64_t>(), mr, sb, se, false, p.alive_l.as<uint8_t>()));
+        const int W16 = dom16_words(D);
+        if (p.u16) {
+            SKY_TRY(p.r16.ensure((size_t)std::max<uint32_t>(mr, 1) * W16 * 4));
+            launch_pack16(D, p.rep_rows.as<float>(), mr, nullptr, p.r16.as<uint32_t>(), st);
+            SKY_TRY(sfs_run16(c, p, p.r16.as<uint32_t>(), mr, sb, se, p.alive_l.as<uint8_t>(), W16));
+        } else {
+            SKY_TRY(sfs_run(c, p, p.rep_rows.p, p.rep_key.as<uint64_t>(), mr, sb, se, false,
+                            p.alive_l.as<uint8_t>()));
+        }
         if (tm) tm->mark(6, st);
 
         // ---- global merge over the union of the local skylines
@@ -496,9 +645,18 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                                                    orand[0] ^ orand[1], p.scratch.as<uint32_t>(), st);
                 const uint64_t *gk = galt ? p.gkey_alt.as<uint64_t>() : p.gkey.as<uint64_t>();
                 const uint32_t *gv = galt ? p.gval_alt.as<uint32_t>() : p.gval.as<uint32_t>();
-                launch_gather_rows(D, p.f64, p.rep_rows.p, gv, mg, p.grows.p, st);
                 HIP_TRY(hipMemsetAsync(p.galive.p, 0, mg, st));
-                SKY_TRY(sfs_run(c, p, p.grows.p, gk, mg, {0u}, {mg}, true, p.galive.as<uint8_t>()));
+                // computed keys: a vector has one partition, so the union of the
+                // partitions' representatives is duplicate-free and the distinct-row
+                // test applies; given keys (lists of a merge) may repeat a vector
+                if (p.u16 && !in.keys) {
+                    SKY_TRY(p.r16g.ensure((size_t)mg * W16 * 4));
+                    launch_pack16(D, p.rep_rows.as<float>(), mg, gv, p.r16g.as<uint32_t>(), st);
+                    SKY_TRY(sfs_run16(c, p, p.r16g.as<uint32_t>(), mg, {0u}, {mg}, p.galive.as<uint8_t>(), W16));
+                } else {
+                    launch_gather_rows(D, p.f64, p.rep_rows.p, gv, mg, p.grows.p, st);
+                    SKY_TRY(sfs_run(c, p, p.grows.p, gk, mg, {0u}, {mg}, true, p.galive.as<uint8_t>()));
+                }
                 launch_scatter_alive(gv, p.galive.as<uint8_t>(), mg, p.alive_g.as<uint8_t>(), st);
                 STAGE(st, "global");
             }

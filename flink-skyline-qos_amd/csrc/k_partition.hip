@@ -364,6 +364,13 @@ __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part
     const float f = (float)s;
     inexact |= (double)f != s;
     if (inexact) lflags |= kFlagScoreTies;
+    bool u16 = true;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        const double x = (double)tv[d];
+        u16 &= (x >= 0.0) & (x <= 65535.0) & (x == floor(x));
+    }
+    if (!u16) lflags |= kFlagNotU16;
     uint32_t h = 0x9e3779b9u;
 #pragma unroll
     for (int d = 0; d < D; d++) {

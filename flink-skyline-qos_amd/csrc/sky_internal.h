@@ -173,6 +173,24 @@ void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t 
                           hipStream_t st);
 void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
 
+// ---- k_dom16.hip (integer-valued rows packed as u16 pairs) ----
+struct DomItem { uint32_t seg, y0, ny, x0, nx, flags; };
+constexpr uint32_t kDomDiag = 1u;             // x and y ranges overlap: only x before y
+constexpr uint32_t kDomRest = 2u;             // x from xbuf[seg] (X'), count from xcnt[seg]
+constexpr int kDomPPT = 8;                    // y rows per lane
+constexpr uint32_t kDomTy = 64u * kDomPPT;    // y rows per work item (one wave)
+constexpr uint32_t kDomTx = 1024u;            // x rows per work item
+int dom16_words(int D);
+void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, uint32_t *out, hipStream_t st);
+void launch_dom16(int W, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
+                  uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st);
+void launch_xcompact16(int W, const uint32_t *rows, const uint32_t *idx, const SfsSeg *xseg, uint32_t nslots,
+                       uint32_t xcap, uint32_t *dead, uint32_t *xbuf, uint32_t *xcnt, uint8_t *alive, hipStream_t st);
+void launch_keep16(const uint32_t *dead, uint32_t n, uint32_t *keep, hipStream_t st);
+void launch_move16(int W, const uint32_t *keep, const uint32_t *scan, uint32_t n, const uint32_t *idx,
+                   const uint32_t *rows, uint32_t *idx_out, uint32_t *rows_out, hipStream_t st);
+void launch_gather_u32(const uint32_t *src, const uint32_t *at, uint32_t n, uint32_t *out, hipStream_t st);
+
 // ---- k_synth.hip ----
 void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
                   int64_t *ids, hipStream_t st);
