@@ -37,6 +37,50 @@ from skyline import _abi  # noqa: E402
 from skyline.dist import distributed_query  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
+# VALU compare peak: 256 CU x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz = one 32-bit compare per
+# lane-cycle (MI355X_MICROARCH.md: SIMD-32, wave64 VALU op over 2 cycles; 157.3 TF fp32
+# vector = 78.6 T FMA/s).  tools/probe/valu_probe measured 65 T v_add_f32 lane-ops/s.
+VALU_PEAK_CMPS = 256 * 4 * 32 * 2.4e9
+
+
+def dominance_run(dev, D, P, n, seed, steps, warmup):
+    """Dominance-bound companion measurement (SURVEY §7 'std-anti'): the reference
+    formula's 8D stream has ONE distinct skyline vector, so the pairwise phase is
+    priced on the labelled standard anti-correlated generator instead.  achieved =
+    D x W / (time of the dominance kernels), W = algorithmic pair tests over distinct
+    vectors (sky_profile_dominance)."""
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev.index or 0)
+    vals = torch.empty((n, D), dtype=torch.float64, device=dev)
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.synth_dev("std_anti", n, vals, ids, seed=seed)
+    out_ids = torch.empty(n, dtype=torch.int64, device=dev)
+    out_org = torch.empty(n, dtype=torch.int32, device=dev)
+    for _ in range(warmup):
+        eng.query_dev(ids, vals, out_ids, out_org, n)
+    eng.sync()
+    eng.profile(True)
+    eng.profile_reset()
+    t0 = time.perf_counter()
+    g = 0
+    for _ in range(steps):
+        g = eng.query_dev(ids, vals, out_ids, out_org, n)
+    eng.sync()
+    dt = (time.perf_counter() - t0) / steps
+    eng.profile(False)
+    w = eng.dominance_work()
+    dom_ms, dom_launches, _ = eng.kernel_time("dom")
+    phases, counters = eng.phases()
+    dom_ms /= steps
+    achieved = D * w / (dom_ms / 1e3) if dom_ms > 0 else 0.0
+    eng.close()
+    return {"bound": "valu", "kernel": "k_dom16 (+k_xcompact16), HIP events over every SFS round",
+            "workload": f"std_anti (labelled extension generator) {D}D, {n} tuples, MR-Angle P={P}",
+            "tuples_per_s": n / dt, "ms_per_query": dt * 1e3, "skyline_size": g,
+            "pair_tests_W": w, "compares": D * w, "dominance_ms": dom_ms,
+            "achieved": achieved, "peak": VALU_PEAK_CMPS, "unit": "compares/s",
+            "frac": achieved / VALU_PEAK_CMPS, "path": "u16" if int(counters[7]) & 4 else "f32/f64",
+            "local_sfs_ms": phases["local_sfs"], "global_sfs_ms": phases["global_sfs"],
+            "sfs_rounds": int(counters[5])}
 
 
 def cpu_baseline(d, P, dist_name, seed, sample, domain):
@@ -66,6 +110,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1242)
     ap.add_argument("--cpu-sample", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
+    ap.add_argument("--no-dominance", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +193,9 @@ def main():
                    "sample": f"first {args.cpu_sample} tuples of the same stream, oracle/ C restatement of the "
                              f"reference per-key BNL (buffer 5000) + single-threaded global BNL, "
                              f"{dt:.1f} s, skyline {gs}"}
+        domr = None
+        if world == 1 and not args.no_dominance:
+            domr = dominance_run(dev, D, P, args.dom_n, args.seed, 2, 1)
         line = {
             "metric": "skyline tuples/sec + p50 query latency, 8D anti-corr, 1/2/4/8 MI355X",
             "value": value,
@@ -174,6 +223,7 @@ def main():
                                    "distinct_reps": int(counters[2]), "global_candidates": int(counters[3]),
                                    "output": int(counters[4]), "sfs_rounds": int(counters[5])},
             "cpu_baseline": cpu,
+            "dominance_roofline": domr,
         }
         print(json.dumps(line), flush=True)
     if distributed:

@@ -77,7 +77,8 @@ static void store_stats(sky_ctx *c, const Pipe &p) {
     c->counters[4] = p.nout;
     c->counters[5] = p.sfs_rounds;
     c->counters[6] = p.sfs_pairs_upper;
-    c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0);
+    c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0) | (p.u16 ? 4 : 0);
+    c->dom_w = p.dom_w;
 }
 
 extern "C" {
@@ -609,6 +610,11 @@ int sky_profile_kernel(sky_ctx *c, const char *name, double *total_ms, int64_t *
     if (total_ms) *total_ms = it == c->kt.end() ? 0.0 : it->second.ms;
     if (launches) *launches = it == c->kt.end() ? 0 : it->second.launches;
     if (units) *units = it == c->kt.end() ? 0 : it->second.units;
+    return SKY_OK;
+}
+int sky_profile_dominance(sky_ctx *c, int64_t *work_out) {
+    ARG_CHECK(c && work_out, "null argument");
+    *work_out = c->dom_w;
     return SKY_OK;
 }
 int sky_profile_reset(sky_ctx *c) {

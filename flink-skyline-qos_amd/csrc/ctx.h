@@ -52,6 +52,7 @@ struct Ctx {
     PhaseTimer pt;
     double phase_ms[SKY_PHASES] = {};
     int64_t counters[8] = {};
+    int64_t dom_w = 0;          // algorithmic dominance pair tests of the last query
     std::map<std::string, KTime> kt;
     std::vector<hipEvent_t> event_pool;
     // staging for the host-buffer entry points

@@ -65,7 +65,7 @@ struct Pipe {
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers
     DevBuf r16, r16g, r16a, r16b, i16a, i16b, dead16, keep16, scan16, xbuf16, xcnt16, xseg16, items16, at16, atv16;
-    DevBuf scratch, flags, totals, orand, lsz, surv;
+    DevBuf scratch, flags, totals, orand, lsz, surv, segalive;
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;
@@ -78,6 +78,10 @@ struct Pipe {
     std::vector<int32_t> h_entries;
     std::vector<unsigned long long> h_lsz, h_surv;
     int64_t sfs_rounds = 0, sfs_pairs_upper = 0;
+    // algorithmic dominance work of the last run: distinct vectors per
+    // partition n_k, distinct local-skyline vectors s_k, W = pair tests
+    std::vector<uint32_t> h_seg_n, h_seg_s;
+    int64_t dom_w = 0;
 
     // pinned bump buffer for small host->device uploads (segment tables, tile lists):
     // asynchronous, no implicit synchronisation of the stream

@@ -301,7 +301,8 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     int flip = 0;
     std::vector<uint32_t> work;
     std::vector<SfsSeg> xseg;
-    std::vector<DomItem> tri, rest;
+    std::vector<DomItem> tri, tdiag, rest;
+    const uint32_t Ty = 64u * (uint32_t)dom16_ppt();     // y rows per work item
     std::vector<uint32_t> at;
     for (;;) {
         work.clear();
@@ -316,6 +317,7 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         }
         xseg.clear();
         tri.clear();
+        tdiag.clear();
         rest.clear();
         bool more = false;
         uint32_t maxch = 0;
@@ -331,31 +333,34 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
                 const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
                 if (cx * kDomTx >= xk) continue;
                 const uint32_t x0 = b + cx * kDomTx, nx = std::min(kDomTx, xk - cx * kDomTx);
-                for (uint32_t y = 0; y < xk; y += kDomTy) {
-                    const uint32_t y0 = b + y, ny = std::min(kDomTy, xk - y);
+                for (uint32_t y = 0; y < xk; y += Ty) {
+                    const uint32_t y0 = b + y, ny = std::min(Ty, xk - y);
                     if (x0 >= y0 + ny) continue;                 // every x after every y
-                    tri.push_back(DomItem{s, y0, ny, x0, nx, x0 + nx > y0 ? kDomDiag : 0u});
+                    if (x0 + nx > y0) tdiag.push_back(DomItem{s, y0, ny, x0, nx, kDomDiag});
+                    else tri.push_back(DomItem{s, y0, ny, x0, nx, 0u});
                     p.sfs_pairs_upper += (int64_t)ny * nx;
                 }
-                for (uint32_t y = xk; y < cnt[k]; y += kDomTy) {
-                    const uint32_t ny = std::min(kDomTy, cnt[k] - y);
+                for (uint32_t y = xk; y < cnt[k]; y += Ty) {
+                    const uint32_t ny = std::min(Ty, cnt[k] - y);
                     rest.push_back(DomItem{s, b + y, ny, cx * kDomTx, nx, kDomRest});
                     p.sfs_pairs_upper += (int64_t)ny * nx;
                 }
             }
         HIP_TRY(hipMemsetAsync(p.dead16.p, 0, (size_t)npos * 4, st));
-        SKY_TRY(p.items16.ensure((tri.size() + rest.size()) * sizeof(DomItem)));
-        SKY_TRY(p.upload(p.items16.p, tri.data(), tri.size() * sizeof(DomItem), st));
-        if (!rest.empty())
-            SKY_TRY(p.upload(p.items16.as<DomItem>() + tri.size(), rest.data(), rest.size() * sizeof(DomItem), st));
+        const size_t nt = tri.size(), nd = tdiag.size(), nr = rest.size();
+        SKY_TRY(p.items16.ensure((nt + nd + nr) * sizeof(DomItem)));
+        DomItem *di = p.items16.as<DomItem>();
+        if (nt) SKY_TRY(p.upload(di, tri.data(), nt * sizeof(DomItem), st));
+        if (nd) SKY_TRY(p.upload(di + nt, tdiag.data(), nd * sizeof(DomItem), st));
+        if (nr) SKY_TRY(p.upload(di + nt + nd, rest.data(), nr * sizeof(DomItem), st));
         SKY_TRY(p.upload(p.xseg16.p, xseg.data(), xseg.size() * sizeof(SfsSeg), st));
         c.ktimer_begin("dom", st);
-        launch_dom16(W, cur_rows, nullptr, nullptr, p.items16.as<DomItem>(), (uint32_t)tri.size(), 0,
-                     p.dead16.as<uint32_t>(), st);
+        launch_dom16(W, false, cur_rows, nullptr, nullptr, di, (uint32_t)nt, 0, p.dead16.as<uint32_t>(), st);
+        launch_dom16(W, true, cur_rows, nullptr, nullptr, di + nt, (uint32_t)nd, 0, p.dead16.as<uint32_t>(), st);
         launch_xcompact16(W, cur_rows, cur_idx, p.xseg16.as<SfsSeg>(), (uint32_t)work.size(), B,
                           p.dead16.as<uint32_t>(), p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), alive, st);
-        launch_dom16(W, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(),
-                     p.items16.as<DomItem>() + tri.size(), (uint32_t)rest.size(), B, p.dead16.as<uint32_t>(), st);
+        launch_dom16(W, false, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), di + nt + nd,
+                     (uint32_t)nr, B, p.dead16.as<uint32_t>(), st);
         c.ktimer_end("dom", st, 0);
         STAGE(st, "dom16");
         if (!more) break;
@@ -418,6 +423,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
     p.sfs_rounds = p.sfs_pairs_upper = 0;
+    p.h_seg_n.clear();
+    p.h_seg_s.clear();
     p.h_lsz.assign(p.K, 0);
     p.h_surv.assign(p.K, 0);
     const uint32_t tiles = (n + kTile - 1) / kTile;
@@ -616,6 +623,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             SKY_TRY(sfs_run(c, p, p.rep_rows.p, p.rep_key.as<uint64_t>(), mr, sb, se, false,
                             p.alive_l.as<uint8_t>()));
         }
+        SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+        HIP_TRY(hipMemsetAsync(p.segalive.p, 0, (size_t)p.Kp * 4, st));
+        launch_seg_alive(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), mr, p.segalive.as<uint32_t>(), st);
+        p.h_seg_n.assign(se.begin(), se.end());
         if (tm) tm->mark(6, st);
 
         // ---- global merge over the union of the local skylines
@@ -694,8 +705,21 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     STAGE(st, "fate");
     uint32_t nout = 0;
     std::vector<unsigned long long> sh_l((size_t)kStatShards * p.K), sh_s((size_t)kStatShards * p.K);
-    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, stat_bytes}, {p.surv.p, stat_bytes}},
-                      {&nout, sh_l.data(), sh_s.data()}));
+    const bool have_seg = mt && !p.h_seg_n.empty();
+    p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
+    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, stat_bytes}, {p.surv.p, stat_bytes},
+                              {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}},
+                      {&nout, sh_l.data(), sh_s.data(), p.h_seg_s.data()}));
+    p.dom_w = 0;
+    if (have_seg) {
+        int64_t sg = 0;
+        for (int k = 0; k < p.Kp; k++) {
+            const int64_t nk = p.h_seg_n[k], sk = p.h_seg_s[k];
+            p.dom_w += sk * (sk - 1) / 2 + (nk - sk);
+            sg += sk;
+        }
+        if (in.global && !in.single) p.dom_w += sg * (sg - 1) / 2;
+    }
     for (int sh = 0; sh < kStatShards; sh++)
         for (int k = 0; k < p.K; k++) {
             p.h_lsz[k] += sh_l[(size_t)sh * p.K + k];

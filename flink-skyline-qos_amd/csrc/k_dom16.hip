@@ -21,6 +21,8 @@
 //   keep = !dead -> exclusive scan -> k_move16 (next round's layout)
 // Work items are (segment, 64*PPT y, <= kDomTx x) tiles, one wave each; a tile
 // whose y are all dead skips its remaining x.
+#include <cstdlib>
+
 #include "sky_internal.h"
 
 namespace sky {
@@ -77,41 +79,68 @@ __device__ __forceinline__ void dom_row(const uint32_t (&x)[W], int32_t t0, cons
     }
 }
 
-template <int W, int PPT, bool DIAG>
+// x row vs every lane's PPT rows, VALU only: acc[p] = min over x of OR_w sat(x_w - y_w),
+// so y is dominated iff acc[p] == 0 (no VALU -> SGPR -> SALU dependency per pair)
+template <int W, int PPT>
+__device__ __forceinline__ void dom_row_acc(const uint32_t (&x)[W], const uint32_t (&y)[PPT][W],
+                                            uint32_t (&acc)[PPT]) {
+#pragma unroll
+    for (int p = 0; p < PPT; p++) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) r |= satsub_u16x2(x[w], y[p][w]);
+        acc[p] = acc[p] < r ? acc[p] : r;
+    }
+}
+
+template <int W, int PPT, int R, bool DIAG>
 __device__ __forceinline__ void dom_scan(const uint32_t *__restrict__ xs, uint32_t nx, int32_t tbase,
                                          const uint32_t (&y)[PPT][W], uint64_t (&dom)[PPT]) {
+    uint32_t acc[PPT];
+#pragma unroll
+    for (int p = 0; p < PPT; p++) acc[p] = 0xffffffffu;
     for (uint32_t i = 0; i < nx;) {
         const uint32_t cn = nx - i < 16u ? nx - i : 16u;
-        const uint32_t n4 = cn & ~3u;
-        for (uint32_t r = 0; r < n4; r += 4) {
-            uint32_t x[4][W];
+        const uint32_t nr = cn - cn % R;
+        for (uint32_t r = 0; r < nr; r += R) {
+            uint32_t x[R][W];
 #pragma unroll
-            for (int q = 0; q < 4; q++)
+            for (int q = 0; q < R; q++)
 #pragma unroll
                 for (int w = 0; w < W; w++) x[q][w] = xs[(size_t)(i + r + q) * W + w];
 #pragma unroll
-            for (int q = 0; q < 4; q++) dom_row<W, PPT, DIAG>(x[q], tbase + (int32_t)(i + r + q), y, dom);
+            for (int q = 0; q < R; q++) {
+                if constexpr (DIAG) dom_row<W, PPT, true>(x[q], tbase + (int32_t)(i + r + q), y, dom);
+                else dom_row_acc<W, PPT>(x[q], y, acc);
+            }
         }
-        for (uint32_t r = n4; r < cn; r++) {
+        for (uint32_t r = nr; r < cn; r++) {
             uint32_t x[W];
 #pragma unroll
             for (int w = 0; w < W; w++) x[w] = xs[(size_t)(i + r) * W + w];
-            dom_row<W, PPT, DIAG>(x, tbase + (int32_t)(i + r), y, dom);
+            if constexpr (DIAG) dom_row<W, PPT, true>(x, tbase + (int32_t)(i + r), y, dom);
+            else dom_row_acc<W, PPT>(x, y, acc);
         }
         i += cn;
         uint64_t all = ~0ull;
 #pragma unroll
-        for (int p = 0; p < PPT; p++) all &= dom[p];
+        for (int p = 0; p < PPT; p++) {
+            if constexpr (!DIAG) dom[p] |= __ballot(acc[p] == 0u);
+            all &= dom[p];
+        }
         if (all == ~0ull) break;
     }
 }
 
-template <int W, int PPT>
-__global__ __launch_bounds__(64) void k_dom16(const uint32_t *__restrict__ rows, const uint32_t *__restrict__ xbuf,
-                                              const uint32_t *__restrict__ xcnt, const DomItem *__restrict__ items,
-                                              uint32_t xcap, uint32_t *__restrict__ dead) {
-    const DomItem it = items[blockIdx.x];
-    const int lane = threadIdx.x;
+template <int W, int PPT, int R, bool DIAG>
+__global__ __launch_bounds__(256, 8) void k_dom16(const uint32_t *__restrict__ rows, const uint32_t *__restrict__ xbuf,
+                                               const uint32_t *__restrict__ xcnt, const DomItem *__restrict__ items,
+                                               uint32_t nitems, uint32_t xcap, uint32_t *__restrict__ dead) {
+    // one work item per wave (4 per workgroup): waves never synchronise
+    const uint32_t wi = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wi >= nitems) return;
+    const DomItem it = items[wi];
+    const int lane = threadIdx.x & 63;
     const uint32_t *xs;
     uint32_t nx = it.nx;
     if (it.flags & kDomRest) {
@@ -146,8 +175,7 @@ __global__ __launch_bounds__(64) void k_dom16(const uint32_t *__restrict__ rows,
         }
     }
     if (all == ~0ull) return;
-    if (it.flags & kDomDiag) dom_scan<W, PPT, true>(xs, nx, (int32_t)(it.x0 - it.y0), y, dom);
-    else dom_scan<W, PPT, false>(xs, nx, 0, y, dom);
+    dom_scan<W, PPT, R, DIAG>(xs, nx, (int32_t)(it.x0 - it.y0), y, dom);
 #pragma unroll
     for (int p = 0; p < PPT; p++) {
         const uint32_t q = (uint32_t)(p * 64 + lane);
@@ -236,11 +264,46 @@ void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, ui
     else { SKY_DISPATCH_D(D, (k_pack16<DD, 8><<<nb16(m), kThreads, 0, st>>>(rows, m, idx, out))); }
 }
 
-void launch_dom16(int W, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
-                  uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
+// SKY_DOM_PPT in {4, 8, 16} (y rows per lane), SKY_DOM_R in {2, 4} (x rows per
+// scalar-load batch): tuning knobs, defaults measured on the MI355X
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+int dom16_ppt() {
+    static int v = [] {
+        const int p = env_int("SKY_DOM_PPT", 4);
+        return (p == 8 || p == 16) ? p : 4;
+    }();
+    return v;
+}
+static int dom16_r() {
+    static int v = env_int("SKY_DOM_R", 4) == 2 ? 2 : 4;
+    return v;
+}
+
+template <int W, int PPT, int R>
+static void dom16_t(bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
+                    const DomItem *items, uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
+    const unsigned g = (nitems + 3) / 4;
+    if (diag) k_dom16<W, PPT, R, true><<<g, 256, 0, st>>>(rows, xbuf, xcnt, items, nitems, xcap, dead);
+    else k_dom16<W, PPT, R, false><<<g, 256, 0, st>>>(rows, xbuf, xcnt, items, nitems, xcap, dead);
+}
+template <int W>
+static void dom16_w(bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
+                    const DomItem *items, uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
+    const int ppt = dom16_ppt(), r = dom16_r();
+#define DOM16_CASE(P_, R_) \
+    if (ppt == P_ && r == R_) { dom16_t<W, P_, R_>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st); return; }
+    DOM16_CASE(4, 2) DOM16_CASE(4, 4) DOM16_CASE(8, 2) DOM16_CASE(8, 4) DOM16_CASE(16, 2) DOM16_CASE(16, 4)
+#undef DOM16_CASE
+}
+
+void launch_dom16(int W, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
+                  const DomItem *items, uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
     if (!nitems) return;
-    if (W == 4) k_dom16<4, kDomPPT><<<nitems, 64, 0, st>>>(rows, xbuf, xcnt, items, xcap, dead);
-    else k_dom16<8, kDomPPT><<<nitems, 64, 0, st>>>(rows, xbuf, xcnt, items, xcap, dead);
+    if (W == 4) dom16_w<4>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
+    else dom16_w<8>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
 }
 
 void launch_xcompact16(int W, const uint32_t *rows, const uint32_t *idx, const SfsSeg *xseg, uint32_t nslots,

@@ -311,6 +311,8 @@ __global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__rest
                                                           const uint32_t *__restrict__ alive_scan, uint32_t mr,
                                                           uint64_t *__restrict__ gkey, uint32_t *__restrict__ gval,
                                                           unsigned long long *__restrict__ orand) {
+    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
+    __shared__ int s_any[kThreads / 64];
     const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
     uint64_t o = 0, an = ~0ull;
     const bool any = __ballot(r < mr && alive_l[r]) != 0ull;
@@ -327,9 +329,18 @@ __global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__rest
         o |= __shfl_xor(o, s, 64);
         an &= __shfl_xor(an, s, 64);
     }
-    if ((threadIdx.x & 63) == 0 && any) {
-        atomicOr(&orand[0], (unsigned long long)o);
-        atomicAnd(&orand[1], (unsigned long long)an);
+    // one pair of global atomics per workgroup (per-wave atomics on one address serialise)
+    if ((threadIdx.x & 63) == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; s_any[threadIdx.x >> 6] = any; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bo = 0, ba = ~0ull;
+        int has = 0;
+        for (int q = 0; q < kThreads / 64; q++)
+            if (s_any[q]) { bo |= s_o[q]; ba &= s_a[q]; has = 1; }
+        if (has) {
+            atomicOr(&orand[0], bo);
+            atomicAnd(&orand[1], ba);
+        }
     }
 }
 
@@ -371,6 +382,38 @@ __global__ __launch_bounds__(kThreads) void k_u8_to_u32(const uint8_t *__restric
                                                         uint32_t *__restrict__ out) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j < n) out[j] = in[j] ? 1u : 0u;
+}
+
+// distinct local-skyline vectors per partition (for the algorithmic work count W)
+__global__ __launch_bounds__(kThreads) void k_seg_alive(const uint64_t *__restrict__ rep_key,
+                                                        const uint8_t *__restrict__ alive, uint32_t mr,
+                                                        uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t s_c[kMaxK];
+    for (int q = threadIdx.x; q < kMaxK; q += kThreads) s_c[q] = 0;
+    __syncthreads();
+    for (uint32_t r = blockIdx.x * kThreads + threadIdx.x; r < mr; r += gridDim.x * kThreads) {
+        const bool a = alive[r] != 0;
+        const uint32_t k = a ? (uint32_t)(rep_key[r] >> 56) : 0u;
+        // reps are sorted by partition: a wave is nearly always one partition
+        const uint64_t am = __ballot(a);
+        if (!am) continue;
+        const uint32_t k0 = __shfl(k, __ffsll((unsigned long long)am) - 1, 64);
+        if (__ballot(a && k != k0) == 0ull) {
+            if ((threadIdx.x & 63) == __ffsll((unsigned long long)am) - 1) atomicAdd(&s_c[k0], (uint32_t)__popcll(am));
+        } else if (a) {
+            atomicAdd(&s_c[k], 1u);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < kMaxK; q += kThreads)
+        if (s_c[q]) atomicAdd(&cnt[q], s_c[q]);
+}
+
+void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st) {
+    if (!mr) return;
+    unsigned g = (mr + kThreads - 1) / kThreads;
+    if (g > 1024) g = 1024;
+    k_seg_alive<<<g, kThreads, 0, st>>>(rep_key, alive, mr, cnt);
 }
 
 // ---- launchers ------------------------------------------------------------------

@@ -171,18 +171,18 @@ void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, u
                         hipStream_t st);
 void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t mg, uint8_t *alive_g,
                           hipStream_t st);
+void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st);
 void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
 
 // ---- k_dom16.hip (integer-valued rows packed as u16 pairs) ----
 struct DomItem { uint32_t seg, y0, ny, x0, nx, flags; };
 constexpr uint32_t kDomDiag = 1u;             // x and y ranges overlap: only x before y
 constexpr uint32_t kDomRest = 2u;             // x from xbuf[seg] (X'), count from xcnt[seg]
-constexpr int kDomPPT = 8;                    // y rows per lane
-constexpr uint32_t kDomTy = 64u * kDomPPT;    // y rows per work item (one wave)
+int dom16_ppt();                              // y rows per lane (work item = 64 * ppt y rows)
 constexpr uint32_t kDomTx = 1024u;            // x rows per work item
 int dom16_words(int D);
 void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, uint32_t *out, hipStream_t st);
-void launch_dom16(int W, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
+void launch_dom16(int W, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
                   uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st);
 void launch_xcompact16(int W, const uint32_t *rows, const uint32_t *idx, const SfsSeg *xseg, uint32_t nslots,
                        uint32_t xcap, uint32_t *dead, uint32_t *xbuf, uint32_t *xcnt, uint8_t *alive, hipStream_t st);

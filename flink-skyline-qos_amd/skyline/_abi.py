@@ -73,6 +73,7 @@ SIGNATURES = {
     "sky_profile_enable": [c_p, c_int],
     "sky_profile_phases": [c_p, c_p, c_p],
     "sky_profile_kernel": [c_p, ctypes.c_char_p, P_dbl, P_i64, P_i64],
+    "sky_profile_dominance": [c_p, P_i64],
     "sky_profile_reset": [c_p],
     "sky_last_error": [],
     "sky_version": [],

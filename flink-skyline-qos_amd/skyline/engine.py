@@ -152,6 +152,12 @@ class SkylineEngine:
         check(lib().sky_profile_phases(self.h, _ptr(ms), _ptr(cnt)))
         return dict(zip(_abi.PHASES, ms.tolist())), cnt
 
+    def dominance_work(self):
+        """Algorithmic pair tests (distinct vectors) of the last query."""
+        w = ctypes.c_int64(0)
+        check(lib().sky_profile_dominance(self.h, ctypes.byref(w)))
+        return w.value
+
     def kernel_time(self, name):
         ms = ctypes.c_double(0)
         la = ctypes.c_int64(0)

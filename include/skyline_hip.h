@@ -154,6 +154,11 @@ int sky_profile_enable(sky_ctx *ctx, int on);
 int sky_profile_phases(sky_ctx *ctx, double *ms_out /* SKY_PHASES */, int64_t *counters_out /* 8 */);
 int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
                        int64_t *units);
+/* algorithmic dominance work of the last query, in pair tests over distinct vectors
+ * (SURVEY.md §8d): W = sum_k [s_k(s_k-1)/2 + (n_k - s_k)] + s_G(s_G-1)/2, with n_k / s_k
+ * the distinct vectors / distinct local-skyline vectors of partition k and s_G the
+ * distinct union of the local skylines; D compares per pair test */
+int sky_profile_dominance(sky_ctx *ctx, int64_t *work_out);
 int sky_profile_reset(sky_ctx *ctx);
 
 #ifdef __cplusplus

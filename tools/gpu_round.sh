@@ -23,8 +23,13 @@ fi
 if [[ $STEPS == *trace* ]]; then
   export TMPDIR=/tmp
   rm -rf $OUT/trace_$TAG
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$TAG -o run -- python3 -u $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/trace_$TAG.log 2>&1 || { tail -30 $OUT/trace_$TAG.log; exit 1; }
+  # C4 alone (the bench line's k_filter), then the dominance-bound companion alone
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$TAG -o run -- python3 -u $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-dominance ${BENCH_ARGS} > $OUT/trace_$TAG.log 2>&1 || { tail -30 $OUT/trace_$TAG.log; exit 1; }
   grep '^{' $OUT/trace_$TAG.log > $OUT/bench_trace_$TAG.json || true
   python tools/prof_summary.py trace $OUT/trace_$TAG > $OUT/trace_${TAG}_summary.txt
   head -25 $OUT/trace_${TAG}_summary.txt
+  rm -rf $OUT/trace_dom_$TAG
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_dom_$TAG -o run -- python3 -u $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-dominance --dist std_anti --n 2000000 > $OUT/trace_dom_$TAG.log 2>&1 || { tail -30 $OUT/trace_dom_$TAG.log; exit 1; }
+  python tools/prof_summary.py trace $OUT/trace_dom_$TAG > $OUT/trace_dom_${TAG}_summary.txt
+  head -12 $OUT/trace_dom_${TAG}_summary.txt
 fi
