@@ -517,7 +517,7 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
         OutArgs oa{};
         oa.status = p.status.as<uint16_t>();
         oa.n = p.n;
-        oa.blk_off = p.blk_off.as<uint32_t>();
+        oa.slot_of = p.slot_of.as<uint32_t>();
         oa.slot_fate = p.slot_fate.as<uint8_t>();
         oa.pruner_fate = p.pruner_fate.as<uint8_t>();
         oa.M = p.M;

@@ -51,7 +51,7 @@ struct PhaseTimer;
 // multi-GPU import can run on the union while the local shard's state is kept).
 struct Pipe {
     // per tuple / per tile
-    DevBuf status, blk_cnt, blk_off, out_cnt, out_off;
+    DevBuf status, slot_of, out_cnt, out_off;
     // pruners
     DevBuf pmin, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     // candidates (slot order) and sort
@@ -65,7 +65,7 @@ struct Pipe {
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers
     DevBuf r16, r16g, r16a, r16b, i16a, i16b, dead16, keep16, scan16, xbuf16, xcnt16, xseg16, items16, at16, atv16;
-    DevBuf scratch, flags, totals, orand, lsz, surv, segalive;
+    DevBuf scratch, flags, totals, orand, lsz, surv, statk, segalive;
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;

@@ -277,9 +277,11 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     hipStream_t st = c.st;
     const uint32_t nseg = (uint32_t)begin.size();
     if (nrep == 0 || nseg == 0) return SKY_OK;
-    uint32_t maxc = 0;
-    for (uint32_t k = 0; k < nseg; k++) maxc = std::max(maxc, cnt[k]);
-    const uint32_t B = maxc > 65536 ? 16384u : 4096u;     // X per round
+    // X per round: start small (few-skyline streams die in the first round's rest
+    // filter); double while most of the rest survives a round (large skylines)
+    constexpr uint32_t kBmax = 16384u;
+    uint32_t B = 2048u;
+    uint64_t rest_before = 0;
     const size_t rowb = (size_t)W * 4;
     SKY_TRY(p.dead16.ensure((size_t)nrep * 4));
     SKY_TRY(p.keep16.ensure(((size_t)nrep + 1) * 4));
@@ -288,7 +290,7 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     SKY_TRY(p.r16b.ensure((size_t)nrep * rowb));
     SKY_TRY(p.i16a.ensure((size_t)nrep * 4));
     SKY_TRY(p.i16b.ensure((size_t)nrep * 4));
-    SKY_TRY(p.xbuf16.ensure((size_t)nseg * B * rowb));
+    SKY_TRY(p.xbuf16.ensure((size_t)nseg * kBmax * rowb));
     SKY_TRY(p.xcnt16.ensure((size_t)nseg * 4));
     SKY_TRY(p.xseg16.ensure((size_t)nseg * sizeof(SfsSeg)));
     SKY_TRY(p.at16.ensure((size_t)nseg * 8));
@@ -302,7 +304,9 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     std::vector<uint32_t> work;
     std::vector<SfsSeg> xseg;
     std::vector<DomItem> tri, tdiag, rest;
-    const uint32_t Ty = 64u * (uint32_t)dom16_ppt();     // y rows per work item
+    const int ppt = dom16_ppt();
+    const uint32_t Ty = 64u * (uint32_t)ppt;              // y rows per rest work item
+    const uint32_t Tt = 64u * (uint32_t)kDomTriPPT;       // y rows per tri work item
     std::vector<uint32_t> at;
     for (;;) {
         work.clear();
@@ -321,6 +325,8 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         rest.clear();
         bool more = false;
         uint32_t maxch = 0;
+        rest_before = 0;
+        for (uint32_t k : work) rest_before += cnt[k] - std::min(B, cnt[k]);
         for (uint32_t s = 0; s < (uint32_t)work.size(); s++) {
             const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
             xseg.push_back(SfsSeg{b, xk});
@@ -333,8 +339,8 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
                 const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
                 if (cx * kDomTx >= xk) continue;
                 const uint32_t x0 = b + cx * kDomTx, nx = std::min(kDomTx, xk - cx * kDomTx);
-                for (uint32_t y = 0; y < xk; y += Ty) {
-                    const uint32_t y0 = b + y, ny = std::min(Ty, xk - y);
+                for (uint32_t y = 0; y < xk; y += Tt) {
+                    const uint32_t y0 = b + y, ny = std::min(Tt, xk - y);
                     if (x0 >= y0 + ny) continue;                 // every x after every y
                     if (x0 + nx > y0) tdiag.push_back(DomItem{s, y0, ny, x0, nx, kDomDiag});
                     else tri.push_back(DomItem{s, y0, ny, x0, nx, 0u});
@@ -347,7 +353,19 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
                 }
             }
         HIP_TRY(hipMemsetAsync(p.dead16.p, 0, (size_t)npos * 4, st));
+        // each list is ordered by x chunk; the chunk-0 items go in a launch of their own
+        // so that later chunks start after the most dominating rows have marked their y
+        auto first_chunk_end = [&](const std::vector<DomItem> &v, bool rest_list) {
+            size_t c = 0;
+            for (; c < v.size(); c++) {
+                const uint32_t off = rest_list ? v[c].x0 : v[c].x0 - xseg[v[c].seg].begin;
+                if (off >= kDomTx) break;
+            }
+            return c;
+        };
         const size_t nt = tri.size(), nd = tdiag.size(), nr = rest.size();
+        const size_t nt0 = first_chunk_end(tri, false), nd0 = first_chunk_end(tdiag, false);
+        const size_t nr0 = first_chunk_end(rest, true);
         SKY_TRY(p.items16.ensure((nt + nd + nr) * sizeof(DomItem)));
         DomItem *di = p.items16.as<DomItem>();
         if (nt) SKY_TRY(p.upload(di, tri.data(), nt * sizeof(DomItem), st));
@@ -355,12 +373,20 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         if (nr) SKY_TRY(p.upload(di + nt + nd, rest.data(), nr * sizeof(DomItem), st));
         SKY_TRY(p.upload(p.xseg16.p, xseg.data(), xseg.size() * sizeof(SfsSeg), st));
         c.ktimer_begin("dom", st);
-        launch_dom16(W, false, cur_rows, nullptr, nullptr, di, (uint32_t)nt, 0, p.dead16.as<uint32_t>(), st);
-        launch_dom16(W, true, cur_rows, nullptr, nullptr, di + nt, (uint32_t)nd, 0, p.dead16.as<uint32_t>(), st);
+        // tri: the chunk-0 tiles (plain, diagonal), then the later chunks
+        uint32_t *dd = p.dead16.as<uint32_t>();
+        const int tp = kDomTriPPT;
+        launch_dom16(W, tp, false, cur_rows, nullptr, nullptr, di, (uint32_t)nt0, 0, dd, st);
+        launch_dom16(W, tp, true, cur_rows, nullptr, nullptr, di + nt, (uint32_t)nd0, 0, dd, st);
+        launch_dom16(W, tp, false, cur_rows, nullptr, nullptr, di + nt0, (uint32_t)(nt - nt0), 0, dd, st);
+        launch_dom16(W, tp, true, cur_rows, nullptr, nullptr, di + nt + nd0, (uint32_t)(nd - nd0), 0, dd, st);
         launch_xcompact16(W, cur_rows, cur_idx, p.xseg16.as<SfsSeg>(), (uint32_t)work.size(), B,
                           p.dead16.as<uint32_t>(), p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), alive, st);
-        launch_dom16(W, false, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), di + nt + nd,
-                     (uint32_t)nr, B, p.dead16.as<uint32_t>(), st);
+        DomItem *dr = di + nt + nd;
+        launch_dom16(W, ppt, false, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), dr, (uint32_t)nr0, B,
+                     p.dead16.as<uint32_t>(), st);
+        launch_dom16(W, ppt, false, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), dr + nr0,
+                     (uint32_t)(nr - nr0), B, p.dead16.as<uint32_t>(), st);
         c.ktimer_end("dom", st, 0);
         STAGE(st, "dom16");
         if (!more) break;
@@ -381,11 +407,14 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         SKY_TRY(sync_read(p, st, {{p.atv16.p, at.size() * 4}}, {atv.data()}));
         std::fill(cnt.begin(), cnt.end(), 0u);
         npos = 0;
+        uint64_t rest_after = 0;
         for (size_t s = 0; s < work.size(); s++) {
             begin[work[s]] = atv[2 * s];
             cnt[work[s]] = atv[2 * s + 1] - atv[2 * s];
             npos = std::max(npos, atv[2 * s + 1]);
+            rest_after += cnt[work[s]];
         }
+        if (rest_after * 2 > rest_before) B = std::min(kBmax, B * 2);
         cur_rows = nrows;
         cur_idx = nidx;
         flip ^= 1;
@@ -450,14 +479,27 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
-    // ---- the HBM stream: keys + pruner test + status
+    // ---- the HBM stream: keys + pruner test + status, candidates appended to slots
+    //      (f64 rows + sort keys); the row type (f32/f64), the OR/AND of the sort keys
+    //      and the slot count are read back in ONE synchronisation
+    const int KM = p.Kp * p.M;
+    const size_t rb64 = row_bytes(true, D);
+    const size_t cap = (size_t)n + KM;
     SKY_TRY(p.status.ensure((size_t)n * 2));
-    SKY_TRY(p.blk_cnt.ensure((size_t)tiles * 4));
-    SKY_TRY(p.blk_off.ensure((size_t)tiles * 4));
-    SKY_TRY(p.dup_cnt.ensure((size_t)p.Kp * p.M * 4));
-    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
-    HIP_TRY(hipMemsetAsync(p.dup_cnt.p, 0, (size_t)p.Kp * p.M * 4, st));
+    SKY_TRY(p.slot_of.ensure((size_t)n * 4));
+    SKY_TRY(p.rows.ensure(cap * rb64));
+    SKY_TRY(p.sortkey.ensure(cap * 8));
+    SKY_TRY(p.slot_src.ensure(cap * 4));
+    SKY_TRY(p.tile_orand.ensure((size_t)tiles * 16));
+    SKY_TRY(p.dup_cnt.ensure((size_t)KM * 4));
+    SKY_TRY(p.pr_entries.ensure((size_t)KM * 4));
+    SKY_TRY(p.pruner_slot.ensure((size_t)KM * 4));
+    SKY_TRY(p.orand.ensure(16));
+    HIP_TRY(hipMemsetAsync(p.dup_cnt.p, 0, (size_t)KM * 4, st));
     HIP_TRY(hipMemsetAsync(p.flags.p, 0, 64, st));
+    HIP_TRY(hipMemsetAsync(p.totals.p, 0, 64, st));
+    HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
+    HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
     FilterArgs fa{};
     fa.vals = in.vals;
     fa.n = n;
@@ -469,7 +511,13 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.M = p.M;
     fa.Kp = p.Kp;
     fa.status = p.status.as<uint16_t>();
-    fa.blk_cnt = p.blk_cnt.as<uint32_t>();
+    fa.crow = p.rows.as<double>();
+    fa.sortkey = p.sortkey.as<uint64_t>();
+    fa.slot_src = p.slot_src.as<uint32_t>();
+    fa.slot_of = p.slot_of.as<uint32_t>();
+    fa.m_total = p.totals.as<uint32_t>();
+    fa.tile_orand = p.tile_orand.as<unsigned long long>();
+    fa.orand = p.orand.as<unsigned long long>();
     fa.dup_cnt = p.dup_cnt.as<uint32_t>();
     fa.flags = p.flags.as<uint32_t>();
     const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;
@@ -477,44 +525,16 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.defer.ensure((size_t)n * 4));
         fa.defer_list = p.defer.as<uint32_t>();
         fa.defer_cnt = p.totals.as<uint32_t>() + 6;
-        HIP_TRY(hipMemsetAsync(fa.defer_cnt, 0, 4, st));
     }
     c.ktimer_begin("filter", st);
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
     if (angle_keys) launch_filter_deferred(D, fa, st);
+    launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
     STAGE(st, "filter");
-    scan_excl_u32(p.blk_cnt.as<uint32_t>(), p.blk_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>(),
-                  p.scratch.as<uint32_t>(), st);
     if (tm) tm->mark(2, st);
 
-    // ---- compaction into candidate slots + one slot per duplicated pruner; the row
-    //      type (f32/f64), the OR/AND of the sort keys and the slot count are all
-    //      produced on the device and read back in ONE synchronisation
-    const int KM = p.Kp * p.M;
-    const size_t rb64 = row_bytes(true, D);
-    const size_t cap = (size_t)n + KM;
-    SKY_TRY(p.rows.ensure(cap * rb64));
-    SKY_TRY(p.sortkey.ensure(cap * 8));
-    SKY_TRY(p.slot_src.ensure(cap * 4));
-    SKY_TRY(p.pr_entries.ensure((size_t)KM * 4));
-    SKY_TRY(p.pruner_slot.ensure((size_t)KM * 4));
-    SKY_TRY(p.orand.ensure(16));
-    HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
-        HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
-    CompactArgs ca{};
-    ca.vals = in.vals;
-    ca.n = n;
-    ca.status = p.status.as<uint16_t>();
-    ca.blk_off = p.blk_off.as<uint32_t>();
-    ca.rows = p.rows.p;
-    ca.sortkey = p.sortkey.as<uint64_t>();
-    ca.slot_src = p.slot_src.as<uint32_t>();
-    ca.flags = p.flags.as<uint32_t>();
-    SKY_TRY(p.tile_orand.ensure((size_t)tiles * 16));
-    ca.tile_orand = p.tile_orand.as<unsigned long long>();
-    launch_compact(D, ca, st);
-    launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
+    // ---- one slot per duplicated pruner (device-side, no host round trip)
     AppendArgs aa{};
     aa.pruners = p.pruners.as<double>();
     aa.dup_cnt = p.dup_cnt.as<uint32_t>();
@@ -660,7 +680,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 // computed keys: a vector has one partition, so the union of the
                 // partitions' representatives is duplicate-free and the distinct-row
                 // test applies; given keys (lists of a merge) may repeat a vector
-                if (p.u16 && !in.keys) {
+                if (p.u16 && !in.keys && mg > 2048) {     // small unions: one k_sfs_small launch
                     SKY_TRY(p.r16g.ensure((size_t)mg * W16 * 4));
                     launch_pack16(D, p.rep_rows.as<float>(), mg, gv, p.r16g.as<uint32_t>(), st);
                     SKY_TRY(sfs_run16(c, p, p.r16g.as<uint32_t>(), mg, {0u}, {mg}, p.galive.as<uint8_t>(), W16));
@@ -685,7 +705,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = n;
-    oa.blk_off = p.blk_off.as<uint32_t>();
+    oa.slot_of = p.slot_of.as<uint32_t>();
     oa.slot_fate = p.slot_fate.as<uint8_t>();
     oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;
@@ -704,12 +724,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     c.ktimer_end("out", st, n);
     STAGE(st, "fate");
     uint32_t nout = 0;
-    std::vector<unsigned long long> sh_l((size_t)kStatShards * p.K), sh_s((size_t)kStatShards * p.K);
+    SKY_TRY(p.statk.ensure((size_t)p.K * 16));
+    launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
+                       p.statk.as<unsigned long long>(), st);
+    std::vector<unsigned long long> sk2((size_t)p.K * 2);
     const bool have_seg = mt && !p.h_seg_n.empty();
     p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
-    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.lsz.p, stat_bytes}, {p.surv.p, stat_bytes},
+    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
                               {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}},
-                      {&nout, sh_l.data(), sh_s.data(), p.h_seg_s.data()}));
+                      {&nout, sk2.data(), p.h_seg_s.data()}));
     p.dom_w = 0;
     if (have_seg) {
         int64_t sg = 0;
@@ -720,11 +743,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         }
         if (in.global && !in.single) p.dom_w += sg * (sg - 1) / 2;
     }
-    for (int sh = 0; sh < kStatShards; sh++)
-        for (int k = 0; k < p.K; k++) {
-            p.h_lsz[k] += sh_l[(size_t)sh * p.K + k];
-            p.h_surv[k] += sh_s[(size_t)sh * p.K + k];
-        }
+    for (int k = 0; k < p.K; k++) {
+        p.h_lsz[k] = sk2[k];
+        p.h_surv[k] = sk2[(size_t)p.K + k];
+    }
     p.nout = nout;
     if (tm) tm->mark(8, st);
     return SKY_OK;
@@ -742,7 +764,7 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = p.n;
-    oa.blk_off = p.blk_off.as<uint32_t>();
+    oa.slot_of = p.slot_of.as<uint32_t>();
     oa.slot_fate = p.slot_fate.as<uint8_t>();
     oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;

@@ -93,42 +93,59 @@ __device__ __forceinline__ void dom_row_acc(const uint32_t (&x)[W], const uint32
     }
 }
 
+// Scan nx x rows in batches of R, the next batch's scalar loads in flight while the
+// current batch is compared (a lone wave otherwise waits a K$/L2 round trip per batch).
 template <int W, int PPT, int R, bool DIAG>
 __device__ __forceinline__ void dom_scan(const uint32_t *__restrict__ xs, uint32_t nx, int32_t tbase,
                                          const uint32_t (&y)[PPT][W], uint64_t (&dom)[PPT]) {
     uint32_t acc[PPT];
 #pragma unroll
     for (int p = 0; p < PPT; p++) acc[p] = 0xffffffffu;
-    for (uint32_t i = 0; i < nx;) {
-        const uint32_t cn = nx - i < 16u ? nx - i : 16u;
-        const uint32_t nr = cn - cn % R;
-        for (uint32_t r = 0; r < nr; r += R) {
-            uint32_t x[R][W];
+    const uint32_t nb = nx / R;                              // full batches
+    uint32_t xn[R][W];
+    if (nb) {
+#pragma unroll
+        for (int q = 0; q < R; q++)
+#pragma unroll
+            for (int w = 0; w < W; w++) xn[q][w] = xs[(size_t)q * W + w];
+    }
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t x[R][W];
+#pragma unroll
+        for (int q = 0; q < R; q++)
+#pragma unroll
+            for (int w = 0; w < W; w++) x[q][w] = xn[q][w];
+        if (b + 1 < nb) {
 #pragma unroll
             for (int q = 0; q < R; q++)
 #pragma unroll
-                for (int w = 0; w < W; w++) x[q][w] = xs[(size_t)(i + r + q) * W + w];
+                for (int w = 0; w < W; w++) xn[q][w] = xs[(size_t)((b + 1) * R + q) * W + w];
+        }
 #pragma unroll
-            for (int q = 0; q < R; q++) {
-                if constexpr (DIAG) dom_row<W, PPT, true>(x[q], tbase + (int32_t)(i + r + q), y, dom);
-                else dom_row_acc<W, PPT>(x[q], y, acc);
+        for (int q = 0; q < R; q++) {
+            if constexpr (DIAG) dom_row<W, PPT, true>(x[q], tbase + (int32_t)(b * R + q), y, dom);
+            else dom_row_acc<W, PPT>(x[q], y, acc);
+        }
+        if (((b + 1) * R) % 16u == 0u || b + 1 == nb) {
+            uint64_t all = ~0ull;
+#pragma unroll
+            for (int p = 0; p < PPT; p++) {
+                if constexpr (!DIAG) dom[p] |= __ballot(acc[p] == 0u);
+                all &= dom[p];
             }
+            if (all == ~0ull) return;
         }
-        for (uint32_t r = nr; r < cn; r++) {
-            uint32_t x[W];
+    }
+    for (uint32_t i = nb * R; i < nx; i++) {
+        uint32_t x[W];
 #pragma unroll
-            for (int w = 0; w < W; w++) x[w] = xs[(size_t)(i + r) * W + w];
-            if constexpr (DIAG) dom_row<W, PPT, true>(x, tbase + (int32_t)(i + r), y, dom);
-            else dom_row_acc<W, PPT>(x, y, acc);
-        }
-        i += cn;
-        uint64_t all = ~0ull;
+        for (int w = 0; w < W; w++) x[w] = xs[(size_t)i * W + w];
+        if constexpr (DIAG) dom_row<W, PPT, true>(x, tbase + (int32_t)i, y, dom);
+        else dom_row_acc<W, PPT>(x, y, acc);
+    }
+    if constexpr (!DIAG) {
 #pragma unroll
-        for (int p = 0; p < PPT; p++) {
-            if constexpr (!DIAG) dom[p] |= __ballot(acc[p] == 0u);
-            all &= dom[p];
-        }
-        if (all == ~0ull) break;
+        for (int p = 0; p < PPT; p++) dom[p] |= __ballot(acc[p] == 0u);
     }
 }
 
@@ -175,7 +192,18 @@ __global__ __launch_bounds__(256, 8) void k_dom16(const uint32_t *__restrict__ r
         }
     }
     if (all == ~0ull) return;
-    dom_scan<W, PPT, R, DIAG>(xs, nx, (int32_t)(it.x0 - it.y0), y, dom);
+    if constexpr (DIAG) {
+        // x before y0: plain rows; x in [y0, y0+ny): masked rows; x after: no dominator
+        const int32_t t0 = (int32_t)it.x0 - (int32_t)it.y0;              // < 0: x starts before y0
+        const uint32_t nplain = t0 < 0 ? ((uint32_t)(-t0) < nx ? (uint32_t)(-t0) : nx) : 0u;
+        const int64_t xend = (int64_t)it.y0 + it.ny - it.x0;            // x index past the last y
+        const uint32_t nlim = xend < (int64_t)nx ? (uint32_t)(xend > 0 ? xend : 0) : nx;
+        if (nplain) dom_scan<W, PPT, R, false>(xs, nplain, 0, y, dom);
+        if (nlim > nplain)
+            dom_scan<W, PPT, R, true>(xs + (size_t)nplain * W, nlim - nplain, t0 + (int32_t)nplain, y, dom);
+    } else {
+        dom_scan<W, PPT, R, false>(xs, nx, 0, y, dom);
+    }
 #pragma unroll
     for (int p = 0; p < PPT; p++) {
         const uint32_t q = (uint32_t)(p * 64 + lane);
@@ -264,7 +292,7 @@ void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, ui
     else { SKY_DISPATCH_D(D, (k_pack16<DD, 8><<<nb16(m), kThreads, 0, st>>>(rows, m, idx, out))); }
 }
 
-// SKY_DOM_PPT in {4, 8, 16} (y rows per lane), SKY_DOM_R in {2, 4} (x rows per
+// SKY_DOM_PPT in {4, 8} (y rows per lane of the rest tiles; tri tiles use 1), SKY_DOM_R in {2, 4} (x rows per
 // scalar-load batch): tuning knobs, defaults measured on the MI355X
 static int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
@@ -273,7 +301,7 @@ static int env_int(const char *name, int dflt) {
 int dom16_ppt() {
     static int v = [] {
         const int p = env_int("SKY_DOM_PPT", 4);
-        return (p == 8 || p == 16) ? p : 4;
+        return p == 8 ? 8 : 4;
     }();
     return v;
 }
@@ -290,20 +318,20 @@ static void dom16_t(bool diag, const uint32_t *rows, const uint32_t *xbuf, const
     else k_dom16<W, PPT, R, false><<<g, 256, 0, st>>>(rows, xbuf, xcnt, items, nitems, xcap, dead);
 }
 template <int W>
-static void dom16_w(bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
+static void dom16_w(int ppt, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
                     const DomItem *items, uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
-    const int ppt = dom16_ppt(), r = dom16_r();
+    const int r = dom16_r();
 #define DOM16_CASE(P_, R_) \
     if (ppt == P_ && r == R_) { dom16_t<W, P_, R_>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st); return; }
-    DOM16_CASE(4, 2) DOM16_CASE(4, 4) DOM16_CASE(8, 2) DOM16_CASE(8, 4) DOM16_CASE(16, 2) DOM16_CASE(16, 4)
+    DOM16_CASE(1, 2) DOM16_CASE(1, 4) DOM16_CASE(4, 2) DOM16_CASE(4, 4) DOM16_CASE(8, 2) DOM16_CASE(8, 4)
 #undef DOM16_CASE
 }
 
-void launch_dom16(int W, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
+void launch_dom16(int W, int ppt, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt,
                   const DomItem *items, uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st) {
     if (!nitems) return;
-    if (W == 4) dom16_w<4>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
-    else dom16_w<8>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
+    if (W == 4) dom16_w<4>(ppt, diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
+    else dom16_w<8>(ppt, diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st);
 }
 
 void launch_xcompact16(int W, const uint32_t *rows, const uint32_t *idx, const SfsSeg *xseg, uint32_t nslots,

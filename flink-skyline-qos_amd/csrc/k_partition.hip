@@ -16,6 +16,8 @@
 //   k_out_count / k_out_write
 //                    per tuple: is it in its local / the global skyline? -> stats
 //                    (|L_k|, survivors_k) and the stream-ordered output ids
+#include <algorithm>
+
 #include "sky_internal.h"
 
 namespace sky {
@@ -213,6 +215,72 @@ __global__ __launch_bounds__(64) void k_pick_pruners(const double *__restrict__ 
     if (j == 0) npr[k] = __popcll(b);
 }
 
+// score = f64 sum of the (exact) T values in dimension order, each clamped to
+// [-1e300, 1e300] so that +inf and -inf never meet (the clamp is monotone, so the
+// score stays a linear extension of dominance).  A tie-free key needs no clamp, an
+// exact sum and an exact f32 of it -> otherwise flag kFlagScoreTies.
+template <typename T, int D>
+__device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part, uint32_t &lflags) {
+    double s = 0.0;
+    bool inexact = false;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        const double raw = (double)tv[d];
+        const double x = raw > 1e300 ? 1e300 : (raw < -1e300 ? -1e300 : raw);
+        inexact |= x != raw;
+        const double sn = s + x;
+        const double bb = sn - s;
+        const double err = (s - (sn - bb)) + (x - bb);
+        inexact |= err != 0.0;
+        s = sn;
+    }
+    const float f = (float)s;
+    inexact |= (double)f != s;
+    if (inexact) lflags |= kFlagScoreTies;
+    bool u16 = true;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        const double x = (double)tv[d];
+        u16 &= (x >= 0.0) & (x <= 65535.0) & (x == floor(x));
+    }
+    if (!u16) lflags |= kFlagNotU16;
+    uint32_t h = 0x9e3779b9u;
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        uint64_t bits;
+        if constexpr (sizeof(T) == 4) bits = __float_as_uint(tv[d] == T(0) ? T(0) : tv[d]);
+        else bits = (uint64_t)__double_as_longlong(tv[d] == T(0) ? T(0) : tv[d]);
+        h = mix32(h ^ (uint32_t)bits ^ (uint32_t)(bits >> 32) * 0x85ebca6bu);
+    }
+    return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffffu);
+}
+
+// A candidate joins the slot list (wave-aggregated append, unordered): f64 row,
+// sort key (partition | score | hash), source index, and slot_of[i] for the
+// per-tuple fate pass.  OR / AND of the keys accumulate in o / an.
+template <int D>
+__device__ __forceinline__ void append_candidate(const FilterArgs &a, bool cand, const double (&v)[D], int32_t k,
+                                                 uint32_t i, uint32_t &lflags, uint64_t &o, uint64_t &an) {
+    const uint64_t cm = __ballot(cand);
+    if (!cm) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)cm) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(a.m_total, (uint32_t)__popcll(cm));
+    base = __shfl(base, leader, 64);
+    if (!cand) return;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t slot = base + (uint32_t)__popcll(cm & lt);
+    constexpr int DP = padded_dims<double>(D);
+    store_row<double, D>(a.crow + (size_t)slot * DP, v);
+    const uint64_t key = make_sortkey<double, D>(v, (uint32_t)k, lflags);
+    a.sortkey[slot] = key;
+    a.slot_src[slot] = i;
+    a.slot_of[i] = slot;
+    o |= key;
+    an &= key;
+}
+
 // Classify one tuple of partition k: dropped (dominated by a pruner of k), exact
 // duplicate of pruner j (code 1+j), or candidate.  Pruners are tested in f64.
 template <int D>
@@ -255,12 +323,15 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
 // this kernel carries no exact-fdlibm code (no call, no scratch, fewer VGPRs).
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // [Kp*M*D]
+    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // [Kp*M*D] pruners, then [Kp*M] u32 dup counts
+    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * a.M * D);
     __shared__ int32_t s_npr[kMaxK];
-    __shared__ uint32_t s_dup[2048];
-    __shared__ uint32_t s_w[kThreads / 64];
+    // candidates of this tile, per wave: (partition << 16) | offset in the tile
+    __shared__ uint32_t s_cand[kTile];
+    __shared__ uint32_t s_wc[kThreads / 64], s_base;
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
-    uint32_t lflags = 0, mycnt = 0;
+    uint32_t lflags = 0, wcnt = 0;
+    uint64_t o = 0, an = ~0ull;
     const uint32_t base = blockIdx.x * kTile;
     const int lane = threadIdx.x & 63;
     // software pipeline: the row of item r+1 is in flight while item r is classified
@@ -300,16 +371,68 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
                 a.defer_list[wbase + __popcll(dm & lt)] = i;
             }
         }
-        if (!valid || defer) continue;
-        uint16_t code = kCodeCandidate;
-        if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
-        else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-        else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
-        mycnt += code == kCodeCandidate;
-        a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+        bool cand = false;
+        if (valid && !defer) {
+            uint16_t code = kCodeCandidate;
+            if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
+            else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
+            else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+            cand = code == kCodeCandidate;
+            a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+        }
+        // record the candidate in this wave's LDS list (no global atomics in the stream)
+        const uint64_t cm = __ballot(cand);
+        if (cand) {
+            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+            s_cand[(threadIdx.x >> 6) * (kItems * 64) + wcnt + (uint32_t)__popcll(cm & lt)] =
+                ((uint32_t)k << 16) | (i - base);
+        }
+        wcnt += (uint32_t)__popcll(cm);
     }
-    const uint32_t tot = block_sum(mycnt, s_w);
-    if (threadIdx.x == 0) a.blk_cnt[blockIdx.x] = tot;
+    // the tile's candidates: ONE slot reservation per tile, then rows re-read (cache
+    // hot) and appended with their sort keys
+    if (lane == 0) s_wc[threadIdx.x >> 6] = wcnt;
+    __syncthreads();
+    uint32_t woff[kThreads / 64 + 1];
+    woff[0] = 0;
+#pragma unroll
+    for (int q = 0; q < kThreads / 64; q++) woff[q + 1] = woff[q] + s_wc[q];
+    const uint32_t total = woff[kThreads / 64];
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(a.m_total, total) : 0u;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < total; q += kThreads) {
+        int w = 0;
+#pragma unroll
+        for (int t = 1; t < kThreads / 64; t++) w += q >= woff[t] ? 1 : 0;
+        const uint32_t e = s_cand[w * (kItems * 64) + (q - woff[w])];
+        const uint32_t i = base + (e & 0xffffu);
+        const uint32_t k = e >> 16;
+        double v[D];
+        load_row<D>(a.vals + (size_t)i * D, v);
+        const uint32_t slot = s_base + q;
+        constexpr int DP = padded_dims<double>(D);
+        store_row<double, D>(a.crow + (size_t)slot * DP, v);
+        const uint64_t key = make_sortkey<double, D>(v, k, lflags);
+        a.sortkey[slot] = key;
+        a.slot_src[slot] = i;
+        a.slot_of[i] = slot;
+        o |= key;
+        an &= key;
+    }
+    // per-tile OR / AND of the sort keys#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        o |= __shfl_xor(o, sh, 64);
+        an &= __shfl_xor(an, sh, 64);
+    }
+    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
+    if (lane == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long bo = 0, ba = ~0ull;
+        for (int q = 0; q < kThreads / 64; q++) { bo |= s_o[q]; ba &= s_a[q]; }
+        a.tile_orand[2 * blockIdx.x] = bo;
+        a.tile_orand[2 * blockIdx.x + 1] = ba;
+    }
     for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads)
         if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
     if (lflags) atomicOr(a.flags, lflags);
@@ -320,66 +443,46 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
     extern __shared__ __attribute__((aligned(16))) double s_pr[];
+    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * a.M * D);
     __shared__ int32_t s_npr[kMaxK];
-    __shared__ uint32_t s_dup[2048];
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
     const uint32_t cnt = *a.defer_cnt;
     uint32_t lflags = 0;
-    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < cnt; q += gridDim.x * kThreads) {
-        const uint32_t i = a.defer_list[q];
+    uint64_t o = 0, an = ~0ull;
+    const uint32_t span = (cnt + gridDim.x * kThreads - 1) / (gridDim.x * kThreads) * (gridDim.x * kThreads);
+    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < span; q += gridDim.x * kThreads) {
+        const bool valid = q < cnt;                       // every lane runs the wave-wide append
+        const uint32_t i = valid ? a.defer_list[q] : 0u;
         double v[D];
-        load_row<D>(a.vals + (size_t)i * D, v);
-        int32_t k = angle_key_exact<D>(v, a.kp.P);
-        uint16_t code;
-        if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-        else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
-        if (code == kCodeCandidate) atomicAdd(&a.blk_cnt[i / kTile], 1u);
-        a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+        int32_t k = 0;
+        bool cand = false;
+        if (valid) {
+            load_row<D>(a.vals + (size_t)i * D, v);
+            k = angle_key_exact<D>(v, a.kp.P);
+            uint16_t code;
+            if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
+            else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+            cand = code == kCodeCandidate;
+            a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; d++) v[d] = 0.0;
+        }
+        append_candidate<D>(a, cand, v, k, i, lflags, o, an);
+    }
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        o |= __shfl_xor(o, sh, 64);
+        an &= __shfl_xor(an, sh, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && o != 0ull) {
+        atomicOr(a.orand, (unsigned long long)o);
+        atomicAnd(a.orand + 1, (unsigned long long)an);
     }
     __syncthreads();
     for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads)
         if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
     if (lflags) atomicOr(a.flags, lflags);
-}
-
-// score = f64 sum of the (exact) T values in dimension order, each clamped to
-// [-1e300, 1e300] so that +inf and -inf never meet (the clamp is monotone, so the
-// score stays a linear extension of dominance).  A tie-free key needs no clamp, an
-// exact sum and an exact f32 of it -> otherwise flag kFlagScoreTies.
-template <typename T, int D>
-__device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part, uint32_t &lflags) {
-    double s = 0.0;
-    bool inexact = false;
-#pragma unroll
-    for (int d = 0; d < D; d++) {
-        const double raw = (double)tv[d];
-        const double x = raw > 1e300 ? 1e300 : (raw < -1e300 ? -1e300 : raw);
-        inexact |= x != raw;
-        const double sn = s + x;
-        const double bb = sn - s;
-        const double err = (s - (sn - bb)) + (x - bb);
-        inexact |= err != 0.0;
-        s = sn;
-    }
-    const float f = (float)s;
-    inexact |= (double)f != s;
-    if (inexact) lflags |= kFlagScoreTies;
-    bool u16 = true;
-#pragma unroll
-    for (int d = 0; d < D; d++) {
-        const double x = (double)tv[d];
-        u16 &= (x >= 0.0) & (x <= 65535.0) & (x == floor(x));
-    }
-    if (!u16) lflags |= kFlagNotU16;
-    uint32_t h = 0x9e3779b9u;
-#pragma unroll
-    for (int d = 0; d < D; d++) {
-        uint64_t bits;
-        if constexpr (sizeof(T) == 4) bits = __float_as_uint(tv[d] == T(0) ? T(0) : tv[d]);
-        else bits = (uint64_t)__double_as_longlong(tv[d] == T(0) ? T(0) : tv[d]);
-        h = mix32(h ^ (uint32_t)bits ^ (uint32_t)(bits >> 32) * 0x85ebca6bu);
-    }
-    return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffffu);
 }
 
 // Blocked tile layout for the status-word passes: thread t of tile b owns the
@@ -422,67 +525,6 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_w, u
     __syncthreads();
     total = tot;
     return wb + inc - v;
-}
-
-template <typename T, int D>
-__device__ __forceinline__ uint64_t emit_candidate(const double *__restrict__ vals, uint32_t i, uint32_t part,
-                                                   T *rows, uint32_t slot, uint64_t *sortkey, uint32_t &lflags) {
-    constexpr int DP = padded_dims<T>(D);
-    double v[D];
-    load_row<D>(vals + (size_t)i * D, v);
-    T tv[D];
-#pragma unroll
-    for (int d = 0; d < D; d++) tv[d] = (T)v[d];
-    store_row<T, D>(rows + (size_t)slot * DP, tv);
-    const uint64_t key = make_sortkey<T, D>(tv, part, lflags);
-    sortkey[slot] = key;
-    return key;
-}
-
-// Order-preserving compaction of the candidates.  The row type is chosen on the
-// device: f32 unless the filter saw a candidate value that is not exactly an f32.
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_compact(CompactArgs a) {
-    __shared__ uint32_t s_w[kThreads / 64];
-    const bool f64 = (*a.flags & kFlagNotF32) != 0;
-    uint32_t lflags = 0;
-    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kItems;
-    uint16_t st[kItems];
-    load_status8(a.status, a.n, i0, st);
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < kItems; k++) c += (i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate) ? 1u : 0u;
-    uint32_t tot;
-    uint32_t slot = a.blk_off[blockIdx.x] + block_scan_excl(c, s_w, tot);
-    uint64_t o = 0, an = ~0ull;
-    for (int k = 0; k < kItems; k++) {
-        if (!(i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate)) continue;
-        const uint32_t i = i0 + k;
-        const uint64_t key =
-            f64 ? emit_candidate<double, D>(a.vals, i, st[k] >> 8, (double *)a.rows, slot, a.sortkey, lflags)
-                : emit_candidate<float, D>(a.vals, i, st[k] >> 8, (float *)a.rows, slot, a.sortkey, lflags);
-        a.slot_src[slot] = i;
-        o |= key;
-        an &= key;
-        slot++;
-    }
-    // OR / AND of the sort keys (which key bytes vary -> radix passes): one partial
-    // per tile (plain stores; one global address hit by every tile would serialise)
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        o |= __shfl_xor(o, s, 64);
-        an &= __shfl_xor(an, s, 64);
-    }
-    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
-    if ((threadIdx.x & 63) == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long bo = 0, ba = ~0ull;
-        for (int q = 0; q < kThreads / 64; q++) { bo |= s_o[q]; ba &= s_a[q]; }
-        a.tile_orand[2 * blockIdx.x] = bo;
-        a.tile_orand[2 * blockIdx.x + 1] = ba;
-    }
-    if (lflags) atomicOr(a.flags, lflags);
 }
 
 __global__ __launch_bounds__(kThreads) void k_orand_reduce(const unsigned long long *__restrict__ part, uint32_t np,
@@ -533,7 +575,6 @@ __device__ __forceinline__ uint64_t emit_pruner(const double *pr, uint32_t part,
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
     __shared__ uint32_t s_w[kThreads / 64];
-    const bool f64 = (*a.flags & kFlagNotF32) != 0;
     const uint32_t m = *a.m_total;
     const int KM = a.Kp * a.M;
     uint32_t run = 0, lflags = 0;
@@ -549,8 +590,7 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
             a.pruner_slot[q] = (int32_t)slot;
             a.slot_src[slot] = 0x80000000u | e;
             const double *pr = a.pruners + (size_t)q * D;
-            const uint64_t key = f64 ? emit_pruner<double, D>(pr, q / a.M, (double *)a.rows, slot, a.sortkey, lflags)
-                                     : emit_pruner<float, D>(pr, q / a.M, (float *)a.rows, slot, a.sortkey, lflags);
+            const uint64_t key = emit_pruner<double, D>(pr, q / a.M, (double *)a.rows, slot, a.sortkey, lflags);
             o |= key;
             an &= key;
         } else if (q < KM) {
@@ -577,10 +617,14 @@ __global__ __launch_bounds__(kThreads) void k_gather_runs(RepArgs a) {
     constexpr int DP = padded_dims<T>(D);
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= a.mt) return;
-    const T *src = reinterpret_cast<const T *>(a.rows) + (size_t)a.perm[j] * DP;
+    // slot rows are f64 (written by the filter before the row type was known)
+    const double *src = reinterpret_cast<const double *>(a.rows) + (size_t)a.perm[j] * padded_dims<double>(D);
     T *dst = reinterpret_cast<T *>(a.rows_sorted) + (size_t)j * DP;
+    double dv[D];
+    load_trow<double, D>(src, dv);
     T v[D];
-    load_trow<T, D>(src, v);
+#pragma unroll
+    for (int d = 0; d < D; d++) v[d] = (T)dv[d];
     store_row<T, D>(dst, v);
     a.runflag[j] = (j == 0 || a.skey[j] != a.skey[j - 1]) ? 1u : 0u;
 }
@@ -679,58 +723,69 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(uint32_t mt, const uin
     }
 }
 
-template <bool WRITE>
-__global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
+// Count pass: kOutTPB tiles per workgroup, every tile's status words loaded up front
+// (the pass is latency-bound per workgroup otherwise); per-tile selected counts via
+// wave sums, per-(shard, origin) stats flushed once per workgroup.
+constexpr int kOutTPB = 4;
+
+__global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
     __shared__ unsigned long long s_lsz[kMaxK];
     __shared__ unsigned long long s_surv[kMaxK];
     __shared__ uint8_t s_pf[2048];
-    __shared__ uint32_t s_w[kThreads / 64];
-    const bool stats = !WRITE && a.lsz != nullptr;
+    __shared__ uint32_t s_tw[kOutTPB][kThreads / 64];
+    const bool stats = a.lsz != nullptr;
     if (stats)
         for (int q = threadIdx.x; q < a.K; q += kThreads) { s_lsz[q] = 0; s_surv[q] = 0; }
     for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
-    __syncthreads();
-    const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * kItems;
-    uint16_t st[kItems];
-    load_status8(a.status, a.n, i0, st);
-    uint32_t c = 0;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t0 = blockIdx.x * kOutTPB;
+    uint16_t st[kOutTPB][kItems];
 #pragma unroll
-    for (int k = 0; k < kItems; k++) c += (i0 + k < a.n && (st[k] & 0xff) == kCodeCandidate) ? 1u : 0u;
-    uint32_t tot;
-    uint32_t slot = a.blk_off[blockIdx.x] + block_scan_excl(c, s_w, tot);
-    uint8_t fate[kItems];
-    uint32_t nsel = 0;
-    const int shift = a.select_local ? 0 : 1;
+    for (int t = 0; t < kOutTPB; t++) {
+        const uint32_t i0 = (t0 + t) * kTile + threadIdx.x * kItems;
+        if (t0 + t < ntiles) load_status8(a.status, a.n, i0, st[t]);
+        else {
 #pragma unroll
-    for (int k = 0; k < kItems; k++) {
-        const uint32_t code = st[k] & 0xff;
-        uint8_t f = 0;
-        if (i0 + k < a.n) {
-            if (code == kCodeCandidate) f = a.slot_fate[slot++];
-            else if (code != kCodeDropped) f = s_pf[(st[k] >> 8) * a.M + (code - 1)];
+            for (int k = 0; k < kItems; k++) st[t][k] = 0;
         }
-        fate[k] = f;
-        nsel += (f >> shift) & 1u;
     }
-    if (!WRITE) {
-        uint32_t bt;
-        (void)block_scan_excl(nsel, s_w, bt);
-        if (threadIdx.x == 0) a.out_cnt[blockIdx.x] = bt;
+    __syncthreads();                                   // s_pf ready
+    const int shift = a.select_local ? 0 : 1;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < kOutTPB; t++) {
+        const uint32_t i0 = (t0 + t) * kTile + threadIdx.x * kItems;
+        uint8_t fate[kItems];
+        uint32_t nsel = 0;
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            const uint32_t code = st[t][k] & 0xff;
+            uint8_t f = 0;
+            if (i0 + k < a.n) {
+                if (code == kCodeCandidate) f = a.slot_fate[a.slot_of[i0 + k]];
+                else if (code != kCodeDropped) f = s_pf[(st[t][k] >> 8) * a.M + (code - 1)];
+            }
+            fate[k] = f;
+            nsel += (f >> shift) & 1u;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nsel += __shfl_xor(nsel, o, 64);
+        if (lane == 0) s_tw[t][threadIdx.x >> 6] = nsel;
         if (a.row_flags) {
 #pragma unroll
             for (int k = 0; k < kItems; k++)
                 if (i0 + k < a.n) a.row_flags[i0 + k] = fate[k];
         }
         if (stats) {
-            // per thread: one (origin, |L| weight, |G| weight) triple when its tuples share
-            // an origin (else per-tuple LDS atomics); per wave: one add when uniform
+            // per thread: one (origin, |L| weight, |G| weight) triple when its tuples
+            // share an origin (else per-tuple LDS atomics); per wave: one add when uniform
             int o1 = -1;
             bool mixed = false;
             unsigned long long wl = 0, wg = 0;
             for (int k = 0; k < kItems; k++) {
                 if (!(fate[k] & 1)) continue;
                 const uint32_t i = i0 + k;
-                const int o = a.given_origin ? a.given_origin[i] : (int)(st[k] >> 8);
+                const int o = a.given_origin ? a.given_origin[i] : (int)(st[t][k] >> 8);
                 const unsigned long long w = a.given_w ? (unsigned long long)a.given_w[i] : 1ull;
                 if (o1 < 0) o1 = o;
                 if (o == o1 && !mixed) {
@@ -752,7 +807,7 @@ __global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
                         wl += __shfl_xor(wl, sh, 64);
                         wg += __shfl_xor(wg, sh, 64);
                     }
-                    if ((threadIdx.x & 63) == 0) {
+                    if (lane == 0) {
                         atomicAdd(&s_lsz[o0], wl);
                         if (wg) atomicAdd(&s_surv[o0], wg);
                     }
@@ -761,51 +816,82 @@ __global__ __launch_bounds__(kThreads) void k_out(OutArgs a) {
                     if (wg) atomicAdd(&s_surv[o1], wg);
                 }
             }
-            __syncthreads();
-            // sharded accumulators: one global address per (shard, origin), summed by the host
-            const size_t sh = (size_t)(blockIdx.x % kStatShards) * a.K;
-            for (int q = threadIdx.x; q < a.K; q += kThreads) {
-                if (s_lsz[q]) atomicAdd(&a.lsz[sh + q], s_lsz[q]);
-                if (s_surv[q]) atomicAdd(&a.surv[sh + q], s_surv[q]);
-            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kOutTPB && t0 + threadIdx.x < ntiles) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; w++) c += s_tw[threadIdx.x][w];
+        a.out_cnt[t0 + threadIdx.x] = c;
+    }
+    if (stats) {
+        // sharded accumulators: one global address per (shard, origin), reduced on device
+        const size_t sh = (size_t)(blockIdx.x % kStatShards) * a.K;
+        for (int q = threadIdx.x; q < a.K; q += kThreads) {
+            if (s_lsz[q]) atomicAdd(&a.lsz[sh + q], s_lsz[q]);
+            if (s_surv[q]) atomicAdd(&a.surv[sh + q], s_surv[q]);
+        }
+    }
+}
+
+// Write pass: one tile per workgroup; the tile's selected ids / origins are staged
+// in LDS in stream order, then written as one contiguous, coalesced run.
+__global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
+    __shared__ uint8_t s_pf[2048];
+    __shared__ uint32_t s_w[kThreads / 64];
+    __shared__ int64_t s_oid[kTile];
+    __shared__ int32_t s_oorg[kTile];
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t i0 = tile * kTile + threadIdx.x * kItems;
+    uint16_t st[kItems];
+    load_status8(a.status, a.n, i0, st);
+    int64_t idv[kItems];
+    if (a.ids && i0 + kItems <= a.n) {
+        const longlong2 *q = reinterpret_cast<const longlong2 *>(a.ids + i0);
+#pragma unroll
+        for (int k = 0; k < kItems / 2; k++) {
+            const longlong2 x = q[k];
+            idv[2 * k] = x.x;
+            idv[2 * k + 1] = x.y;
         }
     } else {
-        // the tile's selected ids / origins are staged in LDS in stream order, then
-        // written out as one contiguous, coalesced run per tile
-        __shared__ int64_t s_oid[kTile];
-        __shared__ int32_t s_oorg[kTile];
-        uint32_t bt;
-        uint32_t pl = block_scan_excl(nsel, s_w, bt);
-        const uint32_t base = a.out_off[blockIdx.x];
-        int64_t idv[kItems];
-        if (nsel && a.ids && i0 + kItems <= a.n) {
-            const longlong2 *q = reinterpret_cast<const longlong2 *>(a.ids + i0);
 #pragma unroll
-            for (int k = 0; k < kItems / 2; k++) {
-                const longlong2 x = q[k];
-                idv[2 * k] = x.x;
-                idv[2 * k + 1] = x.y;
-            }
-        } else {
+        for (int k = 0; k < kItems; k++) idv[k] = i0 + k < a.n ? (a.ids ? a.ids[i0 + k] : (int64_t)(i0 + k)) : 0;
+    }
+    __syncthreads();                                   // s_pf ready
+    const int shift = a.select_local ? 0 : 1;
+    uint8_t fate[kItems];
+    uint32_t nsel = 0;
 #pragma unroll
-            for (int k = 0; k < kItems; k++)
-                idv[k] = (nsel && i0 + k < a.n) ? (a.ids ? a.ids[i0 + k] : (int64_t)(i0 + k)) : 0;
+    for (int k = 0; k < kItems; k++) {
+        const uint32_t code = st[k] & 0xff;
+        uint8_t f = 0;
+        if (i0 + k < a.n) {
+            if (code == kCodeCandidate) f = a.slot_fate[a.slot_of[i0 + k]];
+            else if (code != kCodeDropped) f = s_pf[(st[k] >> 8) * a.M + (code - 1)];
         }
+        fate[k] = f;
+        nsel += (f >> shift) & 1u;
+    }
+    uint32_t bt;
+    uint32_t pl = block_scan_excl(nsel, s_w, bt);
+    const uint32_t base = a.out_off[tile];
 #pragma unroll
-        for (int k = 0; k < kItems; k++) {
-            if (!((fate[k] >> shift) & 1)) continue;
-            const uint32_t i = i0 + k;
-            s_oid[pl] = idv[k];
-            s_oorg[pl] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
-            if (a.rows_out)
-                for (int d = 0; d < a.D; d++) a.rows_out[(size_t)(base + pl) * a.D + d] = a.vals[(size_t)i * a.D + d];
-            pl++;
-        }
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
-            if (a.ids_out) a.ids_out[base + q] = s_oid[q];
-            if (a.origin_out) a.origin_out[base + q] = s_oorg[q];
-        }
+    for (int k = 0; k < kItems; k++) {
+        if (!((fate[k] >> shift) & 1)) continue;
+        const uint32_t i = i0 + k;
+        s_oid[pl] = idv[k];
+        s_oorg[pl] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
+        if (a.rows_out)
+            for (int d = 0; d < a.D; d++) a.rows_out[(size_t)(base + pl) * a.D + d] = a.vals[(size_t)i * a.D + d];
+        pl++;
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
+        if (a.ids_out) a.ids_out[base + q] = s_oid[q];
+        if (a.origin_out) a.origin_out[base + q] = s_oorg[q];
     }
 }
 
@@ -851,17 +937,13 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double);
+    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
     SKY_DISPATCH_D(D, (k_filter<DD><<<nblk(a.n, kTile), kThreads, lds, st>>>(a)));
 }
 
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double);
+    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
     SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<256, kThreads, lds, st>>>(a)));
-}
-
-void launch_compact(int D, const CompactArgs &a, hipStream_t st) {
-    if (a.n) { SKY_DISPATCH_D(D, (k_compact<DD><<<nblk(a.n, kTile), kThreads, 0, st>>>(a))); }
 }
 
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
@@ -901,10 +983,10 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
                                                                 pr_entries, mult);
 }
 void launch_out_count(const OutArgs &a, hipStream_t st) {
-    if (a.n) k_out<false><<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
+    if (a.n) k_out_count<<<nblk(nblk(a.n, kTile), kOutTPB), kThreads, 0, st>>>(a);
 }
 void launch_out_write(const OutArgs &a, hipStream_t st) {
-    if (a.n) k_out<true><<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
+    if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
 }
 void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
                         const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,

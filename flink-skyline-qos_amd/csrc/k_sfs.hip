@@ -378,6 +378,36 @@ __global__ __launch_bounds__(kThreads) void k_scatter_alive(const uint32_t *__re
     if (j < mg) alive_g[gval[j]] = galive[j];
 }
 
+// sum the [shard][K] stat accumulators into [K] (one workgroup per key)
+__global__ __launch_bounds__(kThreads) void k_stat_reduce(const unsigned long long *__restrict__ lsz,
+                                                          const unsigned long long *__restrict__ surv, int K,
+                                                          unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long s_l[kThreads / 64], s_s[kThreads / 64];
+    const int k = blockIdx.x;
+    unsigned long long l = 0, sv = 0;
+    for (int sh = threadIdx.x; sh < kStatShards; sh += kThreads) {
+        l += lsz[(size_t)sh * K + k];
+        sv += surv[(size_t)sh * K + k];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        l += __shfl_xor(l, o, 64);
+        sv += __shfl_xor(sv, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) { s_l[threadIdx.x >> 6] = l; s_s[threadIdx.x >> 6] = sv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < kThreads / 64; q++) { l = s_l[0] += s_l[q]; sv = s_s[0] += s_s[q]; }
+        out[k] = s_l[0];
+        out[K + k] = s_s[0];
+    }
+}
+
+void launch_stat_reduce(const unsigned long long *lsz, const unsigned long long *surv, int K, unsigned long long *out,
+                        hipStream_t st) {
+    if (K > 0) k_stat_reduce<<<K, kThreads, 0, st>>>(lsz, surv, K, out);
+}
+
 __global__ __launch_bounds__(kThreads) void k_u8_to_u32(const uint8_t *__restrict__ in, uint32_t n,
                                                         uint32_t *__restrict__ out) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;

@@ -10,7 +10,7 @@ constexpr int kMaxK = SKY_MAX_PARTITIONS;
 constexpr int kThreads = 256;                 // 4 waves of 64
 constexpr int kItems = 8;                     // tuples per thread per tile
 constexpr int kTile = kThreads * kItems;      // 2048 tuples per workgroup tile
-constexpr int kStatShards = 64;               // |L_k| / survivors_k accumulators are [shard][K]
+constexpr int kStatShards = 1024;             // |L_k| / survivors_k accumulators are [shard][K], reduced on device
 
 // per-tuple status word (u16): high byte = partition key, low byte = code
 constexpr uint16_t kCodeDropped = 0;          // dominated by a pruner / key never queried

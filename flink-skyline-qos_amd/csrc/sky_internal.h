@@ -52,7 +52,14 @@ struct FilterArgs {
     const int32_t *npr;           // [Kp]
     int M, Kp;
     uint16_t *status;             // [n]
-    uint32_t *blk_cnt;            // [tiles] candidates per tile
+    // candidate slots (unordered append): f64 rows, sort keys, source index, slot per tuple
+    double *crow;                 // [n + Kp*M][pad(D)]
+    uint64_t *sortkey;
+    uint32_t *slot_src;
+    uint32_t *slot_of;            // [n] (written for candidates only)
+    uint32_t *m_total;
+    unsigned long long *tile_orand;   // [tiles][2] per-tile {OR, AND} of the sort keys
+    unsigned long long *orand;        // device {OR, AND} (deferred tuples add atomically)
     uint32_t *dup_cnt;            // [Kp*M]
     uint32_t *flags;              // kFlag*
     uint32_t *defer_list;         // [n] MR-Angle tuples whose key needs the exact path
@@ -66,18 +73,6 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
                            double *pruners, int32_t *npr, hipStream_t st);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
-struct CompactArgs {
-    const double *vals;
-    uint32_t n;
-    const uint16_t *status;
-    const uint32_t *blk_off;      // exclusive scan of blk_cnt
-    void *rows;                   // [mt][DP] f32 or f64 (chosen on the device from flags)
-    uint64_t *sortkey;            // [mt]
-    uint32_t *slot_src;           // [mt] source tuple index (bit31: pruner entry)
-    uint32_t *flags;
-    unsigned long long *tile_orand;   // [tiles][2] per-tile {OR, AND} of the sort keys
-};
-void launch_compact(int D, const CompactArgs &a, hipStream_t st);
 void launch_orand_reduce(const unsigned long long *part, uint32_t np, unsigned long long *orand, hipStream_t st);
 struct AppendArgs {
     const double *pruners;        // [Kp][M][D]
@@ -87,7 +82,7 @@ struct AppendArgs {
     uint32_t *nps_total;          // device out: number of pruner slots
     int32_t *entries;             // [nps] -> k*M+j
     int32_t *pruner_slot;         // [Kp*M] -> slot or -1
-    void *rows;
+    void *rows;                   // f64 slot rows
     uint64_t *sortkey;
     uint32_t *slot_src;
     uint32_t *flags;
@@ -122,7 +117,7 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
 struct OutArgs {
     const uint16_t *status;
     uint32_t n;
-    const uint32_t *blk_off;      // candidate slot base per tile
+    const uint32_t *slot_of;      // candidate slot per tuple
     const uint8_t *slot_fate;     // [mt] inL | inG << 1
     const uint8_t *pruner_fate;   // [Kp*M]
     int M, KM;
@@ -171,6 +166,8 @@ void launch_gather_rows(int D, bool f64, const void *src, const uint32_t *idx, u
                         hipStream_t st);
 void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t mg, uint8_t *alive_g,
                           hipStream_t st);
+void launch_stat_reduce(const unsigned long long *lsz, const unsigned long long *surv, int K, unsigned long long *out,
+                        hipStream_t st);
 void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st);
 void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
 
@@ -179,10 +176,11 @@ struct DomItem { uint32_t seg, y0, ny, x0, nx, flags; };
 constexpr uint32_t kDomDiag = 1u;             // x and y ranges overlap: only x before y
 constexpr uint32_t kDomRest = 2u;             // x from xbuf[seg] (X'), count from xcnt[seg]
 int dom16_ppt();                              // y rows per lane (work item = 64 * ppt y rows)
-constexpr uint32_t kDomTx = 1024u;            // x rows per work item
+constexpr uint32_t kDomTx = 512u;             // x rows per work item
 int dom16_words(int D);
 void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, uint32_t *out, hipStream_t st);
-void launch_dom16(int W, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
+constexpr int kDomTriPPT = 1;                 // tri tiles: 64 y per wave (latency-bound, many waves)
+void launch_dom16(int W, int ppt, bool diag, const uint32_t *rows, const uint32_t *xbuf, const uint32_t *xcnt, const DomItem *items,
                   uint32_t nitems, uint32_t xcap, uint32_t *dead, hipStream_t st);
 void launch_xcompact16(int W, const uint32_t *rows, const uint32_t *idx, const SfsSeg *xseg, uint32_t nslots,
                        uint32_t xcap, uint32_t *dead, uint32_t *xbuf, uint32_t *xcnt, uint8_t *alive, hipStream_t st);

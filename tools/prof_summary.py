@@ -129,5 +129,23 @@ def main():
     print("wrote", out)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and sys.argv[1] != "timeline":
     main()
+
+
+def timeline(d, last_n=120):
+    """The last `last_n` dispatches in start order: name, start offset (us), duration, gap."""
+    rows = []
+    for r in _rows(d, "*kernel_trace.csv"):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "?")))
+    rows.sort()
+    rows = rows[-last_n:]
+    t0 = rows[0][0]
+    prev_end = t0
+    for s, e, n in rows:
+        print(f"{(s - t0) / 1000:10.1f} {(e - s) / 1000:9.1f} gap {(s - prev_end) / 1000:8.1f}  {n[:90]}")
+        prev_end = max(prev_end, e)
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[1] == "timeline":
+    timeline(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 120)
