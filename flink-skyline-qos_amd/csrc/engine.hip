@@ -582,8 +582,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mt), scan_scratch_words(mt + 1)) * 4 + 64));
         launch_iota(p.perm.as<uint32_t>(), mt, st);
         const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
-                                          p.val_alt.as<uint32_t>(), mt, orand[0] ^ orand[1],
-                                          p.scratch.as<uint32_t>(), st);
+                                          p.val_alt.as<uint32_t>(), mt, orand[0], orand[1],
+                                          p.scratch.as<uint32_t>(), p.flags.as<uint32_t>(), st);
         STAGE(st, "sort");
         const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
         const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
@@ -625,9 +625,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                           p.seg_end.as<uint32_t>(), st);
         STAGE(st, "dedup");
         std::vector<uint32_t> sb(p.Kp), se(p.Kp);
+        uint32_t flags2 = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
-                                  {p.seg_end.p, (size_t)p.Kp * 4}},
-                          {&mr, sb.data(), se.data()}));
+                                  {p.seg_end.p, (size_t)p.Kp * 4}, {p.flags.p, 4}},
+                          {&mr, sb.data(), se.data(), &flags2}));
+        if (flags2 & kFlagRadixSpin) {
+            set_error("radix sort look-back exceeded its spin bound");
+            return SKY_E_HIP;
+        }
         p.mr = mr;
         for (int k = 0; k < p.Kp; k++) se[k] -= sb[k];
         if (tm) tm->mark(5, st);
@@ -673,7 +678,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 SKY_TRY(p.galive.ensure((size_t)mg));
                 const bool galt = radix_sort_pairs(p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(),
                                                    p.gkey_alt.as<uint64_t>(), p.gval_alt.as<uint32_t>(), mg,
-                                                   orand[0] ^ orand[1], p.scratch.as<uint32_t>(), st);
+                                                   orand[0], orand[1], p.scratch.as<uint32_t>(),
+                                                   p.flags.as<uint32_t>(), st);
                 const uint64_t *gk = galt ? p.gkey_alt.as<uint64_t>() : p.gkey.as<uint64_t>();
                 const uint32_t *gv = galt ? p.gval_alt.as<uint32_t>() : p.gval.as<uint32_t>();
                 HIP_TRY(hipMemsetAsync(p.galive.p, 0, mg, st));

@@ -252,7 +252,9 @@ __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part
         else bits = (uint64_t)__double_as_longlong(tv[d] == T(0) ? T(0) : tv[d]);
         h = mix32(h ^ (uint32_t)bits ^ (uint32_t)(bits >> 32) * 0x85ebca6bu);
     }
-    return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffffu);
+    // 16 hash bits: equal vectors stay adjacent; a collision only lengthens one
+    // equal-key run, which k_rep_of resolves by exact row compares
+    return ((uint64_t)part << 56) | ((uint64_t)f32_order_key(f) << 24) | (uint64_t)(h & 0xffffu);
 }
 
 // A candidate joins the slot list (wave-aggregated append, unordered): f64 row,

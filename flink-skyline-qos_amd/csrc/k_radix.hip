@@ -1,18 +1,22 @@
-// k_radix.hip — stable LSD radix sort of (u64 key, u32 value) pairs, 8-bit digits.
+// k_radix.hip — stable LSD radix sort of (u64 key, u32 value) pairs, 8-bit digits,
+// one kernel per pass ("onesweep": decoupled look-back instead of a per-pass scan).
 //
-// Per pass:  k_radix_hist   (per-tile digit histogram, LDS atomics, per-wave copies)
-//            scan           (digit-major [256][tiles] offsets, k_scan.hip)
-//            k_radix_scatter(stable tile-local ranks from wave64 ballots; the tile is
-//                            staged in LDS in digit order and written out as
-//                            contiguous runs, so HBM writes are coalesced)
+//   k_rs_hist_all   digit histograms of EVERY pass in one read of the keys (the
+//                   global count of a digit does not depend on the key order)
+//   k_rs_scan_all   per pass: exclusive scan -> global digit bases
+//   k_rs_onesweep   per pass: a tile (taken in launch order from an atomic ticket)
+//                   ranks its keys stably (wave64 ballots), publishes its digit
+//                   counts, looks back over the earlier tiles' published counts for
+//                   its exclusive prefix (bounded spin), then writes the tile staged
+//                   in LDS in digit order as contiguous runs (coalesced)
 // Only bytes that differ between keys are sorted (OR/AND reduction first).
 #include "sky_internal.h"
 
 namespace sky {
 
 constexpr int kRadixThreads = 256;
-constexpr int kRadixItems = 16;
-constexpr int kRadixTile = kRadixThreads * kRadixItems;   // 4096
+constexpr int kRadixItems = 4;
+constexpr int kRadixTile = kRadixThreads * kRadixItems;   // 1024 (short tiles: more workgroups in flight)
 
 __global__ __launch_bounds__(256) void k_key_orand(const uint64_t *__restrict__ keys, uint32_t m,
                                                    unsigned long long *__restrict__ orand) {
@@ -32,28 +36,94 @@ __global__ __launch_bounds__(256) void k_key_orand(const uint64_t *__restrict__ 
     }
 }
 
-__global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint64_t *__restrict__ keys, uint32_t m,
-                                                              int shift, uint32_t ntiles,
-                                                              uint32_t *__restrict__ hist) {
-    __shared__ uint32_t s_h[4][256];
-    const int t = threadIdx.x, w = t >> 6;
-#pragma unroll
-    for (int i = 0; i < 4; i++) s_h[i][t] = 0;
+struct RsShifts { int s[8]; };
+
+__global__ __launch_bounds__(kRadixThreads) void k_rs_hist_all(const uint64_t *__restrict__ keys, uint32_t m,
+                                                               RsShifts shifts, int npass,
+                                                               uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t s_h[8][256];
+    const int t = threadIdx.x;
+    for (int p = 0; p < 8; p++) s_h[p][t] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * kRadixTile;
+    int sh[8];
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
-        const uint32_t i = base + r * kRadixThreads + t;
-        if (i < m) atomicAdd(&s_h[w][(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    for (int p = 0; p < 8; p++) sh[p] = p < npass ? shifts.s[p] : 0;
+    for (uint32_t i = blockIdx.x * kRadixThreads + t; i < m; i += gridDim.x * kRadixThreads) {
+        const uint64_t k = keys[i];
+#pragma unroll
+        for (int p = 0; p < 8; p++)
+            if (p < npass) atomicAdd(&s_h[p][(uint32_t)(k >> sh[p]) & 255u], 1u);
     }
     __syncthreads();
-    hist[(size_t)t * ntiles + blockIdx.x] = s_h[0][t] + s_h[1][t] + s_h[2][t] + s_h[3][t];
+    for (int p = 0; p < npass; p++)
+        if (s_h[p][t]) atomicAdd(&ghist[p * 256 + t], s_h[p][t]);
 }
 
-__global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
+__global__ __launch_bounds__(256) void k_rs_scan_all(uint32_t *__restrict__ ghist, int npass) {
+    __shared__ uint32_t s_w[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int p = 0; p < npass; p++) {
+        const uint32_t c = ghist[p * 256 + t];
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        uint32_t wb = 0;
+        for (int i = 0; i < w; i++) wb += s_w[i];
+        ghist[p * 256 + t] = wb + inc - c;
+        __syncthreads();
+    }
+}
+
+// order-preserving compression of the varying key bits (the constant bits are equal
+// in every key, so comparing the remaining bits in significance order is comparing
+// the keys): runs of consecutive varying bits, LSB first
+struct RsRuns { int n; uint8_t start[32], len[32]; };
+
+__global__ __launch_bounds__(256) void k_rs_compress(const uint64_t *__restrict__ keys, uint32_t m, RsRuns runs,
+                                                     uint64_t *__restrict__ dense) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t k = keys[i];
+    uint64_t o = 0;
+    int pos = 0;
+    for (int r = 0; r < runs.n; r++) {
+        const int l = runs.len[r];
+        const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
+        o |= ((k >> runs.start[r]) & msk) << pos;
+        pos += l;
+    }
+    dense[i] = o;
+}
+
+// inverse of k_rs_compress: scatter the dense bits back and restore the constant bits
+__global__ __launch_bounds__(256) void k_rs_expand(const uint64_t *__restrict__ dense, uint32_t m, RsRuns runs,
+                                                   uint64_t const_bits, uint64_t *__restrict__ keys) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t d = dense[i];
+    uint64_t k = const_bits;
+    int pos = 0;
+    for (int r = 0; r < runs.n; r++) {
+        const int l = runs.len[r];
+        const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
+        k |= ((d >> pos) & msk) << runs.start[r];
+        pos += l;
+    }
+    keys[i] = k;
+}
+
+constexpr uint32_t kRsAgg = 1u << 30, kRsInc = 2u << 30, kRsCount = (1u << 30) - 1;
+
+__global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     const uint64_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
     uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, uint32_t m, int shift,
-    uint32_t ntiles, const uint32_t *__restrict__ offs) {
+    const uint32_t *__restrict__ gbase, uint32_t *__restrict__ status, uint32_t *__restrict__ ticket,
+    uint32_t *__restrict__ err) {
     __shared__ uint64_t s_key[kRadixTile];
     __shared__ uint32_t s_val[kRadixTile];
     __shared__ uint32_t s_cnt[4][256];
@@ -62,13 +132,17 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_goff[256];
     __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_tile;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t base = blockIdx.x * kRadixTile;
+    // tiles are numbered in the order workgroups start: a tile only ever waits for
+    // tiles that started before it (forward progress of the look-back)
+    if (t == 0) s_tile = atomicAdd(ticket, 1u);
 #pragma unroll
     for (int i = 0; i < 4; i++) s_cnt[i][t] = 0;
     s_run[t] = 0;
-    s_goff[t] = offs[(size_t)t * ntiles + blockIdx.x];
     __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t base = tile * kRadixTile;
 
     uint64_t k[kRadixItems];
     uint32_t v[kRadixItems];
@@ -103,6 +177,34 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
         }
         __syncthreads();
         rk[r] = valid ? s_wb[w][d] + pre : 0xffffffffu;
+    }
+    // publish this tile's digit count, look back for the exclusive prefix
+    {
+        const uint32_t agg = s_run[t];
+        uint32_t *mine = status + (size_t)tile * 256 + t;
+        uint32_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(mine, kRsInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(mine, kRsAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t pt = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            while (pt >= 0) {
+                const uint32_t v = __hip_atomic_load(status + (size_t)pt * 256 + t, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t f = v & ~kRsCount;
+                if (f == 0u) {
+                    if (++spins > (1u << 24)) { atomicOr(err, kFlagRadixSpin); break; }   // bounded spin
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += v & kRsCount;
+                if (f == kRsInc) break;
+                pt--;
+            }
+            __hip_atomic_store(mine, kRsInc | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_goff[t] = gbase[t] + excl;
     }
     // tile-local digit starts
     {
@@ -146,34 +248,75 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
 }
 
 size_t radix_scratch_words(size_t m) {
-    size_t tiles = (m + kRadixTile - 1) / kRadixTile;
-    return 2 * 256 * tiles + scan_scratch_words(256 * tiles) + 16;
+    const size_t tiles = (m + kRadixTile - 1) / kRadixTile;
+    return 8 * 256 + 8 * 256 * tiles + 8 + 8 + 64 + 4 * m + 4 + 2 * m;
 }
 
 // Sorts (keys, vals) by key; ping-pongs with (keys_alt, vals_alt).  Returns true if
-// the result ended in the alt buffers.  `orand_host` = {OR, AND} of all keys (host
-// computed by caller via radix_key_orand) selects which bytes to sort.
+// the result ended in the alt buffers.  key_or / key_and: OR and AND of all keys; the
+// varying bits are compressed into dense keys first when that saves passes (the
+// scratch holds the dense ping-pong pair and an index array; the original keys
+// are gathered back at the end).
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
-                      uint64_t varying_bits, uint32_t *scratch, hipStream_t st) {
+                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st) {
+    const uint64_t varying_bits = key_or ^ key_and;
     if (m <= 1 || varying_bits == 0) return false;
     const uint32_t tiles = (m + kRadixTile - 1) / kRadixTile;
-    uint32_t *hist = scratch;
-    uint32_t *offs = scratch + 256 * (size_t)tiles;
-    uint32_t *scan_tmp = offs + 256 * (size_t)tiles;
+    RsRuns runs{};
+    int nbits = 0;
+    for (int b = 0; b < 64;) {
+        if (!((varying_bits >> b) & 1ull)) { b++; continue; }
+        int e = b;
+        while (e < 64 && ((varying_bits >> e) & 1ull)) e++;
+        runs.start[runs.n] = (uint8_t)b;
+        runs.len[runs.n] = (uint8_t)(e - b);
+        runs.n++;
+        nbits += e - b;
+        b = e;
+    }
+    int byte_passes = 0;
+    for (int byte = 0; byte < 8; byte++) byte_passes += ((varying_bits >> (8 * byte)) & 0xffull) ? 1 : 0;
+    const int dense_passes = (nbits + 7) / 8;
+    const bool compress = dense_passes < byte_passes;
+    RsShifts shifts{};
+    int npass = 0;
+    if (compress) {
+        for (int p = 0; p < dense_passes; p++) shifts.s[npass++] = 8 * p;
+    } else {
+        for (int byte = 0; byte < 8; byte++)
+            if ((varying_bits >> (8 * byte)) & 0xffull) shifts.s[npass++] = 8 * byte;
+    }
+    uint32_t *ghist = scratch;                                   // [8][256]
+    uint32_t *status = ghist + 8 * 256;                          // [8][tiles][256]
+    uint32_t *tickets = status + (size_t)8 * 256 * tiles;        // [8]
+    uint64_t *dense = reinterpret_cast<uint64_t *>(
+        (reinterpret_cast<uintptr_t>(tickets + 16) + 15) & ~uintptr_t(15));   // [2][m]
+    (void)hipMemsetAsync(scratch, 0, ((size_t)8 * 256 + (size_t)npass * 256 * tiles) * 4, st);
+    (void)hipMemsetAsync(tickets, 0, 8 * 4, st);
+    uint64_t *k0 = keys, *k1 = keys_alt;
+    if (compress) {
+        k0 = dense;
+        k1 = dense + m;
+        k_rs_compress<<<(m + 255) / 256, 256, 0, st>>>(keys, m, runs, k0);
+    }
+    unsigned hb = tiles < 1024 ? tiles : 1024;
+    k_rs_hist_all<<<hb, kRadixThreads, 0, st>>>(k0, m, shifts, npass, ghist);
+    k_rs_scan_all<<<1, 256, 0, st>>>(ghist, npass);
     bool alt = false;
-    for (int byte = 0; byte < 8; byte++) {
-        if (((varying_bits >> (8 * byte)) & 0xffull) == 0) continue;
-        const int shift = 8 * byte;
-        const uint64_t *kin = alt ? keys_alt : keys;
+    for (int p = 0; p < npass; p++) {
+        const uint64_t *kin = alt ? k1 : k0;
         const uint32_t *vin = alt ? vals_alt : vals;
-        uint64_t *kout = alt ? keys : keys_alt;
+        uint64_t *kout = alt ? k0 : k1;
         uint32_t *vout = alt ? vals : vals_alt;
-        k_radix_hist<<<tiles, kRadixThreads, 0, st>>>(kin, m, shift, tiles, hist);
-        scan_excl_u32(hist, offs, 256 * (size_t)tiles, nullptr, scan_tmp, st);
-        k_radix_scatter<<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shift, tiles, offs);
+        k_rs_onesweep<<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], ghist + p * 256,
+                                                       status + (size_t)p * 256 * tiles, tickets + p, err);
         alt = !alt;
     }
-    return alt;
+    if (!compress) return alt;
+    // sorted keys -> keys_alt (expanded back), values -> vals_alt
+    if (!alt) (void)hipMemcpyAsync(vals_alt, vals, (size_t)m * 4, hipMemcpyDeviceToDevice, st);
+    k_rs_expand<<<(m + 255) / 256, 256, 0, st>>>(alt ? k1 : k0, m, runs, key_and & ~varying_bits, keys_alt);
+    return true;
 }
 
 void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st) {

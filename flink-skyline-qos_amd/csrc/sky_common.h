@@ -21,6 +21,7 @@ constexpr uint16_t kCodeCandidate = 255;      // goes to sort + SFS
 constexpr uint32_t kFlagNotF32 = 1u;          // some candidate value is not exactly an f32
 constexpr uint32_t kFlagNaN = 2u;             // a NaN was seen
 constexpr uint32_t kFlagScoreTies = 4u;       // score key is not strictly monotone
+constexpr uint32_t kFlagRadixSpin = 16u;      // a radix look-back hit its spin bound (result invalid)
 constexpr uint32_t kFlagNotU16 = 8u;          // some candidate value is not an integer in [0, 65535]
 
 // padded row width in elements so every row starts 16-byte aligned

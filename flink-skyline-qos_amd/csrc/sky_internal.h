@@ -37,8 +37,10 @@ void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_tota
 
 // ---- k_radix.hip ----
 size_t radix_scratch_words(size_t m);
+// err: device word, kFlagRadixSpin is OR-ed in if a look-back spin ran out (never
+// expected; the caller checks it at its next synchronisation)
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
-                      uint64_t varying_bits, uint32_t *scratch, hipStream_t st);
+                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st);
 void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st);
 
 // ---- k_partition.hip ----
