@@ -112,20 +112,27 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
     ap.add_argument("--no-dominance", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, the measured path) or gloo (rehearsing ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)   # > 1 rank per GPU only with gloo
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     D, P, n = args.dims, args.partitions, args.n
-    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, local_rank)
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
     vals = torch.empty((n, D), dtype=torch.float64, device=dev)
     ids = torch.empty(n, dtype=torch.int64, device=dev)
     eng.synth_dev(args.dist, n, vals, ids, seed=args.seed, id0=rank * n)
@@ -161,10 +168,10 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.profile(False)
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        gt = torch.tensor([g], dtype=torch.int64, device=dev)
+        gt = torch.tensor([g], dtype=torch.int64, device=red_dev)
         dist.all_reduce(gt)
         g = int(gt.item())
     phases, counters = eng.phases()

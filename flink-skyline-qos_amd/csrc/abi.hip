@@ -435,6 +435,7 @@ int sky_export_local_dev(sky_ctx *c, const int64_t *d_ids, const double *d_value
     in.n = (uint32_t)n;
     in.ids = d_ids;
     in.global = false;
+    in.fate = false;
     in.K = c->Kq();
     SKY_TRY(pipe_run(*c, c->main, in, nullptr));
     Pipe &p = c->main;

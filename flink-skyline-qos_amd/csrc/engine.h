@@ -42,6 +42,7 @@ struct PipeIn {
     const int64_t *weights = nullptr;
     bool single = false;            // one partition (global merge of lists, local state insert)
     bool global = true;             // run the global merge after the local skylines
+    bool fate = true;               // per-tuple fate pass (stats, output counts)
     int K = 1;                      // stats slots
 };
 

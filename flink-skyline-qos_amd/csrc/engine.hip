@@ -113,13 +113,11 @@ static int debug_level() {
     }();
     return lvl;
 }
-// SKY_SFS16=0 forces the generic f32/f64 SFS (used by the tests to cover both paths)
+// SKY_SFS16=0 forces the generic f32/f64 SFS (read per query: the tests compare the
+// two paths in one process)
 static bool sfs16_disabled() {
-    static bool off = [] {
-        const char *e = getenv("SKY_SFS16");
-        return e && atoi(e) == 0;
-    }();
-    return off;
+    const char *e = getenv("SKY_SFS16");
+    return e && atoi(e) == 0;
 }
 static int stage_check(hipStream_t st, const char *where) {
     hipError_t e = hipGetLastError();
@@ -704,6 +702,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     launch_fate_tables(mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(), KM,
                        p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(), p.pruner_fate.as<uint8_t>(), st);
     if (tm) tm->mark(7, st);
+    if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
+        p.nout = 0;
+        if (tm) tm->mark(8, st);
+        return SKY_OK;
+    }
 
     // ---- per-tuple fate: stats + output counts
     SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));

@@ -37,8 +37,13 @@ def unpack_union(packed, counts, D):
 
 def allgather_varlen(packed, group=None):
     """Gather a [n, W] int64 tensor of per-rank length n from every rank.
-    Returns (stacked [world, maxn, W], counts list)."""
+    Returns (stacked [world, maxn, W], counts list).  With a gloo group (CPU
+    collectives: tests, or rehearsing several ranks on one GPU) device tensors are
+    staged through host memory; with nccl (RCCL) they stay in HBM."""
     world = dist.get_world_size(group)
+    if packed.device.type == "cuda" and dist.get_backend(group) == "gloo":
+        out, counts = allgather_varlen(packed.cpu(), group)
+        return out.to(packed.device), counts
     dev = packed.device
     cnt = torch.tensor([packed.shape[0]], dtype=torch.int64, device=dev)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]

@@ -210,3 +210,29 @@ def test_device_query_matches_host_query(gpu_engine_factory, oracle):
     np.testing.assert_array_equal(oi[:g].cpu().numpy(), hid)
     np.testing.assert_array_equal(oo[:g].cpu().numpy(), horg)
     eng.close()
+
+
+@pytest.mark.parametrize("dist,D,n", [("std_anti", 8, 300000), ("uniform", 6, 400000), ("anti_correlated", 4, 400000)])
+def test_u16_path_equals_generic_path_at_scale(dist, D, n, gpu_engine_factory, oracle, monkeypatch):
+    """The integer-packed dominance path (k_dom16: multi-round SFS, growing blocks,
+    tiled tri/rest items) against the generic f32 SFS on streams too large for the
+    oracle's SFS; both are checked against the oracle on the smaller cases above."""
+    vals = oracle.synth(DISTS[dist], D, n, seed=500 + D)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SKY_SFS16", flag)
+        eng = gpu_engine_factory(D, 16, "mr-angle")
+        ids, org = eng.query(vals)
+        ls, sv = eng.stats()
+        res.append((ids, org, ls, sv))
+        eng.close()
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_u16_path_tiny_segments_and_ties(gpu_engine_factory, oracle):
+    """Integer rows with many equal scores, one-element partitions and P=256."""
+    rng = np.random.default_rng(17)
+    vals = rng.integers(0, 6, size=(30000, 5)).astype(np.float64)
+    for algo, P in (("mr-angle", 256), ("mr-dim", 3), ("mr-grid", 32)):
+        check_vs_oracle(gpu_engine_factory, oracle, vals, P, algo)
