@@ -103,7 +103,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=100_000_000, help="tuples per rank")
+    ap.add_argument("--tuples", type=int, default=100_000_000, help="tuples per rank (GPU)")
     ap.add_argument("--dims", type=int, default=8)
     ap.add_argument("--partitions", type=int, default=16)
     ap.add_argument("--dist", default="anti_correlated")
@@ -131,7 +131,7 @@ def main():
             dist.init_process_group("gloo")
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
-    D, P, n = args.dims, args.partitions, args.n
+    D, P, n = args.dims, args.partitions, args.tuples
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
     vals = torch.empty((n, D), dtype=torch.float64, device=dev)
     ids = torch.empty(n, dtype=torch.int64, device=dev)

@@ -512,6 +512,10 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
     // recount this shard's output with the imported global fates (no stats: those came from the union)
     {
         const uint32_t tiles = (p.n + kTile - 1) / kTile;
+        // the export ran without a fate pass: size the per-tile count buffers here
+        SKY_TRY(p.out_cnt.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
+        SKY_TRY(p.out_off.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
+        SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
         launch_fate_tables(p.mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
                            p.Kp * p.M, p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(),
                            p.pruner_fate.as<uint8_t>(), c->st);

@@ -578,6 +578,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.key_alt.ensure((size_t)mt * 8));
         SKY_TRY(p.val_alt.ensure((size_t)mt * 4));
         SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mt), scan_scratch_words(mt + 1)) * 4 + 64));
+        if (debug_level() >= 4) {
+            SKY_TRY(p.segalive.ensure(64));
+            radix_key_orand(p.sortkey.as<uint64_t>(), mt, p.segalive.as<unsigned long long>(), st);
+            unsigned long long chk[2] = {0, 0};
+            SKY_TRY(sync_read(p, st, {{p.segalive.p, 16}}, {chk}));
+            fprintf(stderr, "[sky] orand filter %016llx %016llx recomputed %016llx %016llx\n", orand[0], orand[1],
+                    chk[0], chk[1]);
+        }
         launch_iota(p.perm.as<uint32_t>(), mt, st);
         const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
                                           p.val_alt.as<uint32_t>(), mt, orand[0], orand[1],
@@ -585,6 +593,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         STAGE(st, "sort");
         const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
         const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
+        if (debug_level() >= 4 && alt) {
+            SKY_TRY(p.runflag.ensure((size_t)mt * 4));
+            HIP_TRY(hipMemsetAsync(p.totals.as<uint32_t>() + 7, 0, 4, st));
+            radix_debug_check(p.sortkey.as<uint64_t>(), skey, perm, mt, p.runflag.as<uint32_t>(),
+                              p.totals.as<uint32_t>() + 7, st);
+            uint32_t bad = 0;
+            SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 7, 4}}, {&bad}));
+            fprintf(stderr, "[sky] sort check m=%u bad=%u\n", mt, bad);
+        }
         if (tm) tm->mark(4, st);
 
         // ---- collapse exact duplicates: one representative per distinct vector
@@ -757,6 +774,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.h_surv[k] = sk2[(size_t)p.K + k];
     }
     p.nout = nout;
+    if (debug_level() >= 3) {
+        fprintf(stderr, "[sky] run n=%u m=%u nps=%u mr=%u mg=%u nout=%u u16=%d seg_n:", n, p.m, p.nps, p.mr, p.mg,
+                nout, (int)p.u16);
+        for (uint32_t x : p.h_seg_n) fprintf(stderr, " %u", x);
+        fprintf(stderr, " seg_s:");
+        for (uint32_t x : p.h_seg_s) fprintf(stderr, " %u", x);
+        fprintf(stderr, "\n");
+    }
     if (tm) tm->mark(8, st);
     return SKY_OK;
 }

@@ -10,6 +10,8 @@
 //                   its exclusive prefix (bounded spin), then writes the tile staged
 //                   in LDS in digit order as contiguous runs (coalesced)
 // Only bytes that differ between keys are sorted (OR/AND reduction first).
+#include <cstdlib>
+
 #include "sky_internal.h"
 
 namespace sky {
@@ -82,7 +84,8 @@ __global__ __launch_bounds__(256) void k_rs_scan_all(uint32_t *__restrict__ ghis
 // order-preserving compression of the varying key bits (the constant bits are equal
 // in every key, so comparing the remaining bits in significance order is comparing
 // the keys): runs of consecutive varying bits, LSB first
-struct RsRuns { int n; uint8_t start[32], len[32]; };
+constexpr int kRsMaxRuns = 8;          // more runs of varying bits: sort the raw bytes
+struct RsRuns { int n; int start[kRsMaxRuns], len[kRsMaxRuns]; };
 
 __global__ __launch_bounds__(256) void k_rs_compress(const uint64_t *__restrict__ keys, uint32_t m, RsRuns runs,
                                                      uint64_t *__restrict__ dense) {
@@ -91,28 +94,42 @@ __global__ __launch_bounds__(256) void k_rs_compress(const uint64_t *__restrict_
     const uint64_t k = keys[i];
     uint64_t o = 0;
     int pos = 0;
-    for (int r = 0; r < runs.n; r++) {
-        const int l = runs.len[r];
-        const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
-        o |= ((k >> runs.start[r]) & msk) << pos;
-        pos += l;
+    // constant indices only: the run table stays in SGPRs loaded at wave start (a
+    // dynamically indexed by-value kernel-argument array is read from the kernarg
+    // buffer by late waves, and late waves of a long grid read it corrupted)
+#pragma unroll
+    for (int r = 0; r < kRsMaxRuns; r++) {
+        if (r < runs.n) {
+            const int l = runs.len[r];
+            const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
+            o |= ((k >> runs.start[r]) & msk) << pos;
+            pos += l;
+        }
     }
     dense[i] = o;
 }
 
-// inverse of k_rs_compress: scatter the dense bits back and restore the constant bits
+// inverse of k_rs_compress: scatter the dense bits back and restore the constant bits;
+// vals_src != nullptr: also move the values into the alt buffer (a kernel, not an
+// async copy: a DMA copy engine read the previous kernel's values stale)
 __global__ __launch_bounds__(256) void k_rs_expand(const uint64_t *__restrict__ dense, uint32_t m, RsRuns runs,
-                                                   uint64_t const_bits, uint64_t *__restrict__ keys) {
+                                                   uint64_t const_bits, uint64_t *__restrict__ keys,
+                                                   const uint32_t *__restrict__ vals_src,
+                                                   uint32_t *__restrict__ vals_dst) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= m) return;
+    if (vals_src) vals_dst[i] = vals_src[i];
     const uint64_t d = dense[i];
     uint64_t k = const_bits;
     int pos = 0;
-    for (int r = 0; r < runs.n; r++) {
-        const int l = runs.len[r];
-        const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
-        k |= ((d >> pos) & msk) << runs.start[r];
-        pos += l;
+#pragma unroll
+    for (int r = 0; r < kRsMaxRuns; r++) {
+        if (r < runs.n) {
+            const int l = runs.len[r];
+            const uint64_t msk = l >= 64 ? ~0ull : ((1ull << l) - 1ull);
+            k |= ((d >> pos) & msk) << runs.start[r];
+            pos += l;
+        }
     }
     keys[i] = k;
 }
@@ -247,6 +264,25 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     }
 }
 
+// debug check (SKY_DEBUG >= 4): sorted, a permutation, keys match their source slots
+__global__ __launch_bounds__(256) void k_rs_check(const uint64_t *__restrict__ orig, const uint64_t *__restrict__ skey,
+                                                  const uint32_t *__restrict__ perm, uint32_t m,
+                                                  uint32_t *__restrict__ seen, uint32_t *__restrict__ bad) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= m) return;
+    if (j > 0 && skey[j - 1] > skey[j]) atomicOr(bad, 1u);
+    const uint32_t s = perm[j];
+    if (s >= m) { atomicOr(bad, 2u); return; }
+    if (orig[s] != skey[j]) atomicOr(bad, 4u);
+    if (atomicAdd(&seen[s], 1u) != 0u) atomicOr(bad, 8u);
+}
+
+void radix_debug_check(const uint64_t *orig, const uint64_t *skey, const uint32_t *perm, uint32_t m, uint32_t *seen,
+                       uint32_t *bad, hipStream_t st) {
+    (void)hipMemsetAsync(seen, 0, (size_t)m * 4, st);
+    if (m) k_rs_check<<<(m + 255) / 256, 256, 0, st>>>(orig, skey, perm, m, seen, bad);
+}
+
 size_t radix_scratch_words(size_t m) {
     const size_t tiles = (m + kRadixTile - 1) / kRadixTile;
     return 8 * 256 + 8 * 256 * tiles + 8 + 8 + 64 + 4 * m + 4 + 2 * m;
@@ -264,12 +300,14 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     const uint32_t tiles = (m + kRadixTile - 1) / kRadixTile;
     RsRuns runs{};
     int nbits = 0;
+    bool too_many_runs = false;
     for (int b = 0; b < 64;) {
         if (!((varying_bits >> b) & 1ull)) { b++; continue; }
         int e = b;
         while (e < 64 && ((varying_bits >> e) & 1ull)) e++;
-        runs.start[runs.n] = (uint8_t)b;
-        runs.len[runs.n] = (uint8_t)(e - b);
+        if (runs.n == kRsMaxRuns) { too_many_runs = true; break; }
+        runs.start[runs.n] = b;
+        runs.len[runs.n] = e - b;
         runs.n++;
         nbits += e - b;
         b = e;
@@ -277,7 +315,11 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     int byte_passes = 0;
     for (int byte = 0; byte < 8; byte++) byte_passes += ((varying_bits >> (8 * byte)) & 0xffull) ? 1 : 0;
     const int dense_passes = (nbits + 7) / 8;
-    const bool compress = dense_passes < byte_passes;
+    static const int comp_mode = [] {            // SKY_RADIX_COMPRESS=0 disables (debug)
+        const char *e = getenv("SKY_RADIX_COMPRESS");
+        return e ? atoi(e) : 1;
+    }();
+    const bool compress = comp_mode && !too_many_runs && dense_passes < byte_passes;
     RsShifts shifts{};
     int npass = 0;
     if (compress) {
@@ -314,8 +356,8 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     }
     if (!compress) return alt;
     // sorted keys -> keys_alt (expanded back), values -> vals_alt
-    if (!alt) (void)hipMemcpyAsync(vals_alt, vals, (size_t)m * 4, hipMemcpyDeviceToDevice, st);
-    k_rs_expand<<<(m + 255) / 256, 256, 0, st>>>(alt ? k1 : k0, m, runs, key_and & ~varying_bits, keys_alt);
+    k_rs_expand<<<(m + 255) / 256, 256, 0, st>>>(alt ? k1 : k0, m, runs, key_and & ~varying_bits, keys_alt,
+                                                 alt ? nullptr : vals, vals_alt);
     return true;
 }
 

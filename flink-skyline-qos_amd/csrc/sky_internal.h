@@ -41,6 +41,8 @@ size_t radix_scratch_words(size_t m);
 // expected; the caller checks it at its next synchronisation)
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
                       uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st);
+void radix_debug_check(const uint64_t *orig, const uint64_t *skey, const uint32_t *perm, uint32_t m, uint32_t *seen,
+                       uint32_t *bad, hipStream_t st);
 void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st);
 
 // ---- k_partition.hip ----

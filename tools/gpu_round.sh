@@ -20,6 +20,13 @@ if [[ $STEPS == *bench* ]]; then
   timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
   cat $OUT/bench_$TAG.json
 fi
+if [[ $STEPS == *dist* ]]; then
+  # two ranks rehearsed on the one GPU over gloo (the driver's 8-GPU run uses RCCL)
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --tuples 50000000 \
+      > $OUT/bench_dist2_$TAG.json 2> $OUT/bench_dist2_$TAG.err || { tail -30 $OUT/bench_dist2_$TAG.err; exit 1; }
+  grep '^{' $OUT/bench_dist2_$TAG.json | cut -c1-400
+fi
 if [[ $STEPS == *trace* ]]; then
   export TMPDIR=/tmp
   rm -rf $OUT/trace_$TAG
@@ -29,7 +36,7 @@ if [[ $STEPS == *trace* ]]; then
   python tools/prof_summary.py trace $OUT/trace_$TAG > $OUT/trace_${TAG}_summary.txt
   head -25 $OUT/trace_${TAG}_summary.txt
   rm -rf $OUT/trace_dom_$TAG
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_dom_$TAG -o run -- python3 -u $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-dominance --dist std_anti --n 2000000 > $OUT/trace_dom_$TAG.log 2>&1 || { tail -30 $OUT/trace_dom_$TAG.log; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_dom_$TAG -o run -- python3 -u $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-dominance --dist std_anti --tuples 2000000 > $OUT/trace_dom_$TAG.log 2>&1 || { tail -30 $OUT/trace_dom_$TAG.log; exit 1; }
   python tools/prof_summary.py trace $OUT/trace_dom_$TAG > $OUT/trace_dom_${TAG}_summary.txt
   head -12 $OUT/trace_dom_${TAG}_summary.txt
 fi
