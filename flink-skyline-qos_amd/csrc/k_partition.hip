@@ -17,6 +17,7 @@
 //                    per tuple: is it in its local / the global skyline? -> stats
 //                    (|L_k|, survivors_k) and the stream-ordered output ids
 #include <algorithm>
+#include <cstdlib>
 
 #include "sky_internal.h"
 
@@ -77,6 +78,11 @@ __device__ __forceinline__ void load_trow(const T *__restrict__ p, T (&v)[D]) {
             if (2 * d + 1 < D) v[2 * d + 1] = x.y;
         }
     }
+}
+
+// number of set bits of the wave mask m below this lane (v_mbcnt, no lane mask register)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // exclusive rank of `flag` in (round, thread) order within the block; `base` carries
@@ -283,25 +289,44 @@ __device__ __forceinline__ void append_candidate(const FilterArgs &a, bool cand,
     an &= key;
 }
 
+// LDS image of the pruner table.  8D rows are 64 bytes; with partitions M rows
+// apart every partition's row j starts on the same banks, so a wave whose lanes
+// hold up to 16 partitions reads them 16-way conflicted.  For D == 8 each
+// partition gets 64 bytes of padding (partition k -> 64-byte slot k % 4 of a
+// 256-byte bank row) and its rows' 16-byte chunks are XOR-permuted by (k / 4) % 4:
+// the 16 partitions of a ds_read_b128 lane group then hit 16 distinct bank quads.
+template <int D>
+__host__ __device__ constexpr int pr_stride(int M) { return M * D + (D == 8 ? 8 : 0); }   // doubles per partition
+template <int D>
+__device__ __forceinline__ int pr_off(int k, int j, int d) {   // within partition k's rows
+    if constexpr (D == 8) return j * D + ((((d >> 1) ^ ((k >> 2) & 3)) << 1) | (d & 1));
+    else return j * D + d;
+}
+template <int D>
+constexpr size_t pruner_lds_bytes(int Kp, int M) {
+    return (size_t)Kp * pr_stride<D>(M) * sizeof(double) + (size_t)Kp * M * 4;
+}
+
 // Classify one tuple of partition k: dropped (dominated by a pruner of k), exact
-// duplicate of pruner j (code 1+j), or candidate.  Pruners are tested in f64.
+// duplicate of pruner j (code 1+j, counted by count_dups), or candidate.  Pruners
+// are tested in f64.
 template <int D>
 __device__ __forceinline__ uint16_t classify(const double (&v)[D], int32_t k, const double *s_pr, const int32_t *s_npr,
-                                             uint32_t *s_dup, int M, uint32_t &lflags) {
+                                             int M, uint32_t &lflags) {
     uint16_t code = kCodeCandidate;
     const int np = s_npr[k];
-    const double *pr = s_pr + (size_t)k * M * D;
+    const double *pr = s_pr + k * pr_stride<D>(M);
     for (int j = 0; j < np; j++) {
         bool le = true, lt = false, eq = true;
 #pragma unroll
         for (int d = 0; d < D; d++) {
-            const double p = pr[j * D + d];
+            const double p = pr[pr_off<D>(k, j, d)];
             le &= p <= v[d];
             lt |= p < v[d];
             eq &= p == v[d];
         }
         if (le && lt) { code = kCodeDropped; break; }
-        if (eq) { code = (uint16_t)(1 + j); atomicAdd(&s_dup[k * M + j], 1u); break; }
+        if (eq) { code = (uint16_t)(1 + j); break; }
     }
     if (code == kCodeCandidate) {
 #pragma unroll
@@ -311,102 +336,145 @@ __device__ __forceinline__ uint16_t classify(const double (&v)[D], int32_t k, co
     return code;
 }
 
+// Per-(partition, pruner) duplicate counts: the wave's first duplicate's (k, j)
+// with ONE LDS atomic for all lanes sharing it (duplicates of one pruner usually
+// fill whole waves; per-lane atomics on one address serialise), the others per
+// lane.  All lanes call it.
+__device__ __forceinline__ void count_dups(uint16_t code, int32_t k, int M, uint32_t *s_dup) {
+    const bool dup = code != kCodeCandidate && code != kCodeDropped;
+    const uint64_t m = __ballot(dup);
+    if (!m) return;                                                  // wave-uniform
+    const uint32_t kj = (uint32_t)k * M + code - 1;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const uint32_t kj0 = __shfl(kj, leader, 64);
+    const bool same = dup && kj == kj0;
+    const uint64_t sm = __ballot(same);
+    if ((threadIdx.x & 63) == leader) atomicAdd(&s_dup[kj0], (uint32_t)__popcll(sm));
+    if (dup && !same) atomicAdd(&s_dup[kj], 1u);
+}
+
 template <int D>
 __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_pr, int32_t *s_npr, uint32_t *s_dup) {
     const int nprw = a.Kp * a.M;
-    for (int q = threadIdx.x; q < nprw * D; q += kThreads) s_pr[q] = a.pruners[q];
+    const int MD = a.M * D;
+    for (int q = threadIdx.x; q < nprw * D; q += kThreads) {
+        const int k = q / MD, r = q - k * MD;
+        s_pr[k * pr_stride<D>(a.M) + pr_off<D>(k, r / D, r % D)] = a.pruners[q];
+    }
     for (int q = threadIdx.x; q < a.Kp; q += kThreads) s_npr[q] = a.npr[q];
     for (int q = threadIdx.x; q < nprw; q += kThreads) s_dup[q] = 0;
     __syncthreads();
 }
 
 // The HBM stream.  MR-Angle keys the fast path cannot certify are appended to a
-// deferred list (wave-aggregated atomics) and finished by k_filter_deferred, so
-// this kernel carries no exact-fdlibm code (no call, no scratch, fewer VGPRs).
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // [Kp*M*D] pruners, then [Kp*M] u32 dup counts
-    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * a.M * D);
+// deferred list and finished by k_filter_deferred, so this kernel carries no
+// exact-fdlibm code (no call, no scratch, fewer VGPRs).
+//
+// Memory-pipeline rules this loop is built around (gfx950):
+//  * the row of item r+1 is in flight while item r is classified, and NOTHING else
+//    issued in the loop is a vector-memory op that a later wait must cover, except
+//    the status store of item r-1, issued together with that prefetch (vmcnt counts
+//    loads and stores together, in issue order: a store issued after the prefetch
+//    would make every wait for the row also wait for the store's acknowledgement);
+//  * every load is unconditional (row index clamped into [0, n)), so the prefetch
+//    registers never merge with a not-loaded path (no copies that wait for them);
+//  * waves_per_eu(6) caps the allocation at 80 VGPRs (72 in practice: 7 waves per
+//    SIMD), +5 % over the 81-VGPR default allocation (5 waves).  Row loads as whole 1 KB pieces transposed
+//    through LDS (full lines per instruction) measured 1.5 % SLOWER, at the lower
+//    occupancy their LDS image allows: the row-per-lane loads are not the limit.
+// Candidates (partition << 16 | offset) fill each wave's LDS list from the front,
+// deferred offsets from the back; the tile reserves its slots with one atomic.
+template <int D, bool GIVEN>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 7 : 1))) void k_filter(FilterArgs a) {
+    constexpr int kList = kItems * 64;                           // list entries per wave
+    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // pruner image (pr_stride), then [Kp*M] u32 dup counts
+    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * pr_stride<D>(a.M));
     __shared__ int32_t s_npr[kMaxK];
-    // candidates of this tile, per wave: (partition << 16) | offset in the tile
-    __shared__ uint32_t s_cand[kTile];
-    __shared__ uint32_t s_wc[kThreads / 64], s_base;
+    __shared__ uint32_t s_list[kTile];
+    __shared__ uint32_t s_wc[kThreads / 64], s_wd[kThreads / 64], s_base, s_dbase;
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
-    uint32_t lflags = 0, wcnt = 0;
+    uint32_t lflags = 0, wcnt = 0, dcnt = 0;
     uint64_t o = 0, an = ~0ull;
     const uint32_t base = blockIdx.x * kTile;
-    const int lane = threadIdx.x & 63;
-    // software pipeline: the row of item r+1 is in flight while item r is classified
-    double vn[D];
-    {
-        const uint32_t i = base + threadIdx.x;
-        if (i < a.n) load_row<D>(a.vals + (size_t)i * D, vn);
-        else {
-#pragma unroll
-            for (int d = 0; d < D; d++) vn[d] = 0.0;
-        }
-    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *wlist = s_list + __builtin_amdgcn_readfirstlane(wave) * kList;
+    const uint32_t nl = a.n - 1;
+    double vn[D];                                                // the row of item r+1, in flight
+    int32_t kn = 0;
+#define SKY_FILTER_FETCH(I)                                                                \
+    do {                                                                                   \
+        const uint32_t i_ = min((uint32_t)(I), nl);                                        \
+        load_row<D>(a.vals + (size_t)i_ * D, vn);                                          \
+        if constexpr (GIVEN) kn = a.given_keys[i_];                                        \
+    } while (0)
+    SKY_FILTER_FETCH(base + threadIdx.x);
+    uint16_t st_prev = 0;
 #pragma unroll 1
     for (int r = 0; r < kItems; r++) {
         const uint32_t i = base + r * kThreads + threadIdx.x;
-        if (base + r * kThreads >= a.n) break;                       // block-uniform
         const bool valid = i < a.n;
         double v[D];
 #pragma unroll
         for (int d = 0; d < D; d++) v[d] = vn[d];
-        if (r + 1 < kItems) {
-            const uint32_t i2 = i + kThreads;
-            if (i2 < a.n) load_row<D>(a.vals + (size_t)i2 * D, vn);
-        }
+        const int32_t kg = kn;
+        if (r > 0 && i - kThreads < a.n) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
+        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : i);           // past the tile: a cache hit
         bool nan = false;
 #pragma unroll
         for (int d = 0; d < D; d++) nan |= v[d] != v[d];
-        int32_t k = a.single ? 0 : a.given_keys ? (valid ? a.given_keys[i] : 0) : partition_key_fast<D>(v, a.kp);
-        const bool defer = valid && !nan && !a.single && !a.given_keys && k == kAngleUndecided;
+        int32_t k = GIVEN ? kg : a.single ? 0 : partition_key_fast<D>(v, a.kp);
+        const bool defer = !GIVEN && valid && !nan && !a.single && k == kAngleUndecided;
         const uint64_t dm = __ballot(defer);
-        if (dm) {
-            uint32_t wbase = 0;
-            if (lane == __ffsll((unsigned long long)dm) - 1) wbase = atomicAdd(a.defer_cnt, (uint32_t)__popcll(dm));
-            wbase = __shfl(wbase, __ffsll((unsigned long long)dm) - 1, 64);
-            if (defer) {
-                const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-                a.defer_list[wbase + __popcll(dm & lt)] = i;
-            }
-        }
+        if (defer) wlist[kList - 1 - (dcnt + lanes_below(dm))] = i - base;
+        dcnt += (uint32_t)__popcll(dm);
         bool cand = false;
+        uint16_t st = 0;                                             // deferred: rewritten by k_filter_deferred
         if (valid && !defer) {
             uint16_t code = kCodeCandidate;
             if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
             else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-            else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+            else code = classify<D>(v, k, s_pr, s_npr, a.M, lflags);
             cand = code == kCodeCandidate;
-            a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
+            st = (uint16_t)(((uint32_t)k << 8) | code);
         }
-        // record the candidate in this wave's LDS list (no global atomics in the stream)
+        count_dups((uint16_t)(st & 0xffu), (int32_t)(st >> 8), a.M, s_dup);
         const uint64_t cm = __ballot(cand);
-        if (cand) {
-            const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-            s_cand[(threadIdx.x >> 6) * (kItems * 64) + wcnt + (uint32_t)__popcll(cm & lt)] =
-                ((uint32_t)k << 16) | (i - base);
-        }
+        if (cand) wlist[wcnt + lanes_below(cm)] = ((uint32_t)k << 16) | (i - base);
         wcnt += (uint32_t)__popcll(cm);
+        st_prev = st;
+    }
+#undef SKY_FILTER_FETCH
+    {
+        const uint32_t il = base + (kItems - 1) * kThreads + threadIdx.x;
+        if (il < a.n) a.status[il] = st_prev;
     }
     // the tile's candidates: ONE slot reservation per tile, then rows re-read (cache
     // hot) and appended with their sort keys
-    if (lane == 0) s_wc[threadIdx.x >> 6] = wcnt;
+    if (lane == 0) { s_wc[wave] = wcnt; s_wd[wave] = dcnt; }
     __syncthreads();
-    uint32_t woff[kThreads / 64 + 1];
+    uint32_t woff[kThreads / 64 + 1], doff[kThreads / 64 + 1];
     woff[0] = 0;
+    doff[0] = 0;
 #pragma unroll
-    for (int q = 0; q < kThreads / 64; q++) woff[q + 1] = woff[q] + s_wc[q];
-    const uint32_t total = woff[kThreads / 64];
+    for (int q = 0; q < kThreads / 64; q++) {
+        woff[q + 1] = woff[q] + s_wc[q];
+        doff[q + 1] = doff[q] + s_wd[q];
+    }
+    const uint32_t total = woff[kThreads / 64], dtotal = doff[kThreads / 64];
     if (threadIdx.x == 0) s_base = total ? atomicAdd(a.m_total, total) : 0u;
+    if (threadIdx.x == 64 && dtotal) s_dbase = atomicAdd(a.defer_cnt, dtotal);
     __syncthreads();
+    for (uint32_t q = threadIdx.x; q < dtotal; q += kThreads) {
+        int w = 0;
+#pragma unroll
+        for (int t = 1; t < kThreads / 64; t++) w += q >= doff[t] ? 1 : 0;
+        a.defer_list[s_dbase + q] = base + s_list[w * kList + kList - 1 - (q - doff[w])];
+    }
     for (uint32_t q = threadIdx.x; q < total; q += kThreads) {
         int w = 0;
 #pragma unroll
         for (int t = 1; t < kThreads / 64; t++) w += q >= woff[t] ? 1 : 0;
-        const uint32_t e = s_cand[w * (kItems * 64) + (q - woff[w])];
+        const uint32_t e = s_list[w * kList + (q - woff[w])];
         const uint32_t i = base + (e & 0xffffu);
         const uint32_t k = e >> 16;
         double v[D];
@@ -421,13 +489,14 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
         o |= key;
         an &= key;
     }
-    // per-tile OR / AND of the sort keys#pragma unroll
+    // per-tile OR / AND of the sort keys
+#pragma unroll
     for (int sh = 32; sh >= 1; sh >>= 1) {
         o |= __shfl_xor(o, sh, 64);
         an &= __shfl_xor(an, sh, 64);
     }
     __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
-    if (lane == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
+    if (lane == 0) { s_o[wave] = o; s_a[wave] = an; }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long bo = 0, ba = ~0ull;
@@ -445,7 +514,7 @@ __global__ __launch_bounds__(kThreads) void k_filter(FilterArgs a) {
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
     extern __shared__ __attribute__((aligned(16))) double s_pr[];
-    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * a.M * D);
+    uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * pr_stride<D>(a.M));
     __shared__ int32_t s_npr[kMaxK];
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
     const uint32_t cnt = *a.defer_cnt;
@@ -458,18 +527,19 @@ __global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
         double v[D];
         int32_t k = 0;
         bool cand = false;
+        uint16_t code = kCodeDropped;
         if (valid) {
             load_row<D>(a.vals + (size_t)i * D, v);
             k = angle_key_exact<D>(v, a.kp.P);
-            uint16_t code;
             if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-            else code = classify<D>(v, k, s_pr, s_npr, s_dup, a.M, lflags);
+            else code = classify<D>(v, k, s_pr, s_npr, a.M, lflags);
             cand = code == kCodeCandidate;
             a.status[i] = (uint16_t)(((uint32_t)k << 8) | code);
         } else {
 #pragma unroll
             for (int d = 0; d < D; d++) v[d] = 0.0;
         }
+        count_dups(code, k, a.M, s_dup);
         append_candidate<D>(a, cand, v, k, i, lflags, o, an);
     }
 #pragma unroll
@@ -939,12 +1009,15 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
-    SKY_DISPATCH_D(D, (k_filter<DD><<<nblk(a.n, kTile), kThreads, lds, st>>>(a)));
+    const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
+    const unsigned g = nblk(a.n, kTile);
+    if (!g) return;
+    if (a.given_keys) { SKY_DISPATCH_D(D, (k_filter<DD, true><<<g, kThreads, lds, st>>>(a))); }
+    else { SKY_DISPATCH_D(D, (k_filter<DD, false><<<g, kThreads, lds, st>>>(a))); }
 }
 
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
-    const size_t lds = (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
+    const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
     SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<256, kThreads, lds, st>>>(a)));
 }
 
