@@ -516,14 +516,22 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
         SKY_TRY(p.out_cnt.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
         SKY_TRY(p.out_off.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
-        launch_fate_tables(p.mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
-                           p.Kp * p.M, p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(),
-                           p.pruner_fate.as<uint8_t>(), c->st);
+        FateArgs fta{};
+        fta.mt = p.mt;
+        fta.slot_rep = p.slot_rep.as<uint32_t>();
+        fta.slot_src = p.slot_src.as<uint32_t>();
+        fta.alive_l = p.alive_l.as<uint8_t>();
+        fta.alive_g = p.alive_g.as<uint8_t>();
+        fta.KM = p.Kp * p.M;
+        fta.M = p.M;
+        fta.K = p.K;
+        fta.pruner_slot = p.pruner_slot.as<int32_t>();
+        fta.status = p.status.as<uint16_t>();
+        fta.pruner_fate = p.pruner_fate.as<uint8_t>();
+        launch_fate_tables(fta, c->st);             // no stats: those came from the union
         OutArgs oa{};
         oa.status = p.status.as<uint16_t>();
         oa.n = p.n;
-        oa.slot_of = p.slot_of.as<uint32_t>();
-        oa.slot_fate = p.slot_fate.as<uint8_t>();
         oa.pruner_fate = p.pruner_fate.as<uint8_t>();
         oa.M = p.M;
         oa.KM = p.Kp * p.M;

@@ -52,7 +52,7 @@ struct PhaseTimer;
 // multi-GPU import can run on the union while the local shard's state is kept).
 struct Pipe {
     // per tuple / per tile
-    DevBuf status, slot_of, out_cnt, out_off;
+    DevBuf status, out_cnt, out_off;
     // pruners
     DevBuf pmin, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     // candidates (slot order) and sort
@@ -61,7 +61,7 @@ struct Pipe {
     DevBuf alive_l, alive_g, alive_u32, alive_scan, mult;
     // SFS
     DevBuf act, act2, keep, keep_scan, conf_rows, nconf, segs, seg_list, tiles, seg_begin, seg_end, segcnt;
-    DevBuf conf_small, seg_small, slot_fate, pruner_fate, defer, tile_orand, xkeep;
+    DevBuf conf_small, seg_small, pruner_fate, defer, tile_orand, xkeep;
     // global
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers

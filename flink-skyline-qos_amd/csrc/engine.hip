@@ -305,6 +305,7 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     const int ppt = dom16_ppt();
     const uint32_t Ty = 64u * (uint32_t)ppt;              // y rows per rest work item
     const uint32_t Tt = 64u * (uint32_t)kDomTriPPT;       // y rows per tri work item
+    const uint32_t Tx_env = dom16_tx();                   // x rows per work item (0: adaptive)
     std::vector<uint32_t> at;
     for (;;) {
         work.clear();
@@ -325,18 +326,32 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         uint32_t maxch = 0;
         rest_before = 0;
         for (uint32_t k : work) rest_before += cnt[k] - std::min(B, cnt[k]);
+        // x rows per item: a round with few items is latency-bound (one wave scans its
+        // x rows serially), so halve the chunk until ~8k items fill the machine
+        uint32_t Tx = Tx_env ? Tx_env : kDomTx;
+        if (!Tx_env) {
+            auto items_at = [&](uint32_t tx) {
+                uint64_t c = 0;
+                for (uint32_t k : work) {
+                    const uint32_t xk = std::min(B, cnt[k]);
+                    c += (uint64_t)((xk + tx - 1) / tx) * ((xk + Tt - 1) / Tt / 2 + 1 + (cnt[k] - xk + Ty - 1) / Ty);
+                }
+                return c;
+            };
+            while (Tx > 64 && items_at(Tx) < 8192) Tx /= 2;
+        }
         for (uint32_t s = 0; s < (uint32_t)work.size(); s++) {
             const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
             xseg.push_back(SfsSeg{b, xk});
             more |= cnt[k] > xk;
-            maxch = std::max(maxch, (xk + kDomTx - 1) / kDomTx);
+            maxch = std::max(maxch, (xk + Tx - 1) / Tx);
         }
         // items ordered by x chunk, so the first chunks (most dominating rows) run first
         for (uint32_t cx = 0; cx < maxch; cx++)
             for (uint32_t s = 0; s < (uint32_t)work.size(); s++) {
                 const uint32_t k = work[s], b = begin[k], xk = std::min(B, cnt[k]);
-                if (cx * kDomTx >= xk) continue;
-                const uint32_t x0 = b + cx * kDomTx, nx = std::min(kDomTx, xk - cx * kDomTx);
+                if (cx * Tx >= xk) continue;
+                const uint32_t x0 = b + cx * Tx, nx = std::min(Tx, xk - cx * Tx);
                 for (uint32_t y = 0; y < xk; y += Tt) {
                     const uint32_t y0 = b + y, ny = std::min(Tt, xk - y);
                     if (x0 >= y0 + ny) continue;                 // every x after every y
@@ -346,7 +361,7 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
                 }
                 for (uint32_t y = xk; y < cnt[k]; y += Ty) {
                     const uint32_t ny = std::min(Ty, cnt[k] - y);
-                    rest.push_back(DomItem{s, b + y, ny, cx * kDomTx, nx, kDomRest});
+                    rest.push_back(DomItem{s, b + y, ny, cx * Tx, nx, kDomRest});
                     p.sfs_pairs_upper += (int64_t)ny * nx;
                 }
             }
@@ -483,8 +498,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const int KM = p.Kp * p.M;
     const size_t rb64 = row_bytes(true, D);
     const size_t cap = (size_t)n + KM;
-    SKY_TRY(p.status.ensure((size_t)n * 2));
-    SKY_TRY(p.slot_of.ensure((size_t)n * 4));
+    SKY_TRY(p.status.ensure((size_t)tiles * kTile * 2));         // whole tiles: see load_status8
     SKY_TRY(p.rows.ensure(cap * rb64));
     SKY_TRY(p.sortkey.ensure(cap * 8));
     SKY_TRY(p.slot_src.ensure(cap * 4));
@@ -512,7 +526,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.crow = p.rows.as<double>();
     fa.sortkey = p.sortkey.as<uint64_t>();
     fa.slot_src = p.slot_src.as<uint32_t>();
-    fa.slot_of = p.slot_of.as<uint32_t>();
     fa.m_total = p.totals.as<uint32_t>();
     fa.tile_orand = p.tile_orand.as<unsigned long long>();
     fa.orand = p.orand.as<unsigned long long>();
@@ -569,7 +582,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
     SKY_TRY(p.alive_g.ensure(std::max<size_t>(mt, 1)));
-    SKY_TRY(p.slot_fate.ensure(std::max<size_t>(mt, 1)));
     SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
     uint32_t mr = 0;
     if (mt) {
@@ -716,8 +728,25 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
         }
     }
-    launch_fate_tables(mt, p.slot_rep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(), KM,
-                       p.pruner_slot.as<int32_t>(), p.slot_fate.as<uint8_t>(), p.pruner_fate.as<uint8_t>(), st);
+    // stats: summed over slots (unit weights, computed origins) or, for given origins /
+    // weights, over tuples in the count pass
+    const bool slot_stats = in.fate && !in.origin && !in.weights;
+    FateArgs fta{};
+    fta.mt = mt;
+    fta.slot_rep = p.slot_rep.as<uint32_t>();
+    fta.slot_src = p.slot_src.as<uint32_t>();
+    fta.alive_l = p.alive_l.as<uint8_t>();
+    fta.alive_g = p.alive_g.as<uint8_t>();
+    fta.KM = KM;
+    fta.M = p.M;
+    fta.K = p.K;
+    fta.pruner_slot = p.pruner_slot.as<int32_t>();
+    fta.status = p.status.as<uint16_t>();
+    fta.pruner_fate = p.pruner_fate.as<uint8_t>();
+    fta.dup_cnt = p.dup_cnt.as<uint32_t>();
+    fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
+    fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
+    launch_fate_tables(fta, st);
     if (tm) tm->mark(7, st);
     if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
         p.nout = 0;
@@ -731,20 +760,20 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = n;
-    oa.slot_of = p.slot_of.as<uint32_t>();
-    oa.slot_fate = p.slot_fate.as<uint8_t>();
     oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;
     oa.KM = p.Kp * p.M;
     oa.given_origin = in.origin;
     oa.given_w = in.weights;
     oa.K = p.K;
-    oa.lsz = p.lsz.as<unsigned long long>();
-    oa.surv = p.surv.as<unsigned long long>();
+    oa.lsz = slot_stats ? nullptr : p.lsz.as<unsigned long long>();
+    oa.surv = slot_stats ? nullptr : p.surv.as<unsigned long long>();
     oa.out_cnt = p.out_cnt.as<uint32_t>();
     oa.select_local = 0;
     c.ktimer_begin("out", st);
+    c.ktimer_begin("outc", st);
     launch_out_count(oa, st);
+    c.ktimer_end("outc", st, n);
     scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
                   p.scratch.as<uint32_t>(), st);
     c.ktimer_end("out", st, n);
@@ -798,8 +827,6 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = p.n;
-    oa.slot_of = p.slot_of.as<uint32_t>();
-    oa.slot_fate = p.slot_fate.as<uint8_t>();
     oa.pruner_fate = p.pruner_fate.as<uint8_t>();
     oa.M = p.M;
     oa.KM = p.Kp * p.M;
@@ -824,7 +851,9 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     }
     if (d_ids_out || d_origin_out || d_rows_out) {
         c.ktimer_begin("out", c.st);
+        c.ktimer_begin("outw", c.st);
         launch_out_write(oa, c.st);
+        c.ktimer_end("outw", c.st, p.n);
         c.ktimer_end("out", c.st, 0);
     }
     return SKY_OK;

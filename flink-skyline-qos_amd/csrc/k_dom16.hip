@@ -149,6 +149,57 @@ __device__ __forceinline__ void dom_scan(const uint32_t *__restrict__ xs, uint32
     }
 }
 
+// R == 64: the x rows come in vector batches of 64 (lane l loads row b0 + l, the
+// next batch in flight while the current one is compared) and are broadcast to
+// SGPRs by v_readlane: one L2 round trip per 64 rows instead of per R rows, which
+// is what bounds a lone wave's scan (small rounds, few items: latency, not VALU).
+template <int W>
+__device__ __forceinline__ void load_xrow(const uint32_t *__restrict__ xs, uint32_t row, uint32_t (&x)[W]) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(xs + (size_t)row * W);
+#pragma unroll
+    for (int v = 0; v < W / 4; v++) {
+        const uint4 t = src[v];
+        x[4 * v] = t.x; x[4 * v + 1] = t.y; x[4 * v + 2] = t.z; x[4 * v + 3] = t.w;
+    }
+}
+
+template <int W, int PPT, bool DIAG>
+__device__ __forceinline__ void dom_scan_v(const uint32_t *__restrict__ xs, uint32_t nx, int32_t tbase,
+                                           const uint32_t (&y)[PPT][W], uint64_t (&dom)[PPT]) {
+    uint32_t acc[PPT];
+#pragma unroll
+    for (int p = 0; p < PPT; p++) acc[p] = 0xffffffffu;
+    const uint32_t lane = threadIdx.x & 63, last = nx - 1;
+    uint32_t xa[W], xb[W];
+    load_xrow<W>(xs, min(lane, last), xa);
+    for (uint32_t b0 = 0; b0 < nx; b0 += 64) {
+        load_xrow<W>(xs, min(b0 + 64 + lane, last), xb);           // unconditional: clamped past the end
+        const uint32_t cnt = min(64u, nx - b0);
+        for (uint32_t q = 0; q < cnt; q++) {
+            uint32_t x[W];
+#pragma unroll
+            for (int w = 0; w < W; w++) x[w] = __builtin_amdgcn_readlane(xa[w], q);
+            if constexpr (DIAG) dom_row<W, PPT, true>(x, tbase + (int32_t)(b0 + q), y, dom);
+            else dom_row_acc<W, PPT>(x, y, acc);
+            if ((q & 15u) == 15u) {
+                uint64_t all = ~0ull;
+#pragma unroll
+                for (int p = 0; p < PPT; p++) {
+                    if constexpr (!DIAG) dom[p] |= __ballot(acc[p] == 0u);
+                    all &= dom[p];
+                }
+                if (all == ~0ull) return;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < W; w++) xa[w] = xb[w];
+    }
+    if constexpr (!DIAG) {
+#pragma unroll
+        for (int p = 0; p < PPT; p++) dom[p] |= __ballot(acc[p] == 0u);
+    }
+}
+
 template <int W, int PPT, int R, bool DIAG>
 __global__ __launch_bounds__(256, 8) void k_dom16(const uint32_t *__restrict__ rows, const uint32_t *__restrict__ xbuf,
                                                const uint32_t *__restrict__ xcnt, const DomItem *__restrict__ items,
@@ -171,22 +222,22 @@ __global__ __launch_bounds__(256, 8) void k_dom16(const uint32_t *__restrict__ r
     uint32_t y[PPT][W];
     uint64_t dom[PPT];
     uint64_t all = ~0ull;
+    // every y row and dead flag loaded unconditionally (index clamped into the tile),
+    // so the PPT loads are in flight together instead of one round trip each
+    uint32_t dflag[PPT];
 #pragma unroll
     for (int p = 0; p < PPT; p++) {
         const uint32_t q = (uint32_t)(p * 64 + lane);
-        const bool valid = q < it.ny;
-        const uint32_t j = it.y0 + q;
-        const bool d0 = valid ? dead[j] != 0u : true;
-        dom[p] = __ballot(d0);
-        all &= dom[p];
-        if (valid) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(rows + (size_t)j * W);
+        const uint32_t j = it.y0 + (q < it.ny ? q : it.ny - 1);
+        dflag[p] = dead[j];
+        load_xrow<W>(rows, j, y[p]);
+    }
 #pragma unroll
-            for (int v = 0; v < W / 4; v++) {
-                const uint4 t = src[v];
-                y[p][4 * v] = t.x; y[p][4 * v + 1] = t.y; y[p][4 * v + 2] = t.z; y[p][4 * v + 3] = t.w;
-            }
-        } else {
+    for (int p = 0; p < PPT; p++) {
+        const bool valid = (uint32_t)(p * 64 + lane) < it.ny;
+        dom[p] = __ballot(!valid || dflag[p] != 0u);
+        all &= dom[p];
+        if (!valid) {
 #pragma unroll
             for (int w = 0; w < W; w++) y[p][w] = 0xffffffffu;
         }
@@ -198,9 +249,17 @@ __global__ __launch_bounds__(256, 8) void k_dom16(const uint32_t *__restrict__ r
         const uint32_t nplain = t0 < 0 ? ((uint32_t)(-t0) < nx ? (uint32_t)(-t0) : nx) : 0u;
         const int64_t xend = (int64_t)it.y0 + it.ny - it.x0;            // x index past the last y
         const uint32_t nlim = xend < (int64_t)nx ? (uint32_t)(xend > 0 ? xend : 0) : nx;
-        if (nplain) dom_scan<W, PPT, R, false>(xs, nplain, 0, y, dom);
-        if (nlim > nplain)
-            dom_scan<W, PPT, R, true>(xs + (size_t)nplain * W, nlim - nplain, t0 + (int32_t)nplain, y, dom);
+        if constexpr (R == 64) {
+            if (nplain) dom_scan_v<W, PPT, false>(xs, nplain, 0, y, dom);
+            if (nlim > nplain)
+                dom_scan_v<W, PPT, true>(xs + (size_t)nplain * W, nlim - nplain, t0 + (int32_t)nplain, y, dom);
+        } else {
+            if (nplain) dom_scan<W, PPT, R, false>(xs, nplain, 0, y, dom);
+            if (nlim > nplain)
+                dom_scan<W, PPT, R, true>(xs + (size_t)nplain * W, nlim - nplain, t0 + (int32_t)nplain, y, dom);
+        }
+    } else if constexpr (R == 64) {
+        dom_scan_v<W, PPT, false>(xs, nx, 0, y, dom);
     } else {
         dom_scan<W, PPT, R, false>(xs, nx, 0, y, dom);
     }
@@ -293,7 +352,7 @@ void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, ui
 }
 
 // SKY_DOM_PPT in {4, 8} (y rows per lane of the rest tiles; tri tiles use 1), SKY_DOM_R in {2, 4} (x rows per
-// scalar-load batch): tuning knobs, defaults measured on the MI355X
+// scalar-load batch) or 64 (vector batches + v_readlane): tuning knobs, defaults measured on the MI355X
 static int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -305,9 +364,13 @@ int dom16_ppt() {
     }();
     return v;
 }
+uint32_t dom16_tx() {                          // 0: adaptive (sfs_run16)
+    const int t = env_int("SKY_DOM_TX", 0);
+    return t >= 64 && t <= 4096 ? (uint32_t)t : 0u;
+}
 static int dom16_r() {
-    static int v = env_int("SKY_DOM_R", 4) == 2 ? 2 : 4;
-    return v;
+    const int r = env_int("SKY_DOM_R", 4);
+    return r == 2 || r == 64 ? r : 4;
 }
 
 template <int W, int PPT, int R>
@@ -324,6 +387,7 @@ static void dom16_w(int ppt, bool diag, const uint32_t *rows, const uint32_t *xb
 #define DOM16_CASE(P_, R_) \
     if (ppt == P_ && r == R_) { dom16_t<W, P_, R_>(diag, rows, xbuf, xcnt, items, nitems, xcap, dead, st); return; }
     DOM16_CASE(1, 2) DOM16_CASE(1, 4) DOM16_CASE(4, 2) DOM16_CASE(4, 4) DOM16_CASE(8, 2) DOM16_CASE(8, 4)
+    DOM16_CASE(1, 64) DOM16_CASE(4, 64) DOM16_CASE(8, 64)
 #undef DOM16_CASE
 }
 

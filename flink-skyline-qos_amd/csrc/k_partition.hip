@@ -264,8 +264,8 @@ __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part
 }
 
 // A candidate joins the slot list (wave-aggregated append, unordered): f64 row,
-// sort key (partition | score | hash), source index, and slot_of[i] for the
-// per-tuple fate pass.  OR / AND of the keys accumulate in o / an.
+// sort key (partition | score | hash) and source index.  OR / AND of the keys
+// accumulate in o / an.
 template <int D>
 __device__ __forceinline__ void append_candidate(const FilterArgs &a, bool cand, const double (&v)[D], int32_t k,
                                                  uint32_t i, uint32_t &lflags, uint64_t &o, uint64_t &an) {
@@ -284,7 +284,6 @@ __device__ __forceinline__ void append_candidate(const FilterArgs &a, bool cand,
     const uint64_t key = make_sortkey<double, D>(v, (uint32_t)k, lflags);
     a.sortkey[slot] = key;
     a.slot_src[slot] = i;
-    a.slot_of[i] = slot;
     o |= key;
     an &= key;
 }
@@ -485,7 +484,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         const uint64_t key = make_sortkey<double, D>(v, k, lflags);
         a.sortkey[slot] = key;
         a.slot_src[slot] = i;
-        a.slot_of[i] = slot;
         o |= key;
         an &= key;
     }
@@ -563,17 +561,16 @@ __global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
 // block-wide exclusive scan per tile gives order-preserving ranks.
 __device__ __forceinline__ void load_status8(const uint16_t *__restrict__ status, uint32_t n, uint32_t i0,
                                              uint16_t (&st)[kItems]) {
-    if (i0 + kItems <= n) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(status + i0);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    // the status array is allocated to whole tiles (engine.hip), so one clamped
+    // 16-byte load always stays inside it: no partial-tile branch, whose merge
+    // would make the loads of consecutive tiles wait for each other
+    const uint32_t ic = min(i0, (n + kTile - 1) / kTile * kTile - kItems);
+    const uint4 q = *reinterpret_cast<const uint4 *>(status + ic);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            st[2 * k] = (uint16_t)(w[k] & 0xffffu);
-            st[2 * k + 1] = (uint16_t)(w[k] >> 16);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < kItems; k++) st[k] = i0 + k < n ? status[i0 + k] : (uint16_t)0;
+    for (int k = 0; k < 4; k++) {
+        st[2 * k] = i0 + 2 * k < n ? (uint16_t)(w[k] & 0xffffu) : (uint16_t)0;
+        st[2 * k + 1] = i0 + 2 * k + 1 < n ? (uint16_t)(w[k] >> 16) : (uint16_t)0;
     }
 }
 
@@ -771,122 +768,193 @@ __global__ __launch_bounds__(kThreads) void k_rep_mult(uint32_t mt, const uint32
 }
 
 // ---- output: per tuple local / global membership ------------------------------
-// fate byte = inL | inG << 1, precomputed per candidate slot and per (partition,
-// pruner) duplicate group, so the per-tuple pass does at most one lookup.
-__global__ __launch_bounds__(kThreads) void k_fate_tables(uint32_t mt, const uint32_t *__restrict__ slot_rep,
-                                                          const uint8_t *__restrict__ alive_l,
-                                                          const uint8_t *__restrict__ alive_g, int KM,
-                                                          const int32_t *__restrict__ pruner_slot,
-                                                          uint8_t *__restrict__ slot_fate,
-                                                          uint8_t *__restrict__ pruner_fate) {
+// fate = inL | inG << 1.  A candidate's fate is written into its own status word
+// (code kCodeFate0 + fate, from its slot's representative), a duplicate group's per
+// (partition, pruner) into pruner_fate, so the per-tuple passes read the status
+// word and at most one LDS byte: no dependent global lookups.
+//
+// Stats (|L_k|, survivors_k) for unit weights and computed origins: every stream
+// tuple in L_k is a candidate (one slot, weight 1) or a duplicate of a pruner
+// (weight dup_cnt), so they are summed over slots here instead of over tuples.
+__global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
+    __shared__ unsigned long long s_l[kMaxK], s_s[kMaxK];
+    const bool stats = a.lsz != nullptr;
+    if (stats) {
+        for (int q = threadIdx.x; q < a.K; q += kThreads) { s_l[q] = 0; s_s[q] = 0; }
+        __syncthreads();
+    }
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    if (j < mt) {
-        const uint32_t r = slot_rep[j];
-        slot_fate[j] = (uint8_t)((alive_l[r] ? 1 : 0) | (alive_g[r] ? 2 : 0));
-    } else if (j - mt < (uint32_t)KM) {
-        const uint32_t q = j - mt;
-        const int32_t ps = pruner_slot[q];
-        uint8_t f = 0;
-        if (ps >= 0) {
-            const uint32_t r = slot_rep[ps];
-            f = (uint8_t)((alive_l[r] ? 1 : 0) | (alive_g[r] ? 2 : 0));
+    int k = -1;
+    unsigned long long w = 0;
+    uint32_t f = 0;
+    if (j < a.mt) {
+        const uint32_t src = a.slot_src[j];
+        if (!(src & 0x80000000u)) {                    // (appended pruner slots: below)
+            const uint32_t r = a.slot_rep[j];
+            f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            const uint16_t s0 = a.status[src];
+            a.status[src] = (uint16_t)((s0 & 0xff00u) | (kCodeFate0 + f));
+            k = s0 >> 8;
+            w = 1;
         }
-        pruner_fate[q] = f;
+    } else if (j - a.mt < (uint32_t)a.KM) {
+        const uint32_t q = j - a.mt;
+        const int32_t ps = a.pruner_slot[q];
+        if (ps >= 0) {
+            const uint32_t r = a.slot_rep[ps];
+            f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            k = (int)(q / (uint32_t)a.M);
+            w = stats ? a.dup_cnt[q] : 0u;
+        }
+        a.pruner_fate[q] = (uint8_t)f;
+    }
+    if (stats) {
+        if (k >= 0 && (f & 1u)) {
+            atomicAdd(&s_l[k], w);
+            if (f & 2u) atomicAdd(&s_s[k], w);
+        }
+        __syncthreads();
+        const size_t sh = (size_t)(blockIdx.x % kStatShards) * a.K;
+        for (int q = threadIdx.x; q < a.K; q += kThreads) {
+            if (s_l[q]) atomicAdd(&a.lsz[sh + q], s_l[q]);
+            if (s_s[q]) atomicAdd(&a.surv[sh + q], s_s[q]);
+        }
     }
 }
 
+// fate of one tuple from its status word (candidates: after k_fate_tables), branch
+// free: one unconditional LDS byte read (index 0 when unused)
+__device__ __forceinline__ uint32_t tuple_fate(uint16_t st, const uint8_t *s_pf, int M) {
+    const uint32_t code = st & 0xffu;
+    const bool dup = code != kCodeDropped && code < kCodeFate0;
+    const uint32_t pf = s_pf[dup ? (uint32_t)(st >> 8) * (uint32_t)M + code - 1u : 0u];
+    const uint32_t cf = code >= kCodeFate0 && code != kCodeCandidate ? code - kCodeFate0 : 0u;
+    return dup ? pf : cf;
+}
+
 // Count pass: kOutTPB tiles per workgroup, every tile's status words loaded up front
-// (the pass is latency-bound per workgroup otherwise); per-tile selected counts via
-// wave sums, per-(shard, origin) stats flushed once per workgroup.
+// (the pass is latency-bound per workgroup otherwise); per-tile selected counts by
+// ballot + popcount.  Stats (|L_k|, survivors_k): unit weights by wave ballots per
+// origin (see below); given weights (GW) per thread over all its tuples, one wave
+// add when the threads agree on the origin; flushed once per workgroup into
+// per-shard accumulators.  GO / GW: given origins / weights.
 constexpr int kOutTPB = 4;
 
+template <bool GO, bool GW>
 __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
     __shared__ unsigned long long s_lsz[kMaxK];
     __shared__ unsigned long long s_surv[kMaxK];
     __shared__ uint8_t s_pf[2048];
     __shared__ uint32_t s_tw[kOutTPB][kThreads / 64];
     const bool stats = a.lsz != nullptr;
-    if (stats)
-        for (int q = threadIdx.x; q < a.K; q += kThreads) { s_lsz[q] = 0; s_surv[q] = 0; }
-    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     const uint32_t t0 = blockIdx.x * kOutTPB;
+    const uint32_t nl = a.n - 1;
+    // the status words first, then the small tables: all in flight together (one
+    // round trip per workgroup, not one for the tables and another for the stream)
     uint16_t st[kOutTPB][kItems];
 #pragma unroll
     for (int t = 0; t < kOutTPB; t++) {
         const uint32_t i0 = (t0 + t) * kTile + threadIdx.x * kItems;
-        if (t0 + t < ntiles) load_status8(a.status, a.n, i0, st[t]);
-        else {
-#pragma unroll
-            for (int k = 0; k < kItems; k++) st[t][k] = 0;
-        }
+        load_status8(a.status, a.n, i0, st[t]);                     // past the last tile: all masked
     }
+    if (stats)
+        for (int q = threadIdx.x; q < a.K; q += kThreads) { s_lsz[q] = 0; s_surv[q] = 0; }
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     __syncthreads();                                   // s_pf ready
     const int shift = a.select_local ? 0 : 1;
     const int lane = threadIdx.x & 63;
+    // !GW (unit weights): wave-wide counts by ballot + popcount (SALU, no cross-lane
+    // shuffles): the wave's selected tuples of its first origin o0 are counted
+    // together, tuples of any other origin by per-lane LDS atomics
+    int o0 = -1;                                       // wave-uniform
+    unsigned long long cl = 0, cg = 0;                 // wave-uniform counts for o0
+    // GW: per-thread (origin, weights) accumulation, reduced below
+    int o1 = -1;
+    bool mixed = false;
+    unsigned long long wl = 0, wg = 0;
 #pragma unroll
     for (int t = 0; t < kOutTPB; t++) {
         const uint32_t i0 = (t0 + t) * kTile + threadIdx.x * kItems;
-        uint8_t fate[kItems];
-        uint32_t nsel = 0;
+        uint32_t fate[kItems];
+        uint32_t nsel = 0;                             // wave-uniform
 #pragma unroll
         for (int k = 0; k < kItems; k++) {
-            const uint32_t code = st[t][k] & 0xff;
-            uint8_t f = 0;
-            if (i0 + k < a.n) {
-                if (code == kCodeCandidate) f = a.slot_fate[a.slot_of[i0 + k]];
-                else if (code != kCodeDropped) f = s_pf[(st[t][k] >> 8) * a.M + (code - 1)];
-            }
-            fate[k] = f;
-            nsel += (f >> shift) & 1u;
+            fate[k] = tuple_fate(st[t][k], s_pf, a.M);             // past n: status 0, fate 0
+            nsel += (uint32_t)__popcll(__ballot((fate[k] >> shift) & 1u));
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) nsel += __shfl_xor(nsel, o, 64);
         if (lane == 0) s_tw[t][threadIdx.x >> 6] = nsel;
         if (a.row_flags) {
 #pragma unroll
             for (int k = 0; k < kItems; k++)
-                if (i0 + k < a.n) a.row_flags[i0 + k] = fate[k];
+                if (i0 + k < a.n) a.row_flags[i0 + k] = (uint8_t)fate[k];
         }
         if (stats) {
-            // per thread: one (origin, |L| weight, |G| weight) triple when its tuples
-            // share an origin (else per-tuple LDS atomics); per wave: one add when uniform
-            int o1 = -1;
-            bool mixed = false;
-            unsigned long long wl = 0, wg = 0;
+#pragma unroll
             for (int k = 0; k < kItems; k++) {
-                if (!(fate[k] & 1)) continue;
-                const uint32_t i = i0 + k;
-                const int o = a.given_origin ? a.given_origin[i] : (int)(st[t][k] >> 8);
-                const unsigned long long w = a.given_w ? (unsigned long long)a.given_w[i] : 1ull;
-                if (o1 < 0) o1 = o;
-                if (o == o1 && !mixed) {
-                    wl += w;
-                    if (fate[k] & 2) wg += w;
+                const bool sel = fate[k] & 1u;
+                const int o = GO ? a.given_origin[min(i0 + k, nl)] : (int)(st[t][k] >> 8);
+                if constexpr (!GW) {
+                    const uint64_t bl = __ballot(sel);
+                    if (bl) {                                          // wave-uniform
+                        if (o0 < 0) o0 = __builtin_amdgcn_readlane(o, __ffsll((unsigned long long)bl) - 1);
+                        const uint64_t bad = __ballot(sel && o != o0);
+                        cl += (unsigned long long)__popcll(bl & ~bad);
+                        cg += (unsigned long long)__popcll(__ballot(sel && (fate[k] & 2u)) & ~bad);
+                        if (bad && sel && o != o0) {
+                            atomicAdd(&s_lsz[o], 1ull);
+                            if (fate[k] & 2u) atomicAdd(&s_surv[o], 1ull);
+                        }
+                    }
                 } else {
-                    mixed = true;
-                    atomicAdd(&s_lsz[o], w);
-                    if (fate[k] & 2) atomicAdd(&s_surv[o], w);
+                    const unsigned long long w = (unsigned long long)a.given_w[min(i0 + k, nl)];
+                    o1 = sel && o1 < 0 ? o : o1;
+                    mixed |= sel && o != o1;
+                    wl += sel ? w : 0ull;
+                    wg += sel && (fate[k] & 2u) ? w : 0ull;
                 }
             }
-            const bool has = o1 >= 0;
-            const uint64_t act = __ballot(has);
-            if (act) {
-                const int o0 = __shfl(o1, __ffsll((unsigned long long)act) - 1, 64);
-                if (__ballot(has && o1 != o0) == 0ull) {
-#pragma unroll
-                    for (int sh = 32; sh >= 1; sh >>= 1) {
-                        wl += __shfl_xor(wl, sh, 64);
-                        wg += __shfl_xor(wg, sh, 64);
-                    }
-                    if (lane == 0) {
-                        atomicAdd(&s_lsz[o0], wl);
-                        if (wg) atomicAdd(&s_surv[o0], wg);
-                    }
-                } else if (has) {
-                    atomicAdd(&s_lsz[o1], wl);
-                    if (wg) atomicAdd(&s_surv[o1], wg);
+        }
+    }
+    if (stats && !GW) {
+        if (lane == 0 && o0 >= 0) {
+            atomicAdd(&s_lsz[o0], cl);
+            if (cg) atomicAdd(&s_surv[o0], cg);
+        }
+    }
+    if (stats && GW) {
+        if (mixed) {                                   // this thread saw two origins: per tuple
+#pragma unroll 1
+            for (int t = 0; t < kOutTPB; t++) {
+                const uint32_t i0 = (t0 + t) * kTile + threadIdx.x * kItems;
+                for (int k = 0; k < kItems; k++) {
+                    const uint32_t f = tuple_fate(st[t][k], s_pf, a.M);
+                    if (!(f & 1u)) continue;
+                    const int o = GO ? a.given_origin[i0 + k] : (int)(st[t][k] >> 8);
+                    const unsigned long long w = (unsigned long long)a.given_w[i0 + k];
+                    atomicAdd(&s_lsz[o], w);
+                    if (f & 2u) atomicAdd(&s_surv[o], w);
                 }
+            }
+        }
+        const bool has = o1 >= 0 && !mixed;
+        unsigned long long rl = has ? wl : 0ull, rg = has ? wg : 0ull;
+        const uint64_t act = __ballot(has);
+        if (act) {                                     // wave-uniform
+            const int oa0 = __shfl(o1, __ffsll((unsigned long long)act) - 1, 64);
+            if (__ballot(has && o1 != oa0) == 0ull) {
+#pragma unroll
+                for (int sh = 32; sh >= 1; sh >>= 1) {
+                    rl += __shfl_xor(rl, sh, 64);
+                    rg += __shfl_xor(rg, sh, 64);
+                }
+                if (lane == 0) {
+                    atomicAdd(&s_lsz[oa0], rl);
+                    if (rg) atomicAdd(&s_surv[oa0], rg);
+                }
+            } else if (has) {
+                atomicAdd(&s_lsz[o1], rl);
+                if (rg) atomicAdd(&s_surv[o1], rg);
             }
         }
     }
@@ -907,43 +975,34 @@ __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
     }
 }
 
-// Write pass: one tile per workgroup; the tile's selected ids / origins are staged
-// in LDS in stream order, then written as one contiguous, coalesced run.
 __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     __shared__ uint8_t s_pf[2048];
     __shared__ uint32_t s_w[kThreads / 64];
     __shared__ int64_t s_oid[kTile];
     __shared__ int32_t s_oorg[kTile];
-    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     const uint32_t tile = blockIdx.x;
     const uint32_t i0 = tile * kTile + threadIdx.x * kItems;
+    // status, ids and the pruner-fate table in flight together
     uint16_t st[kItems];
     load_status8(a.status, a.n, i0, st);
     int64_t idv[kItems];
-    if (a.ids && i0 + kItems <= a.n) {
-        const longlong2 *q = reinterpret_cast<const longlong2 *>(a.ids + i0);
+    if (a.ids) {
+        // one load per id, index clamped into [0, n) (no partial-tile branch); ids
+        // past n are never selected
 #pragma unroll
-        for (int k = 0; k < kItems / 2; k++) {
-            const longlong2 x = q[k];
-            idv[2 * k] = x.x;
-            idv[2 * k + 1] = x.y;
-        }
+        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k, a.n - 1)];
     } else {
 #pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = i0 + k < a.n ? (a.ids ? a.ids[i0 + k] : (int64_t)(i0 + k)) : 0;
+        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k);
     }
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     __syncthreads();                                   // s_pf ready
     const int shift = a.select_local ? 0 : 1;
     uint8_t fate[kItems];
     uint32_t nsel = 0;
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-        const uint32_t code = st[k] & 0xff;
-        uint8_t f = 0;
-        if (i0 + k < a.n) {
-            if (code == kCodeCandidate) f = a.slot_fate[a.slot_of[i0 + k]];
-            else if (code != kCodeDropped) f = s_pf[(st[k] >> 8) * a.M + (code - 1)];
-        }
+        const uint8_t f = tuple_fate(st[k], s_pf, a.M);
         fate[k] = f;
         nsel += (f >> shift) & 1u;
     }
@@ -1025,11 +1084,9 @@ void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
     SKY_DISPATCH_D(D, (k_append_pruners<DD><<<1, kThreads, 0, st>>>(a)));
 }
 
-void launch_fate_tables(uint32_t mt, const uint32_t *slot_rep, const uint8_t *alive_l, const uint8_t *alive_g, int KM,
-                        const int32_t *pruner_slot, uint8_t *slot_fate, uint8_t *pruner_fate, hipStream_t st) {
-    const size_t tot = (size_t)mt + KM;
-    if (tot) k_fate_tables<<<nblk(tot, kThreads), kThreads, 0, st>>>(mt, slot_rep, alive_l, alive_g, KM, pruner_slot,
-                                                                     slot_fate, pruner_fate);
+void launch_fate_tables(const FateArgs &a, hipStream_t st) {
+    const size_t tot = (size_t)a.mt + a.KM;
+    if (tot) k_fate_tables<<<nblk(tot, kThreads), kThreads, 0, st>>>(a);
 }
 
 void launch_gather_runs(int D, bool f64, const RepArgs &a, hipStream_t st) {
@@ -1058,7 +1115,13 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
                                                                 pr_entries, mult);
 }
 void launch_out_count(const OutArgs &a, hipStream_t st) {
-    if (a.n) k_out_count<<<nblk(nblk(a.n, kTile), kOutTPB), kThreads, 0, st>>>(a);
+    if (!a.n) return;
+    const unsigned g = nblk(nblk(a.n, kTile), kOutTPB);
+    const bool go = a.given_origin != nullptr, gw = a.given_w != nullptr;
+    if (go && gw) k_out_count<true, true><<<g, kThreads, 0, st>>>(a);
+    else if (go) k_out_count<true, false><<<g, kThreads, 0, st>>>(a);
+    else if (gw) k_out_count<false, true><<<g, kThreads, 0, st>>>(a);
+    else k_out_count<false, false><<<g, kThreads, 0, st>>>(a);
 }
 void launch_out_write(const OutArgs &a, hipStream_t st) {
     if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);

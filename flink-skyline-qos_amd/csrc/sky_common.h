@@ -15,6 +15,7 @@ constexpr int kStatShards = 1024;             // |L_k| / survivors_k accumulator
 // per-tuple status word (u16): high byte = partition key, low byte = code
 constexpr uint16_t kCodeDropped = 0;          // dominated by a pruner / key never queried
 constexpr uint16_t kCodeCandidate = 255;      // goes to sort + SFS
+constexpr uint16_t kCodeFate0 = 251;          // candidate after the fate pass: 251 + (inL | inG << 1)
 // codes 1..254: exact duplicate of pruner (code-1) of its partition
 
 // flag bits (device u32)

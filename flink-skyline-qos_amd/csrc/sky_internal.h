@@ -60,7 +60,6 @@ struct FilterArgs {
     double *crow;                 // [n + Kp*M][pad(D)]
     uint64_t *sortkey;
     uint32_t *slot_src;
-    uint32_t *slot_of;            // [n] (written for candidates only)
     uint32_t *m_total;
     unsigned long long *tile_orand;   // [tiles][2] per-tile {OR, AND} of the sort keys
     unsigned long long *orand;        // device {OR, AND} (deferred tuples add atomically)
@@ -93,8 +92,18 @@ struct AppendArgs {
     unsigned long long *orand;
 };
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st);
-void launch_fate_tables(uint32_t mt, const uint32_t *slot_rep, const uint8_t *alive_l, const uint8_t *alive_g, int KM,
-                        const int32_t *pruner_slot, uint8_t *slot_fate, uint8_t *pruner_fate, hipStream_t st);
+struct FateArgs {
+    uint32_t mt;                          // slots (candidates + appended pruner slots)
+    const uint32_t *slot_rep, *slot_src;
+    const uint8_t *alive_l, *alive_g;     // per representative
+    int KM, M, K;
+    const int32_t *pruner_slot;
+    uint16_t *status;                     // candidates' words rewritten: kCodeFate0 + fate
+    uint8_t *pruner_fate;
+    const uint32_t *dup_cnt;              // stats only
+    unsigned long long *lsz, *surv;       // [kStatShards][K] stat shards, or nullptr: no stats
+};
+void launch_fate_tables(const FateArgs &a, hipStream_t st);
 
 struct RepArgs {
     uint32_t mt;                  // sorted slots
@@ -121,8 +130,6 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
 struct OutArgs {
     const uint16_t *status;
     uint32_t n;
-    const uint32_t *slot_of;      // candidate slot per tuple
-    const uint8_t *slot_fate;     // [mt] inL | inG << 1
     const uint8_t *pruner_fate;   // [Kp*M]
     int M, KM;
     const int32_t *given_origin;  // per tuple origin (nullptr: partition key)
@@ -180,7 +187,8 @@ struct DomItem { uint32_t seg, y0, ny, x0, nx, flags; };
 constexpr uint32_t kDomDiag = 1u;             // x and y ranges overlap: only x before y
 constexpr uint32_t kDomRest = 2u;             // x from xbuf[seg] (X'), count from xcnt[seg]
 int dom16_ppt();                              // y rows per lane (work item = 64 * ppt y rows)
-constexpr uint32_t kDomTx = 512u;             // x rows per work item
+uint32_t dom16_tx();                          // x rows per work item: SKY_DOM_TX, 0 = adaptive
+constexpr uint32_t kDomTx = 512u;             // largest adaptive x rows per work item
 int dom16_words(int D);
 void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, uint32_t *out, hipStream_t st);
 constexpr int kDomTriPPT = 1;                 // tri tiles: 64 y per wave (latency-bound, many waves)

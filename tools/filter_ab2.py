@@ -1,11 +1,14 @@
-"""Interleaved A/B of k_filter variants in ONE process on one 100M-tuple 8D stream
-(box-to-box clock differences cancel): VARIANTS="SKY_FILTER_XP=0;SKY_FILTER_XP=1,..."
-(';' between variants, ',' between the variables of one), ALGO (default mr-angle).
-Prints the median filter-kernel time of each variant over REPS rounds."""
+"""Interleaved A/B of engine variants (environment knobs read per launch) in ONE
+process on one synthetic 8D stream (box-to-box clock differences cancel):
+VARIANTS="SKY_DOM_R=4;SKY_DOM_R=64,..." (';' between variants, ',' between the
+variables of one), ALGO (default mr-angle), DIST, N.  Prints per variant the median
+over REPS rounds of each kernel timer in KERNELS (default filter) and of the whole
+query (host wall clock, synchronised)."""
 import json
 import os
 import statistics
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "flink-skyline-qos_amd"))
@@ -26,7 +29,8 @@ eng.synth_dev(os.environ.get("DIST", "anti_correlated"), n, vals, ids, seed=1242
 eng.query_dev(ids, vals, oi, oo, n)
 eng.sync()
 ref = oi[:10].clone()
-times = {v: [] for v in variants}
+kernels = os.environ.get("KERNELS", "filter").split(",")
+times = {v: {k: [] for k in kernels + ["query"]} for v in variants}
 for _ in range(reps):
     for v in variants:
         for kv in v.split(","):
@@ -34,12 +38,15 @@ for _ in range(reps):
             os.environ[k] = x
         eng.profile(True)
         eng.profile_reset()
+        t0 = time.perf_counter()
         for _ in range(2):
             g = eng.query_dev(ids, vals, oi, oo, n)
         eng.sync()
-        ms, la, _ = eng.kernel_time("filter")
+        times[v]["query"].append((time.perf_counter() - t0) * 500.0)
+        for kn in kernels:
+            ms, la, _ = eng.kernel_time(kn)
+            times[v][kn].append(ms / max(la, 1) if kn == "filter" else ms / 2)
         eng.profile(False)
-        times[v].append(ms / la)
         for kv in v.split(","):
             os.environ.pop(kv.split("=")[0])
 # the box's streaming reference: torch's own reduction over the same 6.4 GB
@@ -52,7 +59,9 @@ for _ in range(5):
     en.record()
     torch.cuda.synchronize()
     tsum.append(st.elapsed_time(en))
-res = {v: {"filter_ms_median": statistics.median(t), "min": min(t), "GBps": n * 66 / statistics.median(t) / 1e6}
-       for v, t in times.items()}
+res = {v: {k: round(statistics.median(t), 4) for k, t in kt.items()} for v, kt in times.items()}
+for v in res:
+    if "filter" in res[v]:
+        res[v]["filter_GBps"] = round(n * 66 / res[v]["filter"] / 1e6)
 res["torch_sum_ref"] = {"ms_median": statistics.median(tsum), "GBps": n * D * 8 / statistics.median(tsum) / 1e6}
 print(json.dumps(res, indent=1))
