@@ -639,3 +639,163 @@ int sky_profile_reset(sky_ctx *c) {
 }
 
 }  // extern "C"
+
+// ---- bulk CSV ingest (k_csv.hip) ---------------------------------------------
+// ServiceTuple.fromString (ServiceTuple.java:89-104) + filter(nonNull) (FlinkSkyline.java:103)
+// + Long.parseLong(id) (FlinkSkyline.java:276), over a whole device-resident buffer of records.
+int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d_ids_out, double *d_values_out,
+                      int64_t cap, int64_t *n_out, int64_t *counts_out, uint8_t *d_status_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && n_out && (nbytes == 0 || d_text), "null argument");
+    ARG_CHECK(nbytes >= 0 && nbytes < ((int64_t)1 << 40), "nbytes out of range");
+    ARG_CHECK(cap >= 0, "cap out of range");
+    SKY_TRY(bind(c));
+    const uint8_t *text = reinterpret_cast<const uint8_t *>(d_text);
+    const int64_t nb = csv_chunks(nbytes);
+    const int D = c->D;
+    SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 16));
+    SKY_TRY(c->csv_scr.ensure(scan_scratch_words((size_t)std::max<int64_t>(nb, 1)) * 4));
+    SKY_TRY(c->csv_counts.ensure(64));
+    uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1);
+    uint32_t h_nl = 0;
+    uint8_t last = '\n';
+    if (nb) {
+        c->ktimer_begin("k_csv_index", c->st);
+        launch_csv_nl_count(text, nbytes, blk, c->st);
+        scan_excl_u32(blk, blk_off, (size_t)nb, d_nl, c->csv_scr.as<uint32_t>(), c->st);
+        HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
+    }
+    const int64_t nl = h_nl;
+    const int64_t nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
+    const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
+    SKY_TRY(c->csv_lines.ensure((size_t)std::max<int64_t>(nl, 1) * 8));
+    SKY_TRY(c->csv_status.ensure(nr1));
+    if (nl) launch_csv_nl_write(text, nbytes, blk_off, c->csv_lines.as<int64_t>(), c->st);
+    if (nb) c->ktimer_end("k_csv_index", c->st, nbytes);
+    const bool direct = cap >= nrec && d_ids_out && d_values_out;
+    int64_t *pid = d_ids_out;
+    double *pval = d_values_out;
+    if (!direct) {
+        SKY_TRY(c->csv_ids.ensure(nr1 * 8));
+        SKY_TRY(c->csv_vals.ensure(nr1 * D * 8));
+        pid = c->csv_ids.as<int64_t>();
+        pval = c->csv_vals.as<double>();
+    }
+    unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(d_cnt, 0, 32, c->st));
+    c->ktimer_begin("k_csv_parse", c->st);
+    launch_csv_parse(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval, c->csv_status.as<uint8_t>(),
+                     d_cnt, c->st);
+    c->ktimer_end("k_csv_parse", c->st, nrec);
+    HIP_TRY(hipGetLastError());
+    unsigned long long h_cnt[4] = {};
+    HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 32, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    const int64_t nbad = (int64_t)(h_cnt[1] + h_cnt[2] + h_cnt[3]);
+    const int64_t nacc = nrec - nbad;
+    if (counts_out) {
+        counts_out[0] = nrec;
+        for (int k = 1; k < 4; k++) counts_out[k] = (int64_t)h_cnt[k];
+    }
+    *n_out = nacc;
+    if (d_status_out && nrec)
+        HIP_TRY(hipMemcpyAsync(d_status_out, c->csv_status.p, (size_t)nrec, hipMemcpyDeviceToDevice, c->st));
+    if (nacc > cap) {
+        HIP_TRY(hipStreamSynchronize(c->st));
+        set_error("output capacity too small for the accepted records");
+        return SKY_E_CAPACITY;
+    }
+    ARG_CHECK(nacc == 0 || (d_ids_out && d_values_out), "null output buffers");
+    if (nbad > 0 || !direct) {
+        if (direct) {   // rows were parsed in place: move them aside, then compact back
+            SKY_TRY(c->csv_ids.ensure(nr1 * 8));
+            SKY_TRY(c->csv_vals.ensure(nr1 * D * 8));
+            HIP_TRY(hipMemcpyAsync(c->csv_ids.p, d_ids_out, (size_t)nrec * 8, hipMemcpyDeviceToDevice, c->st));
+            HIP_TRY(hipMemcpyAsync(c->csv_vals.p, d_values_out, (size_t)nrec * D * 8, hipMemcpyDeviceToDevice,
+                                   c->st));
+        }
+        SKY_TRY(c->csv_keep.ensure(nr1 * 4));
+        SKY_TRY(c->csv_pos.ensure(nr1 * 4 + 16));
+        SKY_TRY(c->csv_scr.ensure(scan_scratch_words(nr1) * 4));
+        launch_csv_keep(c->csv_status.as<uint8_t>(), nrec, c->csv_keep.as<uint32_t>(), c->st);
+        scan_excl_u32(c->csv_keep.as<uint32_t>(), c->csv_pos.as<uint32_t>(), (size_t)nrec,
+                      c->csv_pos.as<uint32_t>() + nr1, c->csv_scr.as<uint32_t>(), c->st);
+        launch_csv_compact(c->csv_status.as<uint8_t>(), c->csv_pos.as<uint32_t>(), nrec, D, c->csv_ids.as<int64_t>(),
+                           c->csv_vals.as<double>(), d_ids_out, d_values_out, c->st);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (c->profile) c->ktimer_collect();
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_parse_csv(sky_ctx *c, const char *text, int64_t nbytes, int64_t *ids_out, double *values_out, int64_t cap,
+                  int64_t *n_out, int64_t *counts_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && n_out && (nbytes == 0 || text), "null argument");
+    ARG_CHECK(nbytes >= 0 && nbytes < ((int64_t)1 << 40), "nbytes out of range");
+    SKY_TRY(bind(c));
+    SKY_TRY(c->csv_text.ensure((size_t)std::max<int64_t>(nbytes, 1)));
+    if (nbytes) HIP_TRY(hipMemcpyAsync(c->csv_text.p, text, (size_t)nbytes, hipMemcpyHostToDevice, c->st));
+    // records are at most nbytes/2 + 1 ("x\n" is the shortest non-empty record)
+    const int64_t rmax = nbytes / 2 + 1;
+    SKY_TRY(c->h_ids.ensure((size_t)rmax * 8));
+    SKY_TRY(c->h_vals.ensure((size_t)rmax * c->D * 8));
+    int64_t n = 0;
+    SKY_TRY(sky_parse_csv_dev(c, c->csv_text.as<char>(), nbytes, c->h_ids.as<int64_t>(), c->h_vals.as<double>(), rmax,
+                              &n, counts_out, nullptr));
+    *n_out = n;
+    if (n > cap) {
+        set_error("output capacity too small for the accepted records");
+        return SKY_E_CAPACITY;
+    }
+    ARG_CHECK(n == 0 || (ids_out && values_out), "null output buffers");
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(ids_out, c->h_ids.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipMemcpyAsync(values_out, c->h_vals.p, (size_t)n * c->D * 8, hipMemcpyDeviceToHost, c->st));
+    }
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_format_csv_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int64_t n, char *d_text, int64_t cap,
+                       int64_t *nbytes_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && nbytes_out && (n == 0 || (d_ids && d_values)), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
+    SKY_TRY(bind(c));
+    const size_t n1 = (size_t)std::max<int64_t>(n, 1);
+    SKY_TRY(c->csv_keep.ensure(n1 * 4));
+    SKY_TRY(c->csv_pos.ensure(n1 * 4 + 16));
+    SKY_TRY(c->csv_scr.ensure(scan_scratch_words(n1) * 4));
+    SKY_TRY(c->csv_counts.ensure(64));
+    unsigned long long *d_te = c->csv_counts.as<unsigned long long>();
+    HIP_TRY(hipMemsetAsync(d_te, 0, 16, c->st));
+    launch_csv_fmt_len(d_ids, d_values, n, c->D, c->csv_keep.as<uint32_t>(), d_te, c->st);
+    unsigned long long h_te[2] = {};
+    HIP_TRY(hipMemcpyAsync(h_te, d_te, 16, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (h_te[1]) {
+        set_error("sky_format_csv_dev formats integral values |v| < 2^53 only");
+        return SKY_E_ARG;
+    }
+    *nbytes_out = (int64_t)h_te[0];
+    if (!d_text || cap == 0) return SKY_OK;
+    if ((int64_t)h_te[0] > cap) {
+        set_error("text capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    ARG_CHECK(h_te[0] < 0xffffffffull, "formatted text must stay below 4 GiB per call");
+    scan_excl_u32(c->csv_keep.as<uint32_t>(), c->csv_pos.as<uint32_t>(), (size_t)n, c->csv_pos.as<uint32_t>() + n1,
+                  c->csv_scr.as<uint32_t>(), c->st);
+    launch_csv_fmt_write(d_ids, d_values, n, c->D, c->csv_pos.as<uint32_t>(), reinterpret_cast<uint8_t *>(d_text),
+                         c->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}

@@ -207,4 +207,19 @@ void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id
 void synth_host(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
                 int64_t *ids);
 
+// ---- k_csv.hip ----
+int64_t csv_chunks(int64_t nbytes);
+void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, hipStream_t st);
+void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
+                         hipStream_t st);
+void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
+                      int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, hipStream_t st);
+void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st);
+void launch_csv_compact(const uint8_t *status, const uint32_t *pos, int64_t n, int D, const int64_t *ids_in,
+                        const double *vals_in, int64_t *ids_out, double *vals_out, hipStream_t st);
+void launch_csv_fmt_len(const int64_t *ids, const double *vals, int64_t n, int D, uint32_t *len,
+                        unsigned long long *tot_err, hipStream_t st);
+void launch_csv_fmt_write(const int64_t *ids, const double *vals, int64_t n, int D, const uint32_t *off,
+                          uint8_t *text, hipStream_t st);
+
 }  // namespace sky

@@ -27,6 +27,8 @@ SKY_E_NAN = -4
 SKY_E_NOMEM = -5
 SKY_E_NOLIB = -6
 
+CSV_OK, CSV_MALFORMED, CSV_BAD_ID, CSV_ARITY = 0, 1, 2, 3
+
 ALGO_DIM, ALGO_GRID, ALGO_ANGLE = 0, 1, 2
 ALGOS = {"mr-dim": ALGO_DIM, "mr-grid": ALGO_GRID, "mr-angle": ALGO_ANGLE}
 SEM_REFERENCE, SEM_COMPLETE = 0, 1
@@ -64,6 +66,9 @@ SIGNATURES = {
     "sky_export_local_dev": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_export_copy_dev": [c_p, c_p, c_p, c_p, c_i64],
     "sky_import_union_dev": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, P_i64],
+    "sky_parse_csv_dev": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64, c_p],
+    "sky_parse_csv": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64],
+    "sky_format_csv_dev": [c_p, c_p, c_p, c_i64, c_p, c_i64, P_i64],
     "sky_synth_dev": [c_p, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_synth": [c_int, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_dev_alloc": [c_p, c_i64, ctypes.POINTER(c_p)],

@@ -134,6 +134,36 @@ class SkylineEngine:
             dist = _abi.DISTS[dist]
         check(lib().sky_synth_dev(self.h, dist, dmin, dmax, seed, id0, n, _tptr(d_values), _tptr(d_ids)))
 
+    # ---- bulk CSV ingest (ServiceTuple.fromString over raw records, ServiceTuple.java:89-104)
+    def parse_csv(self, text):
+        """Host bytes -> (ids int64[n], values f64[n, D], counts int64[4]); counts =
+        [records, malformed, bad id, wrong arity].  Decoded on the device."""
+        b = bytes(text)
+        rmax = len(b) // 2 + 1
+        ids = np.empty(rmax, np.int64)
+        vals = np.empty((rmax, self.dims), np.float64)
+        n = ctypes.c_int64(0)
+        cnt = np.zeros(4, np.int64)
+        check(lib().sky_parse_csv(self.h, b, len(b), _ptr(ids), _ptr(vals), rmax, ctypes.byref(n),
+                                  cnt.ctypes.data_as(_abi.P_i64)))
+        return ids[:n.value].copy(), vals[:n.value].copy(), cnt
+
+    def parse_csv_dev(self, d_text, nbytes, d_ids_out, d_values_out, cap, d_status_out=None):
+        """Device bytes -> device rows; returns (accepted, counts int64[4])."""
+        n = ctypes.c_int64(0)
+        cnt = np.zeros(4, np.int64)
+        check(lib().sky_parse_csv_dev(self.h, _tptr(d_text), nbytes, _tptr(d_ids_out), _tptr(d_values_out), cap,
+                                      ctypes.byref(n), cnt.ctypes.data_as(_abi.P_i64), _tptr(d_status_out)))
+        return n.value, cnt
+
+    def format_csv_dev(self, d_ids, d_values, n, d_text=None, cap=0):
+        """The producers' "id,v1,...,vD\n" payload of a device stream; returns its byte count
+        (call with d_text=None first to size the buffer)."""
+        nb = ctypes.c_int64(0)
+        check(lib().sky_format_csv_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_text), cap,
+                                       ctypes.byref(nb)))
+        return nb.value
+
     def set_stream(self, stream_ptr):
         check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 

@@ -25,6 +25,10 @@
  *   sky_query[_dev]      <- the whole keyBy -> local -> global path for a trigger that arrives
  *                           after the last tuple (FlinkSkyline.java:138-174)
  *   dominance            <- ServiceTuple.dominates (ServiceTuple.java:67-77)
+ *   sky_parse_csv[_dev]  <- ServiceTuple.fromString (ServiceTuple.java:89-104) mapped over the raw
+ *                           Kafka values + .filter(Objects::nonNull) (FlinkSkyline.java:103-104)
+ *                           + Long.parseLong(point.id) (FlinkSkyline.java:276)
+ *   sky_synth_csv_dev    <- the producers' "id,v1,...,vD" payload (python/unified_producer.py:174)
  */
 #ifndef SKYLINE_HIP_H
 #define SKYLINE_HIP_H
@@ -135,6 +139,32 @@ int sky_export_copy_dev(sky_ctx *ctx, double *d_rows_out, int32_t *d_keys_out,
 int sky_import_union_dev(sky_ctx *ctx, const double *d_rows, const int32_t *d_keys,
                          const int64_t *d_mult, int64_t n_union, int64_t self_offset,
                          int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);
+
+/* ---- bulk CSV ingest ------------------------------------------------------ */
+/* Decodes '\n'-separated records "id,v1,...,vD" (a non-empty unterminated tail is one
+ * more record) exactly as the reference's ingest does per Kafka value: String.split(",")
+ * (trailing empty fields dropped), Double.parseDouble on each value (trim, NaN, Infinity,
+ * hex, decimal with exponent, one f/F/d/D suffix; correctly rounded), Long.parseLong on
+ * the id.  Accepted records are written in record order (ids_out[i], values_out[i*dims..]);
+ * the others are dropped and counted per cause in counts_out[4]:
+ *   [0] records, [SKY_CSV_MALFORMED] fromString returned null (the reference filters it),
+ *   [SKY_CSV_BAD_ID] the id is not a Java long (the reference task would fail),
+ *   [SKY_CSV_ARITY]  a well-formed record whose value count is not the context's dims.
+ * *n_out = accepted records; SKY_E_CAPACITY (with *n_out set) if cap is too small.
+ * d_status_out (optional, one byte per record) receives each record's SKY_CSV_* code. */
+#define SKY_CSV_OK        0
+#define SKY_CSV_MALFORMED 1
+#define SKY_CSV_BAD_ID    2
+#define SKY_CSV_ARITY     3
+int sky_parse_csv_dev(sky_ctx *ctx, const char *d_text, int64_t nbytes, int64_t *d_ids_out,
+                      double *d_values_out, int64_t cap, int64_t *n_out, int64_t *counts_out,
+                      uint8_t *d_status_out);
+int sky_parse_csv(sky_ctx *ctx, const char *text, int64_t nbytes, int64_t *ids_out, double *values_out,
+                  int64_t cap, int64_t *n_out, int64_t *counts_out);
+/* formats a device-resident stream as the producers' CSV payload ("%d" for integral
+ * values |v| < 2^53, records "id,v1,...,vD\n"); call with cap = 0 to size d_text. */
+int sky_format_csv_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
+                       char *d_text, int64_t cap, int64_t *nbytes_out);
 
 /* ---- utilities ------------------------------------------------------------- */
 int sky_synth_dev(sky_ctx *ctx, int dist, int dmin, int dmax, uint64_t seed, int64_t id0,

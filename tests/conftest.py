@@ -48,6 +48,10 @@ def load_oracle():
         L.orc_skyline_brute.argtypes = [dp, ctypes.c_int64, ctypes.c_int, dp]
         L.orc_synth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                 ctypes.c_int64, ctypes.c_int64, dp]
+        L.orc_java_parse_double.restype = ctypes.c_int
+        L.orc_java_parse_double.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
+        L.orc_parse_csv.restype = ctypes.c_int64
+        L.orc_parse_csv.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int, dp, dp, dp, ctypes.c_int64]
         _ORACLE = L
     return _ORACLE
 
@@ -95,6 +99,25 @@ class Oracle:
         g = self.L.orc_query_sfs(self.ALGO[algo], P(v), n, D, P_, domain, sem, P(keys), P(inl), P(ing), P(ls), P(sv))
         assert g >= 0
         return np.nonzero(ing[:n])[0], keys[:n], ls, sv
+
+    def java_parse_double(self, s):
+        """Double.parseDouble restatement: float, or None for a NumberFormatException."""
+        b = s.encode() if isinstance(s, str) else bytes(s)
+        buf = ctypes.create_string_buffer(b, len(b))
+        out = ctypes.c_double(0)
+        ok = self.L.orc_java_parse_double(buf, ctypes.cast(ctypes.addressof(buf) + len(b), ctypes.c_char_p),
+                                          ctypes.byref(out))
+        return out.value if ok else None
+
+    def parse_csv(self, text, D):
+        """-> (status u8[records], ids i64[records], values f64[records, D]); rows valid where status == 0."""
+        b = bytes(text)
+        cap = len(b) // 2 + 2
+        st = np.zeros(cap, np.uint8)
+        ids = np.zeros(cap, np.int64)
+        vals = np.zeros((cap, D), np.float64)
+        n = self.L.orc_parse_csv(b, len(b), D, P(ids), P(vals), P(st), cap)
+        return st[:n], ids[:n], vals[:n]
 
     def brute(self, vals):
         v = np.ascontiguousarray(vals, np.float64)
