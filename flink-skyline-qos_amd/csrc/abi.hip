@@ -660,9 +660,10 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     uint32_t h_nl = 0;
     uint8_t last = '\n';
     if (nb) {
-        c->ktimer_begin("k_csv_index", c->st);
+        c->ktimer_begin("csv_count", c->st);
         launch_csv_nl_count(text, nbytes, blk, c->st);
         scan_excl_u32(blk, blk_off, (size_t)nb, d_nl, c->csv_scr.as<uint32_t>(), c->st);
+        c->ktimer_end("csv_count", c->st, nbytes);
         HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipStreamSynchronize(c->st));
@@ -672,8 +673,9 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
     SKY_TRY(c->csv_lines.ensure((size_t)std::max<int64_t>(nl, 1) * 8));
     SKY_TRY(c->csv_status.ensure(nr1));
+    c->ktimer_begin("csv_lines", c->st);
     if (nl) launch_csv_nl_write(text, nbytes, blk_off, c->csv_lines.as<int64_t>(), c->st);
-    if (nb) c->ktimer_end("k_csv_index", c->st, nbytes);
+    c->ktimer_end("csv_lines", c->st, nbytes);
     const bool direct = cap >= nrec && d_ids_out && d_values_out;
     int64_t *pid = d_ids_out;
     double *pval = d_values_out;
@@ -684,15 +686,27 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         pval = c->csv_vals.as<double>();
     }
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
-    HIP_TRY(hipMemsetAsync(d_cnt, 0, 32, c->st));
-    c->ktimer_begin("k_csv_parse", c->st);
+    HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));   // [1..3] rejected per cause, [4] queued exact conversions
+    const unsigned long long slow_cap = 1u << 20;
+    SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
+    SKY_TRY(c->csv_keep.ensure((size_t)(csv_parse_blocks(nrec) + 1) * 4));   // spill list of k_csv_fields
+    HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
+    c->ktimer_begin("csv_parse", c->st);
     launch_csv_parse(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval, c->csv_status.as<uint8_t>(),
-                     d_cnt, c->st);
-    c->ktimer_end("k_csv_parse", c->st, nrec);
+                     d_cnt, c->csv_keep.as<uint32_t>(), c->csv_slow.as<longlong3>(), d_cnt + 4, slow_cap, c->st);
+    c->ktimer_end("csv_parse", c->st, nrec);
     HIP_TRY(hipGetLastError());
-    unsigned long long h_cnt[4] = {};
-    HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 32, hipMemcpyDeviceToHost, c->st));
+    unsigned long long h_cnt[5] = {};
+    HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 40, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
+    if (h_cnt[4] > slow_cap) {   // more exact conversions than the queue holds: re-parse every record exactly
+        HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));
+        launch_csv_parse_exact(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval,
+                               c->csv_status.as<uint8_t>(), d_cnt, c->st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 40, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
+    }
     const int64_t nbad = (int64_t)(h_cnt[1] + h_cnt[2] + h_cnt[3]);
     const int64_t nacc = nrec - nbad;
     if (counts_out) {

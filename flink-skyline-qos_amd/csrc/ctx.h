@@ -62,7 +62,7 @@ struct Ctx {
     bool shard_valid = false;
     DevBuf exp_scan;
     // bulk CSV ingest workspace (k_csv.hip)
-    DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text;
+    DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow;
 
     int Kq() const {
         if (algo == SKY_ALGO_GRID && sem == SKY_SEM_COMPLETE) return std::max(P, 1 << D);

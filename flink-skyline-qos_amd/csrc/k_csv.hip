@@ -18,12 +18,12 @@
 //                   against the halfway points, __noinline__ and rare), Long.parseLong.
 //   k_csv_compact   only if some record was rejected: stable compaction of the rows.
 #include "sky_internal.h"
+#include <cstdlib>
 
 namespace sky {
 
 constexpr int kCsvThreads = 256;
 constexpr int kCsvChunk = kCsvThreads * 16;   // bytes per workgroup in the newline passes
-constexpr int kCsvLds = 28 * 1024;            // staged record bytes per workgroup (else read from HBM)
 
 // ---------------------------------------------------------------- newline index
 __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
@@ -115,6 +115,17 @@ struct GlbSrc {
 
 __constant__ double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// 10^k for 0 <= k <= 22, exactly (every partial product is a power of ten <= 1e22, so each
+// multiplication is exact); selects only, no memory access
+__device__ __forceinline__ double exact_pow10(int k) {
+    double p = (k & 1) ? 1e1 : 1.0;
+    p *= (k & 2) ? 1e2 : 1.0;
+    p *= (k & 4) ? 1e4 : 1.0;
+    p *= (k & 8) ? 1e8 : 1.0;
+    p *= (k & 16) ? 1e16 : 1.0;
+    return p;
+}
 
 // ---------------------------------------------------------------- number conversion
 constexpr int kBigLimbs = 112;     // 3584 bits: the exact comparison needs <= ~2700 (see slow path)
@@ -282,9 +293,11 @@ __device__ __forceinline__ int hex_val(uint32_t c) {
 }
 
 // Double.parseDouble on b[s, e) (JDK 11 FloatingDecimal.readJavaFormatString grammar).
-// Returns false on a NumberFormatException.
-template <typename Src>
-__device__ __forceinline__ bool java_parse_double(const Src b, int64_t s, int64_t e, double &out) {
+// Returns 0 on a NumberFormatException, 1 with `out` set, or (kFull = false only) 2 when the
+// string is valid but needs the exact big-integer path: the caller queues it for k_csv_slow,
+// which keeps the scratch-using code out of the streaming kernel.
+template <bool kFull, typename Src>
+__device__ __forceinline__ int java_parse_double(const Src b, int64_t s, int64_t e, double &out) {
     while (s < e && b[s] <= ' ') s++;
     while (e > s && b[e - 1] <= ' ') e--;
     if (s == e) return false;
@@ -393,8 +406,9 @@ __device__ __forceinline__ bool java_parse_double(const Src b, int64_t s, int64_
         const int ex = E + ev;
         if (!trunc && w <= (1ull << 53) && ex >= -22 && ex <= 22) {
             const double wd = (double)w;   // exact
-            v = ex >= 0 ? wd * kP10[ex] : wd / kP10[-ex];
+            v = ex == 0 ? wd : (ex > 0 ? wd * exact_pow10(ex) : wd / exact_pow10(-ex));
         } else {
+            if (!kFull) return 2;
             v = decimal_slow(b.p, b.off, q0, qe, ev, w, ex);
         }
     }
@@ -440,7 +454,7 @@ __device__ __forceinline__ uint8_t parse_record(const Src b, int64_t s, int64_t 
             pending_empty++;   // empty field: fine only if every later field is empty too (split drops them)
         } else {
             double v;
-            if (pending_empty > 0 || !java_parse_double(b, fs, q, v)) bad = true;
+            if (pending_empty > 0 || !java_parse_double<true>(b, fs, q, v)) bad = true;
             else if (nvals < D) row[nvals] = v;
             nvals++;
         }
@@ -455,53 +469,273 @@ __device__ __forceinline__ uint8_t parse_record(const Src b, int64_t s, int64_t 
 }
 
 
-__global__ __launch_bounds__(kCsvThreads) void k_csv_parse(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                           const int64_t *__restrict__ line_end, int64_t nl,
-                                                           int64_t nrec, int D, int64_t *__restrict__ ids,
-                                                           double *__restrict__ vals, uint8_t *__restrict__ status,
-                                                           unsigned long long *__restrict__ counts) {
-    __shared__ uint32_t s_buf[kCsvLds / 4];
-    __shared__ uint32_t s_cnt[4];
+// ---- main pass: one workgroup = 256 consecutive records, one lane per FIELD.
+// Lane-per-record parsing diverges (every lane reaches its commas at a different
+// character); here all lanes run the same short field parse.  Steps:
+//  1. stage the records' bytes in LDS (coalesced dword loads);
+//  2. each lane scans a contiguous run of staged words for ',' / '\n' (zero-byte test),
+//     a block scan numbers the delimiters, and their offsets (u16) + record (u8) go to LDS;
+//  3. fields are parsed round-robin (field f = bytes after delimiter f-1 up to delimiter f):
+//     column 0 -> Long.parseLong, others -> Double.parseDouble, values stored straight into
+//     the row-major output (consecutive fields -> consecutive addresses);
+//  4. per record: split's trailing-empty rule, fromString's null cases, arity -> status.
+// A workgroup whose records exceed the LDS window or kFieldsMax fields is listed for
+// k_csv_records (lane per record, reading HBM).
+constexpr int kFieldsMax = 4096;
+constexpr int kFieldText = 20 * 1024;
+
+__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t w, uint32_t pat) {
+    const uint32_t x = w ^ pat;
+    const uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
+    return (~t) & 0x80808080u;
+}
+
+// SWAR fast path (simdjson's eight-digit parse): bytes [s, s+len) of the staged words, 1 <= len <= 16,
+// all ASCII digits -> value.  Covers the producer's payload (plain non-negative integers).
+__device__ __forceinline__ bool swar8(uint64_t x, int L, uint64_t &v) {   // L in 1..8, first char in the low byte
+    uint64_t y = L == 8 ? x : (x << (8 * (8 - L))) | (0x3030303030303030ull >> (8 * L));
+    if ((y & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull ||
+        ((y + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull)
+        return false;
+    y -= 0x3030303030303030ull;
+    y = (y * 10u) + (y >> 8);
+    y = (((y & 0x000000FF000000FFull) * 0x000F424000000064ull) +
+         (((y >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
+    v = (uint32_t)y;
+    return true;
+}
+__device__ __forceinline__ bool swar_digits(const uint32_t *__restrict__ buf, int s, int len, uint64_t &v) {
+    if (len < 1 || len > 16) return false;
+    const int k = s >> 2, sh = (s & 3) * 8;
+    const uint64_t A = (uint64_t)buf[k] | ((uint64_t)buf[k + 1] << 32);
+    const uint64_t B = (uint64_t)buf[k + 2] | ((uint64_t)buf[k + 3] << 32);
+    const uint64_t x0 = sh ? (A >> sh) | (B << (64 - sh)) : A;
+    if (len <= 8) return swar8(x0, len, v);
+    const uint64_t C = buf[k + 4];
+    const uint64_t x1 = sh ? (B >> sh) | (C << (64 - sh)) : B;
+    uint64_t hi, lo;
+    if (!swar8(x0, 8, hi) || !swar8(x1, len - 8, lo)) return false;
+    uint64_t p = 1;
+    for (int i = 0; i < len - 8; i++) p *= 10u;
+    v = hi * p + lo;
+    return true;
+}
+
+__global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
+                                                            const int64_t *__restrict__ line_end, int64_t nl,
+                                                            int64_t nrec, int D, int64_t *__restrict__ ids,
+                                                            double *__restrict__ vals, uint8_t *__restrict__ status,
+                                                            unsigned long long *__restrict__ counts,
+                                                            uint32_t *__restrict__ spill,
+                                                            longlong3 *__restrict__ slow,
+                                                            unsigned long long *__restrict__ slow_n,
+                                                            unsigned long long slow_cap, int stop) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kFieldText / 4 + 8];
+    __shared__ uint16_t s_dpos[kFieldsMax];
+    __shared__ uint8_t s_drec[kFieldsMax];
+    __shared__ uint16_t s_rfirst[kCsvThreads + 1];
+    __shared__ int s_last[kCsvThreads], s_fempty[kCsvThreads];
+    __shared__ uint32_t s_bad[kCsvThreads], s_idok[kCsvThreads];
+    __shared__ long long s_id[kCsvThreads];
+    __shared__ uint32_t s_w[8], s_cnt[4];
+    const int tid = threadIdx.x;
     const int64_t r0 = (int64_t)blockIdx.x * kCsvThreads;
-    const int64_t rl = r0 + kCsvThreads - 1 < nrec ? r0 + kCsvThreads - 1 : nrec - 1;
+    const int nr = (int)(nrec - r0 < kCsvThreads ? nrec - r0 : kCsvThreads);
+    const int64_t rl = r0 + nr - 1;
     const int64_t span_s = r0 == 0 ? 0 : line_end[r0 - 1] + 1;
-    const int64_t span_e = rl < nl ? line_end[rl] : nbytes;
-    const int64_t a0 = span_s & ~3ll;
-    const bool staged = span_e - a0 <= kCsvLds;
-    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
-    if (staged) {
-        const int nw = (int)((span_e - a0 + 3) >> 2);
-        const bool aligned = ((uintptr_t)text & 3) == 0;
-        for (int i = threadIdx.x; i < nw; i += kCsvThreads) {
-            const int64_t o = a0 + 4 * (int64_t)i;
-            uint32_t x;
-            if (aligned && o + 4 <= nbytes) {
-                x = *reinterpret_cast<const uint32_t *>(text + o);
+    const bool tail_open = rl >= nl;                       // last record has no '\n'
+    const int64_t span_e = tail_open ? nbytes : line_end[rl] + 1;   // includes the final '\n'
+    const int64_t a0 = span_s & ~15ll;
+    if (span_e - a0 > kFieldText) {                        // uniform per block
+        if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+        return;
+    }
+    const int nw = (int)((span_e - a0 + 3) >> 2);
+    {
+        const int nq = (nw + 3) >> 2;
+        const bool aligned = ((uintptr_t)text & 15) == 0;
+        for (int i = tid; i < nq; i += kCsvThreads) {
+            const int64_t o = a0 + 16 * (int64_t)i;
+            uint4 x;
+            if (aligned && o + 16 <= nbytes) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(text + o));
+                x = make_uint4(y.x, y.y, y.z, y.w);
             } else {
-                x = 0;
-                for (int k = 0; k < 4; k++)
-                    if (o + k < nbytes) x |= (uint32_t)text[o + k] << (8 * k);
+                uint32_t t[4] = {0, 0, 0, 0};
+                for (int k = 0; k < 16; k++)
+                    if (o + k < nbytes) t[k >> 2] |= (uint32_t)text[o + k] << (8 * (k & 3));
+                x = make_uint4(t[0], t[1], t[2], t[3]);
             }
-            s_buf[i] = x;
+            reinterpret_cast<uint4 *>(s_buf)[i] = x;
+        }
+    }
+    if (stop == 1) { __syncthreads(); if (s_buf[tid] == 0x12345678u) status[0] = 9; return; }
+    if (tid < 4) s_cnt[tid] = 0;
+    s_last[tid] = 0;
+    s_fempty[tid] = 0x7fffffff;
+    s_bad[tid] = 0;
+    __syncthreads();
+    // 2. delimiters, in order: lane tid owns words [w0, w1)
+    const int per = (nw + kCsvThreads - 1) / kCsvThreads;
+    const int w0 = tid * per, w1 = min(w0 + per, nw);
+    const int lo = (int)(span_s - a0), hi = (int)(span_e - a0);   // staged byte range of the records
+    uint32_t nd = 0, nn = 0;
+    for (int w = w0; w < w1; w++) {
+        const uint32_t x = s_buf[w];
+        uint32_t mc = byte_eq_mask(x, 0x2c2c2c2cu), mn = byte_eq_mask(x, 0x0a0a0a0au);
+        const int b0 = 4 * w;
+        if (b0 < lo || b0 + 4 > hi) {                      // clip to [lo, hi)
+            uint32_t keep = 0;
+            for (int k = 0; k < 4; k++)
+                if (b0 + k >= lo && b0 + k < hi) keep |= 0x80u << (8 * k);
+            mc &= keep;
+            mn &= keep;
+        }
+        nd += __popc(mc | mn);
+        nn += __popc(mn);
+    }
+    // block exclusive scans of (nd, nn)
+    const int lane = tid & 63, wv = tid >> 6;
+    uint32_t id_ = nd, in_ = nn;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = __shfl_up(id_, o, 64), b = __shfl_up(in_, o, 64);
+        if (lane >= o) { id_ += a; in_ += b; }
+    }
+    if (lane == 63) { s_w[wv] = id_; s_w[4 + wv] = in_; }
+    __syncthreads();
+    uint32_t fbase = id_ - nd, rbase = in_ - nn, ftot = 0;
+    for (int i = 0; i < 4; i++) {
+        if (i < wv) { fbase += s_w[i]; rbase += s_w[4 + i]; }
+        ftot += s_w[i];
+    }
+    const int nf = (int)ftot + (tail_open ? 1 : 0);
+    if (nf > kFieldsMax) {                                 // uniform per block
+        if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+        return;
+    }
+    if (tid == 0) {
+        s_rfirst[0] = 0;
+        if (tail_open) {                                   // virtual delimiter closing the tail record
+            s_dpos[nf - 1] = (uint16_t)hi;
+            s_drec[nf - 1] = (uint8_t)(nr - 1);
+        }
+    }
+    {
+        uint32_t f = fbase, rec = rbase;
+        for (int w = w0; w < w1; w++) {
+            const uint32_t x = s_buf[w];
+            uint32_t mc = byte_eq_mask(x, 0x2c2c2c2cu), mn = byte_eq_mask(x, 0x0a0a0a0au);
+            const int b0 = 4 * w;
+            if (b0 < lo || b0 + 4 > hi) {
+                uint32_t keep = 0;
+                for (int k = 0; k < 4; k++)
+                    if (b0 + k >= lo && b0 + k < hi) keep |= 0x80u << (8 * k);
+                mc &= keep;
+                mn &= keep;
+            }
+            uint32_t m = mc | mn;
+            while (m) {
+                const int bit = __ffs(m) - 1;
+                m &= m - 1;
+                s_dpos[f] = (uint16_t)(b0 + (bit >> 3));
+                s_drec[f] = (uint8_t)rec;
+                if ((mn >> bit) & 1u) {
+                    rec++;
+                    s_rfirst[rec] = (uint16_t)(f + 1);
+                }
+                f++;
+            }
         }
     }
     __syncthreads();
-    const int64_t r = r0 + threadIdx.x;
-    uint8_t st = SKY_CSV_OK;
-    if (r < nrec) {
-        const int64_t s = r == 0 ? 0 : line_end[r - 1] + 1;
-        const int64_t e = r < nl ? line_end[r] : nbytes;
-        int64_t id = 0;
-        double *row = vals + r * D;
-        if (staged) st = parse_record(LdsSrc{reinterpret_cast<const uint8_t *>(s_buf), a0}, s, e, D, id, row);
-        else st = parse_record(GlbSrc{text, 0}, s, e, D, id, row);
-        ids[r] = id;
-        status[r] = st;
+    if (stop == 2) { if (s_dpos[tid] == 0x1234) status[0] = 9; return; }
+    // 3. fields
+    const LdsSrc src{reinterpret_cast<const uint8_t *>(s_buf), 0};
+    for (int f = tid; f < nf; f += kCsvThreads) {
+        const int s = f == 0 ? lo : (int)s_dpos[f - 1] + 1;
+        const int e = s_dpos[f];
+        const int j = s_drec[f];
+        const int col = f - (int)s_rfirst[j];
+        uint64_t u = 0;
+        const bool fast = swar_digits(s_buf, s, e - s, u);
+        if (col == 0) {
+            int64_t v = (int64_t)u;
+            const bool ok = fast || java_parse_long(src, s, e, v);
+            s_id[j] = (long long)v;
+            s_idok[j] = ok;
+        } else if (s == e) {
+            atomicMin(&s_fempty[j], col);
+        } else {
+            double v = (double)u;                          // exact: < 10^16 ... only used when len <= 15
+            const int pr = fast && e - s <= 15 ? 1 : java_parse_double<false>(src, s, e, v);
+            if (pr == 0) {
+                s_bad[j] = 1;
+            } else if (col <= D) {
+                const int64_t o = (r0 + j) * D + col - 1;
+                if (pr == 1) {
+                    vals[o] = v;
+                } else {                                   // exact path, in k_csv_slow
+                    const unsigned long long k = atomicAdd(slow_n, 1ull);
+                    if (k < slow_cap) slow[k] = make_longlong3(a0 + s, a0 + e, o);
+                }
+            }
+            atomicMax(&s_last[j], col);
+        }
+    }
+    __syncthreads();
+    if (stop == 3) return;
+    // 4. records
+    if (tid < nr) {
+        const int last = s_last[tid];
+        uint8_t st;
+        if (s_bad[tid] || last == 0 || s_fempty[tid] < last) st = SKY_CSV_MALFORMED;   // ServiceTuple.java:93,101
+        else if (!s_idok[tid]) st = SKY_CSV_BAD_ID;                                      // FlinkSkyline.java:276
+        else if (last != D) st = SKY_CSV_ARITY;
+        else st = SKY_CSV_OK;
+        ids[r0 + tid] = s_id[tid];
+        status[r0 + tid] = st;
         if (st != SKY_CSV_OK) atomicAdd(&s_cnt[st], 1u);
     }
     __syncthreads();
-    if (threadIdx.x >= 1 && threadIdx.x < 4 && s_cnt[threadIdx.x])
-        atomicAdd(&counts[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+    if (tid >= 1 && tid < 4 && s_cnt[tid]) atomicAdd(&counts[tid], (unsigned long long)s_cnt[tid]);
+}
+
+// ---- the queued exact conversions (long significands, exponents beyond the fast path)
+__global__ __launch_bounds__(kCsvThreads) void k_csv_slow(const uint8_t *__restrict__ text,
+                                                          const longlong3 *__restrict__ slow,
+                                                          const unsigned long long *__restrict__ slow_n,
+                                                          unsigned long long slow_cap, double *__restrict__ vals) {
+    const unsigned long long n = *slow_n < slow_cap ? *slow_n : slow_cap;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * kCsvThreads + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * kCsvThreads) {
+        const longlong3 it = slow[i];
+        double v = 0.0;
+        java_parse_double<true>(GlbSrc{text, 0}, it.x, it.y, v);
+        vals[it.z] = v;
+    }
+}
+
+// ---- fallback: the workgroups k_csv_fields listed (very long records), lane per record from HBM
+__global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__restrict__ text, int64_t nbytes,
+                                                             const int64_t *__restrict__ line_end, int64_t nl,
+                                                             int64_t nrec, int D, int64_t *__restrict__ ids,
+                                                             double *__restrict__ vals, uint8_t *__restrict__ status,
+                                                             unsigned long long *__restrict__ counts,
+                                                             const uint32_t *__restrict__ spill, int64_t all_blocks) {
+    const int64_t nlist = all_blocks ? all_blocks : (int64_t)spill[0];
+    for (int64_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+        const int64_t r = (all_blocks ? li : (int64_t)spill[1 + li]) * kCsvThreads + threadIdx.x;
+        if (r >= nrec) continue;
+        const int64_t s = r == 0 ? 0 : line_end[r - 1] + 1;
+        const int64_t e = r < nl ? line_end[r] : nbytes;
+        int64_t id = 0;
+        const uint8_t st = parse_record(GlbSrc{text, 0}, s, e, D, id, vals + r * D);
+        ids[r] = id;
+        status[r] = st;
+        if (st != SKY_CSV_OK) atomicAdd(&counts[st], 1ull);
+    }
 }
 
 __global__ void k_csv_keep(const uint8_t *__restrict__ status, int64_t n, uint32_t *__restrict__ keep) {
@@ -611,12 +845,34 @@ void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *bl
     const bool aligned = ((uintptr_t)text & 15) == 0;
     k_csv_nl_write<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_off, line_end);
 }
+static int csv_stop() {
+    const char *e = getenv("SKY_CSV_STOP");
+    return e ? atoi(e) : 0;
+}
+// spill: device u32 [1 + blocks], spill[0] zeroed by the caller; slow: queue of exact
+// conversions (slow_n zeroed by the caller).  If *slow_n ends above slow_cap the caller
+// re-parses everything with launch_csv_parse_exact.
 void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
-                      int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, hipStream_t st) {
+                      int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
+                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, hipStream_t st) {
     if (nrec == 0) return;
     const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
-    k_csv_parse<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts);
+    k_csv_fields<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts,
+                                                      spill, slow, slow_n, slow_cap, csv_stop());
+    const unsigned g = (unsigned)(nb < 1024 ? nb : 1024);
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, spill, 0);
+    k_csv_slow<<<1024, kCsvThreads, 0, st>>>(text, slow, slow_n, slow_cap, vals);
 }
+void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
+                            int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
+                            hipStream_t st) {
+    if (nrec == 0) return;
+    const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
+    const unsigned g = (unsigned)(nb < 4096 ? nb : 4096);
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, nullptr,
+                                             nb);
+}
+int64_t csv_parse_blocks(int64_t nrec) { return (nrec + kCsvThreads - 1) / kCsvThreads; }
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st) {
     if (n == 0) return;
     k_csv_keep<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(status, n, keep);

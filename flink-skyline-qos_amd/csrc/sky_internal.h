@@ -213,7 +213,12 @@ void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt,
 void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
                          hipStream_t st);
 void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
-                      int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, hipStream_t st);
+                      int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
+                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, hipStream_t st);
+void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
+                            int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
+                            hipStream_t st);
+int64_t csv_parse_blocks(int64_t nrec);
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st);
 void launch_csv_compact(const uint8_t *status, const uint32_t *pos, int64_t n, int D, const int64_t *ids_in,
                         const double *vals_in, int64_t *ids_out, double *vals_out, hipStream_t st);
