@@ -659,11 +659,15 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1);
     uint32_t h_nl = 0;
     uint8_t last = '\n';
+    unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
+    unsigned long long h_commas = 0;
     if (nb) {
+        HIP_TRY(hipMemsetAsync(d_cnt + 5, 0, 8, c->st));
         c->ktimer_begin("csv_count", c->st);
-        launch_csv_nl_count(text, nbytes, blk, c->st);
+        launch_csv_nl_count(text, nbytes, blk, d_cnt + 5, c->st);
         scan_excl_u32(blk, blk_off, (size_t)nb, d_nl, c->csv_scr.as<uint32_t>(), c->st);
         c->ktimer_end("csv_count", c->st, nbytes);
+        HIP_TRY(hipMemcpyAsync(&h_commas, d_cnt + 5, 8, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipStreamSynchronize(c->st));
@@ -685,15 +689,15 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         pid = c->csv_ids.as<int64_t>();
         pval = c->csv_vals.as<double>();
     }
-    unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
     HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));   // [1..3] rejected per cause, [4] queued exact conversions
     const unsigned long long slow_cap = 1u << 20;
     SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
-    SKY_TRY(c->csv_keep.ensure((size_t)(csv_parse_blocks(nrec) + 1) * 4));   // spill list of k_csv_fields
+    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
+    SKY_TRY(c->csv_keep.ensure((size_t)((nrec + R - 1) / R + 1) * 4));   // spill list of k_csv_fields
     HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
     c->ktimer_begin("csv_parse", c->st);
     launch_csv_parse(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval, c->csv_status.as<uint8_t>(),
-                     d_cnt, c->csv_keep.as<uint32_t>(), c->csv_slow.as<longlong3>(), d_cnt + 4, slow_cap, c->st);
+                     d_cnt, c->csv_keep.as<uint32_t>(), c->csv_slow.as<longlong3>(), d_cnt + 4, slow_cap, R, c->st);
     c->ktimer_end("csv_parse", c->st, nrec);
     HIP_TRY(hipGetLastError());
     unsigned long long h_cnt[5] = {};

@@ -18,6 +18,7 @@
 //                   against the halfway points, __noinline__ and rare), Long.parseLong.
 //   k_csv_compact   only if some record was rejected: stable compaction of the rows.
 #include "sky_internal.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace sky {
@@ -31,6 +32,12 @@ __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
     const uint32_t x = w ^ 0x0a0a0a0au;
     const uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
     return (~t) & 0x80808080u;   // bit 7 of byte b set iff byte b == '\n'
+}
+
+__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t w, uint32_t pat) {
+    const uint32_t x = w ^ pat;
+    const uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
+    return (~t) & 0x80808080u;
 }
 
 __device__ __forceinline__ void load16(const uint8_t *__restrict__ text, int64_t nbytes, int64_t base, bool aligned,
@@ -54,19 +61,27 @@ __device__ __forceinline__ void load16(const uint8_t *__restrict__ text, int64_t
 }
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                              bool aligned, uint32_t *__restrict__ blk_cnt) {
-    __shared__ uint32_t s_w[kCsvThreads / 64];
+                                                              bool aligned, uint32_t *__restrict__ blk_cnt,
+                                                              unsigned long long *__restrict__ ncomma) {
+    __shared__ uint32_t s_w[kCsvThreads / 64], s_c[kCsvThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * kCsvChunk + threadIdx.x * 16;
     uint32_t w[4];
     load16(text, nbytes, base, aligned, w);
-    uint32_t c = 0;
+    uint32_t c = 0, cm = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) c += __popc(nl_in_word(w[k]));
+    for (int k = 0; k < 4; k++) {
+        c += __popc(nl_in_word(w[k]));
+        cm += __popc(byte_eq_mask(w[k], 0x2c2c2c2cu));
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+    for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o, 64); cm += __shfl_xor(cm, o, 64); }
+    if ((threadIdx.x & 63) == 0) { s_w[threadIdx.x >> 6] = c; s_c[threadIdx.x >> 6] = cm; }
     __syncthreads();
-    if (threadIdx.x == 0) blk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (threadIdx.x == 0) {
+        blk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        const uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        if (t) atomicAdd(ncomma, (unsigned long long)t);
+    }
 }
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_write(const uint8_t *__restrict__ text, int64_t nbytes,
@@ -481,14 +496,9 @@ __device__ __forceinline__ uint8_t parse_record(const Src b, int64_t s, int64_t 
 //  4. per record: split's trailing-empty rule, fromString's null cases, arity -> status.
 // A workgroup whose records exceed the LDS window or kFieldsMax fields is listed for
 // k_csv_records (lane per record, reading HBM).
-constexpr int kFieldsMax = 4096;
-constexpr int kFieldText = 20 * 1024;
+constexpr int kFieldsMax = 2048;
+constexpr int kFieldText = 10 * 1024;   // ~19 KB of LDS per workgroup in all: 8 workgroups (32 waves) per CU
 
-__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t w, uint32_t pat) {
-    const uint32_t x = w ^ pat;
-    const uint32_t t = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;
-    return (~t) & 0x80808080u;
-}
 
 // SWAR fast path (simdjson's eight-digit parse): bytes [s, s+len) of the staged words, 1 <= len <= 16,
 // all ASCII digits -> value.  Covers the producer's payload (plain non-negative integers).
@@ -508,6 +518,15 @@ __device__ __forceinline__ bool swar_digits(const uint32_t *__restrict__ buf, in
     if (len < 1 || len > 16) return false;
     const int k = s >> 2, sh = (s & 3) * 8;
     const uint64_t A = (uint64_t)buf[k] | ((uint64_t)buf[k + 1] << 32);
+    if (len <= 4) {                                        // 32-bit SWAR: the common short value
+        const uint32_t x = (uint32_t)(A >> sh);
+        uint32_t y = len == 4 ? x : (x << (8 * (4 - len))) | (0x30303030u >> (8 * len));
+        if ((y & 0xF0F0F0F0u) != 0x30303030u || ((y + 0x06060606u) & 0xF0F0F0F0u) != 0x30303030u) return false;
+        y -= 0x30303030u;
+        y = y * 10u + (y >> 8);
+        v = (y & 0xFFu) * 100u + ((y >> 16) & 0xFFu);
+        return true;
+    }
     const uint64_t B = (uint64_t)buf[k + 2] | ((uint64_t)buf[k + 3] << 32);
     const uint64_t x0 = sh ? (A >> sh) | (B << (64 - sh)) : A;
     if (len <= 8) return swar8(x0, len, v);
@@ -529,18 +548,17 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                                                             uint32_t *__restrict__ spill,
                                                             longlong3 *__restrict__ slow,
                                                             unsigned long long *__restrict__ slow_n,
-                                                            unsigned long long slow_cap, int stop) {
+                                                            unsigned long long slow_cap, int R, int stop) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kFieldText / 4 + 8];
     __shared__ uint16_t s_dpos[kFieldsMax];
     __shared__ uint8_t s_drec[kFieldsMax];
     __shared__ uint16_t s_rfirst[kCsvThreads + 1];
     __shared__ int s_last[kCsvThreads], s_fempty[kCsvThreads];
-    __shared__ uint32_t s_bad[kCsvThreads], s_idok[kCsvThreads];
-    __shared__ long long s_id[kCsvThreads];
+    __shared__ uint8_t s_bad[kCsvThreads], s_idok[kCsvThreads];
     __shared__ uint32_t s_w[8], s_cnt[4];
     const int tid = threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.x * kCsvThreads;
-    const int nr = (int)(nrec - r0 < kCsvThreads ? nrec - r0 : kCsvThreads);
+    const int64_t r0 = (int64_t)blockIdx.x * R;             // R <= 256 records per workgroup (host-chosen)
+    const int nr = (int)(nrec - r0 < R ? nrec - r0 : R);
     const int64_t rl = r0 + nr - 1;
     const int64_t span_s = r0 == 0 ? 0 : line_end[r0 - 1] + 1;
     const bool tail_open = rl >= nl;                       // last record has no '\n'
@@ -550,13 +568,21 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
         return;
     }
-    const int nw = (int)((span_e - a0 + 3) >> 2);
-    {
-        const int nq = (nw + 3) >> 2;
-        const bool aligned = ((uintptr_t)text & 15) == 0;
-        for (int i = tid; i < nq; i += kCsvThreads) {
-            const int64_t o = a0 + 16 * (int64_t)i;
-            uint4 x;
+    if (stop == 4) return;
+    // 1+2. lane tid owns the 16-byte units [tid*per, tid*per + per) of the staged span: it loads
+    // them (into registers and LDS) and numbers its delimiters without re-reading LDS
+    constexpr int kUnits = (kFieldText / 16 + kCsvThreads - 1) / kCsvThreads;   // 3
+    const int nq = (int)((span_e - a0 + 15) >> 4);
+    const int per = (nq + kCsvThreads - 1) / kCsvThreads;
+    const int lo = (int)(span_s - a0), hi = (int)(span_e - a0);   // staged byte range of the records
+    const bool aligned = ((uintptr_t)text & 15) == 0;
+    uint32_t dw[kUnits * 4];
+#pragma unroll
+    for (int u = 0; u < kUnits; u++) {
+        const int q = tid * per + u;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (u < per && q < nq) {
+            const int64_t o = a0 + 16 * (int64_t)q;
             if (aligned && o + 16 <= nbytes) {
                 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(text + o));
@@ -567,31 +593,32 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                     if (o + k < nbytes) t[k >> 2] |= (uint32_t)text[o + k] << (8 * (k & 3));
                 x = make_uint4(t[0], t[1], t[2], t[3]);
             }
-            reinterpret_cast<uint4 *>(s_buf)[i] = x;
+            reinterpret_cast<uint4 *>(s_buf)[q] = x;
         }
+        dw[4 * u] = x.x; dw[4 * u + 1] = x.y; dw[4 * u + 2] = x.z; dw[4 * u + 3] = x.w;
     }
     if (stop == 1) { __syncthreads(); if (s_buf[tid] == 0x12345678u) status[0] = 9; return; }
     if (tid < 4) s_cnt[tid] = 0;
     s_last[tid] = 0;
     s_fempty[tid] = 0x7fffffff;
     s_bad[tid] = 0;
-    __syncthreads();
-    // 2. delimiters, in order: lane tid owns words [w0, w1)
-    const int per = (nw + kCsvThreads - 1) / kCsvThreads;
-    const int w0 = tid * per, w1 = min(w0 + per, nw);
-    const int lo = (int)(span_s - a0), hi = (int)(span_e - a0);   // staged byte range of the records
+    uint32_t mcs[kUnits * 4], mns[kUnits * 4];
     uint32_t nd = 0, nn = 0;
-    for (int w = w0; w < w1; w++) {
-        const uint32_t x = s_buf[w];
-        uint32_t mc = byte_eq_mask(x, 0x2c2c2c2cu), mn = byte_eq_mask(x, 0x0a0a0a0au);
-        const int b0 = 4 * w;
-        if (b0 < lo || b0 + 4 > hi) {                      // clip to [lo, hi)
+#pragma unroll
+    for (int k = 0; k < kUnits * 4; k++) {
+        const int b0 = 16 * (tid * per) + 4 * k;
+        uint32_t mc = byte_eq_mask(dw[k], 0x2c2c2c2cu), mn = byte_eq_mask(dw[k], 0x0a0a0a0au);
+        if (k >= per * 4 || b0 + 4 <= lo || b0 >= hi) {
+            mc = mn = 0;
+        } else if (b0 < lo || b0 + 4 > hi) {               // clip to [lo, hi)
             uint32_t keep = 0;
-            for (int k = 0; k < 4; k++)
-                if (b0 + k >= lo && b0 + k < hi) keep |= 0x80u << (8 * k);
+            for (int t = 0; t < 4; t++)
+                if (b0 + t >= lo && b0 + t < hi) keep |= 0x80u << (8 * t);
             mc &= keep;
             mn &= keep;
         }
+        mcs[k] = mc;
+        mns[k] = mn;
         nd += __popc(mc | mn);
         nn += __popc(mn);
     }
@@ -624,18 +651,11 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     }
     {
         uint32_t f = fbase, rec = rbase;
-        for (int w = w0; w < w1; w++) {
-            const uint32_t x = s_buf[w];
-            uint32_t mc = byte_eq_mask(x, 0x2c2c2c2cu), mn = byte_eq_mask(x, 0x0a0a0a0au);
-            const int b0 = 4 * w;
-            if (b0 < lo || b0 + 4 > hi) {
-                uint32_t keep = 0;
-                for (int k = 0; k < 4; k++)
-                    if (b0 + k >= lo && b0 + k < hi) keep |= 0x80u << (8 * k);
-                mc &= keep;
-                mn &= keep;
-            }
-            uint32_t m = mc | mn;
+#pragma unroll
+        for (int k = 0; k < kUnits * 4; k++) {
+            const int b0 = 16 * (tid * per) + 4 * k;
+            const uint32_t mn = mns[k];
+            uint32_t m = mcs[k] | mn;
             while (m) {
                 const int bit = __ffs(m) - 1;
                 m &= m - 1;
@@ -663,7 +683,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         if (col == 0) {
             int64_t v = (int64_t)u;
             const bool ok = fast || java_parse_long(src, s, e, v);
-            s_id[j] = (long long)v;
+            ids[r0 + j] = v;
             s_idok[j] = ok;
         } else if (s == e) {
             atomicMin(&s_fempty[j], col);
@@ -694,7 +714,6 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         else if (!s_idok[tid]) st = SKY_CSV_BAD_ID;                                      // FlinkSkyline.java:276
         else if (last != D) st = SKY_CSV_ARITY;
         else st = SKY_CSV_OK;
-        ids[r0 + tid] = s_id[tid];
         status[r0 + tid] = st;
         if (st != SKY_CSV_OK) atomicAdd(&s_cnt[st], 1u);
     }
@@ -723,10 +742,12 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__re
                                                              int64_t nrec, int D, int64_t *__restrict__ ids,
                                                              double *__restrict__ vals, uint8_t *__restrict__ status,
                                                              unsigned long long *__restrict__ counts,
-                                                             const uint32_t *__restrict__ spill, int64_t all_blocks) {
+                                                             const uint32_t *__restrict__ spill, int64_t all_blocks,
+                                                             int R) {
     const int64_t nlist = all_blocks ? all_blocks : (int64_t)spill[0];
     for (int64_t li = blockIdx.x; li < nlist; li += gridDim.x) {
-        const int64_t r = (all_blocks ? li : (int64_t)spill[1 + li]) * kCsvThreads + threadIdx.x;
+        if ((int)threadIdx.x >= R) continue;
+        const int64_t r = (all_blocks ? li : (int64_t)spill[1 + li]) * R + threadIdx.x;
         if (r >= nrec) continue;
         const int64_t s = r == 0 ? 0 : line_end[r - 1] + 1;
         const int64_t e = r < nl ? line_end[r] : nbytes;
@@ -832,11 +853,12 @@ void launch_csv_fmt_write(const int64_t *ids, const double *vals, int64_t n, int
 
 int64_t csv_chunks(int64_t nbytes) { return (nbytes + kCsvChunk - 1) / kCsvChunk; }
 
-void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, hipStream_t st) {
+void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, unsigned long long *ncomma,
+                         hipStream_t st) {
     const int64_t nb = csv_chunks(nbytes);
     if (nb == 0) return;
     const bool aligned = ((uintptr_t)text & 15) == 0;
-    k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt);
+    k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt, ncomma);
 }
 void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
                          hipStream_t st) {
@@ -854,13 +876,15 @@ static int csv_stop() {
 // re-parses everything with launch_csv_parse_exact.
 void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
                       int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
-                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, hipStream_t st) {
+                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, int R,
+                      hipStream_t st) {
     if (nrec == 0) return;
-    const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
+    const int64_t nb = (nrec + R - 1) / R;
     k_csv_fields<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts,
-                                                      spill, slow, slow_n, slow_cap, csv_stop());
+                                                      spill, slow, slow_n, slow_cap, R, csv_stop());
     const unsigned g = (unsigned)(nb < 1024 ? nb : 1024);
-    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, spill, 0);
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, spill, 0,
+                                             R);
     k_csv_slow<<<1024, kCsvThreads, 0, st>>>(text, slow, slow_n, slow_cap, vals);
 }
 void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
@@ -870,9 +894,18 @@ void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *
     const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
     const unsigned g = (unsigned)(nb < 4096 ? nb : 4096);
     k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, nullptr,
-                                             nb);
+                                             nb, kCsvThreads);
 }
-int64_t csv_parse_blocks(int64_t nrec) { return (nrec + kCsvThreads - 1) / kCsvThreads; }
+// records per k_csv_fields workgroup: as many as fit the LDS windows at the stream's average
+// record length and field count (outliers spill to k_csv_records)
+int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields) {
+    if (nrec <= 0) return kCsvThreads;
+    const double len = (double)nbytes / (double)nrec, nf = (double)nfields / (double)nrec;
+    int R = kCsvThreads;
+    R = std::min<int>(R, (int)(0.8 * kFieldText / std::max(len, 1.0)));
+    R = std::min<int>(R, (int)(0.8 * kFieldsMax / std::max(nf, 1.0)));
+    return std::max(R, 8);
+}
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st) {
     if (n == 0) return;
     k_csv_keep<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(status, n, keep);

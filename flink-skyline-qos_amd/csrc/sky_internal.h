@@ -209,16 +209,18 @@ void synth_host(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0,
 
 // ---- k_csv.hip ----
 int64_t csv_chunks(int64_t nbytes);
-void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, hipStream_t st);
+void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, unsigned long long *ncomma,
+                         hipStream_t st);
 void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
                          hipStream_t st);
 void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
                       int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
-                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, hipStream_t st);
+                      longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, int R,
+                      hipStream_t st);
 void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
                             int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
                             hipStream_t st);
-int64_t csv_parse_blocks(int64_t nrec);
+int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields);
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st);
 void launch_csv_compact(const uint8_t *status, const uint32_t *pos, int64_t n, int D, const int64_t *ids_in,
                         const double *vals_in, int64_t *ids_out, double *vals_out, hipStream_t st);
