@@ -655,23 +655,25 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const int D = c->D;
     SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 16));
     SKY_TRY(c->csv_scr.ensure(scan_scratch_words((size_t)std::max<int64_t>(nb, 1)) * 4));
-    SKY_TRY(c->csv_counts.ensure(64));
+    SKY_TRY(c->csv_counts.ensure(64 + 256 * 8));
     uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1);
     uint32_t h_nl = 0;
     uint8_t last = '\n';
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
     unsigned long long h_commas = 0;
+    std::vector<unsigned long long> h_shards(256, 0);
     if (nb) {
-        HIP_TRY(hipMemsetAsync(d_cnt + 5, 0, 8, c->st));
+        HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
         c->ktimer_begin("csv_count", c->st);
-        launch_csv_nl_count(text, nbytes, blk, d_cnt + 5, c->st);
+        launch_csv_nl_count(text, nbytes, blk, d_cnt + 8, c->st);
         scan_excl_u32(blk, blk_off, (size_t)nb, d_nl, c->csv_scr.as<uint32_t>(), c->st);
         c->ktimer_end("csv_count", c->st, nbytes);
-        HIP_TRY(hipMemcpyAsync(&h_commas, d_cnt + 5, 8, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipMemcpyAsync(h_shards.data(), d_cnt + 8, 256 * 8, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipStreamSynchronize(c->st));
     }
+    for (unsigned long long x : h_shards) h_commas += x;
     const int64_t nl = h_nl;
     const int64_t nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);

@@ -25,6 +25,7 @@ namespace sky {
 
 constexpr int kCsvThreads = 256;
 constexpr int kCsvChunk = kCsvThreads * 16;   // bytes per workgroup in the newline passes
+constexpr int kCommaShards = 256;             // comma-count accumulators (one global atomic per workgroup)
 
 // ---------------------------------------------------------------- newline index
 __device__ __forceinline__ uint32_t nl_in_word(uint32_t w) {
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__r
     if (threadIdx.x == 0) {
         blk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
         const uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
-        if (t) atomicAdd(ncomma, (unsigned long long)t);
+        if (t) atomicAdd(&ncomma[blockIdx.x & (kCommaShards - 1)], (unsigned long long)t);   // sharded: no hot spot
     }
 }
 
