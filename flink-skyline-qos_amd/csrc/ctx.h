@@ -134,3 +134,14 @@ struct sky_part {
     int64_t n = 0;
     sky::DevBuf cat_ids, cat_rows;
 };
+
+struct sky_stream {
+    sky_ctx *ctx = nullptr;
+    int64_t window = 0;         // 0: landmark
+    sky::DevBuf ids[2], rows[2];
+    int cur = 0;
+    int64_t off = 0, n = 0;     // resident tuples: [off, off + n) of buffer `cur`
+    int64_t cap = 0;            // capacity (tuples) of both buffers
+    int64_t appended = 0;
+    sky::DevBuf out_ids, out_org;
+};

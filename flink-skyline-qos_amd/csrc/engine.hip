@@ -817,13 +817,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
 
 int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,
                 double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags) {
-    (void)select_local;
-    if (n_out) *n_out = p.nout;
-    if ((int64_t)p.nout > cap && (d_ids_out || d_origin_out || d_rows_out)) {
-        set_error("output capacity " + std::to_string(cap) + " < skyline size " + std::to_string(p.nout));
-        return SKY_E_CAPACITY;
-    }
-    if (p.n == 0) return SKY_OK;
+    // the run's count pass selected G (global runs) or L (single-partition runs); the local
+    // skyline of a global run needs its own count + scan (stats untouched)
+    const bool recount = select_local && in.global && p.n > 0;
+    uint32_t nsel = p.nout;
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = p.n;
@@ -842,6 +839,23 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     oa.origin_out = d_origin_out;
     oa.rows_out = d_rows_out;
     oa.select_local = 0;
+    if (recount) {
+        const uint32_t tiles = (p.n + kTile - 1) / kTile;
+        oa.select_local = 1;
+        oa.lsz = nullptr;
+        oa.surv = nullptr;
+        oa.row_flags = nullptr;
+        launch_out_count(oa, c.st);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), c.st);
+        SKY_TRY(sync_read(p, c.st, {{p.totals.as<uint32_t>() + 3, 4}}, {&nsel}));
+    }
+    if (n_out) *n_out = nsel;
+    if ((int64_t)nsel > cap && (d_ids_out || d_origin_out || d_rows_out)) {
+        set_error("output capacity " + std::to_string(cap) + " < skyline size " + std::to_string(nsel));
+        return SKY_E_CAPACITY;
+    }
+    if (p.n == 0) return SKY_OK;
     if (d_row_flags) {
         oa.row_flags = d_row_flags;
         oa.lsz = nullptr;

@@ -6,4 +6,4 @@
 All skyline computation runs in libskyline_hip.so (gfx950 HIP kernels).
 """
 from ._abi import SkylineError, lib, LIB_PATH  # noqa: F401
-from .engine import SkylineEngine, synth_host  # noqa: F401
+from .engine import SkylineEngine, SkylineStream, synth_host  # noqa: F401

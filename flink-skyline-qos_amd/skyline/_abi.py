@@ -69,6 +69,13 @@ SIGNATURES = {
     "sky_parse_csv_dev": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64, c_p],
     "sky_parse_csv": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64],
     "sky_format_csv_dev": [c_p, c_p, c_p, c_i64, c_p, c_i64, P_i64],
+    "sky_stream_create": [c_p, c_i64, ctypes.POINTER(c_p)],
+    "sky_stream_destroy": [c_p],
+    "sky_stream_append": [c_p, c_p, c_p, c_i64],
+    "sky_stream_append_dev": [c_p, c_p, c_p, c_i64],
+    "sky_stream_size": [c_p, P_i64, P_i64],
+    "sky_stream_query": [c_p, c_p, c_p, c_i64, P_i64],
+    "sky_stream_query_dev": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_synth_dev": [c_p, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_synth": [c_int, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_dev_alloc": [c_p, c_i64, ctypes.POINTER(c_p)],

@@ -204,3 +204,60 @@ def synth_host(dist, dims, n, seed=1234, id0=0, dmin=0, dmax=1000):
     ids = np.empty(n, np.int64)
     check(lib().sky_synth(dist, dims, dmin, dmax, seed, id0, n, _ptr(v), _ptr(ids)))
     return v, ids
+
+
+class SkylineStream:
+    """Continuous queries over an append-only stream on one engine (sky_stream_*).
+
+    window=0: the reference's landmark window (FlinkSkyline.java:265-316 + :417-444): a
+    query covers every tuple appended so far; between queries only the local-skyline
+    tuples stay resident.  window=W > 0: count-based sliding window over the last W
+    appended tuples (an extension; the reference has no window)."""
+
+    def __init__(self, engine, window=0):
+        self.engine = engine
+        self.window = int(window)
+        h = ctypes.c_void_p()
+        check(lib().sky_stream_create(engine.h, self.window, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().sky_stream_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append(self, ids, values):
+        """Host arrays (numpy): ids int64[n], values f64[n, D]."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        v = np.ascontiguousarray(values, np.float64)
+        check(lib().sky_stream_append(self.h, _ptr(ids), _ptr(v), len(ids)))
+
+    def append_dev(self, d_ids, d_values, n=None):
+        n = d_values.shape[0] if n is None else n
+        check(lib().sky_stream_append_dev(self.h, _tptr(d_ids), _tptr(d_values), n))
+
+    def size(self):
+        r, a = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().sky_stream_size(self.h, ctypes.byref(r), ctypes.byref(a)))
+        return r.value, a.value
+
+    def query(self):
+        """-> (ids int64[g], origin int32[g]) of the global skyline, arrival order."""
+        r, _ = self.size()
+        cap = max(r, 1)
+        ids = np.empty(cap, np.int64)
+        org = np.empty(cap, np.int32)
+        g = ctypes.c_int64(0)
+        check(lib().sky_stream_query(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
+        return ids[:g.value], org[:g.value]
+
+    def query_dev(self, d_ids_out, d_origin_out, cap):
+        g = ctypes.c_int64(0)
+        check(lib().sky_stream_query_dev(self.h, _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(g)))
+        return g.value

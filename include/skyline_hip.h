@@ -70,6 +70,7 @@ extern "C" {
 
 typedef struct sky_ctx sky_ctx;
 typedef struct sky_part sky_part;
+typedef struct sky_stream sky_stream;
 
 /* ---- context ------------------------------------------------------------ */
 /* devices/ndev: HIP device ordinals; one process drives one device (ndev == 1),
@@ -123,6 +124,27 @@ int sky_query(sky_ctx *ctx, const int64_t *ids, const double *values, int64_t n,
               int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
 int sky_query_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
                   int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);
+
+/* ---- continuous queries over a stream ---- */
+/* A device-resident stream state behind the operators' continuous queries.
+ * window == 0: the reference's landmark window (every tuple since the start counts,
+ *   FlinkSkyline.java:265-316 state + :417-444 BNL).  Only the tuples of the last
+ *   query's local skylines stay resident (SKY(L_k ∪ new) = SKY(all of key k)), plus
+ *   the tuples appended since; each query re-runs keys -> local -> global over them.
+ * window == W > 0: count-based sliding window over the last W appended tuples
+ *   (an extension: the reference has no window; expiry needs the non-skyline
+ *   tuples, so all W stay resident and each query runs over the window).
+ * Results (ids in arrival order, origin keys) and sky_global_stats match a whole-
+ * stream sky_query over the same tuples (landmark) / the window's tuples (sliding). */
+int sky_stream_create(sky_ctx *ctx, int64_t window, sky_stream **out);
+int sky_stream_destroy(sky_stream *s);
+int sky_stream_append(sky_stream *s, const int64_t *ids, const double *values, int64_t n);
+int sky_stream_append_dev(sky_stream *s, const int64_t *d_ids, const double *d_values, int64_t n);
+/* resident tuples and tuples appended since creation */
+int sky_stream_size(sky_stream *s, int64_t *resident, int64_t *appended);
+int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
+int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
+                         int64_t *n_out);
 
 /* ---- multi-GPU (one process per GPU; the caller moves bytes with RCCL) ------ */
 /* Phase 1 on each rank: local skylines of this rank's shard; export their
