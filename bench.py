@@ -128,6 +128,45 @@ def csv_ingest_run(eng, ids, vals, n, D, steps, out_ids, out_org):
             "all_passes_GBs": alg / (k_ms / 1e3) / 1e9}
 
 
+def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000, window=0):
+    """Config C5: continuous queries over a 6D mixed stream (65536-tuple blocks
+    cycling the producer's uniform / correlated / anti-correlated formulas), MR-Angle, P = 8
+    (Flink parallelism 4).  Micro-batches of `batch` tuples arrive from pinned host memory
+    (H2D included); a query_trigger every `per_trigger` tuples.  Latency = trigger -> global
+    skyline ids in host memory.  window=0: the reference's landmark window; window=W:
+    the count-based sliding window extension."""
+    import numpy as np
+    D, P = 6, 8
+    n = triggers * per_trigger
+    vals_np, ids_np = skyline.synth_host(_abi.DISTS["mixed"], D, n, seed=seed)
+    vals = torch.from_numpy(vals_np).pin_memory().numpy()
+    ids = torch.from_numpy(ids_np).pin_memory().numpy()
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
+    st = skyline.SkylineStream(eng, window)
+    lat, sizes = [], []
+    t_start = time.perf_counter()
+    for t in range(triggers):
+        base = t * per_trigger
+        for b0 in range(base, base + per_trigger, batch):
+            st.append(ids[b0:b0 + batch], vals[b0:b0 + batch])
+        tq = time.perf_counter()
+        g = st.query_host_view()
+        lat.append((time.perf_counter() - tq) * 1e3)
+        sizes.append(g)
+    total = time.perf_counter() - t_start
+    resident, _ = st.size()
+    st.close()
+    eng.close()
+    rate = n / total
+    return {"workload": (f"C5: 6D mixed stream, MR-Angle P={P}, {batch}-tuple micro-batches from pinned host "
+                         f"memory, query_trigger every {per_trigger} tuples, {triggers} triggers, "
+                         + ("landmark window (reference semantics)" if window == 0
+                            else f"count-based sliding window W={window} (extension)")),
+            "ingest_tuples_per_s": rate, "sustains_10M_per_s": rate >= 1e7,
+            "p50_query_latency_ms": statistics.median(lat), "max_query_latency_ms": max(lat),
+            "skyline_size_last": sizes[-1], "resident_tuples_last": resident}
+
+
 def cpu_baseline(d, P, dist_name, seed, sample, domain):
     """Reference algorithm restated in C (per-key BNL, buffer 5000, single-threaded
     global BNL), one thread, on the first `sample` tuples of the same stream."""
@@ -158,6 +197,7 @@ def main():
     ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
     ap.add_argument("--no-dominance", action="store_true")
     ap.add_argument("--no-csv", action="store_true", help="skip the CSV-ingest companion measurement")
+    ap.add_argument("--no-stream", action="store_true", help="skip the C5 continuous-query companion measurement")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the measured path) or gloo (rehearsing ranks on one GPU)")
     args = ap.parse_args()
@@ -249,6 +289,10 @@ def main():
         csvr = None
         if world == 1 and not args.no_csv:
             csvr = csv_ingest_run(eng, ids, vals, n, D, 3, out_ids, out_org)
+        streamr = None
+        if world == 1 and not args.no_stream:
+            streamr = {"landmark": stream_run(dev_index, args.seed),
+                       "sliding_10M": stream_run(dev_index, args.seed, window=10_000_000)}
         domr = None
         if world == 1 and not args.no_dominance:
             domr = dominance_run(dev, D, P, args.dom_n, args.seed, 2, 1)
@@ -281,6 +325,7 @@ def main():
             "cpu_baseline": cpu,
             "dominance_roofline": domr,
             "csv_ingest": csvr,
+            "stream_c5": streamr,
         }
         print(json.dumps(line), flush=True)
     if distributed:

@@ -247,15 +247,40 @@ class SkylineStream:
         check(lib().sky_stream_size(self.h, ctypes.byref(r), ctypes.byref(a)))
         return r.value, a.value
 
+    def _out(self, cap):
+        """Reusable page-locked result buffers (D2H at full PCIe rate), numpy views."""
+        if getattr(self, "_cap", 0) < cap:
+            cap = max(cap, 2 * getattr(self, "_cap", 0))
+            if _abi.torch is not None and _abi.torch.cuda.is_available():
+                t = _abi.torch
+                self._ids = t.empty(cap, dtype=t.int64, pin_memory=True).numpy()
+                self._org = t.empty(cap, dtype=t.int32, pin_memory=True).numpy()
+            else:
+                self._ids = np.empty(cap, np.int64)
+                self._org = np.empty(cap, np.int32)
+            self._cap = cap
+        return self._ids, self._org
+
     def query(self):
-        """-> (ids int64[g], origin int32[g]) of the global skyline, arrival order."""
+        """-> (ids int64[g], origin int32[g]) of the global skyline, arrival order (copies)."""
         r, _ = self.size()
         cap = max(r, 1)
-        ids = np.empty(cap, np.int64)
-        org = np.empty(cap, np.int32)
+        ids, org = self._out(cap)
         g = ctypes.c_int64(0)
         check(lib().sky_stream_query(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
-        return ids[:g.value], org[:g.value]
+        return ids[:g.value].copy(), org[:g.value].copy()
+
+    def query_host_view(self):
+        """Query into the reusable page-locked buffers; returns g (results in view()[:g])."""
+        r, _ = self.size()
+        cap = max(r, 1)
+        ids, org = self._out(cap)
+        g = ctypes.c_int64(0)
+        check(lib().sky_stream_query(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
+        return g.value
+
+    def view(self):
+        return self._ids, self._org
 
     def query_dev(self, d_ids_out, d_origin_out, cap):
         g = ctypes.c_int64(0)
