@@ -27,6 +27,7 @@ SKY_E_NAN = -4
 SKY_E_NOMEM = -5
 SKY_E_NOLIB = -6
 
+SKY_MAX_DIMS = 16
 CSV_OK, CSV_MALFORMED, CSV_BAD_ID, CSV_ARITY = 0, 1, 2, 3
 
 ALGO_DIM, ALGO_GRID, ALGO_ANGLE = 0, 1, 2

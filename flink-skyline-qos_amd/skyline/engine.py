@@ -34,6 +34,7 @@ class SkylineEngine:
         self.P = int(num_partitions)
         self.algo = int(algo)
         self.domain = float(domain)
+        self.device = int(device)
         h = ctypes.c_void_p()
         dev = (ctypes.c_int32 * 1)(device)
         check(lib().sky_ctx_create(dev, 1, self.dims, self.P, self.algo, self.domain, ctypes.byref(h)))

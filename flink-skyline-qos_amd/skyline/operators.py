@@ -43,41 +43,67 @@ def java_format_4f(x):
 class ServiceTuple:
     """ServiceTuple.java:15-115 (data model; dominance is evaluated on the device)."""
 
-    __slots__ = ("id", "values", "originPartition")
+    __slots__ = ("id", "values", "originPartition", "bad_id")
 
     def __init__(self, id=None, values=None):
         self.id = id
         self.values = values
         self.originPartition = -1
+        self.bad_id = False
+
+    @staticmethod
+    def fromStrings(lines, engine):
+        """ServiceTuple.fromString (:89-104) over a batch of raw values, decoded on the device
+        (sky_parse_csv, k_csv.hip): one entry per line, None where fromString returns null.
+        A record whose id is not a Java long yields a tuple flagged `bad_id`; the reference
+        only fails on it later, at Long.parseLong (FlinkSkyline.java:276)."""
+        lines = list(lines)
+        if not lines:
+            return []
+        text = ("\n".join(lines) + "\n").encode("utf-8", "surrogateescape")
+        if any("\n" in x for x in lines):
+            raise ValueError("a raw record contains a newline")
+        import torch
+        dev = torch.device("cuda", engine.device)
+        d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev)
+        R = len(lines)
+        ids = torch.empty(R, dtype=torch.int64, device=dev)
+        vals = torch.empty((R, engine.dims), dtype=torch.float64, device=dev)
+        stat = torch.empty(R, dtype=torch.uint8, device=dev)
+        n, _ = engine.parse_csv_dev(d_text, len(text), ids, vals, R, stat)
+        st = stat.cpu().numpy()
+        ids = ids[:n].cpu().numpy()
+        vals = vals[:n].cpu().numpy()
+        out, k = [], 0
+        for i, c in enumerate(st):
+            if c == _abi.CSV_OK:
+                out.append(ServiceTuple(str(int(ids[k])), vals[k].tolist()))
+                k += 1
+            elif c == _abi.CSV_BAD_ID:
+                t = ServiceTuple(lines[i].split(",", 1)[0], None)
+                t.bad_id = True
+                out.append(t)
+            else:   # malformed (null) or a value count other than the job's dims
+                out.append(None)
+        return out
+
+    _engines = {}
 
     @staticmethod
     def fromString(s):
-        """ServiceTuple.fromString (:89-104): "id,v1,...,vD" -> tuple, None if malformed."""
-        try:
-            p = s.split(",")
-            if len(p) < 2:
-                return None
-            return ServiceTuple(p[0], [_java_parse_double(x) for x in p[1:]])
-        except Exception:
+        """ServiceTuple.fromString (:89-104) for one raw value, decoded on the device."""
+        D = len(s.rstrip(",").split(",")) - 1
+        if D < 1:
             return None
+        if D > _abi.SKY_MAX_DIMS:
+            raise ValueError("more than %d values per tuple" % _abi.SKY_MAX_DIMS)
+        eng = ServiceTuple._engines.get(D)
+        if eng is None:
+            eng = ServiceTuple._engines[D] = SkylineEngine(D, 1, "mr-dim", 1000.0, 0)
+        return ServiceTuple.fromStrings([s], eng)[0]
 
     def __repr__(self):
         return "ID:" + str(self.id) + " " + str(self.values)
-
-
-def _java_parse_double(s):
-    t = s.strip()
-    if t in ("NaN", "+NaN", "-NaN"):
-        return float("nan")
-    if t.endswith(("d", "D", "f", "F")):
-        t = t[:-1]
-    if t.lower() in ("inf", "+inf", "-inf", "infinity", "+infinity", "-infinity", "nan"):
-        if t in ("Infinity", "+Infinity"):
-            return float("inf")
-        if t == "-Infinity":
-            return float("-inf")
-        raise ValueError(s)
-    return float(t)
 
 
 class PartitioningLogic:
@@ -188,6 +214,8 @@ class SkylineLocalProcessor:
         self._state(key)
         if key not in self.startTimeState:
             self.startTimeState[key] = now_ms()
+        if point.bad_id:                                             # Long.parseLong throws (:276)
+            raise ValueError('NumberFormatException: For input string: "%s"' % point.id)
         current_id = int(point.id)                                   # Long.parseLong (:276)
         max_id = self.maxSeenIdState.get(key, -1)
         if current_id > max_id:
@@ -323,7 +351,7 @@ def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=
     local = SkylineLocalProcessor(eng)
     glob = GlobalSkylineAggregator(eng, P)
     emitted, results = [], []
-    tuples = [ServiceTuple.fromString(s) for s in csv_lines]
+    tuples = ServiceTuple.fromStrings(csv_lines, eng)                 # .map(fromString) (:103), on the device
     valid = [t for t in tuples if t is not None]
     keys = part.getKeys(np.asarray([t.values for t in valid], np.float64)) if valid else []
     trig = sorted(triggers)

@@ -173,11 +173,3 @@ def test_java_format_4f():
     assert java_format_4f(0.7378999999999999) == "0.7379"
     assert java_format_4f(2 / 3) == "0.6667"
     assert java_format_4f(0.0) == "0.0000"
-
-
-def test_service_tuple_from_string():
-    from skyline.operators import ServiceTuple
-    t = ServiceTuple.fromString("101,25.5,0.99")
-    assert t.id == "101" and t.values == [25.5, 0.99]
-    assert ServiceTuple.fromString("7") is None
-    assert ServiceTuple.fromString("x,abc") is None

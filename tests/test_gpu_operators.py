@@ -140,3 +140,15 @@ def test_multi_rank_decomposition(gpu_engine_factory, oracle):
     np.testing.assert_array_equal(go, exp_org)
     for e in engs:
         e.close()
+
+
+def test_service_tuple_from_string_on_device():
+    """ServiceTuple.fromString (ServiceTuple.java:89-104) decoded by k_csv.hip."""
+    from skyline.operators import ServiceTuple
+    t = ServiceTuple.fromString("101,25.5,0.99")
+    assert t.id == "101" and t.values == [25.5, 0.99]
+    assert ServiceTuple.fromString("7") is None
+    assert ServiceTuple.fromString("x,abc") is None
+    t = ServiceTuple.fromString("x,1.5")          # fromString accepts it; Long.parseLong fails later
+    assert t is not None and t.bad_id
+    assert ServiceTuple.fromString("5,1e3f, 2 ,") .values == [1000.0, 2.0]
