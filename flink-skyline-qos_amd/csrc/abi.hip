@@ -985,3 +985,52 @@ int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64
     return SKY_OK;
     GUARD_END
 }
+
+int sky_profile_sort_dev(sky_ctx *c, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int32_t *passes_out,
+                         double *ms_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && d_keys && d_vals && n >= 0 && n < (int64_t)0xffffffffLL, "bad arguments");
+    SKY_TRY(bind(c));
+    const uint32_t m = (uint32_t)n;
+    SKY_TRY(c->prof_k.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    SKY_TRY(c->prof_v.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    SKY_TRY(c->prof_scr.ensure(radix_scratch_words(m) * 4 + 64));
+    SKY_TRY(c->csv_counts.ensure(64 + 256 * 8));
+    unsigned long long *d_orand = c->csv_counts.as<unsigned long long>();
+    radix_key_orand(d_keys, m, d_orand, c->st);
+    unsigned long long orand[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(orand, d_orand, 16, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    const uint64_t varying = orand[0] ^ orand[1];
+    int passes = 0;
+    for (int b = 0; b < 8; b++) passes += ((varying >> (8 * b)) & 0xff) ? 1 : 0;
+    const int nbits = __builtin_popcountll(varying);
+    uint32_t *err = reinterpret_cast<uint32_t *>(d_orand + 4);
+    HIP_TRY(hipMemsetAsync(err, 0, 4, c->st));
+    hipEvent_t a = c->take_event(), b = c->take_event();
+    HIP_TRY(hipEventRecord(a, c->st));
+    const bool alt = radix_sort_pairs(d_keys, d_vals, c->prof_k.as<uint64_t>(), c->prof_v.as<uint32_t>(), m, orand[0],
+                                      orand[1], c->prof_scr.as<uint32_t>(), err, c->st);
+    HIP_TRY(hipEventRecord(b, c->st));
+    if (alt) {
+        HIP_TRY(hipMemcpyAsync(d_keys, c->prof_k.p, (size_t)n * 8, hipMemcpyDeviceToDevice, c->st));
+        HIP_TRY(hipMemcpyAsync(d_vals, c->prof_v.p, (size_t)n * 4, hipMemcpyDeviceToDevice, c->st));
+    }
+    uint32_t h_err = 0;
+    HIP_TRY(hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    c->event_pool.push_back(a);
+    c->event_pool.push_back(b);
+    if (h_err) {
+        set_error("radix sort look-back spin bound reached");
+        return SKY_E_HIP;
+    }
+    (void)passes;
+    (void)nbits;
+    if (passes_out) *passes_out = radix_last_passes();
+    if (ms_out) *ms_out = ms;
+    return SKY_OK;
+    GUARD_END
+}

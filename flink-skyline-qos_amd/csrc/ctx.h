@@ -63,6 +63,7 @@ struct Ctx {
     DevBuf exp_scan;
     // bulk CSV ingest workspace (k_csv.hip)
     DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow;
+    DevBuf prof_k, prof_v, prof_scr;   // sky_profile_sort_dev workspace
 
     int Kq() const {
         if (algo == SKY_ALGO_GRID && sem == SKY_SEM_COMPLETE) return std::max(P, 1 << D);

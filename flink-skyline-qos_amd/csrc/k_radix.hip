@@ -136,15 +136,26 @@ __global__ __launch_bounds__(256) void k_rs_expand(const uint64_t *__restrict__ 
 
 constexpr uint32_t kRsAgg = 1u << 30, kRsInc = 2u << 30, kRsCount = (1u << 30) - 1;
 
+// One LSD pass over ITEMS*256-key tiles.  Wave w of a tile owns the contiguous chunk
+// [w*64*ITEMS, (w+1)*64*ITEMS): it ranks its keys digit by digit with 8 ballots per item
+// and a per-wave running count in LDS (the peer group's leader updates it; the others get
+// the old value by a shuffle), so the ranking needs no workgroup barrier per item; the
+// order (wave, item, lane) is the index order, so the pass is stable.  Then: tile digit
+// counts published, decoupled look-back for the exclusive prefix, keys staged in LDS in
+// digit order, coalesced writes of each digit run.  Large tiles (ITEMS = 16) keep the
+// runs of one digit long (write coalescing); short tiles (ITEMS = 4) keep more
+// workgroups in flight for the small candidate sorts of a query.
+template <int ITEMS>
 __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     const uint64_t *__restrict__ keys_in, const uint32_t *__restrict__ vals_in,
     uint64_t *__restrict__ keys_out, uint32_t *__restrict__ vals_out, uint32_t m, int shift,
     const uint32_t *__restrict__ gbase, uint32_t *__restrict__ status, uint32_t *__restrict__ ticket,
     uint32_t *__restrict__ err) {
-    __shared__ uint64_t s_key[kRadixTile];
-    __shared__ uint32_t s_val[kRadixTile];
-    __shared__ uint32_t s_cnt[4][256];
-    __shared__ uint32_t s_wb[4][256];
+    constexpr int TILE = kRadixThreads * ITEMS;
+    constexpr int WCH = 64 * ITEMS;
+    __shared__ uint64_t s_key[TILE];
+    __shared__ uint32_t s_val[TILE];
+    __shared__ uint32_t s_wc[4][256];
     __shared__ uint32_t s_run[256];
     __shared__ uint32_t s_start[256];
     __shared__ uint32_t s_goff[256];
@@ -155,22 +166,26 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     // tiles that started before it (forward progress of the look-back)
     if (t == 0) s_tile = atomicAdd(ticket, 1u);
 #pragma unroll
-    for (int i = 0; i < 4; i++) s_cnt[i][t] = 0;
-    s_run[t] = 0;
+    for (int i = 0; i < 4; i++) s_wc[i][t] = 0;
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint32_t base = tile * kRadixTile;
+    const uint32_t base = tile * TILE;
 
-    uint64_t k[kRadixItems];
-    uint32_t v[kRadixItems];
-    uint32_t rk[kRadixItems];
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    uint32_t rk[ITEMS];
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
-        const uint32_t i = base + r * kRadixThreads + t;
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t i = base + w * WCH + r * 64 + lane;
         const bool valid = i < m;
         k[r] = valid ? keys_in[i] : 0ull;
         v[r] = valid ? vals_in[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; r++) {
+        const uint32_t i = base + w * WCH + r * 64 + lane;
+        const bool valid = i < m;
         const uint32_t d = (uint32_t)(k[r] >> shift) & 255u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -180,20 +195,23 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
             peers &= bit ? bb : ~bb;
         }
         const uint32_t pre = __popcll(peers & lt_mask);
-        if (valid && pre == 0) s_cnt[w][d] = __popcll(peers);
-        __syncthreads();
-        {
-            const uint32_t c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
-            const uint32_t run = s_run[t];
-            s_wb[0][t] = run;
-            s_wb[1][t] = run + c0;
-            s_wb[2][t] = run + c0 + c1;
-            s_wb[3][t] = run + c0 + c1 + c2;
-            s_run[t] = run + c0 + c1 + c2 + c3;
-            s_cnt[0][t] = 0; s_cnt[1][t] = 0; s_cnt[2][t] = 0; s_cnt[3][t] = 0;
+        uint32_t old = 0;
+        if (valid && pre == 0) {
+            old = s_wc[w][d];
+            s_wc[w][d] = old + __popcll(peers);
         }
-        __syncthreads();
-        rk[r] = valid ? s_wb[w][d] + pre : 0xffffffffu;
+        const int leader = peers ? __ffsll((long long)peers) - 1 : 0;
+        old = __shfl(old, leader, 64);
+        rk[r] = valid ? old + pre : 0xffffffffu;
+    }
+    __syncthreads();
+    {   // digit t: wave bases within the tile and the tile aggregate
+        const uint32_t c0 = s_wc[0][t], c1 = s_wc[1][t], c2 = s_wc[2][t], c3 = s_wc[3][t];
+        s_wc[0][t] = 0;
+        s_wc[1][t] = c0;
+        s_wc[2][t] = c0 + c1;
+        s_wc[3][t] = c0 + c1 + c2;
+        s_run[t] = c0 + c1 + c2 + c3;
     }
     // publish this tile's digit count, look back for the exclusive prefix
     {
@@ -207,15 +225,15 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
             int64_t pt = (int64_t)tile - 1;
             uint32_t spins = 0;
             while (pt >= 0) {
-                const uint32_t v = __hip_atomic_load(status + (size_t)pt * 256 + t, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t f = v & ~kRsCount;
+                const uint32_t sv = __hip_atomic_load(status + (size_t)pt * 256 + t, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t f = sv & ~kRsCount;
                 if (f == 0u) {
                     if (++spins > (1u << 24)) { atomicOr(err, kFlagRadixSpin); break; }   // bounded spin
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                excl += v & kRsCount;
+                excl += sv & kRsCount;
                 if (f == kRsInc) break;
                 pt--;
             }
@@ -225,15 +243,14 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     }
     // tile-local digit starts
     {
-        const int lanei = t & 63;
         uint32_t c = s_run[t];
         uint32_t inc = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             uint32_t y = __shfl_up(inc, o, 64);
-            if (lanei >= o) inc += y;
+            if (lane >= o) inc += y;
         }
-        if (lanei == 63) s_w[w] = inc;
+        if (lane == 63) s_w[w] = inc;
         __syncthreads();
         uint32_t wb = 0;
         for (int i = 0; i < w; i++) wb += s_w[i];
@@ -241,18 +258,18 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
+    for (int r = 0; r < ITEMS; r++) {
         if (rk[r] != 0xffffffffu) {
             const uint32_t d = (uint32_t)(k[r] >> shift) & 255u;
-            const uint32_t p = s_start[d] + rk[r];
+            const uint32_t p = s_start[d] + s_wc[w][d] + rk[r];
             s_key[p] = k[r];
             s_val[p] = v[r];
         }
     }
     __syncthreads();
-    const uint32_t nvalid = m - base < (uint32_t)kRadixTile ? m - base : (uint32_t)kRadixTile;
+    const uint32_t nvalid = m - base < (uint32_t)TILE ? m - base : (uint32_t)TILE;
 #pragma unroll
-    for (int r = 0; r < kRadixItems; r++) {
+    for (int r = 0; r < ITEMS; r++) {
         const uint32_t q = r * kRadixThreads + t;
         if (q < nvalid) {
             const uint64_t kk = s_key[q];
@@ -263,6 +280,9 @@ __global__ __launch_bounds__(kRadixThreads) void k_rs_onesweep(
         }
     }
 }
+
+static thread_local int g_radix_last_passes = 0;
+int radix_last_passes() { return g_radix_last_passes; }
 
 // debug check (SKY_DEBUG >= 4): sorted, a permutation, keys match their source slots
 __global__ __launch_bounds__(256) void k_rs_check(const uint64_t *__restrict__ orig, const uint64_t *__restrict__ skey,
@@ -296,8 +316,11 @@ size_t radix_scratch_words(size_t m) {
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
                       uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st) {
     const uint64_t varying_bits = key_or ^ key_and;
+    g_radix_last_passes = 0;
     if (m <= 1 || varying_bits == 0) return false;
-    const uint32_t tiles = (m + kRadixTile - 1) / kRadixTile;
+    const bool big = m >= (1u << 22);   // 4096-key tiles for large sorts, 1024 for the query's candidates
+    const uint32_t tile_sz = big ? 4096u : (uint32_t)kRadixTile;
+    const uint32_t tiles = (m + tile_sz - 1) / tile_sz;
     RsRuns runs{};
     int nbits = 0;
     bool too_many_runs = false;
@@ -345,13 +368,20 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     k_rs_hist_all<<<hb, kRadixThreads, 0, st>>>(k0, m, shifts, npass, ghist);
     k_rs_scan_all<<<1, 256, 0, st>>>(ghist, npass);
     bool alt = false;
+    g_radix_last_passes = npass;
     for (int p = 0; p < npass; p++) {
         const uint64_t *kin = alt ? k1 : k0;
         const uint32_t *vin = alt ? vals_alt : vals;
         uint64_t *kout = alt ? k0 : k1;
         uint32_t *vout = alt ? vals : vals_alt;
-        k_rs_onesweep<<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], ghist + p * 256,
-                                                       status + (size_t)p * 256 * tiles, tickets + p, err);
+        if (big)
+            k_rs_onesweep<16><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], ghist + p * 256,
+                                                               status + (size_t)p * 256 * tiles, tickets + p, err);
+        else
+            k_rs_onesweep<kRadixItems><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p],
+                                                                        ghist + p * 256,
+                                                                        status + (size_t)p * 256 * tiles,
+                                                                        tickets + p, err);
         alt = !alt;
     }
     if (!compress) return alt;
@@ -362,8 +392,10 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
 }
 
 void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st) {
-    unsigned long long init[2] = {0ull, ~0ull};
-    hipMemcpyAsync(d_orand, init, sizeof(init), hipMemcpyHostToDevice, st);
+    // OR accumulator = 0, AND accumulator = all ones (memsets: no host buffer whose
+    // lifetime would have to outlast an asynchronous copy)
+    hipMemsetAsync(d_orand, 0, 8, st);
+    hipMemsetAsync(d_orand + 1, 0xff, 8, st);
     unsigned blocks = (unsigned)((m + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     if (blocks == 0) blocks = 1;

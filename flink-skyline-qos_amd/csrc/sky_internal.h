@@ -37,6 +37,7 @@ void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_tota
 
 // ---- k_radix.hip ----
 size_t radix_scratch_words(size_t m);
+int radix_last_passes();   // digit passes of this thread's last radix_sort_pairs
 // err: device word, kFlagRadixSpin is OR-ed in if a look-back spin ran out (never
 // expected; the caller checks it at its next synchronisation)
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,

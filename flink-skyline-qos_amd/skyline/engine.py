@@ -165,6 +165,15 @@ class SkylineEngine:
                                        ctypes.byref(nb)))
         return nb.value
 
+    def profile_sort_dev(self, d_keys, d_vals):
+        """Runs the pipeline's radix sort alone on (int64 keys as u64, int32 values as u32),
+        in place; returns (passes, ms)."""
+        p = ctypes.c_int32(0)
+        ms = ctypes.c_double(0)
+        check(lib().sky_profile_sort_dev(self.h, _tptr(d_keys), _tptr(d_vals), d_keys.numel(), ctypes.byref(p),
+                                         ctypes.byref(ms)))
+        return p.value, ms.value
+
     def set_stream(self, stream_ptr):
         check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 

@@ -212,6 +212,11 @@ int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t
  * distinct union of the local skylines; D compares per pair test */
 int sky_profile_dominance(sky_ctx *ctx, int64_t *work_out);
 int sky_profile_reset(sky_ctx *ctx);
+/* the pipeline's device radix sort (k_radix.hip: onesweep LSD, 8-bit digits over the varying
+ * key bits) run alone on n (u64 key, u32 value) pairs in place, for the sort-phase HBM
+ * roofline at scale; *passes_out = digit passes, *ms_out = HIP-event time of the sort */
+int sky_profile_sort_dev(sky_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int32_t *passes_out,
+                         double *ms_out);
 
 #ifdef __cplusplus
 }
