@@ -196,6 +196,83 @@ int64_t orc_query_bnl(int algo, const double *vals, const int64_t *ids, int64_t 
     return g <= cap ? g : -1;
 }
 
+/*
+ * The same query with the local phase run the way the Flink job parallelises it:
+ * one thread per operator subtask, each owning the keys k with k % nthreads == t
+ * (Flink's murmur key-group assignment is not vendored; round-robin stands in for
+ * it), running the per-key buffer + BNL of processElement1/processBuffer
+ * (FlinkSkyline.java:265-316, :417-444) over its keys' tuples in stream order.
+ * The global merge stays single-threaded, as GlobalSkylineAggregator is keyed by
+ * the query (:515-569).  Used only as the multi-core CPU baseline of bench.py;
+ * results are identical to orc_query_bnl (the keys are independent).
+ */
+#include <pthread.h>
+
+typedef struct {
+    const double *vals;
+    const int32_t *keys;
+    int64_t n;
+    int D, K, buffer_size, t, T;
+    ilist *state;
+} bnl_task;
+
+static void *bnl_worker(void *arg) {
+    bnl_task *a = (bnl_task *)arg;
+    ilist *buf = (ilist *)calloc((size_t)a->K, sizeof(ilist));
+    for (int64_t i = 0; i < a->n; i++) {
+        int32_t k = a->keys[i];
+        if (k < 0 || k >= a->K || k % a->T != a->t) continue;
+        il_push(&buf[k], i);
+        if (buf[k].len >= a->buffer_size) {
+            for (int64_t j = 0; j < buf[k].len; j++) bnl_step(&a->state[k], buf[k].a[j], a->vals, a->D);
+            buf[k].len = 0;
+        }
+    }
+    for (int k = a->t; k < a->K; k += a->T) {
+        for (int64_t j = 0; j < buf[k].len; j++) bnl_step(&a->state[k], buf[k].a[j], a->vals, a->D);
+        free(buf[k].a);
+    }
+    free(buf);
+    return NULL;
+}
+
+int64_t orc_query_bnl_mt(int algo, const double *vals, const int64_t *ids, int64_t n, int D, int P, double domain,
+                         int buffer_size, int nthreads, int64_t *out_ids, int32_t *out_origin, int64_t cap,
+                         int64_t *local_sizes, int64_t *survivors) {
+    const int K = P;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    int32_t *keys = (int32_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+    orc_keys(algo, vals, n, D, P, domain, keys);
+    ilist *state = (ilist *)calloc((size_t)K, sizeof(ilist));
+    pthread_t th[256];
+    bnl_task task[256];
+    for (int t = 0; t < nthreads; t++) {
+        task[t] = (bnl_task){vals, keys, n, D, K, buffer_size, t, nthreads, state};
+        pthread_create(&th[t], NULL, bnl_worker, &task[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    ilist G = {0};
+    int32_t *origin_of = (int32_t *)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+    for (int k = 0; k < K; k++) {
+        local_sizes[k] = state[k].len;
+        survivors[k] = 0;
+        for (int64_t j = 0; j < state[k].len; j++) {
+            origin_of[state[k].a[j]] = k;
+            bnl_step(&G, state[k].a[j], vals, D);
+        }
+    }
+    int64_t g = G.len;
+    for (int64_t j = 0; j < g; j++) {
+        int64_t r = G.a[j];
+        survivors[origin_of[r]]++;
+        if (j < cap) { out_ids[j] = ids[r]; out_origin[j] = origin_of[r]; }
+    }
+    for (int k = 0; k < K; k++) free(state[k].a);
+    free(state); free(G.a); free(keys); free(origin_of);
+    return g <= cap ? g : -1;
+}
+
 /* Definition check: brute-force skyline membership (test oracle for BNL). */
 void orc_skyline_brute(const double *vals, int64_t n, int D, uint8_t *in_sky) {
     for (int64_t i = 0; i < n; i++) {

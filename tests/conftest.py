@@ -42,6 +42,9 @@ def load_oracle():
         L.orc_query_bnl.restype = ctypes.c_int64
         L.orc_query_bnl.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_double, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.c_int64, dp, dp]
+        L.orc_query_bnl_mt.restype = ctypes.c_int64
+        L.orc_query_bnl_mt.argtypes = [ctypes.c_int, dp, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_int, ctypes.c_int, dp, dp, ctypes.c_int64, dp, dp]
         L.orc_query_sfs.restype = ctypes.c_int64
         L.orc_query_sfs.argtypes = [ctypes.c_int, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                     ctypes.c_int, dp, dp, dp, dp, dp]
@@ -84,6 +87,19 @@ class Oracle:
         sv = np.zeros(K, np.int64)
         g = self.L.orc_query_bnl(self.ALGO[algo], P(v), P(ids), n, D, P_, domain, buffer_size, sem, P(oi), P(oo),
                                  n, P(ls), P(sv))
+        assert g >= 0
+        return oi[:g], oo[:g], ls, sv
+
+    def query_bnl_mt(self, algo, vals, ids, P_, threads, domain=1000.0, buffer_size=5000):
+        v = np.ascontiguousarray(vals, np.float64)
+        ids = np.ascontiguousarray(ids, np.int64)
+        n, D = v.shape
+        oi = np.zeros(max(n, 1), np.int64)
+        oo = np.zeros(max(n, 1), np.int32)
+        ls = np.zeros(P_, np.int64)
+        sv = np.zeros(P_, np.int64)
+        g = self.L.orc_query_bnl_mt(self.ALGO[algo], P(v), P(ids), n, D, P_, domain, buffer_size, threads, P(oi),
+                                    P(oo), n, P(ls), P(sv))
         assert g >= 0
         return oi[:g], oo[:g], ls, sv
 

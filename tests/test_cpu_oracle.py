@@ -173,3 +173,15 @@ def test_java_format_4f():
     assert java_format_4f(0.7378999999999999) == "0.7379"
     assert java_format_4f(2 / 3) == "0.6667"
     assert java_format_4f(0.0) == "0.0000"
+
+
+def test_multithreaded_bnl_equals_single(oracle):
+    """The multi-core CPU baseline (one thread per subtask) gives the same answer."""
+    for dist, D in ((2, 4), (0, 3), (1, 6)):
+        vals = oracle.synth(dist, D, 20000, seed=3)
+        ids = np.arange(20000, dtype=np.int64)
+        a = oracle.query_bnl("angle", vals, ids, 8)
+        for T in (1, 3, 8):
+            b = oracle.query_bnl_mt("angle", vals, ids, 8, T)
+            assert sorted(a[0].tolist()) == sorted(b[0].tolist())
+            assert (a[2] == b[2]).all() and (a[3] == b[3]).all()
