@@ -148,6 +148,27 @@ int sky_ctx_set_stream(sky_ctx *c, void *s) {
     return SKY_OK;
 }
 
+int sky_ctx_wait_stream(sky_ctx *c, void *s) {
+    ARG_CHECK(c, "ctx is null");
+    SKY_TRY(bind(c));
+    if ((hipStream_t)s == c->st) return SKY_OK;
+    hipEvent_t e = c->take_event();
+    HIP_TRY(hipEventRecord(e, (hipStream_t)s));
+    HIP_TRY(hipStreamWaitEvent(c->st, e, 0));
+    c->event_pool.push_back(e);   // re-recording later does not affect the enqueued wait
+    return SKY_OK;
+}
+int sky_ctx_signal_stream(sky_ctx *c, void *s) {
+    ARG_CHECK(c, "ctx is null");
+    SKY_TRY(bind(c));
+    if ((hipStream_t)s == c->st) return SKY_OK;
+    hipEvent_t e = c->take_event();
+    HIP_TRY(hipEventRecord(e, c->st));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)s, e, 0));
+    c->event_pool.push_back(e);
+    return SKY_OK;
+}
+
 int sky_ctx_sync(sky_ctx *c) {
     ARG_CHECK(c, "ctx is null");
     SKY_TRY(bind(c));

@@ -53,6 +53,8 @@ SIGNATURES = {
     "sky_ctx_set_semantics": [c_p, c_int],
     "sky_ctx_set_stream": [c_p, c_p],
     "sky_ctx_sync": [c_p],
+    "sky_ctx_wait_stream": [c_p, c_p],
+    "sky_ctx_signal_stream": [c_p, c_p],
     "sky_partition_keys": [c_p, c_p, c_i64, c_p],
     "sky_partition_keys_dev": [c_p, c_p, c_i64, c_p],
     "sky_part_open": [c_p, c_i32, ctypes.POINTER(c_p)],

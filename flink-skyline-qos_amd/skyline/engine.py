@@ -19,6 +19,29 @@ def _tptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+class _Ordered:
+    """Brackets a *_dev call: the library's stream first waits for the caller's current
+    torch stream (which produced the inputs), and the torch stream then waits for the
+    library (which wrote the outputs).  GPU-side events only."""
+
+    def __init__(self, h, device):
+        self.h = h
+        self.s = None
+        t = _abi.torch
+        if t is not None and t.cuda.is_available():
+            self.s = ctypes.c_void_p(t.cuda.current_stream(device).cuda_stream)
+
+    def __enter__(self):
+        if self.s is not None:
+            check(lib().sky_ctx_wait_stream(self.h, self.s))
+        return self
+
+    def __exit__(self, *exc):
+        if self.s is not None and exc[0] is None:
+            check(lib().sky_ctx_signal_stream(self.h, self.s))
+        return False
+
+
 class SkylineEngine:
     """One context = one device, D dims, P partitions, one partitioner.
 
@@ -63,7 +86,8 @@ class SkylineEngine:
 
     def partition_keys_dev(self, d_values, d_keys_out):
         n = d_values.numel() // self.dims
-        check(lib().sky_partition_keys_dev(self.h, _tptr(d_values), n, _tptr(d_keys_out)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_partition_keys_dev(self.h, _tptr(d_values), n, _tptr(d_keys_out)))
 
     # ---- fused query ---------------------------------------------------------------
     def query(self, values, ids=None):
@@ -82,8 +106,9 @@ class SkylineEngine:
     def query_dev(self, d_ids, d_values, d_ids_out, d_origin_out, cap):
         n = d_values.numel() // self.dims
         cnt = ctypes.c_int64(0)
-        check(lib().sky_query_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_ids_out),
-                                  _tptr(d_origin_out), cap, ctypes.byref(cnt)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_query_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_ids_out),
+                                      _tptr(d_origin_out), cap, ctypes.byref(cnt)))
         return cnt.value
 
     def stats(self):
@@ -117,23 +142,27 @@ class SkylineEngine:
     def export_local_dev(self, d_ids, d_values):
         n = d_values.numel() // self.dims
         cnt = ctypes.c_int64(0)
-        check(lib().sky_export_local_dev(self.h, _tptr(d_ids), _tptr(d_values), n, ctypes.byref(cnt)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_export_local_dev(self.h, _tptr(d_ids), _tptr(d_values), n, ctypes.byref(cnt)))
         return cnt.value
 
     def export_copy_dev(self, d_rows, d_keys, d_mult, cap):
-        check(lib().sky_export_copy_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), cap))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_export_copy_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), cap))
 
     def import_union_dev(self, d_rows, d_keys, d_mult, n_union, self_offset, d_ids_out, d_origin_out, cap):
         cnt = ctypes.c_int64(0)
-        check(lib().sky_import_union_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), n_union, self_offset,
-                                         _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(cnt)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_import_union_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), n_union, self_offset,
+                                             _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(cnt)))
         return cnt.value
 
     # ---- utilities -----------------------------------------------------------------------
     def synth_dev(self, dist, n, d_values, d_ids=None, seed=1234, id0=0, dmin=0, dmax=1000):
         if isinstance(dist, str):
             dist = _abi.DISTS[dist]
-        check(lib().sky_synth_dev(self.h, dist, dmin, dmax, seed, id0, n, _tptr(d_values), _tptr(d_ids)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_synth_dev(self.h, dist, dmin, dmax, seed, id0, n, _tptr(d_values), _tptr(d_ids)))
 
     # ---- bulk CSV ingest (ServiceTuple.fromString over raw records, ServiceTuple.java:89-104)
     def parse_csv(self, text):
@@ -153,16 +182,18 @@ class SkylineEngine:
         """Device bytes -> device rows; returns (accepted, counts int64[4])."""
         n = ctypes.c_int64(0)
         cnt = np.zeros(4, np.int64)
-        check(lib().sky_parse_csv_dev(self.h, _tptr(d_text), nbytes, _tptr(d_ids_out), _tptr(d_values_out), cap,
-                                      ctypes.byref(n), cnt.ctypes.data_as(_abi.P_i64), _tptr(d_status_out)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_parse_csv_dev(self.h, _tptr(d_text), nbytes, _tptr(d_ids_out), _tptr(d_values_out), cap,
+                                          ctypes.byref(n), cnt.ctypes.data_as(_abi.P_i64), _tptr(d_status_out)))
         return n.value, cnt
 
     def format_csv_dev(self, d_ids, d_values, n, d_text=None, cap=0):
         """The producers' "id,v1,...,vD\n" payload of a device stream; returns its byte count
         (call with d_text=None first to size the buffer)."""
         nb = ctypes.c_int64(0)
-        check(lib().sky_format_csv_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_text), cap,
-                                       ctypes.byref(nb)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_format_csv_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_text), cap,
+                                           ctypes.byref(nb)))
         return nb.value
 
     def profile_sort_dev(self, d_keys, d_vals):
@@ -170,8 +201,9 @@ class SkylineEngine:
         in place; returns (passes, ms)."""
         p = ctypes.c_int32(0)
         ms = ctypes.c_double(0)
-        check(lib().sky_profile_sort_dev(self.h, _tptr(d_keys), _tptr(d_vals), d_keys.numel(), ctypes.byref(p),
-                                         ctypes.byref(ms)))
+        with _Ordered(self.h, self.device):
+            check(lib().sky_profile_sort_dev(self.h, _tptr(d_keys), _tptr(d_vals), d_keys.numel(), ctypes.byref(p),
+                                             ctypes.byref(ms)))
         return p.value, ms.value
 
     def set_stream(self, stream_ptr):
@@ -250,7 +282,8 @@ class SkylineStream:
 
     def append_dev(self, d_ids, d_values, n=None):
         n = d_values.shape[0] if n is None else n
-        check(lib().sky_stream_append_dev(self.h, _tptr(d_ids), _tptr(d_values), n))
+        with _Ordered(self.engine.h, self.engine.device):
+            check(lib().sky_stream_append_dev(self.h, _tptr(d_ids), _tptr(d_values), n))
 
     def size(self):
         r, a = ctypes.c_int64(0), ctypes.c_int64(0)
@@ -294,5 +327,6 @@ class SkylineStream:
 
     def query_dev(self, d_ids_out, d_origin_out, cap):
         g = ctypes.c_int64(0)
-        check(lib().sky_stream_query_dev(self.h, _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(g)))
+        with _Ordered(self.engine.h, self.engine.device):
+            check(lib().sky_stream_query_dev(self.h, _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(g)))
         return g.value

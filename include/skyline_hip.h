@@ -85,6 +85,13 @@ int sky_ctx_set_semantics(sky_ctx *ctx, int semantics);
  * NULL returns to the context's own stream. */
 int sky_ctx_set_stream(sky_ctx *ctx, void *hip_stream);
 int sky_ctx_sync(sky_ctx *ctx);
+/* cross-stream ordering for *_dev callers that produce / consume the device buffers on
+ * their own HIP stream (e.g. a framework's current stream): wait_stream makes the
+ * context's later work wait for everything already enqueued on `hip_stream`;
+ * signal_stream makes `hip_stream`'s later work wait for everything already enqueued
+ * on the context.  GPU-side only (events), no host synchronisation. */
+int sky_ctx_wait_stream(sky_ctx *ctx, void *hip_stream);
+int sky_ctx_signal_stream(sky_ctx *ctx, void *hip_stream);
 const char *sky_last_error(void);
 const char *sky_version(void);
 
