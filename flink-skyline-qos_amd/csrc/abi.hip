@@ -148,6 +148,12 @@ int sky_ctx_set_stream(sky_ctx *c, void *s) {
     return SKY_OK;
 }
 
+int sky_ctx_set_grid_filter(sky_ctx *c, int on) {
+    ARG_CHECK(c, "ctx is null");
+    c->grid_filter = on ? 1 : 0;
+    return SKY_OK;
+}
+
 int sky_ctx_wait_stream(sky_ctx *c, void *s) {
     ARG_CHECK(c, "ctx is null");
     SKY_TRY(bind(c));

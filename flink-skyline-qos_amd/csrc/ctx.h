@@ -42,7 +42,7 @@ struct KTime {
 };
 
 struct Ctx {
-    int dev = 0, D = 2, P = 8, algo = SKY_ALGO_ANGLE, sem = SKY_SEM_REFERENCE;
+    int dev = 0, D = 2, P = 8, algo = SKY_ALGO_ANGLE, sem = SKY_SEM_REFERENCE, grid_filter = 0;
     double domain = 1000.0;
     hipStream_t own = nullptr, st = nullptr;
     Pipe main, aux;
@@ -77,6 +77,7 @@ struct Ctx {
         k.dim_width = domain / (double)P;
         k.grid_mid = domain / 2.0;
         k.margin = angle_margin(P);
+        k.grid_filter = algo == SKY_ALGO_GRID ? grid_filter : 0;
         return k;
     }
     hipEvent_t take_event() {

@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kThreads) void k_keys(const double *__restrict__ va
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
         double v[D];
         load_row<D>(vals + (size_t)i * D, v);
-        keys[i] = partition_key<D>(v, kp);
+        const int32_t kk = partition_key<D>(v, kp);
+        keys[i] = kk == kKeyFiltered ? -1 : kk;   // API: -1 = removed by the grid filter
     }
 }
 

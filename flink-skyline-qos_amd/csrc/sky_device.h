@@ -119,6 +119,8 @@ struct KeyParams {
     double dim_width;  // maxVal / partitions  (:710)
     double grid_mid;   // maxVal / 2.0          (:756)
     double margin;     // MR-Angle fast path: distance of avg*P from an integer that is certain
+    int grid_filter;   // MR-Grid dominance filter (FlinkSkyline.java:716-733, disabled in the reference):
+                       // tuples with every value >= maxVal/2 get key -1 (removed before keyBy)
 };
 
 // Error budget of the f32 estimate in t = avg*P (inputs with nonzero magnitudes in
@@ -191,6 +193,7 @@ __device__ __forceinline__ int32_t angle_key_exact(const double (&v)[D], int P) 
 // kAngleUndecided: the fast path could not certify the key (non-ranged input or
 // t within `margin` of an integer); the caller runs angle_key_exact.
 constexpr int32_t kAngleUndecided = -1;
+constexpr int32_t kKeyFiltered = -2;   // removed by the MR-Grid dominance filter (never queried)
 
 template <int D>
 __device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, double margin) {
@@ -249,6 +252,7 @@ __device__ __forceinline__ int32_t partition_key_fast(const double (&v)[D], cons
 #pragma unroll
         for (int i = 0; i < D; i++)
             if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
+        if (kp.grid_filter && mask == (D >= 32 ? ~0u : (1u << D) - 1u)) return kKeyFiltered;
         return (int32_t)mask;
     }
     return angle_key_fast<D>(v, kp.P, kp.margin);
@@ -262,6 +266,7 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
 #pragma unroll
         for (int i = 0; i < D; i++)
             if (v[i] >= kp.grid_mid) mask |= (1u << (i & 31));
+        if (kp.grid_filter && mask == (D >= 32 ? ~0u : (1u << D) - 1u)) return kKeyFiltered;
         return (int32_t)mask;
     }
     const int32_t k = angle_key_fast<D>(v, kp.P, kp.margin);

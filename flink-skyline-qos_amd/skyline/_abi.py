@@ -52,6 +52,7 @@ SIGNATURES = {
     "sky_ctx_destroy": [c_p],
     "sky_ctx_set_semantics": [c_p, c_int],
     "sky_ctx_set_stream": [c_p, c_p],
+    "sky_ctx_set_grid_filter": [c_p, c_int],
     "sky_ctx_sync": [c_p],
     "sky_ctx_wait_stream": [c_p, c_p],
     "sky_ctx_signal_stream": [c_p, c_p],

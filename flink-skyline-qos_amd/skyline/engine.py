@@ -50,7 +50,7 @@ class SkylineEngine:
     """
 
     def __init__(self, dims, num_partitions, algo="mr-angle", domain=1000.0, device=0,
-                 semantics="reference"):
+                 semantics="reference", grid_filter=False):
         if isinstance(algo, str):
             algo = _abi.ALGOS.get(algo.lower(), _abi.ALGO_ANGLE)  # reference default branch (:129-133)
         self.dims = int(dims)
@@ -64,6 +64,8 @@ class SkylineEngine:
         self.h = h
         if semantics != "reference":
             check(lib().sky_ctx_set_semantics(self.h, _abi.SEM_COMPLETE))
+        if grid_filter:   # GridDominanceFilter (FlinkSkyline.java:716-733)
+            check(lib().sky_ctx_set_grid_filter(self.h, 1))
         self.K = self.P if not (self.algo == _abi.ALGO_GRID and semantics == "complete") else max(self.P, 1 << self.dims)
 
     def close(self):

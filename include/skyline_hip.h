@@ -81,6 +81,11 @@ int sky_ctx_create(const int *devices, int ndev, int dims, int num_partitions, i
                    double domain_max, sky_ctx **out);
 int sky_ctx_destroy(sky_ctx *ctx);
 int sky_ctx_set_semantics(sky_ctx *ctx, int semantics);
+/* MR-Grid dominance filter (FlinkSkyline.java:716-733, commented out in the reference, with
+ * its `processedData` hook at :107): on = drop every tuple whose values are all >= maxVal/2
+ * before keyBy (its key becomes -1).  Such a tuple is dominated whenever the stream holds a
+ * tuple with every value < maxVal/2, so the skyline is unchanged then.  Off by default. */
+int sky_ctx_set_grid_filter(sky_ctx *ctx, int on);
 /* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
  * NULL returns to the context's own stream. */
 int sky_ctx_set_stream(sky_ctx *ctx, void *hip_stream);

@@ -58,11 +58,21 @@ int32_t orc_key_dim(const double *v, int P, double maxVal) {
 /* GridPartitioner (FlinkSkyline.java:750-789): mids[i] = maxVal/2.0 (:756);
  * mask |= (1 << i) when values[i] >= mids[i] (:780-785).  Java's int shift
  * uses (i & 31).  No clamp and no modulo: keys lie in [0, 2^D). */
+/* GridDominanceFilter (FlinkSkyline.java:716-733, commented out in the reference):
+ * when enabled, a tuple is kept iff some value is < maxVal/2 ("!allWorse"); a removed
+ * tuple never reaches keyBy (key -1 here).  Process-wide switch for the tests. */
+static int g_grid_filter = 0;
+void orc_set_grid_filter(int on) { g_grid_filter = on; }
+
 int32_t orc_key_grid(const double *v, int D, double maxVal) {
     double mid = maxVal / 2.0;
     uint32_t mask = 0;
-    for (int i = 0; i < D; i++)
+    int allWorse = 1;
+    for (int i = 0; i < D; i++) {
         if (v[i] >= mid) mask |= (1u << (i & 31));
+        if (v[i] < mid) allWorse = 0;                 /* :726-729 */
+    }
+    if (g_grid_filter && allWorse) return -1;
     return (int32_t)mask;
 }
 

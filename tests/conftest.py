@@ -51,6 +51,7 @@ def load_oracle():
         L.orc_skyline_brute.argtypes = [dp, ctypes.c_int64, ctypes.c_int, dp]
         L.orc_synth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                 ctypes.c_int64, ctypes.c_int64, dp]
+        L.orc_set_grid_filter.argtypes = [ctypes.c_int]
         L.orc_java_parse_double.restype = ctypes.c_int
         L.orc_java_parse_double.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
         L.orc_parse_csv.restype = ctypes.c_int64

@@ -185,3 +185,19 @@ def test_multithreaded_bnl_equals_single(oracle):
             b = oracle.query_bnl_mt("angle", vals, ids, 8, T)
             assert sorted(a[0].tolist()) == sorted(b[0].tolist())
             assert (a[2] == b[2]).all() and (a[3] == b[3]).all()
+
+
+def test_grid_filter_oracle_is_exact_when_best_quadrant_nonempty(oracle):
+    """The filter only removes tuples dominated by any all-better tuple."""
+    for dist in (0, 1, 2):
+        vals = oracle.synth(dist, 3, 5000, seed=9)
+        ids = np.arange(5000, dtype=np.int64)
+        if not (vals < 500).all(axis=1).any():
+            continue
+        a = oracle.query_bnl("grid", vals, ids, 8)[0]
+        oracle.L.orc_set_grid_filter(1)
+        try:
+            b = oracle.query_bnl("grid", vals, ids, 8)[0]
+        finally:
+            oracle.L.orc_set_grid_filter(0)
+        assert sorted(a.tolist()) == sorted(b.tolist())

@@ -236,3 +236,34 @@ def test_u16_path_tiny_segments_and_ties(gpu_engine_factory, oracle):
     vals = rng.integers(0, 6, size=(30000, 5)).astype(np.float64)
     for algo, P in (("mr-angle", 256), ("mr-dim", 3), ("mr-grid", 32)):
         check_vs_oracle(gpu_engine_factory, oracle, vals, P, algo)
+
+
+@pytest.mark.parametrize("D,P_,dist", [(2, 8, 0), (3, 8, 2), (3, 4, 1), (4, 16, 0)])
+def test_grid_dominance_filter(gpu_engine_factory, oracle, D, P_, dist):
+    """MR-Grid dominance filter (FlinkSkyline.java:716-733, disabled in the reference):
+    tuples with every value >= maxVal/2 are removed before keyBy (key -1); the query
+    equals the oracle's job with the same filter.  Also: with a tuple in the all-better
+    quadrant present, the filtered skyline equals the unfiltered one."""
+    import skyline
+    vals = oracle.synth(dist, D, 30000, seed=21 + D)
+    ids = np.arange(len(vals), dtype=np.int64)
+    eng = skyline.SkylineEngine(D, P_, "mr-grid", 1000.0, 0, grid_filter=True)
+    try:
+        oracle.L.orc_set_grid_filter(1)
+        keys = eng.partition_keys(vals)
+        np.testing.assert_array_equal(keys, oracle.keys("grid", vals, P_))
+        assert (keys == -1).sum() == int((vals >= 500.0).all(axis=1).sum())
+        got, org = eng.query(vals, ids)
+        exp, _, els, esv = oracle.query_bnl("grid", vals, ids, P_)
+        assert sorted(got.tolist()) == sorted(exp.tolist())
+        ls, sv = eng.stats()
+        assert (ls == els).all() and (sv == esv).all()
+    finally:
+        oracle.L.orc_set_grid_filter(0)
+    if ((vals < 500.0).all(axis=1)).any():
+        plain = skyline.SkylineEngine(D, P_, "mr-grid", 1000.0, 0)
+        g2, _ = plain.query(vals, ids)
+        if 2 ** D <= P_:   # every key is queried: the filter cannot change the skyline
+            assert sorted(g2.tolist()) == sorted(got.tolist())
+        plain.close()
+    eng.close()
