@@ -1028,10 +1028,6 @@ int sky_profile_sort_dev(sky_ctx *c, uint64_t *d_keys, uint32_t *d_vals, int64_t
     unsigned long long orand[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(orand, d_orand, 16, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
-    const uint64_t varying = orand[0] ^ orand[1];
-    int passes = 0;
-    for (int b = 0; b < 8; b++) passes += ((varying >> (8 * b)) & 0xff) ? 1 : 0;
-    const int nbits = __builtin_popcountll(varying);
     uint32_t *err = reinterpret_cast<uint32_t *>(d_orand + 4);
     HIP_TRY(hipMemsetAsync(err, 0, 4, c->st));
     hipEvent_t a = c->take_event(), b = c->take_event();
@@ -1054,8 +1050,6 @@ int sky_profile_sort_dev(sky_ctx *c, uint64_t *d_keys, uint32_t *d_vals, int64_t
         set_error("radix sort look-back spin bound reached");
         return SKY_E_HIP;
     }
-    (void)passes;
-    (void)nbits;
     if (passes_out) *passes_out = radix_last_passes();
     if (ms_out) *ms_out = ms;
     return SKY_OK;
