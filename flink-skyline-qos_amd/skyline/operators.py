@@ -194,7 +194,18 @@ class SkylineLocalProcessor:
 
     BUFFER_SIZE = 5000   # :232
 
-    def __init__(self, engine):
+    def __init__(self, engine, barrier="per-key"):
+        """barrier="per-key": the reference's release rule, per key maxId >= R (:306,351),
+        kept with its off-by-one and its wait for a later tuple.  barrier="global" (SURVEY
+        §8f row 3): a query "q,R" covers exactly the ids < R -- it is released once every id
+        < R has been ingested (ids arrive dense and in order, unified_producer.py:174-185),
+        and tuples with id >= R are held back until then, so the answer does not depend on
+        timing and no key waits for a tuple it never gets."""
+        if barrier not in ("per-key", "global"):
+            raise ValueError("barrier must be 'per-key' or 'global'")
+        self.barrier = barrier
+        self.watermark = 0               # global: every id < watermark has been ingested
+        self.held = []                   # global: (point, key) with id >= a pending R
         self.engine = engine
         self.localSkylineState = {}      # key -> _LocalPart
         self.inputBuffer = {}            # key -> list of (id, values)
@@ -209,7 +220,61 @@ class SkylineLocalProcessor:
             self.inputBuffer[key] = []
         return self.localSkylineState[key]
 
+    def _min_pending(self):
+        rs = [self._required(q) for qs in self.pendingQueriesState.values() for q in qs]
+        return min(rs) if rs else None
+
+    @staticmethod
+    def _required(q):
+        parts = q[1].split(",")
+        return int(parts[1]) if len(parts) > 1 else 0
+
+    def _release_global(self, out):
+        """Answer every pending query whose ids < R are all in, then replay held tuples."""
+        while True:
+            released = False
+            for key, pending in list(self.pendingQueriesState.items()):
+                keep = []
+                for q in pending:
+                    if self._required(q) <= self.watermark:
+                        self.processQuery(q, key, out)
+                        released = True
+                    else:
+                        keep.append(q)
+                self.pendingQueriesState[key] = keep
+            if not released or not self.held:
+                return
+            held, self.held = self.held, []
+            for point, key in held:
+                self._ingest_global(point, key, out)
+
+    def _ingest_global(self, point, key, out):
+        if point.bad_id:
+            raise ValueError('NumberFormatException: For input string: "%s"' % point.id)
+        current_id = int(point.id)
+        rmin = self._min_pending()
+        if rmin is not None and current_id >= rmin:   # belongs after the pending query
+            self.held.append((point, key))
+            return
+        self._state(key)
+        if key not in self.startTimeState:
+            self.startTimeState[key] = now_ms()
+        if current_id > self.maxSeenIdState.get(key, -1):
+            self.maxSeenIdState[key] = current_id
+        buf = self.inputBuffer[key]
+        buf.append((current_id, point.values))
+        if len(buf) >= self.BUFFER_SIZE:
+            self.processBuffer(key)
+        self.watermark = max(self.watermark, current_id + 1)
+
     def processElement1(self, point, key, out):
+        if self.barrier == "global":
+            start = time.perf_counter_ns()
+            self._ingest_global(point, key, out)
+            self.accumulatedCpuNanosState[key] = self.accumulatedCpuNanosState.get(key, 0) + \
+                (time.perf_counter_ns() - start)
+            self._release_global(out)
+            return
         start = time.perf_counter_ns()
         self._state(key)
         if key not in self.startTimeState:
@@ -246,6 +311,12 @@ class SkylineLocalProcessor:
         key = trigger[0]
         parts = trigger[1].split(",")
         required = int(parts[1]) if len(parts) > 1 else 0
+        if self.barrier == "global":
+            if self.watermark >= required:
+                self.processQuery(trigger, key, out)
+            else:
+                self.pendingQueriesState.setdefault(key, []).append(trigger)
+            return
         current = self.maxSeenIdState.get(key, -1)
         if current >= required or current == -1:
             self.processQuery(trigger, key, out)
@@ -338,7 +409,8 @@ class GlobalSkylineAggregator:
             self.last_result = (gids, gorg)
 
 
-def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=1000.0, device=0):
+def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=1000.0, device=0,
+            barrier="per-key"):
     """Single-process rendition of the topology of FlinkSkyline.main (:61-186):
     parse -> keyBy(partitioner) -> SkylineLocalProcessor <- broadcast triggers
     -> keyBy(payload) -> GlobalSkylineAggregator.  `triggers` is a list of
@@ -348,7 +420,7 @@ def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=
     P = 2 * parallelism
     part = make_partitioner(algo, P, domain, dims, device)
     eng = part.engine
-    local = SkylineLocalProcessor(eng)
+    local = SkylineLocalProcessor(eng, barrier)
     glob = GlobalSkylineAggregator(eng, P)
     emitted, results = [], []
     tuples = ServiceTuple.fromStrings(csv_lines, eng)                 # .map(fromString) (:103), on the device

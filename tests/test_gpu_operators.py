@@ -152,3 +152,23 @@ def test_service_tuple_from_string_on_device():
     t = ServiceTuple.fromString("x,1.5")          # fromString accepts it; Long.parseLong fails later
     assert t is not None and t.bad_id
     assert ServiceTuple.fromString("5,1e3f, 2 ,") .values == [1000.0, 2.0]
+
+
+def test_run_job_global_barrier(oracle):
+    """Deterministic global-watermark barrier: a trigger 'q,R' that
+    arrives early is answered over exactly the ids < R -- later tuples are held back --
+    however the keys interleave; the reference's per-key maxId >= R rule needs id R itself
+    in every key and answers over whatever had arrived by then."""
+    from skyline.operators import run_job
+    vals = oracle.synth(2, 3, 12000, seed=17)
+    ids = np.arange(len(vals), dtype=np.int64)
+    lines = [f"{i}," + ",".join(str(int(x)) for x in row) for i, row in enumerate(vals)]
+    trig = [(0, "1,4000"), (10, "2,8000"), (9000, "3,9000"), (12000, "4,12000")]
+    out, last = run_job(lines, trig, algo="mr-angle", parallelism=2, dims=3, barrier="global")
+    res = {json.loads(o)["query_id"]: json.loads(o) for o in out}
+    assert set(res) == {"1", "2", "3", "4"}
+    for q, R in (("1", 4000), ("2", 8000), ("3", 9000), ("4", 12000)):
+        exp, _, els, esv = oracle.query_bnl("angle", vals[:R], ids[:R], 4)
+        assert res[q]["skyline_size"] == len(exp), q
+    gids, _ = last
+    assert sorted(gids.tolist()) == sorted(oracle.query_bnl("angle", vals, ids, 4)[0].tolist())
