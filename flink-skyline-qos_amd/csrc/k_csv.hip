@@ -501,44 +501,45 @@ constexpr int kFieldsMax = 2048;
 constexpr int kFieldText = 10 * 1024;   // ~19 KB of LDS per workgroup in all: 8 workgroups (32 waves) per CU
 
 
-// SWAR fast path (simdjson's eight-digit parse): bytes [s, s+len) of the staged words, 1 <= len <= 16,
-// all ASCII digits -> value.  Covers the producer's payload (plain non-negative integers).
-__device__ __forceinline__ bool swar8(uint64_t x, int L, uint64_t &v) {   // L in 1..8, first char in the low byte
-    uint64_t y = L == 8 ? x : (x << (8 * (8 - L))) | (0x3030303030303030ull >> (8 * L));
-    if ((y & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull ||
-        ((y + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) != 0x3030303030303030ull)
-        return false;
+// SWAR fast path (simdjson's eight-digit parse), branch-free: bytes [s, s+len) of the staged
+// words, 1 <= len <= 16, all ASCII digits -> value.  Covers the producer's payload (plain
+// non-negative integers).  Two 8-byte windows are always formed, padded with leading '0's,
+// validated and converted with selects only, so a wave whose lanes hold ids and values of
+// different lengths runs one straight-line sequence.
+__device__ __forceinline__ uint64_t swar_pad(uint64_t x, int L) {   // L in 0..8, first char in the low byte
+    const uint64_t z = 0x3030303030303030ull;
+    const int l = L < 1 ? 1 : (L > 7 ? 7 : L);                      // keep both shifts in 8..56
+    const uint64_t y = (x << (8 * (8 - l))) | (z >> (8 * l));
+    return L == 0 ? z : (L == 8 ? x : y);
+}
+__device__ __forceinline__ bool swar_is_digits(uint64_t y) {
+    return (y & 0xF0F0F0F0F0F0F0F0ull) == 0x3030303030303030ull &&
+           ((y + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) == 0x3030303030303030ull;
+}
+__device__ __forceinline__ uint32_t swar_value(uint64_t y) {
     y -= 0x3030303030303030ull;
     y = (y * 10u) + (y >> 8);
     y = (((y & 0x000000FF000000FFull) * 0x000F424000000064ull) +
          (((y >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
-    v = (uint32_t)y;
-    return true;
+    return (uint32_t)y;
 }
 __device__ __forceinline__ bool swar_digits(const uint32_t *__restrict__ buf, int s, int len, uint64_t &v) {
-    if (len < 1 || len > 16) return false;
     const int k = s >> 2, sh = (s & 3) * 8;
     const uint64_t A = (uint64_t)buf[k] | ((uint64_t)buf[k + 1] << 32);
-    if (len <= 4) {                                        // 32-bit SWAR: the common short value
-        const uint32_t x = (uint32_t)(A >> sh);
-        uint32_t y = len == 4 ? x : (x << (8 * (4 - len))) | (0x30303030u >> (8 * len));
-        if ((y & 0xF0F0F0F0u) != 0x30303030u || ((y + 0x06060606u) & 0xF0F0F0F0u) != 0x30303030u) return false;
-        y -= 0x30303030u;
-        y = y * 10u + (y >> 8);
-        v = (y & 0xFFu) * 100u + ((y >> 16) & 0xFFu);
-        return true;
-    }
     const uint64_t B = (uint64_t)buf[k + 2] | ((uint64_t)buf[k + 3] << 32);
-    const uint64_t x0 = sh ? (A >> sh) | (B << (64 - sh)) : A;
-    if (len <= 8) return swar8(x0, len, v);
     const uint64_t C = buf[k + 4];
-    const uint64_t x1 = sh ? (B >> sh) | (C << (64 - sh)) : B;
-    uint64_t hi, lo;
-    if (!swar8(x0, 8, hi) || !swar8(x1, len - 8, lo)) return false;
-    uint64_t p = 1;
-    for (int i = 0; i < len - 8; i++) p *= 10u;
-    v = hi * p + lo;
-    return true;
+    const int shr = sh ? 64 - sh : 32;                               // unused when sh == 0
+    const uint64_t x0 = sh ? (A >> sh) | (B << shr) : A;
+    const uint64_t x1 = sh ? (B >> sh) | (C << shr) : B;
+    const int L0 = len < 8 ? len : 8, L1 = len > 8 ? len - 8 : 0;   // L1 <= 8 for len <= 16
+    const uint64_t y0 = swar_pad(x0, L0), y1 = swar_pad(x1, L1 > 8 ? 8 : L1);
+    const bool ok = len >= 1 && len <= 16 && swar_is_digits(y0) && swar_is_digits(y1);
+    uint32_t p = (L1 & 1) ? 10u : 1u;
+    p *= (L1 & 2) ? 100u : 1u;
+    p *= (L1 & 4) ? 10000u : 1u;
+    p = (L1 & 8) ? 100000000u : p;
+    v = (uint64_t)swar_value(y0) * p + swar_value(y1);
+    return ok;
 }
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
@@ -681,16 +682,21 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         const int col = f - (int)s_rfirst[j];
         uint64_t u = 0;
         const bool fast = swar_digits(s_buf, s, e - s, u);
-        if (col == 0) {
-            int64_t v = (int64_t)u;
-            const bool ok = fast || java_parse_long(src, s, e, v);
-            ids[r0 + j] = v;
-            s_idok[j] = ok;
-        } else if (s == e) {
+        const bool is_id = col == 0, empty = s == e;
+        int64_t idv = (int64_t)u;                          // < 10^16
+        double v = (double)u;                              // exact when len <= 15
+        bool idok = fast;
+        int pr = 1;
+        if (!(fast && (is_id || e - s <= 15)) && !empty) {   // rare: the full Java grammar
+            if (is_id) idok = java_parse_long(src, s, e, idv);
+            else pr = java_parse_double<false>(src, s, e, v);
+        }
+        if (is_id) {
+            ids[r0 + j] = idv;
+            s_idok[j] = idok;
+        } else if (empty) {
             atomicMin(&s_fempty[j], col);
         } else {
-            double v = (double)u;                          // exact: < 10^16 ... only used when len <= 15
-            const int pr = fast && e - s <= 15 ? 1 : java_parse_double<false>(src, s, e, v);
             if (pr == 0) {
                 s_bad[j] = 1;
             } else if (col <= D) {
