@@ -119,6 +119,11 @@ static bool sfs16_disabled() {
     const char *e = getenv("SKY_SFS16");
     return e && atoi(e) == 0;
 }
+// SKY_GATHER=0 reads counters back by one hipMemcpyAsync per range (A/B knob)
+static bool gather_disabled() {
+    const char *e = getenv("SKY_GATHER");
+    return e && atoi(e) == 0;
+}
 static int stage_check(hipStream_t st, const char *where) {
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && debug_level()) {
@@ -440,10 +445,28 @@ static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const 
     size_t tot = 0;
     for (auto &s : srcs) tot += (s.second + 15) & ~size_t(15);
     SKY_TRY(p.pinned(tot));
+    // small word-aligned ranges: one gather launch writing into the host-mapped buffer
+    FillSet g;
+    bool batched = srcs.size() <= (size_t)kFillMax && tot <= (64u << 10) && !gather_disabled();
     size_t off = 0;
     for (auto &s : srcs) {
-        if (s.second) HIP_TRY(hipMemcpyAsync((char *)p.pin + off, s.first, s.second, hipMemcpyDeviceToHost, st));
+        batched &= ((uintptr_t)s.first & 3u) == 0 && (s.second & 3u) == 0;
+        if (batched && s.second) {
+            g.p[g.n] = (uint8_t *)s.first;
+            g.bytes[g.n] = (uint32_t)s.second;
+            g.val[g.n] = (uint32_t)off;
+            g.n++;
+        }
         off += (s.second + 15) & ~size_t(15);
+    }
+    if (batched) {
+        if (g.n) HIP_TRY(launch_gather_words(g, p.pin, st));
+    } else {
+        off = 0;
+        for (auto &s : srcs) {
+            if (s.second) HIP_TRY(hipMemcpyAsync((char *)p.pin + off, s.first, s.second, hipMemcpyDeviceToHost, st));
+            off += (s.second + 15) & ~size_t(15);
+        }
     }
     HIP_TRY(hipStreamSynchronize(st));
     p.up_used = 0;
@@ -475,9 +498,13 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.surv.ensure(stat_bytes));
     SKY_TRY(p.totals.ensure(64));
     SKY_TRY(p.flags.ensure(64));
-    HIP_TRY(hipMemsetAsync(p.lsz.p, 0, stat_bytes, st));
-    HIP_TRY(hipMemsetAsync(p.surv.p, 0, stat_bytes, st));
-    if (n == 0) return SKY_OK;
+    FillSet fill;
+    fill.add(p.lsz.p, stat_bytes);
+    fill.add(p.surv.p, stat_bytes);
+    if (n == 0) {
+        HIP_TRY(fill.launch(st));
+        return SKY_OK;
+    }
     KeyParams kp = c.kp();
     kp.K = p.Kp;
     if (tm) tm->mark(0, st);
@@ -507,11 +534,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.pr_entries.ensure((size_t)KM * 4));
     SKY_TRY(p.pruner_slot.ensure((size_t)KM * 4));
     SKY_TRY(p.orand.ensure(16));
-    HIP_TRY(hipMemsetAsync(p.dup_cnt.p, 0, (size_t)KM * 4, st));
-    HIP_TRY(hipMemsetAsync(p.flags.p, 0, 64, st));
-    HIP_TRY(hipMemsetAsync(p.totals.p, 0, 64, st));
-    HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
-    HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
+    fill.add(p.dup_cnt.p, (size_t)KM * 4);      // with lsz / surv: one launch for the query's counters
+    fill.add(p.flags.p, 64);
+    fill.add(p.totals.p, 64);
+    fill.add(p.orand.p, 8, 0);
+    fill.add(p.orand.as<char>() + 8, 8, 0xff);
+    HIP_TRY(fill.launch(st));
     FilterArgs fa{};
     fa.vals = in.vals;
     fa.n = n;
@@ -646,8 +674,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_build_reps(D, p.f64, ra, st);
         SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
         SKY_TRY(p.seg_end.ensure((size_t)p.Kp * 4));
-        HIP_TRY(hipMemsetAsync(p.seg_begin.p, 0, (size_t)p.Kp * 4, st));
-        HIP_TRY(hipMemsetAsync(p.seg_end.p, 0, (size_t)p.Kp * 4, st));
+        fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
+        fill.add(p.seg_end.p, (size_t)p.Kp * 4);
+        HIP_TRY(fill.launch(st));
         launch_seg_bounds(p.rep_key.as<uint64_t>(), mt, p.totals.as<uint32_t>() + 1, p.seg_begin.as<uint32_t>(),
                           p.seg_end.as<uint32_t>(), st);
         STAGE(st, "dedup");
@@ -665,7 +694,17 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         if (tm) tm->mark(5, st);
 
         // ---- local skylines
-        HIP_TRY(hipMemsetAsync(p.alive_l.p, 0, mr, st));
+        // the flags and counters of the SFS / global phases, zeroed in one launch
+        const bool gmerge = in.global && !in.single;
+        SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+        fill.add(p.alive_l.p, mr);
+        fill.add(p.segalive.p, (size_t)p.Kp * 4);
+        if (gmerge) {
+            fill.add(p.alive_g.p, mr);
+            fill.add(p.orand.p, 8, 0);
+            fill.add(p.orand.as<char>() + 8, 8, 0xff);
+        }
+        HIP_TRY(fill.launch(st));
         const int W16 = dom16_words(D);
         if (p.u16) {
             SKY_TRY(p.r16.ensure((size_t)std::max<uint32_t>(mr, 1) * W16 * 4));
@@ -675,14 +714,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             SKY_TRY(sfs_run(c, p, p.rep_rows.p, p.rep_key.as<uint64_t>(), mr, sb, se, false,
                             p.alive_l.as<uint8_t>()));
         }
-        SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
-        HIP_TRY(hipMemsetAsync(p.segalive.p, 0, (size_t)p.Kp * 4, st));
         launch_seg_alive(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), mr, p.segalive.as<uint32_t>(), st);
         p.h_seg_n.assign(se.begin(), se.end());
         if (tm) tm->mark(6, st);
 
         // ---- global merge over the union of the local skylines
-        if (in.global && !in.single) {
+        if (gmerge) {
             SKY_TRY(p.alive_u32.ensure((size_t)mr * 4));
             SKY_TRY(p.alive_scan.ensure((size_t)mr * 4));
             SKY_TRY(p.gkey.ensure((size_t)mr * 8));
@@ -690,14 +727,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             launch_flag_u8_to_u32(p.alive_l.as<uint8_t>(), mr, p.alive_u32.as<uint32_t>(), st);
             scan_excl_u32(p.alive_u32.as<uint32_t>(), p.alive_scan.as<uint32_t>(), mr, p.totals.as<uint32_t>() + 2,
                           p.scratch.as<uint32_t>(), st);
-            HIP_TRY(hipMemsetAsync(p.orand.p, 0, 8, st));
-                HIP_TRY(hipMemsetAsync(p.orand.as<char>() + 8, 0xff, 8, st));
             launch_global_keys(p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), mr,
                                p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(), p.orand.as<unsigned long long>(), st);
             uint32_t mg = 0;
             SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 2, 4}, {p.orand.p, 16}}, {&mg, orand}));
             p.mg = mg;
-            HIP_TRY(hipMemsetAsync(p.alive_g.p, 0, mr, st));
             if (mg) {
                 SKY_TRY(p.gkey_alt.ensure((size_t)mg * 8));
                 SKY_TRY(p.gval_alt.ensure((size_t)mg * 4));

@@ -356,8 +356,10 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     uint32_t *tickets = status + (size_t)8 * 256 * tiles;        // [8]
     uint64_t *dense = reinterpret_cast<uint64_t *>(
         (reinterpret_cast<uintptr_t>(tickets + 16) + 15) & ~uintptr_t(15));   // [2][m]
-    (void)hipMemsetAsync(scratch, 0, ((size_t)8 * 256 + (size_t)npass * 256 * tiles) * 4, st);
-    (void)hipMemsetAsync(tickets, 0, 8 * 4, st);
+    FillSet fill;                                                // histograms, look-back status, tickets
+    fill.add(scratch, ((size_t)8 * 256 + (size_t)npass * 256 * tiles) * 4);
+    fill.add(tickets, 8 * 4);
+    (void)fill.launch(st);
     uint64_t *k0 = keys, *k1 = keys_alt;
     if (compress) {
         k0 = dense;

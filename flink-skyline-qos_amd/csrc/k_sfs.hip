@@ -305,6 +305,65 @@ __global__ __launch_bounds__(kThreads) void k_iota(uint32_t *__restrict__ a, uin
     if (j < n) a[j] = j;
 }
 
+// Batched fill: the small per-query zero/0xff ranges of one phase in ONE launch
+// (each hipMemsetAsync is its own dispatch plus ~5-10 us of CP gap).  blockIdx.y
+// picks the range; the range fields are read by compile-time index only (see
+// DESIGN §8 on dynamically indexed kernel-argument arrays).
+__global__ __launch_bounds__(kThreads) void k_fill_multi(FillSet f) {
+    uint8_t *p = nullptr;
+    uint32_t bytes = 0, val = 0;
+#pragma unroll
+    for (int j = 0; j < kFillMax; j++)
+        if ((int)blockIdx.y == j) { p = f.p[j]; bytes = f.bytes[j]; val = f.val[j]; }
+    if (!p) return;
+    const uint32_t words = bytes >> 2;
+    const uint32_t w4 = val * 0x01010101u;
+    uint32_t *p4 = reinterpret_cast<uint32_t *>(p);
+    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < words; q += gridDim.x * kThreads) p4[q] = w4;
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 3u)) p[words * 4 + threadIdx.x] = (uint8_t)val;
+}
+
+void FillSet::add(void *ptr, size_t nbytes, int value) {
+    if (!ptr || !nbytes) return;
+    if (n == kFillMax) { fprintf(stderr, "[sky] FillSet overflow\n"); abort(); }
+    if (((uintptr_t)ptr & 3u) || nbytes > 0xffffffffull) {
+        fprintf(stderr, "[sky] FillSet: unaligned or oversized range\n");
+        abort();
+    }
+    p[n] = (uint8_t *)ptr;
+    bytes[n] = (uint32_t)nbytes;
+    val[n] = (uint32_t)(value & 0xff);
+    n++;
+}
+
+hipError_t FillSet::launch(hipStream_t st) {
+    if (!n) return hipSuccess;
+    uint32_t mx = 0;
+    for (int j = 0; j < n; j++) mx = std::max(mx, bytes[j]);
+    const uint32_t gx = std::max(1u, std::min(256u, (mx / 4 + kThreads * 4 - 1) / (kThreads * 4)));
+    k_fill_multi<<<dim3(gx, (unsigned)n), kThreads, 0, st>>>(*this);
+    n = 0;
+    return hipGetLastError();
+}
+
+// Batched read-back: the small counters one host synchronisation needs, copied by
+// ONE launch straight into the pinned (host-mapped) staging buffer instead of one
+// copy-engine dispatch per range.  Words only (4-byte aligned ranges).
+__global__ __launch_bounds__(kThreads) void k_gather_words(FillSet g, uint32_t *__restrict__ dst) {
+    const uint32_t *src = nullptr;
+    uint32_t words = 0, off = 0;
+#pragma unroll
+    for (int j = 0; j < kFillMax; j++)
+        if ((int)blockIdx.x == j) { src = reinterpret_cast<const uint32_t *>(g.p[j]); words = g.bytes[j] >> 2; off = g.val[j] >> 2; }
+    if (!src) return;
+    for (uint32_t q = threadIdx.x; q < words; q += kThreads) dst[off + q] = src[q];
+}
+
+hipError_t launch_gather_words(const FillSet &g, void *pinned_dst, hipStream_t st) {
+    k_gather_words<<<g.n, kThreads, 0, st>>>(g, reinterpret_cast<uint32_t *>(pinned_dst));
+    return hipGetLastError();
+}
+
 // global merge ordering: (score | rep index) for the alive local representatives
 __global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__restrict__ rep_key,
                                                           const uint8_t *__restrict__ alive_l,

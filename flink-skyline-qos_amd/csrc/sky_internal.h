@@ -167,6 +167,18 @@ void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uin
                         const SfsTile *tiles, uint32_t ntiles, uint32_t *act_new, uint32_t *segcnt,
                         hipStream_t st);
 void launch_iota(uint32_t *a, uint32_t n, hipStream_t st);
+// up to kFillMax byte ranges (4-byte aligned starts) filled by one k_fill_multi launch
+constexpr int kFillMax = 8;
+struct FillSet {
+    uint8_t *p[kFillMax] = {};
+    uint32_t bytes[kFillMax] = {};
+    uint32_t val[kFillMax] = {};
+    int n = 0;
+    void add(void *ptr, size_t nbytes, int value = 0);
+    hipError_t launch(hipStream_t st);
+};
+// ranges g.p[j] (g.bytes[j] bytes, 4-aligned) copied to pinned_dst + g.val[j] in one launch
+hipError_t launch_gather_words(const FillSet &g, void *pinned_dst, hipStream_t st);
 void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
                          uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
