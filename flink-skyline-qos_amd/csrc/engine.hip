@@ -152,6 +152,22 @@ static size_t row_bytes(bool f64, int D) {
 }
 
 // ---- segmented blocked SFS -------------------------------------------------------
+// Several small host arrays (work lists, segment tables) staged into ONE device
+// buffer by one upload: one copy dispatch instead of one per array.
+struct UpBlob {
+    std::vector<char> h;
+    size_t put(const void *src, size_t bytes) {
+        const size_t off = (h.size() + 255) & ~size_t(255);
+        h.resize(off + bytes);
+        if (bytes) memcpy(h.data() + off, src, bytes);
+        return off;
+    }
+    int send(Pipe &p, DevBuf &dst, hipStream_t st) {
+        SKY_TRY(dst.ensure(std::max<size_t>(h.size(), 256)));
+        return p.upload(dst.p, h.data(), h.size(), st);
+    }
+};
+
 static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint32_t nrep,
                    std::vector<uint32_t> begin, std::vector<uint32_t> cnt, bool full, uint8_t *alive) {
     hipStream_t st = c.st;
@@ -191,12 +207,15 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         }
         if (!small.empty()) {
             SKY_TRY(p.conf_small.ensure((size_t)nrep * rb));
-            SKY_TRY(p.seg_small.ensure(small.size() * 4));
-            SKY_TRY(p.upload(p.segs.p, hsegs.data(), nseg * sizeof(SfsSeg), st));
-            SKY_TRY(p.upload(p.seg_small.p, small.data(), small.size() * 4, st));
+            UpBlob ub;
+            const size_t o_segs = ub.put(hsegs.data(), nseg * sizeof(SfsSeg));
+            const size_t o_small = ub.put(small.data(), small.size() * 4);
+            SKY_TRY(ub.send(p, p.seg_small, st));
             c.ktimer_begin("sfs_small", st);
-            launch_sfs_small(D, p.f64, full, p.ties, std::min(512, B / 2), rows, key, p.segs.as<SfsSeg>(),
-                             p.seg_small.as<uint32_t>(), (uint32_t)small.size(), alive, p.conf_small.p, st);
+            launch_sfs_small(D, p.f64, full, p.ties, std::min(512, B / 2), rows, key,
+                             (const SfsSeg *)(p.seg_small.as<char>() + o_segs),
+                             (const uint32_t *)(p.seg_small.as<char>() + o_small), (uint32_t)small.size(), alive,
+                             p.conf_small.p, st);
             c.ktimer_end("sfs_small", st, 0);
             STAGE(st, "sfs_small");
             for (uint32_t k : small) cnt[k] = 0;
@@ -370,7 +389,11 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
                     p.sfs_pairs_upper += (int64_t)ny * nx;
                 }
             }
-        HIP_TRY(hipMemsetAsync(p.dead16.p, 0, (size_t)npos * 4, st));
+        {
+            FillSet fill;
+            fill.add(p.dead16.p, (size_t)npos * 4);
+            HIP_TRY(fill.launch(st));
+        }
         // each list is ordered by x chunk; the chunk-0 items go in a launch of their own
         // so that later chunks start after the most dominating rows have marked their y
         auto first_chunk_end = [&](const std::vector<DomItem> &v, bool rest_list) {
@@ -384,12 +407,16 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         const size_t nt = tri.size(), nd = tdiag.size(), nr = rest.size();
         const size_t nt0 = first_chunk_end(tri, false), nd0 = first_chunk_end(tdiag, false);
         const size_t nr0 = first_chunk_end(rest, true);
-        SKY_TRY(p.items16.ensure((nt + nd + nr) * sizeof(DomItem)));
-        DomItem *di = p.items16.as<DomItem>();
-        if (nt) SKY_TRY(p.upload(di, tri.data(), nt * sizeof(DomItem), st));
-        if (nd) SKY_TRY(p.upload(di + nt, tdiag.data(), nd * sizeof(DomItem), st));
-        if (nr) SKY_TRY(p.upload(di + nt + nd, rest.data(), nr * sizeof(DomItem), st));
-        SKY_TRY(p.upload(p.xseg16.p, xseg.data(), xseg.size() * sizeof(SfsSeg), st));
+        // the three item lists (contiguous) and the x segments: one upload
+        UpBlob ub;
+        const size_t o_items = ub.put(tri.data(), nt * sizeof(DomItem));
+        ub.h.resize(o_items + (nt + nd + nr) * sizeof(DomItem));
+        if (nd) memcpy(ub.h.data() + o_items + nt * sizeof(DomItem), tdiag.data(), nd * sizeof(DomItem));
+        if (nr) memcpy(ub.h.data() + o_items + (nt + nd) * sizeof(DomItem), rest.data(), nr * sizeof(DomItem));
+        const size_t o_xseg = ub.put(xseg.data(), xseg.size() * sizeof(SfsSeg));
+        SKY_TRY(ub.send(p, p.items16, st));
+        DomItem *di = (DomItem *)(p.items16.as<char>() + o_items);
+        const SfsSeg *xsegd = (const SfsSeg *)(p.items16.as<char>() + o_xseg);
         c.ktimer_begin("dom", st);
         // tri: the chunk-0 tiles (plain, diagonal), then the later chunks
         uint32_t *dd = p.dead16.as<uint32_t>();
@@ -398,7 +425,7 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
         launch_dom16(W, tp, true, cur_rows, nullptr, nullptr, di + nt, (uint32_t)nd0, 0, dd, st);
         launch_dom16(W, tp, false, cur_rows, nullptr, nullptr, di + nt0, (uint32_t)(nt - nt0), 0, dd, st);
         launch_dom16(W, tp, true, cur_rows, nullptr, nullptr, di + nt + nd0, (uint32_t)(nd - nd0), 0, dd, st);
-        launch_xcompact16(W, cur_rows, cur_idx, p.xseg16.as<SfsSeg>(), (uint32_t)work.size(), B,
+        launch_xcompact16(W, cur_rows, cur_idx, xsegd, (uint32_t)work.size(), B,
                           p.dead16.as<uint32_t>(), p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), alive, st);
         DomItem *dr = di + nt + nd;
         launch_dom16(W, ppt, false, cur_rows, p.xbuf16.as<uint32_t>(), p.xcnt16.as<uint32_t>(), dr, (uint32_t)nr0, B,
@@ -743,7 +770,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                                                    p.flags.as<uint32_t>(), st);
                 const uint64_t *gk = galt ? p.gkey_alt.as<uint64_t>() : p.gkey.as<uint64_t>();
                 const uint32_t *gv = galt ? p.gval_alt.as<uint32_t>() : p.gval.as<uint32_t>();
-                HIP_TRY(hipMemsetAsync(p.galive.p, 0, mg, st));
+                FillSet gfill;
+                gfill.add(p.galive.p, mg);
+                HIP_TRY(gfill.launch(st));
                 // computed keys: a vector has one partition, so the union of the
                 // partitions' representatives is duplicate-free and the distinct-row
                 // test applies; given keys (lists of a merge) may repeat a vector
