@@ -316,17 +316,19 @@ __device__ __forceinline__ uint16_t classify(const double (&v)[D], int32_t k, co
     uint16_t code = kCodeCandidate;
     const int np = s_npr[k];
     const double *pr = s_pr + k * pr_stride<D>(M);
+    // two compares per dimension: with no NaN (rejected before this), all(p <= v) and
+    // any(p < v) holds iff all(p <= v) and not all(p == v).  The kernel is VALU-issue
+    // bound (SQ_INSTS_VALU x 4 cycles ~ the launch's cycles), so each compare counts.
     for (int j = 0; j < np; j++) {
-        bool le = true, lt = false, eq = true;
+        bool le = true, eq = true;
 #pragma unroll
         for (int d = 0; d < D; d++) {
             const double p = pr[pr_off<D>(k, j, d)];
             le &= p <= v[d];
-            lt |= p < v[d];
             eq &= p == v[d];
         }
-        if (le && lt) { code = kCodeDropped; break; }
         if (eq) { code = (uint16_t)(1 + j); break; }
+        if (le) { code = kCodeDropped; break; }
     }
     if (code == kCodeCandidate) {
 #pragma unroll
