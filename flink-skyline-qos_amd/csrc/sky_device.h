@@ -156,8 +156,11 @@ __device__ __forceinline__ float atan_poly01(float a) {
 __device__ __forceinline__ float atan2_est(float h, float x) {
     const float ax = fabsf(x);
     const float mn = fminf(h, ax), mx = fmaxf(h, ax);
-    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
-    float r = atan_poly01(a > 1.0f ? 1.0f : a);
+    // mx == 0 means mn == 0: 0 * rcp(1e-30) = 0 without a compare/select (every mx > 0
+    // the callers pass is >= 1e-15, so the max does not change it); rcp rounding can
+    // push mn/mx past 1, clamped by one min (a is never NaN here)
+    const float a = fminf(mn * __builtin_amdgcn_rcpf(fmaxf(mx, 1e-30f)), 1.0f);
+    float r = atan_poly01(a);
     r = h > ax ? 1.57079632679489662f - r : r;
     return signbit(x) ? 3.14159265358979324f - r : r;
 }
@@ -202,19 +205,21 @@ __device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, d
     // square underflows, so the reference's f64 s_i is 0 exactly when v_j == 0 for
     // every j > i, and f32 holds every s_i without overflow
     bool ranged = true;
+    bool iz[D];                                            // v[i] == 0, one compare shared below
 #pragma unroll
     for (int i = 0; i < D; i++) {
         const double a = fabs(v[i]);
-        ranged &= (a == 0.0) | ((a >= 1e-15) & (a <= 1e15));
+        iz[i] = v[i] == 0.0;
+        ranged &= iz[i] | ((a >= 1e-15) & (a <= 1e15));
     }
     if (ranged) {
         bool zero_after[D > 1 ? D - 1 : 1];
         bool z = true, special = true;
 #pragma unroll
         for (int i = D - 2; i >= 0; i--) {
-            z &= v[i + 1] == 0.0;
+            z &= iz[i + 1];
             zero_after[i] = z;
-            special &= z | (v[i] == 0.0);
+            special &= z | iz[i];
         }
         if (special) {
             double normalized = 0.0;
