@@ -537,18 +537,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     if (tm) tm->mark(0, st);
 
     // ---- pruners from a strided sample
-    const uint32_t S = std::min<uint32_t>(n, 65536);
-    SKY_TRY(p.pmin.ensure((size_t)p.Kp * p.M * 8));
-    SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
-    SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
-    launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
-                          p.pruners.as<double>(), p.npr.as<int32_t>(), st);
-    STAGE(st, "pruners");
-    if (tm) tm->mark(1, st);
-
-    // ---- the HBM stream: keys + pruner test + status, candidates appended to slots
-    //      (f64 rows + sort keys); the row type (f32/f64), the OR/AND of the sort keys
-    //      and the slot count are read back in ONE synchronisation
+    // buffers of the HBM stream (below) first: its counters are zeroed by the same
+    // launch that initialises the pruner sample
     const int KM = p.Kp * p.M;
     const size_t rb64 = row_bytes(true, D);
     const size_t cap = (size_t)n + KM;
@@ -566,7 +556,20 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fill.add(p.totals.p, 64);
     fill.add(p.orand.p, 8, 0);
     fill.add(p.orand.as<char>() + 8, 8, 0xff);
+    const uint32_t S = std::min<uint32_t>(n, 65536);
+    SKY_TRY(p.pmin.ensure((size_t)p.Kp * p.M * 8));
+    SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
+    SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
+    fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);   // per-slot sample minima start all-ones
     HIP_TRY(fill.launch(st));
+    launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
+                          p.pruners.as<double>(), p.npr.as<int32_t>(), st);
+    STAGE(st, "pruners");
+    if (tm) tm->mark(1, st);
+
+    // ---- the HBM stream: keys + pruner test + status, candidates appended to slots
+    //      (f64 rows + sort keys); the row type (f32/f64), the OR/AND of the sort keys
+    //      and the slot count are read back in ONE synchronisation
     FilterArgs fa{};
     fa.vals = in.vals;
     fa.n = n;

@@ -1063,8 +1063,7 @@ void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int
 void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
                            double *pruners, int32_t *npr, hipStream_t st) {
-    if (S == 0) return;
-    (void)hipMemsetAsync(gmin, 0xff, (size_t)Kp * M * 8, st);
+    if (S == 0) return;                               // gmin: all-ones on entry (the caller's fill)
     SKY_DISPATCH_D(D, (k_sample_min<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
                                                                                  Kp, M, gmin)));
     SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
