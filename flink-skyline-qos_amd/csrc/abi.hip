@@ -894,25 +894,40 @@ static int stream_append(sky_stream *s, const int64_t *ids, const double *values
     sky_ctx *c = s->ctx;
     SKY_TRY(bind(c));
     const int D = c->D;
+    const int64_t n_all = n;
+    bool drop_resident = false;
     if (s->window > 0 && n >= s->window) {   // only the newest `window` tuples of this batch can stay
         ids += n - s->window;
         values += (n - s->window) * D;
-        s->appended += n - s->window;
         n = s->window;
-        s->off += s->n;
-        s->n = 0;
+        drop_resident = true;
     }
     SKY_TRY(stream_reserve(s, n));
     const int64_t at = s->off + s->n;
     HIP_TRY(hipMemcpyAsync(s->ids[s->cur].as<int64_t>() + at, ids, (size_t)n * 8, kind, c->st));
     HIP_TRY(hipMemcpyAsync(s->rows[s->cur].as<double>() + at * D, values, (size_t)n * D * 8, kind, c->st));
+    // admission: a NaN row never becomes resident (the state stays queryable); the
+    // batch is rejected whole, as sky_part_insert rejects it
+    SKY_TRY(s->nanflag.ensure(64));
+    HIP_TRY(hipMemsetAsync(s->nanflag.p, 0, 4, c->st));
+    launch_nan_any(s->rows[s->cur].as<double>() + at * D, (size_t)n * D, s->nanflag.as<uint32_t>(), c->st);
+    uint32_t nan = 0;
+    HIP_TRY(hipMemcpyAsync(&nan, s->nanflag.p, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));   // also: the caller's host buffer is free
+    if (nan) {
+        set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; batch rejected");
+        return SKY_E_NAN;
+    }
+    if (drop_resident) {
+        s->off = at;
+        s->n = 0;
+    }
     s->n += n;
-    s->appended += n;
+    s->appended += n_all;
     if (s->window > 0 && s->n > s->window) {   // expire the oldest tuples
         s->off += s->n - s->window;
         s->n = s->window;
     }
-    if (kind == hipMemcpyHostToDevice) HIP_TRY(hipStreamSynchronize(c->st));   // caller's host buffer is free
     return SKY_OK;
     GUARD_END
 }
@@ -1032,8 +1047,10 @@ int sky_profile_sort_dev(sky_ctx *c, uint64_t *d_keys, uint32_t *d_vals, int64_t
     HIP_TRY(hipMemsetAsync(err, 0, 4, c->st));
     hipEvent_t a = c->take_event(), b = c->take_event();
     HIP_TRY(hipEventRecord(a, c->st));
+    hipError_t lerr = hipSuccess;
     const bool alt = radix_sort_pairs(d_keys, d_vals, c->prof_k.as<uint64_t>(), c->prof_v.as<uint32_t>(), m, orand[0],
-                                      orand[1], c->prof_scr.as<uint32_t>(), err, c->st);
+                                      orand[1], c->prof_scr.as<uint32_t>(), err, c->st, &lerr);
+    HIP_TRY(lerr);
     HIP_TRY(hipEventRecord(b, c->st));
     if (alt) {
         HIP_TRY(hipMemcpyAsync(d_keys, c->prof_k.p, (size_t)n * 8, hipMemcpyDeviceToDevice, c->st));

@@ -145,5 +145,5 @@ struct sky_stream {
     int64_t off = 0, n = 0;     // resident tuples: [off, off + n) of buffer `cur`
     int64_t cap = 0;            // capacity (tuples) of both buffers
     int64_t appended = 0;
-    sky::DevBuf out_ids, out_org;
+    sky::DevBuf out_ids, out_org, nanflag;
 };

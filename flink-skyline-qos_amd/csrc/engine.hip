@@ -657,9 +657,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                     chk[0], chk[1]);
         }
         launch_iota(p.perm.as<uint32_t>(), mt, st);
+        hipError_t lerr = hipSuccess;
         const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
                                           p.val_alt.as<uint32_t>(), mt, orand[0], orand[1],
-                                          p.scratch.as<uint32_t>(), p.flags.as<uint32_t>(), st);
+                                          p.scratch.as<uint32_t>(), p.flags.as<uint32_t>(), st, &lerr);
+        HIP_TRY(lerr);
         STAGE(st, "sort");
         const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
         const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
@@ -767,10 +769,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 SKY_TRY(p.gval_alt.ensure((size_t)mg * 4));
                 SKY_TRY(p.grows.ensure((size_t)mg * rb));
                 SKY_TRY(p.galive.ensure((size_t)mg));
+                hipError_t glerr = hipSuccess;
                 const bool galt = radix_sort_pairs(p.gkey.as<uint64_t>(), p.gval.as<uint32_t>(),
                                                    p.gkey_alt.as<uint64_t>(), p.gval_alt.as<uint32_t>(), mg,
                                                    orand[0], orand[1], p.scratch.as<uint32_t>(),
-                                                   p.flags.as<uint32_t>(), st);
+                                                   p.flags.as<uint32_t>(), st, &glerr);
+                HIP_TRY(glerr);
                 const uint64_t *gk = galt ? p.gkey_alt.as<uint64_t>() : p.gkey.as<uint64_t>();
                 const uint32_t *gv = galt ? p.gval_alt.as<uint32_t>() : p.gval.as<uint32_t>();
                 FillSet gfill;
@@ -823,6 +827,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // ---- per-tuple fate: stats + output counts
     SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
     SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
+    // the tile scan below needs its scratch even when no tuple was a candidate (mt == 0:
+    // every tuple in an unqueried MR-Grid cell or removed by the grid filter)
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
     oa.n = n;

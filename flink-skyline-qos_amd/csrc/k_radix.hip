@@ -314,8 +314,10 @@ size_t radix_scratch_words(size_t m) {
 // scratch holds the dense ping-pong pair and an index array; the original keys
 // are gathered back at the end).
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
-                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st) {
+                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st,
+                      hipError_t *launch_err) {
     const uint64_t varying_bits = key_or ^ key_and;
+    if (launch_err) *launch_err = hipSuccess;
     g_radix_last_passes = 0;
     if (m <= 1 || varying_bits == 0) return false;
     const bool big = m >= (1u << 22);   // 4096-key tiles for large sorts, 1024 for the query's candidates
@@ -359,7 +361,8 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     FillSet fill;                                                // histograms, look-back status, tickets
     fill.add(scratch, ((size_t)8 * 256 + (size_t)npass * 256 * tiles) * 4);
     fill.add(tickets, 8 * 4);
-    (void)fill.launch(st);
+    const hipError_t fe = fill.launch(st);
+    if (fe != hipSuccess && launch_err) *launch_err = fe;
     uint64_t *k0 = keys, *k1 = keys_alt;
     if (compress) {
         k0 = dense;

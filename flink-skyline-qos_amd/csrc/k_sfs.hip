@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void k_iota(uint32_t *__restrict__ a, uin
 // (each hipMemsetAsync is its own dispatch plus ~5-10 us of CP gap).  blockIdx.y
 // picks the range; the range fields are read by compile-time index only (see
 // DESIGN §8 on dynamically indexed kernel-argument arrays).
-__global__ __launch_bounds__(kThreads) void k_fill_multi(FillSet f) {
+__global__ __launch_bounds__(kThreads) void k_fill_multi(FillRanges f) {
     uint8_t *p = nullptr;
     uint32_t bytes = 0, val = 0;
 #pragma unroll
@@ -325,31 +325,48 @@ __global__ __launch_bounds__(kThreads) void k_fill_multi(FillSet f) {
 
 void FillSet::add(void *ptr, size_t nbytes, int value) {
     if (!ptr || !nbytes) return;
-    if (n == kFillMax) { fprintf(stderr, "[sky] FillSet overflow\n"); abort(); }
-    if (((uintptr_t)ptr & 3u) || nbytes > 0xffffffffull) {
-        fprintf(stderr, "[sky] FillSet: unaligned or oversized range\n");
-        abort();
+    if ((uintptr_t)ptr & 3u) {
+        plain.push_back({{ptr, nbytes}, value});
+        return;
     }
-    p[n] = (uint8_t *)ptr;
-    bytes[n] = (uint32_t)nbytes;
-    val[n] = (uint32_t)(value & 0xff);
-    n++;
+    constexpr size_t kPiece = size_t(1) << 31;   // < 4 GiB per range, 4-aligned pieces
+    for (size_t off = 0; off < nbytes; off += kPiece) {
+        if (n == kFillMax) {
+            full.push_back(static_cast<const FillRanges &>(*this));
+            n = 0;
+        }
+        p[n] = (uint8_t *)ptr + off;
+        bytes[n] = (uint32_t)std::min(kPiece, nbytes - off);
+        val[n] = (uint32_t)(value & 0xff);
+        n++;
+    }
+}
+
+static void launch_fill_ranges(const FillRanges &f, hipStream_t st) {
+    uint32_t mx = 0;
+    for (int j = 0; j < f.n; j++) mx = std::max(mx, f.bytes[j]);
+    const uint32_t gx = std::max(1u, std::min(256u, (mx / 4 + kThreads * 4 - 1) / (kThreads * 4)));
+    k_fill_multi<<<dim3(gx, (unsigned)f.n), kThreads, 0, st>>>(f);
 }
 
 hipError_t FillSet::launch(hipStream_t st) {
-    if (!n) return hipSuccess;
-    uint32_t mx = 0;
-    for (int j = 0; j < n; j++) mx = std::max(mx, bytes[j]);
-    const uint32_t gx = std::max(1u, std::min(256u, (mx / 4 + kThreads * 4 - 1) / (kThreads * 4)));
-    k_fill_multi<<<dim3(gx, (unsigned)n), kThreads, 0, st>>>(*this);
+    hipError_t e = hipSuccess;
+    for (const FillRanges &f : full) launch_fill_ranges(f, st);
+    if (n) launch_fill_ranges(*this, st);
+    for (auto &q : plain)
+        if (hipMemsetAsync(q.first.first, q.second, q.first.second, st) != hipSuccess && e == hipSuccess)
+            e = hipGetLastError();
+    full.clear();
+    plain.clear();
     n = 0;
-    return hipGetLastError();
+    const hipError_t l = hipGetLastError();
+    return e != hipSuccess ? e : l;
 }
 
 // Batched read-back: the small counters one host synchronisation needs, copied by
 // ONE launch straight into the pinned (host-mapped) staging buffer instead of one
 // copy-engine dispatch per range.  Words only (4-byte aligned ranges).
-__global__ __launch_bounds__(kThreads) void k_gather_words(FillSet g, uint32_t *__restrict__ dst) {
+__global__ __launch_bounds__(kThreads) void k_gather_words(FillRanges g, uint32_t *__restrict__ dst) {
     const uint32_t *src = nullptr;
     uint32_t words = 0, off = 0;
 #pragma unroll
@@ -359,7 +376,7 @@ __global__ __launch_bounds__(kThreads) void k_gather_words(FillSet g, uint32_t *
     for (uint32_t q = threadIdx.x; q < words; q += kThreads) dst[off + q] = src[q];
 }
 
-hipError_t launch_gather_words(const FillSet &g, void *pinned_dst, hipStream_t st) {
+hipError_t launch_gather_words(const FillRanges &g, void *pinned_dst, hipStream_t st) {
     k_gather_words<<<g.n, kThreads, 0, st>>>(g, reinterpret_cast<uint32_t *>(pinned_dst));
     return hipGetLastError();
 }
@@ -585,6 +602,21 @@ void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uin
 
 void launch_iota(uint32_t *a, uint32_t n, hipStream_t st) {
     if (n) k_iota<<<nb(n), kThreads, 0, st>>>(a, n);
+}
+
+// *flag |= 1 if any of the `count` doubles is NaN (the stream append's admission check)
+__global__ __launch_bounds__(kThreads) void k_nan_any(const double *__restrict__ v, size_t count,
+                                                      uint32_t *__restrict__ flag) {
+    bool nan = false;
+    for (size_t q = (size_t)blockIdx.x * kThreads + threadIdx.x; q < count; q += (size_t)gridDim.x * kThreads)
+        nan |= v[q] != v[q];
+    if (__ballot(nan) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+void launch_nan_any(const double *v, size_t count, uint32_t *flag, hipStream_t st) {
+    if (!count) return;
+    const size_t blocks = std::min<size_t>(2048, (count + kThreads - 1) / kThreads);
+    k_nan_any<<<(unsigned)blocks, kThreads, 0, st>>>(v, count, flag);
 }
 
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <utility>
+#include <vector>
 #include "sky_common.h"
 #include "sky_device.h"
 
@@ -40,8 +42,11 @@ size_t radix_scratch_words(size_t m);
 int radix_last_passes();   // digit passes of this thread's last radix_sort_pairs
 // err: device word, kFlagRadixSpin is OR-ed in if a look-back spin ran out (never
 // expected; the caller checks it at its next synchronisation)
+// launch_err (optional): a failed launch of the scratch fill (the kernels' own launch
+// errors stay sticky for the caller's next hipGetLastError)
 bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
-                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st);
+                      uint64_t key_or, uint64_t key_and, uint32_t *scratch, uint32_t *err, hipStream_t st,
+                      hipError_t *launch_err = nullptr);
 void radix_debug_check(const uint64_t *orig, const uint64_t *skey, const uint32_t *perm, uint32_t m, uint32_t *seen,
                        uint32_t *bad, hipStream_t st);
 void radix_key_orand(const uint64_t *keys, uint32_t m, unsigned long long *d_orand, hipStream_t st);
@@ -167,18 +172,26 @@ void launch_act_compact(const uint32_t *act_old, const uint32_t *keep, const uin
                         const SfsTile *tiles, uint32_t ntiles, uint32_t *act_new, uint32_t *segcnt,
                         hipStream_t st);
 void launch_iota(uint32_t *a, uint32_t n, hipStream_t st);
-// up to kFillMax byte ranges (4-byte aligned starts) filled by one k_fill_multi launch
+void launch_nan_any(const double *v, size_t count, uint32_t *flag, hipStream_t st);
+// up to kFillMax byte ranges (4-byte aligned starts, < 4 GiB each): the kernel argument of
+// one k_fill_multi / k_gather_words launch
 constexpr int kFillMax = 8;
-struct FillSet {
+struct FillRanges {
     uint8_t *p[kFillMax] = {};
     uint32_t bytes[kFillMax] = {};
     uint32_t val[kFillMax] = {};
     int n = 0;
+};
+// any number of fills: batched kFillMax per k_fill_multi launch; ranges of 4 GiB or more are
+// split, unaligned ranges go through hipMemsetAsync.  Never aborts.
+struct FillSet : FillRanges {
+    std::vector<FillRanges> full;                 // batches already complete
+    std::vector<std::pair<std::pair<void *, size_t>, int>> plain;   // unaligned: hipMemsetAsync
     void add(void *ptr, size_t nbytes, int value = 0);
     hipError_t launch(hipStream_t st);
 };
 // ranges g.p[j] (g.bytes[j] bytes, 4-aligned) copied to pinned_dst + g.val[j] in one launch
-hipError_t launch_gather_words(const FillSet &g, void *pinned_dst, hipStream_t st);
+hipError_t launch_gather_words(const FillRanges &g, void *pinned_dst, hipStream_t st);
 void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
                          uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,

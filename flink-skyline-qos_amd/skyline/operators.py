@@ -410,22 +410,34 @@ class GlobalSkylineAggregator:
 
 
 def run_job(csv_lines, triggers, algo="mr-angle", parallelism=4, dims=2, domain=1000.0, device=0,
-            barrier="per-key"):
+            barrier="per-key", out=None):
     """Single-process rendition of the topology of FlinkSkyline.main (:61-186):
     parse -> keyBy(partitioner) -> SkylineLocalProcessor <- broadcast triggers
     -> keyBy(payload) -> GlobalSkylineAggregator.  `triggers` is a list of
     (position, payload): the trigger is injected after that many input lines,
     like unified_producer.py:177-185.  Returns the emitted JSON strings and the
-    result ids of the last query."""
+    result ids of the last query.  `out`: an optional list the JSON strings are appended to as
+    they are emitted (still filled when a later record fails the job)."""
     P = 2 * parallelism
     part = make_partitioner(algo, P, domain, dims, device)
     eng = part.engine
     local = SkylineLocalProcessor(eng, barrier)
     glob = GlobalSkylineAggregator(eng, P)
-    emitted, results = [], []
+    emitted = []
+    results = out if out is not None else []
     tuples = ServiceTuple.fromStrings(csv_lines, eng)                 # .map(fromString) (:103), on the device
     valid = [t for t in tuples if t is not None]
-    keys = part.getKeys(np.asarray([t.values for t in valid], np.float64)) if valid else []
+    # keys only for tuples with values; a bad-id tuple gets a placeholder key and raises
+    # its NumberFormatException in stream order, at processElement1 (:276)
+    good = [t for t in valid if not t.bad_id]
+    gkeys = part.getKeys(np.asarray([t.values for t in good], np.float64)) if good else []
+    keys, gi = [], 0
+    for t in valid:
+        if t.bad_id:
+            keys.append(0)
+        else:
+            keys.append(int(gkeys[gi]))
+            gi += 1
     trig = sorted(triggers)
     ti = 0
     pos = 0

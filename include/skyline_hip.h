@@ -28,7 +28,7 @@
  *   sky_parse_csv[_dev]  <- ServiceTuple.fromString (ServiceTuple.java:89-104) mapped over the raw
  *                           Kafka values + .filter(Objects::nonNull) (FlinkSkyline.java:103-104)
  *                           + Long.parseLong(point.id) (FlinkSkyline.java:276)
- *   sky_synth_csv_dev    <- the producers' "id,v1,...,vD" payload (python/unified_producer.py:174)
+ *   sky_format_csv_dev   <- the producers' "id,v1,...,vD" payload (python/unified_producer.py:174)
  */
 #ifndef SKYLINE_HIP_H
 #define SKYLINE_HIP_H

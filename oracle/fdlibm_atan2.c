@@ -10,8 +10,9 @@
  * Third-party dependency: the JDK's fdlibm is NOT under /root/reference and no
  * JDK exists in this container, so the restatement is pinned by (a) the hex
  * words fdlibm publishes next to each constant (checked by
- * tests/test_oracle_fdlibm.py) and (b) agreement with glibc's correctly-rounded
- * atan2 to within 1 ulp.  Compile with -ffp-contract=off: Java never contracts.
+ * tests/test_cpu_oracle.py::test_fdlibm_constants_match_published_hex) and (b)
+ * bit-exact agreement with V8's independent fdlibm port on the committed vectors
+ * (tests/test_cpu_oracle.py::test_fdlibm_atan2_vs_v8_golden).  Compile with -ffp-contract=off: Java never contracts.
  */
 #include <stdint.h>
 #include <string.h>

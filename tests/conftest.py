@@ -48,6 +48,10 @@ def load_oracle():
         L.orc_query_sfs.restype = ctypes.c_int64
         L.orc_query_sfs.argtypes = [ctypes.c_int, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                     ctypes.c_int, dp, dp, dp, dp, dp]
+        L.orc_query_sfs_chunked.restype = ctypes.c_int64
+        L.orc_query_sfs_chunked.argtypes = [ctypes.c_int, dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_double, ctypes.c_int, ctypes.c_int64, ctypes.c_int, dp, dp, dp,
+                                            dp, dp]
         L.orc_skyline_brute.argtypes = [dp, ctypes.c_int64, ctypes.c_int, dp]
         L.orc_synth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                 ctypes.c_int64, ctypes.c_int64, dp]
@@ -116,6 +120,25 @@ class Oracle:
         g = self.L.orc_query_sfs(self.ALGO[algo], P(v), n, D, P_, domain, sem, P(keys), P(inl), P(ing), P(ls), P(sv))
         assert g >= 0
         return np.nonzero(ing[:n])[0], keys[:n], ls, sv
+
+    def query_sfs_chunked(self, algo, vals, P_, domain=1000.0, sem=0, chunk=1 << 20, threads=None):
+        """orc_query_sfs_chunked (oracle/skyline_oracle_big.c): the same outputs as query_sfs, computed
+        as SKY(U SKY(chunk)) per key then globally, over distinct vectors, on `threads` threads.
+        Returns (global ids = row indices, keys, |L_k|, survivors_k, in_local flags)."""
+        v = np.ascontiguousarray(vals, np.float64)
+        n, D = v.shape
+        K = P_ if not (self.ALGO[algo] == 1 and sem == 1) else max(P_, 1 << D)
+        if threads is None:
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        keys = np.zeros(max(n, 1), np.int32)
+        inl = np.zeros(max(n, 1), np.uint8)
+        ing = np.zeros(max(n, 1), np.uint8)
+        ls = np.zeros(K, np.int64)
+        sv = np.zeros(K, np.int64)
+        g = self.L.orc_query_sfs_chunked(self.ALGO[algo], P(v), n, D, P_, domain, sem, int(chunk), int(threads),
+                                         P(keys), P(inl), P(ing), P(ls), P(sv))
+        assert g >= 0
+        return np.nonzero(ing[:n])[0], keys[:n], ls, sv, inl[:n]
 
     def java_parse_double(self, s):
         """Double.parseDouble restatement: float, or None for a NumberFormatException."""

@@ -201,3 +201,43 @@ def test_grid_filter_oracle_is_exact_when_best_quadrant_nonempty(oracle):
         finally:
             oracle.L.orc_set_grid_filter(0)
         assert sorted(a.tolist()) == sorted(b.tolist())
+
+
+# ---- chunked oracle (oracle/skyline_oracle_big.c): the checker of the full-size configs ----
+@pytest.mark.parametrize("path", golden_streams(), ids=lambda p: os.path.basename(p)[7:-4])
+def test_chunked_oracle_matches_golden(path, oracle):
+    """SKY(U SKY(chunk)) per key and globally, over distinct vectors, equals the golden BNL
+    results for every chunk size (including chunks smaller than a partition's share)."""
+    g = load_golden(path)
+    vals = g["values"]
+    for algo in ("dim", "grid", "angle"):
+        for P in (4, 16):
+            for chunk in (97, 1000, 1 << 20):
+                gi, keys, ls, sv, _ = oracle.query_sfs_chunked(algo, vals, P, chunk=chunk, threads=4)
+                np.testing.assert_array_equal(gi, g[f"gsky_{algo}_{P}"])
+                np.testing.assert_array_equal(ls, g[f"lsz_{algo}_{P}"])
+                np.testing.assert_array_equal(sv, g[f"surv_{algo}_{P}"])
+
+
+def test_chunked_oracle_edge_values(oracle):
+    """Duplicates, -0.0 == +0.0, infinities, negatives, complete MR-Grid semantics: the
+    chunked oracle equals the single-threaded SFS restatement and the BNL restatement."""
+    rng = np.random.default_rng(12)
+    vals = rng.integers(-5, 6, size=(20000, 4)).astype(np.float64)
+    vals[rng.random(20000) < 0.1, 0] = -0.0
+    vals[rng.random(20000) < 0.03, 1] = np.inf
+    vals[rng.random(20000) < 0.03, 2] = -np.inf
+    ids = np.arange(len(vals), dtype=np.int64)
+    for algo in ("dim", "grid", "angle"):
+        for sem in (0, 1):
+            if sem and algo != "grid":
+                continue
+            exp, ekeys, els, esv = oracle.query_sfs(algo, vals, 8, sem=sem)
+            for chunk in (333, 5000):
+                gi, keys, ls, sv, _ = oracle.query_sfs_chunked(algo, vals, 8, sem=sem, chunk=chunk, threads=3)
+                np.testing.assert_array_equal(gi, exp)
+                np.testing.assert_array_equal(keys, ekeys)
+                np.testing.assert_array_equal(ls, els)
+                np.testing.assert_array_equal(sv, esv)
+        bnl, _, bls, bsv = oracle.query_bnl(algo, vals, ids, 8)
+        np.testing.assert_array_equal(np.sort(bnl), oracle.query_sfs_chunked(algo, vals, 8, chunk=777)[0])
