@@ -909,12 +909,13 @@ static int stream_append(sky_stream *s, const int64_t *ids, const double *values
     // admission: a NaN row never becomes resident (the state stays queryable); the
     // batch is rejected whole, as sky_part_insert rejects it
     SKY_TRY(s->nanflag.ensure(64));
+    if (!s->nan_host) HIP_TRY(hipHostMalloc(&s->nan_host, 64, hipHostMallocDefault));
     HIP_TRY(hipMemsetAsync(s->nanflag.p, 0, 4, c->st));
     launch_nan_any(s->rows[s->cur].as<double>() + at * D, (size_t)n * D, s->nanflag.as<uint32_t>(), c->st);
-    uint32_t nan = 0;
-    HIP_TRY(hipMemcpyAsync(&nan, s->nanflag.p, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(s->nan_host, s->nanflag.p, 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));   // also: the caller's host buffer is free
-    if (nan) {
+    if (*(volatile uint32_t *)s->nan_host) {
         set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; batch rejected");
         return SKY_E_NAN;
     }
@@ -980,6 +981,7 @@ int sky_stream_destroy(sky_stream *s) {
     if (!s) return SKY_OK;
     hipSetDevice(s->ctx->dev);
     hipStreamSynchronize(s->ctx->st);
+    if (s->nan_host) hipHostFree(s->nan_host);
     delete s;
     return SKY_OK;
 }

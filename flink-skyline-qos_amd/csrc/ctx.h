@@ -146,4 +146,5 @@ struct sky_stream {
     int64_t cap = 0;            // capacity (tuples) of both buffers
     int64_t appended = 0;
     sky::DevBuf out_ids, out_org, nanflag;
+    void *nan_host = nullptr;   // pinned word: the append's NaN admission flag
 };
