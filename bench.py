@@ -1,25 +1,32 @@
 #!/usr/bin/env python3
 """bench.py — skyline tuples/sec (+ p50 query latency) on MI355X.
 
-Workload (BASELINE.json metric, config C4 on one GPU per rank): MR-Angle, 8D,
-anti-correlated stream (the reference producer's formula,
-python/unified_producer.py:89-123, counter RNG), P = 16 partitions, domain
-[0,1000], N tuples per rank (default 100M) generated directly in HBM.
+Headline workload (BASELINE.json metric; config C4 on one GPU per rank): MR-Angle, 8D,
+anti-correlated stream (the reference producer's formula, python/unified_producer.py:89-123,
+counter RNG), P = 16 partitions, domain [0,1000], 100M tuples per rank generated in HBM.
 
-A step = one query over the whole landmark window (every tuple of the rank's
-shard): partition keys -> local skylines of the P partitions -> global merge ->
-stream-ordered skyline ids, with inputs already resident in HBM.  With N GPUs
-(one process per GPU, launched by torch.distributed.run) every rank holds its
-own N-tuple shard (weak scaling) and the ranks exchange their local skylines'
-distinct vectors with one RCCL all-gather (skyline/dist.py).
+A step = one query over the whole landmark window (every tuple of the rank's shard):
+partition keys -> local skylines of the P partitions -> global merge -> stream-ordered
+skyline ids, inputs already resident in HBM.  With N GPUs (one process per GPU, launched
+by torch.distributed.run) every rank owns a shard; the ranks exchange their local
+skylines' distinct vectors with one RCCL all-gather and each rank filters ITS OWN
+vectors against the union (skyline/dist.py).  --scaling weak (default): N x 100M tuples;
+--scaling strong: 100M tuples in total, split over the ranks.
 
-Extra fields: "roofline" for the dominant kernel (k_filter, HBM-bound), timed
-with HIP events on the stream it is launched on; "cpu_baseline" = the C
-restatement of the reference BNL operators (oracle/, 1 thread) timed on a
-bounded prefix of the same stream (rank 0, N=1 only).
+--config C1..C5 runs one BASELINE configuration as the headline line instead:
+  C1 MR-Dim 2D uniform 1M P=8 | C2 MR-Grid 4D correlated 10M P=8 | C3 MR-Angle 4D anti 50M P=8
+  C4 MR-Angle 8D anti 100M P=16 | C5 6D mixed continuous queries, MR-Angle P=8.
+The default run (C4) also carries every other configuration as a sub-line under
+"configs" (each with its own roofline and cpu_baseline), the end-to-end C4 rates with the
+host->device transfer (rows, or CSV text) inside the timed region, and the companion
+rooflines of the dominance, CSV-decode and sort kernels.
+
+"roofline": the dominant kernel (k_filter, HBM-bound), HIP events on the stream it is
+launched on.  "cpu_baseline": the C restatement of the reference operators (oracle/,
+test infrastructure) on a bounded sample of the same stream, rank 0, N=1 only, with the
+extrapolation to the full size from the committed sweep (tools/cpu_baseline_sweep.py).
 """
 import argparse
-import ctypes
 import json
 import os
 import statistics
@@ -36,11 +43,249 @@ import skyline  # noqa: E402
 from skyline import _abi  # noqa: E402
 from skyline.dist import distributed_query  # noqa: E402
 
+METRIC = "skyline tuples/sec + p50 query latency, 8D anti-corr, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
-# VALU compare peak: 256 CU x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz = one 32-bit compare per
-# lane-cycle (MI355X_MICROARCH.md: SIMD-32, wave64 VALU op over 2 cycles; 157.3 TF fp32
-# vector = 78.6 T FMA/s).  tools/probe/valu_probe measured 65 T v_add_f32 lane-ops/s.
-VALU_PEAK_CMPS = 256 * 4 * 32 * 2.4e9
+# VALU compare peaks: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T 32-bit lane-ops/s; k_dom16
+# compares packed u16 pairs (v_pk_sub_u16: 2 compares per lane-op) -> 157.3 T compares/s
+VALU_PEAK_32 = 256 * 4 * 32 * 2.4e9
+VALU_PEAK_PK16 = 2 * VALU_PEAK_32
+
+CONFIGS = {
+    "C1": dict(algo="mr-dim", dims=2, dist="uniform", tuples=1_000_000, partitions=8, cpu_sample=1_000_000,
+               workload="C1: MR-Dim 2D independent (uniform), P=8 (Flink parallelism 4), landmark-window query"),
+    "C2": dict(algo="mr-grid", dims=4, dist="correlated", tuples=10_000_000, partitions=8, cpu_sample=1_000_000,
+               workload="C2: MR-Grid 4D correlated, P=8, landmark-window query"),
+    "C3": dict(algo="mr-angle", dims=4, dist="anti_correlated", tuples=50_000_000, partitions=8, cpu_sample=100_000,
+               workload="C3: MR-Angle 4D anti-correlated, P=8, landmark-window query"),
+    "C4": dict(algo="mr-angle", dims=8, dist="anti_correlated", tuples=100_000_000, partitions=16, cpu_sample=60_000,
+               workload="C4: MR-Angle 8D anti-correlated, P=16, landmark-window query"),
+}
+# the one published reference number for a configured workload: MR-Dim, 2D, 1M tuples,
+# TotalTime 19,544 ms (python/graph_paper_figures.py:29; hardware unstated)
+C1_PUBLISHED_MS = 19544.0
+
+
+def host_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def filter_roofline(eng, D):
+    """k_filter over the timed launches: algorithmic bytes = the f64 row read once + the u16
+    status word written (8D + 2 per tuple), / its HIP-event time."""
+    f_ms, f_launch, f_units = eng.kernel_time("filter")
+    if not f_launch:
+        return None
+    bpt = D * 8 + 2
+    avg_ms = f_ms / f_launch
+    units = f_units / f_launch
+    achieved = bpt * units / (avg_ms / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": "k_filter", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_unit": bpt,
+            "units_per_launch": units, "avg_launch_ms": avg_ms, "launches": f_launch}
+
+
+def traffic_for(n, D, dist_name):
+    tf = os.path.join(REPO, "profiles", "traffic_filter.json")
+    try:
+        tj = json.load(open(tf))
+        if tj.get("n") == n and tj.get("dims") == D and tj.get("dist") == dist_name:
+            return tj.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def sweep_alpha(cfg_name):
+    """Exponent of t = a * N^alpha from the committed CPU sweep (None if absent)."""
+    for f in ("r02_cpu_baseline_sweep.json",):
+        p = os.path.join(REPO, "profiles", f)
+        try:
+            sw = json.load(open(p))
+            fit = sw["configs"][cfg_name]["fit"]
+            return max(float(v["alpha"]) for v in fit.values()), f
+        except Exception:
+            continue
+    return None, None
+
+
+def cpu_baseline(cfg_name, cfg, seed):
+    """The reference operators restated in C (oracle/, test infrastructure: the checker and
+    this baseline only): per-key BNL with 5000-tuple buffers, one thread per Flink subtask
+    (keys round-robin over p = Flink parallelism = P/2 threads), then the single-threaded
+    global BNL merge, on the first `sample` tuples of the same stream."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import Oracle
+    orc = Oracle()
+    n_s = cfg["cpu_sample"]
+    D, P = cfg["dims"], cfg["partitions"]
+    vals = orc.synth(_abi.DISTS[cfg["dist"]], D, n_s, seed=seed)
+    ids = np.arange(n_s, dtype=np.int64)
+    algo = cfg["algo"][3:]
+    p = max(1, min(P // 2, host_cores()))
+    t0 = time.perf_counter()
+    g, _, _, _ = orc.query_bnl_mt(algo, vals, ids, P, p)
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    g1, _, _, _ = orc.query_bnl(algo, vals, ids, P)
+    dt1 = time.perf_counter() - t0
+    assert sorted(g.tolist()) == sorted(g1.tolist())
+    out = {"value": n_s / dt, "unit": "tuples/s", "cores": p, "kind": "port",
+           "sample": f"first {n_s} tuples of the same {cfg['dist']} stream (seed {seed}); oracle/ C restatement of "
+                     f"the reference operators: per-key BNL (buffer 5000) on {p} subtask threads, single-threaded "
+                     f"global BNL: {dt:.2f} s, skyline {len(g)}",
+           "single_thread": {"value": n_s / dt1, "cores": 1, "seconds": dt1}}
+    N = cfg["tuples"]
+    if n_s < N:
+        alpha, src = sweep_alpha(cfg_name)
+        if alpha is not None:
+            t_full = dt * (N / n_s) ** alpha
+            out["extrapolated_full"] = {"tuples": N, "seconds": t_full, "tuples_per_s": N / t_full,
+                                        "alpha": alpha, "fit_source": "profiles/" + src,
+                                        "note": "EXTRAPOLATION t(N) = t(sample) * (N/sample)^alpha, alpha fitted "
+                                                "over the N-sweep; the reference BNL is quadratic in the "
+                                                "duplicate all-zero tuples (SURVEY §3)"}
+    return out
+
+
+def make_stream(eng, dist_name, n, seed, id0, dev):
+    vals = torch.empty((n, eng.dims), dtype=torch.float64, device=dev)
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.synth_dev(dist_name, n, vals, ids, seed=seed, id0=id0)
+    eng.sync()
+    return vals, ids
+
+
+def time_steps(step, eng, steps, warmup, distributed):
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    eng.profile_reset()
+    step_ms = []
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = 0
+    for _ in range(steps):
+        ts = time.perf_counter()
+        g = step()
+        eng.sync()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.profile(False)
+    return elapsed, step_ms, g
+
+
+def config_line(name, dev, dev_index, steps, warmup, with_cpu):
+    """One BASELINE configuration on one GPU (sub-line of the default run, or --config)."""
+    cfg = CONFIGS[name]
+    D, P, n = cfg["dims"], cfg["partitions"], cfg["tuples"]
+    seed = 1234 + D
+    eng = skyline.SkylineEngine(D, P, cfg["algo"], 1000.0, dev_index)
+    vals, ids = make_stream(eng, cfg["dist"], n, seed, 0, dev)
+    out_ids = torch.empty(n, dtype=torch.int64, device=dev)
+    out_org = torch.empty(n, dtype=torch.int32, device=dev)
+    elapsed, step_ms, g = time_steps(lambda: eng.query_dev(ids, vals, out_ids, out_org, n), eng, steps, warmup, False)
+    phases, counters = eng.phases()
+    roof = filter_roofline(eng, D)
+    if roof:
+        roof["traffic"] = traffic_for(n, D, cfg["dist"])
+    ms = elapsed * 1e3 / steps
+    line = {"metric": METRIC, "value": n / (ms / 1e3), "unit": "tuples/s", "n_gpus": 1, "steps": steps,
+            "warmup": warmup, "ms_per_step": ms, "p50_query_latency_ms": statistics.median(step_ms),
+            "dtype": "f64", "config": {"workload": cfg["workload"], "tuples": n, "dims": D, "partitions": P,
+                                       "algo": cfg["algo"], "dist": cfg["dist"], "seed": seed, "skyline_size": g},
+            "roofline": roof, "phases_ms_last_step": phases,
+            "counters_last_step": {"candidates": int(counters[1]), "distinct_reps": int(counters[2]),
+                                   "global_candidates": int(counters[3]), "output": int(counters[4])}}
+    if name == "C1":
+        ref_rate = 1e6 / (C1_PUBLISHED_MS / 1e3)
+        line["vs_published"] = {"reference_total_ms": C1_PUBLISHED_MS, "reference_tuples_per_s": ref_rate,
+                                "ratio": line["value"] / ref_rate,
+                                "source": "python/graph_paper_figures.py:29 (MR-Dim 2D 1M TotalTime, includes "
+                                          "Kafka ingest; hardware unstated)"}
+    if with_cpu:
+        line["cpu_baseline"] = cpu_baseline(name, cfg, seed)
+    eng.close()
+    del vals, ids, out_ids, out_org
+    torch.cuda.empty_cache()
+    return line
+
+
+def end_to_end_c4(eng, vals, ids, n, D, steps, out_ids, out_org):
+    """C4 with the host->device transfer inside the timed region (the reference's
+    total_processing_time_ms spans first tuple to emission, FlinkSkyline.java:581-587):
+    (a) f64 rows + i64 ids from pinned host memory -> HBM -> query;
+    (b) the producers' CSV text (unified_producer.py:174) from pinned host memory -> HBM ->
+        device CSV decode (k_csv.hip) -> query."""
+    dev = vals.device
+    h_vals = torch.empty(vals.shape, dtype=vals.dtype, pin_memory=True)
+    h_ids = torch.empty(ids.shape, dtype=ids.dtype, pin_memory=True)
+    h_vals.copy_(vals)
+    h_ids.copy_(ids)
+    d_vals = torch.empty_like(vals)
+    d_ids = torch.empty_like(ids)
+    res = {}
+
+    def rows_step():
+        d_vals.copy_(h_vals, non_blocking=True)
+        d_ids.copy_(h_ids, non_blocking=True)
+        return eng.query_dev(d_ids, d_vals, out_ids, out_org, n)
+
+    for _ in range(1):
+        rows_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g = rows_step()
+    eng.sync()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        d_vals.copy_(h_vals, non_blocking=True)
+        d_ids.copy_(h_ids, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = (time.perf_counter() - t1) / steps
+    byts = n * (8 * D + 8)
+    res["rows_h2d"] = {"workload": f"C4, {n} f64 rows + i64 ids from pinned host memory, H2D + query per step",
+                       "tuples_per_s": n / dt, "ms_per_step": dt * 1e3, "skyline_size": g,
+                       "h2d_ms": h2d * 1e3, "h2d_GBs": byts / h2d / 1e9, "h2d_bytes": byts}
+    del h_vals, h_ids
+    nb = eng.format_csv_dev(ids, vals, n)
+    text = torch.empty(nb, dtype=torch.uint8, device=dev)
+    eng.format_csv_dev(ids, vals, n, text, nb)
+    h_text = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h_text.copy_(text)
+
+    def csv_step():
+        text.copy_(h_text, non_blocking=True)
+        eng.parse_csv_dev(text, nb, d_ids, d_vals, n)
+        return eng.query_dev(d_ids, d_vals, out_ids, out_org, n)
+
+    csv_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g = csv_step()
+    eng.sync()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    res["csv_h2d"] = {"workload": f"C4 as producer CSV text ({nb} bytes) from pinned host memory: H2D + device "
+                                  f"decode + query per step", "tuples_per_s": n / dt, "ms_per_step": dt * 1e3,
+                      "skyline_size": g, "text_bytes": nb}
+    del text, h_text, d_vals, d_ids
+    torch.cuda.empty_cache()
+    return res
 
 
 def dominance_run(dev, D, P, n, seed, steps, warmup):
@@ -77,8 +322,12 @@ def dominance_run(dev, D, P, n, seed, steps, warmup):
             "workload": f"std_anti (labelled extension generator) {D}D, {n} tuples, MR-Angle P={P}",
             "tuples_per_s": n / dt, "ms_per_query": dt * 1e3, "skyline_size": g,
             "pair_tests_W": w, "compares": D * w, "dominance_ms": dom_ms,
-            "achieved": achieved, "peak": VALU_PEAK_CMPS, "unit": "compares/s",
-            "frac": achieved / VALU_PEAK_CMPS, "path": "u16" if int(counters[7]) & 4 else "f32/f64",
+            "achieved": achieved, "peak": VALU_PEAK_PK16, "unit": "compares/s",
+            "frac": achieved / VALU_PEAK_PK16,
+            "peak_note": "packed-u16 compare peak (2 compares per v_pk_sub_u16 lane-op); the 32-bit lane-op "
+                         "peak is half of it",
+            "peak_32bit": VALU_PEAK_32, "frac_32bit": achieved / VALU_PEAK_32,
+            "path": "u16" if int(counters[7]) & 4 else "f32/f64",
             "local_sfs_ms": phases["local_sfs"], "global_sfs_ms": phases["global_sfs"],
             "sfs_rounds": int(counters[5])}
 
@@ -115,7 +364,7 @@ def csv_ingest_run(eng, ids, vals, n, D, steps, out_ids, out_org):
     p_ms = kt["csv_parse"][0] / max(kt["csv_parse"][1], 1)
     k_ms = sum(kt[k][0] / max(kt[k][1], 1) for k in kt)
     del text, pi, pv
-    achieved = (nb + n * (8 + 8 * D)) / (p_ms / 1e3) / 1e9
+    achieved = alg / (p_ms / 1e3) / 1e9
     return {"bound": "hbm", "kernel": "k_csv_parse (+ k_csv_nl_count, k_csv_nl_write)",
             "workload": f"C4 stream as producer CSV text, {n} records, {nb} bytes",
             "text_bytes": nb, "records": m,
@@ -135,7 +384,6 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     (H2D included); a query_trigger every `per_trigger` tuples.  Latency = trigger -> global
     skyline ids in host memory.  window=0: the reference's landmark window; window=W:
     the count-based sliding window extension."""
-    import numpy as np
     D, P = 6, 8
     n = triggers * per_trigger
     vals_np, ids_np = skyline.synth_host(_abi.DISTS["mixed"], D, n, seed=seed)
@@ -144,6 +392,8 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
     st = skyline.SkylineStream(eng, window)
     lat, sizes = [], []
+    eng.profile(True)
+    eng.profile_reset()
     t_start = time.perf_counter()
     for t in range(triggers):
         base = t * per_trigger
@@ -154,6 +404,8 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
         lat.append((time.perf_counter() - tq) * 1e3)
         sizes.append(g)
     total = time.perf_counter() - t_start
+    eng.profile(False)
+    roof = filter_roofline(eng, D)
     resident, _ = st.size()
     st.close()
     eng.close()
@@ -163,15 +415,16 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
                          + ("landmark window (reference semantics)" if window == 0
                             else f"count-based sliding window W={window} (extension)")),
             "ingest_tuples_per_s": rate, "sustains_10M_per_s": rate >= 1e7,
-            "p50_query_latency_ms": statistics.median(lat), "max_query_latency_ms": max(lat),
-            "skyline_size_last": sizes[-1], "resident_tuples_last": resident}
+            "p50_query_latency_ms": statistics.median(lat), "p90_query_latency_ms": sorted(lat)[int(0.9 * len(lat))],
+            "max_query_latency_ms": max(lat), "skyline_size_last": sizes[-1], "resident_tuples_last": resident,
+            "roofline": roof}
 
 
 def sort_run(eng, n, dev, steps=3):
     """Sort phase at scale (HBM GB/s of the sort): the pipeline's radix sort
     (k_radix.hip) alone on n pairs keyed like its candidate keys (4-bit partition | 32-bit
-    score | 16-bit hash, 52 varying bits -> 7 onesweep passes).  Algorithmic bytes =
-    passes x n x 24 (read + write a u64 key and a u32 value per pass)."""
+    score | 16-bit hash, 52 varying bits).  Algorithmic bytes = passes x n x 24 (read +
+    write a u64 key and a u32 value per pass)."""
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     part = torch.randint(0, 16, (n,), device=dev, dtype=torch.int64, generator=g)
@@ -180,14 +433,6 @@ def sort_run(eng, n, dev, steps=3):
     keys0 = (part << 56) | (score << 24) | hsh
     del part, score, hsh
     vals0 = torch.arange(n, device=dev, dtype=torch.int32)
-    kor = torch.zeros((), dtype=torch.int64, device=dev)
-    kand = torch.full((), -1, dtype=torch.int64, device=dev)
-    for b in range(64):   # varying key bits / bytes, to cross-check the library's pass count
-        bit = (keys0 >> b) & 1
-        kor |= bit.max() << b
-        kand &= (bit.min() << b) | ~(torch.ones((), dtype=torch.int64, device=dev) << b)
-    varying = int((kor ^ kand).item())
-    var_bytes = sum(1 for byte in range(8) if (varying >> (8 * byte)) & 0xff)
     best, passes = None, 0
     for i in range(steps + 1):
         keys = keys0.clone()
@@ -202,35 +447,9 @@ def sort_run(eng, n, dev, steps=3):
     achieved = alg / (best / 1e3) / 1e9
     del keys0, vals0, keys, vals
     return {"bound": "hbm", "kernel": "k_rs_onesweep (+ k_rs_hist_all, k_rs_scan_all)",
-            "workload": f"{n} (u64 key, u32 value) pairs, {bin(varying & ((1 << 64) - 1)).count('1')} varying "
-                        f"key bits in {var_bytes} bytes", "passes": passes,
-            "ms": best, "keys_per_s": n / (best / 1e3), "alg_bytes": alg,
+            "workload": f"{n} (u64 key, u32 value) pairs, 4-bit partition | 32-bit score | 16-bit hash",
+            "passes": passes, "ms": best, "keys_per_s": n / (best / 1e3), "alg_bytes": alg,
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}
-
-
-def cpu_baseline(d, P, dist_name, seed, sample, domain):
-    """Reference algorithm restated in C (per-key BNL, buffer 5000, single-threaded
-    global BNL), one thread, on the first `sample` tuples of the same stream."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from conftest import Oracle   # test infrastructure: the checker / CPU baseline only
-    orc = Oracle()
-    vals = orc.synth(_abi.DISTS[dist_name], d, sample, seed=seed)
-    ids = np.arange(sample, dtype=np.int64)
-    t0 = time.perf_counter()
-    g, _, _, _ = orc.query_bnl("angle", vals, ids, P, domain)
-    dt = time.perf_counter() - t0
-    # one thread per Flink subtask for the local phase (keys round-robin), single-threaded merge
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores, P))
-    t0 = time.perf_counter()
-    g2, _, _, _ = orc.query_bnl_mt("angle", vals, ids, P, threads, domain)
-    dt2 = time.perf_counter() - t0
-    assert sorted(g.tolist()) == sorted(g2.tolist())
-    return sample / dt, dt, len(g), sample / dt2, dt2, threads
 
 
 def main():
@@ -238,18 +457,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--tuples", type=int, default=100_000_000, help="tuples per rank (GPU)")
-    ap.add_argument("--dims", type=int, default=8)
-    ap.add_argument("--partitions", type=int, default=16)
-    ap.add_argument("--dist", default="anti_correlated")
-    ap.add_argument("--seed", type=int, default=1242)
-    ap.add_argument("--cpu-sample", type=int, default=60000)
+    ap.add_argument("--config", default="C4", choices=["C1", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --tuples per rank; strong: --tuples in total, split over the ranks")
+    ap.add_argument("--tuples", type=int, default=None, help="override the config's tuple count")
+    ap.add_argument("--dist", default=None, help="override the config's distribution (e.g. std_anti)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
     ap.add_argument("--no-dominance", action="store_true")
     ap.add_argument("--no-csv", action="store_true", help="skip the CSV-ingest companion measurement")
     ap.add_argument("--no-stream", action="store_true", help="skip the C5 continuous-query companion measurement")
     ap.add_argument("--no-sort", action="store_true", help="skip the radix-sort-at-scale companion measurement")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C3 sub-lines")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (H2D inside) C4 rates")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the measured path) or gloo (rehearsing ranks on one GPU)")
     args = ap.parse_args()
@@ -269,12 +489,36 @@ def main():
             dist.init_process_group("gloo")
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
-    D, P, n = args.dims, args.partitions, args.tuples
-    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
-    vals = torch.empty((n, D), dtype=torch.float64, device=dev)
-    ids = torch.empty(n, dtype=torch.int64, device=dev)
-    eng.synth_dev(args.dist, n, vals, ids, seed=args.seed, id0=rank * n)
-    eng.sync()
+    if args.config == "C5":
+        if rank == 0:
+            lm = stream_run(dev_index, 1234 + 6)
+            sl = stream_run(dev_index, 1234 + 6, window=10_000_000)
+            line = {"metric": METRIC, "value": lm["ingest_tuples_per_s"], "unit": "tuples/s", "n_gpus": 1,
+                    "steps": 20, "warmup": 0, "ms_per_step": lm["p50_query_latency_ms"],
+                    "p50_query_latency_ms": lm["p50_query_latency_ms"], "higher_is_better": True,
+                    "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                    "data": "synthetic (6D mixed blocks of the reference formulas)",
+                    "config": {"workload": lm["workload"]}, "roofline": lm["roofline"],
+                    "cpu_baseline": None, "landmark": lm, "sliding_10M": sl}
+            print(json.dumps(line), flush=True)
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    cfg = dict(CONFIGS[args.config])
+    if args.dist:
+        cfg["dist"] = args.dist
+    D, P = cfg["dims"], cfg["partitions"]
+    n_cfg = args.tuples or cfg["tuples"]
+    if args.scaling == "strong":
+        lo, hi = rank * n_cfg // world, (rank + 1) * n_cfg // world
+        n, id0, total = hi - lo, lo, n_cfg
+    else:
+        n, id0, total = n_cfg, rank * n_cfg, n_cfg * world
+    seed = 1234 + D
+    eng = skyline.SkylineEngine(D, P, cfg["algo"], 1000.0, dev_index)
+    vals, ids = make_stream(eng, cfg["dist"], n, seed, id0, dev)
     out_ids = torch.empty(n, dtype=torch.int64, device=dev)
     out_org = torch.empty(n, dtype=torch.int32, device=dev)
 
@@ -283,108 +527,76 @@ def main():
             return distributed_query(eng, ids, vals, out_ids, out_org, n)
         return eng.query_dev(ids, vals, out_ids, out_org, n)
 
-    for _ in range(args.warmup):
-        step()
-    eng.sync()
-    torch.cuda.synchronize()
-    eng.profile(True)
-    eng.profile_reset()
-    step_ms = []
+    elapsed, step_ms, g = time_steps(step, eng, args.steps, args.warmup, distributed)
+    p50 = statistics.median(step_ms)
     if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    g = 0
-    for _ in range(args.steps):
-        ts = time.perf_counter()
-        g = step()
-        eng.sync()
-        step_ms.append((time.perf_counter() - ts) * 1e3)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    eng.profile(False)
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([elapsed, p50], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, p50 = float(t[0].item()), float(t[1].item())
         gt = torch.tensor([g], dtype=torch.int64, device=red_dev)
         dist.all_reduce(gt)
         g = int(gt.item())
     phases, counters = eng.phases()
-    f_ms, f_launch, f_units = eng.kernel_time("filter")
+    roof = filter_roofline(eng, D)
+    dist_stats = eng.last_dist_stats if distributed else None
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
-        total = n * world
         value = total / (ms_per_step / 1e3)
-        bytes_per_tuple = D * 8 + 2            # read the f64 row once, write the u16 status word
-        avg_ms = f_ms / max(f_launch, 1)
-        achieved = (bytes_per_tuple * (f_units / max(f_launch, 1))) / (avg_ms / 1e3) / 1e9 if f_launch else 0.0
-        traffic = None
-        tf = os.path.join(REPO, "profiles", "traffic_filter.json")
-        if os.path.exists(tf):
-            try:
-                tj = json.load(open(tf))
-                if tj.get("n") == n and tj.get("dims") == D and tj.get("dist") == args.dist:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        if roof:
+            roof["traffic"] = traffic_for(n, D, cfg["dist"])
+        solo = world == 1
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            rate, dt, gs, rate_mt, dt_mt, thr = cpu_baseline(D, P, args.dist, args.seed, args.cpu_sample, 1000.0)
-            cpu = {"value": rate_mt, "unit": "tuples/s", "cores": thr, "kind": "port",
-                   "sample": f"first {args.cpu_sample} tuples of the same stream, oracle/ C restatement of the "
-                             f"reference per-key BNL (buffer 5000), one thread per subtask ({thr}), then the "
-                             f"single-threaded global BNL: {dt_mt:.1f} s, skyline {gs}",
-                   "single_thread": {"value": rate, "cores": 1, "seconds": dt}}
-        csvr = None
-        if world == 1 and not args.no_csv:
-            csvr = csv_ingest_run(eng, ids, vals, n, D, 3, out_ids, out_org)
-        sortr = None
-        if world == 1 and not args.no_sort:
-            sortr = sort_run(eng, n, dev)
-        streamr = None
-        if world == 1 and not args.no_stream:
-            streamr = {"landmark": stream_run(dev_index, args.seed),
-                       "sliding_10M": stream_run(dev_index, args.seed, window=10_000_000)}
-        domr = None
-        if world == 1 and not args.no_dominance:
-            domr = dominance_run(dev, D, P, args.dom_n, args.seed, 2, 1)
+        if solo and not args.no_cpu_baseline:
+            c = dict(cfg)
+            c["tuples"] = n_cfg
+            cpu = cpu_baseline(args.config, c, seed)
+        extra = {}
+        if solo and args.config == "C4" and n_cfg == CONFIGS["C4"]["tuples"] and not args.dist:
+            if not args.no_e2e:
+                extra["end_to_end"] = end_to_end_c4(eng, vals, ids, n, D, 3, out_ids, out_org)
+            if not args.no_csv:
+                extra["csv_ingest"] = csv_ingest_run(eng, ids, vals, n, D, 3, out_ids, out_org)
+            if not args.no_sort:
+                extra["sort_roofline"] = sort_run(eng, n, dev)
+            if not args.no_configs:
+                extra["configs"] = {nm: config_line(nm, dev, dev_index, args.steps, args.warmup,
+                                                    not args.no_cpu_baseline)
+                                    for nm in ("C1", "C2", "C3")}
+                if not args.no_stream:
+                    extra["configs"]["C5"] = {"landmark": stream_run(dev_index, 1234 + 6),
+                                              "sliding_10M": stream_run(dev_index, 1234 + 6, window=10_000_000)}
+            if not args.no_dominance:
+                extra["dominance_roofline"] = dominance_run(dev, D, P, args.dom_n, seed, 2, 1)
         line = {
-            "metric": "skyline tuples/sec + p50 query latency, 8D anti-corr, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value,
             "unit": "tuples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
-            "p50_query_latency_ms": statistics.median(step_ms),
+            "p50_query_latency_ms": p50,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (reference anti-correlated formula, counter RNG, generated in HBM)",
-            "config": {"workload": "C4: MR-Angle 8D anti-correlated, P=16, landmark-window query",
-                       "tuples_per_gpu": n, "dims": D, "partitions": P, "algo": "mr-angle",
-                       "dist": args.dist, "domain": [0, 1000], "compare_dtype": "f32 (values exact)",
+            "data": "synthetic (reference generator formulas, counter RNG, generated in HBM)",
+            "config": {"workload": cfg["workload"], "tuples_per_gpu": n, "tuples_total": total, "dims": D,
+                       "partitions": P, "algo": cfg["algo"], "dist": cfg["dist"], "domain": [0, 1000],
+                       "seed": seed, "compare_dtype": "f32 / packed u16 when the values are exact",
                        "parallelism": f"shards{world}", "skyline_size": g},
-            "roofline": {"bound": "hbm", "kernel": "k_filter", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_unit": bytes_per_tuple, "units_per_launch": f_units / max(f_launch, 1),
-                         "avg_launch_ms": avg_ms, "launches": f_launch},
+            "roofline": roof,
             "phases_ms_last_step": phases,
             "counters_last_step": {"n": int(counters[0]), "candidates": int(counters[1]),
                                    "distinct_reps": int(counters[2]), "global_candidates": int(counters[3]),
                                    "output": int(counters[4]), "sfs_rounds": int(counters[5])},
+            "dist_exchange": dist_stats,
             "cpu_baseline": cpu,
-            "dominance_roofline": domr,
-            "csv_ingest": csvr,
-            "stream_c5": streamr,
-            "sort_roofline": sortr,
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
+    eng.close()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -281,6 +281,14 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
     GUARD_END
 }
 
+int sky_global_stats_set(sky_ctx *c, int32_t k, const int64_t *local_sizes, const int64_t *survivors) {
+    ARG_CHECK(c && k >= 0 && k <= 65536 && (k == 0 || (local_sizes && survivors)), "bad arguments");
+    c->K_last = k;
+    c->lsz.assign(local_sizes, local_sizes + k);
+    c->surv.assign(survivors, survivors + k);
+    return SKY_OK;
+}
+
 int sky_global_stats(sky_ctx *c, int64_t *local_sizes, int64_t *survivors, int32_t *k_out) {
     ARG_CHECK(c, "ctx is null");
     if (k_out) *k_out = c->K_last;
@@ -486,8 +494,11 @@ int sky_export_local_dev(sky_ctx *c, const int64_t *d_ids, const double *d_value
         launch_rep_mult(p.mt, p.perm.as<uint32_t>(), p.slot_src.as<uint32_t>(), p.slot_rep.as<uint32_t>(),
                         in.weights, p.dup_cnt.as<uint32_t>(), p.pr_entries.as<int32_t>(),
                         p.mult.as<unsigned long long>(), c->st);
-        HIP_TRY(hipMemcpyAsync(&ne, p.totals.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, c->st));
+        SKY_TRY(p.pinned(64));
+        HIP_TRY(hipMemcpyAsync(p.pin, p.totals.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, c->st));
         HIP_TRY(hipStreamSynchronize(c->st));
+        p.up_used = 0;
+        ne = *(volatile uint32_t *)p.pin;
     }
     c->shard = in;
     c->shard_valid = true;
@@ -521,63 +532,72 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
     ARG_CHECK(c && c->shard_valid, "call sky_export_local_dev first");
     ARG_CHECK(n_union >= 0 && n_union < (int64_t)0x7fffffffLL, "n_union out of range");
     ARG_CHECK(self_offset >= 0 && self_offset + c->counters[3] <= n_union, "self_offset out of range");
+    ARG_CHECK(n_union == 0 || (d_rows && d_keys && d_mult), "null union buffers");
     SKY_TRY(bind(c));
-    PipeIn u;
-    u.vals = d_rows;
-    u.n = (uint32_t)n_union;
-    u.keys = d_keys;
-    u.weights = d_mult;
-    u.global = true;
-    u.K = c->Kq();
-    SKY_TRY(pipe_run(*c, c->aux, u, nullptr));
-    store_stats(c, c->aux);
-    SKY_TRY(c->h_flags.ensure((size_t)std::max<int64_t>(n_union, 1)));
-    SKY_TRY(pipe_output(*c, c->aux, u, false, nullptr, nullptr, nullptr, 0, nullptr, c->h_flags.as<uint8_t>()));
     Pipe &p = c->main;
+    const uint32_t n_own = (uint32_t)c->counters[3];
+    const int K = c->Kq();
+    // this rank's own vectors against the union: flags + this rank's share of |L_k| / survivors_k
+    SKY_TRY(c->h_flags.ensure((size_t)std::max<int64_t>(n_union, 1)));
+    SKY_TRY(p.statk.ensure((size_t)K * 16));
+    unsigned long long *d_lsz = p.statk.as<unsigned long long>(), *d_surv = d_lsz + K;
+    HIP_TRY(hipMemsetAsync(d_lsz, 0, (size_t)K * 16, c->st));
+    c->ktimer_begin("union_fate", c->st);
+    launch_union_fate(c->D, d_rows, d_keys, d_mult, (uint32_t)n_union, (uint32_t)self_offset, n_own, K,
+                      c->h_flags.as<uint8_t>(), d_lsz, d_surv, c->st);
+    c->ktimer_end("union_fate", c->st, (int64_t)n_own * n_union);
+    HIP_TRY(hipGetLastError());
     launch_import_flags(p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), p.mr, c->h_flags.as<uint8_t>(),
                         (uint32_t)self_offset, p.alive_g.as<uint8_t>(), c->st);
-    // recount this shard's output with the imported global fates (no stats: those came from the union)
-    {
-        const uint32_t tiles = (p.n + kTile - 1) / kTile;
-        // the export ran without a fate pass: size the per-tile count buffers here
-        SKY_TRY(p.out_cnt.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
-        SKY_TRY(p.out_off.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
-        SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
-        FateArgs fta{};
-        fta.mt = p.mt;
-        fta.slot_rep = p.slot_rep.as<uint32_t>();
-        fta.slot_src = p.slot_src.as<uint32_t>();
-        fta.alive_l = p.alive_l.as<uint8_t>();
-        fta.alive_g = p.alive_g.as<uint8_t>();
-        fta.KM = p.Kp * p.M;
-        fta.M = p.M;
-        fta.K = p.K;
-        fta.pruner_slot = p.pruner_slot.as<int32_t>();
-        fta.status = p.status.as<uint16_t>();
-        fta.pruner_fate = p.pruner_fate.as<uint8_t>();
-        launch_fate_tables(fta, c->st);             // no stats: those came from the union
-        OutArgs oa{};
-        oa.status = p.status.as<uint16_t>();
-        oa.n = p.n;
-        oa.pruner_fate = p.pruner_fate.as<uint8_t>();
-        oa.M = p.M;
-        oa.KM = p.Kp * p.M;
-        oa.K = p.K;
-        oa.out_cnt = p.out_cnt.as<uint32_t>();
-        if (p.n) {
-            launch_out_count(oa, c->st);
-            scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                          p.scratch.as<uint32_t>(), c->st);
-            uint32_t nout = 0;
-            HIP_TRY(hipMemcpyAsync(&nout, p.totals.as<uint32_t>() + 3, 4, hipMemcpyDeviceToHost, c->st));
-            HIP_TRY(hipStreamSynchronize(c->st));
-            p.nout = nout;
-        } else {
-            p.nout = 0;
-        }
+    // recount this shard's output with the imported global fates
+    const uint32_t tiles = (p.n + kTile - 1) / kTile;
+    // the export ran without a fate pass: size the per-tile count buffers here
+    SKY_TRY(p.out_cnt.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
+    SKY_TRY(p.out_off.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
+    FateArgs fta{};
+    fta.mt = p.mt;
+    fta.slot_rep = p.slot_rep.as<uint32_t>();
+    fta.slot_src = p.slot_src.as<uint32_t>();
+    fta.alive_l = p.alive_l.as<uint8_t>();
+    fta.alive_g = p.alive_g.as<uint8_t>();
+    fta.KM = p.Kp * p.M;
+    fta.M = p.M;
+    fta.K = p.K;
+    fta.pruner_slot = p.pruner_slot.as<int32_t>();
+    fta.status = p.status.as<uint16_t>();
+    fta.pruner_fate = p.pruner_fate.as<uint8_t>();
+    launch_fate_tables(fta, c->st);             // no stats: the union kernel summed this rank's share
+    OutArgs oa{};
+    oa.status = p.status.as<uint16_t>();
+    oa.n = p.n;
+    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
+    oa.M = p.M;
+    oa.KM = p.Kp * p.M;
+    oa.K = p.K;
+    oa.out_cnt = p.out_cnt.as<uint32_t>();
+    if (p.n) {
+        launch_out_count(oa, c->st);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), c->st);
     }
+    // one read-back: the output count and the K-sized stat shares
+    SKY_TRY(p.pinned((size_t)K * 16 + 64));
+    HIP_TRY(hipMemcpyAsync(p.pin, d_lsz, (size_t)K * 16, hipMemcpyDeviceToHost, c->st));
+    if (p.n)
+        HIP_TRY(hipMemcpyAsync((char *)p.pin + (size_t)K * 16, p.totals.as<uint32_t>() + 3, 4, hipMemcpyDeviceToHost,
+                               c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    p.up_used = 0;
+    const unsigned long long *hs = (const unsigned long long *)p.pin;
+    p.nout = p.n ? *(const uint32_t *)((const char *)p.pin + (size_t)K * 16) : 0;
+    c->K_last = K;
+    c->lsz.assign(hs, hs + K);
+    c->surv.assign(hs + K, hs + 2 * K);
+    c->counters[4] = p.nout;
     SKY_TRY(pipe_output(*c, p, c->shard, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr));
     HIP_TRY(hipGetLastError());
+    finish_profile(c);
     return SKY_OK;
     GUARD_END
 }

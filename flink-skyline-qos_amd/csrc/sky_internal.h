@@ -194,6 +194,11 @@ struct FillSet : FillRanges {
 hipError_t launch_gather_words(const FillRanges &g, void *pinned_dst, hipStream_t st);
 void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
                          uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
+// own exported vectors [off, off+n_own) of the gathered union -> flags (bit0 in L_k, bit1 in G)
+// and this rank's multiplicity sums into lsz[K] / surv[K]
+void launch_union_fate(int D, const double *urows, const int32_t *ukeys, const int64_t *umult, uint32_t n_union,
+                       uint32_t off, uint32_t n_own, int K, uint8_t *flags, unsigned long long *lsz,
+                       unsigned long long *surv, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
                         uint64_t *gkey, uint32_t *gval, unsigned long long *orand, hipStream_t st);
 void launch_sfs_small(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,

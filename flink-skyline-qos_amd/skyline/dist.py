@@ -1,16 +1,25 @@
 """Multi-GPU skyline: one process per GPU, shards of the tuple stream per rank.
 
-Exactness: SKY(u_k SKY(P_k)) = SKY(u P_k) for ANY split, so each rank reduces its
-own shard to the distinct vectors of its local skylines (sky_export_local_dev),
-the ranks exchange those vectors with ONE all-gather (RCCL over xGMI when the
-process group is "nccl"; gloo on CPU for tests), and every rank finishes the
-per-partition and global skylines over the union (sky_import_union_dev).
+Exactness: SKY(u_k SKY(P_k)) = SKY(u P_k) for ANY split, so:
+  1. each rank reduces its own shard to the distinct vectors of its local skylines, with
+     partition key and multiplicity (sky_export_local_dev);
+  2. the ranks exchange those vectors with ONE all-gather (RCCL over xGMI when the process
+     group is "nccl"; gloo on CPU for tests), counts first;
+  3. each rank decides the fate of ITS OWN vectors against the gathered union
+     (sky_import_union_dev: in L_k iff no union vector of key k dominates it, in G iff no
+     union vector dominates it) -- |own| x |union| pair tests per rank, so the global phase
+     shrinks with the number of ranks instead of being replicated on every rank;
+  4. the per-rank shares of |L_k| and survivors_k are summed with one all-reduce of 2K
+     integers (the optimality inputs, FlinkSkyline.java:593-608).
 Tuple ids never leave their rank: each rank emits its own global-skyline ids.
 
 Wire format of one exported vector (int64 words): D value words (f64 bits),
 1 partition key, 1 multiplicity  ->  [count, D+2] int64 per rank, padded to the
 largest count (counts are all-gathered first).
 """
+import time
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -58,11 +67,25 @@ def allgather_varlen(packed, group=None):
     return out, counts
 
 
+def allreduce_stats(ls, sv, device, group=None):
+    """Sum the per-rank |L_k| / survivors_k shares over the ranks (one all-reduce)."""
+    K = len(ls)
+    backend = dist.get_backend(group)
+    dev = device if (backend != "gloo" and device.type == "cuda") else torch.device("cpu")
+    t = torch.from_numpy(np.concatenate([ls, sv]).astype(np.int64)).to(dev)
+    dist.all_reduce(t, group=group)
+    t = t.cpu().numpy()
+    return t[:K], t[K:]
+
+
 def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, cap, group=None):
     """One query over the union of every rank's shard.  Returns this rank's
-    number of global-skyline ids written to d_ids_out (stream order)."""
+    number of global-skyline ids written to d_ids_out (stream order); afterwards
+    engine.stats() holds the job-wide |L_k| / survivors_k and engine.last_dist_stats
+    the exchange's sizes and phase times."""
     D = engine.dims
     dev = d_vals.device
+    t0 = time.perf_counter()
     ne = engine.export_local_dev(d_ids, d_vals)
     rows = torch.empty((max(ne, 1), D), dtype=torch.float64, device=dev)
     keys = torch.empty(max(ne, 1), dtype=torch.int32, device=dev)
@@ -70,10 +93,26 @@ def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, cap, group
     if ne:
         engine.export_copy_dev(rows, keys, mult, ne)
     engine.sync()
+    t1 = time.perf_counter()
     packed = pack_export(rows[:ne], keys[:ne], mult[:ne])
     gathered, counts = allgather_varlen(packed, group)
     urows, ukeys, umult = unpack_union(gathered, counts, D)
     rank = dist.get_rank(group)
     self_off = sum(counts[:rank])
-    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
-    return engine.import_union_dev(urows, ukeys, umult, urows.shape[0], self_off, d_ids_out, d_origin_out, cap)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    g = engine.import_union_dev(urows, ukeys, umult, urows.shape[0], self_off, d_ids_out, d_origin_out, cap)
+    ls, sv = engine.stats()                      # this rank's share
+    t3 = time.perf_counter()
+    ls, sv = allreduce_stats(ls, sv, dev, group)
+    engine.set_stats(ls, sv)
+    t4 = time.perf_counter()
+    n_union = int(urows.shape[0])
+    engine.last_dist_stats = {
+        "world": dist.get_world_size(group), "union_vectors": n_union, "own_vectors": ne,
+        "exchange_bytes_per_rank": int(gathered.numel() * 8),
+        "own_x_union_pair_tests": ne * n_union,
+        "ms": {"export": (t1 - t0) * 1e3, "allgather": (t2 - t1) * 1e3, "import": (t3 - t2) * 1e3,
+               "stats_allreduce": (t4 - t3) * 1e3}}
+    return g

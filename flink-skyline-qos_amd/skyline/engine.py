@@ -66,6 +66,7 @@ class SkylineEngine:
             check(lib().sky_ctx_set_semantics(self.h, _abi.SEM_COMPLETE))
         if grid_filter:   # GridDominanceFilter (FlinkSkyline.java:716-733)
             check(lib().sky_ctx_set_grid_filter(self.h, 1))
+        self.last_dist_stats = None      # set by skyline.dist.distributed_query
         self.K = self.P if not (self.algo == _abi.ALGO_GRID and semantics == "complete") else max(self.P, 1 << self.dims)
 
     def close(self):
@@ -121,6 +122,13 @@ class SkylineEngine:
         sv = np.zeros(max(k.value, 1), np.int64)
         check(lib().sky_global_stats(self.h, _ptr(ls), _ptr(sv), ctypes.byref(k)))
         return ls[:k.value], sv[:k.value]
+
+    def set_stats(self, local_sizes, survivors):
+        """Record job-wide |L_k| / survivors_k (the all-reduced per-rank shares of a
+        multi-GPU query) so that stats() returns them."""
+        ls = np.ascontiguousarray(local_sizes, np.int64)
+        sv = np.ascontiguousarray(survivors, np.int64)
+        check(lib().sky_global_stats_set(self.h, len(ls), _ptr(ls), _ptr(sv)))
 
     # ---- global merge of local lists ------------------------------------------------
     def global_merge(self, part_ids, ids_lists, values_lists):

@@ -128,6 +128,9 @@ int sky_global_merge(sky_ctx *ctx, int nparts, const int32_t *part_ids,
  * local_sizes[k] = |L_k|, survivors[k] = |G n L_k| for k < K
  * (K = P, or max(P, 2^D) for MR-Grid with SKY_SEM_COMPLETE). */
 int sky_global_stats(sky_ctx *ctx, int64_t *local_sizes, int64_t *survivors, int32_t *k_out);
+/* records job-wide integers (e.g. the all-reduced per-rank shares after sky_import_union_dev)
+ * so that sky_global_stats returns them until the next query */
+int sky_global_stats_set(sky_ctx *ctx, int32_t k, const int64_t *local_sizes, const int64_t *survivors);
 
 /* ---- fused whole-stream query --------------------------------------------- */
 /* keyBy -> per-key local skylines -> global merge, the trigger arriving after
@@ -167,9 +170,13 @@ int sky_export_local_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_val
 int sky_export_copy_dev(sky_ctx *ctx, double *d_rows_out, int32_t *d_keys_out,
                         int64_t *d_mult_out, int64_t cap);
 /* Phase 2: the all-gathered union of every rank's exported vectors (this rank's
- * own export starts at row self_offset); computes L_k (for stats) and G over the
- * union; writes this rank's global-skyline ids (stream order).  The shard buffers
- * passed to sky_export_local_dev must still be valid. */
+ * own export starts at row self_offset).  Each rank decides the fate of ITS OWN
+ * vectors only: v (key k) is in L_k iff no union vector of key k
+ * dominates it, and in G iff no union vector dominates it; the per-rank work is
+ * |own| x |union|, not a re-run over the whole union.  Writes this rank's global-
+ * skyline ids (stream order).  sky_global_stats afterwards returns THIS RANK'S SHARE
+ * of |L_k| and survivors_k: the caller sums them over the ranks (one all-reduce of
+ * 2K integers).  The shard buffers passed to sky_export_local_dev must still be valid. */
 int sky_import_union_dev(sky_ctx *ctx, const double *d_rows, const int32_t *d_keys,
                          const int64_t *d_mult, int64_t n_union, int64_t self_offset,
                          int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);

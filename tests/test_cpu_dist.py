@@ -1,11 +1,14 @@
-"""World-size-2 gloo test (CPU) of the multi-GPU exchange in skyline/dist.py.
+"""gloo tests (CPU, world sizes 2 and 4) of the multi-GPU exchange in skyline/dist.py.
 
-The device phases are stood in for by the oracle (test infrastructure): each
-rank reduces its shard to the distinct vectors of its local skylines with
-multiplicities, the ranks exchange them with skyline.dist.allgather_varlen /
-pack_export / unpack_union over gloo, and each rank finishes the union.  The
-result must equal the single-process answer (the decomposition the GPU path
-uses: SKY(u SKY(shard_r)) = SKY(u shard_r))."""
+The device phases are stood in for by the oracle (test infrastructure): each rank reduces
+its shard to the distinct vectors of its local skylines with partition + multiplicity
+(sky_export_local_dev), the ranks exchange them with skyline.dist.allgather_varlen /
+pack_export / unpack_union over gloo, each rank decides the fate of ITS OWN vectors
+against the union (sky_import_union_dev's rule: in L_k iff no union vector of key k
+dominates it, in G iff no union vector dominates it), and the per-rank shares of |L_k| /
+survivors_k are summed by skyline.dist.allreduce_stats.  The result must equal the
+single-process answer, and each rank's global-phase work must be its share (|own| x
+|union|, about 1/G of the |union|^2 a replicated merge would cost)."""
 import os
 import socket
 import sys
@@ -28,17 +31,16 @@ def _free_port():
 
 def _local_export(orc, vals, P):
     """distinct vectors of the local skylines of one shard, with partition + multiplicity"""
-    sky, keys, _, _ = orc.query_sfs("angle", vals, P)
-    inl = np.zeros(len(vals), bool)
-    # local skylines (all partitions): run per partition via 'complete' trick -> use SFS per key
-    for k in np.unique(keys):
-        idx = np.nonzero(keys == k)[0]
-        loc = orc.brute(vals[idx])
-        inl[idx[loc]] = True
+    _, keys, _, _, inl = orc.query_sfs_chunked("angle", vals, P)
+    inl = inl.astype(bool)
     rows = vals[inl]
     ks = keys[inl]
-    uniq, inv, cnt = np.unique(np.column_stack([ks, rows]), axis=0, return_inverse=True, return_counts=True)
+    uniq, cnt = np.unique(np.column_stack([ks, rows]), axis=0, return_counts=True)
     return uniq[:, 1:].copy(), uniq[:, 0].astype(np.int32), cnt.astype(np.int64)
+
+
+def _dominates(a, b):
+    return bool((a <= b).all() and (a < b).any())
 
 
 def _worker(rank, world, port, shards, P, D, ret):
@@ -46,7 +48,7 @@ def _worker(rank, world, port, shards, P, D, ret):
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "flink-skyline-qos_amd"))
     import torch.distributed as dist
     from conftest import Oracle
-    from skyline.dist import allgather_varlen, pack_export, unpack_union
+    from skyline.dist import allgather_varlen, allreduce_stats, pack_export, unpack_union
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     orc = Oracle()
     rows, keys, mult = _local_export(orc, shards[rank], P)
@@ -54,36 +56,60 @@ def _worker(rank, world, port, shards, P, D, ret):
     gathered, counts = allgather_varlen(packed)
     urows, ukeys, umult = unpack_union(gathered, counts, D)
     assert sum(counts) == urows.shape[0]
-    assert torch.equal(urows[sum(counts[:rank]):sum(counts[:rank]) + counts[rank]], torch.from_numpy(rows))
-    # finish on the union: global skyline vectors and their total multiplicity
-    u = urows.numpy()
-    g = orc.brute(u)
-    gset = {tuple(r) for r in u[g]}
-    total = int(umult.numpy()[g].sum())
-    ret[rank] = (sorted(gset), total)
+    off = sum(counts[:rank])
+    assert torch.equal(urows[off:off + counts[rank]], torch.from_numpy(rows))
+    u, uk = urows.numpy(), ukeys.numpy()
+    ls = np.zeros(P, np.int64)
+    sv = np.zeros(P, np.int64)
+    gvecs = []
+    pairs = 0
+    for j in range(counts[rank]):               # own vectors only, each against the whole union
+        y, ky = u[off + j], uk[off + j]
+        dom_l = dom_g = False
+        for i in range(len(u)):
+            pairs += 1
+            if _dominates(u[i], y):
+                dom_g = True
+                if uk[i] == ky:
+                    dom_l = True
+                    break
+        if not dom_l:
+            ls[ky] += mult[j]
+        if not dom_g:
+            sv[ky] += mult[j]
+            gvecs.append(tuple(y))
+    tls, tsv = allreduce_stats(ls, sv, torch.device("cpu"))
+    ret[rank] = (sorted(gvecs), tls.tolist(), tsv.tolist(), pairs, len(u))
     dist.destroy_process_group()
 
 
-def test_two_rank_exchange_equals_single_process(oracle):
-    n, D, P = 6000, 4, 8
-    vals = oracle.synth(2, D, n, seed=3)
-    shards = [vals[: n // 2], vals[n // 2:]]
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_exchange_equals_single_process(world, oracle):
+    n, D, P = 8000, 4, 8
+    vals = oracle.synth(0, D, n, seed=3 + world)
+    bounds = np.linspace(0, n, world + 1).astype(int)
+    shards = [vals[bounds[r]:bounds[r + 1]] for r in range(world)]
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     ret = mgr.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, shards, P, D, ret)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, P, D, ret)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(180)
         assert p.exitcode == 0
-    exp = oracle.brute(vals)
+    exp, keys, els, esv = oracle.query_sfs("angle", vals, P)
     exp_set = sorted({tuple(r) for r in vals[exp]})
-    for r in range(2):
-        got_set, total = ret[r]
-        assert got_set == exp_set
-        assert total == len(exp)          # every skyline tuple counted exactly once
+    got_set = sorted({v for r in range(world) for v in ret[r][0]})
+    assert got_set == exp_set
+    n_union = ret[0][4]
+    for r in range(world):
+        assert ret[r][1] == els.tolist()          # job-wide integers after the all-reduce
+        assert ret[r][2] == esv.tolist()
+        # global-phase work of one rank: its own vectors against the union, ~1/G of |U|^2
+        assert ret[r][3] <= 1.6 * n_union * n_union / world
+    assert sum(ret[r][3] for r in range(world)) <= n_union * n_union
 
 
 def test_pack_unpack_roundtrip():

@@ -189,6 +189,7 @@ def test_c3_angle_4d_anti_50m_one_gpu_and_sharded(gpu_engine_factory, oracle):
         ukeys = torch.cat([x[1] for x in exports]).contiguous()
         umult = torch.cat([x[2] for x in exports]).contiguous()
         off, ids_all, org_all = 0, [], []
+        tot_ls, tot_sv = np.zeros_like(got[2]), np.zeros_like(got[3])
         for r, e in enumerate(engs):
             lo, hi = int(bounds[r]), int(bounds[r + 1])
             oi = torch.empty(hi - lo, dtype=torch.int64, device="cuda")
@@ -197,11 +198,13 @@ def test_c3_angle_4d_anti_50m_one_gpu_and_sharded(gpu_engine_factory, oracle):
             e.sync()
             ids_all.append(oi[:g].cpu().numpy())
             org_all.append(oo[:g].cpu().numpy())
-            ls, sv = e.stats()
-            np.testing.assert_array_equal(ls, got[2])
-            np.testing.assert_array_equal(sv, got[3])
+            ls, sv = e.stats()                   # this rank's share of the optimality integers
+            tot_ls += ls
+            tot_sv += sv
             off += exports[r][0].shape[0]
             e.close()
+        np.testing.assert_array_equal(tot_ls, got[2])
+        np.testing.assert_array_equal(tot_sv, got[3])
         np.testing.assert_array_equal(np.concatenate(ids_all), got[0])
         np.testing.assert_array_equal(np.concatenate(org_all), got[1])
     del dv, di

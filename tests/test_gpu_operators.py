@@ -124,6 +124,7 @@ def test_multi_rank_decomposition(gpu_engine_factory, oracle):
     assert int(umult.sum()) <= n
     got = []
     off = 0
+    tot_ls, tot_sv = np.zeros_like(exp_ls), np.zeros_like(exp_sv)
     for r, (e, s) in enumerate(zip(engs, shards)):
         oi = torch.empty(len(s), dtype=torch.int64, device="cuda")
         oo = torch.empty(len(s), dtype=torch.int32, device="cuda")
@@ -131,9 +132,11 @@ def test_multi_rank_decomposition(gpu_engine_factory, oracle):
         e.sync()
         got.append((oi[:g].cpu().numpy(), oo[:g].cpu().numpy()))
         off += exports[r][0].shape[0]
-        ls, sv = e.stats()
-        np.testing.assert_array_equal(ls, exp_ls)
-        np.testing.assert_array_equal(sv, exp_sv)
+        ls, sv = e.stats()                       # this rank's share: summed over the ranks
+        tot_ls += ls
+        tot_sv += sv
+    np.testing.assert_array_equal(tot_ls, exp_ls)
+    np.testing.assert_array_equal(tot_sv, exp_sv)
     gi = np.concatenate([x[0] for x in got])
     go = np.concatenate([x[1] for x in got])
     np.testing.assert_array_equal(gi, exp_ids)
