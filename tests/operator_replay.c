@@ -1,0 +1,214 @@
+/*
+ * tests/operator_replay.c — a C caller of libskyline_hip.so that replays the reference
+ * operators' call sequence, the way the JNI shim (jni/skyline_hip_jni.c) drives the library
+ * from the Java operators.  Run by tests/test_gpu_replay.py on the golden streams.
+ *
+ *   input     the producers' payload "id,v1,...,vD\n" (python/unified_producer.py:174), read
+ *             from a file and decoded on the device: sky_parse_csv
+ *             (.map(ServiceTuple::fromString).filter(nonNull), FlinkSkyline.java:102-104)
+ *   keyBy     sky_partition_keys (getKey, FlinkSkyline.java:138, :707-712/:774-789/:827-875)
+ *   local     SkylineLocalProcessor: per key, buffer 5000 tuples then sky_part_insert
+ *             (processElement1 + processBuffer, :265-316, :417-444); a trigger "q,N" after the
+ *             last tuple: per key 0..P-1 flush + sky_part_snapshot (processQuery, :367-404)
+ *   global    GlobalSkylineAggregator: sky_global_merge over the P lists + sky_global_stats
+ *             (:515-608), then the JSON payload of :631-648 plus "query_latency_ms"
+ *
+ * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain]
+ * stdout: the JSON line, then "ids" and the sorted global skyline ids, then "lsz" / "surv".
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "skyline_hip.h"
+
+#define BUFFER_SIZE 5000   /* FlinkSkyline.java:232 */
+
+static void die(const char *what, int rc) {
+    fprintf(stderr, "%s failed: status %d: %s\n", what, rc, sky_last_error());
+    exit(1);
+}
+#define CHECK(call)                       \
+    do {                                  \
+        int rc_ = (call);                 \
+        if (rc_ != SKY_OK) die(#call, rc_); \
+    } while (0)
+
+static int64_t now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    return (int64_t)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
+/* String.format(Locale.US, "%.4f", x): Java rounds HALF_UP on the shortest decimal string
+ * that reads back as x (FormattedFloatingDecimal); x in [0, 1] here. */
+static void java_format_4f(double x, char *out, size_t cap) {
+    char s[64];
+    for (int p = 1; p <= 17; p++) {   /* shortest %e string that reads back as x */
+        snprintf(s, sizeof s, "%.*e", p - 1, x);
+        if (strtod(s, NULL) == x) break;
+    }
+    char dg[32];
+    int nd = 0;
+    const char *c = s;
+    for (; *c && *c != 'e'; c++)
+        if (*c >= '0' && *c <= '9') dg[nd++] = *c;
+    const int e = atoi(c + 1);   /* x = d0.d1d2... x 10^e, x >= 0 */
+    long long ip = 0;
+    int fr[6] = {0};             /* fr[j]: digit of 10^-j */
+    for (int pw = e; pw >= 0; pw--) {
+        const int i = e - pw;
+        ip = ip * 10 + (i < nd ? dg[i] - '0' : 0);
+    }
+    for (int i = 0; i < nd; i++) {
+        const int pw = e - i;
+        if (pw < 0 && pw >= -5) fr[-pw] = dg[i] - '0';
+    }
+    int f4 = fr[1] * 1000 + fr[2] * 100 + fr[3] * 10 + fr[4];
+    if (fr[5] >= 5 && ++f4 == 10000) {   /* HALF_UP: the discarded part is >= half a unit */
+        f4 = 0;
+        ip++;
+    }
+    snprintf(out, cap, "%lld.%04d", ip, f4);
+}
+
+typedef struct {
+    int32_t key;
+    sky_part *part;
+    int64_t *ids;
+    double *vals;
+    int64_t n;
+} keyed_state;
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && strcmp(argv[1], "--fmt") == 0) {   /* formatter self-check (no device) */
+        for (int i = 2; i < argc; i++) {
+            char o[64];
+            java_format_4f(strtod(argv[i], NULL), o, sizeof o);
+            printf("%s\n", o);
+        }
+        return 0;
+    }
+    if (argc < 5) {
+        fprintf(stderr, "usage: %s <csv> <dims> <parallelism> <algo> [domain]\n", argv[0]);
+        return 2;
+    }
+    const int D = atoi(argv[2]), par = atoi(argv[3]), algo = atoi(argv[4]);
+    const double domain = argc > 5 ? atof(argv[5]) : 1000.0;
+    const int P = 2 * par;   /* FlinkSkyline.java:76 */
+    FILE *f = fopen(argv[1], "rb");
+    if (!f) { perror("open"); return 2; }
+    fseek(f, 0, SEEK_END);
+    const long nbytes = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char *text = (char *)malloc((size_t)nbytes + 1);
+    if (fread(text, 1, (size_t)nbytes, f) != (size_t)nbytes) { perror("read"); return 2; }
+    fclose(f);
+
+    int dev = 0;
+    sky_ctx *ctx = NULL;
+    CHECK(sky_ctx_create(&dev, 1, D, P, algo, domain, &ctx));
+    const int64_t rmax = nbytes / 2 + 1;
+    int64_t *ids = (int64_t *)malloc((size_t)rmax * 8);
+    double *vals = (double *)malloc((size_t)rmax * D * 8);
+    int64_t n = 0, counts[4] = {0};
+    CHECK(sky_parse_csv(ctx, text, nbytes, ids, vals, rmax, &n, counts));
+    if (counts[SKY_CSV_BAD_ID]) { fprintf(stderr, "NumberFormatException\n"); return 3; }
+    int32_t *keys = (int32_t *)malloc((size_t)(n > 0 ? n : 1) * 4);
+    CHECK(sky_partition_keys(ctx, vals, n, keys));
+
+    /* keyed state: every key that receives a tuple (MR-Grid keys may exceed P) */
+    int kmax = P;
+    for (int64_t i = 0; i < n; i++)
+        if (keys[i] + 1 > kmax) kmax = keys[i] + 1;
+    keyed_state *ks = (keyed_state *)calloc((size_t)kmax, sizeof(keyed_state));
+    for (int k = 0; k < kmax; k++) {
+        ks[k].key = k;
+        ks[k].ids = (int64_t *)malloc(BUFFER_SIZE * 8);
+        ks[k].vals = (double *)malloc((size_t)BUFFER_SIZE * D * 8);
+        CHECK(sky_part_open(ctx, k, &ks[k].part));
+    }
+    /* processElement1: buffer, flush through processBuffer at BUFFER_SIZE */
+    for (int64_t i = 0; i < n; i++) {
+        const int k = keys[i];
+        if (k < 0) continue;   /* removed by the (optional) grid dominance filter */
+        keyed_state *s = &ks[k];
+        s->ids[s->n] = ids[i];
+        memcpy(s->vals + s->n * D, vals + i * D, (size_t)D * 8);
+        if (++s->n == BUFFER_SIZE) {
+            CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
+            s->n = 0;
+        }
+    }
+    /* trigger "1,N" after the last tuple, broadcast to keys 0..P-1 (:145-157) */
+    const int64_t dispatch = now_ms();
+    int32_t *part_ids = (int32_t *)malloc((size_t)P * 4);
+    int64_t **lid = (int64_t **)malloc((size_t)P * sizeof(int64_t *));
+    double **lval = (double **)malloc((size_t)P * sizeof(double *));
+    int64_t *lcnt = (int64_t *)malloc((size_t)P * 8);
+    int64_t total = 0;
+    for (int k = 0; k < P; k++) {   /* processQuery: flush, then the local skyline snapshot */
+        keyed_state *s = &ks[k];
+        if (s->n) {
+            CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
+            s->n = 0;
+        }
+        int64_t m = 0;
+        int rc = sky_part_snapshot(s->part, NULL, NULL, 0, &m);
+        if (rc != SKY_OK && rc != SKY_E_CAPACITY) die("sky_part_snapshot (size)", rc);
+        lid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+        lval[k] = (double *)malloc((size_t)(m > 0 ? m : 1) * D * 8);
+        CHECK(sky_part_snapshot(s->part, lid[k], lval[k], m, &m));
+        part_ids[k] = k;
+        lcnt[k] = m;
+        total += m;
+    }
+    /* GlobalSkylineAggregator: merge on the last arrival, optimality integers */
+    int64_t *gids = (int64_t *)malloc((size_t)(total > 0 ? total : 1) * 8);
+    int32_t *gorg = (int32_t *)malloc((size_t)(total > 0 ? total : 1) * 4);
+    int64_t g = 0;
+    CHECK(sky_global_merge(ctx, P, part_ids, (const int64_t *const *)lid, (const double *const *)lval, lcnt, gids,
+                           gorg, total, &g));
+    int64_t *lsz = (int64_t *)malloc((size_t)P * 8), *surv = (int64_t *)malloc((size_t)P * 8);
+    int32_t K = 0;
+    CHECK(sky_global_stats(ctx, lsz, surv, &K));
+    const int64_t finish = now_ms();
+    double opt = 0.0;
+    for (int k = 0; k < P; k++)
+        if (lsz[k] > 0) opt += (double)surv[k] / (double)lsz[k];
+    opt /= P;
+    char ostr[64];
+    java_format_4f(opt, ostr, sizeof ostr);
+    printf("{\"query_id\": \"1\", \"record_count\": %lld, \"skyline_size\": %lld, \"optimality\": %s, "
+           "\"ingestion_time_ms\": 0, \"local_processing_time_ms\": 0, \"global_processing_time_ms\": %lld, "
+           "\"total_processing_time_ms\": %lld, \"query_latency_ms\": %lld}\n",
+           (long long)n, (long long)g, ostr, (long long)(finish - dispatch), (long long)(finish - dispatch),
+           (long long)(finish - dispatch));
+    /* sorted global ids (insertion sort is enough for golden sizes; qsort otherwise) */
+    int cmp_i64(const void *a, const void *b);
+    qsort(gids, (size_t)g, 8, cmp_i64);
+    printf("ids");
+    for (int64_t j = 0; j < g; j++) printf(" %lld", (long long)gids[j]);
+    printf("\nlsz");
+    for (int k = 0; k < P; k++) printf(" %lld", (long long)lsz[k]);
+    printf("\nsurv");
+    for (int k = 0; k < P; k++) printf(" %lld", (long long)surv[k]);
+    printf("\n");
+    for (int k = 0; k < kmax; k++) {
+        CHECK(sky_part_close(ks[k].part));
+        free(ks[k].ids);
+        free(ks[k].vals);
+    }
+    for (int k = 0; k < P; k++) { free(lid[k]); free(lval[k]); }
+    CHECK(sky_ctx_destroy(ctx));
+    free(ks); free(lid); free(lval); free(lcnt); free(part_ids); free(gids); free(gorg); free(lsz); free(surv);
+    free(keys); free(ids); free(vals); free(text);
+    return 0;
+}
+
+int cmp_i64(const void *a, const void *b) {
+    const int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+    return x < y ? -1 : x > y;
+}

@@ -241,3 +241,21 @@ def test_chunked_oracle_edge_values(oracle):
                 np.testing.assert_array_equal(sv, esv)
         bnl, _, bls, bsv = oracle.query_bnl(algo, vals, ids, 8)
         np.testing.assert_array_equal(np.sort(bnl), oracle.query_sfs_chunked(algo, vals, 8, chunk=777)[0])
+
+
+def test_c_replay_formats_optimality_like_java():
+    """tests/operator_replay.c formats optimality as String.format(Locale.US, "%.4f", x):
+    HALF_UP on the shortest repr (not C's round-half-even on the binary value)."""
+    import subprocess
+    from skyline.operators import java_format_4f
+    binp = os.path.join(os.path.dirname(GOLDEN), "..", "flink-skyline-qos_amd", "build", "operator_replay")
+    if not os.path.exists(binp):
+        pytest.skip("operator_replay not built")
+    xs = [0.0, 1.0, 0.25, 1 / 3, 2 / 3, 0.00005, 0.00015, 0.12345, 0.99995, 0.999949999, 0.7379, 0.5415,
+          0.000049999999, 1e-9, 0.0625 + 1e-12, 0.1 + 0.2]
+    rng = np.random.default_rng(1)
+    xs += [float(x) for x in rng.random(300)]
+    xs += [k / 10000 + 0.00005 for k in range(0, 10000, 97)]
+    out = subprocess.run([binp, "--fmt"] + [repr(x) for x in xs], capture_output=True, text=True, check=True)
+    got = out.stdout.split()
+    assert got == [java_format_4f(x) for x in xs]
