@@ -1,0 +1,283 @@
+package org.main;
+
+import org.apache.flink.api.common.state.ListState;
+import org.apache.flink.api.common.state.ListStateDescriptor;
+import org.apache.flink.api.common.state.ValueState;
+import org.apache.flink.api.common.state.ValueStateDescriptor;
+import org.apache.flink.api.common.typeinfo.TypeHint;
+import org.apache.flink.api.common.typeinfo.TypeInformation;
+import org.apache.flink.api.java.tuple.Tuple3;
+import org.apache.flink.api.java.tuple.Tuple6;
+import org.apache.flink.configuration.Configuration;
+import org.apache.flink.streaming.api.functions.KeyedProcessFunction;
+import org.apache.flink.streaming.api.functions.co.KeyedCoProcessFunction;
+import org.apache.flink.util.Collector;
+
+import java.util.ArrayList;
+import java.util.HashMap;
+import java.util.List;
+import java.util.Locale;
+import java.util.Map;
+
+/**
+ * Drop-in replacements for the two hot-path operators of FlinkSkyline.java, running their
+ * dominance work in libskyline_hip.so on the MI355X (through SkylineHip / JNI).
+ *
+ * Topology change in FlinkSkyline.main (:162-176):
+ *   keyedData.connect(keyedTriggers).process(new HipSkylineOperators.LocalProcessor(dims, P, algo, domain))
+ *   ...keyBy(t -> t.f1).process(new HipSkylineOperators.GlobalAggregator(P, dims, algo, domain))
+ * Everything else (Kafka source and sink, fromString, the partitioners, the trigger
+ * broadcast) is unchanged.  Not compiled in the build container (no JDK); the identical C
+ * call sequence runs in tests/operator_replay.c on the GPU box.
+ *
+ * Deliberate differences from the reference (DESIGN.md §5): the input buffer is per key (the
+ * reference's is shared by a subtask's keys, :223,244); NaN values fail the task
+ * (ArithmeticException); the JSON adds "query_latency_ms" (computed at :588, never emitted).
+ */
+public final class HipSkylineOperators {
+    private HipSkylineOperators() {}
+
+    static final int BUFFER_SIZE = 5000;   // FlinkSkyline.java:232
+
+    /** Per-key tuple buffer flattened for one JNI call. */
+    static final class KeyBuffer {
+        final long[] ids = new long[BUFFER_SIZE];
+        final double[] values;
+        final int dims;
+        int n;
+
+        KeyBuffer(int dims) {
+            this.dims = dims;
+            this.values = new double[BUFFER_SIZE * dims];
+        }
+
+        boolean add(long id, double[] v) {
+            ids[n] = id;
+            System.arraycopy(v, 0, values, n * dims, dims);
+            return ++n == BUFFER_SIZE;
+        }
+    }
+
+    /**
+     * SkylineLocalProcessor (FlinkSkyline.java:214-445) with the per-key skyline held on the
+     * device: processBuffer's BNL (:417-444) is sky_part_insert on a micro-batch; processQuery's
+     * snapshot (:387-392) is sky_part_snapshot.  The id barrier (:276-356) is unchanged.
+     */
+    public static class LocalProcessor extends KeyedCoProcessFunction<Integer, ServiceTuple,
+            Tuple3<Integer, String, Long>, Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> {
+        private final int dims, partitions, algo;
+        private final double domain;
+        private transient long ctx;
+        private transient Map<Integer, Long> parts;          // key -> sky_part handle
+        private transient Map<Integer, KeyBuffer> buffers;   // key -> pending tuples
+        private transient ValueState<Long> maxSeenIdState;
+        private transient ListState<Tuple3<Integer, String, Long>> pendingQueriesState;
+        private transient ValueState<Long> startTimeState;
+        private transient ValueState<Long> accumulatedCpuNanosState;
+
+        public LocalProcessor(int dims, int partitions, String algo, double domain) {
+            this.dims = dims;
+            this.partitions = partitions;
+            this.algo = SkylineHip.algoOf(algo);
+            this.domain = domain;
+        }
+
+        @Override
+        public void open(Configuration config) {
+            ctx = SkylineHip.ctxCreate(0, dims, partitions, algo, domain);
+            parts = new HashMap<>();
+            buffers = new HashMap<>();
+            maxSeenIdState = getRuntimeContext().getState(new ValueStateDescriptor<>("maxId", Long.class));
+            pendingQueriesState = getRuntimeContext().getListState(new ListStateDescriptor<>("pendingQs",
+                    TypeInformation.of(new TypeHint<Tuple3<Integer, String, Long>>() {})));
+            startTimeState = getRuntimeContext().getState(new ValueStateDescriptor<>("jobStartTime", Long.class));
+            accumulatedCpuNanosState = getRuntimeContext().getState(new ValueStateDescriptor<>("cpuTime", Long.class));
+        }
+
+        @Override
+        public void close() {   // the reference has no close(); device state is released here
+            for (long p : parts.values()) SkylineHip.partClose(p);
+            parts.clear();
+            if (ctx != 0) SkylineHip.ctxDestroy(ctx);
+            ctx = 0;
+        }
+
+        private long part(int key) {
+            return parts.computeIfAbsent(key, k -> SkylineHip.partOpen(ctx, k));
+        }
+
+        private void flush(int key) {
+            KeyBuffer b = buffers.get(key);
+            if (b != null && b.n > 0) {
+                SkylineHip.partInsert(part(key), b.ids, b.values, b.n);   // S <- SKY(S u buffer)
+                b.n = 0;
+            }
+        }
+
+        private static long required(Tuple3<Integer, String, Long> q) {
+            String[] parts = q.f1.split(",");
+            return parts.length > 1 ? Long.parseLong(parts[1].trim()) : 0L;
+        }
+
+        private void addCpu(long startNano) throws Exception {
+            Long acc = accumulatedCpuNanosState.value();
+            accumulatedCpuNanosState.update((acc == null ? 0L : acc) + (System.nanoTime() - startNano));
+        }
+
+        @Override
+        public void processElement1(ServiceTuple point, Context c,
+                                    Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                throws Exception {
+            final long startNano = System.nanoTime();
+            final int key = c.getCurrentKey();
+            if (startTimeState.value() == null) startTimeState.update(System.currentTimeMillis());
+            final long id = Long.parseLong(point.id);                // throws as the reference does (:276)
+            Long maxId = maxSeenIdState.value();
+            if (maxId == null || id > maxId) {
+                maxSeenIdState.update(id);
+                maxId = id;
+            }
+            if (buffers.computeIfAbsent(key, k -> new KeyBuffer(dims)).add(id, point.values)) flush(key);
+            addCpu(startNano);
+            List<Tuple3<Integer, String, Long>> remaining = new ArrayList<>();
+            boolean released = false;
+            for (Tuple3<Integer, String, Long> q : pendingQueriesState.get()) {
+                if (maxId >= required(q)) {
+                    processQuery(q, key, out);
+                    released = true;
+                } else {
+                    remaining.add(q);
+                }
+            }
+            if (released) pendingQueriesState.update(remaining);
+        }
+
+        @Override
+        public void processElement2(Tuple3<Integer, String, Long> trigger, Context c,
+                                    Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                throws Exception {
+            Long current = maxSeenIdState.value();
+            long cur = current == null ? -1L : current;
+            if (cur >= required(trigger) || cur == -1L) processQuery(trigger, c.getCurrentKey(), out);
+            else pendingQueriesState.add(trigger);
+        }
+
+        private void processQuery(Tuple3<Integer, String, Long> trigger, int key,
+                                  Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                throws Exception {
+            final long startNano = System.nanoTime();
+            flush(key);
+            final long p = part(key);
+            int n = (int) SkylineHip.partSize(p);
+            long[] ids = new long[n];
+            double[] vals = new double[n * dims];
+            n = SkylineHip.partSnapshot(p, ids, vals);
+            addCpu(startNano);
+            List<ServiceTuple> sky = new ArrayList<>(n);
+            for (int i = 0; i < n; i++) {
+                double[] v = new double[dims];
+                System.arraycopy(vals, i * dims, v, 0, dims);
+                ServiceTuple t = new ServiceTuple(Long.toString(ids[i]), v);
+                t.originPartition = key;
+                sky.add(t);
+            }
+            Long start = startTimeState.value();
+            Long cpu = accumulatedCpuNanosState.value();
+            out.collect(new Tuple6<>(trigger.f0, trigger.f1, trigger.f2,
+                    start == null ? System.currentTimeMillis() : start, sky, cpu == null ? 0L : cpu / 1_000_000L));
+        }
+    }
+
+    /**
+     * GlobalSkylineAggregator (FlinkSkyline.java:460-660): collects the P local skylines of one
+     * query, then ONE sky_global_merge (the BNL merge of :548-566) and sky_global_stats (the
+     * optimality integers of :593-608) on the last arrival, and the JSON payload of :631-648.
+     */
+    public static class GlobalAggregator extends KeyedProcessFunction<String,
+            Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>, String> {
+        private final int totalPartitions, dims, algo;
+        private final double domain;
+        private transient long ctx;
+        private transient ValueState<List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>> arrived;
+        private transient ValueState<Long> minStartTimeState;
+
+        public GlobalAggregator(int totalPartitions, int dims, String algo, double domain) {
+            this.totalPartitions = totalPartitions;
+            this.dims = dims;
+            this.algo = SkylineHip.algoOf(algo);
+            this.domain = domain;
+        }
+
+        @Override
+        public void open(Configuration config) {
+            ctx = SkylineHip.ctxCreate(0, dims, totalPartitions, algo, domain);
+            arrived = getRuntimeContext().getState(new ValueStateDescriptor<>("arrived",
+                    TypeInformation.of(new TypeHint<List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>>() {})));
+            minStartTimeState = getRuntimeContext().getState(new ValueStateDescriptor<>("minStart", Long.class));
+        }
+
+        @Override
+        public void close() {
+            if (ctx != 0) SkylineHip.ctxDestroy(ctx);
+            ctx = 0;
+        }
+
+        @Override
+        public void processElement(Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long> in, Context c,
+                                   Collector<String> out) throws Exception {
+            Long minStart = minStartTimeState.value();
+            if (minStart == null || in.f3 < minStart) minStartTimeState.update(in.f3);
+            List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> lists = arrived.value();
+            if (lists == null) lists = new ArrayList<>();
+            lists.add(in);
+            if (lists.size() < totalPartitions) {
+                arrived.update(lists);
+                return;
+            }
+            final long lastArrival = System.currentTimeMillis();
+            final int np = lists.size();
+            int[] partIds = new int[np];
+            long[][] ids = new long[np][];
+            double[][] vals = new double[np][];
+            long maxCpu = 0;
+            int total = 0;
+            for (int k = 0; k < np; k++) {
+                Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long> t = lists.get(k);
+                partIds[k] = t.f0;
+                List<ServiceTuple> l = t.f4;
+                ids[k] = new long[l.size()];
+                vals[k] = new double[l.size() * dims];
+                for (int i = 0; i < l.size(); i++) {
+                    ids[k][i] = Long.parseLong(l.get(i).id);
+                    System.arraycopy(l.get(i).values, 0, vals[k], i * dims, dims);
+                }
+                total += l.size();
+                maxCpu = Math.max(maxCpu, t.f5);
+            }
+            long[] gids = new long[Math.max(total, 1)];
+            int[] gorg = new int[Math.max(total, 1)];
+            final int g = SkylineHip.globalMerge(ctx, partIds, ids, vals, gids, gorg);
+            long[] lsz = new long[np], surv = new long[np];
+            SkylineHip.globalStats(ctx, lsz, surv);           // indexed by list, like partIds
+            double sum = 0.0;
+            for (int k = 0; k < np; k++)
+                if (partIds[k] < totalPartitions && lsz[k] > 0) sum += (double) surv[k] / lsz[k];
+            final double optimality = sum / totalPartitions;
+            final long finish = System.currentTimeMillis();
+            final long jobStart = minStartTimeState.value();
+            final long mapWall = lastArrival - jobStart;
+            final long ingest = Math.max(0, mapWall - maxCpu);
+            String[] payload = in.f1.split(",");
+            String records = payload.length > 1 ? payload[1].trim() : "unknown";
+            out.collect("{\"query_id\": \"" + payload[0].trim() + "\", \"record_count\": " + records
+                    + ", \"skyline_size\": " + g
+                    + ", \"optimality\": " + String.format(Locale.US, "%.4f", optimality)
+                    + ", \"ingestion_time_ms\": " + ingest
+                    + ", \"local_processing_time_ms\": " + maxCpu
+                    + ", \"global_processing_time_ms\": " + (finish - lastArrival)
+                    + ", \"total_processing_time_ms\": " + (finish - jobStart)
+                    + ", \"query_latency_ms\": " + (finish - in.f2) + "}");
+            arrived.clear();   // minStart survives, as in the reference (:653-657)
+        }
+    }
+}

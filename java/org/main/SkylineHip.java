@@ -1,0 +1,60 @@
+package org.main;
+
+/**
+ * JNI entry points of libskyline_hip.so (include/skyline_hip.h, via jni/skyline_hip_jni.c).
+ *
+ * Not compiled in the build container (no JDK there); the same call sequence is exercised by
+ * tests/operator_replay.c (C) and by the Python binding (flink-skyline-qos_amd/skyline/).
+ *
+ * Handles are opaque longs.  Arrays: ids long[n], values double[n * dims] row-major.
+ * Failures throw RuntimeException(sky_last_error()); a NaN value throws ArithmeticException.
+ * Methods returning an int count return -required when an output array is too small.
+ */
+public final class SkylineHip {
+    static {
+        System.loadLibrary("skyline_hip_jni");   // links libskyline_hip.so
+    }
+
+    private SkylineHip() {}
+
+    /** FlinkSkyline.main --algo values (FlinkSkyline.java:112-134). */
+    public static final int ALGO_DIM = 0, ALGO_GRID = 1, ALGO_ANGLE = 2;
+    public static final int SEM_REFERENCE = 0, SEM_COMPLETE = 1;
+    public static final int CSV_MALFORMED = 1, CSV_BAD_ID = 2, CSV_ARITY = 3;
+
+    public static int algoOf(String flag) {
+        switch (flag.toLowerCase()) {
+            case "mr-dim": return ALGO_DIM;
+            case "mr-grid": return ALGO_GRID;
+            default: return ALGO_ANGLE;            // the reference's default branch
+        }
+    }
+
+    public static native long ctxCreate(int device, int dims, int partitions, int algo, double domain);
+    public static native void ctxDestroy(long ctx);
+    public static native void ctxSetSemantics(long ctx, int semantics);
+    public static native void ctxSetGridFilter(long ctx, boolean on);
+
+    public static native void partitionKeys(long ctx, double[] values, int n, int[] keysOut);
+
+    public static native long partOpen(long ctx, int key);
+    public static native void partClose(long part);
+    public static native void partInsert(long part, long[] ids, double[] values, int n);
+    public static native long partSize(long part);
+    public static native int partSnapshot(long part, long[] idsOut, double[] valuesOut);
+
+    public static native int globalMerge(long ctx, int[] partIds, long[][] ids, double[][] values,
+                                         long[] idsOut, int[] originOut);
+    public static native int globalStats(long ctx, long[] localSizes, long[] survivors);
+
+    public static native int query(long ctx, long[] ids, double[] values, int n, long[] idsOut, int[] originOut);
+
+    public static native int parseCsv(long ctx, byte[] text, int nbytes, long[] idsOut, double[] valuesOut,
+                                      long[] countsOut);
+
+    public static native long streamCreate(long ctx, long window);
+    public static native void streamDestroy(long stream);
+    public static native void streamAppend(long stream, long[] ids, double[] values, int n);
+    public static native int streamQuery(long stream, long[] idsOut, int[] originOut);
+    public static native long streamResident(long stream);
+}
