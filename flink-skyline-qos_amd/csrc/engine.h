@@ -67,12 +67,14 @@ struct Pipe {
     // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers
     DevBuf r16, r16g, r16a, r16b, i16a, i16b, dead16, keep16, scan16, xbuf16, xcnt16, xseg16, items16, at16, atv16;
     DevBuf scratch, flags, totals, orand, lsz, surv, statk, segalive;
+    // candidate prefilter (second-level pruners) and its compaction targets
+    DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2;
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;
 
     // results of the last run
-    uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0;
+    uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0, mt_pre = 0;
     int M = 1, Kp = 1, K = 1;
     bool f64 = false, ties = false, u16 = false;
     std::vector<uint32_t> h_dup;

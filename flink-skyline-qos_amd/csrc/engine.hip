@@ -119,6 +119,12 @@ static bool sfs16_disabled() {
     const char *e = getenv("SKY_SFS16");
     return e && atoi(e) == 0;
 }
+// SKY_PREFILTER=0 skips the candidate prefilter (A/B knob; read per query)
+static bool prefilter_disabled() {
+    const char *e = getenv("SKY_PREFILTER");
+    return e && atoi(e) == 0;
+}
+constexpr uint32_t kPrefilterMin = 4096;   // fewer slots: the SFS runs in one small pass anyway
 // SKY_GATHER=0 reads counters back by one hipMemcpyAsync per range (A/B knob)
 static bool gather_disabled() {
     const char *e = getenv("SKY_GATHER");
@@ -635,6 +641,53 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.ties = (flags & kFlagScoreTies) != 0;
     p.u16 = !p.f64 && !p.ties && (flags & kFlagNotU16) == 0 && !sfs16_disabled();
     p.mt = m + nps;
+    p.mt_pre = p.mt;
+    // ---- candidate prefilter: second-level pruners drawn from the candidates drop the
+    //      candidates they dominate before the sort (worth it once the candidates
+    //      outnumber what one small-SFS workgroup per partition handles)
+    if (p.mt >= kPrefilterMin && !prefilter_disabled()) {
+        const uint32_t mt0 = p.mt;
+        const int M2 = std::min(32, 2048 / p.Kp);
+        const int KM2 = p.Kp * M2;
+        const int KM = p.Kp * p.M;
+        SKY_TRY(p.cmin.ensure((size_t)KM2 * 8));
+        SKY_TRY(p.pr2.ensure((size_t)KM2 * D * 8));
+        SKY_TRY(p.npr2.ensure((size_t)p.Kp * 4));
+        SKY_TRY(p.live.ensure((size_t)mt0 * 4));
+        SKY_TRY(p.livepos.ensure((size_t)(mt0 + 1) * 4));
+        SKY_TRY(p.rows2.ensure((size_t)mt0 * rb64));
+        SKY_TRY(p.sortkey2.ensure((size_t)mt0 * 8));
+        SKY_TRY(p.slot_src2.ensure((size_t)mt0 * 4));
+        SKY_TRY(p.scratch.ensure(scan_scratch_words(mt0 + 1) * 4 + 64));
+        fill.add(p.cmin.p, (size_t)KM2 * 8, 0xff);
+        HIP_TRY(fill.launch(st));
+        CandArgs ca{};
+        ca.mt = mt0;
+        ca.rows = p.rows.as<double>();
+        ca.key = p.sortkey.as<uint64_t>();
+        ca.src = p.slot_src.as<uint32_t>();
+        ca.Kp = p.Kp;
+        ca.M2 = M2;
+        ca.cmin = p.cmin.as<unsigned long long>();
+        ca.pr2 = p.pr2.as<double>();
+        ca.npr2 = p.npr2.as<int32_t>();
+        ca.live = p.live.as<uint32_t>();
+        c.ktimer_begin("prefilter", st);
+        launch_cand_prefilter(D, ca, st);
+        scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), mt0, p.totals.as<uint32_t>() + 8, p.scratch.as<uint32_t>(),
+                      st);
+        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), p.rows2.as<double>(), p.sortkey2.as<uint64_t>(),
+                            p.slot_src2.as<uint32_t>(), p.pruner_slot.as<int32_t>(), KM, st);
+        c.ktimer_end("prefilter", st, mt0);
+        STAGE(st, "prefilter");
+        uint32_t live_n = 0;
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 8, 4}}, {&live_n}));
+        std::swap(p.rows, p.rows2);
+        std::swap(p.sortkey, p.sortkey2);
+        std::swap(p.slot_src, p.slot_src2);
+        p.mt = live_n;
+        if (debug_level() >= 3) fprintf(stderr, "[sky] prefilter %u -> %u slots (M2=%d)\n", mt0, live_n, M2);
+    }
     const uint32_t mt = p.mt;
     const size_t rb = row_bytes(p.f64, D);
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));

@@ -683,6 +683,140 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
     if (threadIdx.x == 0) *a.nps_total = run;
 }
 
+// ---- candidate prefilter: second-level pruners drawn from the candidates ------------
+// The first-level pruners come from a 65536-tuple sample (<= 8 per partition, they live in
+// k_filter's LDS).  The candidates that survive them are far closer to each partition's
+// skyline, so per partition up to M2 (<= 64) candidates minimising positive-weight linear
+// criteria (never dominated among the candidates: skyline points, up to the f32 rounding of
+// the criterion, re-checked exactly below) prune every other candidate of that partition by
+// one brute-force pass (|candidates| x M2 pair tests) before the sort.  A candidate they
+// dominate is outside L_k; equal vectors are never dropped.  Exactness: dominance in f64.
+template <int D>
+__device__ __forceinline__ float cand_criterion(const float (&f)[D], float sum, int j) {
+    if (j == 0) return sum;
+    if (j <= D) return sum + 3.0f * f[j - 1];
+    const int a = (j - 1) % D, b = (j - 1 + 1 + (j - 1) / D) % D;
+    return sum + 3.0f * (f[a] + f[b]);
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cand_min(const double *__restrict__ rows, const uint64_t *__restrict__ key,
+                                                       uint32_t mt, int Kp, int M2,
+                                                       unsigned long long *__restrict__ gmin) {
+    constexpr int DP = padded_dims<double>(D);
+    __shared__ unsigned long long s_min[2048];
+    const int KM = Kp * M2;
+    for (int q = threadIdx.x; q < KM; q += kThreads) s_min[q] = ~0ull;
+    __syncthreads();
+    for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < mt; j += gridDim.x * kThreads) {
+        const int k = (int)(key[j] >> 56);
+        double v[D];
+        load_trow<double, D>(rows + (size_t)j * DP, v);
+        float f[D];
+        float sum = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; d++) { f[d] = (float)v[d]; sum += f[d]; }
+        for (int c = 0; c < M2; c++) {
+            const float cv = cand_criterion<D>(f, sum, c);
+            if (cv != cv) continue;
+            atomicMin(&s_min[k * M2 + c], ((unsigned long long)f32_order_key(cv) << 32) | j);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < KM; q += kThreads)
+        if (s_min[q] != ~0ull) atomicMin(&gmin[q], s_min[q]);
+}
+
+// one 64-lane workgroup per partition: winners deduplicated and mutually non-dominated
+template <int D>
+__global__ __launch_bounds__(64) void k_cand_pick(const double *__restrict__ rows,
+                                                  const unsigned long long *__restrict__ gmin, int M2,
+                                                  double *__restrict__ pr2, int32_t *__restrict__ npr2) {
+    constexpr int DP = padded_dims<double>(D);
+    __shared__ double s_c[64][D];
+    __shared__ int s_ok[64];
+    const int k = blockIdx.x, j = threadIdx.x;
+    const unsigned long long w = j < M2 ? gmin[k * M2 + j] : ~0ull;
+    const bool has = w != ~0ull;
+    if (has) {
+        const uint32_t slot = (uint32_t)(w & 0xffffffffu);
+#pragma unroll
+        for (int d = 0; d < D; d++) s_c[j][d] = rows[(size_t)slot * DP + d];
+    }
+    s_ok[j] = has ? 1 : 0;
+    __syncthreads();
+    bool ok = has;
+    for (int q = 0; q < M2 && ok; q++) {
+        if (q == j || !s_ok[q]) continue;
+        bool le = true, lt = false, eq = true;
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            le &= s_c[q][d] <= s_c[j][d];
+            lt |= s_c[q][d] < s_c[j][d];
+            eq &= s_c[q][d] == s_c[j][d];
+        }
+        if ((le && lt) || (eq && q < j)) ok = false;
+    }
+    const uint64_t b = __ballot(ok);
+    if (ok) {
+        const int pos = __popcll(b & (j == 0 ? 0ull : (~0ull >> (64 - j))));
+#pragma unroll
+        for (int d = 0; d < D; d++) pr2[((size_t)k * M2 + pos) * D + d] = s_c[j][d];
+    }
+    if (j == 0) npr2[k] = __popcll(b);
+}
+
+// live[j] = candidate j is not dominated by a second-level pruner of its partition
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restrict__ rows,
+                                                          const uint64_t *__restrict__ key, uint32_t mt, int M2,
+                                                          const double *__restrict__ pr2,
+                                                          const int32_t *__restrict__ npr2,
+                                                          uint32_t *__restrict__ live) {
+    constexpr int DP = padded_dims<double>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= mt) return;
+    const int k = (int)(key[j] >> 56);
+    double v[D];
+    load_trow<double, D>(rows + (size_t)j * DP, v);
+    const int np = npr2[k];
+    const double *pr = pr2 + (size_t)k * M2 * D;
+    bool dom = false;
+    for (int q = 0; q < np && !dom; q++) {
+        bool le = true, lt = false;
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const double x = pr[q * D + d];
+            le &= x <= v[d];
+            lt |= x < v[d];
+        }
+        dom = le && lt;
+    }
+    live[j] = dom ? 0u : 1u;
+}
+
+// order-preserving compaction of the live slots (rows, keys, sources); the appended
+// pruner slots' indices are remapped (a dropped one: its duplicate group's fate is 0)
+__global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, int DP, const uint32_t *__restrict__ live,
+                                                           const uint32_t *__restrict__ pos,
+                                                           const double *__restrict__ rows,
+                                                           const uint64_t *__restrict__ key,
+                                                           const uint32_t *__restrict__ src, double *__restrict__ rows2,
+                                                           uint64_t *__restrict__ key2, uint32_t *__restrict__ src2,
+                                                           int32_t *__restrict__ pruner_slot, int KM) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j < mt && live[j]) {
+        const uint32_t o = pos[j];
+        for (int d = 0; d < DP; d++) rows2[(size_t)o * DP + d] = rows[(size_t)j * DP + d];
+        key2[o] = key[j];
+        src2[o] = src[j];
+    }
+    if (j < (uint32_t)KM) {
+        const int32_t ps = pruner_slot[j];
+        if (ps >= 0) pruner_slot[j] = live[ps] ? (int32_t)pos[ps] : -1;
+    }
+}
+
 // ---- duplicate collapse after the sort --------------------------------------
 template <typename T, int D>
 __global__ __launch_bounds__(kThreads) void k_gather_runs(RepArgs a) {
@@ -1084,6 +1218,23 @@ void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
 
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
     SKY_DISPATCH_D(D, (k_append_pruners<DD><<<1, kThreads, 0, st>>>(a)));
+}
+
+void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st) {
+    if (!a.mt) return;
+    const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 1024u);
+    SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.Kp, a.M2, a.cmin)));
+    SKY_DISPATCH_D(D, (k_cand_pick<DD><<<a.Kp, 64, 0, st>>>(a.rows, a.cmin, a.M2, a.pr2, a.npr2)));
+    SKY_DISPATCH_D(D, (k_cand_filter<DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a.rows, a.key, a.mt, a.M2, a.pr2,
+                                                                                   a.npr2, a.live)));
+}
+
+void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
+                         int32_t *pruner_slot, int KM, hipStream_t st) {
+    const uint32_t n = std::max<uint32_t>(a.mt, (uint32_t)KM);
+    if (!n) return;
+    k_cand_compact<<<nblk(n, kThreads), kThreads, 0, st>>>(a.mt, padded_dims<double>(D), a.live, pos, a.rows, a.key,
+                                                           a.src, rows2, key2, src2, pruner_slot, KM);
 }
 
 void launch_fate_tables(const FateArgs &a, hipStream_t st) {

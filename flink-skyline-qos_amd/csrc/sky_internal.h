@@ -111,6 +111,22 @@ struct FateArgs {
 };
 void launch_fate_tables(const FateArgs &a, hipStream_t st);
 
+// candidate prefilter (second-level pruners drawn from the candidates, k_partition.hip)
+struct CandArgs {
+    uint32_t mt;                  // slots
+    const double *rows;           // [mt][pad(D)] f64 slot rows
+    const uint64_t *key;          // [mt] sort keys (partition in bits 63..56)
+    const uint32_t *src;          // [mt] slot sources
+    int Kp, M2;                   // Kp * M2 <= 2048, M2 <= 64
+    unsigned long long *cmin;     // [Kp*M2], all-ones on entry
+    double *pr2;                  // [Kp][M2][D]
+    int32_t *npr2;                // [Kp]
+    uint32_t *live;               // [mt] out
+};
+void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st);
+void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
+                         int32_t *pruner_slot, int KM, hipStream_t st);
+
 struct RepArgs {
     uint32_t mt;                  // sorted slots
     const uint32_t *perm;         // sorted position -> slot

@@ -287,3 +287,22 @@ def test_batched_readback_equals_per_range_copies(gpu_engine_factory, oracle, mo
         np.testing.assert_array_equal(x, y)
     monkeypatch.setenv("SKY_GATHER", "1")
     check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
+
+
+@pytest.mark.parametrize("dist,D,P_,algo", [("anti_correlated", 8, 16, "mr-angle"), ("uniform", 6, 256, "mr-angle"),
+                                            ("correlated", 4, 8, "mr-grid"), ("std_anti", 3, 8, "mr-dim"),
+                                            ("uniform", 1, 4, "mr-dim")])
+def test_candidate_prefilter_is_exact(dist, D, P_, algo, gpu_engine_factory, oracle, monkeypatch):
+    """The candidate prefilter (second-level pruners drawn from the candidates, dropping the
+    candidates they dominate before the sort) never changes a result: on and off (SKY_PREFILTER)
+    give the same ids, origins and |L_k| / survivors_k, and both equal the oracle."""
+    n = 150_000
+    vals = oracle.synth(DISTS[dist], D, n, seed=900 + D + P_)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SKY_PREFILTER", flag)
+        res.append(run_query(gpu_engine_factory, vals, P_, algo))
+    for a, b in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
+        np.testing.assert_array_equal(a, b)
+    monkeypatch.setenv("SKY_PREFILTER", "1")
+    check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
