@@ -125,6 +125,10 @@ static bool prefilter_disabled() {
     return e && atoi(e) == 0;
 }
 constexpr uint32_t kPrefilterMin = 4096;   // fewer slots: the SFS runs in one small pass anyway
+static bool brute_disabled() {
+    const char *e = getenv("SKY_BRUTE");
+    return e && atoi(e) == 0;
+}
 // SKY_GATHER=0 reads counters back by one hipMemcpyAsync per range (A/B knob)
 static bool gather_disabled() {
     const char *e = getenv("SKY_GATHER");
@@ -689,6 +693,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         if (debug_level() >= 3) fprintf(stderr, "[sky] prefilter %u -> %u slots (M2=%d)\n", mt0, live_n, M2);
     }
     const uint32_t mt = p.mt;
+    // small candidate sets (typical after the prefilter): both skyline levels by one
+    // brute-force launch instead of the round-based SFS (SKY_BRUTE=0: A/B knob)
+    const bool brute = in.fate && mt > 0 && mt <= kBruteMax && !brute_disabled();
     const size_t rb = row_bytes(p.f64, D);
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
@@ -765,6 +772,21 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_seg_bounds(p.rep_key.as<uint64_t>(), mt, p.totals.as<uint32_t>() + 1, p.seg_begin.as<uint32_t>(),
                           p.seg_end.as<uint32_t>(), st);
         STAGE(st, "dedup");
+        if (brute) {
+            // ---- small rep set: both skyline levels in one launch, no host round trip
+            //      (mr, the segment bounds and the flags come back with the final read)
+            if (tm) tm->mark(5, st);
+            SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+            fill.add(p.segalive.p, (size_t)p.Kp * 4);
+            HIP_TRY(fill.launch(st));
+            c.ktimer_begin("brute", st);
+            launch_brute_fates(D, p.f64, p.rep_rows.p, p.rep_key.as<uint64_t>(), p.totals.as<uint32_t>() + 1, mt,
+                               in.global && !in.single, p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
+                               p.segalive.as<uint32_t>(), st);
+            c.ktimer_end("brute", st, 0);
+            STAGE(st, "brute");
+            if (tm) tm->mark(6, st);
+        } else {
         std::vector<uint32_t> sb(p.Kp), se(p.Kp);
         uint32_t flags2 = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
@@ -850,6 +872,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         } else {
             HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
         }
+        }   // !brute
     }
     // stats: summed over slots (unit weights, computed origins) or, for given origins /
     // weights, over tuples in the count pass
@@ -909,11 +932,33 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
                        p.statk.as<unsigned long long>(), st);
     std::vector<unsigned long long> sk2((size_t)p.K * 2);
-    const bool have_seg = mt && !p.h_seg_n.empty();
+    const bool have_seg = mt && (brute || !p.h_seg_n.empty());
     p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
-    SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                              {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}},
-                      {&nout, sk2.data(), p.h_seg_s.data()}));
+    if (brute) {
+        std::vector<uint32_t> sb(p.Kp), se(p.Kp);
+        uint32_t mr_b = 0, flags2 = 0;
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
+                                  {p.segalive.p, (size_t)p.Kp * 4}, {p.totals.as<uint32_t>() + 1, 4},
+                                  {p.seg_begin.p, (size_t)p.Kp * 4}, {p.seg_end.p, (size_t)p.Kp * 4},
+                                  {p.flags.p, 4}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &mr_b, sb.data(), se.data(), &flags2}));
+        if (flags2 & kFlagRadixSpin) {
+            set_error("radix sort look-back exceeded its spin bound");
+            return SKY_E_HIP;
+        }
+        p.mr = mr_b;
+        p.h_seg_n.resize(p.Kp);
+        uint32_t alive_sum = 0;
+        for (int k = 0; k < p.Kp; k++) {
+            p.h_seg_n[k] = se[k] - sb[k];
+            alive_sum += p.h_seg_s[k];
+        }
+        p.mg = in.global && !in.single ? alive_sum : 0;
+    } else {
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
+                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}},
+                          {&nout, sk2.data(), p.h_seg_s.data()}));
+    }
     p.dom_w = 0;
     if (have_seg) {
         int64_t sg = 0;

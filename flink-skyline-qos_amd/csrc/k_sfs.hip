@@ -596,6 +596,76 @@ void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr
     k_seg_alive<<<g, kThreads, 0, st>>>(rep_key, alive, mr, cnt);
 }
 
+// Both skyline levels of a SMALL representative set in one launch (no sort, no rounds, no
+// host round trip): rep y is in L_k iff no rep of its partition dominates it, and in G iff
+// no rep at all dominates it (a dominator outside the union of the L_k is itself dominated
+// by a member of it: transitivity).  Full dominance test (reps of different partitions may
+// be equal vectors when keys are given).  A rep with a larger f32 score is skipped (the
+// clamped f64 sum rounded to f32 is monotone under dominance).  mr is read on the device;
+// the grid covers an upper bound.  Also counts the alive reps per partition (segalive).
+constexpr int kBruteTile = 256;
+template <typename T, int D>
+__global__ __launch_bounds__(kThreads) void k_brute_fates(const T *__restrict__ rows, const uint64_t *__restrict__ key,
+                                                          const uint32_t *__restrict__ d_mr, int gmerge,
+                                                          uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g,
+                                                          uint32_t *__restrict__ segalive) {
+    constexpr int DP = padded_dims<T>(D);
+    __shared__ T s_x[kBruteTile * DP];
+    __shared__ uint32_t s_k[kBruteTile];                         // f32 order key of the score
+    __shared__ uint8_t s_p[kBruteTile];                          // partition
+    const uint32_t mr = *d_mr;
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (blockIdx.x * kThreads >= mr) return;                    // block-uniform
+    const bool valid = j < mr;
+    T y[DP];
+#pragma unroll
+    for (int d = 0; d < DP; d++) y[d] = valid ? rows[(size_t)j * DP + d] : T(0);
+    const uint64_t ky = valid ? key[j] : 0ull;
+    const uint32_t py = (uint32_t)(ky >> 56), sy = (uint32_t)(ky >> 24);
+    bool dom_l = false, dom_g = false;
+    for (uint32_t t0 = 0; t0 < mr; t0 += kBruteTile) {
+        const uint32_t cn = mr - t0 < (uint32_t)kBruteTile ? mr - t0 : (uint32_t)kBruteTile;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < cn * DP; q += kThreads) s_x[q] = rows[(size_t)t0 * DP + q];
+        for (uint32_t q = threadIdx.x; q < cn; q += kThreads) {
+            const uint64_t kx = key[t0 + q];
+            s_k[q] = (uint32_t)(kx >> 24);                        // score bits 55..24
+            s_p[q] = (uint8_t)(kx >> 56);
+        }
+        __syncthreads();
+        if (valid && !dom_l) {
+            for (uint32_t i = 0; i < cn; i++) {
+                if (s_k[i] > sy) continue;                        // larger score: cannot dominate
+                if (!dominates_full<D, T>(s_x + (size_t)i * DP, y)) continue;
+                dom_g = true;
+                if (s_p[i] == py) {
+                    dom_l = true;                                 // implies dom_g: settled
+                    break;
+                }
+            }
+        }
+        if (!__syncthreads_or(valid && !dom_l)) break;
+    }
+    if (!valid) return;
+    alive_l[j] = dom_l ? 0 : 1;
+    alive_g[j] = (gmerge ? dom_g : dom_l) ? 0 : 1;
+    if (!dom_l) atomicAdd(&segalive[py], 1u);
+}
+
+void launch_brute_fates(int D, bool f64, const void *rows, const uint64_t *key, const uint32_t *d_mr, uint32_t mr_max,
+                        bool gmerge, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, hipStream_t st) {
+    if (!mr_max) return;
+    const unsigned g = (mr_max + kThreads - 1) / kThreads;
+    if (f64)
+        SKY_DISPATCH_D(D, (k_brute_fates<double, DD><<<g, kThreads, 0, st>>>((const double *)rows, key, d_mr,
+                                                                             gmerge ? 1 : 0, alive_l, alive_g,
+                                                                             segalive)));
+    else
+        SKY_DISPATCH_D(D, (k_brute_fates<float, DD><<<g, kThreads, 0, st>>>((const float *)rows, key, d_mr,
+                                                                            gmerge ? 1 : 0, alive_l, alive_g,
+                                                                            segalive)));
+}
+
 // ---- launchers ------------------------------------------------------------------
 static inline unsigned nb(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 

@@ -294,15 +294,19 @@ def test_batched_readback_equals_per_range_copies(gpu_engine_factory, oracle, mo
                                             ("uniform", 1, 4, "mr-dim")])
 def test_candidate_prefilter_is_exact(dist, D, P_, algo, gpu_engine_factory, oracle, monkeypatch):
     """The candidate prefilter (second-level pruners drawn from the candidates, dropping the
-    candidates they dominate before the sort) never changes a result: on and off (SKY_PREFILTER)
-    give the same ids, origins and |L_k| / survivors_k, and both equal the oracle."""
+    candidates they dominate before the sort) and the one-launch brute-force fates of small rep
+    sets never change a result: every on/off combination (SKY_PREFILTER, SKY_BRUTE) gives the
+    same ids, origins and |L_k| / survivors_k, equal to the oracle."""
     n = 150_000
     vals = oracle.synth(DISTS[dist], D, n, seed=900 + D + P_)
     res = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SKY_PREFILTER", flag)
+    for pre, brute in (("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("SKY_PREFILTER", pre)
+        monkeypatch.setenv("SKY_BRUTE", brute)
         res.append(run_query(gpu_engine_factory, vals, P_, algo))
-    for a, b in zip(res[0][0] + res[0][1], res[1][0] + res[1][1]):
-        np.testing.assert_array_equal(a, b)
+    for r in res[1:]:
+        for a, b in zip(res[0][0] + res[0][1], r[0] + r[1]):
+            np.testing.assert_array_equal(a, b)
     monkeypatch.setenv("SKY_PREFILTER", "1")
+    monkeypatch.setenv("SKY_BRUTE", "1")
     check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
