@@ -656,14 +656,15 @@ void launch_brute_fates(int D, bool f64, const void *rows, const uint64_t *key, 
                         bool gmerge, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, hipStream_t st) {
     if (!mr_max) return;
     const unsigned g = (mr_max + kThreads - 1) / kThreads;
-    if (f64)
+    if (f64) {
         SKY_DISPATCH_D(D, (k_brute_fates<double, DD><<<g, kThreads, 0, st>>>((const double *)rows, key, d_mr,
                                                                              gmerge ? 1 : 0, alive_l, alive_g,
                                                                              segalive)));
-    else
+    } else {
         SKY_DISPATCH_D(D, (k_brute_fates<float, DD><<<g, kThreads, 0, st>>>((const float *)rows, key, d_mr,
                                                                             gmerge ? 1 : 0, alive_l, alive_g,
                                                                             segalive)));
+    }
 }
 
 // ---- launchers ------------------------------------------------------------------
