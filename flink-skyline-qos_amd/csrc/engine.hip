@@ -777,12 +777,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             //      (mr, the segment bounds and the flags come back with the final read)
             if (tm) tm->mark(5, st);
             SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+            SKY_TRY(p.keep.ensure((size_t)mt * 4));              // per-rep domination bits
             fill.add(p.segalive.p, (size_t)p.Kp * 4);
+            fill.add(p.keep.p, (size_t)mt * 4);
             HIP_TRY(fill.launch(st));
             c.ktimer_begin("brute", st);
             launch_brute_fates(D, p.f64, p.rep_rows.p, p.rep_key.as<uint64_t>(), p.totals.as<uint32_t>() + 1, mt,
-                               in.global && !in.single, p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
-                               p.segalive.as<uint32_t>(), st);
+                               in.global && !in.single, p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(),
+                               p.alive_g.as<uint8_t>(), p.segalive.as<uint32_t>(), st);
             c.ktimer_end("brute", st, 0);
             STAGE(st, "brute");
             if (tm) tm->mark(6, st);
