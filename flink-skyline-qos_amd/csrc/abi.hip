@@ -491,7 +491,7 @@ int sky_export_local_dev(sky_ctx *c, const int64_t *d_ids, const double *d_value
                       p.scratch.as<uint32_t>(), c->st);
         SKY_TRY(p.perm.ensure((size_t)p.mt * 4));
         launch_iota(p.perm.as<uint32_t>(), p.mt, c->st);   // identity: slot order
-        launch_rep_mult(p.mt, p.perm.as<uint32_t>(), p.slot_src.as<uint32_t>(), p.slot_rep.as<uint32_t>(),
+        launch_rep_mult(p.mt, p.perm.as<uint32_t>(), p.s_src->as<uint32_t>(), p.slot_rep.as<uint32_t>(),
                         in.weights, p.dup_cnt.as<uint32_t>(), p.pr_entries.as<int32_t>(),
                         p.mult.as<unsigned long long>(), c->st);
         SKY_TRY(p.pinned(64));
@@ -558,7 +558,7 @@ int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys
     FateArgs fta{};
     fta.mt = p.mt;
     fta.slot_rep = p.slot_rep.as<uint32_t>();
-    fta.slot_src = p.slot_src.as<uint32_t>();
+    fta.slot_src = p.s_src->as<uint32_t>();
     fta.alive_l = p.alive_l.as<uint8_t>();
     fta.alive_g = p.alive_g.as<uint8_t>();
     fta.KM = p.Kp * p.M;

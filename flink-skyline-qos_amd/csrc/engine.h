@@ -69,6 +69,10 @@ struct Pipe {
     DevBuf scratch, flags, totals, orand, lsz, surv, statk, segalive;
     // candidate prefilter (second-level pruners) and its compaction targets
     DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2;
+    // the candidate slots after the filter (rows / sortkey / slot_src) or, after the
+    // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so
+    // the stream-sized buffers keep their capacity across queries)
+    DevBuf *s_rows = &rows, *s_key = &sortkey, *s_src = &slot_src;
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;

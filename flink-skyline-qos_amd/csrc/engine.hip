@@ -646,6 +646,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.u16 = !p.f64 && !p.ties && (flags & kFlagNotU16) == 0 && !sfs16_disabled();
     p.mt = m + nps;
     p.mt_pre = p.mt;
+    p.s_rows = &p.rows;
+    p.s_key = &p.sortkey;
+    p.s_src = &p.slot_src;
     // ---- candidate prefilter: second-level pruners drawn from the candidates drop the
     //      candidates they dominate before the sort (worth it once the candidates
     //      outnumber what one small-SFS workgroup per partition handles)
@@ -686,9 +689,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         STAGE(st, "prefilter");
         uint32_t live_n = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 8, 4}}, {&live_n}));
-        std::swap(p.rows, p.rows2);
-        std::swap(p.sortkey, p.sortkey2);
-        std::swap(p.slot_src, p.slot_src2);
+        p.s_rows = &p.rows2;
+        p.s_key = &p.sortkey2;
+        p.s_src = &p.slot_src2;
         p.mt = live_n;
         if (debug_level() >= 3) fprintf(stderr, "[sky] prefilter %u -> %u slots (M2=%d)\n", mt0, live_n, M2);
     }
@@ -710,7 +713,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mt), scan_scratch_words(mt + 1)) * 4 + 64));
         if (debug_level() >= 4) {
             SKY_TRY(p.segalive.ensure(64));
-            radix_key_orand(p.sortkey.as<uint64_t>(), mt, p.segalive.as<unsigned long long>(), st);
+            radix_key_orand(p.s_key->as<uint64_t>(), mt, p.segalive.as<unsigned long long>(), st);
             unsigned long long chk[2] = {0, 0};
             SKY_TRY(sync_read(p, st, {{p.segalive.p, 16}}, {chk}));
             fprintf(stderr, "[sky] orand filter %016llx %016llx recomputed %016llx %016llx\n", orand[0], orand[1],
@@ -718,17 +721,17 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         }
         launch_iota(p.perm.as<uint32_t>(), mt, st);
         hipError_t lerr = hipSuccess;
-        const bool alt = radix_sort_pairs(p.sortkey.as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
+        const bool alt = radix_sort_pairs(p.s_key->as<uint64_t>(), p.perm.as<uint32_t>(), p.key_alt.as<uint64_t>(),
                                           p.val_alt.as<uint32_t>(), mt, orand[0], orand[1],
                                           p.scratch.as<uint32_t>(), p.flags.as<uint32_t>(), st, &lerr);
         HIP_TRY(lerr);
         STAGE(st, "sort");
-        const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.sortkey.as<uint64_t>();
+        const uint64_t *skey = alt ? p.key_alt.as<uint64_t>() : p.s_key->as<uint64_t>();
         const uint32_t *perm = alt ? p.val_alt.as<uint32_t>() : p.perm.as<uint32_t>();
         if (debug_level() >= 4 && alt) {
             SKY_TRY(p.runflag.ensure((size_t)mt * 4));
             HIP_TRY(hipMemsetAsync(p.totals.as<uint32_t>() + 7, 0, 4, st));
-            radix_debug_check(p.sortkey.as<uint64_t>(), skey, perm, mt, p.runflag.as<uint32_t>(),
+            radix_debug_check(p.s_key->as<uint64_t>(), skey, perm, mt, p.runflag.as<uint32_t>(),
                               p.totals.as<uint32_t>() + 7, st);
             uint32_t bad = 0;
             SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 7, 4}}, {&bad}));
@@ -746,7 +749,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         ra.mt = mt;
         ra.perm = perm;
         ra.skey = skey;
-        ra.rows = p.rows.p;
+        ra.rows = p.s_rows->p;
         ra.rows_sorted = p.rows_sorted.p;
         ra.runflag = p.runflag.as<uint32_t>();
         ra.runscan = p.runscan.as<uint32_t>();
@@ -882,7 +885,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     FateArgs fta{};
     fta.mt = mt;
     fta.slot_rep = p.slot_rep.as<uint32_t>();
-    fta.slot_src = p.slot_src.as<uint32_t>();
+    fta.slot_src = p.s_src->as<uint32_t>();
     fta.alive_l = p.alive_l.as<uint8_t>();
     fta.alive_g = p.alive_g.as<uint8_t>();
     fta.KM = KM;
