@@ -226,6 +226,9 @@ int sky_query_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int6
     in.ids = d_ids;
     in.global = true;
     in.K = c->Kq();
+    in.out_ids = d_ids_out;
+    in.out_org = d_origin_out;
+    in.out_cap = cap;
     c->shard_valid = false;
     int r = pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr);
     if (r == SKY_OK) {
@@ -255,6 +258,11 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
     in.ids = ids ? c->h_ids.as<int64_t>() : nullptr;
     in.global = true;
     in.K = c->Kq();
+    SKY_TRY(c->h_out_ids.ensure(nn * 8));
+    SKY_TRY(c->h_out_org.ensure(nn * 4));
+    in.out_ids = c->h_out_ids.as<int64_t>();
+    in.out_org = c->h_out_org.as<int32_t>();
+    in.out_cap = n;
     c->shard_valid = false;
     if (c->profile) {
         if (!c->pt.ok) c->pt.init();
@@ -268,10 +276,8 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
         set_error("output capacity too small");
         return SKY_E_CAPACITY;
     }
-    SKY_TRY(c->h_out_ids.ensure((size_t)std::max<int64_t>(g, 1) * 8));
-    SKY_TRY(c->h_out_org.ensure((size_t)std::max<int64_t>(g, 1) * 4));
     SKY_TRY(pipe_output(*c, c->main, in, false, c->h_out_ids.as<int64_t>(), c->h_out_org.as<int32_t>(), nullptr,
-                        std::max<int64_t>(g, 0), nullptr, nullptr));
+                        n, nullptr, nullptr));
     if (g && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->h_out_ids.p, (size_t)g * 8, hipMemcpyDeviceToHost, c->st));
     if (g && origin_out)
         HIP_TRY(hipMemcpyAsync(origin_out, c->h_out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, c->st));
@@ -962,6 +968,9 @@ static int stream_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out
     in.n = (uint32_t)s->n;
     in.global = true;
     in.K = c->Kq();
+    in.out_ids = d_ids_out;
+    in.out_org = d_origin_out;
+    in.out_cap = cap;
     c->shard_valid = false;
     if (c->profile) {
         if (!c->pt.ok) c->pt.init();

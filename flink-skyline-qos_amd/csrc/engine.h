@@ -44,6 +44,11 @@ struct PipeIn {
     bool global = true;             // run the global merge after the local skylines
     bool fate = true;               // per-tuple fate pass (stats, output counts)
     int K = 1;                      // stats slots
+    // optional: the global skyline's stream-ordered ids / origins, written by the run itself
+    // (single-pass output) when the stats come from the slots; pipe_output then only checks
+    int64_t *out_ids = nullptr;
+    int32_t *out_org = nullptr;
+    int64_t out_cap = 0;
 };
 
 struct PhaseTimer;
@@ -73,6 +78,11 @@ struct Pipe {
     // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so
     // the stream-sized buffers keep their capacity across queries)
     DevBuf *s_rows = &rows, *s_key = &sortkey, *s_src = &slot_src;
+    // single-pass output: look-back words per tile; what the last run wrote
+    DevBuf lbuf;
+    bool fused = false;
+    const int64_t *fused_ids = nullptr;
+    const int32_t *fused_org = nullptr;
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;

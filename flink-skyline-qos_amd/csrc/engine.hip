@@ -125,6 +125,10 @@ static bool prefilter_disabled() {
     return e && atoi(e) == 0;
 }
 constexpr uint32_t kPrefilterMin = 4096;   // fewer slots: the SFS runs in one small pass anyway
+static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
+    const char *e = getenv("SKY_FUSED_OUT");
+    return e && atoi(e) == 0;
+}
 static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
     return e && atoi(e) == 0;
@@ -524,6 +528,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.Kp = in.single ? 1 : c.Kq();
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
+    p.fused = false;
     p.sfs_rounds = p.sfs_pairs_upper = 0;
     p.h_seg_n.clear();
     p.h_seg_s.clear();
@@ -924,12 +929,31 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     oa.surv = slot_stats ? nullptr : p.surv.as<unsigned long long>();
     oa.out_cnt = p.out_cnt.as<uint32_t>();
     oa.select_local = 0;
+    p.fused = slot_stats && (in.out_ids || in.out_org) && !fused_disabled();
+    p.fused_ids = in.out_ids;
+    p.fused_org = in.out_org;
     c.ktimer_begin("out", st);
-    c.ktimer_begin("outc", st);
-    launch_out_count(oa, st);
-    c.ktimer_end("outc", st, n);
-    scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                  p.scratch.as<uint32_t>(), st);
+    if (p.fused) {
+        // count + prefix + write in one pass (ids / origins straight into the caller's buffers)
+        SKY_TRY(p.lbuf.ensure((size_t)tiles * 8 + 64));
+        fill.add(p.lbuf.p, (size_t)tiles * 8);
+        fill.add(p.totals.as<uint32_t>() + 9, 4);          // ticket
+        HIP_TRY(fill.launch(st));
+        oa.ids = in.ids;
+        oa.ids_out = in.out_ids;
+        oa.origin_out = in.out_org;
+        oa.given_origin = nullptr;
+        c.ktimer_begin("outw", st);
+        launch_out_fused(oa, p.lbuf.as<unsigned long long>(), p.totals.as<uint32_t>() + 9,
+                         p.totals.as<uint32_t>() + 3, p.flags.as<uint32_t>(), in.out_cap, st);
+        c.ktimer_end("outw", st, n);
+    } else {
+        c.ktimer_begin("outc", st);
+        launch_out_count(oa, st);
+        c.ktimer_end("outc", st, n);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), st);
+    }
     c.ktimer_end("out", st, n);
     STAGE(st, "fate");
     uint32_t nout = 0;
@@ -960,9 +984,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         }
         p.mg = in.global && !in.single ? alive_sum : 0;
     } else {
+        uint32_t flags3 = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}},
-                          {&nout, sk2.data(), p.h_seg_s.data()}));
+                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3}));
+        if (flags3 & kFlagRadixSpin) {
+            set_error("a look-back (radix sort / output) exceeded its spin bound");
+            return SKY_E_HIP;
+        }
     }
     p.dom_w = 0;
     if (have_seg) {
@@ -995,7 +1024,12 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
                 double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags) {
     // the run's count pass selected G (global runs) or L (single-partition runs); the local
     // skyline of a global run needs its own count + scan (stats untouched)
-    const bool recount = select_local && in.global && p.n > 0;
+    const bool writes = d_ids_out || d_origin_out || d_rows_out || d_row_flags;
+    const bool fused_done = p.fused && !select_local && !d_rows_out && !d_row_flags && d_ids_out == p.fused_ids &&
+                            d_origin_out == p.fused_org;
+    // the local skyline of a global run, or other buffers than the single-pass output wrote:
+    // a count pass + scan of its own (stats untouched)
+    const bool recount = p.n > 0 && ((select_local && in.global) || (p.fused && writes && !fused_done));
     uint32_t nsel = p.nout;
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();
@@ -1017,7 +1051,7 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     oa.select_local = 0;
     if (recount) {
         const uint32_t tiles = (p.n + kTile - 1) / kTile;
-        oa.select_local = 1;
+        oa.select_local = select_local ? 1 : 0;
         oa.lsz = nullptr;
         oa.surv = nullptr;
         oa.row_flags = nullptr;
@@ -1032,6 +1066,7 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
         return SKY_E_CAPACITY;
     }
     if (p.n == 0) return SKY_OK;
+    if (fused_done) return SKY_OK;          // the run's single-pass output already wrote them
     if (d_row_flags) {
         oa.row_flags = d_row_flags;
         oa.lsz = nullptr;

@@ -1163,6 +1163,93 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     }
 }
 
+// Single-pass output (unit weights, stats already summed over slots): per tile, the
+// selected tuples' ranks by a block scan, the tile's exclusive prefix by a decoupled
+// look-back over the earlier tiles' published counts (tiles numbered in start order by a
+// ticket: a tile only waits for tiles already running; bounded spin -> error flag), then
+// the ids / origins staged in LDS and written coalesced.  Replaces count pass + scan +
+// host read + write pass; positions >= cap are not written (the caller reports
+// SKY_E_CAPACITY from the total).
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbCount = (1ull << 62) - 1;
+__global__ __launch_bounds__(kThreads) void k_out_fused(OutArgs a, unsigned long long *__restrict__ lb,
+                                                        uint32_t *__restrict__ ticket, uint32_t *__restrict__ d_total,
+                                                        uint32_t *__restrict__ err, int64_t cap) {
+    __shared__ uint8_t s_pf[2048];
+    __shared__ uint32_t s_w[kThreads / 64];
+    __shared__ int64_t s_oid[kTile];
+    __shared__ int32_t s_oorg[kTile];
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_prefix;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t i0 = tile * kTile + threadIdx.x * kItems;
+    uint16_t st[kItems];
+    load_status8(a.status, a.n, i0, st);
+    int64_t idv[kItems];
+    if (a.ids) {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k, a.n - 1)];
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k);
+    }
+    const int shift = a.select_local ? 0 : 1;
+    uint8_t fate[kItems];
+    uint32_t nsel = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        fate[k] = (uint8_t)tuple_fate(st[k], s_pf, a.M);
+        nsel += (fate[k] >> shift) & 1u;
+    }
+    uint32_t bt;
+    uint32_t pl = block_scan_excl(nsel, s_w, bt);
+    if (threadIdx.x == 0) {
+        unsigned long long excl = 0;
+        unsigned long long *mine = lb + tile;
+        if (tile == 0) {
+            __hip_atomic_store(mine, kLbInc | bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(mine, kLbAgg | bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t pt = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            while (pt >= 0) {
+                const unsigned long long sv =
+                    __hip_atomic_load(lb + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long f = sv & ~kLbCount;
+                if (f == 0ull) {
+                    if (++spins > (1u << 24)) { atomicOr(err, kFlagRadixSpin); break; }   // bounded spin
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += sv & kLbCount;
+                if (f == kLbInc) break;
+                pt--;
+            }
+            __hip_atomic_store(mine, kLbInc | (excl + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_prefix = excl;
+        if (tile == ntiles - 1) *d_total = (uint32_t)(excl + bt);
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; k++) {
+        if (!((fate[k] >> shift) & 1)) continue;
+        s_oid[pl] = idv[k];
+        s_oorg[pl] = a.given_origin ? a.given_origin[i0 + k] : (int32_t)(st[k] >> 8);
+        pl++;
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)s_prefix;
+    for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
+        const int64_t dst = base + q;
+        if (dst >= cap) break;
+        if (a.ids_out) a.ids_out[dst] = s_oid[q];
+        if (a.origin_out) a.origin_out[dst] = s_oorg[q];
+    }
+}
+
 template <typename T, int D>
 __global__ __launch_bounds__(kThreads) void k_export_reps(uint32_t mr, const T *__restrict__ rep_rows,
                                                           const uint64_t *__restrict__ rep_key,
@@ -1276,6 +1363,12 @@ void launch_out_count(const OutArgs &a, hipStream_t st) {
     else if (gw) k_out_count<false, true><<<g, kThreads, 0, st>>>(a);
     else k_out_count<false, false><<<g, kThreads, 0, st>>>(a);
 }
+void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket, uint32_t *d_total, uint32_t *err,
+                      int64_t cap, hipStream_t st) {
+    const uint32_t tiles = (a.n + kTile - 1) / kTile;
+    if (tiles) k_out_fused<<<tiles, kThreads, 0, st>>>(a, lb, ticket, d_total, err, cap);
+}
+
 void launch_out_write(const OutArgs &a, hipStream_t st) {
     if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
 }

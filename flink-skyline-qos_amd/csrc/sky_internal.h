@@ -171,6 +171,10 @@ struct OutArgs {
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);
 void launch_out_write(const OutArgs &a, hipStream_t st);
+// count + prefix + write in one pass (decoupled look-back over tiles): lb [tiles] u64 and
+// *ticket zeroed by the caller; *d_total = selected tuples; writes positions < cap only
+void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket, uint32_t *d_total, uint32_t *err,
+                      int64_t cap, hipStream_t st);
 void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
                         const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,
                         double *rows_out, int32_t *keys_out, int64_t *mult_out, hipStream_t st);

@@ -295,18 +295,47 @@ def test_batched_readback_equals_per_range_copies(gpu_engine_factory, oracle, mo
 def test_candidate_prefilter_is_exact(dist, D, P_, algo, gpu_engine_factory, oracle, monkeypatch):
     """The candidate prefilter (second-level pruners drawn from the candidates, dropping the
     candidates they dominate before the sort) and the one-launch brute-force fates of small rep
-    sets never change a result: every on/off combination (SKY_PREFILTER, SKY_BRUTE) gives the
+    sets and the single-pass output never change a result: on/off combinations (SKY_PREFILTER,
+    SKY_BRUTE, SKY_FUSED_OUT) give the
     same ids, origins and |L_k| / survivors_k, equal to the oracle."""
     n = 150_000
     vals = oracle.synth(DISTS[dist], D, n, seed=900 + D + P_)
     res = []
-    for pre, brute in (("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")):
+    for pre, brute, fused in (("1", "1", "1"), ("0", "0", "0"), ("1", "0", "1"), ("0", "1", "0")):
         monkeypatch.setenv("SKY_PREFILTER", pre)
         monkeypatch.setenv("SKY_BRUTE", brute)
+        monkeypatch.setenv("SKY_FUSED_OUT", fused)
         res.append(run_query(gpu_engine_factory, vals, P_, algo))
     for r in res[1:]:
         for a, b in zip(res[0][0] + res[0][1], r[0] + r[1]):
             np.testing.assert_array_equal(a, b)
-    monkeypatch.setenv("SKY_PREFILTER", "1")
-    monkeypatch.setenv("SKY_BRUTE", "1")
+    for k in ("SKY_PREFILTER", "SKY_BRUTE", "SKY_FUSED_OUT"):
+        monkeypatch.setenv(k, "1")
     check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
+
+
+def test_device_query_capacity_and_buffer_reuse(gpu_engine_factory, oracle):
+    """sky_query_dev with too small an output (SKY_E_CAPACITY, the required count reported),
+    then with other output buffers on the same context: the single-pass output and the
+    count + write path agree, and a later run never reuses a stale output decision."""
+    from skyline._abi import SkylineError
+    n, D = 120_000, 4
+    vals = oracle.synth(2, D, n, seed=41)
+    exp, keys, _, _ = oracle.query_sfs("angle", vals, 8)
+    eng = gpu_engine_factory(D, 8)
+    dv = torch.from_numpy(vals).cuda()
+    di = torch.arange(n, dtype=torch.int64, device="cuda") * 3
+    small_i = torch.empty(5, dtype=torch.int64, device="cuda")
+    small_o = torch.empty(5, dtype=torch.int32, device="cuda")
+    with pytest.raises(SkylineError) as e:
+        eng.query_dev(di, dv, small_i, small_o, 5)
+    assert e.value.code == -3
+    for _ in range(2):
+        oi = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+        oo = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        g = eng.query_dev(di, dv, oi, oo, n)
+        eng.sync()
+        np.testing.assert_array_equal(oi[:g].cpu().numpy(), exp * 3)
+        np.testing.assert_array_equal(oo[:g].cpu().numpy(), keys[exp])
+        assert (oi[g:].cpu().numpy() == -1).all()
+    eng.close()
