@@ -710,7 +710,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.alive_g.ensure(std::max<size_t>(mt, 1)));
     SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
     uint32_t mr = 0;
-    if (mt) {
+    if (mt && !brute) {
         // ---- sort the candidates by (partition, score, hash)
         SKY_TRY(p.perm.ensure((size_t)mt * 4));
         SKY_TRY(p.key_alt.ensure((size_t)mt * 8));
@@ -780,23 +780,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_seg_bounds(p.rep_key.as<uint64_t>(), mt, p.totals.as<uint32_t>() + 1, p.seg_begin.as<uint32_t>(),
                           p.seg_end.as<uint32_t>(), st);
         STAGE(st, "dedup");
-        if (brute) {
-            // ---- small rep set: both skyline levels in one launch, no host round trip
-            //      (mr, the segment bounds and the flags come back with the final read)
-            if (tm) tm->mark(5, st);
-            SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
-            SKY_TRY(p.keep.ensure((size_t)mt * 4));              // per-rep domination bits
-            fill.add(p.segalive.p, (size_t)p.Kp * 4);
-            fill.add(p.keep.p, (size_t)mt * 4);
-            HIP_TRY(fill.launch(st));
-            c.ktimer_begin("brute", st);
-            launch_brute_fates(D, p.f64, p.rep_rows.p, p.rep_key.as<uint64_t>(), p.totals.as<uint32_t>() + 1, mt,
-                               in.global && !in.single, p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(),
-                               p.alive_g.as<uint8_t>(), p.segalive.as<uint32_t>(), st);
-            c.ktimer_end("brute", st, 0);
-            STAGE(st, "brute");
-            if (tm) tm->mark(6, st);
-        } else {
         std::vector<uint32_t> sb(p.Kp), se(p.Kp);
         uint32_t flags2 = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 1, 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
@@ -882,7 +865,28 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         } else {
             HIP_TRY(hipMemcpyAsync(p.alive_g.p, p.alive_l.p, mr, hipMemcpyDeviceToDevice, st));
         }
-        }   // !brute
+    } else if (brute) {
+        // ---- small slot set (typical after the prefilter): both skyline levels straight over
+        //      the candidate slots, duplicates included (equal vectors never dominate each other),
+        //      in one pair launch: no sort, no duplicate collapse, no SFS rounds, no host round
+        //      trip (the per-partition counts come back with the final read)
+        if (tm) tm->mark(4, st);
+        if (tm) tm->mark(5, st);
+        SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+        SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
+        SKY_TRY(p.keep.ensure((size_t)mt * 4));              // per-slot domination bits
+        SKY_TRY(p.slot_rep.ensure((size_t)mt * 4));
+        fill.add(p.segalive.p, (size_t)p.Kp * 4);
+        fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
+        fill.add(p.keep.p, (size_t)mt * 4);
+        HIP_TRY(fill.launch(st));
+        c.ktimer_begin("brute", st);
+        launch_brute_fates(D, p.s_rows->p, p.s_key->as<uint64_t>(), mt, in.global && !in.single,
+                           p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
+                           p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st);
+        c.ktimer_end("brute", st, (int64_t)mt * mt);
+        STAGE(st, "brute");
+        if (tm) tm->mark(6, st);
     }
     // stats: summed over slots (unit weights, computed origins) or, for given origins /
     // weights, over tuples in the count pass
@@ -964,24 +968,19 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const bool have_seg = mt && (brute || !p.h_seg_n.empty());
     p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
     if (brute) {
-        std::vector<uint32_t> sb(p.Kp), se(p.Kp);
-        uint32_t mr_b = 0, flags2 = 0;
+        uint32_t flags2 = 0;
+        p.h_seg_n.assign(p.Kp, 0u);
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                                  {p.segalive.p, (size_t)p.Kp * 4}, {p.totals.as<uint32_t>() + 1, 4},
-                                  {p.seg_begin.p, (size_t)p.Kp * 4}, {p.seg_end.p, (size_t)p.Kp * 4},
+                                  {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
                                   {p.flags.p, 4}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), &mr_b, sb.data(), se.data(), &flags2}));
+                          {&nout, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2}));
         if (flags2 & kFlagRadixSpin) {
-            set_error("radix sort look-back exceeded its spin bound");
+            set_error("a look-back (output) exceeded its spin bound");
             return SKY_E_HIP;
         }
-        p.mr = mr_b;
-        p.h_seg_n.resize(p.Kp);
+        p.mr = mt;                            // brute mode: slots (duplicates not collapsed)
         uint32_t alive_sum = 0;
-        for (int k = 0; k < p.Kp; k++) {
-            p.h_seg_n[k] = se[k] - sb[k];
-            alive_sum += p.h_seg_s[k];
-        }
+        for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
         p.mg = in.global && !in.single ? alive_sum : 0;
     } else {
         uint32_t flags3 = 0;

@@ -1206,32 +1206,47 @@ __global__ __launch_bounds__(kThreads) void k_out_fused(OutArgs a, unsigned long
     }
     uint32_t bt;
     uint32_t pl = block_scan_excl(nsel, s_w, bt);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
+        // wave-parallel look-back: 64 predecessors per step, nearest inclusive prefix by ballot
+        const int lane = threadIdx.x;
         unsigned long long excl = 0;
-        unsigned long long *mine = lb + tile;
-        if (tile == 0) {
-            __hip_atomic_store(mine, kLbInc | bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(mine, kLbAgg | bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t pt = (int64_t)tile - 1;
+        if (lane == 0)
+            __hip_atomic_store(lb + tile, (tile == 0 ? kLbInc : kLbAgg) | bt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tile > 0) {
+            int64_t end = (int64_t)tile - 1;
             uint32_t spins = 0;
-            while (pt >= 0) {
-                const unsigned long long sv =
-                    __hip_atomic_load(lb + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                const int64_t idx = end - lane;
+                const unsigned long long sv = idx >= 0 ? __hip_atomic_load(lb + idx, __ATOMIC_RELAXED,
+                                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                                       : kLbInc;                 // before tile 0: prefix 0
                 const unsigned long long f = sv & ~kLbCount;
-                if (f == 0ull) {
-                    if (++spins > (1u << 24)) { atomicOr(err, kFlagRadixSpin); break; }   // bounded spin
+                const uint64_t inc = __ballot(f == kLbInc), zero = __ballot(f == 0ull);
+                const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+                if (zero & upto) {                                   // a predecessor not yet published
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0) atomicOr(err, kFlagRadixSpin);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                excl += sv & kLbCount;
-                if (f == kLbInc) break;
-                pt--;
+                unsigned long long c = lane <= first ? (sv & kLbCount) : 0ull;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (first < 64) break;
+                end -= 64;
             }
-            __hip_atomic_store(mine, kLbInc | (excl + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(lb + tile, kLbInc | (excl + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        s_prefix = excl;
-        if (tile == ntiles - 1) *d_total = (uint32_t)(excl + bt);
+        if (lane == 0) {
+            s_prefix = excl;
+            if (tile == ntiles - 1) *d_total = (uint32_t)(excl + bt);
+        }
     }
 #pragma unroll
     for (int k = 0; k < kItems; k++) {

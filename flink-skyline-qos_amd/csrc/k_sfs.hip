@@ -596,29 +596,27 @@ void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr
     k_seg_alive<<<g, kThreads, 0, st>>>(rep_key, alive, mr, cnt);
 }
 
-// Both skyline levels of a SMALL representative set without sort, rounds or host round
-// trips: rep y is in L_k iff no rep of its partition dominates it, and in G iff no rep at
-// all dominates it (a dominator outside the union of the L_k is itself dominated by a
-// member of it: transitivity).  Full dominance test (reps of different partitions may be
-// equal vectors when keys are given).  A rep with a larger f32 score is skipped (the
-// clamped f64 sum rounded to f32 is monotone under dominance).
-//   k_brute_pairs   grid (y blocks of 64 = one wave, x chunks of 256 rows in LDS): the
+// Both skyline levels of a SMALL candidate-slot set without sort, duplicate collapse, rounds
+// or host round trips: slot y is in L_k iff no slot of its partition dominates it, and in G
+// iff no slot at all dominates it (a dominator outside the union of the L_k is itself
+// dominated by a member of it: transitivity).  Full dominance test in f64 (duplicates stay:
+// equal vectors never dominate each other, so they share their fate).  A slot with a larger
+// f32 score is skipped (the clamped f64 sum rounded to f32 is monotone under dominance).
+//   k_brute_pairs   grid (y blocks of 64 = one wave, x chunks of 64 rows in LDS): the
 //                   wave's lanes test their y against the chunk; hits are OR-ed into
 //                   domf[y] (bit0: same partition, bit1: any)
-//   k_brute_finish  alive_l / alive_g from domf, alive reps counted per partition
-// mr is read on the device; the grids cover the host's upper bound.
-constexpr int kBruteY = 64, kBruteX = 256;
-template <typename T, int D>
-__global__ __launch_bounds__(kBruteY) void k_brute_pairs(const T *__restrict__ rows, const uint64_t *__restrict__ key,
-                                                         const uint32_t *__restrict__ d_mr,
+//   k_brute_finish  alive_l / alive_g from domf, identity slot -> rep map, per-partition
+//                   slot and alive counts
+constexpr int kBruteY = 64, kBruteX = 64;
+template <int D>
+__global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restrict__ rows,
+                                                         const uint64_t *__restrict__ key, uint32_t mr,
                                                          uint32_t *__restrict__ domf) {
-    constexpr int DP = padded_dims<T>(D);
-    __shared__ T s_x[kBruteX * DP];
+    constexpr int DP = padded_dims<double>(D);
+    __shared__ double s_x[kBruteX * DP];
     __shared__ uint32_t s_k[kBruteX];                         // f32 order key of the score
     __shared__ uint32_t s_p[kBruteX];                         // partition
-    const uint32_t mr = *d_mr;
     const uint32_t y0 = blockIdx.x * kBruteY, x0 = blockIdx.y * kBruteX;
-    if (y0 >= mr || x0 >= mr) return;                        // block-uniform
     const uint32_t cn = mr - x0 < (uint32_t)kBruteX ? mr - x0 : (uint32_t)kBruteX;
     for (uint32_t q = threadIdx.x; q < cn * DP; q += kBruteY) s_x[q] = rows[(size_t)x0 * DP + q];
     for (uint32_t q = threadIdx.x; q < cn; q += kBruteY) {
@@ -628,49 +626,47 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const T *__restrict__ r
     }
     const uint32_t j = y0 + threadIdx.x;
     const bool valid = j < mr;
-    T y[DP];
+    double y[D];
 #pragma unroll
-    for (int d = 0; d < DP; d++) y[d] = valid ? rows[(size_t)j * DP + d] : T(0);
+    for (int d = 0; d < D; d++) y[d] = valid ? rows[(size_t)j * DP + d] : 0.0;
     const uint64_t ky = valid ? key[j] : 0ull;
     const uint32_t py = (uint32_t)(ky >> 56), sy = valid ? (uint32_t)(ky >> 24) : 0u;
     __syncthreads();
     uint32_t f = 0;
     for (uint32_t i = 0; i < cn; i++) {
         if (s_k[i] > sy) continue;                            // larger score: cannot dominate
-        if (!dominates_full<D, T>(s_x + (size_t)i * DP, y)) continue;
+        if (!dominates_full<D, double>(s_x + (size_t)i * DP, y)) continue;
         f |= s_p[i] == py ? 3u : 2u;
         if (f & 1u) break;                                    // settled
     }
     if (valid && f) atomicOr(&domf[j], f);
 }
 
-__global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key,
-                                                           const uint32_t *__restrict__ d_mr, int gmerge,
+__global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key, uint32_t mr, int gmerge,
                                                            const uint32_t *__restrict__ domf,
                                                            uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g,
-                                                           uint32_t *__restrict__ segalive) {
-    const uint32_t mr = *d_mr;
+                                                           uint32_t *__restrict__ segalive,
+                                                           uint32_t *__restrict__ segn, uint32_t *__restrict__ slot_rep) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j >= mr) return;
     const uint32_t f = domf[j];
     const bool in_l = !(f & 1u);
+    const uint32_t k = (uint32_t)(key[j] >> 56);
     alive_l[j] = in_l ? 1 : 0;
     alive_g[j] = (gmerge ? !(f & 2u) : in_l) ? 1 : 0;
-    if (in_l) atomicAdd(&segalive[key[j] >> 56], 1u);
+    slot_rep[j] = j;                                          // every slot is its own representative
+    atomicAdd(&segn[k], 1u);
+    if (in_l) atomicAdd(&segalive[k], 1u);
 }
 
-void launch_brute_fates(int D, bool f64, const void *rows, const uint64_t *key, const uint32_t *d_mr, uint32_t mr_max,
-                        bool gmerge, uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive,
+void launch_brute_fates(int D, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge, uint32_t *domf,
+                        uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn, uint32_t *slot_rep,
                         hipStream_t st) {
-    if (!mr_max) return;
-    const dim3 g((mr_max + kBruteY - 1) / kBruteY, (mr_max + kBruteX - 1) / kBruteX);
-    if (f64) {
-        SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, d_mr, domf)));
-    } else {
-        SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const float *)rows, key, d_mr, domf)));
-    }
-    k_brute_finish<<<(mr_max + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, d_mr, gmerge ? 1 : 0, domf, alive_l,
-                                                                             alive_g, segalive);
+    if (!mr) return;
+    const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
+    SKY_DISPATCH_D(D, (k_brute_pairs<DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+    k_brute_finish<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, mr, gmerge ? 1 : 0, domf, alive_l,
+                                                                         alive_g, segalive, segn, slot_rep);
 }
 
 // ---- launchers ------------------------------------------------------------------
