@@ -124,10 +124,22 @@ static bool prefilter_disabled() {
     const char *e = getenv("SKY_PREFILTER");
     return e && atoi(e) == 0;
 }
+static int prefilter_m2() {   // second-level pruners per partition (SKY_PREFILTER_M2, default 16)
+    static const int m = [] {
+        const char *e = getenv("SKY_PREFILTER_M2");
+        const int v = e ? atoi(e) : 16;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return m;
+}
 constexpr uint32_t kPrefilterMin = 4096;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = getenv("SKY_FUSED_OUT");
     return e && atoi(e) == 0;
+}
+static bool fused_onepass() {   // SKY_FUSED_OUT=2: the one-pass look-back output kernel
+    const char *e = getenv("SKY_FUSED_OUT");
+    return e && atoi(e) == 2;
 }
 static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
@@ -659,7 +671,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     //      outnumber what one small-SFS workgroup per partition handles)
     if (p.mt >= kPrefilterMin && !prefilter_disabled()) {
         const uint32_t mt0 = p.mt;
-        const int M2 = std::min(32, 2048 / p.Kp);
+        const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
         const int KM2 = p.Kp * M2;
         const int KM = p.Kp * p.M;
         SKY_TRY(p.cmin.ensure((size_t)KM2 * 8));
@@ -937,8 +949,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.fused_ids = in.out_ids;
     p.fused_org = in.out_org;
     c.ktimer_begin("out", st);
-    if (p.fused) {
-        // count + prefix + write in one pass (ids / origins straight into the caller's buffers)
+    if (p.fused && fused_onepass()) {
+        // count + prefix + write in one pass (decoupled look-back; A/B knob SKY_FUSED_OUT=2)
         SKY_TRY(p.lbuf.ensure((size_t)tiles * 8 + 64));
         fill.add(p.lbuf.p, (size_t)tiles * 8);
         fill.add(p.totals.as<uint32_t>() + 9, 4);          // ticket
@@ -950,6 +962,23 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         c.ktimer_begin("outw", st);
         launch_out_fused(oa, p.lbuf.as<unsigned long long>(), p.totals.as<uint32_t>() + 9,
                          p.totals.as<uint32_t>() + 3, p.flags.as<uint32_t>(), in.out_cap, st);
+        c.ktimer_end("outw", st, n);
+    } else if (p.fused) {
+        // count pass -> tile scan -> write pass, chained on the device (no host read in
+        // between; positions >= out_cap are not written, the final read reports the total)
+        c.ktimer_begin("outc", st);
+        launch_out_count(oa, st);
+        c.ktimer_end("outc", st, n);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), st);
+        OutArgs ow = oa;
+        ow.out_off = p.out_off.as<uint32_t>();
+        ow.ids = in.ids;
+        ow.ids_out = in.out_ids;
+        ow.origin_out = in.out_org;
+        ow.out_cap = in.out_cap;
+        c.ktimer_begin("outw", st);
+        launch_out_write(ow, st);
         c.ktimer_end("outw", st, n);
     } else {
         c.ktimer_begin("outc", st);

@@ -1152,12 +1152,13 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
         const uint32_t i = i0 + k;
         s_oid[pl] = idv[k];
         s_oorg[pl] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
-        if (a.rows_out)
+        if (a.rows_out && (int64_t)base + pl < a.out_cap)
             for (int d = 0; d < a.D; d++) a.rows_out[(size_t)(base + pl) * a.D + d] = a.vals[(size_t)i * a.D + d];
         pl++;
     }
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
+        if ((int64_t)base + q >= a.out_cap) break;
         if (a.ids_out) a.ids_out[base + q] = s_oid[q];
         if (a.origin_out) a.origin_out[base + q] = s_oorg[q];
     }

@@ -647,16 +647,25 @@ __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__res
                                                            uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g,
                                                            uint32_t *__restrict__ segalive,
                                                            uint32_t *__restrict__ segn, uint32_t *__restrict__ slot_rep) {
+    __shared__ uint32_t s_n[kMaxK], s_a[kMaxK];
+    for (int q = threadIdx.x; q < kMaxK; q += kThreads) { s_n[q] = 0; s_a[q] = 0; }
+    __syncthreads();
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    if (j >= mr) return;
-    const uint32_t f = domf[j];
-    const bool in_l = !(f & 1u);
-    const uint32_t k = (uint32_t)(key[j] >> 56);
-    alive_l[j] = in_l ? 1 : 0;
-    alive_g[j] = (gmerge ? !(f & 2u) : in_l) ? 1 : 0;
-    slot_rep[j] = j;                                          // every slot is its own representative
-    atomicAdd(&segn[k], 1u);
-    if (in_l) atomicAdd(&segalive[k], 1u);
+    if (j < mr) {
+        const uint32_t f = domf[j];
+        const bool in_l = !(f & 1u);
+        const uint32_t k = (uint32_t)(key[j] >> 56);
+        alive_l[j] = in_l ? 1 : 0;
+        alive_g[j] = (gmerge ? !(f & 2u) : in_l) ? 1 : 0;
+        slot_rep[j] = j;                                      // every slot is its own representative
+        atomicAdd(&s_n[k], 1u);                               // per-block counts, then one global add
+        if (in_l) atomicAdd(&s_a[k], 1u);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < kMaxK; q += kThreads) {
+        if (s_n[q]) atomicAdd(&segn[q], s_n[q]);
+        if (s_a[q]) atomicAdd(&segalive[q], s_a[q]);
+    }
 }
 
 void launch_brute_fates(int D, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge, uint32_t *domf,

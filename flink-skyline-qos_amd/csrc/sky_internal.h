@@ -167,6 +167,7 @@ struct OutArgs {
     int32_t *origin_out;
     double *rows_out;
     uint8_t *row_flags;           // optional per tuple: bit0 inL, bit1 inG
+    int64_t out_cap = INT64_MAX;  // write pass: output positions >= out_cap are not written
     int select_local;             // output tuples in L instead of G
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);

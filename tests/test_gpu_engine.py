@@ -301,7 +301,7 @@ def test_candidate_prefilter_is_exact(dist, D, P_, algo, gpu_engine_factory, ora
     n = 150_000
     vals = oracle.synth(DISTS[dist], D, n, seed=900 + D + P_)
     res = []
-    for pre, brute, fused in (("1", "1", "1"), ("0", "0", "0"), ("1", "0", "1"), ("0", "1", "0")):
+    for pre, brute, fused in (("1", "1", "1"), ("0", "0", "0"), ("1", "0", "2"), ("0", "1", "2")):
         monkeypatch.setenv("SKY_PREFILTER", pre)
         monkeypatch.setenv("SKY_BRUTE", brute)
         monkeypatch.setenv("SKY_FUSED_OUT", fused)
