@@ -72,10 +72,10 @@ def host_cores():
         return os.cpu_count() or 1
 
 
-def filter_roofline(eng, D):
+def filter_roofline(eng, D, kt=None):
     """k_filter over the timed launches: algorithmic bytes = the f64 row read once + the u16
     status word written (8D + 2 per tuple), / its HIP-event time."""
-    f_ms, f_launch, f_units = eng.kernel_time("filter")
+    f_ms, f_launch, f_units = kt if kt is not None else eng.kernel_time("filter")
     if not f_launch:
         return None
     bpt = D * 8 + 2
@@ -160,11 +160,13 @@ def make_stream(eng, dist_name, n, seed, id0, dev):
 
 
 def time_steps(step, eng, steps, warmup, distributed):
+    """W untimed steps, then K timed steps with the light kernel timers on (HIP events around
+    the timed kernels only: the roofline), then one untimed step with the phase events on."""
     for _ in range(warmup):
         step()
     eng.sync()
     torch.cuda.synchronize()
-    eng.profile(True)
+    eng.profile(1)
     eng.profile_reset()
     step_ms = []
     if distributed:
@@ -181,8 +183,12 @@ def time_steps(step, eng, steps, warmup, distributed):
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kt = eng.kernel_time("filter")   # the timed launches only
+    eng.profile(2)                   # phase split of one more (untimed) step
+    step()
+    eng.sync()
     eng.profile(False)
-    return elapsed, step_ms, g
+    return elapsed, step_ms, g, kt
 
 
 def config_line(name, dev, dev_index, steps, warmup, with_cpu):
@@ -194,9 +200,10 @@ def config_line(name, dev, dev_index, steps, warmup, with_cpu):
     vals, ids = make_stream(eng, cfg["dist"], n, seed, 0, dev)
     out_ids = torch.empty(n, dtype=torch.int64, device=dev)
     out_org = torch.empty(n, dtype=torch.int32, device=dev)
-    elapsed, step_ms, g = time_steps(lambda: eng.query_dev(ids, vals, out_ids, out_org, n), eng, steps, warmup, False)
+    elapsed, step_ms, g, kt = time_steps(lambda: eng.query_dev(ids, vals, out_ids, out_org, n), eng, steps, warmup,
+                                         False)
     phases, counters = eng.phases()
-    roof = filter_roofline(eng, D)
+    roof = filter_roofline(eng, D, kt)
     if roof:
         roof["traffic"] = traffic_for(n, D, cfg["dist"])
     ms = elapsed * 1e3 / steps
@@ -527,7 +534,7 @@ def main():
             return distributed_query(eng, ids, vals, out_ids, out_org, n)
         return eng.query_dev(ids, vals, out_ids, out_org, n)
 
-    elapsed, step_ms, g = time_steps(step, eng, args.steps, args.warmup, distributed)
+    elapsed, step_ms, g, kt = time_steps(step, eng, args.steps, args.warmup, distributed)
     p50 = statistics.median(step_ms)
     if distributed:
         t = torch.tensor([elapsed, p50], dtype=torch.float64, device=red_dev)
@@ -537,8 +544,8 @@ def main():
         dist.all_reduce(gt)
         g = int(gt.item())
     phases, counters = eng.phases()
-    roof = filter_roofline(eng, D)
-    dist_stats = eng.last_dist_stats if distributed else None
+    roof = filter_roofline(eng, D, kt)
+    dist_stats = getattr(eng, "last_dist_stats", None) if distributed else None
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -577,6 +584,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "p50_query_latency_ms": p50,
+            "step_ms": [round(x, 3) for x in step_ms],
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,

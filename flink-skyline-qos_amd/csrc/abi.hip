@@ -216,7 +216,7 @@ int sky_query_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int6
     ARG_CHECK(c && (n == 0 || d_values), "null argument");
     ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
     SKY_TRY(bind(c));
-    if (c->profile) {
+    if (c->profile >= 2) {
         if (!c->pt.ok) c->pt.init();
         c->pt.reset();
     }
@@ -230,7 +230,7 @@ int sky_query_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int6
     in.out_org = d_origin_out;
     in.out_cap = cap;
     c->shard_valid = false;
-    int r = pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr);
+    int r = pipe_run(*c, c->main, in, c->profile >= 2 ? &c->pt : nullptr);
     if (r == SKY_OK) {
         store_stats(c, c->main);
         r = pipe_output(*c, c->main, in, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr);
@@ -264,11 +264,11 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
     in.out_org = c->h_out_org.as<int32_t>();
     in.out_cap = n;
     c->shard_valid = false;
-    if (c->profile) {
+    if (c->profile >= 2) {
         if (!c->pt.ok) c->pt.init();
         c->pt.reset();
     }
-    SKY_TRY(pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr));
+    SKY_TRY(pipe_run(*c, c->main, in, c->profile >= 2 ? &c->pt : nullptr));
     store_stats(c, c->main);
     const int64_t g = c->main.nout;
     if (n_out) *n_out = g;
@@ -658,7 +658,7 @@ int sky_memcpy_d2h(sky_ctx *c, void *h_dst, const void *d_src, int64_t bytes) {
 
 int sky_profile_enable(sky_ctx *c, int on) {
     ARG_CHECK(c, "ctx is null");
-    c->profile = on != 0;
+    c->profile = on < 0 ? 0 : (on > 2 ? 2 : on);
     return SKY_OK;
 }
 int sky_profile_phases(sky_ctx *c, double *ms_out, int64_t *counters_out) {
@@ -972,11 +972,11 @@ static int stream_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out
     in.out_org = d_origin_out;
     in.out_cap = cap;
     c->shard_valid = false;
-    if (c->profile) {
+    if (c->profile >= 2) {
         if (!c->pt.ok) c->pt.init();
         c->pt.reset();
     }
-    SKY_TRY(pipe_run(*c, c->main, in, c->profile ? &c->pt : nullptr));
+    SKY_TRY(pipe_run(*c, c->main, in, c->profile >= 2 ? &c->pt : nullptr));
     store_stats(c, c->main);
     SKY_TRY(pipe_output(*c, c->main, in, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr));
     if (s->window == 0 && s->n) {   // landmark: keep only the local-skyline tuples, in arrival order

@@ -48,7 +48,7 @@ struct Ctx {
     Pipe main, aux;
     std::vector<int64_t> lsz, surv;
     int K_last = 0;
-    bool profile = false;
+    int profile = 0;            // 0 off, 1 kernel timers (HIP events per timed kernel), 2 + phase events
     PhaseTimer pt;
     double phase_ms[SKY_PHASES] = {};
     int64_t counters[8] = {};

@@ -893,7 +893,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         fill.add(p.keep.p, (size_t)mt * 4);
         HIP_TRY(fill.launch(st));
         c.ktimer_begin("brute", st);
-        launch_brute_fates(D, p.s_rows->p, p.s_key->as<uint64_t>(), mt, in.global && !in.single,
+        launch_brute_fates(D, !p.f64, p.s_rows->p, p.s_key->as<uint64_t>(), mt, in.global && !in.single,
                            p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
                            p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st);
         c.ktimer_end("brute", st, (int64_t)mt * mt);

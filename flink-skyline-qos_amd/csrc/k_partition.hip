@@ -637,7 +637,11 @@ __device__ __forceinline__ uint64_t emit_pruner(const double *pr, uint32_t part,
     constexpr int DP = padded_dims<T>(D);
     T tv[D];
 #pragma unroll
-    for (int d = 0; d < D; d++) tv[d] = (T)pr[d];
+    for (int d = 0; d < D; d++) {
+        tv[d] = (T)pr[d];
+        // a duplicated pruner is a slot like any candidate: its values decide the row type too
+        if ((double)(float)pr[d] != pr[d]) lflags |= kFlagNotF32;
+    }
     store_row<T, D>(rows_t + (size_t)slot * DP, tv);
     const uint64_t key = make_sortkey<T, D>(tv, part, lflags);
     sortkey[slot] = key;

@@ -608,17 +608,22 @@ void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr
 //   k_brute_finish  alive_l / alive_g from domf, identity slot -> rep map, per-partition
 //                   slot and alive counts
 constexpr int kBruteY = 64, kBruteX = 64;
-template <int D>
+// T: the compare type (f32 when every candidate value is exactly an f32, else f64); the slot
+// rows in HBM are f64 either way
+template <typename T, int D>
 __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
-    __shared__ double s_x[kBruteX * DP];
+    __shared__ T s_x[kBruteX * D];
     __shared__ uint32_t s_k[kBruteX];                         // f32 order key of the score
     __shared__ uint32_t s_p[kBruteX];                         // partition
     const uint32_t y0 = blockIdx.x * kBruteY, x0 = blockIdx.y * kBruteX;
     const uint32_t cn = mr - x0 < (uint32_t)kBruteX ? mr - x0 : (uint32_t)kBruteX;
-    for (uint32_t q = threadIdx.x; q < cn * DP; q += kBruteY) s_x[q] = rows[(size_t)x0 * DP + q];
+    for (uint32_t q = threadIdx.x; q < cn * D; q += kBruteY) {
+        const uint32_t r = q / D, d = q - r * D;
+        s_x[q] = (T)rows[(size_t)(x0 + r) * DP + d];
+    }
     for (uint32_t q = threadIdx.x; q < cn; q += kBruteY) {
         const uint64_t kx = key[x0 + q];
         s_k[q] = (uint32_t)(kx >> 24);                        // score bits 55..24
@@ -626,18 +631,18 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restric
     }
     const uint32_t j = y0 + threadIdx.x;
     const bool valid = j < mr;
-    double y[D];
+    T y[D];
 #pragma unroll
-    for (int d = 0; d < D; d++) y[d] = valid ? rows[(size_t)j * DP + d] : 0.0;
+    for (int d = 0; d < D; d++) y[d] = valid ? (T)rows[(size_t)j * DP + d] : T(0);
     const uint64_t ky = valid ? key[j] : 0ull;
     const uint32_t py = (uint32_t)(ky >> 56), sy = valid ? (uint32_t)(ky >> 24) : 0u;
     __syncthreads();
     uint32_t f = 0;
+#pragma unroll 4
     for (uint32_t i = 0; i < cn; i++) {
-        if (s_k[i] > sy) continue;                            // larger score: cannot dominate
-        if (!dominates_full<D, double>(s_x + (size_t)i * DP, y)) continue;
-        f |= s_p[i] == py ? 3u : 2u;
-        if (f & 1u) break;                                    // settled
+        const bool cand = s_k[i] <= sy;                       // a larger score cannot dominate
+        const bool dom = cand && dominates_full<D, T>(s_x + (size_t)i * D, y);
+        f |= dom ? (s_p[i] == py ? 3u : 2u) : 0u;
     }
     if (valid && f) atomicOr(&domf[j], f);
 }
@@ -668,12 +673,16 @@ __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__res
     }
 }
 
-void launch_brute_fates(int D, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge, uint32_t *domf,
-                        uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn, uint32_t *slot_rep,
-                        hipStream_t st) {
+void launch_brute_fates(int D, bool f32, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
+                        uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
+                        uint32_t *slot_rep, hipStream_t st) {
     if (!mr) return;
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
-    SKY_DISPATCH_D(D, (k_brute_pairs<DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+    if (f32) {
+        SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+    } else {
+        SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+    }
     k_brute_finish<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, mr, gmerge ? 1 : 0, domf, alive_l,
                                                                          alive_g, segalive, segn, slot_rep);
 }

@@ -235,9 +235,10 @@ void launch_stat_reduce(const unsigned long long *lsz, const unsigned long long 
 constexpr uint32_t kBruteMax = 16384;
 // over f64 candidate slots (rows [mr][pad(D)], sort keys): domf / segalive / segn zeroed by
 // the caller; writes alive_l / alive_g / slot_rep (identity) per slot
-void launch_brute_fates(int D, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge, uint32_t *domf,
-                        uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn, uint32_t *slot_rep,
-                        hipStream_t st);
+// f32: compare in f32 (every candidate value exactly an f32), else f64
+void launch_brute_fates(int D, bool f32, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
+                        uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
+                        uint32_t *slot_rep, hipStream_t st);
 void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st);
 void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
 

@@ -223,7 +223,9 @@ class SkylineEngine:
         check(lib().sky_ctx_sync(self.h))
 
     def profile(self, on=True):
-        check(lib().sky_profile_enable(self.h, 1 if on else 0))
+        """on: False/0 off, 1 kernel timers only, True/2 kernel timers + phase events."""
+        level = 2 if on is True else int(on)
+        check(lib().sky_profile_enable(self.h, level))
 
     def profile_reset(self):
         check(lib().sky_profile_reset(self.h))

@@ -221,6 +221,8 @@ int sky_memcpy_d2h(sky_ctx *ctx, void *h_dst, const void *d_src, int64_t bytes);
 /* profiling: HIP-event timings (ms) of the last query, per phase, and the
  * dominant streaming kernel's accumulated time / launch count since reset */
 #define SKY_PHASES 8
+/* on: 0 off; 1 HIP-event timers around the timed kernels only (light: usable inside a timed
+ * region); 2 also the per-phase events of sky_profile_phases */
 int sky_profile_enable(sky_ctx *ctx, int on);
 int sky_profile_phases(sky_ctx *ctx, double *ms_out /* SKY_PHASES */, int64_t *counters_out /* 8 */);
 int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t *launches,

@@ -339,3 +339,16 @@ def test_device_query_capacity_and_buffer_reuse(gpu_engine_factory, oracle):
         np.testing.assert_array_equal(oo[:g].cpu().numpy(), keys[exp])
         assert (oi[g:].cpu().numpy() == -1).all()
     eng.close()
+
+
+def test_duplicated_pruner_with_non_f32_values(gpu_engine_factory, oracle):
+    """A pruner (sample minimum) whose values are not exact f32 and that other tuples duplicate
+    becomes a slot: the row type must be f64 then, even if every candidate is f32-exact."""
+    rng = np.random.default_rng(5)
+    n, D = 200_000, 3
+    vals = rng.integers(1, 1000, size=(n, D)).astype(np.float64)
+    p = np.array([0.1, 0.2, 0.30000000000000004])          # not representable in f32
+    vals[::7] = p                                          # duplicated, and dominating most tuples
+    vals[3::11] = p + np.array([1e-9, 0.0, 0.0])           # dominated by p only in f64 arithmetic
+    for algo in ("mr-angle", "mr-dim"):
+        check_vs_oracle(gpu_engine_factory, oracle, vals, 8, algo)
