@@ -73,7 +73,7 @@ struct Pipe {
     DevBuf r16, r16g, r16a, r16b, i16a, i16b, dead16, keep16, scan16, xbuf16, xcnt16, xseg16, items16, at16, atv16;
     DevBuf scratch, flags, totals, orand, lsz, surv, statk, segalive;
     // candidate prefilter (second-level pruners) and its compaction targets
-    DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2;
+    DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2, rows3, sortkey3, slot_src3;
     // the candidate slots after the filter (rows / sortkey / slot_src) or, after the
     // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so
     // the stream-sized buffers keep their capacity across queries)

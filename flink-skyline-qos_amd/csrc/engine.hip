@@ -132,7 +132,8 @@ static int prefilter_m2() {   // second-level pruners per partition (SKY_PREFILT
     }();
     return m;
 }
-constexpr uint32_t kPrefilterMin = 4096;   // fewer slots: the SFS runs in one small pass anyway
+constexpr uint32_t kPrefilterMin = 4096;
+constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = getenv("SKY_FUSED_OUT");
     return e && atoi(e) == 0;
@@ -669,27 +670,31 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // ---- candidate prefilter: second-level pruners drawn from the candidates drop the
     //      candidates they dominate before the sort (worth it once the candidates
     //      outnumber what one small-SFS workgroup per partition handles)
-    if (p.mt >= kPrefilterMin && !prefilter_disabled()) {
+    // rounds: a round's survivors draw new pruners; another round runs only while the
+    // survivors are still too many for the brute path and the last round cut them by > 30 %
+    for (int round = 0; round < kPrefilterRounds && p.mt >= kPrefilterMin && !prefilter_disabled(); round++) {
         const uint32_t mt0 = p.mt;
         const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
         const int KM2 = p.Kp * M2;
         const int KM = p.Kp * p.M;
+        DevBuf *dr = round & 1 ? &p.rows3 : &p.rows2, *dk = round & 1 ? &p.sortkey3 : &p.sortkey2,
+               *ds = round & 1 ? &p.slot_src3 : &p.slot_src2;
         SKY_TRY(p.cmin.ensure((size_t)KM2 * 8));
         SKY_TRY(p.pr2.ensure((size_t)KM2 * D * 8));
         SKY_TRY(p.npr2.ensure((size_t)p.Kp * 4));
         SKY_TRY(p.live.ensure((size_t)mt0 * 4));
         SKY_TRY(p.livepos.ensure((size_t)(mt0 + 1) * 4));
-        SKY_TRY(p.rows2.ensure((size_t)mt0 * rb64));
-        SKY_TRY(p.sortkey2.ensure((size_t)mt0 * 8));
-        SKY_TRY(p.slot_src2.ensure((size_t)mt0 * 4));
+        SKY_TRY(dr->ensure((size_t)mt0 * rb64));
+        SKY_TRY(dk->ensure((size_t)mt0 * 8));
+        SKY_TRY(ds->ensure((size_t)mt0 * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(mt0 + 1) * 4 + 64));
         fill.add(p.cmin.p, (size_t)KM2 * 8, 0xff);
         HIP_TRY(fill.launch(st));
         CandArgs ca{};
         ca.mt = mt0;
-        ca.rows = p.rows.as<double>();
-        ca.key = p.sortkey.as<uint64_t>();
-        ca.src = p.slot_src.as<uint32_t>();
+        ca.rows = p.s_rows->as<double>();
+        ca.key = p.s_key->as<uint64_t>();
+        ca.src = p.s_src->as<uint32_t>();
         ca.Kp = p.Kp;
         ca.M2 = M2;
         ca.cmin = p.cmin.as<unsigned long long>();
@@ -700,17 +705,19 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         launch_cand_prefilter(D, ca, st);
         scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), mt0, p.totals.as<uint32_t>() + 8, p.scratch.as<uint32_t>(),
                       st);
-        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), p.rows2.as<double>(), p.sortkey2.as<uint64_t>(),
-                            p.slot_src2.as<uint32_t>(), p.pruner_slot.as<int32_t>(), KM, st);
+        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(), ds->as<uint32_t>(),
+                            p.pruner_slot.as<int32_t>(), KM, st);
         c.ktimer_end("prefilter", st, mt0);
         STAGE(st, "prefilter");
         uint32_t live_n = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 8, 4}}, {&live_n}));
-        p.s_rows = &p.rows2;
-        p.s_key = &p.sortkey2;
-        p.s_src = &p.slot_src2;
+        p.s_rows = dr;
+        p.s_key = dk;
+        p.s_src = ds;
         p.mt = live_n;
-        if (debug_level() >= 3) fprintf(stderr, "[sky] prefilter %u -> %u slots (M2=%d)\n", mt0, live_n, M2);
+        if (debug_level() >= 3)
+            fprintf(stderr, "[sky] prefilter round %d: %u -> %u slots (M2=%d)\n", round, mt0, live_n, M2);
+        if (live_n <= kBruteMax || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
     }
     const uint32_t mt = p.mt;
     // small candidate sets (typical after the prefilter): both skyline levels by one
