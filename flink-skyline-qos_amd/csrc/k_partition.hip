@@ -695,12 +695,23 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
 // the criterion, re-checked exactly below) prune every other candidate of that partition by
 // one brute-force pass (|candidates| x M2 pair tests) before the sort.  A candidate they
 // dominate is outside L_k; equal vectors are never dropped.  Exactness: dominance in f64.
+// Criterion j: a positive-weight sum with pseudo-random weights in [1, 2) (j = 0: the plain
+// sum).  Non-integer weights make ties between distinct integer-valued candidates rare, so
+// the winner of a criterion does not depend on the (unordered) slot order that breaks ties.
+__device__ __forceinline__ float cand_weight(int j, int d) {
+    uint32_t h = (uint32_t)(j * 0x9E3779B1u) ^ (uint32_t)((d + 1) * 0x85EBCA77u);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    return 1.0f + (float)(h >> 8) * (1.0f / 16777216.0f);
+}
 template <int D>
 __device__ __forceinline__ float cand_criterion(const float (&f)[D], float sum, int j) {
     if (j == 0) return sum;
-    if (j <= D) return sum + 3.0f * f[j - 1];
-    const int a = (j - 1) % D, b = (j - 1 + 1 + (j - 1) / D) % D;
-    return sum + 3.0f * (f[a] + f[b]);
+    float c = 0.0f;
+#pragma unroll
+    for (int d = 0; d < D; d++) c += cand_weight(j, d) * f[d];
+    return c;
 }
 
 template <int D>
