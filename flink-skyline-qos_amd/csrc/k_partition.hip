@@ -695,22 +695,31 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
 // the criterion, re-checked exactly below) prune every other candidate of that partition by
 // one brute-force pass (|candidates| x M2 pair tests) before the sort.  A candidate they
 // dominate is outside L_k; equal vectors are never dropped.  Exactness: dominance in f64.
-// Criterion j: a positive-weight sum with pseudo-random weights in [1, 2) (j = 0: the plain
-// sum).  Non-integer weights make ties between distinct integer-valued candidates rare, so
-// the winner of a criterion does not depend on the (unordered) slot order that breaks ties.
-__device__ __forceinline__ float cand_weight(int j, int d) {
-    uint32_t h = (uint32_t)(j * 0x9E3779B1u) ^ (uint32_t)((d + 1) * 0x85EBCA77u);
+// Criterion j: a positive-weight sum.  Base weights spread the winners along the front
+// (j % 16 == 0: the plain sum; 1..D: one dimension weighted 4x, pulling towards a corner;
+// above: pairs), plus a small deterministic perturbation (< 1e-4 per weight) that breaks the
+// ties of integer-valued data by a fixed secondary order instead of by the (unordered) slot
+// order; criteria j and j + 16 share the base and differ in the tie-break.
+__device__ __forceinline__ float cand_eps(int j, int d) {
+    uint32_t h = (uint32_t)((j + 1) * 0x9E3779B1u) ^ (uint32_t)((d + 1) * 0x85EBCA77u);
     h ^= h >> 15;
     h *= 0x2C1B3C6Du;
     h ^= h >> 12;
-    return 1.0f + (float)(h >> 8) * (1.0f / 16777216.0f);
+    return (float)(h >> 8) * (1e-4f / 16777216.0f);
 }
 template <int D>
 __device__ __forceinline__ float cand_criterion(const float (&f)[D], float sum, int j) {
-    if (j == 0) return sum;
+    const int b = j & 15;
+    int da = -1, db = -1;
+    if (b >= 1 && b <= D) da = b - 1;
+    else if (b > D) { da = (b - 1) % D; db = (b - 1 + 1 + (b - 1) / D) % D; }
     float c = 0.0f;
 #pragma unroll
-    for (int d = 0; d < D; d++) c += cand_weight(j, d) * f[d];
+    for (int d = 0; d < D; d++) {
+        const float w = 1.0f + (d == da ? 3.0f : 0.0f) + (d == db ? 3.0f : 0.0f) + cand_eps(j, d);
+        c += w * f[d];
+    }
+    (void)sum;
     return c;
 }
 
