@@ -74,6 +74,10 @@ struct Pipe {
     DevBuf scratch, flags, totals, orand, lsz, surv, statk, segalive;
     // candidate prefilter (second-level pruners) and its compaction targets
     DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2, rows3, sortkey3, slot_src3;
+    // bounding-box pruned all-pairs pass over large rep sets (k_mbr.hip)
+    DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_domf,
+        mbr_pairs;
+    bool used_mbr = false;
     // the candidate slots after the filter (rows / sortkey / slot_src) or, after the
     // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so
     // the stream-sized buffers keep their capacity across queries)

@@ -142,6 +142,22 @@ static bool fused_onepass() {   // SKY_FUSED_OUT=2: the one-pass look-back outpu
     const char *e = getenv("SKY_FUSED_OUT");
     return e && atoi(e) == 2;
 }
+// SKY_MBR=0 keeps the round-based SFS for large rep sets (A/B knob, read per query);
+// SKY_MBR_MIN: smallest rep count for the bounding-box pruned all-pairs pass
+static bool mbr_disabled() {
+    const char *e = getenv("SKY_MBR");
+    return e && atoi(e) == 0;
+}
+static uint32_t mbr_min() {
+    const char *e = getenv("SKY_MBR_MIN");
+    return e ? (uint32_t)atoi(e) : 16384u;
+}
+// SKY_MBR_ROWMIN: reachable y lanes from which an x tile's rows are scanned row by row
+// (fewer: the tile is loaded one row per lane and the reachable y are broadcast)
+static int mbr_row_min() {
+    const char *e = getenv("SKY_MBR_ROWMIN");
+    return e ? atoi(e) : 24;
+}
 static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
     return e && atoi(e) == 0;
@@ -532,6 +548,71 @@ static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const 
     return SKY_OK;
 }
 
+// both skyline levels of the rep set in one bounding-box pruned all-pairs pass (k_mbr.hip)
+static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) {
+    hipStream_t st = c.st;
+    const int D = c.D;
+    const int fmt = p.u16 ? 0 : (p.f64 ? 2 : 1);
+    const int NW = mbr_row_words(D, fmt);
+    const size_t ntiles = mbr_tiles(mr);
+    const void *rows = p.rep_rows.p;
+    if (fmt == 0) {
+        SKY_TRY(p.r16.ensure((size_t)mr * NW * 4));
+        launch_pack16(D, p.rep_rows.as<float>(), mr, nullptr, p.r16.as<uint32_t>(), st);
+        rows = p.r16.p;
+    }
+    SKY_TRY(p.mbr_mm.ensure((size_t)D * 8));
+    SKY_TRY(p.mbr_code.ensure((size_t)mr * 8));
+    SKY_TRY(p.mbr_code2.ensure((size_t)mr * 8));
+    SKY_TRY(p.mbr_idx.ensure((size_t)mr * 4));
+    SKY_TRY(p.mbr_idx2.ensure((size_t)mr * 4));
+    SKY_TRY(p.mbr_rows.ensure(ntiles * 64 * NW * 4));
+    SKY_TRY(p.mbr_part.ensure((size_t)mr * 4));
+    SKY_TRY(p.mbr_min.ensure(ntiles * NW * 4));
+    SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
+    SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
+    SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
+    SKY_TRY(p.mbr_pairs.ensure(8));
+    SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
+    FillSet fill;
+    fill.add(p.mbr_mm.p, (size_t)D * 4, 0xff);
+    fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
+    fill.add(p.mbr_pairs.p, 8, 0);
+    HIP_TRY(fill.launch(st));
+    MbrArgs a;
+    a.D = D;
+    a.fmt = fmt;
+    a.rows = rows;
+    a.rep_key = p.rep_key.as<uint64_t>();
+    a.mr = mr;
+    a.gmerge = gmerge;
+    a.full = fmt != 0 || in.keys != nullptr;   // ±0 twins (f32/f64) or vectors repeated across given keys
+    a.row_min = mbr_row_min();
+    a.mm = p.mbr_mm.as<uint32_t>();
+    a.code = p.mbr_code.as<uint64_t>();
+    a.code_alt = p.mbr_code2.as<uint64_t>();
+    a.idx = p.mbr_idx.as<uint32_t>();
+    a.idx_alt = p.mbr_idx2.as<uint32_t>();
+    a.radix_scratch = p.scratch.as<uint32_t>();
+    a.err = p.flags.as<uint32_t>();
+    a.trows = p.mbr_rows.as<uint32_t>();
+    a.tpart = p.mbr_part.as<uint32_t>();
+    a.tmin = p.mbr_min.as<uint32_t>();
+    a.tmax = p.mbr_max.as<uint32_t>();
+    a.tprange = p.mbr_pr.as<uint32_t>();
+    a.domf = p.mbr_domf.as<uint32_t>();
+    a.pairs = p.mbr_pairs.as<unsigned long long>();
+    a.alive_l = p.alive_l.as<uint8_t>();
+    a.alive_g = p.alive_g.as<uint8_t>();
+    c.ktimer_begin("mbr", st);
+    HIP_TRY(launch_mbr(a, st));
+    c.ktimer_end("mbr", st, mr);
+    STAGE(st, "mbr");
+    p.used_mbr = true;
+    p.sfs_rounds++;
+    return SKY_OK;
+}
+
 int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     hipStream_t st = c.st;
     const int D = c.D;
@@ -542,6 +623,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
     p.fused = false;
+    p.used_mbr = false;
     p.sfs_rounds = p.sfs_pairs_upper = 0;
     p.h_seg_n.clear();
     p.h_seg_s.clear();
@@ -825,7 +907,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         }
         HIP_TRY(fill.launch(st));
         const int W16 = dom16_words(D);
-        if (p.u16) {
+        const bool use_mbr = mr >= mbr_min() && !mbr_disabled();
+        if (use_mbr) {
+            SKY_TRY(mbr_run(c, p, in, mr, gmerge));
+        } else if (p.u16) {
             SKY_TRY(p.r16.ensure((size_t)std::max<uint32_t>(mr, 1) * W16 * 4));
             launch_pack16(D, p.rep_rows.as<float>(), mr, nullptr, p.r16.as<uint32_t>(), st);
             SKY_TRY(sfs_run16(c, p, p.r16.as<uint32_t>(), mr, sb, se, p.alive_l.as<uint8_t>(), W16));
@@ -837,8 +922,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.h_seg_n.assign(se.begin(), se.end());
         if (tm) tm->mark(6, st);
 
-        // ---- global merge over the union of the local skylines
-        if (gmerge) {
+        // ---- global merge over the union of the local skylines (the all-pairs pass did both)
+        if (use_mbr) {
+        } else if (gmerge) {
             SKY_TRY(p.alive_u32.ensure((size_t)mr * 4));
             SKY_TRY(p.alive_scan.ensure((size_t)mr * 4));
             SKY_TRY(p.gkey.ensure((size_t)mr * 8));
@@ -1020,9 +1106,17 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.mg = in.global && !in.single ? alive_sum : 0;
     } else {
         uint32_t flags3 = 0;
+        unsigned long long mbr_pairs = 0;
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3}));
+                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
+                                  {p.mbr_pairs.p, p.used_mbr ? 8u : 0u}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, &mbr_pairs}));
+        if (p.used_mbr) {
+            p.sfs_pairs_upper = (int64_t)mbr_pairs;     // pair tests the pruned pass executed
+            uint32_t alive_sum = 0;
+            for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
+            p.mg = in.global && !in.single ? alive_sum : 0;
+        }
         if (flags3 & kFlagRadixSpin) {
             set_error("a look-back (radix sort / output) exceeded its spin bound");
             return SKY_E_HIP;

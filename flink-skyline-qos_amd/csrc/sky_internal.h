@@ -261,6 +261,32 @@ void launch_move16(int W, const uint32_t *keep, const uint32_t *scan, uint32_t n
                    const uint32_t *rows, uint32_t *idx_out, uint32_t *rows_out, hipStream_t st);
 void launch_gather_u32(const uint32_t *src, const uint32_t *at, uint32_t n, uint32_t *out, hipStream_t st);
 
+// ---- k_mbr.hip (both skyline levels of a large rep set, bounding-box pruned all-pairs) ----
+struct MbrArgs {
+    int D = 0;
+    int fmt = 0;                  // 0: packed u16 rows (dom16 layout), 1: f32 rows, 2: f64 rows
+    const void *rows = nullptr;   // [mr][mbr_row_words] by rep
+    const uint64_t *rep_key = nullptr;   // partition in bits 63..56
+    uint32_t mr = 0;
+    bool gmerge = false;          // the global level (alive_g) too
+    bool full = false;            // complete dominance test (rows may repeat a vector)
+    int row_min = 24;             // y lanes in reach of an x tile from which its rows are scanned
+    uint32_t *mm = nullptr;       // [2D]: {0xffffffff} x D, {0} x D on entry
+    uint64_t *code = nullptr, *code_alt = nullptr;   // [mr]
+    uint32_t *idx = nullptr, *idx_alt = nullptr;     // [mr]
+    uint32_t *radix_scratch = nullptr, *err = nullptr;
+    uint32_t *trows = nullptr;    // [ntiles*64][NW]
+    uint32_t *tpart = nullptr;    // [mr]
+    uint32_t *tmin = nullptr, *tmax = nullptr;       // [NW][ntiles]
+    uint32_t *tprange = nullptr;  // [ntiles]
+    uint32_t *domf = nullptr;     // [mr]
+    unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
+    uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
+};
+int mbr_row_words(int D, int fmt);
+size_t mbr_tiles(uint32_t mr);
+hipError_t launch_mbr(const MbrArgs &a, hipStream_t st);
+
 // ---- k_synth.hip ----
 void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
                   int64_t *ids, hipStream_t st);

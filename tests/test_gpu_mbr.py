@@ -1,0 +1,110 @@
+"""The bounding-box pruned all-pairs pass over large representative sets (k_mbr.hip):
+both skyline levels (L_k, G) in one launch instead of the SFS rounds.  Forced onto small
+sets (SKY_MBR_MIN=1, brute path off) it must equal the oracle for every row type (packed
+u16, f32, f64 with +-0 twins / ties / infinities / negatives), every partitioner, the
+single-partition callers (global merge of lists, the per-key operator state), and at scale
+it must equal the round-based SFS (SKY_MBR=0) that the round-1 suite pinned."""
+import numpy as np
+import pytest
+
+from test_gpu_engine import DISTS, check_vs_oracle, run_query
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def force_mbr(monkeypatch):
+    monkeypatch.setenv("SKY_MBR", "1")
+    monkeypatch.setenv("SKY_MBR_MIN", "1")
+    monkeypatch.setenv("SKY_BRUTE", "0")
+    yield monkeypatch
+
+
+@pytest.mark.parametrize("dist,D,P_,algo,n", [("std_anti", 8, 16, "mr-angle", 20000),
+                                              ("std_anti", 3, 8, "mr-dim", 40000),
+                                              ("anti_correlated", 4, 8, "mr-angle", 60000),
+                                              ("anti_correlated", 8, 16, "mr-angle", 60000),
+                                              ("uniform", 6, 256, "mr-angle", 60000),
+                                              ("correlated", 4, 8, "mr-grid", 60000),
+                                              ("mixed", 6, 8, "mr-angle", 200000),
+                                              ("uniform", 1, 4, "mr-dim", 30000),
+                                              ("std_anti", 16, 8, "mr-angle", 8000),
+                                              ("std_anti", 12, 4, "mr-grid", 8000)])
+@pytest.mark.parametrize("prefilter,rowmin", [("1", "24"), ("0", "0"), ("0", "65")])
+def test_mbr_vs_oracle(dist, D, P_, algo, n, prefilter, rowmin, force_mbr, gpu_engine_factory, oracle):
+    """rowmin 0: every reachable x tile scanned row by row; 65: always one row per lane with
+    the reachable y broadcast; 24: the default mix."""
+    force_mbr.setenv("SKY_PREFILTER", prefilter)
+    force_mbr.setenv("SKY_MBR_ROWMIN", rowmin)
+    vals = oracle.synth(DISTS[dist], D, n, seed=300 + D + P_)
+    check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
+    force_mbr.setenv("SKY_SFS16", "0")                    # the same reps as f32 rows
+    check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
+
+
+def test_mbr_generic_rows(force_mbr, gpu_engine_factory, oracle):
+    """f64 rows (values not exact in f32), score ties, +-0 twins, infinities, negatives."""
+    rng = np.random.default_rng(11)
+    cases = []
+    v = rng.integers(0, 50, size=(30000, 4)).astype(np.float64) + 0.1   # not f32-exact -> f64 rows
+    cases.append(v)
+    v = rng.integers(0, 8, size=(30000, 5)).astype(np.float64)          # many equal scores
+    cases.append(v)
+    v = rng.integers(-3, 3, size=(20000, 3)).astype(np.float64) * 0.5   # negatives, +-0
+    v[v == 0] = np.where(rng.random((v == 0).sum()) < 0.5, -0.0, 0.0)
+    cases.append(v)
+    v = rng.integers(0, 100, size=(20000, 3)).astype(np.float64)
+    v[::97, 1] = np.inf
+    v[5::89, 2] = -np.inf
+    cases.append(v)
+    for vals in cases:
+        for algo, P_ in (("mr-angle", 8), ("mr-dim", 4)):
+            check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
+
+
+def test_mbr_single_partition_callers(force_mbr, gpu_engine_factory, oracle):
+    """sky_global_merge (one partition, given origins) and the per-key operator state
+    (sky_part_insert: local level only) through the pruned pass."""
+    from skyline.operators import _LocalPart
+    rng = np.random.default_rng(3)
+    eng = gpu_engine_factory(4, 8)
+    lists_v, lists_i, pids = [], [], []
+    off = 0
+    for k in range(5):
+        nk = int(rng.integers(1000, 6000))
+        v = oracle.synth(3, 4, nk, seed=40 + k)
+        lists_v.append(v)
+        lists_i.append(np.arange(off, off + nk, dtype=np.int64))
+        pids.append(k)
+        off += nk
+    gids, gorg = eng.global_merge(pids, lists_i, lists_v)
+    allv = np.concatenate(lists_v)
+    alli = np.concatenate(lists_i)
+    exp, _, _, _ = oracle.query_sfs("dim", allv, 1)
+    assert sorted(gids.tolist()) == sorted(alli[exp].tolist())
+    vals = oracle.synth(3, 4, 23000, seed=6)
+    ids = np.arange(len(vals), dtype=np.int64) + 7
+    part = _LocalPart(eng, 3)
+    for s in range(0, len(vals), 5000):
+        part.insert(ids[s:s + 5000], vals[s:s + 5000])
+        got_ids, got_vals = part.snapshot()
+        exp, _, _, _ = oracle.query_sfs("dim", vals[:s + 5000], 1)
+        np.testing.assert_array_equal(got_ids, ids[exp])
+        np.testing.assert_array_equal(got_vals, vals[exp])
+    part.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("dist,D,n", [("std_anti", 8, 300000), ("std_anti", 5, 400000),
+                                      ("uniform", 6, 400000), ("anti_correlated", 4, 400000)])
+def test_mbr_equals_sfs_at_scale(dist, D, n, gpu_engine_factory, oracle, monkeypatch):
+    """Beyond the oracle's reach: the pruned all-pairs pass (default for >= 16384 reps) and
+    the round-based SFS give the same ids, origins and |L_k| / survivors_k."""
+    vals = oracle.synth(DISTS[dist], D, n, seed=700 + D)
+    res = []
+    for mbr in ("1", "0"):
+        monkeypatch.setenv("SKY_MBR", mbr)
+        (ids, org), (ls, sv) = run_query(gpu_engine_factory, vals, 16, "mr-angle")
+        res.append((ids, org, ls, sv))
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
