@@ -152,12 +152,6 @@ static uint32_t mbr_min() {
     const char *e = getenv("SKY_MBR_MIN");
     return e ? (uint32_t)atoi(e) : 16384u;
 }
-// SKY_MBR_ROWMIN: reachable y lanes from which an x tile's rows are scanned row by row
-// (fewer: the tile is loaded one row per lane and the reachable y are broadcast)
-static int mbr_row_min() {
-    const char *e = getenv("SKY_MBR_ROWMIN");
-    return e ? atoi(e) : 24;
-}
 static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
     return e && atoi(e) == 0;
@@ -587,7 +581,10 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.mr = mr;
     a.gmerge = gmerge;
     a.full = fmt != 0 || in.keys != nullptr;   // ±0 twins (f32/f64) or vectors repeated across given keys
-    a.row_min = mbr_row_min();
+    {
+        const char *e = getenv("SKY_MBR_DBG");
+        a.dbg = e ? atoi(e) : 0;
+    }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
     a.code_alt = p.mbr_code2.as<uint64_t>();

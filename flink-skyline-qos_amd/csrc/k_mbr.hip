@@ -160,6 +160,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_minmax(const uint32_t *__restr
             hi[d] = max(hi[d], o);
         }
     }
+    __shared__ uint32_t s_lo[kThreads / 64][D], s_hi[kThreads / 64][D];
 #pragma unroll
     for (int d = 0; d < D; d++) {
 #pragma unroll
@@ -167,13 +168,20 @@ __global__ __launch_bounds__(kThreads) void k_mbr_minmax(const uint32_t *__restr
             lo[d] = min(lo[d], (uint32_t)__shfl_xor((int)lo[d], o, 64));
             hi[d] = max(hi[d], (uint32_t)__shfl_xor((int)hi[d], o, 64));
         }
-    }
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int d = 0; d < D; d++) {
-            atomicMin(&mm[d], lo[d]);
-            atomicMax(&mm[D + d], hi[d]);
+        if ((threadIdx.x & 63) == 0) {
+            s_lo[threadIdx.x >> 6][d] = lo[d];
+            s_hi[threadIdx.x >> 6][d] = hi[d];
         }
+    }
+    __syncthreads();
+    if (threadIdx.x < D) {          // one atomic per dimension and block
+        uint32_t a = s_lo[0][threadIdx.x], b = s_hi[0][threadIdx.x];
+        for (int q = 1; q < kThreads / 64; q++) {
+            a = min(a, s_lo[q][threadIdx.x]);
+            b = max(b, s_hi[q][threadIdx.x]);
+        }
+        atomicMin(&mm[threadIdx.x], a);
+        atomicMax(&mm[D + threadIdx.x], b);
     }
 }
 
@@ -262,118 +270,186 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
 // vector across partitions, and f32/f64 rows may hold -0.0 / +0.0 twins; otherwise the rows
 // are distinct vectors and "x <= y, x at another position" is dominance.
 // GM: the global level is wanted (bit 1); else only the same-partition bit matters.
+//
+// Software pipeline: the scan finds the next reachable x tile and issues the load of its
+// rows (one row per lane) before the current tile is tested, so a wave keeps a tile load in
+// flight while it computes (8 waves per SIMD alone do not hide the HBM / L2 latency of
+// ~250 dependent tile loads per y tile).
 template <class R, bool FULL, bool GM>
 __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tmax,
                                                         const uint32_t *__restrict__ tprange, uint32_t mr,
-                                                        uint32_t ntiles, int row_min, uint32_t *__restrict__ domf,
+                                                        uint32_t ntiles, int dbg, uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs) {
     constexpr int NW = R::NW;
-    const uint32_t yt = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
+    // XCD b % 8; give each XCD a contiguous run of y tiles, whose reachable x tiles then
+    // overlap and stay in that XCD's L2 (the grid is padded to a multiple of 8)
+    const uint32_t per_xcd = gridDim.x / 8u;
+    const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+    const uint32_t yt = __builtin_amdgcn_readfirstlane(blk * (kThreads / 64) + (threadIdx.x >> 6));
     if (yt >= ntiles) return;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
     const bool valid = j < mr;
     uint32_t y[NW], ymax[NW];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)min(j, mr - 1u) * NW);
 #pragma unroll
-    for (int w = 0; w < NW; w++) y[w] = valid ? trows[(size_t)j * NW + w] : 0u;
+        for (int q = 0; q < NW / 4; q++) {
+            const uint4 v = src[q];
+            y[4 * q] = v.x;
+            y[4 * q + 1] = v.y;
+            y[4 * q + 2] = v.z;
+            y[4 * q + 3] = v.w;
+        }
+    }
 #pragma unroll
     for (int w = 0; w < NW; w++) ymax[w] = tmax[(size_t)w * ntiles + yt];
     const uint32_t yr = tprange[yt];
     const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
-    const uint32_t py = valid ? tpart[j] : 0xffffffffu;
+    const uint32_t py = valid ? tpart[min(j, mr - 1u)] : 0xffffffffu;
+    // this wave's y rows and partitions in LDS for the broadcast reads of the tests
+    __shared__ uint32_t s_y[kThreads / 64][64 * NW];
+    __shared__ uint32_t s_py[kThreads / 64][64];
+    uint32_t *sy = s_y[threadIdx.x >> 6], *spy = s_py[threadIdx.x >> 6];
+#pragma unroll
+    for (int w = 0; w < NW; w++) sy[lane * NW + w] = y[w];
+    spy[lane] = py;
+    __builtin_amdgcn_wave_barrier();
     uint32_t f = 0;
     uint64_t live = __ballot(valid);
     uint64_t npairs = 0;
-    // the next 64 tiles' min corners are loaded while the current ones are processed
-    uint32_t tn[NW];
+    // per wave: the reachable x tiles of the current group of 64 (tile index, lane mask)
+    __shared__ uint32_t s_lx[kThreads / 64][64];
+    __shared__ uint64_t s_lm[kThreads / 64][64];
+    uint32_t *lx = s_lx[threadIdx.x >> 6];
+    uint64_t *lmq = s_lm[threadIdx.x >> 6];
+    constexpr int BT = NW <= 8 ? 4 : 2;        // x tiles loaded together (independent loads in flight)
+
+    // loads are unconditional (clamped index; flags mask the values): conditional loads make
+    // the compiler wait for every load in flight
+    auto load_group = [&](uint32_t (&tg)[NW], uint32_t &tr, uint32_t g) {
+        const uint32_t t = min(g + lane, ntiles - 1u);
 #pragma unroll
-    for (int w = 0; w < NW; w++) tn[w] = lane < ntiles ? tmin[(size_t)w * ntiles + lane] : 0u;
-    for (uint32_t base = 0; base < ntiles && live; base += 64) {
-        const uint32_t t = base + lane;
-        uint32_t tm[NW];
+        for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
+        tr = tprange[t];
+    };
+    auto load_tile = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
+        const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);      // rows past mr: masked by xvalid
+        const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
 #pragma unroll
-        for (int w = 0; w < NW; w++) tm[w] = tn[w];
-        if (base + 64 < ntiles) {
-            const uint32_t t2 = t + 64;
-#pragma unroll
-            for (int w = 0; w < NW; w++) tn[w] = t2 < ntiles ? tmin[(size_t)w * ntiles + t2] : 0u;
+        for (int q = 0; q < NW / 4; q++) {
+            const uint4 v = src[q];
+            xv[4 * q] = v.x;
+            xv[4 * q + 1] = v.y;
+            xv[4 * q + 2] = v.z;
+            xv[4 * q + 3] = v.w;
         }
+        px = tpart[xi];
+    };
+    // one x tile (lane = x row) against its reachable y (broadcast from LDS, four at a time);
+    // hits collect in two wave masks, applied to the lanes afterwards
+    auto test_tile = [&](uint32_t xt, uint64_t lm, const uint32_t (&xv)[NW], uint32_t px) {
+        lm &= live;
+        if (!lm) return;
+        const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
+        npairs += (uint64_t)nx * (uint64_t)__popcll(lm);
+        if (dbg & 1) return;
+        const bool xvalid = lane < nx;
+        uint64_t h_any = 0, h_same = 0;
+        while (lm) {
+            uint32_t yb[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {      // the last reachable y repeats when fewer than 4 remain
+                yb[u] = lm ? (uint32_t)__builtin_ctzll(lm) : yb[u > 0 ? u - 1 : 0];
+                lm &= lm - 1;
+            }
+            uint32_t yw[4][NW], pyu[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+#pragma unroll
+                for (int w = 0; w < NW; w++) yw[u][w] = sy[yb[u] * NW + w];
+                pyu[u] = spy[yb[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                // bitwise, not short-circuit: no exec-masked branches per test
+                bool dom = xvalid & R::le(xv, yw[u]);
+                if constexpr (FULL) dom = dom & !R::le(yw[u], xv);
+                else dom = dom & !(xt == yt && lane == yb[u]);
+                if (__ballot(dom)) {
+                    h_any |= 1ull << yb[u];
+                    if (__ballot(dom & (px == pyu[u]))) h_same |= 1ull << yb[u];
+                }
+            }
+        }
+        f |= ((h_same >> lane) & 1ull) ? 3u : (((h_any >> lane) & 1ull) ? 2u : 0u);
+        live &= __ballot(!(f & 1u));
+    };
+    // one group of 64 x tiles: box tests -> LDS list of reachable tiles (returns its length)
+    auto candidates = [&](const uint32_t (&tg)[NW], uint32_t tr, uint32_t g) -> uint32_t {
         // some live lane not yet dominated by any rep (global level only): every tile
         // counts; otherwise only tiles holding rows of the y tile's partitions do
         const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-        bool cand = t < ntiles && R::le(tm, ymax);
-        if (cand && !need_any) {
-            const uint32_t r = tprange[t];
-            cand = (r & 0xffffu) <= yph && (r >> 16) >= ypl;
-        }
-        uint64_t m = __ballot(cand);
-        while (m) {
-            const uint32_t b = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t xt = base + b;
+        bool cand = g + lane < ntiles && R::le(tg, ymax);
+        if (cand && !need_any) cand = (tr & 0xffffu) <= yph && (tr >> 16) >= ypl;
+        uint64_t gm = __ballot(cand);
+        if (dbg & 2) gm = 0;
+        uint32_t cnt = 0;
+        while (gm) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(gm);
+            gm &= gm - 1;
             uint32_t xm[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) xm[w] = (uint32_t)__builtin_amdgcn_readlane((int)tm[w], (int)b);
-            uint64_t lm = live & __ballot(R::le(xm, y));
-            if (!lm) continue;
-            const uint32_t x0 = xt * kMbrT;
-            const uint32_t nx = mr - x0 < (uint32_t)kMbrT ? mr - x0 : (uint32_t)kMbrT;
-            npairs += (uint64_t)nx * (uint64_t)__popcll(lm);
-            if (__popcll(lm) >= row_min) {
-                // many y lanes in reach: every x row (scalar loads) against every lane
-                const uint32_t *xr = trows + (size_t)x0 * NW;
-                const uint32_t *xp = tpart + x0;
-                if (xt == yt && !FULL) {
-                    for (uint32_t q = 0; q < nx; q++) {
-                        uint32_t x[NW];
-#pragma unroll
-                        for (int w = 0; w < NW; w++) x[w] = xr[(size_t)q * NW + w];
-                        const bool dom = R::le(x, y) && q != lane;
-                        f |= dom ? (xp[q] == py ? 3u : 2u) : 0u;
-                    }
-                } else {
-#pragma unroll 4
-                    for (uint32_t q = 0; q < nx; q++) {
-                        uint32_t x[NW];
-#pragma unroll
-                        for (int w = 0; w < NW; w++) x[w] = xr[(size_t)q * NW + w];
-                        bool dom = R::le(x, y);
-                        if constexpr (FULL) dom = dom && !R::le(y, x);
-                        f |= dom ? (xp[q] == py ? 3u : 2u) : 0u;
-                    }
+            for (int w = 0; w < NW; w++) xm[w] = (uint32_t)__builtin_amdgcn_readlane((int)tg[w], (int)b);
+            const uint64_t lm = live & __ballot(R::le(xm, y));
+            if (lm) {
+                if (lane == 0) {
+                    lx[cnt] = g + b;
+                    lmq[cnt] = lm;
                 }
-            } else {
-                // few y lanes in reach: lane = x row (one vector load of the tile), the
-                // reachable y broadcast one at a time
-                const uint32_t xi = x0 + lane;
-                const bool xvalid = lane < nx;
-                uint32_t xv[NW];
-#pragma unroll
-                for (int w = 0; w < NW; w++) xv[w] = xvalid ? trows[(size_t)xi * NW + w] : 0u;
-                const uint32_t px = xvalid ? tpart[xi] : 0xfffffffeu;
-                while (lm) {
-                    const uint32_t yb = (uint32_t)__builtin_ctzll(lm);
-                    lm &= lm - 1;
-                    uint32_t yw[NW];
-#pragma unroll
-                    for (int w = 0; w < NW; w++) yw[w] = (uint32_t)__builtin_amdgcn_readlane((int)y[w], (int)yb);
-                    const uint32_t pyu = (uint32_t)__builtin_amdgcn_readlane((int)py, (int)yb);
-                    bool dom = xvalid && R::le(xv, yw);
-                    if constexpr (FULL) dom = dom && !R::le(yw, xv);
-                    else dom = dom && !(xt == yt && lane == yb);
-                    const uint64_t hit = __ballot(dom);
-                    if (hit) {
-                        const uint32_t bits = __ballot(dom && px == pyu) ? 3u : 2u;
-                        f |= lane == yb ? bits : 0u;
-                    }
-                }
+                cnt++;
             }
-            live &= __ballot(!(f & 1u));
-            if (!live) break;
         }
+        __builtin_amdgcn_wave_barrier();
+        return cnt;
+    };
+    // the listed tiles, BT at a time (their loads in flight together)
+    auto process = [&](uint32_t cnt) {
+        for (uint32_t i = 0; i < cnt && live; i += BT) {
+            uint32_t xt[BT], xv[BT][NW], px[BT];
+            uint64_t lmb[BT];
+#pragma unroll
+            for (int u = 0; u < BT; u++) {
+                // LDS reads are per-lane to the compiler: readfirstlane makes the list entries
+                // wave-uniform (scalar bit loops and branches instead of exec-masked VALU ones)
+                const uint32_t k = min(i + (uint32_t)u, cnt - 1u);
+                xt[u] = __builtin_amdgcn_readfirstlane(lx[k]);
+                const uint64_t e = lmq[k];
+                const uint64_t eu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) << 32) |
+                                    (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
+                lmb[u] = i + u < cnt ? eu : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < BT; u++) load_tile(xt[u], xv[u], px[u]);
+#pragma unroll
+            for (int u = 0; u < BT; u++) test_tile(xt[u], lmb[u], xv[u], px[u]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+
+    // the next group's box corners load into the same registers right after the current
+    // group's list is built, so they are in flight while its tiles are tested (no
+    // loop-carried copy of registers still being loaded)
+    uint32_t tg[NW], tr = 0;
+    load_group(tg, tr, 0);
+    for (uint32_t g = 0; g < ntiles && live; g += 64) {
+        const uint32_t cnt = candidates(tg, tr, g);
+        if (g + 64 < ntiles) load_group(tg, tr, g + 64);
+        process(cnt);
     }
     if (valid) domf[j] = f;
     if (lane == 0 && pairs) atomicAdd(pairs, (unsigned long long)npairs);
@@ -410,7 +486,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t ntiles = (uint32_t)mbr_tiles(mr);
     const unsigned gb = (unsigned)((mr + kThreads - 1) / kThreads);
     const int bits = mbr_bits(D);
-    k_mbr_minmax<R, D><<<gb < 1024 ? gb : 1024, kThreads, 0, st>>>((const uint32_t *)a.rows, mr, a.mm);
+    k_mbr_minmax<R, D><<<gb < 512 ? gb : 512, kThreads, 0, st>>>((const uint32_t *)a.rows, mr, a.mm);
     k_mbr_code<R, D><<<gb, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, mr, bits, a.mm, a.code, a.idx);
     const int tb = bits * D + 8;
     const uint64_t kor = tb >= 64 ? ~0ull : ((1ull << tb) - 1ull);
@@ -418,22 +494,23 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
                                       lerr);
     const uint32_t *perm = alt ? a.idx_alt : a.idx;
     const unsigned gt = (ntiles + 3) / 4;
+    const unsigned gp = (gt + 7) / 8 * 8;          // the pair pass: a multiple of the 8 XCDs
     k_mbr_tiles<R><<<gt, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, perm, mr, ntiles, a.trows, a.tpart,
                                             a.tmin, a.tmax, a.tprange);
     if (a.full) {
         if (a.gmerge)
-            k_mbr_pairs<R, true, true><<<gt, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr, ntiles,
-                                                                a.row_min, a.domf, a.pairs);
+            k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr, ntiles,
+                                                                a.dbg, a.domf, a.pairs);
         else
-            k_mbr_pairs<R, true, false><<<gt, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                 ntiles, a.row_min, a.domf, a.pairs);
+            k_mbr_pairs<R, true, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+                                                                 ntiles, a.dbg, a.domf, a.pairs);
     } else {
         if (a.gmerge)
-            k_mbr_pairs<R, false, true><<<gt, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                 ntiles, a.row_min, a.domf, a.pairs);
+            k_mbr_pairs<R, false, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+                                                                 ntiles, a.dbg, a.domf, a.pairs);
         else
-            k_mbr_pairs<R, false, false><<<gt, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                  ntiles, a.row_min, a.domf, a.pairs);
+            k_mbr_pairs<R, false, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+                                                                  ntiles, a.dbg, a.domf, a.pairs);
     }
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);
 }

@@ -270,7 +270,8 @@ struct MbrArgs {
     uint32_t mr = 0;
     bool gmerge = false;          // the global level (alive_g) too
     bool full = false;            // complete dominance test (rows may repeat a vector)
-    int row_min = 24;             // y lanes in reach of an x tile from which its rows are scanned
+    int row_min = 24;
+    int dbg = 0;                  // SKY_MBR_DBG (measurement only): 1 skip the pair tests, 2 also the lane tests             // y lanes in reach of an x tile from which its rows are scanned
     uint32_t *mm = nullptr;       // [2D]: {0xffffffff} x D, {0} x D on entry
     uint64_t *code = nullptr, *code_alt = nullptr;   // [mr]
     uint32_t *idx = nullptr, *idx_alt = nullptr;     // [mr]

@@ -30,12 +30,9 @@ def force_mbr(monkeypatch):
                                               ("uniform", 1, 4, "mr-dim", 30000),
                                               ("std_anti", 16, 8, "mr-angle", 8000),
                                               ("std_anti", 12, 4, "mr-grid", 8000)])
-@pytest.mark.parametrize("prefilter,rowmin", [("1", "24"), ("0", "0"), ("0", "65")])
-def test_mbr_vs_oracle(dist, D, P_, algo, n, prefilter, rowmin, force_mbr, gpu_engine_factory, oracle):
-    """rowmin 0: every reachable x tile scanned row by row; 65: always one row per lane with
-    the reachable y broadcast; 24: the default mix."""
+@pytest.mark.parametrize("prefilter", ["1", "0"])
+def test_mbr_vs_oracle(dist, D, P_, algo, n, prefilter, force_mbr, gpu_engine_factory, oracle):
     force_mbr.setenv("SKY_PREFILTER", prefilter)
-    force_mbr.setenv("SKY_MBR_ROWMIN", rowmin)
     vals = oracle.synth(DISTS[dist], D, n, seed=300 + D + P_)
     check_vs_oracle(gpu_engine_factory, oracle, vals, P_, algo)
     force_mbr.setenv("SKY_SFS16", "0")                    # the same reps as f32 rows
