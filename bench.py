@@ -437,6 +437,61 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
             "roofline": roof}
 
 
+def operator_run(dev_index, n=10_000_000, buf=5000):
+    """The drop-in operator path (FlinkSkyline.java:265-316, :417-444,
+    :515-569) on the first n tuples of the C4 stream: per-key 5000-tuple flushes through
+    sky_part_insert (host buffers, as the JNI shim passes them) in stream order of their
+    5000th tuple, then at the trigger: the partial buffers flushed, every key's snapshot, and
+    sky_global_merge of the P local skylines.  Per-flush latency = one sky_part_insert call."""
+    import numpy as np
+    from skyline.operators import _LocalPart
+    D, P = 8, 16
+    vals, ids = skyline.synth_host(_abi.DISTS["anti_correlated"], D, n, seed=1234 + D)
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
+    keys = eng.partition_keys(vals)
+    events = []                                # (stream position of the flush, key, lo, hi) over order_k
+    per_key = {}
+    for k in range(P):
+        idx = np.flatnonzero(keys == k)
+        per_key[k] = idx
+        for lo in range(0, len(idx) - len(idx) % buf, buf):
+            events.append((int(idx[lo + buf - 1]), k, lo, lo + buf))
+    events.sort()
+    parts = {k: _LocalPart(eng, k) for k in range(P)}
+    batches = {k: (np.ascontiguousarray(ids[per_key[k]]), np.ascontiguousarray(vals[per_key[k]])) for k in range(P)}
+    lat = []
+    t0 = time.perf_counter()
+    for _, k, lo, hi in events:
+        bi, bv = batches[k]
+        ts = time.perf_counter()
+        parts[k].insert(bi[lo:hi], bv[lo:hi])
+        lat.append((time.perf_counter() - ts) * 1e3)
+    t_ins = time.perf_counter() - t0
+    tq = time.perf_counter()
+    for k in range(P):                         # processQuery: flush the partial buffer (:387)
+        bi, bv = batches[k]
+        rem = len(bi) % buf
+        if rem:
+            parts[k].insert(bi[len(bi) - rem:], bv[len(bv) - rem:])
+    snaps = [parts[k].snapshot() for k in range(P)]
+    gids, _ = eng.global_merge(list(range(P)), [sn[0] for sn in snaps], [sn[1] for sn in snaps])
+    t_q = time.perf_counter() - tq
+    total = time.perf_counter() - t0
+    local_sizes = [len(sn[0]) for sn in snaps]
+    for pt in parts.values():
+        pt.close()
+    eng.close()
+    lat.sort()
+    return {"workload": f"C4 stream prefix, {n} tuples, MR-Angle P={P}, per-key {buf}-tuple flushes from host memory "
+                        f"through sky_part_insert, then snapshots + sky_global_merge",
+            "flushes": len(lat), "insert_phase_s": t_ins, "query_phase_s": t_q,
+            "tuples_per_s": n / total, "ingest_tuples_per_s": (len(lat) * buf) / t_ins,
+            "p50_flush_ms": lat[len(lat) // 2] if lat else None,
+            "p99_flush_ms": lat[int(len(lat) * 0.99)] if lat else None,
+            "max_flush_ms": lat[-1] if lat else None,
+            "skyline_size": int(len(gids)), "local_sizes": local_sizes}
+
+
 def sort_run(eng, n, dev, steps=3):
     """Sort phase at scale (HBM GB/s of the sort): the pipeline's radix sort
     (k_radix.hip) alone on n pairs keyed like its candidate keys (4-bit partition | 32-bit
@@ -487,6 +542,7 @@ def main():
     ap.add_argument("--no-sort", action="store_true", help="skip the radix-sort-at-scale companion measurement")
     ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C3 sub-lines")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (H2D inside) C4 rates")
+    ap.add_argument("--no-operator", action="store_true", help="skip the per-key operator-path companion")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, the measured path) or gloo (rehearsing ranks on one GPU)")
     args = ap.parse_args()
@@ -576,6 +632,8 @@ def main():
                 extra["csv_ingest"] = csv_ingest_run(eng, ids, vals, n, D, 3, out_ids, out_org)
             if not args.no_sort:
                 extra["sort_roofline"] = sort_run(eng, n, dev)
+            if not args.no_operator:
+                extra["operator_path"] = operator_run(dev_index)
             if not args.no_configs:
                 extra["configs"] = {nm: config_line(nm, dev, dev_index, args.steps, args.warmup,
                                                     not args.no_cpu_baseline)

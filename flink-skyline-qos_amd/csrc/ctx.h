@@ -129,12 +129,26 @@ struct Ctx {
 
 struct sky_ctx : sky::Ctx {};
 
+// one Flink key's local skyline (SkylineLocalProcessor.localSkylineState, FlinkSkyline.java:243-248)
+// as distinct vectors + the tuples on them (k_part.hip): an insert costs O(|B| (|B| + R))
 struct sky_part {
     sky_ctx *ctx = nullptr;
     int32_t key = 0;
-    sky::DevBuf ids, rows;    // current local skyline (device), insertion order
-    int64_t n = 0;
-    sky::DevBuf cat_ids, cat_rows;
+    // distinct vectors: rows f64 [R][D], alive flag, tuples per rep
+    sky::DevBuf rrows, ralive, rcnt;
+    uint32_t R = 0;
+    // tuples in insertion order: id, rep; Tdead of them sit on dead reps (compacted lazily)
+    sky::DevBuf tids, trep;
+    uint32_t T = 0;
+    uint64_t Tdead = 0;
+    // batch workspace
+    sky::DevBuf bids, bvals, dom_b, eq_s, eq_b, dom_s, keep, keep_pos, fresh, fresh_pos, scratch, words;
+    // compaction targets and read-out staging
+    sky::DevBuf rrows2, ralive2, rcnt2, tids2, trep2, rk, rp, tk, tp, out_rows;
+    void *pin = nullptr;        // pinned read-back words
+    ~sky_part() {
+        if (pin) (void)hipHostFree(pin);
+    }
 };
 
 struct sky_stream {

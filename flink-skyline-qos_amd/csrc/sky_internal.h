@@ -288,6 +288,25 @@ int mbr_row_words(int D, int fmt);
 size_t mbr_tiles(uint32_t mr);
 hipError_t launch_mbr(const MbrArgs &a, hipStream_t st);
 
+// ---- k_part.hip (per-key operator state, incremental) ----
+void launch_part_pairs(int D, const double *y, uint32_t ny, const double *x, uint32_t nx, const uint8_t *x_alive,
+                       bool same_set, const uint32_t *nanflag, uint32_t *dom, uint32_t *eq, hipStream_t st);
+void launch_part_flags(uint32_t nb, const uint32_t *dom_b, const uint32_t *eq_s, const uint32_t *eq_b, uint32_t *keep,
+                       uint32_t *fresh, hipStream_t st);
+void launch_part_write(int D, uint32_t nb, const int64_t *bids, const double *bvals, const uint32_t *keep,
+                       const uint32_t *keep_pos, const uint32_t *fresh, const uint32_t *fresh_pos, const uint32_t *eq_s,
+                       const uint32_t *eq_b, uint32_t R, uint32_t T, const uint32_t *nanflag, double *rrows,
+                       uint8_t *ralive, uint32_t *rcnt, int64_t *tids, uint32_t *trep, hipStream_t st);
+void launch_part_kill(uint32_t R, const uint32_t *dom_s, const uint32_t *nanflag, uint8_t *ralive, const uint32_t *rcnt,
+                      unsigned long long *dead, hipStream_t st);
+void launch_part_rkeep(uint32_t R, const uint8_t *ralive, uint32_t *keep, hipStream_t st);
+void launch_part_rmove(int D, uint32_t R, const uint32_t *keep, const uint32_t *pos, const double *rows,
+                       const uint32_t *cnt, double *rows2, uint32_t *cnt2, uint8_t *alive2, hipStream_t st);
+void launch_part_tkeep(uint32_t T, const uint32_t *trep, const uint8_t *ralive, uint32_t *keep, hipStream_t st);
+void launch_part_tmove(uint32_t T, const uint32_t *keep, const uint32_t *pos, const uint32_t *rpos, const int64_t *ids,
+                       const uint32_t *trep, int64_t *ids2, uint32_t *trep2, hipStream_t st);
+void launch_part_rows_out(int D, uint32_t T, const uint32_t *trep, const double *rrows, double *out, hipStream_t st);
+
 // ---- k_synth.hip ----
 void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,
                   int64_t *ids, hipStream_t st);
