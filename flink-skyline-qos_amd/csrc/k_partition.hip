@@ -1136,52 +1136,71 @@ __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
     }
 }
 
+// Write pass: item k of thread t is tuple tile*2048 + k*256 + t, so every status / id load
+// of a wave is lane-contiguous (coalesced 128 / 512-byte requests; the thread-contiguous
+// layout of the count pass made the id loads 64-byte strided).  Index order within the tile
+// is (k, wave, lane): a selected tuple's output position is the count of the (k, wave)
+// groups before it (32 per tile, scanned in LDS) plus its rank in its wave's ballot.
 __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     __shared__ uint8_t s_pf[2048];
-    __shared__ uint32_t s_w[kThreads / 64];
+    __shared__ uint32_t s_cnt[kItems * (kThreads / 64)];
+    __shared__ uint32_t s_tot;
     __shared__ int64_t s_oid[kTile];
     __shared__ int32_t s_oorg[kTile];
     const uint32_t tile = blockIdx.x;
-    const uint32_t i0 = tile * kTile + threadIdx.x * kItems;
-    // status, ids and the pruner-fate table in flight together
+    const uint32_t i0 = tile * kTile + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nl = a.n - 1;
+    // status, ids and the pruner-fate table in flight together; indices clamped into [0, n)
+    // (tuples past n are never selected: masked below)
     uint16_t st[kItems];
-    load_status8(a.status, a.n, i0, st);
     int64_t idv[kItems];
-    if (a.ids) {
-        // one load per id, index clamped into [0, n) (no partial-tile branch); ids
-        // past n are never selected
 #pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k, a.n - 1)];
+    for (int k = 0; k < kItems; k++) st[k] = a.status[min(i0 + k * kThreads, nl)];
+    if (a.ids) {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];
     } else {
 #pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k);
+        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k * kThreads);
     }
     for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     __syncthreads();                                   // s_pf ready
     const int shift = a.select_local ? 0 : 1;
-    uint8_t fate[kItems];
-    uint32_t nsel = 0;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint64_t msk[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-        const uint8_t f = tuple_fate(st[k], s_pf, a.M);
-        fate[k] = f;
-        nsel += (f >> shift) & 1u;
+        const bool in = i0 + k * kThreads < a.n;
+        const uint32_t f = in ? tuple_fate(st[k], s_pf, a.M) : 0u;
+        msk[k] = __ballot((f >> shift) & 1u);
+        if (lane == 0) s_cnt[k * (kThreads / 64) + wave] = (uint32_t)__popcll(msk[k]);
     }
-    uint32_t bt;
-    uint32_t pl = block_scan_excl(nsel, s_w, bt);
+    __syncthreads();
+    if (threadIdx.x == 0) {                            // exclusive offsets of the 32 (k, wave) groups
+        uint32_t run = 0;
+        for (int q = 0; q < kItems * (kThreads / 64); q++) {
+            const uint32_t c = s_cnt[q];
+            s_cnt[q] = run;
+            run += c;
+        }
+        s_tot = run;
+    }
+    __syncthreads();
     const uint32_t base = a.out_off[tile];
 #pragma unroll
     for (int k = 0; k < kItems; k++) {
-        if (!((fate[k] >> shift) & 1)) continue;
-        const uint32_t i = i0 + k;
+        if (!((msk[k] >> lane) & 1ull)) continue;
+        const uint32_t pl = s_cnt[k * (kThreads / 64) + wave] + (uint32_t)__popcll(msk[k] & lt);
+        const uint32_t i = i0 + k * kThreads;
         s_oid[pl] = idv[k];
         s_oorg[pl] = a.given_origin ? a.given_origin[i] : (int32_t)(st[k] >> 8);
         if (a.rows_out && (int64_t)base + pl < a.out_cap)
             for (int d = 0; d < a.D; d++) a.rows_out[(size_t)(base + pl) * a.D + d] = a.vals[(size_t)i * a.D + d];
-        pl++;
     }
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < bt; q += kThreads) {
+    const uint32_t total = s_tot;
+    for (uint32_t q = threadIdx.x; q < total; q += kThreads) {
         if ((int64_t)base + q >= a.out_cap) break;
         if (a.ids_out) a.ids_out[base + q] = s_oid[q];
         if (a.origin_out) a.origin_out[base + q] = s_oorg[q];
