@@ -346,7 +346,8 @@ def dominance_run(dev, D, P, n, seed, steps, warmup):
             "peak_32bit": VALU_PEAK_32, "frac_32bit": achieved / VALU_PEAK_32,
             "path": ("mbr-" if mbr else "sfs-") + ("u16" if int(counters[7]) & 4 else "f32/f64"),
             "local_sfs_ms": phases["local_sfs"], "global_sfs_ms": phases["global_sfs"],
-            "sfs_rounds": int(counters[5])}
+            "sfs_rounds": int(counters[5]),
+            "tile_pairs_tested": int(counters[7]) >> 8 if mbr else None}
 
 
 def csv_ingest_run(eng, ids, vals, n, D, steps, out_ids, out_org):

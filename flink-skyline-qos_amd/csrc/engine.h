@@ -78,6 +78,7 @@ struct Pipe {
     DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_domf,
         mbr_pairs;
     bool used_mbr = false;
+    int64_t mbr_tiles = 0;
     // the candidate slots after the filter (rows / sortkey / slot_src) or, after the
     // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so
     // the stream-sized buffers keep their capacity across queries)

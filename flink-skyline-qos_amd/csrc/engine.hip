@@ -566,12 +566,13 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
-    SKY_TRY(p.mbr_pairs.ensure(8));
+    SKY_TRY(p.mbr_pairs.ensure(16));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
     FillSet fill;
     fill.add(p.mbr_mm.p, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
-    fill.add(p.mbr_pairs.p, 8, 0);
+    fill.add(p.mbr_pairs.p, 16, 0);
+    fill.add(p.mbr_domf.p, (size_t)mr * 4, 0);
     HIP_TRY(fill.launch(st));
     MbrArgs a;
     a.D = D;
@@ -584,6 +585,8 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     {
         const char *e = getenv("SKY_MBR_DBG");
         a.dbg = e ? atoi(e) : 0;
+        const char *sp = getenv("SKY_MBR_SPLIT");   // x-tile ranges per y tile (A/B knob)
+        a.nsplit = sp ? std::max(1, atoi(sp)) : 8;
     }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
@@ -1103,13 +1106,14 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.mg = in.global && !in.single ? alive_sum : 0;
     } else {
         uint32_t flags3 = 0;
-        unsigned long long mbr_pairs = 0;
+        unsigned long long mbr_pairs[2] = {0, 0};
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
-                                  {p.mbr_pairs.p, p.used_mbr ? 8u : 0u}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, &mbr_pairs}));
+                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs}));
         if (p.used_mbr) {
-            p.sfs_pairs_upper = (int64_t)mbr_pairs;     // pair tests the pruned pass executed
+            p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
+            p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
             uint32_t alive_sum = 0;
             for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
             p.mg = in.global && !in.single ? alive_sum : 0;

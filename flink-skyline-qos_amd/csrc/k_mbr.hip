@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tmax,
                                                         const uint32_t *__restrict__ tprange, uint32_t mr,
-                                                        uint32_t ntiles, int dbg, uint32_t *__restrict__ domf,
+                                                        uint32_t ntiles, uint32_t nsplit, int dbg, uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs) {
     constexpr int NW = R::NW;
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
@@ -289,8 +289,14 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     // overlap and stay in that XCD's L2 (the grid is padded to a multiple of 8)
     const uint32_t per_xcd = gridDim.x / 8u;
     const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
-    const uint32_t yt = __builtin_amdgcn_readfirstlane(blk * (kThreads / 64) + (threadIdx.x >> 6));
+    // the x tiles are split into nsplit ranges, one work item each: the work of a y tile
+    // varies by orders of magnitude (a loose box reaches many tiles), and one wave per y
+    // tile left the launch waiting for its slowest waves
+    const uint32_t split = blk % nsplit;
+    const uint32_t yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kThreads / 64) + (threadIdx.x >> 6));
     if (yt >= ntiles) return;
+    const uint32_t ngroups = (ntiles + 63) / 64;
+    const uint32_t g_lo = split * ngroups / nsplit * 64, g_hi = min(ntiles, (split + 1) * ngroups / nsplit * 64);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
     const bool valid = j < mr;
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     __builtin_amdgcn_wave_barrier();
     uint32_t f = 0;
     uint64_t live = __ballot(valid);
-    uint64_t npairs = 0;
+    uint64_t npairs = 0, ntested = 0;
     // per wave: the reachable x tiles of the current group of 64 (tile index, lane mask)
     __shared__ uint32_t s_lx[kThreads / 64][64];
     __shared__ uint64_t s_lm[kThreads / 64][64];
@@ -357,6 +363,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
         if (!lm) return;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         npairs += (uint64_t)nx * (uint64_t)__popcll(lm);
+        ntested++;
         if (dbg & 1) return;
         const bool xvalid = lane < nx;
         uint64_t h_any = 0, h_same = 0;
@@ -445,14 +452,17 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     // group's list is built, so they are in flight while its tiles are tested (no
     // loop-carried copy of registers still being loaded)
     uint32_t tg[NW], tr = 0;
-    load_group(tg, tr, 0);
-    for (uint32_t g = 0; g < ntiles && live; g += 64) {
+    if (g_lo < g_hi) load_group(tg, tr, g_lo);
+    for (uint32_t g = g_lo; g < g_hi && live; g += 64) {
         const uint32_t cnt = candidates(tg, tr, g);
-        if (g + 64 < ntiles) load_group(tg, tr, g + 64);
+        if (g + 64 < g_hi) load_group(tg, tr, g + 64);
         process(cnt);
     }
-    if (valid) domf[j] = f;
-    if (lane == 0 && pairs) atomicAdd(pairs, (unsigned long long)npairs);
+    if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
+    if (lane == 0 && pairs) {
+        atomicAdd(pairs, (unsigned long long)npairs);
+        atomicAdd(pairs + 1, (unsigned long long)ntested);
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_mbr_finish(const uint32_t *__restrict__ perm,
@@ -494,23 +504,24 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
                                       lerr);
     const uint32_t *perm = alt ? a.idx_alt : a.idx;
     const unsigned gt = (ntiles + 3) / 4;
-    const unsigned gp = (gt + 7) / 8 * 8;          // the pair pass: a multiple of the 8 XCDs
+    const uint32_t nsplit = a.nsplit < 1 ? 1u : (uint32_t)a.nsplit;
+    const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
     k_mbr_tiles<R><<<gt, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, perm, mr, ntiles, a.trows, a.tpart,
                                             a.tmin, a.tmax, a.tprange);
     if (a.full) {
         if (a.gmerge)
             k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr, ntiles,
-                                                                a.dbg, a.domf, a.pairs);
+                                                                nsplit, a.dbg, a.domf, a.pairs);
         else
             k_mbr_pairs<R, true, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                 ntiles, a.dbg, a.domf, a.pairs);
+                                                                 ntiles, nsplit, a.dbg, a.domf, a.pairs);
     } else {
         if (a.gmerge)
             k_mbr_pairs<R, false, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                 ntiles, a.dbg, a.domf, a.pairs);
+                                                                 ntiles, nsplit, a.dbg, a.domf, a.pairs);
         else
             k_mbr_pairs<R, false, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
-                                                                  ntiles, a.dbg, a.domf, a.pairs);
+                                                                  ntiles, nsplit, a.dbg, a.domf, a.pairs);
     }
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);
 }

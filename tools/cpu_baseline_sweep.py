@@ -27,8 +27,8 @@ from conftest import Oracle  # noqa: E402
 CONFIGS = {
     "C1": dict(algo="dim", dims=2, dist=0, P=8, full=1_000_000, ns=[100_000, 250_000, 500_000, 1_000_000]),
     "C2": dict(algo="grid", dims=4, dist=1, P=8, full=10_000_000, ns=[100_000, 250_000, 500_000, 1_000_000]),
-    "C3": dict(algo="angle", dims=4, dist=2, P=8, full=50_000_000, ns=[100_000, 250_000, 500_000, 1_000_000]),
-    "C4": dict(algo="angle", dims=8, dist=2, P=16, full=100_000_000, ns=[50_000, 100_000, 200_000, 400_000]),
+    "C3": dict(algo="angle", dims=4, dist=2, P=8, full=50_000_000, ns=[50_000, 100_000, 200_000, 400_000]),
+    "C4": dict(algo="angle", dims=8, dist=2, P=16, full=100_000_000, ns=[25_000, 50_000, 100_000, 200_000]),
 }
 
 
