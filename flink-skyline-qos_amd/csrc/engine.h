@@ -75,7 +75,7 @@ struct Pipe {
     // candidate prefilter (second-level pruners) and its compaction targets
     DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2, rows3, sortkey3, slot_src3;
     // bounding-box pruned all-pairs pass over large rep sets (k_mbr.hip)
-    DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_domf,
+    DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_sub, mbr_domf,
         mbr_pairs;
     bool used_mbr = false;
     int64_t mbr_tiles = 0;

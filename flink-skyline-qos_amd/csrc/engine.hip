@@ -565,6 +565,7 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_min.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
+    SKY_TRY(p.mbr_sub.ensure(ntiles * 4 * NW * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
     SKY_TRY(p.mbr_pairs.ensure(16));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
@@ -586,7 +587,7 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
         const char *e = getenv("SKY_MBR_DBG");
         a.dbg = e ? atoi(e) : 0;
         const char *sp = getenv("SKY_MBR_SPLIT");   // x-tile ranges per y tile (A/B knob)
-        a.nsplit = sp ? std::max(1, atoi(sp)) : 8;
+        a.nsplit = sp ? std::max(1, atoi(sp)) : 1;
     }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
@@ -600,6 +601,7 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.tmin = p.mbr_min.as<uint32_t>();
     a.tmax = p.mbr_max.as<uint32_t>();
     a.tprange = p.mbr_pr.as<uint32_t>();
+    a.tsub = p.mbr_sub.as<uint32_t>();
     a.domf = p.mbr_domf.as<uint32_t>();
     a.pairs = p.mbr_pairs.as<unsigned long long>();
     a.alive_l = p.alive_l.as<uint8_t>();

@@ -216,7 +216,8 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
                                                         const uint32_t *__restrict__ perm, uint32_t mr,
                                                         uint32_t ntiles, uint32_t *__restrict__ trows,
                                                         uint32_t *__restrict__ tpart, uint32_t *__restrict__ tmin,
-                                                        uint32_t *__restrict__ tmax, uint32_t *__restrict__ tprange) {
+                                                        uint32_t *__restrict__ tmax, uint32_t *__restrict__ tprange,
+                                                        uint32_t *__restrict__ tsub) {
     constexpr int NW = R::NW;
     const uint32_t tile = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     if (tile >= ntiles) return;
@@ -242,8 +243,10 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
         pl = 0xffffffffu;
         ph = 0u;
     }
+    // offsets 1..8 first: the 16-row sub-boxes' min corners (k_mbr_pairs tests a y against
+    // them before comparing rows), then 16, 32: the whole tile
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
+    for (int o = 1; o <= 32; o <<= 1) {
         uint32_t a[NW], b[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) {
@@ -254,6 +257,10 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
         R::cmax(mx, b);
         pl = min(pl, (uint32_t)__shfl_xor((int)pl, o, 64));
         ph = max(ph, (uint32_t)__shfl_xor((int)ph, o, 64));
+        if (o == 8 && (threadIdx.x & 15) == 0) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) tsub[((size_t)tile * 4 + ((threadIdx.x & 63) >> 4)) * NW + w] = mn[w];
+        }
     }
     if ((threadIdx.x & 63) == 0) {
 #pragma unroll
@@ -280,7 +287,8 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tmax,
-                                                        const uint32_t *__restrict__ tprange, uint32_t mr,
+                                                        const uint32_t *__restrict__ tprange,
+                                                        const uint32_t *__restrict__ tsub, uint32_t mr,
                                                         uint32_t ntiles, uint32_t nsplit, int dbg, uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs) {
     constexpr int NW = R::NW;
@@ -333,7 +341,14 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     __shared__ uint64_t s_lm[kThreads / 64][64];
     uint32_t *lx = s_lx[threadIdx.x >> 6];
     uint64_t *lmq = s_lm[threadIdx.x >> 6];
-    constexpr int BT = NW <= 8 ? 4 : 2;        // x tiles loaded together (independent loads in flight)
+    // the x tile under test (rows, partitions) and its (y, sub-box) entries
+    __shared__ uint32_t s_x[kThreads / 64][64 * NW];
+    __shared__ uint32_t s_px[kThreads / 64][64];
+    __shared__ uint8_t s_e[kThreads / 64][256];
+    uint32_t *sx = s_x[threadIdx.x >> 6], *spx = s_px[threadIdx.x >> 6];
+    uint8_t *se = s_e[threadIdx.x >> 6];
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    constexpr int BT = 2;                      // x tiles loaded together (independent loads in flight)
 
     // loads are unconditional (clamped index; flags mask the values): conditional loads make
     // the compiler wait for every load in flight
@@ -343,9 +358,11 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
         for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
         tr = tprange[t];
     };
-    auto load_tile = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
+    // lane l: row l of the tile and the min corner of its sub-box l / 16
+    auto load_tile = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px, uint32_t (&xs)[NW]) {
         const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);      // rows past mr: masked by xvalid
         const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
+        const uint4 *sb = reinterpret_cast<const uint4 *>(tsub + ((size_t)xt * 4 + (lane >> 4)) * NW);
 #pragma unroll
         for (int q = 0; q < NW / 4; q++) {
             const uint4 v = src[q];
@@ -353,46 +370,79 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
             xv[4 * q + 1] = v.y;
             xv[4 * q + 2] = v.z;
             xv[4 * q + 3] = v.w;
+            const uint4 c = sb[q];
+            xs[4 * q] = c.x;
+            xs[4 * q + 1] = c.y;
+            xs[4 * q + 2] = c.z;
+            xs[4 * q + 3] = c.w;
         }
         px = tpart[xi];
     };
-    // one x tile (lane = x row) against its reachable y (broadcast from LDS, four at a time);
-    // hits collect in two wave masks, applied to the lanes afterwards
-    auto test_tile = [&](uint32_t xt, uint64_t lm, const uint32_t (&xv)[NW], uint32_t px) {
+    // one x tile against its reachable y: each y is first tested against the min corners of
+    // the tile's four 16-row sub-boxes; the surviving (y, sub-box) entries are then compared
+    // four per wave instruction (lanes 16g..16g+15: entry g's 16 rows vs its y, rows and y
+    // read from LDS).  Hits collect in two wave masks, applied to the lanes afterwards.
+    auto test_tile = [&](uint32_t xt, uint64_t lm, const uint32_t (&xv)[NW], uint32_t px, const uint32_t (&xs)[NW]) {
         lm &= live;
         if (!lm) return;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
-        npairs += (uint64_t)nx * (uint64_t)__popcll(lm);
         ntested++;
-        if (dbg & 1) return;
-        const bool xvalid = lane < nx;
+        uint64_t ms[4];
+        uint32_t E = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t c[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) c[w] = (uint32_t)__builtin_amdgcn_readlane((int)xs[w], 16 * b);
+            ms[b] = (uint32_t)(16 * b) < nx ? lm & __ballot(R::le(c, y)) : 0ull;
+            E += (uint32_t)__popcll(ms[b]);
+        }
+        npairs += 16ull * E;
+        if ((dbg & 1) || !E) return;
+        // stage the tile and the entries (y << 2 | sub-box) in LDS
+#pragma unroll
+        for (int w = 0; w < NW; w++) sx[lane * NW + w] = xv[w];
+        spx[lane] = px;
+        {
+            uint32_t eb = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if ((ms[b] >> lane) & 1ull) se[eb + (uint32_t)__popcll(ms[b] & lt)] = (uint8_t)((lane << 2) | b);
+                eb += (uint32_t)__popcll(ms[b]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t g = lane >> 4, r = lane & 15;
         uint64_t h_any = 0, h_same = 0;
-        while (lm) {
-            uint32_t yb[4];
+        for (uint32_t e0 = 0; e0 < E; e0 += 4) {
+            const bool ev = e0 + g < E;
+            const uint32_t ent = se[min(e0 + g, E - 1u)];
+            const uint32_t yb = ent >> 2, xr = (ent & 3u) * 16u + r;
+            uint32_t xw[NW], yw[NW];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {      // the last reachable y repeats when fewer than 4 remain
-                yb[u] = lm ? (uint32_t)__builtin_ctzll(lm) : yb[u > 0 ? u - 1 : 0];
-                lm &= lm - 1;
+            for (int w = 0; w < NW; w++) {
+                xw[w] = sx[xr * NW + w];
+                yw[w] = sy[yb * NW + w];
             }
-            uint32_t yw[4][NW], pyu[4];
+            const uint32_t pxl = spx[xr], pyl = spy[yb];
+            // bitwise, not short-circuit: no exec-masked branches per test
+            bool dom = ev & (xr < nx) & R::le(xw, yw);
+            if constexpr (FULL) dom = dom & !R::le(yw, xw);
+            else dom = dom & !(xt == yt && xr == yb);
+            const uint64_t hm = __ballot(dom);
+            if (hm) {
+                const uint64_t hs = __ballot(dom & (pxl == pyl));
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-#pragma unroll
-                for (int w = 0; w < NW; w++) yw[u][w] = sy[yb[u] * NW + w];
-                pyu[u] = spy[yb[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                // bitwise, not short-circuit: no exec-masked branches per test
-                bool dom = xvalid & R::le(xv, yw[u]);
-                if constexpr (FULL) dom = dom & !R::le(yw[u], xv);
-                else dom = dom & !(xt == yt && lane == yb[u]);
-                if (__ballot(dom)) {
-                    h_any |= 1ull << yb[u];
-                    if (__ballot(dom & (px == pyu[u]))) h_same |= 1ull << yb[u];
+                for (int q = 0; q < 4; q++) {
+                    if ((hm >> (16 * q)) & 0xffffull) {
+                        const uint32_t yq = (uint32_t)__builtin_amdgcn_readlane((int)yb, 16 * q);
+                        h_any |= 1ull << yq;
+                        if ((hs >> (16 * q)) & 0xffffull) h_same |= 1ull << yq;
+                    }
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
         f |= ((h_same >> lane) & 1ull) ? 3u : (((h_any >> lane) & 1ull) ? 2u : 0u);
         live &= __ballot(!(f & 1u));
     };
@@ -427,7 +477,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     // the listed tiles, BT at a time (their loads in flight together)
     auto process = [&](uint32_t cnt) {
         for (uint32_t i = 0; i < cnt && live; i += BT) {
-            uint32_t xt[BT], xv[BT][NW], px[BT];
+            uint32_t xt[BT], xv[BT][NW], px[BT], xs[BT][NW];
             uint64_t lmb[BT];
 #pragma unroll
             for (int u = 0; u < BT; u++) {
@@ -441,9 +491,9 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                 lmb[u] = i + u < cnt ? eu : 0ull;
             }
 #pragma unroll
-            for (int u = 0; u < BT; u++) load_tile(xt[u], xv[u], px[u]);
+            for (int u = 0; u < BT; u++) load_tile(xt[u], xv[u], px[u], xs[u]);
 #pragma unroll
-            for (int u = 0; u < BT; u++) test_tile(xt[u], lmb[u], xv[u], px[u]);
+            for (int u = 0; u < BT; u++) test_tile(xt[u], lmb[u], xv[u], px[u], xs[u]);
         }
         __builtin_amdgcn_wave_barrier();
     };
@@ -507,20 +557,20 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t nsplit = a.nsplit < 1 ? 1u : (uint32_t)a.nsplit;
     const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
     k_mbr_tiles<R><<<gt, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, perm, mr, ntiles, a.trows, a.tpart,
-                                            a.tmin, a.tmax, a.tprange);
+                                            a.tmin, a.tmax, a.tprange, a.tsub);
     if (a.full) {
         if (a.gmerge)
-            k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr, ntiles,
+            k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr, ntiles,
                                                                 nsplit, a.dbg, a.domf, a.pairs);
         else
-            k_mbr_pairs<R, true, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+            k_mbr_pairs<R, true, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
                                                                  ntiles, nsplit, a.dbg, a.domf, a.pairs);
     } else {
         if (a.gmerge)
-            k_mbr_pairs<R, false, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+            k_mbr_pairs<R, false, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
                                                                  ntiles, nsplit, a.dbg, a.domf, a.pairs);
         else
-            k_mbr_pairs<R, false, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, mr,
+            k_mbr_pairs<R, false, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
                                                                   ntiles, nsplit, a.dbg, a.domf, a.pairs);
     }
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);

@@ -271,7 +271,7 @@ struct MbrArgs {
     bool gmerge = false;          // the global level (alive_g) too
     bool full = false;            // complete dominance test (rows may repeat a vector)
     int row_min = 24;
-    int nsplit = 8;               // x-tile ranges per y tile (work items of the pair pass)
+    int nsplit = 1;               // x-tile ranges per y tile (work items of the pair pass)
     int dbg = 0;                  // SKY_MBR_DBG (measurement only): 1 skip the pair tests, 2 also the lane tests             // y lanes in reach of an x tile from which its rows are scanned
     uint32_t *mm = nullptr;       // [2D]: {0xffffffff} x D, {0} x D on entry
     uint64_t *code = nullptr, *code_alt = nullptr;   // [mr]
@@ -281,6 +281,7 @@ struct MbrArgs {
     uint32_t *tpart = nullptr;    // [mr]
     uint32_t *tmin = nullptr, *tmax = nullptr;       // [NW][ntiles]
     uint32_t *tprange = nullptr;  // [ntiles]
+    uint32_t *tsub = nullptr;     // [ntiles][4][NW]: min corners of the 16-row sub-boxes
     uint32_t *domf = nullptr;     // [mr], zeroed by the caller
     unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
