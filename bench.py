@@ -340,7 +340,10 @@ def dominance_run(dev, D, P, n, seed, steps, warmup):
             "achieved_note": ("compares the pruned pass executed (D x pair tests counted on the device) / its time"
                               if mbr else "D x W (algorithmic SFS pair tests over distinct vectors) / SFS time"),
             "W_rate": D * w / (dom_ms / 1e3) if dom_ms > 0 else None,
-            "W_rate_note": "D x W / time: the compare rate a round-based SFS would need to finish in this time",
+            "frac_W": (D * w / (dom_ms / 1e3)) / VALU_PEAK_PK16 if dom_ms > 0 else None,
+            "W_rate_note": ("D x W / time with W = SURVEY §8d's algorithmic pair count (the quadratic SFS/BNL over "
+                            "distinct vectors): the compare rate a pair-by-pair algorithm would need to finish in "
+                            "this time; above the VALU peak because the bounding-box pass skips most pairs"),
             "peak_note": "packed-u16 compare peak (2 compares per v_pk_sub_u16 lane-op); the 32-bit lane-op "
                          "peak is half of it",
             "peak_32bit": VALU_PEAK_32, "frac_32bit": achieved / VALU_PEAK_32,
