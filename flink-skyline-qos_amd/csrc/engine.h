@@ -78,6 +78,8 @@ struct Pipe {
     DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_sub, mbr_domf,
         mbr_pairs;
     bool used_mbr = false;
+    size_t slot_hint = 0;       // candidate slots the next run allocates (grown on overflow)
+    int64_t slot_reruns = 0;    // runs repeated because the slots overflowed
     int64_t mbr_tiles = 0;
     // the candidate slots after the filter (rows / sortkey / slot_src) or, after the
     // prefilter's compaction, its *2 buffers: downstream stages read these (no swap, so

@@ -33,8 +33,13 @@ namespace sky {
 
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap && p) return SKY_OK;
+    // a buffer that has to grow again gets 1.5x headroom: query-to-query size changes (candidate
+    // counts, rep counts) then reallocate rarely (each hipFree synchronises the device and landed
+    // inside a query's latency)
+    const bool regrow = cap != 0;
     release();
     size_t want = std::max<size_t>(bytes, 256);
+    if (regrow) want = std::max(want, bytes + bytes / 2);
     want = (want + 4095) & ~size_t(4095);
     if (hipMalloc(&p, want) != hipSuccess) {
         p = nullptr;
@@ -133,6 +138,11 @@ static int prefilter_m2() {   // second-level pruners per partition (SKY_PREFILT
     return m;
 }
 constexpr uint32_t kPrefilterMin = 4096;
+// candidate slots of a first run (SKY_SLOT_MIN overrides: tests force the overflow re-run)
+static size_t slot_min() {
+    const char *e = getenv("SKY_SLOT_MIN");
+    return e ? (size_t)std::max(1, atoi(e)) : (size_t(1) << 20);
+}
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = getenv("SKY_FUSED_OUT");
@@ -653,7 +663,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // launch that initialises the pruner sample
     const int KM = p.Kp * p.M;
     const size_t rb64 = row_bytes(true, D);
-    const size_t cap = (size_t)n + KM;
+    // candidate slots: sized by the last runs' need (at least 1M), not by n (f64 rows of n + KM
+    // slots were 6.4 GB at 100M tuples for 241k candidates); a run that overflows the slots
+    // (counted on the device, writes past the capacity dropped) is re-run with room for all
+    const size_t cap_full = (size_t)n + KM;
+    const size_t cap = std::min(cap_full, std::max(p.slot_hint, std::min(cap_full, slot_min())));
     SKY_TRY(p.status.ensure((size_t)tiles * kTile * 2));         // whole tiles: see load_status8
     SKY_TRY(p.rows.ensure(cap * rb64));
     SKY_TRY(p.sortkey.ensure(cap * 8));
@@ -701,6 +715,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.orand = p.orand.as<unsigned long long>();
     fa.dup_cnt = p.dup_cnt.as<uint32_t>();
     fa.flags = p.flags.as<uint32_t>();
+    fa.slot_cap = (uint32_t)cap;
     const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;
     if (angle_keys) {
         SKY_TRY(p.defer.ensure((size_t)n * 4));
@@ -730,6 +745,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     aa.slot_src = p.slot_src.as<uint32_t>();
     aa.flags = p.flags.as<uint32_t>();
     aa.orand = p.orand.as<unsigned long long>();
+    aa.slot_cap = (uint32_t)cap;
     launch_append_pruners(D, aa, st);
     STAGE(st, "compact");
     uint32_t m = 0, nps = 0, flags = 0;
@@ -741,6 +757,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; rejected");
         return SKY_E_NAN;
     }
+    if ((size_t)m + nps > cap) {                 // slots overflowed: again, with room for every candidate
+        p.slot_hint = std::min(cap_full, ((size_t)m + nps) * 5 / 4 + (size_t)KM);
+        p.slot_reruns++;
+        return pipe_run(c, p, in, tm);
+    }
+    p.slot_hint = std::max(p.slot_hint, std::min(cap_full, 2 * ((size_t)m + nps)));
     p.m = m;
     p.nps = nps;
     p.f64 = (flags & kFlagNotF32) != 0;

@@ -280,6 +280,7 @@ __device__ __forceinline__ void append_candidate(const FilterArgs &a, bool cand,
     if (!cand) return;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t slot = base + (uint32_t)__popcll(cm & lt);
+    if (slot >= a.slot_cap) return;          // counted; the host re-runs with more slots
     constexpr int DP = padded_dims<double>(D);
     store_row<double, D>(a.crow + (size_t)slot * DP, v);
     const uint64_t key = make_sortkey<double, D>(v, (uint32_t)k, lflags);
@@ -482,6 +483,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         double v[D];
         load_row<D>(a.vals + (size_t)i * D, v);
         const uint32_t slot = s_base + q;
+        if (slot >= a.slot_cap) continue;      // counted; the host re-runs with more slots
         constexpr int DP = padded_dims<double>(D);
         store_row<double, D>(a.crow + (size_t)slot * DP, v);
         const uint64_t key = make_sortkey<double, D>(v, k, lflags);
@@ -664,11 +666,13 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
             const uint32_t slot = m + e;
             a.entries[e] = q;
             a.pruner_slot[q] = (int32_t)slot;
-            a.slot_src[slot] = 0x80000000u | e;
-            const double *pr = a.pruners + (size_t)q * D;
-            const uint64_t key = emit_pruner<double, D>(pr, q / a.M, (double *)a.rows, slot, a.sortkey, lflags);
-            o |= key;
-            an &= key;
+            if (slot < a.slot_cap) {             // past it: the host re-runs with more slots
+                a.slot_src[slot] = 0x80000000u | e;
+                const double *pr = a.pruners + (size_t)q * D;
+                const uint64_t key = emit_pruner<double, D>(pr, q / a.M, (double *)a.rows, slot, a.sortkey, lflags);
+                o |= key;
+                an &= key;
+            }
         } else if (q < KM) {
             a.pruner_slot[q] = -1;
         }

@@ -73,6 +73,7 @@ struct FilterArgs {
     uint32_t *flags;              // kFlag*
     uint32_t *defer_list;         // [n] MR-Angle tuples whose key needs the exact path
     uint32_t *defer_cnt;
+    uint32_t slot_cap;            // slots allocated: appends past it are counted, not written
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
@@ -96,6 +97,7 @@ struct AppendArgs {
     uint32_t *slot_src;
     uint32_t *flags;
     unsigned long long *orand;
+    uint32_t slot_cap;
 };
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st);
 struct FateArgs {

@@ -352,3 +352,23 @@ def test_duplicated_pruner_with_non_f32_values(gpu_engine_factory, oracle):
     vals[3::11] = p + np.array([1e-9, 0.0, 0.0])           # dominated by p only in f64 arithmetic
     for algo in ("mr-angle", "mr-dim"):
         check_vs_oracle(gpu_engine_factory, oracle, vals, 8, algo)
+
+
+@pytest.mark.parametrize("dist,D,algo", [("uniform", 6, "mr-angle"), ("std_anti", 4, "mr-dim"),
+                                         ("anti_correlated", 8, "mr-angle")])
+def test_candidate_slot_overflow_reruns(dist, D, algo, gpu_engine_factory, oracle, monkeypatch):
+    """Candidate slots are sized by the last runs' need, not by n: a run whose candidates
+    overflow them (SKY_SLOT_MIN forces a tiny first allocation) is re-run with room for all of
+    them, with the same result as the oracle; later queries on the context reuse the grown slots."""
+    monkeypatch.setenv("SKY_SLOT_MIN", "64")
+    vals = oracle.synth(DISTS[dist], D, 80000, seed=44 + D)
+    eng = gpu_engine_factory(D, 8, algo)
+    exp, keys, els, esv = oracle.query_sfs(algo[3:], vals, 8)
+    for _ in range(2):
+        ids, org = eng.query(vals)
+        np.testing.assert_array_equal(ids, exp)
+        np.testing.assert_array_equal(org, keys[exp])
+        ls, sv = eng.stats()
+        np.testing.assert_array_equal(ls, els)
+        np.testing.assert_array_equal(sv, esv)
+    eng.close()
