@@ -182,6 +182,48 @@ int sky_ctx_sync(sky_ctx *c) {
     return SKY_OK;
 }
 
+// One-time warm-up (off any timed path): a small device-generated query down each pipeline
+// branch — the bounding-box pass (forced), the brute pass, the sort path — so that the first
+// real query that takes a branch does not pay for its kernels' first launch (code-object
+// loading) and first allocations inside its latency (C5: a 20-30 ms first-use spike).
+int sky_ctx_warmup(sky_ctx *c) {
+    GUARD_BEGIN
+    ARG_CHECK(c, "ctx is null");
+    SKY_TRY(bind(c));
+    const int D = c->D;
+    const int64_t n = 40000;
+    DevBuf v, ids, oi, oo;
+    SKY_TRY(v.ensure((size_t)n * D * 8));
+    SKY_TRY(ids.ensure((size_t)n * 8));
+    SKY_TRY(oi.ensure((size_t)n * 8));
+    SKY_TRY(oo.ensure((size_t)n * 4));
+    for (int pass = 0; pass < 3; pass++) {
+        // std-anti: many distinct candidates (bounding-box pass, then the SFS sort path);
+        // the reference formula: few candidates (brute pass)
+        launch_synth(pass == 2 ? 2 : 3, D, 0, 1000, 99 + pass, 0, n, v.as<double>(), ids.as<int64_t>(), c->st);
+        HIP_TRY(hipGetLastError());
+        PipeIn in;
+        in.vals = v.as<double>();
+        in.ids = ids.as<int64_t>();
+        in.n = (uint32_t)n;
+        in.global = true;
+        in.K = c->Kq();
+        in.out_ids = oi.as<int64_t>();
+        in.out_org = oo.as<int32_t>();
+        in.out_cap = n;
+        c->shard_valid = false;
+        c->warm_mode = pass == 0 ? 1 : (pass == 1 ? 2 : 0);   // 1: force the box pass, 2: force SFS
+        const int rc = pipe_run(*c, c->main, in, nullptr);
+        c->warm_mode = 0;
+        if (rc != SKY_OK) return rc;
+        int64_t g = 0;
+        SKY_TRY(pipe_output(*c, c->main, in, false, in.out_ids, in.out_org, nullptr, n, &g, nullptr));
+    }
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
 int sky_partition_keys_dev(sky_ctx *c, const double *d_values, int64_t n, int32_t *d_keys_out) {
     GUARD_BEGIN
     ARG_CHECK(c && (n == 0 || (d_values && d_keys_out)), "null argument");

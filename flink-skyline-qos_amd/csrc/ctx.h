@@ -49,6 +49,7 @@ struct Ctx {
     std::vector<int64_t> lsz, surv;
     int K_last = 0;
     int profile = 0;            // 0 off, 1 kernel timers (HIP events per timed kernel), 2 + phase events
+    int warm_mode = 0;          // sky_ctx_warmup: 1 force the bounding-box pass, 2 force the SFS path
     PhaseTimer pt;
     double phase_ms[SKY_PHASES] = {};
     int64_t counters[8] = {};

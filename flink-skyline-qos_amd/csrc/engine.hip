@@ -11,6 +11,7 @@
 #include "ctx.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -41,7 +42,13 @@ int DevBuf::ensure(size_t bytes) {
     size_t want = std::max<size_t>(bytes, 256);
     if (regrow) want = std::max(want, bytes + bytes / 2);
     want = (want + 4095) & ~size_t(4095);
-    if (hipMalloc(&p, want) != hipSuccess) {
+    static const bool trace_alloc = getenv("SKY_TRACE_ALLOC") != nullptr;   // measurement only
+    auto t0 = std::chrono::steady_clock::now();
+    const hipError_t me = hipMalloc(&p, want);
+    if (trace_alloc)
+        fprintf(stderr, "[sky] hipMalloc %zu bytes: %.3f ms\n", want,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    if (me != hipSuccess) {
         p = nullptr;
         cap = 0;
         (void)hipGetLastError();
@@ -53,7 +60,14 @@ int DevBuf::ensure(size_t bytes) {
 }
 
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    static const bool trace_alloc = getenv("SKY_TRACE_ALLOC") != nullptr;   // measurement only
+    if (p) {
+        auto t0 = std::chrono::steady_clock::now();
+        (void)hipFree(p);
+        if (trace_alloc)
+            fprintf(stderr, "[sky] hipFree %zu bytes: %.3f ms\n", cap,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
     p = nullptr;
     cap = 0;
 }
@@ -828,7 +842,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const uint32_t mt = p.mt;
     // small candidate sets (typical after the prefilter): both skyline levels by one
     // brute-force launch instead of the round-based SFS (SKY_BRUTE=0: A/B knob)
-    const bool brute = in.fate && mt > 0 && mt <= kBruteMax && !brute_disabled();
+    const bool brute = in.fate && mt > 0 && mt <= kBruteMax && !brute_disabled() && c.warm_mode == 0;
     const size_t rb = row_bytes(p.f64, D);
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
@@ -931,7 +945,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         }
         HIP_TRY(fill.launch(st));
         const int W16 = dom16_words(D);
-        const bool use_mbr = mr >= mbr_min() && !mbr_disabled();
+        const bool use_mbr = c.warm_mode == 1 || (c.warm_mode == 0 && mr >= mbr_min() && !mbr_disabled());
         if (use_mbr) {
             SKY_TRY(mbr_run(c, p, in, mr, gmerge));
         } else if (p.u16) {

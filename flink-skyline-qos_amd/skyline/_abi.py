@@ -54,6 +54,7 @@ SIGNATURES = {
     "sky_ctx_set_stream": [c_p, c_p],
     "sky_ctx_set_grid_filter": [c_p, c_int],
     "sky_ctx_sync": [c_p],
+    "sky_ctx_warmup": [c_p],
     "sky_ctx_wait_stream": [c_p, c_p],
     "sky_ctx_signal_stream": [c_p, c_p],
     "sky_partition_keys": [c_p, c_p, c_i64, c_p],

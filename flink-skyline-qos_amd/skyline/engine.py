@@ -69,6 +69,10 @@ class SkylineEngine:
         self.last_dist_stats = None      # set by skyline.dist.distributed_query
         self.K = self.P if not (self.algo == _abi.ALGO_GRID and semantics == "complete") else max(self.P, 1 << self.dims)
 
+    def warmup(self):
+        """sky_ctx_warmup: first launches and allocations of every pipeline branch, once."""
+        check(lib().sky_ctx_warmup(self.h))
+
     def close(self):
         if self.h:
             lib().sky_ctx_destroy(self.h)
@@ -324,6 +328,11 @@ class SkylineStream:
         g = ctypes.c_int64(0)
         check(lib().sky_stream_query(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
         return ids[:g.value].copy(), org[:g.value].copy()
+
+    def reserve(self, cap):
+        """Size the page-locked result buffers once (pinning hundreds of MB takes tens of ms:
+        not something a trigger should pay)."""
+        self._out(max(int(cap), 1))
 
     def query_host_view(self):
         """Query into the reusable page-locked buffers; returns g (results in view()[:g])."""

@@ -90,6 +90,10 @@ int sky_ctx_set_grid_filter(sky_ctx *ctx, int on);
  * NULL returns to the context's own stream. */
 int sky_ctx_set_stream(sky_ctx *ctx, void *hip_stream);
 int sky_ctx_sync(sky_ctx *ctx);
+/* One-time warm-up: a small device-generated query down each pipeline branch, so that no later
+ * query pays for first kernel launches / first allocations inside its latency.  Optional; call
+ * once after sky_ctx_create (e.g. in the operator's open()), never on a timed path. */
+int sky_ctx_warmup(sky_ctx *ctx);
 /* cross-stream ordering for *_dev callers that produce / consume the device buffers on
  * their own HIP stream (e.g. a framework's current stream): wait_stream makes the
  * context's later work wait for everything already enqueued on `hip_stream`;

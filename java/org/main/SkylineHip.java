@@ -32,6 +32,7 @@ public final class SkylineHip {
 
     public static native long ctxCreate(int device, int dims, int partitions, int algo, double domain);
     public static native void ctxDestroy(long ctx);
+    public static native void ctxWarmup(long ctx);            // once in open(): first launches off the query path
     public static native void ctxSetSemantics(long ctx, int semantics);
     public static native void ctxSetGridFilter(long ctx, boolean on);
 

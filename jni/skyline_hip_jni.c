@@ -48,6 +48,10 @@ JNIEXPORT void JNICALL Java_org_main_SkylineHip_ctxDestroy(JNIEnv *env, jclass c
     fail(env, sky_ctx_destroy(CTX(ctx)));
 }
 
+JNIEXPORT void JNICALL Java_org_main_SkylineHip_ctxWarmup(JNIEnv *env, jclass cls, jlong ctx) {
+    fail(env, sky_ctx_warmup(CTX(ctx)));
+}
+
 JNIEXPORT void JNICALL Java_org_main_SkylineHip_ctxSetSemantics(JNIEnv *env, jclass cls, jlong ctx, jint sem) {
     fail(env, sky_ctx_set_semantics(CTX(ctx), sem));
 }

@@ -372,3 +372,19 @@ def test_candidate_slot_overflow_reruns(dist, D, algo, gpu_engine_factory, oracl
         np.testing.assert_array_equal(ls, els)
         np.testing.assert_array_equal(sv, esv)
     eng.close()
+
+
+def test_warmup_then_queries(gpu_engine_factory, oracle):
+    """sky_ctx_warmup runs every pipeline branch once on device-generated data; the context's
+    later queries (small and large rep sets) are unaffected."""
+    eng = gpu_engine_factory(6, 8, "mr-angle")
+    eng.warmup()
+    for dist, n in (("std_anti", 30000), ("anti_correlated", 60000), ("uniform", 50000)):
+        vals = oracle.synth(DISTS[dist], 6, n, seed=5)
+        ids, org = eng.query(vals)
+        exp, keys, els, esv = oracle.query_sfs("angle", vals, 8)
+        np.testing.assert_array_equal(ids, exp)
+        ls, sv = eng.stats()
+        np.testing.assert_array_equal(ls, els)
+        np.testing.assert_array_equal(sv, esv)
+    eng.close()
