@@ -542,6 +542,18 @@ __device__ __forceinline__ bool swar_digits(const uint32_t *__restrict__ buf, in
     return ok;
 }
 
+// the same for len <= 8 (one window, three LDS words): the producer's ids (< 10^8 for 100M
+// records) and values (<= 4 digits) all take it; chosen per wave, so the branch is uniform
+__device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, int s, int len, uint64_t &v) {
+    const int k = s >> 2, sh = (s & 3) * 8;
+    const uint64_t A = (uint64_t)buf[k] | ((uint64_t)buf[k + 1] << 32);
+    const uint64_t C = buf[k + 2];
+    const uint64_t x0 = sh ? (A >> sh) | (C << (64 - sh)) : A;
+    const uint64_t y0 = swar_pad(x0, len);
+    v = swar_value(y0);
+    return len >= 1 && len <= 8 && swar_is_digits(y0);
+}
+
 __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
                                                             const int64_t *__restrict__ line_end, int64_t nl,
                                                             int64_t nrec, int D, int64_t *__restrict__ ids,
@@ -552,10 +564,9 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                                                             unsigned long long *__restrict__ slow_n,
                                                             unsigned long long slow_cap, int R, int stop) {
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kFieldText / 4 + 8];
-    __shared__ uint16_t s_dpos[kFieldsMax];
-    __shared__ uint8_t s_drec[kFieldsMax];
+    __shared__ uint32_t s_dl[kFieldsMax];                // delimiter f: staged byte offset | record << 16
     __shared__ uint16_t s_rfirst[kCsvThreads + 1];
-    __shared__ int s_last[kCsvThreads], s_fempty[kCsvThreads];
+    __shared__ int s_fempty[kCsvThreads];
     __shared__ uint8_t s_bad[kCsvThreads], s_idok[kCsvThreads];
     __shared__ uint32_t s_w[8], s_cnt[4];
     const int tid = threadIdx.x;
@@ -601,7 +612,6 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     }
     if (stop == 1) { __syncthreads(); if (s_buf[tid] == 0x12345678u) status[0] = 9; return; }
     if (tid < 4) s_cnt[tid] = 0;
-    s_last[tid] = 0;
     s_fempty[tid] = 0x7fffffff;
     s_bad[tid] = 0;
     uint32_t mcs[kUnits * 4], mns[kUnits * 4];
@@ -647,8 +657,8 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     if (tid == 0) {
         s_rfirst[0] = 0;
         if (tail_open) {                                   // virtual delimiter closing the tail record
-            s_dpos[nf - 1] = (uint16_t)hi;
-            s_drec[nf - 1] = (uint8_t)(nr - 1);
+            s_dl[nf - 1] = (uint32_t)hi | ((uint32_t)(nr - 1) << 16);
+            s_rfirst[nr] = (uint16_t)nf;
         }
     }
     {
@@ -661,8 +671,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
             while (m) {
                 const int bit = __ffs(m) - 1;
                 m &= m - 1;
-                s_dpos[f] = (uint16_t)(b0 + (bit >> 3));
-                s_drec[f] = (uint8_t)rec;
+                s_dl[f] = (uint32_t)(b0 + (bit >> 3)) | (rec << 16);
                 if ((mn >> bit) & 1u) {
                     rec++;
                     s_rfirst[rec] = (uint16_t)(f + 1);
@@ -672,16 +681,18 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         }
     }
     __syncthreads();
-    if (stop == 2) { if (s_dpos[tid] == 0x1234) status[0] = 9; return; }
+    if (stop == 2) { if (s_dl[tid] == 0x1234u) status[0] = 9; return; }
     // 3. fields
     const LdsSrc src{reinterpret_cast<const uint8_t *>(s_buf), 0};
     for (int f = tid; f < nf; f += kCsvThreads) {
-        const int s = f == 0 ? lo : (int)s_dpos[f - 1] + 1;
-        const int e = s_dpos[f];
-        const int j = s_drec[f];
+        const uint32_t dl = s_dl[f];
+        const int s = f == 0 ? lo : (int)(s_dl[f - 1] & 0xffffu) + 1;
+        const int e = (int)(dl & 0xffffu);
+        const int j = (int)(dl >> 16);
         const int col = f - (int)s_rfirst[j];
         uint64_t u = 0;
-        const bool fast = swar_digits(s_buf, s, e - s, u);
+        const bool fast = __ballot(e - s > 8) == 0ull ? swar_digits8(s_buf, s, e - s, u)
+                                                       : swar_digits(s_buf, s, e - s, u);
         const bool is_id = col == 0, empty = s == e;
         int64_t idv = (int64_t)u;                          // < 10^16
         double v = (double)u;                              // exact when len <= 15
@@ -708,14 +719,23 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                     if (k < slow_cap) slow[k] = make_longlong3(a0 + s, a0 + e, o);
                 }
             }
-            atomicMax(&s_last[j], col);
         }
     }
     __syncthreads();
     if (stop == 3) return;
-    // 4. records
+    // 4. records.  The last non-empty column: the record's field count - 1 unless it has an empty
+    // field (rare: then its fields are walked here) — no per-field LDS atomic (the lanes of one
+    // record all hit the same word)
     if (tid < nr) {
-        const int last = s_last[tid];
+        const int f0 = s_rfirst[tid], f1 = s_rfirst[tid + 1];   // delimiters [f0, f1) close its fields
+        int last = f1 - f0 - 1;
+        if (s_fempty[tid] != 0x7fffffff) {
+            last = 0;
+            for (int f = f0 + 1; f < f1; f++) {
+                const int fs = (int)(s_dl[f - 1] & 0xffffu) + 1, fe = (int)(s_dl[f] & 0xffffu);
+                if (fe > fs) last = f - f0;
+            }
+        }
         uint8_t st;
         if (s_bad[tid] || last == 0 || s_fempty[tid] < last) st = SKY_CSV_MALFORMED;   // ServiceTuple.java:93,101
         else if (!s_idok[tid]) st = SKY_CSV_BAD_ID;                                      // FlinkSkyline.java:276
