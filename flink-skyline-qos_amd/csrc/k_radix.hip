@@ -320,8 +320,16 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     if (launch_err) *launch_err = hipSuccess;
     g_radix_last_passes = 0;
     if (m <= 1 || varying_bits == 0) return false;
-    const bool big = m >= (1u << 22);   // 4096-key tiles for large sorts, 1024 for the query's candidates
-    const uint32_t tile_sz = big ? 4096u : (uint32_t)kRadixTile;
+    // 6144-key tiles for large sorts (fewer tiles: less look-back, longer digit runs per tile;
+    // 100M pairs: 24 keys per thread 5.86 ms, 16: 6.99, 12: 7.45, 8: 8.44, 32 (1 wave per SIMD):
+    // 7.43), 1024 for the query's candidates
+    const bool big = m >= (1u << 22);
+    static const int big_items = [] {   // SKY_RADIX_ITEMS: keys per thread of the large-sort tiles (A/B knob)
+        const char *e = getenv("SKY_RADIX_ITEMS");
+        const int v = e ? atoi(e) : 24;
+        return v == 8 || v == 12 || v == 16 || v == 24 || v == 32 ? v : 24;
+    }();
+    const uint32_t tile_sz = big ? (uint32_t)(kRadixThreads * big_items) : (uint32_t)kRadixTile;
     const uint32_t tiles = (m + tile_sz - 1) / tile_sz;
     RsRuns runs{};
     int nbits = 0;
@@ -379,9 +387,20 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
         const uint32_t *vin = alt ? vals_alt : vals;
         uint64_t *kout = alt ? k0 : k1;
         uint32_t *vout = alt ? vals : vals_alt;
-        if (big)
-            k_rs_onesweep<16><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], ghist + p * 256,
-                                                               status + (size_t)p * 256 * tiles, tickets + p, err);
+        if (big) {
+            uint32_t *stp = status + (size_t)p * 256 * tiles;
+            const uint32_t *gb = ghist + p * 256;
+            if (big_items == 8)
+                k_rs_onesweep<8><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], gb, stp, tickets + p, err);
+            else if (big_items == 12)
+                k_rs_onesweep<12><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], gb, stp, tickets + p, err);
+            else if (big_items == 32)
+                k_rs_onesweep<32><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], gb, stp, tickets + p, err);
+            else if (big_items == 24)
+                k_rs_onesweep<24><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], gb, stp, tickets + p, err);
+            else
+                k_rs_onesweep<16><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p], gb, stp, tickets + p, err);
+        }
         else
             k_rs_onesweep<kRadixItems><<<tiles, kRadixThreads, 0, st>>>(kin, vin, kout, vout, m, shifts.s[p],
                                                                         ghist + p * 256,
