@@ -76,7 +76,7 @@ struct Pipe {
     DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2, rows3, sortkey3, slot_src3;
     // bounding-box pruned all-pairs pass over large rep sets (k_mbr.hip)
     DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_sub, mbr_domf,
-        mbr_pairs;
+        mbr_pairs, mbr_gmin, mbr_gpr;
     bool used_mbr = false;
     size_t slot_hint = 0;       // candidate slots the next run allocates (grown on overflow)
     int64_t slot_reruns = 0;    // runs repeated because the slots overflowed
@@ -97,7 +97,7 @@ struct Pipe {
     // results of the last run
     uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0, mt_pre = 0;
     int M = 1, Kp = 1, K = 1;
-    bool f64 = false, ties = false, u16 = false;
+    bool f64 = false, ties = false, u16 = false, ints = false;   // ints: every candidate value an integer in [0, 65535]
     std::vector<uint32_t> h_dup;
     std::vector<int32_t> h_entries;
     std::vector<unsigned long long> h_lsz, h_surv;

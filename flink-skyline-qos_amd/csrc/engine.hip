@@ -180,6 +180,11 @@ static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
     return e && atoi(e) == 0;
 }
+// SKY_BRUTE16=0: the small-set pair pass compares f32 even for integer rows (A/B knob)
+static bool brute16_disabled() {
+    const char *e = getenv("SKY_BRUTE16");
+    return e && atoi(e) == 0;
+}
 // SKY_GATHER=0 reads counters back by one hipMemcpyAsync per range (A/B knob)
 static bool gather_disabled() {
     const char *e = getenv("SKY_GATHER");
@@ -590,6 +595,8 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
     SKY_TRY(p.mbr_sub.ensure(ntiles * 4 * NW * 4));
+    SKY_TRY(p.mbr_gmin.ensure(mbr_groups(mr) * NW * 4));
+    SKY_TRY(p.mbr_gpr.ensure(mbr_groups(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
     SKY_TRY(p.mbr_pairs.ensure(16));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
@@ -626,6 +633,8 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.tmax = p.mbr_max.as<uint32_t>();
     a.tprange = p.mbr_pr.as<uint32_t>();
     a.tsub = p.mbr_sub.as<uint32_t>();
+    a.gmin = p.mbr_gmin.as<uint32_t>();
+    a.gprange = p.mbr_gpr.as<uint32_t>();
     a.domf = p.mbr_domf.as<uint32_t>();
     a.pairs = p.mbr_pairs.as<unsigned long long>();
     a.alive_l = p.alive_l.as<uint8_t>();
@@ -781,7 +790,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.nps = nps;
     p.f64 = (flags & kFlagNotF32) != 0;
     p.ties = (flags & kFlagScoreTies) != 0;
-    p.u16 = !p.f64 && !p.ties && (flags & kFlagNotU16) == 0 && !sfs16_disabled();
+    p.ints = !p.f64 && (flags & kFlagNotU16) == 0;
+    p.u16 = p.ints && !p.ties && !sfs16_disabled();
     p.mt = m + nps;
     p.mt_pre = p.mt;
     p.s_rows = &p.rows;
@@ -1024,7 +1034,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         fill.add(p.keep.p, (size_t)mt * 4);
         HIP_TRY(fill.launch(st));
         c.ktimer_begin("brute", st);
-        launch_brute_fates(D, !p.f64, p.s_rows->p, p.s_key->as<uint64_t>(), mt, in.global && !in.single,
+        launch_brute_fates(D, !p.f64, p.ints && !brute16_disabled(), p.s_rows->p, p.s_key->as<uint64_t>(), mt, in.global && !in.single,
                            p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
                            p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st);
         c.ktimer_end("brute", st, (int64_t)mt * mt);

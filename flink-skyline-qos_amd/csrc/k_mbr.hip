@@ -272,6 +272,44 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
     }
 }
 
+// groups of 64 consecutive tiles: min corner and partition range (one wave per group); the
+// pair pass skips a whole group whose corner is not <= the y tile's max corner
+constexpr int kMbrG = 64;   // tiles per group
+
+template <class R>
+__global__ __launch_bounds__(kThreads) void k_mbr_groups(const uint32_t *__restrict__ tmin,
+                                                         const uint32_t *__restrict__ tprange, uint32_t ntiles,
+                                                         uint32_t ngroups, uint32_t *__restrict__ gmin,
+                                                         uint32_t *__restrict__ gprange) {
+    constexpr int NW = R::NW;
+    const uint32_t g = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (g >= ngroups) return;
+    const uint32_t t = g * kMbrG + (threadIdx.x & 63);
+    uint32_t mn[NW], pl = 0xffffffffu, ph = 0u;
+    R::ident_min(mn);
+    if (t < ntiles) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) mn[w] = tmin[(size_t)w * ntiles + t];
+        const uint32_t r = tprange[t];
+        pl = r & 0xffffu;
+        ph = r >> 16;
+    }
+#pragma unroll
+    for (int o = 1; o <= 32; o <<= 1) {
+        uint32_t a[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) a[w] = (uint32_t)__shfl_xor((int)mn[w], o, 64);
+        R::cmin(mn, a);
+        pl = min(pl, (uint32_t)__shfl_xor((int)pl, o, 64));
+        ph = max(ph, (uint32_t)__shfl_xor((int)ph, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) gmin[(size_t)w * ngroups + g] = mn[w];
+        gprange[g] = pl | (ph << 16);
+    }
+}
+
 // ---- the pair pass -------------------------------------------------------------------
 // FULL: the complete test (x <= y and not y <= x) — given partition keys may repeat a
 // vector across partitions, and f32/f64 rows may hold -0.0 / +0.0 twins; otherwise the rows
@@ -288,7 +326,9 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tmax,
                                                         const uint32_t *__restrict__ tprange,
-                                                        const uint32_t *__restrict__ tsub, uint32_t mr,
+                                                        const uint32_t *__restrict__ tsub,
+                                                        const uint32_t *__restrict__ gmin,
+                                                        const uint32_t *__restrict__ gprange, uint32_t mr,
                                                         uint32_t ntiles, uint32_t nsplit, int dbg, uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs) {
     constexpr int NW = R::NW;
@@ -303,8 +343,8 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     const uint32_t split = blk % nsplit;
     const uint32_t yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kThreads / 64) + (threadIdx.x >> 6));
     if (yt >= ntiles) return;
-    const uint32_t ngroups = (ntiles + 63) / 64;
-    const uint32_t g_lo = split * ngroups / nsplit * 64, g_hi = min(ntiles, (split + 1) * ngroups / nsplit * 64);
+    const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
+    const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
     const bool valid = j < mr;
@@ -498,15 +538,41 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
         __builtin_amdgcn_wave_barrier();
     };
 
-    // the next group's box corners load into the same registers right after the current
+    // groups 64 at a time (lane = group): the reachable ones as a wave mask; within it the
+    // next group's tile corners load into the same registers right after the current
     // group's list is built, so they are in flight while its tiles are tested (no
     // loop-carried copy of registers still being loaded)
     uint32_t tg[NW], tr = 0;
-    if (g_lo < g_hi) load_group(tg, tr, g_lo);
-    for (uint32_t g = g_lo; g < g_hi && live; g += 64) {
-        const uint32_t cnt = candidates(tg, tr, g);
-        if (g + 64 < g_hi) load_group(tg, tr, g + 64);
-        process(cnt);
+    for (uint32_t s0 = gs_lo; s0 < gs_hi && live; s0 += 64) {
+        uint64_t gm;
+        {
+            const uint32_t q = min(s0 + lane, ngroups - 1u);
+            uint32_t gc[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
+            const uint32_t gr = gprange[q];
+            const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
+            bool cand = s0 + lane < gs_hi && R::le(gc, ymax);
+            if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
+            gm = __ballot(cand);
+        }
+        if (!gm) continue;
+        uint32_t g = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
+        gm &= gm - 1;
+        load_group(tg, tr, g);
+        for (;;) {
+            const uint32_t cnt = candidates(tg, tr, g);
+            const bool more = gm != 0ull;
+            uint32_t gn = 0;
+            if (more) {
+                gn = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
+                gm &= gm - 1;
+                load_group(tg, tr, gn);
+            }
+            process(cnt);
+            if (!more || !live) break;
+            g = gn;
+        }
     }
     if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
     if (lane == 0 && pairs) {
@@ -539,6 +605,7 @@ static int mbr_bits(int D) {
 }
 
 size_t mbr_tiles(uint32_t mr) { return (mr + kMbrT - 1) / kMbrT; }
+size_t mbr_groups(uint32_t mr) { return (mbr_tiles(mr) + kMbrG - 1) / kMbrG; }
 
 template <class R, int D>
 static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
@@ -558,21 +625,19 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
     k_mbr_tiles<R><<<gt, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, perm, mr, ntiles, a.trows, a.tpart,
                                             a.tmin, a.tmax, a.tprange, a.tsub);
+    const uint32_t ngroups = (uint32_t)mbr_groups(mr);
+    k_mbr_groups<R><<<(ngroups + 3) / 4, kThreads, 0, st>>>(a.tmin, a.tprange, ntiles, ngroups, a.gmin, a.gprange);
+#define SKY_MBR_PAIRS(F, G)                                                                                  \
+    k_mbr_pairs<R, F, G><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, a.gmin,    \
+                                                  a.gprange, mr, ntiles, nsplit, a.dbg, a.domf, a.pairs)
     if (a.full) {
-        if (a.gmerge)
-            k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr, ntiles,
-                                                                nsplit, a.dbg, a.domf, a.pairs);
-        else
-            k_mbr_pairs<R, true, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
-                                                                 ntiles, nsplit, a.dbg, a.domf, a.pairs);
+        if (a.gmerge) SKY_MBR_PAIRS(true, true);
+        else SKY_MBR_PAIRS(true, false);
     } else {
-        if (a.gmerge)
-            k_mbr_pairs<R, false, true><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
-                                                                 ntiles, nsplit, a.dbg, a.domf, a.pairs);
-        else
-            k_mbr_pairs<R, false, false><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, mr,
-                                                                  ntiles, nsplit, a.dbg, a.domf, a.pairs);
+        if (a.gmerge) SKY_MBR_PAIRS(false, true);
+        else SKY_MBR_PAIRS(false, false);
     }
+#undef SKY_MBR_PAIRS
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);
 }
 

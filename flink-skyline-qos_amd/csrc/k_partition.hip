@@ -176,7 +176,8 @@ __global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restric
     }
     __syncthreads();
     for (int q = threadIdx.x; q < KM; q += kThreads)
-        if (s_min[q] != ~0ull) atomicMin(&gmin[q], s_min[q]);
+        if (s_min[q] != ~0ull && s_min[q] < __hip_atomic_load(&gmin[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&gmin[q], s_min[q]);
 }
 
 // One workgroup per partition: the (<= M) winners are deduplicated (equal rows keep
@@ -711,48 +712,63 @@ __device__ __forceinline__ float cand_eps(int j, int d) {
     h ^= h >> 12;
     return (float)(h >> 8) * (1e-4f / 16777216.0f);
 }
-template <int D>
-__device__ __forceinline__ float cand_criterion(const float (&f)[D], float sum, int j) {
+__device__ __forceinline__ float cand_weight(int j, int d, int D) {
     const int b = j & 15;
     int da = -1, db = -1;
     if (b >= 1 && b <= D) da = b - 1;
     else if (b > D) { da = (b - 1) % D; db = (b - 1 + 1 + (b - 1) / D) % D; }
-    float c = 0.0f;
-#pragma unroll
-    for (int d = 0; d < D; d++) {
-        const float w = 1.0f + (d == da ? 3.0f : 0.0f) + (d == db ? 3.0f : 0.0f) + cand_eps(j, d);
-        c += w * f[d];
-    }
-    (void)sum;
-    return c;
+    return 1.0f + (d == da ? 3.0f : 0.0f) + (d == db ? 3.0f : 0.0f) + cand_eps(j, d);
 }
 
+// The weights are row-independent: computed once per workgroup into LDS (read back as
+// broadcasts), and a slot only issues the LDS atomicMin when it beats the value it reads
+// (the minima settle after a few rows, so most slots issue none)
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cand_min(const double *__restrict__ rows, const uint64_t *__restrict__ key,
                                                        uint32_t mt, int Kp, int M2,
                                                        unsigned long long *__restrict__ gmin) {
     constexpr int DP = padded_dims<double>(D);
     __shared__ unsigned long long s_min[2048];
+    __shared__ float s_w[64][D];
     const int KM = Kp * M2;
     for (int q = threadIdx.x; q < KM; q += kThreads) s_min[q] = ~0ull;
+    for (int q = threadIdx.x; q < M2 * D; q += kThreads) s_w[q / D][q % D] = cand_weight(q / D, q % D, D);
     __syncthreads();
-    for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < mt; j += gridDim.x * kThreads) {
-        const int k = (int)(key[j] >> 56);
-        double v[D];
-        load_trow<double, D>(rows + (size_t)j * DP, v);
-        float f[D];
-        float sum = 0.0f;
+    // two rows per thread and iteration, both loads issued before either is used
+    const uint32_t stride = gridDim.x * kThreads;
+    for (uint32_t j0 = blockIdx.x * kThreads + threadIdx.x; j0 < mt; j0 += 2 * stride) {
+        double v[2][D];
+        int k[2];
 #pragma unroll
-        for (int d = 0; d < D; d++) { f[d] = (float)v[d]; sum += f[d]; }
-        for (int c = 0; c < M2; c++) {
-            const float cv = cand_criterion<D>(f, sum, c);
-            if (cv != cv) continue;
-            atomicMin(&s_min[k * M2 + c], ((unsigned long long)f32_order_key(cv) << 32) | j);
+        for (int u = 0; u < 2; u++) {
+            const uint32_t jc = min(j0 + u * stride, mt - 1u);
+            k[u] = (int)(key[jc] >> 56);
+            load_trow<double, D>(rows + (size_t)jc * DP, v[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t j = j0 + u * stride;
+            if (j >= mt) break;
+            float f[D];
+#pragma unroll
+            for (int d = 0; d < D; d++) f[d] = (float)v[u][d];
+            for (int c = 0; c < M2; c++) {
+                float cv = 0.0f;
+#pragma unroll
+                for (int d = 0; d < D; d++) cv += s_w[c][d] * f[d];
+                if (cv != cv) continue;
+                const unsigned long long e = ((unsigned long long)f32_order_key(cv) << 32) | j;
+                unsigned long long *m = &s_min[k[u] * M2 + c];
+                if (e < *m) atomicMin(m, e);
+            }
         }
     }
     __syncthreads();
+    // the global minima: every workgroup's value for one address serialises at L2, so a
+    // workgroup only adds its own when it beats what is already there
     for (int q = threadIdx.x; q < KM; q += kThreads)
-        if (s_min[q] != ~0ull) atomicMin(&gmin[q], s_min[q]);
+        if (s_min[q] != ~0ull && s_min[q] < __hip_atomic_load(&gmin[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(&gmin[q], s_min[q]);
 }
 
 // one 64-lane workgroup per partition: winners deduplicated and mutually non-dominated
@@ -1003,9 +1019,7 @@ __device__ __forceinline__ uint32_t tuple_fate(uint16_t st, const uint8_t *s_pf,
 // origin (see below); given weights (GW) per thread over all its tuples, one wave
 // add when the threads agree on the origin; flushed once per workgroup into
 // per-shard accumulators.  GO / GW: given origins / weights.
-constexpr int kOutTPB = 4;
-
-template <bool GO, bool GW>
+template <bool GO, bool GW, int kOutTPB>
 __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
     __shared__ unsigned long long s_lsz[kMaxK];
     __shared__ unsigned long long s_surv[kMaxK];
@@ -1372,7 +1386,8 @@ void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
 
 void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st) {
     if (!a.mt) return;
-    const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 1024u);
+    // <= 256 workgroups (a few rows per thread): each adds up to Kp*M2 global minima
+    const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 256u);
     SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.Kp, a.M2, a.cmin)));
     SKY_DISPATCH_D(D, (k_cand_pick<DD><<<a.Kp, 64, 0, st>>>(a.rows, a.cmin, a.M2, a.pr2, a.npr2)));
     SKY_DISPATCH_D(D, (k_cand_filter<DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a.rows, a.key, a.mt, a.M2, a.pr2,
@@ -1417,14 +1432,30 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
     if (mt) k_rep_mult<<<nblk(mt, kThreads), kThreads, 0, st>>>(mt, perm, slot_src, rep_of_sorted, given_w, dup_cnt,
                                                                 pr_entries, mult);
 }
+// SKY_OUT_TPB in {4, 8, 16}: tiles per count-pass workgroup (A/B knob)
+static int out_tpb() {
+    static const int v = [] {
+        const char *e = getenv("SKY_OUT_TPB");
+        const int t = e ? atoi(e) : 4;
+        return t == 8 || t == 16 ? t : 4;
+    }();
+    return v;
+}
+template <int TPB>
+static void out_count_t(const OutArgs &a, hipStream_t st) {
+    const unsigned g = nblk(nblk(a.n, kTile), TPB);
+    const bool go = a.given_origin != nullptr, gw = a.given_w != nullptr;
+    if (go && gw) k_out_count<true, true, TPB><<<g, kThreads, 0, st>>>(a);
+    else if (go) k_out_count<true, false, TPB><<<g, kThreads, 0, st>>>(a);
+    else if (gw) k_out_count<false, true, TPB><<<g, kThreads, 0, st>>>(a);
+    else k_out_count<false, false, TPB><<<g, kThreads, 0, st>>>(a);
+}
 void launch_out_count(const OutArgs &a, hipStream_t st) {
     if (!a.n) return;
-    const unsigned g = nblk(nblk(a.n, kTile), kOutTPB);
-    const bool go = a.given_origin != nullptr, gw = a.given_w != nullptr;
-    if (go && gw) k_out_count<true, true><<<g, kThreads, 0, st>>>(a);
-    else if (go) k_out_count<true, false><<<g, kThreads, 0, st>>>(a);
-    else if (gw) k_out_count<false, true><<<g, kThreads, 0, st>>>(a);
-    else k_out_count<false, false><<<g, kThreads, 0, st>>>(a);
+    const int t = out_tpb();
+    if (t == 8) out_count_t<8>(a, st);
+    else if (t == 16) out_count_t<16>(a, st);
+    else out_count_t<4>(a, st);
 }
 void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket, uint32_t *d_total, uint32_t *err,
                       int64_t cap, hipStream_t st) {

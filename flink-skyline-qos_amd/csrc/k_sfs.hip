@@ -647,6 +647,88 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restric
     if (valid && f) atomicOr(&domf[j], f);
 }
 
+// The same two levels for integer rows (every candidate value an integer in [0, 65535]):
+// rows pack into W u32 words of two u16 halves, and for integers
+//     x dominates y  <=>  x <= y everywhere and sum(x) < sum(y)
+// (x <= y with x != y makes the sum strictly smaller; equal vectors have equal sums), i.e.
+//     OR_w sat_u16(x_w - y_w)  |  sat_u32(sum(x) + 1 - sum(y))  == 0.
+// Each lane keeps the minimum of that word over the x chunk (any partition) and of it OR
+// (px ^ py) (same partition): 10 + 3 VALU ops per pair and no per-pair VALU -> SGPR mask
+// traffic.  A workgroup: 256 y (one per lane) against kB16X x rows packed into LDS once.
+constexpr int kB16Y = 256, kB16X = 128;
+
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sat_sub_u16x2(uint32_t x, uint32_t y) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2_t, x),
+                                                                      __builtin_bit_cast(u16x2_t, y)));
+}
+
+template <int D, int W>
+__device__ __forceinline__ uint32_t pack_row16(const double *r, uint32_t (&w)[W]) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < W; q++) {
+        const uint32_t lo = 2 * q < D ? (uint32_t)r[2 * q] : 0u;
+        const uint32_t hi = 2 * q + 1 < D ? (uint32_t)r[2 * q + 1] : 0u;
+        w[q] = lo | (hi << 16);
+        s += lo + hi;
+    }
+    return s;
+}
+
+template <int D, int W>
+__global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restrict__ rows,
+                                                         const uint64_t *__restrict__ key, uint32_t mr,
+                                                         uint32_t *__restrict__ domf) {
+    constexpr int DP = padded_dims<double>(D);
+    __shared__ uint4 s_x[kB16X][W / 4];
+    __shared__ uint2 s_sp[kB16X];                              // (sum + 1, partition)
+    const uint32_t y0 = blockIdx.x * kB16Y, x0 = blockIdx.y * kB16X;
+    const uint32_t cn = mr - x0 < (uint32_t)kB16X ? mr - x0 : (uint32_t)kB16X;
+    if (threadIdx.x < kB16X) {
+        uint32_t w[W];
+        uint2 sp;
+        if (threadIdx.x < cn) {
+            sp.x = pack_row16<D, W>(rows + (size_t)(x0 + threadIdx.x) * DP, w) + 1u;
+            sp.y = (uint32_t)(key[x0 + threadIdx.x] >> 56);
+        } else {                                               // padding: dominates nothing
+#pragma unroll
+            for (int q = 0; q < W; q++) w[q] = 0xffffffffu;
+            sp = make_uint2(0xffffffffu, 0u);
+        }
+#pragma unroll
+        for (int q = 0; q < W / 4; q++) s_x[threadIdx.x][q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        s_sp[threadIdx.x] = sp;
+    }
+    const uint32_t j = y0 + threadIdx.x;
+    const bool valid = j < mr;
+    uint32_t y[W], sy = 0, py = 0;
+    if (valid) {
+        sy = pack_row16<D, W>(rows + (size_t)j * DP, y);
+        py = (uint32_t)(key[j] >> 56);
+    } else {
+#pragma unroll
+        for (int q = 0; q < W; q++) y[q] = 0u;
+    }
+    __syncthreads();
+    const uint32_t cn4 = (cn + 3u) & ~3u;                      // rows cn..cn4-1 are padding
+    uint32_t acc_a = 0xffffffffu, acc_s = 0xffffffffu;
+#pragma unroll 4
+    for (uint32_t i = 0; i < cn4; i++) {
+        uint32_t r = __builtin_elementwise_sub_sat(s_sp[i].x, sy);
+#pragma unroll
+        for (int q = 0; q < W / 4; q++) {
+            const uint4 xw = s_x[i][q];
+            r |= sat_sub_u16x2(xw.x, y[4 * q]) | sat_sub_u16x2(xw.y, y[4 * q + 1]) |
+                 sat_sub_u16x2(xw.z, y[4 * q + 2]) | sat_sub_u16x2(xw.w, y[4 * q + 3]);
+        }
+        acc_a = min(acc_a, r);
+        acc_s = min(acc_s, r | (s_sp[i].y ^ py));
+    }
+    const uint32_t f = (acc_s == 0u ? 3u : 0u) | (acc_a == 0u ? 2u : 0u);
+    if (valid && f) atomicOr(&domf[j], f);
+}
+
 __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key, uint32_t mr, int gmerge,
                                                            const uint32_t *__restrict__ domf,
                                                            uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g,
@@ -673,12 +755,16 @@ __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__res
     }
 }
 
-void launch_brute_fates(int D, bool f32, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
+void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
                         uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
                         uint32_t *slot_rep, hipStream_t st) {
     if (!mr) return;
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
-    if (f32) {
+    if (u16) {
+        const dim3 g16((mr + kB16Y - 1) / kB16Y, (mr + kB16X - 1) / kB16X);
+        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, domf))); }
+        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, domf))); }
+    } else if (f32) {
         SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
     } else {
         SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));

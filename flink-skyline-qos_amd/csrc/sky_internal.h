@@ -237,8 +237,9 @@ void launch_stat_reduce(const unsigned long long *lsz, const unsigned long long 
 constexpr uint32_t kBruteMax = 16384;
 // over f64 candidate slots (rows [mr][pad(D)], sort keys): domf / segalive / segn zeroed by
 // the caller; writes alive_l / alive_g / slot_rep (identity) per slot
-// f32: compare in f32 (every candidate value exactly an f32), else f64
-void launch_brute_fates(int D, bool f32, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
+// f32: compare in f32 (every candidate value exactly an f32), else f64; u16: every candidate
+// value an integer in [0, 65535]: packed u16 compares (k_brute16_pairs)
+void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
                         uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
                         uint32_t *slot_rep, hipStream_t st);
 void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st);
@@ -274,7 +275,7 @@ struct MbrArgs {
     bool full = false;            // complete dominance test (rows may repeat a vector)
     int row_min = 24;
     int nsplit = 1;               // x-tile ranges per y tile (work items of the pair pass)
-    int dbg = 0;                  // SKY_MBR_DBG (measurement only): 1 skip the pair tests, 2 also the lane tests             // y lanes in reach of an x tile from which its rows are scanned
+    int dbg = 0;                  // SKY_MBR_DBG (measurement only): 1 skip the pair tests, 2 also the lane tests
     uint32_t *mm = nullptr;       // [2D]: {0xffffffff} x D, {0} x D on entry
     uint64_t *code = nullptr, *code_alt = nullptr;   // [mr]
     uint32_t *idx = nullptr, *idx_alt = nullptr;     // [mr]
@@ -284,12 +285,15 @@ struct MbrArgs {
     uint32_t *tmin = nullptr, *tmax = nullptr;       // [NW][ntiles]
     uint32_t *tprange = nullptr;  // [ntiles]
     uint32_t *tsub = nullptr;     // [ntiles][4][NW]: min corners of the 16-row sub-boxes
+    uint32_t *gmin = nullptr;     // [NW][ngroups]: min corners of the groups of 64 tiles
+    uint32_t *gprange = nullptr;  // [ngroups]: their partition ranges
     uint32_t *domf = nullptr;     // [mr], zeroed by the caller
     unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
 };
 int mbr_row_words(int D, int fmt);
 size_t mbr_tiles(uint32_t mr);
+size_t mbr_groups(uint32_t mr);
 hipError_t launch_mbr(const MbrArgs &a, hipStream_t st);
 
 // ---- k_part.hip (per-key operator state, incremental) ----

@@ -388,3 +388,21 @@ def test_warmup_then_queries(gpu_engine_factory, oracle):
         np.testing.assert_array_equal(ls, els)
         np.testing.assert_array_equal(sv, esv)
     eng.close()
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 5, 8, 9, 12, 16])
+def test_packed_u16_brute_pass(D, gpu_engine_factory, oracle, monkeypatch):
+    """Small candidate sets of integer rows go through k_brute16_pairs (packed u16 words,
+    sum tie-break); it must agree with the oracle and with the f32 brute pass, at the ends
+    of the u16 range, with heavy duplication and padding words (odd D, D > 8)."""
+    rng = np.random.default_rng(700 + D)
+    n = 12000
+    a = rng.integers(0, 65536, size=(n, D))
+    a[: n // 4] = rng.choice(np.array([0, 1, 65534, 65535]), size=(n // 4, D))
+    a[n // 4: n // 2] = a[rng.integers(0, n // 4, size=n // 4)]          # duplicates
+    vals = rng.permutation(a).astype(np.float64)
+    for algo, P in (("mr-angle", 8), ("mr-dim", 4)):
+        for flag in ("0", "1"):
+            monkeypatch.setenv("SKY_BRUTE16", flag)
+            check_vs_oracle(gpu_engine_factory, oracle, vals, P, algo)
+    monkeypatch.setenv("SKY_BRUTE16", "1")
