@@ -87,6 +87,8 @@ struct Pipe {
     DevBuf *s_rows = &rows, *s_key = &sortkey, *s_src = &slot_src;
     // single-pass output: look-back words per tile; what the last run wrote
     DevBuf lbuf;
+    DevBuf tile_hist, tile_cand;      // per-tile duplicate histograms / surviving candidates (output counts)
+    bool hist_count = false;
     bool fused = false;
     const int64_t *fused_ids = nullptr;
     const int32_t *fused_org = nullptr;

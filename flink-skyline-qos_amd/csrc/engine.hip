@@ -168,6 +168,10 @@ static bool fused_onepass() {   // SKY_FUSED_OUT=2: the one-pass look-back outpu
 }
 // SKY_MBR=0 keeps the round-based SFS for large rep sets (A/B knob, read per query);
 // SKY_MBR_MIN: smallest rep count for the bounding-box pruned all-pairs pass
+static bool hist_disabled() {   // SKY_HIST_COUNT=0: the status-word count pass (A/B knob)
+    const char *e = getenv("SKY_HIST_COUNT");
+    return e && e[0] == '0';
+}
 static bool mbr_disabled() {
     const char *e = getenv("SKY_MBR");
     return e && atoi(e) == 0;
@@ -710,6 +714,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
     fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);   // per-slot sample minima start all-ones
+    // output counts from per-tile duplicate histograms (unit weights, stats over slots, the
+    // single-pass output's buffers): the filter keeps them, the fate pass counts candidates
+    p.hist_count = in.fate && !in.origin && !in.weights && (in.out_ids || in.out_org) && !fused_disabled() &&
+                   !fused_onepass() && KM <= kHistMaxKM && !hist_disabled();
+    if (p.hist_count) {
+        SKY_TRY(p.tile_hist.ensure((size_t)tiles * KM * 4));
+        SKY_TRY(p.tile_cand.ensure((size_t)tiles * 4));
+        fill.add(p.tile_cand.p, (size_t)tiles * 4);
+    }
     HIP_TRY(fill.launch(st));
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
                           p.pruners.as<double>(), p.npr.as<int32_t>(), st);
@@ -739,6 +752,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.dup_cnt = p.dup_cnt.as<uint32_t>();
     fa.flags = p.flags.as<uint32_t>();
     fa.slot_cap = (uint32_t)cap;
+    fa.tile_hist = p.hist_count ? p.tile_hist.as<uint32_t>() : nullptr;
     const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;
     if (angle_keys) {
         SKY_TRY(p.defer.ensure((size_t)n * 4));
@@ -1059,6 +1073,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fta.dup_cnt = p.dup_cnt.as<uint32_t>();
     fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
     fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
+    fta.tile_cand = p.hist_count ? p.tile_cand.as<uint32_t>() : nullptr;
     launch_fate_tables(fta, st);
     if (tm) tm->mark(7, st);
     if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
@@ -1108,7 +1123,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         // count pass -> tile scan -> write pass, chained on the device (no host read in
         // between; positions >= out_cap are not written, the final read reports the total)
         c.ktimer_begin("outc", st);
-        launch_out_count(oa, st);
+        if (p.hist_count)
+            launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
+                                  KM, tiles, p.out_cnt.as<uint32_t>(), st);
+        else
+            launch_out_count(oa, st);
         c.ktimer_end("outc", st, n);
         scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
                       p.scratch.as<uint32_t>(), st);

@@ -396,13 +396,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     __shared__ int32_t s_npr[kMaxK];
     __shared__ uint32_t s_list[kTile];
     __shared__ uint32_t s_wc[kThreads / 64], s_wd[kThreads / 64], s_base, s_dbase;
+    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
-    uint32_t lflags = 0, wcnt = 0, dcnt = 0;
-    uint64_t o = 0, an = ~0ull;
-    const uint32_t base = blockIdx.x * kTile;
+    uint32_t lflags = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *wlist = s_list + __builtin_amdgcn_readfirstlane(wave) * kList;
     const uint32_t nl = a.n - 1;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     double vn[D];                                                // the row of item r+1, in flight
     int32_t kn = 0;
 #define SKY_FILTER_FETCH(I)                                                                \
@@ -411,7 +411,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         load_row<D>(a.vals + (size_t)i_ * D, vn);                                          \
         if constexpr (GIVEN) kn = a.given_keys[i_];                                        \
     } while (0)
-    SKY_FILTER_FETCH(base + threadIdx.x);
+    // a.tpb tiles per workgroup, interleaved over the grid (tile = t * grid + block): the
+    // pruner image is loaded once per workgroup, not once per 2048 tuples
+    SKY_FILTER_FETCH(blockIdx.x * kTile + threadIdx.x);
+#pragma unroll 1
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t wcnt = 0, dcnt = 0;
+    uint64_t o = 0, an = ~0ull;
+    const uint32_t base = tile * kTile;
+    const uint32_t next_base = (tile + gridDim.x) * kTile;       // past the end: clamped, a cache hit
     uint16_t st_prev = 0;
 #pragma unroll 1
     for (int r = 0; r < kItems; r++) {
@@ -422,7 +430,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         for (int d = 0; d < D; d++) v[d] = vn[d];
         const int32_t kg = kn;
         if (r > 0 && i - kThreads < a.n) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
-        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : i);           // past the tile: a cache hit
+        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : next_base + threadIdx.x);
         bool nan = false;
 #pragma unroll
         for (int d = 0; d < D; d++) nan |= v[d] != v[d];
@@ -447,7 +455,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         wcnt += (uint32_t)__popcll(cm);
         st_prev = st;
     }
-#undef SKY_FILTER_FETCH
     {
         const uint32_t il = base + (kItems - 1) * kThreads + threadIdx.x;
         if (il < a.n) a.status[il] = st_prev;
@@ -465,6 +472,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         doff[q + 1] = doff[q] + s_wd[q];
     }
     const uint32_t total = woff[kThreads / 64], dtotal = doff[kThreads / 64];
+    // the tile's duplicate counts: into the per-tile histogram (the output count reads it
+    // instead of the status words) and the per-(partition, pruner) totals
+    for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads) {
+        const uint32_t c = s_dup[q];
+        if (a.tile_hist) a.tile_hist[(size_t)tile * (a.Kp * a.M) + q] = c;
+        if (c) { atomicAdd(&a.dup_cnt[q], c); s_dup[q] = 0; }
+    }
     if (threadIdx.x == 0) s_base = total ? atomicAdd(a.m_total, total) : 0u;
     if (threadIdx.x == 64 && dtotal) s_dbase = atomicAdd(a.defer_cnt, dtotal);
     __syncthreads();
@@ -499,17 +513,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         o |= __shfl_xor(o, sh, 64);
         an &= __shfl_xor(an, sh, 64);
     }
-    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
     if (lane == 0) { s_o[wave] = o; s_a[wave] = an; }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long bo = 0, ba = ~0ull;
         for (int q = 0; q < kThreads / 64; q++) { bo |= s_o[q]; ba &= s_a[q]; }
-        a.tile_orand[2 * blockIdx.x] = bo;
-        a.tile_orand[2 * blockIdx.x + 1] = ba;
+        a.tile_orand[2 * tile] = bo;
+        a.tile_orand[2 * tile + 1] = ba;
     }
-    for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads)
-        if (s_dup[q]) atomicAdd(&a.dup_cnt[q], s_dup[q]);
+    __syncthreads();                           // s_list / s_wc / s_o reused by the next tile
+    }
+#undef SKY_FILTER_FETCH
     if (lflags) atomicOr(a.flags, lflags);
 }
 
@@ -544,6 +558,8 @@ __global__ __launch_bounds__(kThreads) void k_filter_deferred(FilterArgs a) {
             for (int d = 0; d < D; d++) v[d] = 0.0;
         }
         count_dups(code, k, a.M, s_dup);
+        if (a.tile_hist && valid && code != kCodeCandidate && code != kCodeDropped)
+            atomicAdd(&a.tile_hist[(size_t)(i / kTile) * (a.Kp * a.M) + (uint32_t)k * a.M + code - 1], 1u);
         append_candidate<D>(a, cand, v, k, i, lflags, o, an);
     }
 #pragma unroll
@@ -975,6 +991,7 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
             f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
             const uint16_t s0 = a.status[src];
             a.status[src] = (uint16_t)((s0 & 0xff00u) | (kCodeFate0 + f));
+            if (a.tile_cand && (f & 2u)) atomicAdd(&a.tile_cand[src / kTile], 1u);
             k = s0 >> 8;
             w = 1;
         }
@@ -1011,6 +1028,28 @@ __device__ __forceinline__ uint32_t tuple_fate(uint16_t st, const uint8_t *s_pf,
     const uint32_t pf = s_pf[dup ? (uint32_t)(st >> 8) * (uint32_t)M + code - 1u : 0u];
     const uint32_t cf = code >= kCodeFate0 && code != kCodeCandidate ? code - kCodeFate0 : 0u;
     return dup ? pf : cf;
+}
+
+// Count from the filter's per-tile duplicate histograms (unit weights, stats summed over
+// slots, global level selected): a tile's selected tuples = its duplicates of surviving
+// pruner groups + its surviving candidates (counted by k_fate_tables).  One wave per tile
+// reads KM words instead of the tile's 2048 status words.
+__global__ __launch_bounds__(kThreads) void k_out_hist_count(const uint32_t *__restrict__ hist,
+                                                             const uint32_t *__restrict__ tile_cand,
+                                                             const uint8_t *__restrict__ pruner_fate, int KM,
+                                                             uint32_t ntiles, uint32_t *__restrict__ out_cnt) {
+    __shared__ uint8_t s_pf[kHistMaxKM];
+    for (int q = threadIdx.x; q < KM; q += kThreads) s_pf[q] = pruner_fate[q];
+    __syncthreads();
+    const uint32_t tile = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t *h = hist + (size_t)tile * KM;
+    uint32_t c = 0;
+    for (int q = lane; q < KM; q += 64) c += (s_pf[q] & 2u) ? h[q] : 0u;
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) c += __shfl_xor(c, sh, 64);
+    if (lane == 0) out_cnt[tile] = c + tile_cand[tile];
 }
 
 // Count pass: kOutTPB tiles per workgroup, every tile's status words loaded up front
@@ -1369,7 +1408,13 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
-    const unsigned g = nblk(a.n, kTile);
+    static const unsigned tpb = [] {           // tiles per workgroup (SKY_FILTER_TPB, A/B knob)
+        const char *e = getenv("SKY_FILTER_TPB");   // 4: -4 % filter time vs 1 (2: -3 %, 8: -3 %)
+        const int v = e ? atoi(e) : 4;
+        return (unsigned)std::max(1, std::min(v, 64));
+    }();
+    const unsigned tiles = nblk(a.n, kTile);
+    const unsigned g = (tiles + tpb - 1) / tpb;
     if (!g) return;
     if (a.given_keys) { SKY_DISPATCH_D(D, (k_filter<DD, true><<<g, kThreads, lds, st>>>(a))); }
     else { SKY_DISPATCH_D(D, (k_filter<DD, false><<<g, kThreads, lds, st>>>(a))); }
@@ -1461,6 +1506,12 @@ void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket
                       int64_t cap, hipStream_t st) {
     const uint32_t tiles = (a.n + kTile - 1) / kTile;
     if (tiles) k_out_fused<<<tiles, kThreads, 0, st>>>(a, lb, ticket, d_total, err, cap);
+}
+
+void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,
+                           uint32_t ntiles, uint32_t *out_cnt, hipStream_t st) {
+    if (ntiles) k_out_hist_count<<<nblk(ntiles, kThreads / 64), kThreads, 0, st>>>(hist, tile_cand, pruner_fate, KM,
+                                                                                  ntiles, out_cnt);
 }
 
 void launch_out_write(const OutArgs &a, hipStream_t st) {

@@ -95,6 +95,42 @@ __global__ __launch_bounds__(1024) void k_scan_small(uint32_t *__restrict__ a, s
     if (threadIdx.x == 0 && total_out) *total_out = s_carry;
 }
 
+// one workgroup, n <= kScanOneMax: thread t owns the contiguous items [t*per, t*per + per),
+// all loaded up front (one memory round trip), one block scan, written back
+constexpr int kScanOneThreads = 1024;
+constexpr int kScanOnePer = 64;
+constexpr size_t kScanOneMax = (size_t)kScanOneThreads * kScanOnePer;
+__global__ __launch_bounds__(kScanOneThreads) void k_scan_one(const uint32_t *__restrict__ in, uint32_t n,
+                                                              uint32_t *__restrict__ out,
+                                                              uint32_t *__restrict__ total_out) {
+    __shared__ uint32_t s_w[kScanOneThreads / 64];
+    const uint32_t per = (n + kScanOneThreads - 1) / kScanOneThreads;
+    const uint32_t b = threadIdx.x * per;
+    uint32_t v[kScanOnePer];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanOnePer; j++) {
+        v[j] = (uint32_t)j < per && b + j < n ? in[b + j] : 0u;
+        s += v[j];
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(s);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - s, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kScanOneThreads / 64; k++) {
+        run += k < w ? s_w[k] : 0u;
+        tot += s_w[k];
+    }
+#pragma unroll
+    for (int j = 0; j < kScanOnePer; j++) {
+        if ((uint32_t)j < per && b + j < n) out[b + j] = run;
+        run += v[j];
+    }
+    if (threadIdx.x == 0 && total_out) *total_out = tot;
+}
+
 // out[i] = sum(in[0..i)), *d_total = sum(in) ; `scratch` needs scan_scratch_words(n) words
 size_t scan_scratch_words(size_t n) {
     size_t tiles = (n + kScanTile - 1) / kScanTile;
@@ -110,6 +146,10 @@ void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_tota
     const size_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
         k_scan_tile<<<1, kScanThreads, 0, st>>>(in, n, out, nullptr, d_total);
+        return;
+    }
+    if (n <= kScanOneMax) {                    // one launch instead of reduce / partials / tiles
+        k_scan_one<<<1, kScanOneThreads, 0, st>>>(in, (uint32_t)n, out, d_total);
         return;
     }
     uint32_t *partial = scratch;

@@ -74,6 +74,7 @@ struct FilterArgs {
     uint32_t *defer_list;         // [n] MR-Angle tuples whose key needs the exact path
     uint32_t *defer_cnt;
     uint32_t slot_cap;            // slots allocated: appends past it are counted, not written
+    uint32_t *tile_hist;          // [tiles][Kp*M] duplicates per tile (nullptr: not kept; Kp*M <= kHistMaxKM)
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
@@ -110,6 +111,7 @@ struct FateArgs {
     uint8_t *pruner_fate;
     const uint32_t *dup_cnt;              // stats only
     unsigned long long *lsz, *surv;       // [kStatShards][K] stat shards, or nullptr: no stats
+    uint32_t *tile_cand;                  // [tiles] zeroed: += candidates in G per tile (nullptr: not counted)
 };
 void launch_fate_tables(const FateArgs &a, hipStream_t st);
 
@@ -173,6 +175,11 @@ struct OutArgs {
     int select_local;             // output tuples in L instead of G
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);
+// per-tile counts of the global level from the filter's duplicate histograms + k_fate_tables'
+// candidate counts (replaces the count pass for unit weights / slot stats)
+constexpr int kHistMaxKM = 256;
+void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,
+                           uint32_t ntiles, uint32_t *out_cnt, hipStream_t st);
 void launch_out_write(const OutArgs &a, hipStream_t st);
 // count + prefix + write in one pass (decoupled look-back over tiles): lb [tiles] u64 and
 // *ticket zeroed by the caller; *d_total = selected tuples; writes positions < cap only
