@@ -89,6 +89,19 @@ struct Pipe {
     DevBuf lbuf;
     DevBuf tile_hist, tile_cand;      // per-tile duplicate histograms / surviving candidates (output counts)
     bool hist_count = false;
+    // the small-set route of the last query (prefilter rounds + brute pair pass), replayed by
+    // the next with device-sized launches (bounds from this query's counts)
+    struct Plan {
+        static constexpr int kMaxRounds = 3;
+        bool valid = false;
+        int rounds = 0;
+        uint32_t bound[kMaxRounds + 1] = {};   // slots entering round r; bound[rounds]: the brute pass
+        bool f64 = false, ints = false;
+        int D = 0, Kp = 0, M = 0;
+        bool single = false, global = false;
+    } plan;
+    int64_t plan_runs = 0, plan_misses = 0;
+    bool last_planned = false, last_plan_miss = false;   // the last query's route (counters[7] bits 3, 4)
     bool fused = false;
     const int64_t *fused_ids = nullptr;
     const int32_t *fused_org = nullptr;

@@ -166,12 +166,19 @@ static bool fused_onepass() {   // SKY_FUSED_OUT=2: the one-pass look-back outpu
     const char *e = getenv("SKY_FUSED_OUT");
     return e && atoi(e) == 2;
 }
-// SKY_MBR=0 keeps the round-based SFS for large rep sets (A/B knob, read per query);
-// SKY_MBR_MIN: smallest rep count for the bounding-box pruned all-pairs pass
 static bool hist_disabled() {   // SKY_HIST_COUNT=0: the status-word count pass (A/B knob)
     const char *e = getenv("SKY_HIST_COUNT");
     return e && e[0] == '0';
 }
+// SKY_PLAN=0: every query takes the host-synchronised route (A/B knob, read per query)
+static bool plan_disabled() {
+    const char *e = getenv("SKY_PLAN");
+    return e && e[0] == '0';
+}
+// a device-sized launch's bound for a count the last query saw
+static uint32_t plan_bound(uint32_t x) { return x + x / 4 + 1024u; }
+// SKY_MBR=0 keeps the round-based SFS for large rep sets (A/B knob, read per query);
+// SKY_MBR_MIN: smallest rep count for the bounding-box pruned all-pairs pass
 static bool mbr_disabled() {
     const char *e = getenv("SKY_MBR");
     return e && atoi(e) == 0;
@@ -652,12 +659,322 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     return SKY_OK;
 }
 
+// The fate tables, the per-tuple fate / output pass and the final read of a run.  mt: the
+// slots; on the planned route (pr) their bound, the count itself on the device (pr->d_cnt),
+// and the final read verifies the route's assumptions (kPlanMiss: run it again, synchronised).
+constexpr int kPlanMiss = -1000;
+struct PlanRun {
+    size_t cap = 0, cap_full = 0;     // slots allocated / needed at most
+    const uint32_t *d_cnt = nullptr;  // slots entering the brute pass (device)
+    bool k_u16 = false, k_f32 = false;   // the brute pass's compare type
+};
+static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSet &fill, bool brute, uint32_t mt,
+                       uint32_t tiles, const PlanRun *pr) {
+    hipStream_t st = c.st;
+    const uint32_t n = in.n;
+    const int KM = p.Kp * p.M;
+    // stats: summed over slots (unit weights, computed origins) or, for given origins /
+    // weights, over tuples in the count pass
+    const bool slot_stats = in.fate && !in.origin && !in.weights;
+    FateArgs fta{};
+    fta.mt = mt;
+    fta.d_mt = pr ? pr->d_cnt : nullptr;
+    fta.slot_rep = p.slot_rep.as<uint32_t>();
+    fta.slot_src = p.s_src->as<uint32_t>();
+    fta.alive_l = p.alive_l.as<uint8_t>();
+    fta.alive_g = p.alive_g.as<uint8_t>();
+    fta.KM = KM;
+    fta.M = p.M;
+    fta.K = p.K;
+    fta.pruner_slot = p.pruner_slot.as<int32_t>();
+    fta.status = p.status.as<uint16_t>();
+    fta.pruner_fate = p.pruner_fate.as<uint8_t>();
+    fta.dup_cnt = p.dup_cnt.as<uint32_t>();
+    fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
+    fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
+    fta.tile_cand = p.hist_count ? p.tile_cand.as<uint32_t>() : nullptr;
+    launch_fate_tables(fta, st);
+    if (tm) tm->mark(7, st);
+    if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
+        p.nout = 0;
+        if (tm) tm->mark(8, st);
+        return SKY_OK;
+    }
+
+    // ---- per-tuple fate: stats + output counts
+    SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
+    SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
+    // the tile scan below needs its scratch even when no tuple was a candidate (mt == 0:
+    // every tuple in an unqueried MR-Grid cell or removed by the grid filter)
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
+    OutArgs oa{};
+    oa.status = p.status.as<uint16_t>();
+    oa.n = n;
+    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
+    oa.M = p.M;
+    oa.KM = p.Kp * p.M;
+    oa.given_origin = in.origin;
+    oa.given_w = in.weights;
+    oa.K = p.K;
+    oa.lsz = slot_stats ? nullptr : p.lsz.as<unsigned long long>();
+    oa.surv = slot_stats ? nullptr : p.surv.as<unsigned long long>();
+    oa.out_cnt = p.out_cnt.as<uint32_t>();
+    oa.select_local = 0;
+    p.fused = slot_stats && (in.out_ids || in.out_org) && !fused_disabled();
+    p.fused_ids = in.out_ids;
+    p.fused_org = in.out_org;
+    c.ktimer_begin("out", st);
+    if (p.fused && fused_onepass()) {
+        // count + prefix + write in one pass (decoupled look-back; A/B knob SKY_FUSED_OUT=2)
+        SKY_TRY(p.lbuf.ensure((size_t)tiles * 8 + 64));
+        fill.add(p.lbuf.p, (size_t)tiles * 8);
+        fill.add(p.totals.as<uint32_t>() + 9, 4);          // ticket
+        HIP_TRY(fill.launch(st));
+        oa.ids = in.ids;
+        oa.ids_out = in.out_ids;
+        oa.origin_out = in.out_org;
+        oa.given_origin = nullptr;
+        c.ktimer_begin("outw", st);
+        launch_out_fused(oa, p.lbuf.as<unsigned long long>(), p.totals.as<uint32_t>() + 9,
+                         p.totals.as<uint32_t>() + 3, p.flags.as<uint32_t>(), in.out_cap, st);
+        c.ktimer_end("outw", st, n);
+    } else if (p.fused) {
+        // count pass -> tile scan -> write pass, chained on the device (no host read in
+        // between; positions >= out_cap are not written, the final read reports the total)
+        c.ktimer_begin("outc", st);
+        if (p.hist_count)
+            launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
+                                  KM, tiles, p.out_cnt.as<uint32_t>(), st);
+        else
+            launch_out_count(oa, st);
+        c.ktimer_end("outc", st, n);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), st);
+        OutArgs ow = oa;
+        ow.out_off = p.out_off.as<uint32_t>();
+        ow.ids = in.ids;
+        ow.ids_out = in.out_ids;
+        ow.origin_out = in.out_org;
+        ow.out_cap = in.out_cap;
+        c.ktimer_begin("outw", st);
+        launch_out_write(ow, st);
+        c.ktimer_end("outw", st, n);
+    } else {
+        c.ktimer_begin("outc", st);
+        launch_out_count(oa, st);
+        c.ktimer_end("outc", st, n);
+        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                      p.scratch.as<uint32_t>(), st);
+    }
+    c.ktimer_end("out", st, n);
+    STAGE(st, "fate");
+    uint32_t nout = 0;
+    SKY_TRY(p.statk.ensure((size_t)p.K * 16));
+    launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
+                       p.statk.as<unsigned long long>(), st);
+    std::vector<unsigned long long> sk2((size_t)p.K * 2);
+    const bool have_seg = mt && (brute || !p.h_seg_n.empty());
+    p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
+    if (brute) {
+        uint32_t flags2 = 0, tot[16] = {};
+        p.h_seg_n.assign(p.Kp, 0u);
+        SKY_TRY(sync_read(p, st, {{p.totals.p, 64}, {p.statk.p, (size_t)p.K * 16},
+                                  {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
+                                  {p.flags.p, 4}},
+                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2}));
+        nout = tot[3];
+        if (flags2 & kFlagRadixSpin) {
+            set_error("a look-back (output) exceeded its spin bound");
+            return SKY_E_HIP;
+        }
+        if (pr) {
+            // the planned route's assumptions: no NaN, no slot overflow, every count within
+            // the bound its launches were sized for, the small-set size, the compare type
+            if (flags2 & kFlagNaN) {
+                set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; rejected");
+                return SKY_E_NAN;
+            }
+            const uint32_t m = tot[0], nps = tot[5];
+            if ((size_t)m + nps > pr->cap) {
+                p.slot_hint = std::min(pr->cap_full, ((size_t)m + nps) * 5 / 4 + (size_t)KM);
+                p.slot_reruns++;
+                return kPlanMiss;
+            }
+            bool ok = tot[10] <= p.plan.bound[0];
+            for (int r = 0; r < p.plan.rounds; r++) ok &= tot[11 + r] <= p.plan.bound[r + 1];
+            const uint32_t fin = p.plan.rounds ? tot[10 + p.plan.rounds] : tot[10];
+            ok &= fin <= kBruteMax;
+            const bool f64 = (flags2 & kFlagNotF32) != 0, ints = !f64 && (flags2 & kFlagNotU16) == 0;
+            ok &= pr->k_u16 ? ints : (pr->k_f32 ? !f64 : true);
+            if (!ok) return kPlanMiss;
+            p.m = m;
+            p.nps = nps;
+            p.mt_pre = tot[10];
+            p.mt = fin;
+            p.f64 = f64;
+            p.ints = ints;
+            p.ties = (flags2 & kFlagScoreTies) != 0;
+            p.u16 = p.ints && !p.ties && !sfs16_disabled();
+            mt = fin;
+        }
+        p.mr = mt;                            // brute mode: slots (duplicates not collapsed)
+        uint32_t alive_sum = 0;
+        for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
+        p.mg = in.global && !in.single ? alive_sum : 0;
+    } else {
+        uint32_t flags3 = 0;
+        unsigned long long mbr_pairs[2] = {0, 0};
+        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
+                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
+                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs}));
+        if (p.used_mbr) {
+            p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
+            p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
+            uint32_t alive_sum = 0;
+            for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
+            p.mg = in.global && !in.single ? alive_sum : 0;
+        }
+        if (flags3 & kFlagRadixSpin) {
+            set_error("a look-back (radix sort / output) exceeded its spin bound");
+            return SKY_E_HIP;
+        }
+    }
+    p.dom_w = 0;
+    if (have_seg) {
+        int64_t sg = 0;
+        for (int k = 0; k < p.Kp; k++) {
+            const int64_t nk = p.h_seg_n[k], sk = p.h_seg_s[k];
+            p.dom_w += sk * (sk - 1) / 2 + (nk - sk);
+            sg += sk;
+        }
+        if (in.global && !in.single) p.dom_w += sg * (sg - 1) / 2;
+    }
+    for (int k = 0; k < p.K; k++) {
+        p.h_lsz[k] = sk2[k];
+        p.h_surv[k] = sk2[(size_t)p.K + k];
+    }
+    p.nout = nout;
+    if (debug_level() >= 3) {
+        fprintf(stderr, "[sky] run n=%u m=%u nps=%u mr=%u mg=%u nout=%u u16=%d seg_n:", n, p.m, p.nps, p.mr, p.mg,
+                nout, (int)p.u16);
+        for (uint32_t x : p.h_seg_n) fprintf(stderr, " %u", x);
+        fprintf(stderr, " seg_s:");
+        for (uint32_t x : p.h_seg_s) fprintf(stderr, " %u", x);
+        fprintf(stderr, "\n");
+    }
+    if (tm) tm->mark(8, st);
+    return SKY_OK;
+}
+
+
+// The planned route (see pipe_run): the prefilter rounds and the brute pass of the last
+// query's small-set route, every launch sized by the plan's bounds and reading its count
+// from the device; no host synchronisation before pipe_finish's final read.
+static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size_t cap, size_t cap_full,
+                            uint32_t tiles, FillSet &fill) {
+    hipStream_t st = c.st;
+    const int D = c.D;
+    const Pipe::Plan pl = p.plan;
+    const int KM = p.Kp * p.M;
+    const size_t rb64 = row_bytes(true, D);
+    p.plan_runs++;
+    if (tm) tm->mark(3, st);
+    p.f64 = pl.f64;
+    p.ints = pl.ints;
+    p.s_rows = &p.rows;
+    p.s_key = &p.sortkey;
+    p.s_src = &p.slot_src;
+    const uint32_t *d_cnt = p.totals.as<uint32_t>() + 10;   // min(m + nps, cap), by k_append_pruners
+    uint32_t bound = pl.bound[0];
+    for (int round = 0; round < pl.rounds; round++) {
+        const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
+        const int KM2 = p.Kp * M2;
+        DevBuf *dr = round & 1 ? &p.rows3 : &p.rows2, *dk = round & 1 ? &p.sortkey3 : &p.sortkey2,
+               *ds = round & 1 ? &p.slot_src3 : &p.slot_src2;
+        SKY_TRY(p.cmin.ensure((size_t)KM2 * 8));
+        SKY_TRY(p.pr2.ensure((size_t)KM2 * D * 8));
+        SKY_TRY(p.npr2.ensure((size_t)p.Kp * 4));
+        SKY_TRY(p.live.ensure((size_t)bound * 4));
+        SKY_TRY(p.livepos.ensure((size_t)(bound + 1) * 4));
+        SKY_TRY(dr->ensure((size_t)bound * rb64));
+        SKY_TRY(dk->ensure((size_t)bound * 8));
+        SKY_TRY(ds->ensure((size_t)bound * 4));
+        SKY_TRY(p.scratch.ensure(scan_scratch_words(bound + 1) * 4 + 64));
+        fill.add(p.cmin.p, (size_t)KM2 * 8, 0xff);
+        HIP_TRY(fill.launch(st));
+        CandArgs ca{};
+        ca.mt = bound;
+        ca.d_mt = d_cnt;
+        ca.rows = p.s_rows->as<double>();
+        ca.key = p.s_key->as<uint64_t>();
+        ca.src = p.s_src->as<uint32_t>();
+        ca.Kp = p.Kp;
+        ca.M2 = M2;
+        ca.cmin = p.cmin.as<unsigned long long>();
+        ca.pr2 = p.pr2.as<double>();
+        ca.npr2 = p.npr2.as<int32_t>();
+        ca.live = p.live.as<uint32_t>();
+        uint32_t *d_live = p.totals.as<uint32_t>() + 11 + round;
+        c.ktimer_begin("prefilter", st);
+        launch_cand_prefilter(D, ca, st);
+        scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), bound, d_live, p.scratch.as<uint32_t>(), st, d_cnt);
+        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(), ds->as<uint32_t>(),
+                            p.pruner_slot.as<int32_t>(), KM, st);
+        c.ktimer_end("prefilter", st, bound);
+        STAGE(st, "prefilter");
+        p.s_rows = dr;
+        p.s_key = dk;
+        p.s_src = ds;
+        // the next stage reads at most min(count, its bound) <= this bound compacted slots
+        d_cnt = d_live;
+        bound = std::min(pl.bound[round + 1], bound);
+    }
+    if (tm) tm->mark(4, st);
+    if (tm) tm->mark(5, st);
+    SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+    SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
+    SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
+    SKY_TRY(p.slot_rep.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
+    SKY_TRY(p.alive_l.ensure(std::max<uint32_t>(bound, 1)));
+    SKY_TRY(p.alive_g.ensure(std::max<uint32_t>(bound, 1)));
+    SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
+    fill.add(p.segalive.p, (size_t)p.Kp * 4);
+    fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
+    fill.add(p.keep.p, (size_t)std::max<uint32_t>(bound, 1) * 4);
+    HIP_TRY(fill.launch(st));
+    PlanRun pr;
+    pr.cap = cap;
+    pr.cap_full = cap_full;
+    pr.d_cnt = d_cnt;
+    pr.k_u16 = p.ints && !brute16_disabled();
+    pr.k_f32 = !p.f64;
+    c.ktimer_begin("brute", st);
+    launch_brute_fates(D, pr.k_f32, pr.k_u16, p.s_rows->p, p.s_key->as<uint64_t>(), bound, in.global && !in.single,
+                       p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
+                       p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st, d_cnt);
+    c.ktimer_end("brute", st, (int64_t)bound * bound);
+    STAGE(st, "brute");
+    if (tm) tm->mark(6, st);
+    const int r = pipe_finish(c, p, in, tm, fill, true, bound, tiles, &pr);
+    if (r != kPlanMiss) {
+        p.last_planned = r == SKY_OK;
+        return r;
+    }
+    p.plan.valid = false;                      // re-run on the synchronised route (learns a new plan)
+    p.plan_misses++;
+    const int r2 = pipe_run(c, p, in, tm);
+    p.last_plan_miss = true;
+    return r2;
+}
+
 int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     hipStream_t st = c.st;
     const int D = c.D;
     const uint32_t n = in.n;
     p.n = n;
     p.K = in.K;
+    p.last_planned = p.last_plan_miss = false;
     p.Kp = in.single ? 1 : c.Kq();
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
@@ -718,6 +1035,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // single-pass output's buffers): the filter keeps them, the fate pass counts candidates
     p.hist_count = in.fate && !in.origin && !in.weights && (in.out_ids || in.out_org) && !fused_disabled() &&
                    !fused_onepass() && KM <= kHistMaxKM && !hist_disabled();
+    // the planned route: the last query's small-set route (prefilter rounds, then the brute
+    // pair pass) replayed with device-sized launches and no host synchronisation until the
+    // final read, which verifies every assumption (counts within the bounds, the row type);
+    // a miss re-runs the query on the synchronised route.  Results are identical either way
+    // (the prefilter is exact, so its round count does not change the skyline).
+    const bool planned = p.plan.valid && !plan_disabled() && c.warm_mode == 0 && in.fate && !brute_disabled() &&
+                         p.plan.D == D && p.plan.Kp == p.Kp && p.plan.M == p.M && p.plan.single == in.single &&
+                         p.plan.global == in.global && (p.plan.rounds == 0 || !prefilter_disabled()) &&
+                         cap >= p.plan.bound[0];
     if (p.hist_count) {
         SKY_TRY(p.tile_hist.ensure((size_t)tiles * KM * 4));
         SKY_TRY(p.tile_cand.ensure((size_t)tiles * 4));
@@ -783,8 +1109,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     aa.flags = p.flags.as<uint32_t>();
     aa.orand = p.orand.as<unsigned long long>();
     aa.slot_cap = (uint32_t)cap;
+    aa.mt_total = p.totals.as<uint32_t>() + 10;
     launch_append_pruners(D, aa, st);
     STAGE(st, "compact");
+    if (planned) return pipe_run_planned(c, p, in, tm, cap, cap_full, tiles, fill);
     uint32_t m = 0, nps = 0, flags = 0;
     unsigned long long orand[2] = {0ull, 0ull};
     SKY_TRY(sync_read(p, st, {{p.totals.p, 4}, {p.totals.as<uint32_t>() + 5, 4}, {p.flags.p, 4}, {p.orand.p, 16}},
@@ -816,6 +1144,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     //      outnumber what one small-SFS workgroup per partition handles)
     // rounds: a round's survivors draw new pruners; another round runs only while the
     // survivors are still too many for the brute path and the last round cut them by > 30 %
+    int plan_rounds = 0;
+    uint32_t plan_live[kPrefilterRounds] = {};
     for (int round = 0; round < kPrefilterRounds && p.mt >= kPrefilterMin && !prefilter_disabled(); round++) {
         const uint32_t mt0 = p.mt;
         const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
@@ -859,6 +1189,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.s_key = dk;
         p.s_src = ds;
         p.mt = live_n;
+        plan_live[plan_rounds++] = live_n;
         if (debug_level() >= 3)
             fprintf(stderr, "[sky] prefilter round %d: %u -> %u slots (M2=%d)\n", round, mt0, live_n, M2);
         if (live_n <= kBruteMax || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
@@ -867,6 +1198,20 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // small candidate sets (typical after the prefilter): both skyline levels by one
     // brute-force launch instead of the round-based SFS (SKY_BRUTE=0: A/B knob)
     const bool brute = in.fate && mt > 0 && mt <= kBruteMax && !brute_disabled() && c.warm_mode == 0;
+    // the route for the next queries' planned replay: this one's, if it was the small-set one
+    p.plan.valid = brute && plan_rounds <= Pipe::Plan::kMaxRounds;
+    if (p.plan.valid) {
+        p.plan.rounds = plan_rounds;
+        p.plan.bound[0] = plan_bound(p.mt_pre);
+        for (int r = 0; r < plan_rounds; r++) p.plan.bound[r + 1] = plan_bound(plan_live[r]);
+        p.plan.f64 = p.f64;
+        p.plan.ints = p.ints;
+        p.plan.D = D;
+        p.plan.Kp = p.Kp;
+        p.plan.M = p.M;
+        p.plan.single = in.single;
+        p.plan.global = in.global;
+    }
     const size_t rb = row_bytes(p.f64, D);
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<size_t>(mt, 1)));
@@ -1055,166 +1400,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         STAGE(st, "brute");
         if (tm) tm->mark(6, st);
     }
-    // stats: summed over slots (unit weights, computed origins) or, for given origins /
-    // weights, over tuples in the count pass
-    const bool slot_stats = in.fate && !in.origin && !in.weights;
-    FateArgs fta{};
-    fta.mt = mt;
-    fta.slot_rep = p.slot_rep.as<uint32_t>();
-    fta.slot_src = p.s_src->as<uint32_t>();
-    fta.alive_l = p.alive_l.as<uint8_t>();
-    fta.alive_g = p.alive_g.as<uint8_t>();
-    fta.KM = KM;
-    fta.M = p.M;
-    fta.K = p.K;
-    fta.pruner_slot = p.pruner_slot.as<int32_t>();
-    fta.status = p.status.as<uint16_t>();
-    fta.pruner_fate = p.pruner_fate.as<uint8_t>();
-    fta.dup_cnt = p.dup_cnt.as<uint32_t>();
-    fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
-    fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
-    fta.tile_cand = p.hist_count ? p.tile_cand.as<uint32_t>() : nullptr;
-    launch_fate_tables(fta, st);
-    if (tm) tm->mark(7, st);
-    if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
-        p.nout = 0;
-        if (tm) tm->mark(8, st);
-        return SKY_OK;
-    }
-
-    // ---- per-tuple fate: stats + output counts
-    SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
-    SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
-    // the tile scan below needs its scratch even when no tuple was a candidate (mt == 0:
-    // every tuple in an unqueried MR-Grid cell or removed by the grid filter)
-    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
-    OutArgs oa{};
-    oa.status = p.status.as<uint16_t>();
-    oa.n = n;
-    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
-    oa.M = p.M;
-    oa.KM = p.Kp * p.M;
-    oa.given_origin = in.origin;
-    oa.given_w = in.weights;
-    oa.K = p.K;
-    oa.lsz = slot_stats ? nullptr : p.lsz.as<unsigned long long>();
-    oa.surv = slot_stats ? nullptr : p.surv.as<unsigned long long>();
-    oa.out_cnt = p.out_cnt.as<uint32_t>();
-    oa.select_local = 0;
-    p.fused = slot_stats && (in.out_ids || in.out_org) && !fused_disabled();
-    p.fused_ids = in.out_ids;
-    p.fused_org = in.out_org;
-    c.ktimer_begin("out", st);
-    if (p.fused && fused_onepass()) {
-        // count + prefix + write in one pass (decoupled look-back; A/B knob SKY_FUSED_OUT=2)
-        SKY_TRY(p.lbuf.ensure((size_t)tiles * 8 + 64));
-        fill.add(p.lbuf.p, (size_t)tiles * 8);
-        fill.add(p.totals.as<uint32_t>() + 9, 4);          // ticket
-        HIP_TRY(fill.launch(st));
-        oa.ids = in.ids;
-        oa.ids_out = in.out_ids;
-        oa.origin_out = in.out_org;
-        oa.given_origin = nullptr;
-        c.ktimer_begin("outw", st);
-        launch_out_fused(oa, p.lbuf.as<unsigned long long>(), p.totals.as<uint32_t>() + 9,
-                         p.totals.as<uint32_t>() + 3, p.flags.as<uint32_t>(), in.out_cap, st);
-        c.ktimer_end("outw", st, n);
-    } else if (p.fused) {
-        // count pass -> tile scan -> write pass, chained on the device (no host read in
-        // between; positions >= out_cap are not written, the final read reports the total)
-        c.ktimer_begin("outc", st);
-        if (p.hist_count)
-            launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
-                                  KM, tiles, p.out_cnt.as<uint32_t>(), st);
-        else
-            launch_out_count(oa, st);
-        c.ktimer_end("outc", st, n);
-        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                      p.scratch.as<uint32_t>(), st);
-        OutArgs ow = oa;
-        ow.out_off = p.out_off.as<uint32_t>();
-        ow.ids = in.ids;
-        ow.ids_out = in.out_ids;
-        ow.origin_out = in.out_org;
-        ow.out_cap = in.out_cap;
-        c.ktimer_begin("outw", st);
-        launch_out_write(ow, st);
-        c.ktimer_end("outw", st, n);
-    } else {
-        c.ktimer_begin("outc", st);
-        launch_out_count(oa, st);
-        c.ktimer_end("outc", st, n);
-        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                      p.scratch.as<uint32_t>(), st);
-    }
-    c.ktimer_end("out", st, n);
-    STAGE(st, "fate");
-    uint32_t nout = 0;
-    SKY_TRY(p.statk.ensure((size_t)p.K * 16));
-    launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
-                       p.statk.as<unsigned long long>(), st);
-    std::vector<unsigned long long> sk2((size_t)p.K * 2);
-    const bool have_seg = mt && (brute || !p.h_seg_n.empty());
-    p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
-    if (brute) {
-        uint32_t flags2 = 0;
-        p.h_seg_n.assign(p.Kp, 0u);
-        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                                  {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
-                                  {p.flags.p, 4}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2}));
-        if (flags2 & kFlagRadixSpin) {
-            set_error("a look-back (output) exceeded its spin bound");
-            return SKY_E_HIP;
-        }
-        p.mr = mt;                            // brute mode: slots (duplicates not collapsed)
-        uint32_t alive_sum = 0;
-        for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
-        p.mg = in.global && !in.single ? alive_sum : 0;
-    } else {
-        uint32_t flags3 = 0;
-        unsigned long long mbr_pairs[2] = {0, 0};
-        SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
-                                  {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
-                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs}));
-        if (p.used_mbr) {
-            p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
-            p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
-            uint32_t alive_sum = 0;
-            for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
-            p.mg = in.global && !in.single ? alive_sum : 0;
-        }
-        if (flags3 & kFlagRadixSpin) {
-            set_error("a look-back (radix sort / output) exceeded its spin bound");
-            return SKY_E_HIP;
-        }
-    }
-    p.dom_w = 0;
-    if (have_seg) {
-        int64_t sg = 0;
-        for (int k = 0; k < p.Kp; k++) {
-            const int64_t nk = p.h_seg_n[k], sk = p.h_seg_s[k];
-            p.dom_w += sk * (sk - 1) / 2 + (nk - sk);
-            sg += sk;
-        }
-        if (in.global && !in.single) p.dom_w += sg * (sg - 1) / 2;
-    }
-    for (int k = 0; k < p.K; k++) {
-        p.h_lsz[k] = sk2[k];
-        p.h_surv[k] = sk2[(size_t)p.K + k];
-    }
-    p.nout = nout;
-    if (debug_level() >= 3) {
-        fprintf(stderr, "[sky] run n=%u m=%u nps=%u mr=%u mg=%u nout=%u u16=%d seg_n:", n, p.m, p.nps, p.mr, p.mg,
-                nout, (int)p.u16);
-        for (uint32_t x : p.h_seg_n) fprintf(stderr, " %u", x);
-        fprintf(stderr, " seg_s:");
-        for (uint32_t x : p.h_seg_s) fprintf(stderr, " %u", x);
-        fprintf(stderr, "\n");
-    }
-    if (tm) tm->mark(8, st);
-    return SKY_OK;
+    return pipe_finish(c, p, in, tm, fill, brute, mt, tiles, nullptr);
 }
 
 int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,

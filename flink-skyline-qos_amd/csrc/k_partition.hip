@@ -705,7 +705,10 @@ __global__ __launch_bounds__(kThreads) void k_append_pruners(AppendArgs a) {
         atomicAnd(&a.orand[1], (unsigned long long)an);
     }
     if (lflags) atomicOr(a.flags, lflags);
-    if (threadIdx.x == 0) *a.nps_total = run;
+    if (threadIdx.x == 0) {
+        *a.nps_total = run;
+        if (a.mt_total) *a.mt_total = min(m + run, a.slot_cap);   // slots written (device-sized launches)
+    }
 }
 
 // ---- candidate prefilter: second-level pruners drawn from the candidates ------------
@@ -741,9 +744,10 @@ __device__ __forceinline__ float cand_weight(int j, int d, int D) {
 // (the minima settle after a few rows, so most slots issue none)
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cand_min(const double *__restrict__ rows, const uint64_t *__restrict__ key,
-                                                       uint32_t mt, int Kp, int M2,
-                                                       unsigned long long *__restrict__ gmin) {
+                                                       uint32_t mt, const uint32_t *__restrict__ d_mt, int Kp,
+                                                       int M2, unsigned long long *__restrict__ gmin) {
     constexpr int DP = padded_dims<double>(D);
+    if (d_mt) mt = min(mt, *d_mt);             // device-sized launch: mt is the bound
     __shared__ unsigned long long s_min[2048];
     __shared__ float s_w[64][D];
     const int KM = Kp * M2;
@@ -829,12 +833,14 @@ __global__ __launch_bounds__(64) void k_cand_pick(const double *__restrict__ row
 // live[j] = candidate j is not dominated by a second-level pruner of its partition
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restrict__ rows,
-                                                          const uint64_t *__restrict__ key, uint32_t mt, int M2,
+                                                          const uint64_t *__restrict__ key, uint32_t mt,
+                                                          const uint32_t *__restrict__ d_mt, int M2,
                                                           const double *__restrict__ pr2,
                                                           const int32_t *__restrict__ npr2,
                                                           uint32_t *__restrict__ live) {
     constexpr int DP = padded_dims<double>(D);
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (d_mt) mt = min(mt, *d_mt);
     if (j >= mt) return;
     const int k = (int)(key[j] >> 56);
     double v[D];
@@ -857,7 +863,8 @@ __global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restri
 
 // order-preserving compaction of the live slots (rows, keys, sources); the appended
 // pruner slots' indices are remapped (a dropped one: its duplicate group's fate is 0)
-__global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, int DP, const uint32_t *__restrict__ live,
+__global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, const uint32_t *__restrict__ d_mt, int DP,
+                                                           const uint32_t *__restrict__ live,
                                                            const uint32_t *__restrict__ pos,
                                                            const double *__restrict__ rows,
                                                            const uint64_t *__restrict__ key,
@@ -865,6 +872,7 @@ __global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, int DP, 
                                                            uint64_t *__restrict__ key2, uint32_t *__restrict__ src2,
                                                            int32_t *__restrict__ pruner_slot, int KM) {
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (d_mt) mt = min(mt, *d_mt);
     if (j < mt && live[j]) {
         const uint32_t o = pos[j];
         for (int d = 0; d < DP; d++) rows2[(size_t)o * DP + d] = rows[(size_t)j * DP + d];
@@ -873,7 +881,7 @@ __global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, int DP, 
     }
     if (j < (uint32_t)KM) {
         const int32_t ps = pruner_slot[j];
-        if (ps >= 0) pruner_slot[j] = live[ps] ? (int32_t)pos[ps] : -1;
+        if (ps >= 0) pruner_slot[j] = (uint32_t)ps < mt && live[ps] ? (int32_t)pos[ps] : -1;
     }
 }
 
@@ -981,11 +989,12 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
         __syncthreads();
     }
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t mtd = a.d_mt ? min(a.mt, *a.d_mt) : a.mt;   // device-sized: a.mt is the bound
     int k = -1;
     unsigned long long w = 0;
     uint32_t f = 0;
     if (j < a.mt) {
-        const uint32_t src = a.slot_src[j];
+        const uint32_t src = j < mtd ? a.slot_src[j] : 0x80000000u;
         if (!(src & 0x80000000u)) {                    // (appended pruner slots: below)
             const uint32_t r = a.slot_rep[j];
             f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
@@ -998,7 +1007,7 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
     } else if (j - a.mt < (uint32_t)a.KM) {
         const uint32_t q = j - a.mt;
         const int32_t ps = a.pruner_slot[q];
-        if (ps >= 0) {
+        if (ps >= 0 && (uint32_t)ps < mtd) {
             const uint32_t r = a.slot_rep[ps];
             f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
             k = (int)(q / (uint32_t)a.M);
@@ -1433,9 +1442,9 @@ void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st) {
     if (!a.mt) return;
     // <= 256 workgroups (a few rows per thread): each adds up to Kp*M2 global minima
     const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 256u);
-    SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.Kp, a.M2, a.cmin)));
+    SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.cmin)));
     SKY_DISPATCH_D(D, (k_cand_pick<DD><<<a.Kp, 64, 0, st>>>(a.rows, a.cmin, a.M2, a.pr2, a.npr2)));
-    SKY_DISPATCH_D(D, (k_cand_filter<DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a.rows, a.key, a.mt, a.M2, a.pr2,
+    SKY_DISPATCH_D(D, (k_cand_filter<DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a.rows, a.key, a.mt, a.d_mt, a.M2, a.pr2,
                                                                                    a.npr2, a.live)));
 }
 
@@ -1443,7 +1452,7 @@ void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *
                          int32_t *pruner_slot, int KM, hipStream_t st) {
     const uint32_t n = std::max<uint32_t>(a.mt, (uint32_t)KM);
     if (!n) return;
-    k_cand_compact<<<nblk(n, kThreads), kThreads, 0, st>>>(a.mt, padded_dims<double>(D), a.live, pos, a.rows, a.key,
+    k_cand_compact<<<nblk(n, kThreads), kThreads, 0, st>>>(a.mt, a.d_mt, padded_dims<double>(D), a.live, pos, a.rows, a.key,
                                                            a.src, rows2, key2, src2, pruner_slot, KM);
 }
 

@@ -38,8 +38,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t *__restrict__ in, size_t n,
-                                                              uint32_t *__restrict__ partial) {
+                                                              uint32_t *__restrict__ partial,
+                                                              const uint32_t *__restrict__ d_n) {
     __shared__ uint32_t s_w[4];
+    if (d_n) n = min(n, (size_t)*d_n);         // device-sized: n is the bound
     const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
     uint32_t s = 0;
 #pragma unroll
@@ -53,8 +55,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t *__
 __global__ __launch_bounds__(kScanThreads) void k_scan_tile(const uint32_t *__restrict__ in, size_t n,
                                                             uint32_t *__restrict__ out,
                                                             const uint32_t *__restrict__ offs,
-                                                            uint32_t *__restrict__ total_out) {
+                                                            uint32_t *__restrict__ total_out,
+                                                            const uint32_t *__restrict__ d_n) {
     __shared__ uint32_t s_w[4];
+    if (d_n) n = min(n, (size_t)*d_n);
     const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
     uint32_t v[kScanItems];
     uint32_t s = 0;
@@ -102,8 +106,10 @@ constexpr int kScanOnePer = 64;
 constexpr size_t kScanOneMax = (size_t)kScanOneThreads * kScanOnePer;
 __global__ __launch_bounds__(kScanOneThreads) void k_scan_one(const uint32_t *__restrict__ in, uint32_t n,
                                                               uint32_t *__restrict__ out,
-                                                              uint32_t *__restrict__ total_out) {
+                                                              uint32_t *__restrict__ total_out,
+                                                              const uint32_t *__restrict__ d_n) {
     __shared__ uint32_t s_w[kScanOneThreads / 64];
+    if (d_n) n = min(n, *d_n);
     const uint32_t per = (n + kScanOneThreads - 1) / kScanOneThreads;
     const uint32_t b = threadIdx.x * per;
     uint32_t v[kScanOnePer];
@@ -138,24 +144,24 @@ size_t scan_scratch_words(size_t n) {
 }
 
 void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, uint32_t *scratch,
-                   hipStream_t st) {
+                   hipStream_t st, const uint32_t *d_n) {
     if (n == 0) {
         if (d_total) hipMemsetAsync(d_total, 0, 4, st);
         return;
     }
     const size_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
-        k_scan_tile<<<1, kScanThreads, 0, st>>>(in, n, out, nullptr, d_total);
+        k_scan_tile<<<1, kScanThreads, 0, st>>>(in, n, out, nullptr, d_total, d_n);
         return;
     }
     if (n <= kScanOneMax) {                    // one launch instead of reduce / partials / tiles
-        k_scan_one<<<1, kScanOneThreads, 0, st>>>(in, (uint32_t)n, out, d_total);
+        k_scan_one<<<1, kScanOneThreads, 0, st>>>(in, (uint32_t)n, out, d_total, d_n);
         return;
     }
     uint32_t *partial = scratch;
-    k_scan_reduce<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, partial);
+    k_scan_reduce<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, partial, d_n);
     k_scan_small<<<1, 1024, 0, st>>>(partial, tiles, d_total);
-    k_scan_tile<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, out, partial, nullptr);
+    k_scan_tile<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, out, partial, nullptr, d_n);
 }
 
 }  // namespace sky

@@ -613,8 +613,11 @@ constexpr int kBruteY = 64, kBruteX = 64;
 template <typename T, int D>
 __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
+                                                         const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
+    if (d_mr) mr = min(mr, *d_mr);             // device-sized launch: mr is the bound
+    if (blockIdx.x * kBruteY >= mr || blockIdx.y * kBruteX >= mr) return;
     __shared__ T s_x[kBruteX * D];
     __shared__ uint32_t s_k[kBruteX];                         // f32 order key of the score
     __shared__ uint32_t s_p[kBruteX];                         // partition
@@ -679,8 +682,11 @@ __device__ __forceinline__ uint32_t pack_row16(const double *r, uint32_t (&w)[W]
 template <int D, int W>
 __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
+                                                         const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
+    if (d_mr) mr = min(mr, *d_mr);
+    if (blockIdx.x * kB16Y >= mr || blockIdx.y * kB16X >= mr) return;
     __shared__ uint4 s_x[kB16X][W / 4];
     __shared__ uint2 s_sp[kB16X];                              // (sum + 1, partition)
     const uint32_t y0 = blockIdx.x * kB16Y, x0 = blockIdx.y * kB16X;
@@ -729,13 +735,15 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
     if (valid && f) atomicOr(&domf[j], f);
 }
 
-__global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key, uint32_t mr, int gmerge,
+__global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key, uint32_t mr,
+                                                           const uint32_t *__restrict__ d_mr, int gmerge,
                                                            const uint32_t *__restrict__ domf,
                                                            uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g,
                                                            uint32_t *__restrict__ segalive,
                                                            uint32_t *__restrict__ segn, uint32_t *__restrict__ slot_rep) {
     __shared__ uint32_t s_n[kMaxK], s_a[kMaxK];
     for (int q = threadIdx.x; q < kMaxK; q += kThreads) { s_n[q] = 0; s_a[q] = 0; }
+    if (d_mr) mr = min(mr, *d_mr);
     __syncthreads();
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (j < mr) {
@@ -757,19 +765,19 @@ __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__res
 
 void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
                         uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
-                        uint32_t *slot_rep, hipStream_t st) {
+                        uint32_t *slot_rep, hipStream_t st, const uint32_t *d_mr) {
     if (!mr) return;
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
     if (u16) {
         const dim3 g16((mr + kB16Y - 1) / kB16Y, (mr + kB16X - 1) / kB16X);
-        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, domf))); }
-        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, domf))); }
+        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
+        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
     } else if (f32) {
-        SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+        SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, d_mr, domf)));
     } else {
-        SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, domf)));
+        SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, d_mr, domf)));
     }
-    k_brute_finish<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, mr, gmerge ? 1 : 0, domf, alive_l,
+    k_brute_finish<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, mr, d_mr, gmerge ? 1 : 0, domf, alive_l,
                                                                          alive_g, segalive, segn, slot_rep);
 }
 

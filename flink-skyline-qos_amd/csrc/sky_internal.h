@@ -34,8 +34,9 @@ namespace sky {
 
 // ---- k_scan.hip ----
 size_t scan_scratch_words(size_t n);
+// d_n (optional): the item count on the device, n its bound
 void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, uint32_t *scratch,
-                   hipStream_t st);
+                   hipStream_t st, const uint32_t *d_n = nullptr);
 
 // ---- k_radix.hip ----
 size_t radix_scratch_words(size_t m);
@@ -99,6 +100,7 @@ struct AppendArgs {
     uint32_t *flags;
     unsigned long long *orand;
     uint32_t slot_cap;
+    uint32_t *mt_total = nullptr;  // device out (optional): min(m + nps, slot_cap)
 };
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st);
 struct FateArgs {
@@ -112,6 +114,7 @@ struct FateArgs {
     const uint32_t *dup_cnt;              // stats only
     unsigned long long *lsz, *surv;       // [kStatShards][K] stat shards, or nullptr: no stats
     uint32_t *tile_cand;                  // [tiles] zeroed: += candidates in G per tile (nullptr: not counted)
+    const uint32_t *d_mt = nullptr;       // device slot count (mt is then its bound)
 };
 void launch_fate_tables(const FateArgs &a, hipStream_t st);
 
@@ -126,6 +129,7 @@ struct CandArgs {
     double *pr2;                  // [Kp][M2][D]
     int32_t *npr2;                // [Kp]
     uint32_t *live;               // [mt] out
+    const uint32_t *d_mt = nullptr;   // device slot count (mt is then its bound)
 };
 void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st);
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
@@ -246,9 +250,10 @@ constexpr uint32_t kBruteMax = 16384;
 // the caller; writes alive_l / alive_g / slot_rep (identity) per slot
 // f32: compare in f32 (every candidate value exactly an f32), else f64; u16: every candidate
 // value an integer in [0, 65535]: packed u16 compares (k_brute16_pairs)
+// d_mr (optional): the slot count on the device, mr its bound
 void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
                         uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
-                        uint32_t *slot_rep, hipStream_t st);
+                        uint32_t *slot_rep, hipStream_t st, const uint32_t *d_mr = nullptr);
 void launch_seg_alive(const uint64_t *rep_key, const uint8_t *alive, uint32_t mr, uint32_t *cnt, hipStream_t st);
 void launch_flag_u8_to_u32(const uint8_t *in, uint32_t n, uint32_t *out, hipStream_t st);
 

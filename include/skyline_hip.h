@@ -228,6 +228,10 @@ int sky_memcpy_d2h(sky_ctx *ctx, void *h_dst, const void *d_src, int64_t bytes);
 /* on: 0 off; 1 HIP-event timers around the timed kernels only (light: usable inside a timed
  * region); 2 also the per-phase events of sky_profile_phases */
 int sky_profile_enable(sky_ctx *ctx, int on);
+/* counters_out: n, candidates, reps (slots on the small-set route), global reps, output size,
+ * SFS rounds, pair tests, and [7] = bit0 f64 compares, bit1 score ties, bit2 packed u16,
+ * bit3 the planned (device-sized, no mid-query host read) route served the query, bit4 a
+ * planned attempt missed and the query re-ran synchronised, bits 8.. bounding-box tiles */
 int sky_profile_phases(sky_ctx *ctx, double *ms_out /* SKY_PHASES */, int64_t *counters_out /* 8 */);
 int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
                        int64_t *units);

@@ -1,0 +1,133 @@
+"""The planned route (engine.hip pipe_run_planned): a query that repeats the last query's
+small-set route (prefilter rounds, then the brute pair pass) with device-sized launches and
+no host read before the final one, which verifies the route's assumptions and re-runs the
+query synchronised on a miss.  Every answer is checked against the oracle
+(FlinkSkyline.java:417-444 local BNL, :548-566 global BNL, :593-608 stats), whichever route
+served it; counters[7] bit 3 = planned, bit 4 = a planned attempt missed."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import Oracle  # noqa: F401  (the checker)
+
+pytestmark = pytest.mark.gpu
+
+PLANNED, MISSED = 8, 16
+
+
+def route(eng):
+    _, cnt = eng.phases()
+    return int(cnt[7]), int(cnt[1])
+
+
+def check(eng, orc, vals, P, algo="angle"):
+    ids, org = eng.query(vals)
+    exp, keys, els, esv = orc.query_sfs(algo, vals, P)
+    np.testing.assert_array_equal(ids, exp)
+    np.testing.assert_array_equal(org, keys[exp])
+    ls, sv = eng.stats()
+    np.testing.assert_array_equal(ls, els)
+    np.testing.assert_array_equal(sv, esv)
+    return route(eng)
+
+
+@pytest.mark.parametrize("dist,D,n,P", [(2, 8, 200000, 16), (0, 5, 200000, 16), (0, 4, 400000, 8), (1, 3, 100000, 8)])
+def test_planned_equals_oracle(gpu_engine_factory, oracle, dist, D, n, P):
+    """The first query learns the route, the next ones (other seeds, same shape) replay it."""
+    eng = gpu_engine_factory(D, P, "mr-angle")
+    r0, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=11), P)
+    assert not r0 & PLANNED
+    planned = 0
+    for seed in (12, 13, 14):
+        r, m = check(eng, oracle, oracle.synth(dist, D, n, seed=seed), P)
+        planned += bool(r & PLANNED)
+    assert planned >= 2, "the small-set route was not replayed"
+    eng.close()
+
+
+def test_planned_prefilter_rounds(gpu_engine_factory, oracle):
+    """A stream whose candidates pass the prefilter threshold (>= 4096 slots): the replay
+    runs its prefilter rounds on device-sized launches."""
+    eng = gpu_engine_factory(8, 16, "mr-angle")
+    check(eng, oracle, oracle.synth(2, 8, 2500000, seed=21), 16)
+    r, m = check(eng, oracle, oracle.synth(2, 8, 2500000, seed=22), 16)
+    assert m >= 4096
+    assert r & PLANNED
+    eng.close()
+
+
+def test_plan_miss_on_larger_stream(gpu_engine_factory, oracle):
+    """Learned on a stream with few candidates, replayed on one with far more: the counts
+    exceed the bounds, the query re-runs synchronised (and learns the new route)."""
+    eng = gpu_engine_factory(5, 8, "mr-angle")
+    check(eng, oracle, oracle.synth(1, 5, 20000, seed=31), 8)
+    check(eng, oracle, oracle.synth(1, 5, 20000, seed=32), 8)
+    r, _ = check(eng, oracle, oracle.synth(0, 5, 300000, seed=33), 8)
+    assert r & MISSED and not r & PLANNED
+    r, _ = check(eng, oracle, oracle.synth(0, 5, 300000, seed=34), 8)
+    assert r & PLANNED
+    eng.close()
+
+
+def test_plan_miss_on_row_type(gpu_engine_factory, oracle):
+    """Learned on integer rows (packed-u16 pair pass), replayed on f32-exact non-integer rows
+    and on f64 rows: the compare type no longer holds, so the query re-runs."""
+    eng = gpu_engine_factory(4, 8, "mr-angle")
+    base = oracle.synth(0, 4, 100000, seed=41)
+    check(eng, oracle, base, 8)
+    r, _ = check(eng, oracle, base, 8)
+    assert r & PLANNED                                    # planned replay of the integer route
+    r, _ = check(eng, oracle, base + 0.5, 8)
+    assert r & MISSED
+    r, _ = check(eng, oracle, base + 0.1, 8)              # not exact in f32: the f64 pass
+    assert r & MISSED and r & 1
+    r, _ = check(eng, oracle, base + 0.3, 8)              # f64 route replayed
+    assert r & PLANNED and r & 1
+    eng.close()
+
+
+def test_plan_nan_and_recovery(gpu_engine_factory, oracle):
+    """A NaN tuple on the planned route is rejected as on the synchronised one; the context
+    stays usable."""
+    from skyline._abi import SkylineError
+    eng = gpu_engine_factory(4, 8, "mr-angle")
+    vals = oracle.synth(2, 4, 50000, seed=51)
+    check(eng, oracle, vals, 8)
+    check(eng, oracle, vals, 8)
+    bad = vals.copy()
+    bad[4321, 2] = np.nan
+    with pytest.raises(SkylineError) as e:
+        eng.query(bad)
+    assert e.value.code == -4
+    r, _ = check(eng, oracle, oracle.synth(2, 4, 50000, seed=52), 8)
+    eng.close()
+
+
+def test_plan_slot_overflow(gpu_engine_factory, oracle):
+    """Candidate slots sized by a small stream (SKY_SLOT_MIN forces small slots); the planned
+    replay on a stream with more candidates than slots counts the overflow on the device and
+    re-runs with room for all."""
+    os.environ["SKY_SLOT_MIN"] = "64"
+    try:
+        eng = gpu_engine_factory(5, 8, "mr-angle")
+        check(eng, oracle, oracle.synth(1, 5, 20000, seed=61), 8)
+        check(eng, oracle, oracle.synth(1, 5, 20000, seed=62), 8)
+        r, m = check(eng, oracle, oracle.synth(0, 5, 200000, seed=63), 8)
+        assert r & MISSED and m > 64
+        eng.close()
+    finally:
+        del os.environ["SKY_SLOT_MIN"]
+
+
+def test_plan_disabled_equals(gpu_engine_factory, oracle):
+    """SKY_PLAN=0 (read per query) keeps every query on the synchronised route."""
+    os.environ["SKY_PLAN"] = "0"
+    try:
+        eng = gpu_engine_factory(6, 16, "mr-angle")
+        for seed in (71, 72):
+            r, _ = check(eng, oracle, oracle.synth(4, 6, 200000, seed=seed), 16)
+            assert not r & PLANNED
+        eng.close()
+    finally:
+        del os.environ["SKY_PLAN"]
