@@ -318,19 +318,21 @@ __device__ __forceinline__ uint16_t classify(const double (&v)[D], int32_t k, co
     uint16_t code = kCodeCandidate;
     const int np = s_npr[k];
     const double *pr = s_pr + k * pr_stride<D>(M);
-    // two compares per dimension: with no NaN (rejected before this), all(p <= v) and
-    // any(p < v) holds iff all(p <= v) and not all(p == v).  The kernel is VALU-issue
-    // bound (SQ_INSTS_VALU x 4 cycles ~ the launch's cycles), so each compare counts.
+    // one compare per dimension and pruner: the first pruner with all(p <= v) decides, as a
+    // duplicate if all(p == v) (tested for that pruner only), else dropped (p <= v and
+    // p != v is dominance).  A NaN value fails every compare: the tuple comes out a
+    // candidate, and the caller looks for NaN there.
     for (int j = 0; j < np; j++) {
-        bool le = true, eq = true;
+        bool le = true;
 #pragma unroll
-        for (int d = 0; d < D; d++) {
-            const double p = pr[pr_off<D>(k, j, d)];
-            le &= p <= v[d];
-            eq &= p == v[d];
+        for (int d = 0; d < D; d++) le &= pr[pr_off<D>(k, j, d)] <= v[d];
+        if (le) {
+            bool eq = true;
+#pragma unroll
+            for (int d = 0; d < D; d++) eq &= pr[pr_off<D>(k, j, d)] == v[d];
+            code = eq ? (uint16_t)(1 + j) : kCodeDropped;
+            break;
         }
-        if (eq) { code = (uint16_t)(1 + j); break; }
-        if (le) { code = kCodeDropped; break; }
     }
     if (code == kCodeCandidate) {
 #pragma unroll
@@ -431,11 +433,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         const int32_t kg = kn;
         if (r > 0 && i - kThreads < a.n) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
         SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : next_base + threadIdx.x);
-        bool nan = false;
-#pragma unroll
-        for (int d = 0; d < D; d++) nan |= v[d] != v[d];
         int32_t k = GIVEN ? kg : a.single ? 0 : partition_key_fast<D>(v, a.kp);
-        const bool defer = !GIVEN && valid && !nan && !a.single && k == kAngleUndecided;
+        // NaN fails the MR-Angle fast path and every pruner compare: it is looked for only
+        // where a tuple comes out undecided, out of the queried keys or a candidate
+        const bool undecided = !GIVEN && !a.single && k == kAngleUndecided;
+        const bool nan = undecided && any_nan<D>(v);
+        const bool defer = valid && undecided && !nan;
         const uint64_t dm = __ballot(defer);
         if (defer) wlist[kList - 1 - (dcnt + lanes_below(dm))] = i - base;
         dcnt += (uint32_t)__popcll(dm);
@@ -444,8 +447,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         if (valid && !defer) {
             uint16_t code = kCodeCandidate;
             if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
-            else if (k < 0 || k >= a.Kp) { code = kCodeDropped; k = 0; }
-            else code = classify<D>(v, k, s_pr, s_npr, a.M, lflags);
+            else if (k < 0 || k >= a.Kp) {
+                if (any_nan<D>(v)) lflags |= kFlagNaN;
+                code = kCodeDropped;
+                k = 0;
+            } else {
+                code = classify<D>(v, k, s_pr, s_npr, a.M, lflags);
+                if (code == kCodeCandidate && any_nan<D>(v)) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
+            }
             cand = code == kCodeCandidate;
             st = (uint16_t)(((uint32_t)k << 8) | code);
         }

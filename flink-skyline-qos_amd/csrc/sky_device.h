@@ -278,6 +278,14 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
     return k != kAngleUndecided ? k : angle_key_exact<D>(v, kp.P);
 }
 
+template <int D>
+__device__ __forceinline__ bool any_nan(const double (&v)[D]) {
+    bool nan = false;
+#pragma unroll
+    for (int d = 0; d < D; d++) nan |= v[d] != v[d];
+    return nan;
+}
+
 // ---- dominance ----------------------------------------------------------------
 // a dominates b (ServiceTuple.java:67-77): all a<=b and some a<b.  With NaN-free
 // rows the early-exit loop and this branch-free form agree.
