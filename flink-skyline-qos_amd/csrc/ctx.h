@@ -78,6 +78,23 @@ struct Ctx {
         k.dim_width = domain / (double)P;
         k.grid_mid = domain / 2.0;
         k.margin = angle_margin(P);
+        k.ang_scale = D >= 2 ? (float)((2.0 / 3.141592653589793) / (double)(D - 1) * (double)P) : 0.0f;
+        k.ang_lo = (float)k.margin;
+        k.ang_hi = (float)(1.0 - k.margin);
+        // special-case keys: avg = c / (D-1), key = clamp(d2i(avg * P)) (AnglePartitioner,
+        // FlinkSkyline.java:760-780), c = 0..2(D-1) <= 30; keys < P <= 256 fit a byte
+        uint64_t sp[4] = {0, 0, 0, 0};
+        for (int c = 0; D >= 2 && c <= 2 * (D - 1); c++) {
+            const double avg = (double)c / (double)(D - 1);
+            const double t = avg * (double)P;
+            int32_t key = t != t ? 0 : t >= 2147483647.0 ? 2147483647 : t <= -2147483648.0 ? INT32_MIN : (int32_t)t;
+            key = key > P - 1 ? P - 1 : (key < 0 ? 0 : key);
+            sp[c / 8] |= (uint64_t)(uint32_t)key << ((c % 8) * 8);
+        }
+        k.ang_special0 = sp[0];
+        k.ang_special1 = sp[1];
+        k.ang_special2 = sp[2];
+        k.ang_special3 = sp[3];
         k.grid_filter = algo == SKY_ALGO_GRID ? grid_filter : 0;
         return k;
     }

@@ -421,7 +421,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     uint32_t wcnt = 0, dcnt = 0;
     uint64_t o = 0, an = ~0ull;
     const uint32_t base = tile * kTile;
-    const uint32_t next_base = (tile + gridDim.x) * kTile;       // past the end: clamped, a cache hit
     uint16_t st_prev = 0;
 #pragma unroll 1
     for (int r = 0; r < kItems; r++) {
@@ -432,7 +431,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         for (int d = 0; d < D; d++) v[d] = vn[d];
         const int32_t kg = kn;
         if (r > 0 && i - kThreads < a.n) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
-        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : next_base + threadIdx.x);
+        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : i);           // past the tile: a cache hit
         int32_t k = GIVEN ? kg : a.single ? 0 : partition_key_fast<D>(v, a.kp);
         // NaN fails the MR-Angle fast path and every pruner compare: it is looked for only
         // where a tuple comes out undecided, out of the queried keys or a candidate
@@ -530,6 +529,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         a.tile_orand[2 * tile] = bo;
         a.tile_orand[2 * tile + 1] = ba;
     }
+    // the next tile's first row, in flight over the barrier (not over the candidate appends
+    // above: the row registers live across them spilled to scratch, and every scratch
+    // reload's vmcnt wait then also waited for the prefetch)
+    SKY_FILTER_FETCH((tile + gridDim.x) * kTile + threadIdx.x);
     __syncthreads();                           // s_list / s_wc / s_o reused by the next tile
     }
 #undef SKY_FILTER_FETCH

@@ -121,6 +121,13 @@ struct KeyParams {
     double margin;     // MR-Angle fast path: distance of avg*P from an integer that is certain
     int grid_filter;   // MR-Grid dominance filter (FlinkSkyline.java:716-733, disabled in the reference):
                        // tuples with every value >= maxVal/2 get key -1 (removed before keyBy)
+    // the fast path's f32 constants, converted once on the host (kernel arguments stay in
+    // SGPRs; converted in the kernel they were VGPRs live across the whole stream loop)
+    float ang_scale;   // (2/pi) / (D-1) * P
+    float ang_lo, ang_hi;   // margin, 1 - margin
+    // the special case's key for each exact normalized sum c in 0..2(D-1): byte c % 8 of
+    // ang_special[c / 8] = clamp(d2i(c / (D-1) * P)), the reference's f64 ops done on the host
+    uint64_t ang_special0, ang_special1, ang_special2, ang_special3;
 };
 
 // Error budget of the f32 estimate in t = avg*P (inputs with nonzero magnitudes in
@@ -199,7 +206,7 @@ constexpr int32_t kAngleUndecided = -1;
 constexpr int32_t kKeyFiltered = -2;   // removed by the MR-Grid dominance filter (never queried)
 
 template <int D>
-__device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, double margin) {
+__device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], const KeyParams &kp) {
     if (D < 2) return 0;
     // every value 0 or of magnitude in [1e-15, 1e15] (NaN and inf fail): then no
     // square underflows, so the reference's f64 s_i is 0 exactly when v_j == 0 for
@@ -222,14 +229,14 @@ __device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, d
             special &= z | iz[i];
         }
         if (special) {
-            double normalized = 0.0;
+            // normalized is the exact integer c = sum of the per-angle 0 / 1 / 2: the key of
+            // each c was computed on the host (KeyParams::ang_special*)
+            uint32_t c = 0;
 #pragma unroll
-            for (int i = 0; i < D - 1; i++) {
-                const double nrm = zero_after[i] ? (signbit(v[i]) ? 2.0 : 0.0) : 1.0;
-                normalized = normalized + nrm;
-            }
-            const double avg = normalized / (double)(D - 1);
-            return clamp_key(java_d2i(avg * (double)P), P);
+            for (int i = 0; i < D - 1; i++) c += zero_after[i] ? (signbit(v[i]) ? 2u : 0u) : 1u;
+            const uint64_t w = c < 8 ? kp.ang_special0 : c < 16 ? kp.ang_special1 : c < 24 ? kp.ang_special2
+                                                                                         : kp.ang_special3;
+            return (int32_t)((w >> ((c & 7u) * 8u)) & 0xffu);
         }
         float f[D];
 #pragma unroll
@@ -240,10 +247,10 @@ __device__ __forceinline__ int32_t angle_key_fast(const double (&v)[D], int P, d
             s = fmaf(f[i + 1], f[i + 1], s);
             est += atan2_est(__builtin_amdgcn_sqrtf(s), f[i]);
         }
-        const float t = est * (float)((2.0 / 3.141592653589793) / (double)(D - 1) * (double)P);
+        const float t = est * kp.ang_scale;
         const float fl = floorf(t);
         const float fr = t - fl;
-        if (fr > (float)margin && fr < (float)(1.0 - margin)) return clamp_key((int32_t)fl, P);
+        if (fr > kp.ang_lo && fr < kp.ang_hi) return clamp_key((int32_t)fl, kp.P);
     }
     return kAngleUndecided;
 }
@@ -260,7 +267,7 @@ __device__ __forceinline__ int32_t partition_key_fast(const double (&v)[D], cons
         if (kp.grid_filter && mask == (D >= 32 ? ~0u : (1u << D) - 1u)) return kKeyFiltered;
         return (int32_t)mask;
     }
-    return angle_key_fast<D>(v, kp.P, kp.margin);
+    return angle_key_fast<D>(v, kp);
 }
 
 template <int D>
@@ -274,7 +281,7 @@ __device__ __forceinline__ int32_t partition_key(const double (&v)[D], const Key
         if (kp.grid_filter && mask == (D >= 32 ? ~0u : (1u << D) - 1u)) return kKeyFiltered;
         return (int32_t)mask;
     }
-    const int32_t k = angle_key_fast<D>(v, kp.P, kp.margin);
+    const int32_t k = angle_key_fast<D>(v, kp);
     return k != kAngleUndecided ? k : angle_key_exact<D>(v, kp.P);
 }
 
