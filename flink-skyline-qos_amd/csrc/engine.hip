@@ -868,6 +868,29 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
 }
 
 
+// The planned route's zero / all-ones initialisations, added to the run's first fill launch:
+// the criterion minima of every prefilter round (a slice each), the brute pass's domination
+// bits (its bound) and per-partition counts.
+static int plan_prepare(Pipe &p, int D, FillSet &fill) {
+    const Pipe::Plan &pl = p.plan;
+    const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
+    const size_t KM2 = (size_t)p.Kp * M2;
+    uint32_t fin = pl.bound[0];
+    for (int r = 0; r < pl.rounds; r++) fin = std::min(pl.bound[r + 1], fin);
+    if (pl.rounds) {
+        SKY_TRY(p.cmin.ensure(KM2 * pl.rounds * 8));
+        fill.add(p.cmin.p, KM2 * pl.rounds * 8, 0xff);
+    }
+    SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
+    SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
+    SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(fin, 1) * 4));
+    fill.add(p.segalive.p, (size_t)p.Kp * 4);
+    fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
+    fill.add(p.keep.p, (size_t)std::max<uint32_t>(fin, 1) * 4);
+    (void)D;
+    return SKY_OK;
+}
+
 // The planned route (see pipe_run): the prefilter rounds and the brute pass of the last
 // query's small-set route, every launch sized by the plan's bounds and reading its count
 // from the device; no host synchronisation before pipe_finish's final read.
@@ -892,7 +915,6 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         const int KM2 = p.Kp * M2;
         DevBuf *dr = round & 1 ? &p.rows3 : &p.rows2, *dk = round & 1 ? &p.sortkey3 : &p.sortkey2,
                *ds = round & 1 ? &p.slot_src3 : &p.slot_src2;
-        SKY_TRY(p.cmin.ensure((size_t)KM2 * 8));
         SKY_TRY(p.pr2.ensure((size_t)KM2 * D * 8));
         SKY_TRY(p.npr2.ensure((size_t)p.Kp * 4));
         SKY_TRY(p.live.ensure((size_t)bound * 4));
@@ -901,8 +923,6 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         SKY_TRY(dk->ensure((size_t)bound * 8));
         SKY_TRY(ds->ensure((size_t)bound * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(bound + 1) * 4 + 64));
-        fill.add(p.cmin.p, (size_t)KM2 * 8, 0xff);
-        HIP_TRY(fill.launch(st));
         CandArgs ca{};
         ca.mt = bound;
         ca.d_mt = d_cnt;
@@ -911,7 +931,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         ca.src = p.s_src->as<uint32_t>();
         ca.Kp = p.Kp;
         ca.M2 = M2;
-        ca.cmin = p.cmin.as<unsigned long long>();
+        ca.cmin = p.cmin.as<unsigned long long>() + (size_t)round * KM2;   // filled by plan_prepare
         ca.pr2 = p.pr2.as<double>();
         ca.npr2 = p.npr2.as<int32_t>();
         ca.live = p.live.as<uint32_t>();
@@ -932,18 +952,11 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     }
     if (tm) tm->mark(4, st);
     if (tm) tm->mark(5, st);
-    SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
-    SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
-    SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
     SKY_TRY(p.slot_rep.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
     SKY_TRY(p.alive_l.ensure(std::max<uint32_t>(bound, 1)));
     SKY_TRY(p.alive_g.ensure(std::max<uint32_t>(bound, 1)));
     SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
-    fill.add(p.segalive.p, (size_t)p.Kp * 4);
-    fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
-    fill.add(p.keep.p, (size_t)std::max<uint32_t>(bound, 1) * 4);
-    HIP_TRY(fill.launch(st));
-    PlanRun pr;
+    PlanRun pr;                                // segalive / seg_begin / keep: filled by plan_prepare
     pr.cap = cap;
     pr.cap_full = cap_full;
     pr.d_cnt = d_cnt;
@@ -1049,6 +1062,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.tile_cand.ensure((size_t)tiles * 4));
         fill.add(p.tile_cand.p, (size_t)tiles * 4);
     }
+    // the planned route's counters and flags go out with this launch too: one criterion-minima
+    // slice per prefilter round, the brute pass's domination bits and partition counts
+    if (planned) SKY_TRY(plan_prepare(p, D, fill));
     HIP_TRY(fill.launch(st));
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
                           p.pruners.as<double>(), p.npr.as<int32_t>(), st);
@@ -1089,7 +1105,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
     if (angle_keys) launch_filter_deferred(D, fa, st);
-    launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
+    if (!planned)   // the sort keys' OR / AND only size the radix sort (not on the planned route)
+        launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
     STAGE(st, "filter");
     if (tm) tm->mark(2, st);
 

@@ -390,8 +390,11 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
 //    occupancy their LDS image allows: the row-per-lane loads are not the limit.
 // Candidates (partition << 16 | offset) fill each wave's LDS list from the front,
 // deferred offsets from the back; the tile reserves its slots with one atomic.
+#ifndef SKY_FILTER_WPE
+#define SKY_FILTER_WPE 6          // waves per SIMD the register budget is sized for: 6 (80 VGPRs) -3.5 % vs 7, 8 +2 %
+#endif
 template <int D, bool GIVEN>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 7 : 1))) void k_filter(FilterArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8 ? SKY_FILTER_WPE : 1))) void k_filter(FilterArgs a) {
     constexpr int kList = kItems * 64;                           // list entries per wave
     extern __shared__ __attribute__((aligned(16))) double s_pr[];   // pruner image (pr_stride), then [Kp*M] u32 dup counts
     uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * pr_stride<D>(a.M));
