@@ -1005,6 +1005,7 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
     }
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     const uint32_t mtd = a.d_mt ? min(a.mt, *a.d_mt) : a.mt;   // device-sized: a.mt is the bound
+    uint32_t cand_tile = 0xffffffffu;          // a candidate in G: its stream tile (output counts)
     int k = -1;
     unsigned long long w = 0;
     uint32_t f = 0;
@@ -1015,7 +1016,7 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
             f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
             const uint16_t s0 = a.status[src];
             a.status[src] = (uint16_t)((s0 & 0xff00u) | (kCodeFate0 + f));
-            if (a.tile_cand && (f & 2u)) atomicAdd(&a.tile_cand[src / kTile], 1u);
+            cand_tile = (f & 2u) ? src / kTile : 0xffffffffu;
             k = s0 >> 8;
             w = 1;
         }
@@ -1029,6 +1030,18 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
             w = stats ? a.dup_cnt[q] : 0u;
         }
         a.pruner_fate[q] = (uint8_t)f;
+    }
+    if (a.tile_cand) {
+        // one atomic per distinct tile in the wave (slots are in stream-tile order, so a wave
+        // spans one or two tiles; per-lane atomics on one counter serialised: 0.8 ms at 1M slots)
+        uint64_t pend = __ballot(cand_tile != 0xffffffffu);
+        while (pend) {
+            const int leader = __ffsll((unsigned long long)pend) - 1;
+            const uint32_t t0 = __shfl(cand_tile, leader, 64);
+            const uint64_t same = __ballot(cand_tile == t0);
+            if ((int)(threadIdx.x & 63) == leader) atomicAdd(&a.tile_cand[t0], (uint32_t)__popcll(same));
+            pend &= ~same;
+        }
     }
     if (stats) {
         if (k >= 0 && (f & 1u)) {
