@@ -1095,6 +1095,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.flags = p.flags.as<uint32_t>();
     fa.slot_cap = (uint32_t)cap;
     fa.tile_hist = p.hist_count ? p.tile_hist.as<uint32_t>() : nullptr;
+    {
+        static const int fdbg = [] { const char *e = getenv("SKY_FILTER_DBG"); return e ? atoi(e) : 0; }();
+        fa.dbg = fdbg;
+    }
     const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;
     if (angle_keys) {
         SKY_TRY(p.defer.ensure((size_t)n * 4));

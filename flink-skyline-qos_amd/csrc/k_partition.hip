@@ -390,6 +390,9 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
 //    occupancy their LDS image allows: the row-per-lane loads are not the limit.
 // Candidates (partition << 16 | offset) fill each wave's LDS list from the front,
 // deferred offsets from the back; the tile reserves its slots with one atomic.
+#ifndef SKY_FILTER_PF2
+#define SKY_FILTER_PF2 0          // 1: two rows in flight per lane (A/B builds)
+#endif
 #ifndef SKY_FILTER_WPE
 #define SKY_FILTER_WPE 6          // waves per SIMD the register budget is sized for: 6 (80 VGPRs) -3.5 % vs 7, 8 +2 %
 #endif
@@ -410,12 +413,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     double vn[D];                                                // the row of item r+1, in flight
     int32_t kn = 0;
-#define SKY_FILTER_FETCH(I)                                                                \
+#define SKY_FILTER_FETCH_TO(I, VN, KN)                                                     \
     do {                                                                                   \
         const uint32_t i_ = min((uint32_t)(I), nl);                                        \
-        load_row<D>(a.vals + (size_t)i_ * D, vn);                                          \
-        if constexpr (GIVEN) kn = a.given_keys[i_];                                        \
+        load_row<D>(a.vals + (size_t)i_ * D, VN);                                          \
+        if constexpr (GIVEN) KN = a.given_keys[i_];                                        \
     } while (0)
+#if SKY_FILTER_PF2
+    double vn2[D];                                               // the row of item r+2, in flight
+    int32_t kn2 = 0;
+#define SKY_FILTER_FETCH(I)                                                                \
+    do {                                                                                   \
+        SKY_FILTER_FETCH_TO(I, vn, kn);                                                    \
+        SKY_FILTER_FETCH_TO((I) + kThreads, vn2, kn2);                                     \
+    } while (0)
+#else
+#define SKY_FILTER_FETCH(I) SKY_FILTER_FETCH_TO(I, vn, kn)
+#endif
     // a.tpb tiles per workgroup, interleaved over the grid (tile = t * grid + block): the
     // pruner image is loaded once per workgroup, not once per 2048 tuples
     SKY_FILTER_FETCH(blockIdx.x * kTile + threadIdx.x);
@@ -433,8 +447,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #pragma unroll
         for (int d = 0; d < D; d++) v[d] = vn[d];
         const int32_t kg = kn;
-        if (r > 0 && i - kThreads < a.n) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
+        if (r > 0 && i - kThreads < a.n && a.dbg < 2) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
+#if SKY_FILTER_PF2
+#pragma unroll
+        for (int d = 0; d < D; d++) vn[d] = vn2[d];
+        kn = kn2;
+        SKY_FILTER_FETCH_TO(r + 2 < kItems ? i + 2 * kThreads : i, vn2, kn2);
+#else
         SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : i);           // past the tile: a cache hit
+#endif
+        if (a.dbg) {                 // measurement only (SKY_FILTER_DBG=1): the stream without the work
+            double acc = 0;
+#pragma unroll
+            for (int d = 0; d < D; d++) acc += v[d];
+            st_prev = acc == 1234.5 ? 1 : 0;
+            continue;
+        }
         int32_t k = GIVEN ? kg : a.single ? 0 : partition_key_fast<D>(v, a.kp);
         // NaN fails the MR-Angle fast path and every pruner compare: it is looked for only
         // where a tuple comes out undecided, out of the queried keys or a candidate
@@ -468,7 +496,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     }
     {
         const uint32_t il = base + (kItems - 1) * kThreads + threadIdx.x;
-        if (il < a.n) a.status[il] = st_prev;
+        if (il < a.n && a.dbg < 2) a.status[il] = st_prev;
     }
     // the tile's candidates: ONE slot reservation per tile, then rows re-read (cache
     // hot) and appended with their sort keys
@@ -539,6 +567,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     __syncthreads();                           // s_list / s_wc / s_o reused by the next tile
     }
 #undef SKY_FILTER_FETCH
+#undef SKY_FILTER_FETCH_TO
     if (lflags) atomicOr(a.flags, lflags);
 }
 

@@ -76,6 +76,7 @@ struct FilterArgs {
     uint32_t *defer_cnt;
     uint32_t slot_cap;            // slots allocated: appends past it are counted, not written
     uint32_t *tile_hist;          // [tiles][Kp*M] duplicates per tile (nullptr: not kept; Kp*M <= kHistMaxKM)
+    int dbg;                      // SKY_FILTER_DBG (measurement only, results invalid): 1 = loads + status only
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
