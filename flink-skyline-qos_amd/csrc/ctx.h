@@ -1,6 +1,7 @@
 // ctx.h — the object behind an sky_ctx* handle.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -108,8 +109,18 @@ struct Ctx {
         hipEventCreate(&e);
         return e;
     }
+    // level 1 (light, usable inside a timed region): only the single kernels a measurement
+    // reads back; every timed pair is two event records on the stream (≈ 10 µs of gap each
+    // between short kernels), so the small-phase timers run at level 2 only
+    static bool ktimer_light(const char *name) {
+        static const char *const names[] = {"filter", "mbr", "dom", "csv_count", "csv_lines", "csv_parse",
+                                            "union_fate"};
+        for (const char *n : names)
+            if (!strcmp(n, name)) return true;
+        return false;
+    }
     void ktimer_begin(const char *name, hipStream_t s) {
-        if (!profile) return;
+        if (!profile || (profile < 2 && !ktimer_light(name))) return;
         KTime &k = kt[name];
         hipEvent_t a = take_event(), b = take_event();
         hipEventRecord(a, s);
@@ -117,7 +128,7 @@ struct Ctx {
         k.pending_units.push_back(0);
     }
     void ktimer_end(const char *name, hipStream_t s, int64_t units) {
-        if (!profile) return;
+        if (!profile || (profile < 2 && !ktimer_light(name))) return;
         KTime &k = kt[name];
         if (k.pending.empty()) return;
         hipEventRecord(k.pending.back().second, s);
