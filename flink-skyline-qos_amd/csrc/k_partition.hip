@@ -151,8 +151,10 @@ __global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restric
     const int KM = Kp * M;
     for (int q = threadIdx.x; q < KM; q += kThreads) s_min[q] = ~0ull;
     __syncthreads();
-    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
-    if (s < S) {
+    // grid-stride over the sample (few workgroups: each adds its KM minima to the same KM
+    // global words, so 256 workgroups serialised 256 atomics per word at L2)
+#pragma unroll 4
+    for (uint32_t s = blockIdx.x * kThreads + threadIdx.x; s < S; s += gridDim.x * kThreads) {
         const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
         double v[D];
         load_row<D>(vals + (size_t)i * D, v);
@@ -1467,8 +1469,12 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
                            double *pruners, int32_t *npr, hipStream_t st) {
     if (S == 0) return;                               // gmin: all-ones on entry (the caller's fill)
-    SKY_DISPATCH_D(D, (k_sample_min<DD><<<nblk(S, kThreads), kThreads, 0, st>>>(vals, n, S, kp, given_keys, single,
-                                                                                 Kp, M, gmin)));
+    static const unsigned sgrid = [] {        // SKY_SAMPLE_WG: workgroups of the sample pass (A/B knob)
+        const char *e = getenv("SKY_SAMPLE_WG");
+        return e ? (unsigned)std::max(1, atoi(e)) : 256u;   // 32: +20 us, 64: +2 us (latency-bound per row)
+    }();
+    const unsigned g = std::min<unsigned>(nblk(S, kThreads), sgrid);
+    SKY_DISPATCH_D(D, (k_sample_min<DD><<<g, kThreads, 0, st>>>(vals, n, S, kp, given_keys, single, Kp, M, gmin)));
     SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
 }
 
