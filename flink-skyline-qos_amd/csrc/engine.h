@@ -66,7 +66,7 @@ struct Pipe {
     DevBuf alive_l, alive_g, alive_u32, alive_scan, mult;
     // SFS
     DevBuf act, act2, keep, keep_scan, conf_rows, nconf, segs, seg_list, tiles, seg_begin, seg_end, segcnt;
-    DevBuf conf_small, seg_small, pruner_fate, defer, tile_orand, xkeep;
+    DevBuf conf_small, seg_small, pruner_fate, defer, xkeep;
     // global
     DevBuf gkey, gval, gkey_alt, gval_alt, grows, galive, gact_dummy;
     // integer-valued fast path (k_dom16.hip): packed u16 rows, round layouts, X' buffers

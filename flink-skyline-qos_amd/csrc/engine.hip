@@ -1029,7 +1029,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.rows.ensure(cap * rb64));
     SKY_TRY(p.sortkey.ensure(cap * 8));
     SKY_TRY(p.slot_src.ensure(cap * 4));
-    SKY_TRY(p.tile_orand.ensure((size_t)tiles * 16));
     SKY_TRY(p.dup_cnt.ensure((size_t)KM * 4));
     SKY_TRY(p.pr_entries.ensure((size_t)KM * 4));
     SKY_TRY(p.pruner_slot.ensure((size_t)KM * 4));
@@ -1089,7 +1088,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.sortkey = p.sortkey.as<uint64_t>();
     fa.slot_src = p.slot_src.as<uint32_t>();
     fa.m_total = p.totals.as<uint32_t>();
-    fa.tile_orand = p.tile_orand.as<unsigned long long>();
     fa.orand = p.orand.as<unsigned long long>();
     fa.dup_cnt = p.dup_cnt.as<uint32_t>();
     fa.flags = p.flags.as<uint32_t>();
@@ -1109,8 +1107,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
     if (angle_keys) launch_filter_deferred(D, fa, st);
-    if (!planned)   // the sort keys' OR / AND only size the radix sort (not on the planned route)
-        launch_orand_reduce(p.tile_orand.as<unsigned long long>(), tiles, p.orand.as<unsigned long long>(), st);
     STAGE(st, "filter");
     if (tm) tm->mark(2, st);
 

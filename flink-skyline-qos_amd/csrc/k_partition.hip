@@ -406,9 +406,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     __shared__ int32_t s_npr[kMaxK];
     __shared__ uint32_t s_list[kTile];
     __shared__ uint32_t s_wc[kThreads / 64], s_wd[kThreads / 64], s_base, s_dbase;
-    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
     load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
     uint32_t lflags = 0;
+    uint64_t o = 0, an = ~0ull;                                  // OR / AND of the appended sort keys
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *wlist = s_list + __builtin_amdgcn_readfirstlane(wave) * kList;
     const uint32_t nl = a.n - 1;
@@ -438,7 +438,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #pragma unroll 1
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t wcnt = 0, dcnt = 0;
-    uint64_t o = 0, an = ~0ull;
     const uint32_t base = tile * kTile;
     uint16_t st_prev = 0;
 #pragma unroll 1
@@ -548,28 +547,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         o |= key;
         an &= key;
     }
-    // per-tile OR / AND of the sort keys
+    // the next tile's first row, in flight over the barrier (not over the candidate appends
+    // above: the row registers live across them spilled to scratch, and every scratch
+    // reload's vmcnt wait then also waited for the prefetch)
+    SKY_FILTER_FETCH((tile + gridDim.x) * kTile + threadIdx.x);
+    __syncthreads();                           // s_list / s_wc reused by the next tile
+    }
+#undef SKY_FILTER_FETCH
+#undef SKY_FILTER_FETCH_TO
+    // OR / AND of the appended sort keys (they size the radix sort): one atomic pair per wave
+    // that appended any, at the end (no per-tile barrier, table or reduce kernel)
 #pragma unroll
     for (int sh = 32; sh >= 1; sh >>= 1) {
         o |= __shfl_xor(o, sh, 64);
         an &= __shfl_xor(an, sh, 64);
     }
-    if (lane == 0) { s_o[wave] = o; s_a[wave] = an; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long bo = 0, ba = ~0ull;
-        for (int q = 0; q < kThreads / 64; q++) { bo |= s_o[q]; ba &= s_a[q]; }
-        a.tile_orand[2 * tile] = bo;
-        a.tile_orand[2 * tile + 1] = ba;
+    if (lane == 0 && o != 0ull) {
+        atomicOr(a.orand, (unsigned long long)o);
+        atomicAnd(a.orand + 1, (unsigned long long)an);
     }
-    // the next tile's first row, in flight over the barrier (not over the candidate appends
-    // above: the row registers live across them spilled to scratch, and every scratch
-    // reload's vmcnt wait then also waited for the prefetch)
-    SKY_FILTER_FETCH((tile + gridDim.x) * kTile + threadIdx.x);
-    __syncthreads();                           // s_list / s_wc / s_o reused by the next tile
-    }
-#undef SKY_FILTER_FETCH
-#undef SKY_FILTER_FETCH_TO
     if (lflags) atomicOr(a.flags, lflags);
 }
 
@@ -664,34 +660,7 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *s_w, u
     return wb + inc - v;
 }
 
-__global__ __launch_bounds__(kThreads) void k_orand_reduce(const unsigned long long *__restrict__ part, uint32_t np,
-                                                           unsigned long long *__restrict__ orand) {
-    unsigned long long o = 0, an = ~0ull;
-    for (uint32_t q = blockIdx.x * kThreads + threadIdx.x; q < np; q += gridDim.x * kThreads) {
-        o |= part[2 * q];
-        an &= part[2 * q + 1];
-    }
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-        o |= __shfl_xor(o, s, 64);
-        an &= __shfl_xor(an, s, 64);
-    }
-    __shared__ unsigned long long s_o[kThreads / 64], s_a[kThreads / 64];
-    if ((threadIdx.x & 63) == 0) { s_o[threadIdx.x >> 6] = o; s_a[threadIdx.x >> 6] = an; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int q = 1; q < kThreads / 64; q++) { s_o[0] |= s_o[q]; s_a[0] &= s_a[q]; }
-        atomicOr(&orand[0], s_o[0]);
-        atomicAnd(&orand[1], s_a[0]);
-    }
-}
 
-void launch_orand_reduce(const unsigned long long *part, uint32_t np, unsigned long long *orand, hipStream_t st) {
-    if (!np) return;
-    unsigned g = (np + kThreads - 1) / kThreads;
-    if (g > 128) g = 128;
-    k_orand_reduce<<<g, kThreads, 0, st>>>(part, np, orand);
-}
 
 // One workgroup: every pruner that some tuple duplicates becomes one more candidate
 // slot (m + e) carrying that duplicate group; builds entries[e] = k*M+j and

@@ -68,7 +68,6 @@ struct FilterArgs {
     uint64_t *sortkey;
     uint32_t *slot_src;
     uint32_t *m_total;
-    unsigned long long *tile_orand;   // [tiles][2] per-tile {OR, AND} of the sort keys
     unsigned long long *orand;        // device {OR, AND} (deferred tuples add atomically)
     uint32_t *dup_cnt;            // [Kp*M]
     uint32_t *flags;              // kFlag*
@@ -86,7 +85,6 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
                            double *pruners, int32_t *npr, hipStream_t st);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
-void launch_orand_reduce(const unsigned long long *part, uint32_t np, unsigned long long *orand, hipStream_t st);
 struct AppendArgs {
     const double *pruners;        // [Kp][M][D]
     const uint32_t *dup_cnt;      // [Kp*M]
