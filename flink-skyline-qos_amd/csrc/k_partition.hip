@@ -362,7 +362,8 @@ __device__ __forceinline__ void count_dups(uint16_t code, int32_t k, int M, uint
 }
 
 template <int D>
-__device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_pr, int32_t *s_npr, uint32_t *s_dup) {
+__device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_pr, int32_t *s_npr, uint32_t *s_dup,
+                                                 int ndup_arrays = 1) {
     const int nprw = a.Kp * a.M;
     const int MD = a.M * D;
     for (int q = threadIdx.x; q < nprw * D; q += kThreads) {
@@ -370,7 +371,7 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
         s_pr[k * pr_stride<D>(a.M) + pr_off<D>(k, r / D, r % D)] = a.pruners[q];
     }
     for (int q = threadIdx.x; q < a.Kp; q += kThreads) s_npr[q] = a.npr[q];
-    for (int q = threadIdx.x; q < nprw; q += kThreads) s_dup[q] = 0;
+    for (int q = threadIdx.x; q < nprw * ndup_arrays; q += kThreads) s_dup[q] = 0;
     __syncthreads();
 }
 
@@ -392,6 +393,10 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
 //    occupancy their LDS image allows: the row-per-lane loads are not the limit.
 // Candidates (partition << 16 | offset) fill each wave's LDS list from the front,
 // deferred offsets from the back; the tile reserves its slots with one atomic.
+#ifndef SKY_FILTER_FT
+#define SKY_FILTER_FT 1           // output tiles per k_filter iteration (A/B builds)
+#endif
+constexpr int kFilterFT = SKY_FILTER_FT;
 #ifndef SKY_FILTER_PF2
 #define SKY_FILTER_PF2 0          // 1: two rows in flight per lane (A/B builds)
 #endif
@@ -400,19 +405,26 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
 #endif
 template <int D, bool GIVEN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8 ? SKY_FILTER_WPE : 1))) void k_filter(FilterArgs a) {
-    constexpr int kList = kItems * 64;                           // list entries per wave
-    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // pruner image (pr_stride), then [Kp*M] u32 dup counts
+    // one iteration = a span of kFilterFT output tiles (kFilterFT * 2048 tuples): one candidate
+    // reservation, one histogram flush and three barriers per span
+    constexpr int FT = kFilterFT;
+    constexpr int kSpan = FT * kTile;
+    constexpr int kSpanItems = FT * kItems;                      // items per thread per span
+    constexpr int kList = kSpanItems * 64;                       // list entries per wave
+    extern __shared__ __attribute__((aligned(16))) double s_pr[];   // pruner image (pr_stride), then [FT][Kp*M] u32 dup counts
     uint32_t *s_dup = reinterpret_cast<uint32_t *>(s_pr + (size_t)a.Kp * pr_stride<D>(a.M));
     __shared__ int32_t s_npr[kMaxK];
-    __shared__ uint32_t s_list[kTile];
+    __shared__ uint32_t s_list[kSpan];
     __shared__ uint32_t s_wc[kThreads / 64], s_wd[kThreads / 64], s_base, s_dbase;
-    load_pruners_lds<D>(a, s_pr, s_npr, s_dup);
+    load_pruners_lds<D>(a, s_pr, s_npr, s_dup, FT);
     uint32_t lflags = 0;
     uint64_t o = 0, an = ~0ull;                                  // OR / AND of the appended sort keys
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *wlist = s_list + __builtin_amdgcn_readfirstlane(wave) * kList;
     const uint32_t nl = a.n - 1;
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nspans = (a.n + kSpan - 1) / kSpan;
+    const int KM = a.Kp * a.M;
     double vn[D];                                                // the row of item r+1, in flight
     int32_t kn = 0;
 #define SKY_FILTER_FETCH_TO(I, VN, KN)                                                     \
@@ -434,14 +446,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #endif
     // a.tpb tiles per workgroup, interleaved over the grid (tile = t * grid + block): the
     // pruner image is loaded once per workgroup, not once per 2048 tuples
-    SKY_FILTER_FETCH(blockIdx.x * kTile + threadIdx.x);
+    SKY_FILTER_FETCH(blockIdx.x * kSpan + threadIdx.x);
 #pragma unroll 1
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t span = blockIdx.x; span < nspans; span += gridDim.x) {
     uint32_t wcnt = 0, dcnt = 0;
-    const uint32_t base = tile * kTile;
+    const uint32_t base = span * kSpan;
     uint16_t st_prev = 0;
 #pragma unroll 1
-    for (int r = 0; r < kItems; r++) {
+    for (int r = 0; r < kSpanItems; r++) {
         const uint32_t i = base + r * kThreads + threadIdx.x;
         const bool valid = i < a.n;
         double v[D];
@@ -453,9 +465,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #pragma unroll
         for (int d = 0; d < D; d++) vn[d] = vn2[d];
         kn = kn2;
-        SKY_FILTER_FETCH_TO(r + 2 < kItems ? i + 2 * kThreads : i, vn2, kn2);
+        SKY_FILTER_FETCH_TO(r + 2 < kSpanItems ? i + 2 * kThreads : i, vn2, kn2);
 #else
-        SKY_FILTER_FETCH(r + 1 < kItems ? i + kThreads : i);           // past the tile: a cache hit
+        SKY_FILTER_FETCH(r + 1 < kSpanItems ? i + kThreads : i);       // past the span: a cache hit
 #endif
         if (a.dbg) {                 // measurement only (SKY_FILTER_DBG=1): the stream without the work
             double acc = 0;
@@ -489,14 +501,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
             cand = code == kCodeCandidate;
             st = (uint16_t)(((uint32_t)k << 8) | code);
         }
-        count_dups((uint16_t)(st & 0xffu), (int32_t)(st >> 8), a.M, s_dup);
+        count_dups((uint16_t)(st & 0xffu), (int32_t)(st >> 8), a.M, s_dup + (FT > 1 ? (r / kItems) * KM : 0));
         const uint64_t cm = __ballot(cand);
         if (cand) wlist[wcnt + lanes_below(cm)] = ((uint32_t)k << 16) | (i - base);
         wcnt += (uint32_t)__popcll(cm);
         st_prev = st;
     }
     {
-        const uint32_t il = base + (kItems - 1) * kThreads + threadIdx.x;
+        const uint32_t il = base + (kSpanItems - 1) * kThreads + threadIdx.x;
         if (il < a.n && a.dbg < 2) a.status[il] = st_prev;
     }
     // the tile's candidates: ONE slot reservation per tile, then rows re-read (cache
@@ -514,10 +526,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     const uint32_t total = woff[kThreads / 64], dtotal = doff[kThreads / 64];
     // the tile's duplicate counts: into the per-tile histogram (the output count reads it
     // instead of the status words) and the per-(partition, pruner) totals
-    for (int q = threadIdx.x; q < a.Kp * a.M; q += kThreads) {
-        const uint32_t c = s_dup[q];
-        if (a.tile_hist) a.tile_hist[(size_t)tile * (a.Kp * a.M) + q] = c;
-        if (c) { atomicAdd(&a.dup_cnt[q], c); s_dup[q] = 0; }
+    for (int fq = threadIdx.x; fq < FT * KM; fq += kThreads) {
+        const int f = FT > 1 ? fq / KM : 0, q = fq - f * KM;
+        const uint32_t c = s_dup[fq];
+        const uint32_t tile = span * FT + f;
+        if (a.tile_hist && tile < ntiles) a.tile_hist[(size_t)tile * KM + q] = c;
+        if (c) { atomicAdd(&a.dup_cnt[q], c); s_dup[fq] = 0; }
     }
     if (threadIdx.x == 0) s_base = total ? atomicAdd(a.m_total, total) : 0u;
     if (threadIdx.x == 64 && dtotal) s_dbase = atomicAdd(a.defer_cnt, dtotal);
@@ -550,8 +564,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     // the next tile's first row, in flight over the barrier (not over the candidate appends
     // above: the row registers live across them spilled to scratch, and every scratch
     // reload's vmcnt wait then also waited for the prefetch)
-    SKY_FILTER_FETCH((tile + gridDim.x) * kTile + threadIdx.x);
-    __syncthreads();                           // s_list / s_wc reused by the next tile
+    SKY_FILTER_FETCH((span + gridDim.x) * kSpan + threadIdx.x);
+    __syncthreads();                           // s_list / s_wc reused by the next span
     }
 #undef SKY_FILTER_FETCH
 #undef SKY_FILTER_FETCH_TO
@@ -1448,14 +1462,15 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
-    const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
+    const size_t lds = (D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4) +
+                       (size_t)(kFilterFT - 1) * a.Kp * a.M * 4;   // one duplicate-count array per output tile of a span
     static const unsigned tpb = [] {           // tiles per workgroup (SKY_FILTER_TPB, A/B knob)
         const char *e = getenv("SKY_FILTER_TPB");   // 4: -4 % filter time vs 1 (2: -3 %, 8: -3 %)
         const int v = e ? atoi(e) : 4;
         return (unsigned)std::max(1, std::min(v, 64));
     }();
-    const unsigned tiles = nblk(a.n, kTile);
-    const unsigned g = (tiles + tpb - 1) / tpb;
+    const unsigned spans = nblk(a.n, kTile * kFilterFT);
+    const unsigned g = (spans + tpb - 1) / tpb;
     if (!g) return;
     if (a.given_keys) { SKY_DISPATCH_D(D, (k_filter<DD, true><<<g, kThreads, lds, st>>>(a))); }
     else { SKY_DISPATCH_D(D, (k_filter<DD, false><<<g, kThreads, lds, st>>>(a))); }
