@@ -871,10 +871,13 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const int64_t nl = h_nl;
     const int64_t nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
-    SKY_TRY(c->csv_lines.ensure((size_t)std::max<int64_t>(nl, 1) * 8));
+    // group boundaries only (R records per parse workgroup; R >= 8, and the exact path's groups of
+    // 256 need fewer): 8 bytes per group instead of per record
+    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
+    SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
     SKY_TRY(c->csv_status.ensure(nr1));
     c->ktimer_begin("csv_lines", c->st);
-    if (nl) launch_csv_nl_write(text, nbytes, blk_off, c->csv_lines.as<int64_t>(), c->st);
+    if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);
     c->ktimer_end("csv_lines", c->st, nbytes);
     const bool direct = cap >= nrec && d_ids_out && d_values_out;
     int64_t *pid = d_ids_out;
@@ -886,9 +889,12 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         pval = c->csv_vals.as<double>();
     }
     HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));   // [1..3] rejected per cause, [4] queued exact conversions
-    const unsigned long long slow_cap = 1u << 20;
+    // exact-conversion queue (SKY_CSV_SLOW_CAP: tests force the re-parse-everything path)
+    static const unsigned long long slow_cap = [] {
+        const char *e = getenv("SKY_CSV_SLOW_CAP");
+        return e ? (unsigned long long)std::max(1, atoi(e)) : (1ull << 20);
+    }();
     SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
-    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
     SKY_TRY(c->csv_keep.ensure((size_t)((nrec + R - 1) / R + 1) * 4));   // spill list of k_csv_fields
     HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
     c->ktimer_begin("csv_parse", c->st);
@@ -901,6 +907,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     HIP_TRY(hipStreamSynchronize(c->st));
     if (h_cnt[4] > slow_cap) {   // more exact conversions than the queue holds: re-parse every record exactly
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));
+        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, 256, c->csv_lines.as<int64_t>(), c->st);
         launch_csv_parse_exact(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval,
                                c->csv_status.as<uint8_t>(), d_cnt, c->st);
         HIP_TRY(hipGetLastError());

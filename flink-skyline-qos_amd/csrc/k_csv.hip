@@ -9,7 +9,8 @@
 // Passes (all HBM-streaming byte work, no MFMA):
 //   k_csv_nl_count  per 4 KB chunk: number of '\n' (16 B per lane, one vector load)
 //   scan            chunk offsets (k_scan.hip)
-//   k_csv_nl_write  positions of every '\n' -> line_end[] (record boundaries)
+//   k_csv_nl_groups positions of every R-th '\n' -> line_g[] (group boundaries, R records per
+//                   parse workgroup; the fallback finds a group's records itself)
 //   k_csv_parse     one lane per record; the workgroup's 256 records are first staged
 //                   into LDS with coalesced dword loads, then each lane walks its record:
 //                   split semantics, Java trim, the Double.parseDouble grammar, the value
@@ -85,9 +86,14 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__r
     }
 }
 
-__global__ __launch_bounds__(kCsvThreads) void k_csv_nl_write(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                              bool aligned, const uint32_t *__restrict__ blk_off,
-                                                              int64_t *__restrict__ line_end) {
+
+// Only the group boundaries: the position of every newline whose index g (in the text) ends a
+// group of R records ((g + 1) % R == 0) -> line_g[(g + 1) / R - 1].  The parse workgroups need
+// only their group's first and last byte; a record-per-newline array (8 bytes per record,
+// 0.8 GB at 100M records) was written and read for nothing else.
+__global__ __launch_bounds__(kCsvThreads) void k_csv_nl_groups(const uint8_t *__restrict__ text, int64_t nbytes,
+                                                               bool aligned, const uint32_t *__restrict__ blk_off,
+                                                               uint32_t R, int64_t *__restrict__ line_g) {
     __shared__ uint32_t s_w[kCsvThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * kCsvChunk + threadIdx.x * 16;
     uint32_t w[4], m[4];
@@ -104,15 +110,23 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_write(const uint8_t *__r
     }
     if (lane == 63) s_w[wv] = inc;
     __syncthreads();
-    uint32_t off = blk_off[blockIdx.x] + inc - c;
-    for (int i = 0; i < wv; i++) off += s_w[i];
+    uint32_t g0 = blk_off[blockIdx.x] + inc - c;          // index of this thread's first newline
+    for (int i = 0; i < wv; i++) g0 += s_w[i];
+    if (!c) return;
+    // group ends q = (j + 1) R - 1 within [g0, g0 + c): one division per thread, at most
+    // two ends (c <= 16, R >= 8), each located by skipping q - g0 newlines
+    for (uint32_t q = (g0 / R + 1) * R - 1; q < g0 + c; q += R) {
+        uint32_t t = q - g0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        uint32_t mk = m[k];
-        while (mk) {
-            const int bit = __ffs(mk) - 1;
-            mk &= mk - 1;
-            line_end[off++] = base + k * 4 + (bit >> 3);
+        for (int k = 0; k < 4; k++) {
+            const uint32_t ck = __popc(m[k]);
+            if (t < ck) {
+                uint32_t mk = m[k];
+                for (uint32_t u = 0; u < t; u++) mk &= mk - 1;
+                line_g[(q + 1) / R - 1] = base + k * 4 + ((__ffs(mk) - 1) >> 3);
+                break;
+            }
+            t -= ck;
         }
     }
 }
@@ -555,7 +569,7 @@ __device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, i
 }
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                            const int64_t *__restrict__ line_end, int64_t nl,
+                                                            const int64_t *__restrict__ line_g, int64_t nl,
                                                             int64_t nrec, int D, int64_t *__restrict__ ids,
                                                             double *__restrict__ vals, uint8_t *__restrict__ status,
                                                             unsigned long long *__restrict__ counts,
@@ -573,9 +587,11 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     const int64_t r0 = (int64_t)blockIdx.x * R;             // R <= 256 records per workgroup (host-chosen)
     const int nr = (int)(nrec - r0 < R ? nrec - r0 : R);
     const int64_t rl = r0 + nr - 1;
-    const int64_t span_s = r0 == 0 ? 0 : line_end[r0 - 1] + 1;
+    // group boundaries (k_csv_nl_groups): the last group ends at the end of the text (its last
+    // record has no '\n', or its '\n' is the last byte)
+    const int64_t span_s = r0 == 0 ? 0 : line_g[blockIdx.x - 1] + 1;
     const bool tail_open = rl >= nl;                       // last record has no '\n'
-    const int64_t span_e = tail_open ? nbytes : line_end[rl] + 1;   // includes the final '\n'
+    const int64_t span_e = tail_open || nr < R ? nbytes : line_g[blockIdx.x] + 1;   // includes the final '\n'
     const int64_t a0 = span_s & ~15ll;
     if (span_e - a0 > kFieldText) {                        // uniform per block
         if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
@@ -763,26 +779,80 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_slow(const uint8_t *__restr
     }
 }
 
-// ---- fallback: the workgroups k_csv_fields listed (very long records), lane per record from HBM
+// ---- fallback: the workgroups k_csv_fields listed (very long records), lane per record from HBM.
+// The group's records are found here: the workgroup scans its span (group boundaries from
+// k_csv_nl_groups) 4 KB at a time for newlines, numbering them by a block scan.
 __global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                             const int64_t *__restrict__ line_end, int64_t nl,
+                                                             const int64_t *__restrict__ line_g, int64_t nl,
                                                              int64_t nrec, int D, int64_t *__restrict__ ids,
                                                              double *__restrict__ vals, uint8_t *__restrict__ status,
                                                              unsigned long long *__restrict__ counts,
                                                              const uint32_t *__restrict__ spill, int64_t all_blocks,
                                                              int R) {
+    __shared__ int64_t s_end[kCsvThreads];                 // record j of the group ends at s_end[j] ('\n')
+    __shared__ uint32_t s_w[kCsvThreads / 64];
     const int64_t nlist = all_blocks ? all_blocks : (int64_t)spill[0];
+    const bool aligned = ((uintptr_t)text & 15) == 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int64_t li = blockIdx.x; li < nlist; li += gridDim.x) {
-        if ((int)threadIdx.x >= R) continue;
-        const int64_t r = (all_blocks ? li : (int64_t)spill[1 + li]) * R + threadIdx.x;
-        if (r >= nrec) continue;
-        const int64_t s = r == 0 ? 0 : line_end[r - 1] + 1;
-        const int64_t e = r < nl ? line_end[r] : nbytes;
-        int64_t id = 0;
-        const uint8_t st = parse_record(GlbSrc{text, 0}, s, e, D, id, vals + r * D);
-        ids[r] = id;
-        status[r] = st;
-        if (st != SKY_CSV_OK) atomicAdd(&counts[st], 1ull);
+        const int64_t b = all_blocks ? li : (int64_t)spill[1 + li];
+        const int64_t r0 = b * R;
+        const int nr = (int)(nrec - r0 < R ? nrec - r0 : R);
+        const int64_t span_s = r0 == 0 ? 0 : line_g[b - 1] + 1;
+        const bool tail_open = r0 + nr - 1 >= nl;
+        const int64_t span_e = tail_open || nr < R ? nbytes : line_g[b] + 1;
+        uint32_t found = 0;                                // workgroup-uniform
+        for (int64_t a = span_s & ~15ll; a < span_e && found < (uint32_t)nr; a += kCsvChunk) {
+            const int64_t base = a + threadIdx.x * 16;
+            uint32_t w[4], m[4], c = 0;
+            load16(text, nbytes, base, aligned, w);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                m[k] = nl_in_word(w[k]);
+                for (int t = 0; t < 4; t++) {              // only the span's bytes
+                    const int64_t p = base + 4 * k + t;
+                    if (p < span_s || p >= span_e) m[k] &= ~(0x80u << (8 * t));
+                }
+                c += __popc(m[k]);
+            }
+            uint32_t inc = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += t;
+            }
+            if (lane == 63) s_w[wv] = inc;
+            __syncthreads();
+            uint32_t idx = found + inc - c, tot = 0;
+            for (int i = 0; i < kCsvThreads / 64; i++) {
+                if (i < wv) idx += s_w[i];
+                tot += s_w[i];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t mk = m[k];
+                while (mk) {
+                    const int bit = __ffs(mk) - 1;
+                    mk &= mk - 1;
+                    if (idx < (uint32_t)nr) s_end[idx] = base + k * 4 + (bit >> 3);
+                    idx++;
+                }
+            }
+            found += tot;
+            __syncthreads();                               // s_w reused by the next step
+        }
+        if ((int)threadIdx.x < nr) {
+            const int j = threadIdx.x;
+            const int64_t r = r0 + j;
+            const int64_t s = j == 0 ? span_s : s_end[j - 1] + 1;
+            const int64_t e = (uint32_t)j < found ? s_end[j] : nbytes;   // the tail record has no '\n'
+            int64_t id = 0;
+            const uint8_t st = parse_record(GlbSrc{text, 0}, s, e, D, id, vals + r * D);
+            ids[r] = id;
+            status[r] = st;
+            if (st != SKY_CSV_OK) atomicAdd(&counts[st], 1ull);
+        }
+        __syncthreads();                                   // s_end reused by the next group
     }
 }
 
@@ -887,12 +957,12 @@ void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt,
     const bool aligned = ((uintptr_t)text & 15) == 0;
     k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt, ncomma);
 }
-void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
-                         hipStream_t st) {
+void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
+                          hipStream_t st) {
     const int64_t nb = csv_chunks(nbytes);
     if (nb == 0) return;
     const bool aligned = ((uintptr_t)text & 15) == 0;
-    k_csv_nl_write<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_off, line_end);
+    k_csv_nl_groups<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_off, (uint32_t)R, line_g);
 }
 static int csv_stop() {
     const char *e = getenv("SKY_CSV_STOP");
@@ -901,26 +971,26 @@ static int csv_stop() {
 // spill: device u32 [1 + blocks], spill[0] zeroed by the caller; slow: queue of exact
 // conversions (slow_n zeroed by the caller).  If *slow_n ends above slow_cap the caller
 // re-parses everything with launch_csv_parse_exact.
-void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
+void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec, int D,
                       int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
                       longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, int R,
                       hipStream_t st) {
     if (nrec == 0) return;
     const int64_t nb = (nrec + R - 1) / R;
-    k_csv_fields<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts,
+    k_csv_fields<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts,
                                                       spill, slow, slow_n, slow_cap, R, csv_stop());
     const unsigned g = (unsigned)(nb < 1024 ? nb : 1024);
-    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, spill, 0,
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts, spill, 0,
                                              R);
     k_csv_slow<<<1024, kCsvThreads, 0, st>>>(text, slow, slow_n, slow_cap, vals);
 }
-void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
+void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec,
                             int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
                             hipStream_t st) {
     if (nrec == 0) return;
     const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
     const unsigned g = (unsigned)(nb < 4096 ? nb : 4096);
-    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_end, nl, nrec, D, ids, vals, status, counts, nullptr,
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts, nullptr,
                                              nb, kCsvThreads);
 }
 // records per k_csv_fields workgroup: as many as fit the LDS windows at the stream's average

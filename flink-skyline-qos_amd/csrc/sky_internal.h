@@ -336,13 +336,15 @@ void synth_host(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0,
 int64_t csv_chunks(int64_t nbytes);
 void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, unsigned long long *ncomma,
                          hipStream_t st);
-void launch_csv_nl_write(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int64_t *line_end,
-                         hipStream_t st);
-void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec, int D,
+// positions of the newlines that end groups of R records: line_g[g] = end of group g
+void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
+                          hipStream_t st);
+void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec, int D,
                       int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
                       longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, int R,
                       hipStream_t st);
-void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_end, int64_t nl, int64_t nrec,
+// line_g: group boundaries for groups of 256 (kCsvThreads) records
+void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec,
                             int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
                             hipStream_t st);
 int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields);

@@ -119,6 +119,40 @@ def test_csv_long_records_and_numbers(gpu_engine_factory, oracle):
     eng.close()
 
 
+def test_csv_exact_reparse_path():
+    """More exact conversions than the queue holds: every record is re-parsed on the exact
+    path (groups of 256 records, boundaries found by the fallback workgroups).  The queue
+    size is read once per process, so this runs in a child process with a 4-entry queue."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = r"""
+import random, sys
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import skyline
+from conftest import Oracle
+from test_gpu_csv import _check
+rng = random.Random(5)
+lines = []
+for i in range(3000):
+    vals = []
+    for _ in range(2):
+        nd = rng.choice([3, 25, 40])
+        d = str(rng.randrange(1, 10)) + "".join(rng.choice("0123456789") for _ in range(nd - 1))
+        vals.append(d[:1] + "." + d[1:] + "e%%d" %% rng.randrange(-30, 30))
+    lines.append(("%%d," %% i) + ",".join(vals) if i %% 97 else "bad,1,2")
+text = ("\n".join(lines) + "\n").encode()
+eng = skyline.SkylineEngine(2, 8, "mr-angle", 1000.0, 0)
+_check(eng, Oracle(), text, 2)
+_check(eng, Oracle(), text[:-1], 2)          # tail record without a newline
+print("ok")
+""" % (os.path.join(os.path.dirname(here), "flink-skyline-qos_amd"), here)
+    env = dict(os.environ, SKY_CSV_SLOW_CAP="4")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_csv_halfway_values(gpu_engine_factory, oracle):
     from fractions import Fraction
     rng = random.Random(9)
