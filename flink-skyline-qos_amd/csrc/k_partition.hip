@@ -1478,7 +1478,11 @@ void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
 
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
-    SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<256, kThreads, lds, st>>>(a)));
+    static const unsigned dgrid = [] {        // SKY_DEFER_WG: workgroups of the deferred-key pass (A/B knob)
+        const char *e = getenv("SKY_DEFER_WG");
+        return e ? (unsigned)std::max(1, atoi(e)) : 256u;
+    }();
+    SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<dgrid, kThreads, lds, st>>>(a)));
 }
 
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
