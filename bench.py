@@ -88,10 +88,16 @@ def filter_roofline(eng, D, kt=None):
 
 
 def traffic_for(n, D, dist_name):
+    """HBM bytes per k_filter launch from the PMC passes (tools/gpu_pmc.sh: FETCH_SIZE and
+    WRITE_SIZE in separate rocprofv3 runs, gfx950 correction), reported only when they were
+    measured on THIS build (hash of k_filter's sources) and workload; else None."""
     tf = os.path.join(REPO, "profiles", "traffic_filter.json")
     try:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from src_hash import kernel_src_sha
         tj = json.load(open(tf))
-        if tj.get("n") == n and tj.get("dims") == D and tj.get("dist") == dist_name:
+        if (tj.get("n") == n and tj.get("dims") == D and tj.get("dist") == dist_name and
+                tj.get("kernel_src_sha") == kernel_src_sha("k_filter")):
             return tj.get("hbm_bytes_per_launch")
     except Exception:
         pass
@@ -534,6 +540,23 @@ def sort_run(eng, n, dev, steps=3):
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` (N > 1) run directly: start N rank processes through
+    torch.distributed.run as a CHILD process (this parent never initialises the GPU and never
+    exec()s) with the same arguments, and return its exit status.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -553,24 +576,34 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C3 sub-lines")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (H2D inside) C4 rates")
     ap.add_argument("--no-operator", action="store_true", help="skip the per-key operator-path companion")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL over xGMI, the measured path) or gloo (rehearsing ranks on one GPU)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the measured path), gloo (rehearsing several ranks on one "
+                         "GPU), auto: nccl when every rank has a GPU of its own")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks from here, before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    dev_index = local_rank % max(torch.cuda.device_count(), 1)   # > 1 rank per GPU only with gloo
+    n_dev = max(torch.cuda.device_count(), 1)
+    backend = args.dist_backend
+    if backend == "auto":
+        backend = "nccl" if n_dev >= world else "gloo"
+    dev_index = local_rank % n_dev   # > 1 rank per GPU only when rehearsing with gloo
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dist_backend == "nccl":
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
-    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     if args.config == "C5":
         if rank == 0:
@@ -671,7 +704,10 @@ def main():
             "config": {"workload": cfg["workload"], "tuples_per_gpu": n, "tuples_total": total, "dims": D,
                        "partitions": P, "algo": cfg["algo"], "dist": cfg["dist"], "domain": [0, 1000],
                        "seed": seed, "compare_dtype": "f32 / packed u16 when the values are exact",
-                       "parallelism": f"shards{world}", "skyline_size": g},
+                       "parallelism": f"shards{world}", "skyline_size": g,
+                       "transport": (None if world == 1 else
+                                     "RCCL over xGMI (nccl)" if backend == "nccl" else
+                                     f"gloo rehearsal: {world} ranks on {min(n_dev, world)} GPU(s)")},
             "roofline": roof,
             "phases_ms_last_step": phases,
             "counters_last_step": {"n": int(counters[0]), "candidates": int(counters[1]),

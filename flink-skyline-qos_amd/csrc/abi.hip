@@ -1,6 +1,6 @@
 // abi.hip — extern "C" entry points of libskyline_hip.so (include/skyline_hip.h).
 // Status codes only; no exception crosses the boundary.
-#include "ctx.h"
+#include "abi_common.h"
 
 #include <cstring>
 #include <new>
@@ -12,59 +12,6 @@ void set_error(const std::string &m) { g_err = m; }
 }  // namespace sky
 
 using namespace sky;
-
-#define HIP_TRY(expr)                                                                     \
-    do {                                                                                  \
-        hipError_t e_ = (expr);                                                           \
-        if (e_ != hipSuccess) {                                                           \
-            set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #expr);   \
-            return SKY_E_HIP;                                                             \
-        }                                                                                 \
-    } while (0)
-#define SKY_TRY(expr)                \
-    do {                             \
-        int r_ = (expr);             \
-        if (r_ != SKY_OK) return r_; \
-    } while (0)
-#define ARG_CHECK(cond, msg)          \
-    do {                              \
-        if (!(cond)) {                \
-            set_error(msg);           \
-            return SKY_E_ARG;         \
-        }                             \
-    } while (0)
-#define GUARD_BEGIN try {
-#define GUARD_END                                             \
-    }                                                         \
-    catch (const std::bad_alloc &) {                          \
-        set_error("host allocation failed");                  \
-        return SKY_E_NOMEM;                                   \
-    }                                                         \
-    catch (...) {                                             \
-        set_error("internal error");                          \
-        return SKY_E_HIP;                                     \
-    }
-
-static int bind(sky_ctx *c) {
-    // hipGetLastError() is per thread and sticky: drop whatever another library
-    // (e.g. torch) left behind so our launch checks only see our own failures
-    (void)hipGetLastError();
-    HIP_TRY(hipSetDevice(c->dev));
-    return SKY_OK;
-}
-
-static void finish_profile(sky_ctx *c) {
-    if (!c->profile) return;
-    hipStreamSynchronize(c->st);
-    for (int i = 0; i < SKY_PHASES; i++) {
-        float ms = 0;
-        c->phase_ms[i] = 0;
-        if (c->pt.marked[i] && c->pt.marked[i + 1] &&
-            hipEventElapsedTime(&ms, c->pt.ev[i], c->pt.ev[i + 1]) == hipSuccess)
-            c->phase_ms[i] = ms;
-    }
-    c->ktimer_collect();
-}
 
 static void store_stats(sky_ctx *c, const Pipe &p) {
     c->K_last = p.K;
@@ -331,11 +278,13 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
 }
 
 int sky_global_stats_set(sky_ctx *c, int32_t k, const int64_t *local_sizes, const int64_t *survivors) {
+    GUARD_BEGIN
     ARG_CHECK(c && k >= 0 && k <= 65536 && (k == 0 || (local_sizes && survivors)), "bad arguments");
     c->K_last = k;
     c->lsz.assign(local_sizes, local_sizes + k);
     c->surv.assign(survivors, survivors + k);
     return SKY_OK;
+    GUARD_END
 }
 
 int sky_global_stats(sky_ctx *c, int64_t *local_sizes, int64_t *survivors, int32_t *k_out) {
@@ -602,149 +551,6 @@ int sky_part_snapshot(sky_part *p, int64_t *ids_out, double *values_out, int64_t
         HIP_TRY(hipMemcpyAsync(values_out, p->out_rows.p, (size_t)p->T * D * 8, hipMemcpyDeviceToHost, c->st));
     }
     HIP_TRY(hipStreamSynchronize(c->st));
-    return SKY_OK;
-    GUARD_END
-}
-
-// ---- multi-GPU phases ---------------------------------------------------------------
-int sky_export_local_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int64_t n, int64_t *n_out) {
-    GUARD_BEGIN
-    ARG_CHECK(c && (n == 0 || d_values) && n_out, "null argument");
-    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
-    SKY_TRY(bind(c));
-    PipeIn in;
-    in.vals = d_values;
-    in.n = (uint32_t)n;
-    in.ids = d_ids;
-    in.global = false;
-    in.fate = false;
-    in.K = c->Kq();
-    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
-    Pipe &p = c->main;
-    // multiplicity of every representative + export order among the alive ones
-    SKY_TRY(p.mult.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 8));
-    SKY_TRY(p.alive_u32.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 4));
-    SKY_TRY(p.alive_scan.ensure((size_t)std::max<uint32_t>(p.mr, 1) * 4));
-    SKY_TRY(p.scratch.ensure(scan_scratch_words(p.mr + 1) * 4 + 64));
-    uint32_t ne = 0;
-    if (p.mr) {
-        HIP_TRY(hipMemsetAsync(p.mult.p, 0, (size_t)p.mr * 8, c->st));
-        const uint32_t *perm = nullptr;
-        // the sorted permutation lives in perm or val_alt; rep_of_sorted/slot_rep are per sorted position / slot,
-        // so weigh every slot once through slot_rep instead
-        (void)perm;
-        launch_flag_u8_to_u32(p.alive_l.as<uint8_t>(), p.mr, p.alive_u32.as<uint32_t>(), c->st);
-        scan_excl_u32(p.alive_u32.as<uint32_t>(), p.alive_scan.as<uint32_t>(), p.mr, p.totals.as<uint32_t>() + 4,
-                      p.scratch.as<uint32_t>(), c->st);
-        SKY_TRY(p.perm.ensure((size_t)p.mt * 4));
-        launch_iota(p.perm.as<uint32_t>(), p.mt, c->st);   // identity: slot order
-        launch_rep_mult(p.mt, p.perm.as<uint32_t>(), p.s_src->as<uint32_t>(), p.slot_rep.as<uint32_t>(),
-                        in.weights, p.dup_cnt.as<uint32_t>(), p.pr_entries.as<int32_t>(),
-                        p.mult.as<unsigned long long>(), c->st);
-        SKY_TRY(p.pinned(64));
-        HIP_TRY(hipMemcpyAsync(p.pin, p.totals.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, c->st));
-        HIP_TRY(hipStreamSynchronize(c->st));
-        p.up_used = 0;
-        ne = *(volatile uint32_t *)p.pin;
-    }
-    c->shard = in;
-    c->shard_valid = true;
-    c->counters[0] = p.n;
-    c->counters[1] = p.m;
-    c->counters[2] = p.mr;
-    *n_out = ne;
-    c->counters[3] = ne;
-    return SKY_OK;
-    GUARD_END
-}
-
-int sky_export_copy_dev(sky_ctx *c, double *d_rows_out, int32_t *d_keys_out, int64_t *d_mult_out, int64_t cap) {
-    GUARD_BEGIN
-    ARG_CHECK(c && c->shard_valid, "call sky_export_local_dev first");
-    ARG_CHECK(cap >= c->counters[3], "export capacity too small");
-    SKY_TRY(bind(c));
-    Pipe &p = c->main;
-    launch_export_reps(c->D, p.f64, p.mr, p.rep_rows.p, p.rep_key.as<uint64_t>(), p.alive_l.as<uint8_t>(),
-                       p.alive_scan.as<uint32_t>(), p.mult.as<unsigned long long>(), d_rows_out, d_keys_out,
-                       d_mult_out, c->st);
-    HIP_TRY(hipGetLastError());
-    return SKY_OK;
-    GUARD_END
-}
-
-int sky_import_union_dev(sky_ctx *c, const double *d_rows, const int32_t *d_keys, const int64_t *d_mult,
-                         int64_t n_union, int64_t self_offset, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
-                         int64_t *n_out) {
-    GUARD_BEGIN
-    ARG_CHECK(c && c->shard_valid, "call sky_export_local_dev first");
-    ARG_CHECK(n_union >= 0 && n_union < (int64_t)0x7fffffffLL, "n_union out of range");
-    ARG_CHECK(self_offset >= 0 && self_offset + c->counters[3] <= n_union, "self_offset out of range");
-    ARG_CHECK(n_union == 0 || (d_rows && d_keys && d_mult), "null union buffers");
-    SKY_TRY(bind(c));
-    Pipe &p = c->main;
-    const uint32_t n_own = (uint32_t)c->counters[3];
-    const int K = c->Kq();
-    // this rank's own vectors against the union: flags + this rank's share of |L_k| / survivors_k
-    SKY_TRY(c->h_flags.ensure((size_t)std::max<int64_t>(n_union, 1)));
-    SKY_TRY(p.statk.ensure((size_t)K * 16));
-    unsigned long long *d_lsz = p.statk.as<unsigned long long>(), *d_surv = d_lsz + K;
-    HIP_TRY(hipMemsetAsync(d_lsz, 0, (size_t)K * 16, c->st));
-    c->ktimer_begin("union_fate", c->st);
-    launch_union_fate(c->D, d_rows, d_keys, d_mult, (uint32_t)n_union, (uint32_t)self_offset, n_own, K,
-                      c->h_flags.as<uint8_t>(), d_lsz, d_surv, c->st);
-    c->ktimer_end("union_fate", c->st, (int64_t)n_own * n_union);
-    HIP_TRY(hipGetLastError());
-    launch_import_flags(p.alive_l.as<uint8_t>(), p.alive_scan.as<uint32_t>(), p.mr, c->h_flags.as<uint8_t>(),
-                        (uint32_t)self_offset, p.alive_g.as<uint8_t>(), c->st);
-    // recount this shard's output with the imported global fates
-    const uint32_t tiles = (p.n + kTile - 1) / kTile;
-    // the export ran without a fate pass: size the per-tile count buffers here
-    SKY_TRY(p.out_cnt.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
-    SKY_TRY(p.out_off.ensure((size_t)std::max<uint32_t>(tiles, 1) * 4));
-    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
-    FateArgs fta{};
-    fta.mt = p.mt;
-    fta.slot_rep = p.slot_rep.as<uint32_t>();
-    fta.slot_src = p.s_src->as<uint32_t>();
-    fta.alive_l = p.alive_l.as<uint8_t>();
-    fta.alive_g = p.alive_g.as<uint8_t>();
-    fta.KM = p.Kp * p.M;
-    fta.M = p.M;
-    fta.K = p.K;
-    fta.pruner_slot = p.pruner_slot.as<int32_t>();
-    fta.status = p.status.as<uint16_t>();
-    fta.pruner_fate = p.pruner_fate.as<uint8_t>();
-    launch_fate_tables(fta, c->st);             // no stats: the union kernel summed this rank's share
-    OutArgs oa{};
-    oa.status = p.status.as<uint16_t>();
-    oa.n = p.n;
-    oa.pruner_fate = p.pruner_fate.as<uint8_t>();
-    oa.M = p.M;
-    oa.KM = p.Kp * p.M;
-    oa.K = p.K;
-    oa.out_cnt = p.out_cnt.as<uint32_t>();
-    if (p.n) {
-        launch_out_count(oa, c->st);
-        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                      p.scratch.as<uint32_t>(), c->st);
-    }
-    // one read-back: the output count and the K-sized stat shares
-    SKY_TRY(p.pinned((size_t)K * 16 + 64));
-    HIP_TRY(hipMemcpyAsync(p.pin, d_lsz, (size_t)K * 16, hipMemcpyDeviceToHost, c->st));
-    if (p.n)
-        HIP_TRY(hipMemcpyAsync((char *)p.pin + (size_t)K * 16, p.totals.as<uint32_t>() + 3, 4, hipMemcpyDeviceToHost,
-                               c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));
-    p.up_used = 0;
-    const unsigned long long *hs = (const unsigned long long *)p.pin;
-    p.nout = p.n ? *(const uint32_t *)((const char *)p.pin + (size_t)K * 16) : 0;
-    c->K_last = K;
-    c->lsz.assign(hs, hs + K);
-    c->surv.assign(hs + K, hs + 2 * K);
-    c->counters[4] = p.nout;
-    SKY_TRY(pipe_output(*c, p, c->shard, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr));
-    HIP_TRY(hipGetLastError());
-    finish_profile(c);
     return SKY_OK;
     GUARD_END
 }

@@ -62,7 +62,17 @@ struct Ctx {
     // multi-GPU phase-1 state (the shard stays caller-owned)
     PipeIn shard;
     bool shard_valid = false;
-    DevBuf exp_scan;
+    // the one-read multi-GPU step (sky_dist_*): 0 none, 1 exported, 2 exported with a NaN (the
+    // block carries the verdict, the merge only completes the collective pattern), 3 merged
+    int dist_state = 0;
+    int64_t dist_cap = 0;
+    int64_t dist_hist_pairs = -1;   // |own| x |union| of the last merge (-1: none yet)
+    int dist_last_route = 0;        // 0: one pair kernel over the blocks, 1: the bounding-box pass
+    int dist_world = 0;
+    bool dist_merged = false;
+    int64_t host_syncs = 0;     // entry-point level host synchronisations (pipelines count their own)
+    DevBuf dist_sum;            // the merge's summary of every block header (u64 words)
+    DevBuf dist_union, dist_ukey, dist_umult, dist_uflags;   // the compacted union (bounding-box path)
     // bulk CSV ingest workspace (k_csv.hip)
     DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow;
     DevBuf prof_k, prof_v, prof_scr;   // sky_profile_sort_dev workspace

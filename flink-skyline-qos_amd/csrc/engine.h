@@ -43,6 +43,9 @@ struct PipeIn {
     bool single = false;            // one partition (global merge of lists, local state insert)
     bool global = true;             // run the global merge after the local skylines
     bool fate = true;               // per-tuple fate pass (stats, output counts)
+    bool dist = false;              // multi-GPU export (sky_dist_export_dev): local skylines only, the
+                                    // small-set / planned routes allowed, the run's checks deferred to a
+                                    // device verdict (no host read at the end of the run)
     int K = 1;                      // stats slots
     // optional: the global skyline's stream-ordered ids / origins, written by the run itself
     // (single-pass output) when the stats come from the slots; pipe_output then only checks
@@ -105,6 +108,14 @@ struct Pipe {
     bool fused = false;
     const int64_t *fused_ids = nullptr;
     const int32_t *fused_org = nullptr;
+    // multi-GPU step (sky_dist_*): what the export left for the merge
+    DevBuf dverd;                         // u64 words: [0] the run's verdict, [8..15] the merge's summary
+    DevBuf dist_flag, dist_pos, dist_own; // per unit: alive (u32), export position; per own row: fates
+    bool dist_slots = false;              // units = candidate slots (small-set route) or representatives
+    uint32_t dist_n = 0;                  // units (their bound on the planned route)
+    const uint32_t *dist_d_n = nullptr;   // the unit count on the device (planned route)
+    PlanCheck dist_pc;
+    int64_t host_syncs = 0;               // host synchronisations (read-backs) of this pipeline
     // host-visible pinned staging
     void *pin = nullptr;
     size_t pin_cap = 0;
@@ -134,6 +145,9 @@ struct Pipe {
 
 struct Ctx;
 int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
+// read device ranges into host memory in one synchronisation (one gather launch when they are small)
+int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
+              std::vector<void *> dsts);
 // stream-ordered output of the tuples selected by the last run
 int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,
                 double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags);

@@ -82,6 +82,7 @@ int Pipe::upload(void *dst, const void *src, size_t bytes, hipStream_t st) {
     const size_t need = (bytes + 255) & ~size_t(255);
     if (up_used + need > up_cap) {
         // wrap: every earlier upload must have been consumed before the area is reused
+        host_syncs++;
         if (hipStreamSynchronize(st) != hipSuccess) {
             set_error("stream synchronisation failed");
             return SKY_E_HIP;
@@ -352,6 +353,7 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
         STAGE(st, "act_compact");
         SKY_TRY(p.pinned(nseg * 4));
         HIP_TRY(hipMemcpyAsync(p.pin, p.segcnt.p, nseg * 4, hipMemcpyDeviceToHost, st));
+        p.host_syncs++;
         HIP_TRY(hipStreamSynchronize(st));
         p.up_used = 0;
         const uint32_t *sc = (const uint32_t *)p.pin;
@@ -366,8 +368,6 @@ static int sfs_run(Ctx &c, Pipe &p, const void *rows, const uint64_t *key, uint3
     return SKY_OK;
 }
 
-static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
-                     std::vector<void *> dsts);
 // ---- segmented SFS for integer-valued rows (k_dom16.hip) ---------------------------
 // rows16: packed rows by position; segments [begin[k], begin[k]+cnt[k]) sorted by a
 // strictly monotone score.  alive[position of round 0] = 1 for skyline members.
@@ -544,8 +544,9 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
     return SKY_OK;
 }
 
-static int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
-                     std::vector<void *> dsts) {
+int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
+              std::vector<void *> dsts) {
+    p.host_syncs++;
     size_t tot = 0;
     for (auto &s : srcs) tot += (s.second + 15) & ~size_t(15);
     SKY_TRY(p.pinned(tot));
@@ -668,9 +669,41 @@ struct PlanRun {
     const uint32_t *d_cnt = nullptr;  // slots entering the brute pass (device)
     bool k_u16 = false, k_f32 = false;   // the brute pass's compare type
 };
+// The end of a multi-GPU export run (in.dist): nothing is read back.  The route's checks (the
+// planned route's assumptions, NaN, a look-back's spin bound) become a device verdict that the
+// export writes into its block header; the fates of this shard's units follow the union merge.
+static int dist_finish_run(Ctx &c, Pipe &p, PhaseTimer *tm, bool brute, uint32_t mt, const PlanRun *pr) {
+    hipStream_t st = c.st;
+    SKY_TRY(p.dverd.ensure(128));
+    PlanCheck pc{};
+    if (pr) {
+        pc.planned = 1;
+        pc.cap = (uint32_t)pr->cap;
+        pc.rounds = p.plan.rounds;
+        for (int r = 0; r <= p.plan.rounds && r < 4; r++) pc.bound[r] = p.plan.bound[r];
+        pc.brute_max = kBruteMax;
+        pc.k_u16 = pr->k_u16 ? 1 : 0;
+        pc.k_f32 = pr->k_f32 ? 1 : 0;
+    }
+    launch_plan_verdict(p.totals.as<uint32_t>(), p.flags.as<uint32_t>(), pc, p.dverd.as<uint32_t>(), st);
+    p.dist_pc = pc;
+    p.dist_slots = brute;
+    p.dist_n = brute ? mt : p.mr;
+    p.dist_d_n = brute && pr ? pr->d_cnt : nullptr;
+    if (brute) p.mr = p.mt = mt;        // slots (on the planned route: their bound)
+    p.mg = 0;
+    p.nout = 0;
+    if (tm) {
+        tm->mark(7, st);
+        tm->mark(8, st);
+    }
+    return stage_check(st, "dist export");
+}
+
 static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSet &fill, bool brute, uint32_t mt,
                        uint32_t tiles, const PlanRun *pr) {
     hipStream_t st = c.st;
+    if (in.dist) return dist_finish_run(c, p, tm, brute, mt, pr);
     const uint32_t n = in.n;
     const int KM = p.Kp * p.M;
     // stats: summed over slots (unit weights, computed origins) or, for given origins /
@@ -993,6 +1026,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
     p.fused = false;
     p.used_mbr = false;
+    p.mbr_tiles = 0;
     p.sfs_rounds = p.sfs_pairs_upper = 0;
     p.h_seg_n.clear();
     p.h_seg_s.clear();
@@ -1045,14 +1079,15 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);   // per-slot sample minima start all-ones
     // output counts from per-tile duplicate histograms (unit weights, stats over slots, the
     // single-pass output's buffers): the filter keeps them, the fate pass counts candidates
-    p.hist_count = in.fate && !in.origin && !in.weights && (in.out_ids || in.out_org) && !fused_disabled() &&
-                   !fused_onepass() && KM <= kHistMaxKM && !hist_disabled();
+    p.hist_count = ((in.fate && (in.out_ids || in.out_org)) || in.dist) && !in.origin && !in.weights &&
+                   !fused_disabled() && !fused_onepass() && KM <= kHistMaxKM && !hist_disabled();
     // the planned route: the last query's small-set route (prefilter rounds, then the brute
     // pair pass) replayed with device-sized launches and no host synchronisation until the
     // final read, which verifies every assumption (counts within the bounds, the row type);
     // a miss re-runs the query on the synchronised route.  Results are identical either way
     // (the prefilter is exact, so its round count does not change the skyline).
-    const bool planned = p.plan.valid && !plan_disabled() && c.warm_mode == 0 && in.fate && !brute_disabled() &&
+    const bool planned = p.plan.valid && !plan_disabled() && c.warm_mode == 0 && (in.fate || in.dist) &&
+                         !brute_disabled() &&
                          p.plan.D == D && p.plan.Kp == p.Kp && p.plan.M == p.M && p.plan.single == in.single &&
                          p.plan.global == in.global && (p.plan.rounds == 0 || !prefilter_disabled()) &&
                          cap >= p.plan.bound[0];
@@ -1214,7 +1249,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const uint32_t mt = p.mt;
     // small candidate sets (typical after the prefilter): both skyline levels by one
     // brute-force launch instead of the round-based SFS (SKY_BRUTE=0: A/B knob)
-    const bool brute = in.fate && mt > 0 && mt <= kBruteMax && !brute_disabled() && c.warm_mode == 0;
+    const bool brute = (in.fate || in.dist) && mt > 0 && mt <= kBruteMax && !brute_disabled() && c.warm_mode == 0;
     // the route for the next queries' planned replay: this one's, if it was the small-set one
     p.plan.valid = brute && plan_rounds <= Pipe::Plan::kMaxRounds;
     if (p.plan.valid) {

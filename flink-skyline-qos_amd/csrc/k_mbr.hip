@@ -320,16 +320,23 @@ __global__ __launch_bounds__(kThreads) void k_mbr_groups(const uint32_t *__restr
 // rows (one row per lane) before the current tile is tested, so a wave keeps a tile load in
 // flight while it computes (8 waves per SIMD alone do not hide the HBM / L2 latency of
 // ~250 dependent tile loads per y tile).
+// The y tiles (ytrows / ytpart / ytmax / ytprange, ymr rows) may be another set than the x
+// tiles (the multi-GPU merge: own vectors against the union, FULL only); for one set they are
+// the same arrays.
+struct MbrYSet {
+    const uint32_t *trows, *tpart, *tmax, *tprange;
+    uint32_t mr, ntiles;
+};
 template <class R, bool FULL, bool GM>
 __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
-                                                        const uint32_t *__restrict__ tmax,
                                                         const uint32_t *__restrict__ tprange,
                                                         const uint32_t *__restrict__ tsub,
                                                         const uint32_t *__restrict__ gmin,
                                                         const uint32_t *__restrict__ gprange, uint32_t mr,
-                                                        uint32_t ntiles, uint32_t nsplit, int dbg, uint32_t *__restrict__ domf,
+                                                        uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
+                                                        uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs) {
     constexpr int NW = R::NW;
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
@@ -342,15 +349,15 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     // tile left the launch waiting for its slowest waves
     const uint32_t split = blk % nsplit;
     const uint32_t yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kThreads / 64) + (threadIdx.x >> 6));
-    if (yt >= ntiles) return;
+    if (yt >= ys.ntiles) return;
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
     const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
-    const bool valid = j < mr;
+    const bool valid = j < ys.mr;
     uint32_t y[NW], ymax[NW];
     {
-        const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)min(j, mr - 1u) * NW);
+        const uint4 *src = reinterpret_cast<const uint4 *>(ys.trows + (size_t)min(j, ys.mr - 1u) * NW);
 #pragma unroll
         for (int q = 0; q < NW / 4; q++) {
             const uint4 v = src[q];
@@ -361,10 +368,10 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
         }
     }
 #pragma unroll
-    for (int w = 0; w < NW; w++) ymax[w] = tmax[(size_t)w * ntiles + yt];
-    const uint32_t yr = tprange[yt];
+    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
+    const uint32_t yr = ys.tprange[yt];
     const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
-    const uint32_t py = valid ? tpart[min(j, mr - 1u)] : 0xffffffffu;
+    const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
     // this wave's y rows and partitions in LDS for the broadcast reads of the tests
     __shared__ uint32_t s_y[kThreads / 64][64 * NW];
     __shared__ uint32_t s_py[kThreads / 64][64];
@@ -607,29 +614,46 @@ static int mbr_bits(int D) {
 size_t mbr_tiles(uint32_t mr) { return (mr + kMbrT - 1) / kMbrT; }
 size_t mbr_groups(uint32_t mr) { return (mbr_tiles(mr) + kMbrG - 1) / kMbrG; }
 
+// Morton order + 64-row tiles (+ groups of 64 tiles) of one row set; returns the sorted order
+template <class R, int D>
+static const uint32_t *mbr_build(const uint32_t *rows, const uint64_t *rep_key, uint32_t mr, uint32_t *mm,
+                                 uint64_t *code, uint64_t *code_alt, uint32_t *idx, uint32_t *idx_alt,
+                                 uint32_t *radix_scratch, uint32_t *err, uint32_t *trows, uint32_t *tpart,
+                                 uint32_t *tmin, uint32_t *tmax, uint32_t *tprange, uint32_t *tsub, uint32_t *gmin,
+                                 uint32_t *gprange, hipStream_t st, hipError_t *lerr) {
+    const uint32_t ntiles = (uint32_t)mbr_tiles(mr);
+    const unsigned gb = (unsigned)((mr + kThreads - 1) / kThreads);
+    const int bits = mbr_bits(D);
+    k_mbr_minmax<R, D><<<gb < 512 ? gb : 512, kThreads, 0, st>>>(rows, mr, mm);
+    k_mbr_code<R, D><<<gb, kThreads, 0, st>>>(rows, rep_key, mr, bits, mm, code, idx);
+    const int tb = bits * D + 8;
+    const uint64_t kor = tb >= 64 ? ~0ull : ((1ull << tb) - 1ull);
+    const bool alt = radix_sort_pairs(code, idx, code_alt, idx_alt, mr, kor, 0ull, radix_scratch, err, st, lerr);
+    const uint32_t *perm = alt ? idx_alt : idx;
+    k_mbr_tiles<R><<<(ntiles + 3) / 4, kThreads, 0, st>>>(rows, rep_key, perm, mr, ntiles, trows, tpart, tmin, tmax,
+                                                          tprange, tsub);
+    if (gmin) {
+        const uint32_t ngroups = (uint32_t)mbr_groups(mr);
+        k_mbr_groups<R><<<(ngroups + 3) / 4, kThreads, 0, st>>>(tmin, tprange, ntiles, ngroups, gmin, gprange);
+    }
+    return perm;
+}
+
 template <class R, int D>
 static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t mr = a.mr;
     const uint32_t ntiles = (uint32_t)mbr_tiles(mr);
     const unsigned gb = (unsigned)((mr + kThreads - 1) / kThreads);
-    const int bits = mbr_bits(D);
-    k_mbr_minmax<R, D><<<gb < 512 ? gb : 512, kThreads, 0, st>>>((const uint32_t *)a.rows, mr, a.mm);
-    k_mbr_code<R, D><<<gb, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, mr, bits, a.mm, a.code, a.idx);
-    const int tb = bits * D + 8;
-    const uint64_t kor = tb >= 64 ? ~0ull : ((1ull << tb) - 1ull);
-    const bool alt = radix_sort_pairs(a.code, a.idx, a.code_alt, a.idx_alt, mr, kor, 0ull, a.radix_scratch, a.err, st,
-                                      lerr);
-    const uint32_t *perm = alt ? a.idx_alt : a.idx;
+    const uint32_t *perm = mbr_build<R, D>((const uint32_t *)a.rows, a.rep_key, mr, a.mm, a.code, a.code_alt, a.idx,
+                                           a.idx_alt, a.radix_scratch, a.err, a.trows, a.tpart, a.tmin, a.tmax,
+                                           a.tprange, a.tsub, a.gmin, a.gprange, st, lerr);
     const unsigned gt = (ntiles + 3) / 4;
     const uint32_t nsplit = a.nsplit < 1 ? 1u : (uint32_t)a.nsplit;
     const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
-    k_mbr_tiles<R><<<gt, kThreads, 0, st>>>((const uint32_t *)a.rows, a.rep_key, perm, mr, ntiles, a.trows, a.tpart,
-                                            a.tmin, a.tmax, a.tprange, a.tsub);
-    const uint32_t ngroups = (uint32_t)mbr_groups(mr);
-    k_mbr_groups<R><<<(ngroups + 3) / 4, kThreads, 0, st>>>(a.tmin, a.tprange, ntiles, ngroups, a.gmin, a.gprange);
+    const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    k_mbr_pairs<R, F, G><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tmax, a.tprange, a.tsub, a.gmin,    \
-                                                  a.gprange, mr, ntiles, nsplit, a.dbg, a.domf, a.pairs)
+    k_mbr_pairs<R, F, G><<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,          \
+                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs)
     if (a.full) {
         if (a.gmerge) SKY_MBR_PAIRS(true, true);
         else SKY_MBR_PAIRS(true, false);
@@ -639,6 +663,65 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     }
 #undef SKY_MBR_PAIRS
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);
+}
+
+// own rows (y) against the union (x): flags[own row] = inL | inG << 1, and this rank's shares of
+// |L_k| / survivors_k from the own rows' multiplicities
+__global__ __launch_bounds__(kThreads) void k_mbr_union_finish(const uint32_t *__restrict__ perm,
+                                                               const uint32_t *__restrict__ domf, uint32_t mr,
+                                                               const uint64_t *__restrict__ ykey,
+                                                               const int64_t *__restrict__ ymult, int K,
+                                                               uint8_t *__restrict__ flags,
+                                                               unsigned long long *__restrict__ lsz,
+                                                               unsigned long long *__restrict__ surv) {
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    if (j >= mr) return;
+    const uint32_t f = domf[j], r = perm[j];
+    const bool in_l = !(f & 1u), in_g = !(f & 2u);
+    flags[r] = (uint8_t)((in_l ? 1u : 0u) | (in_g ? 2u : 0u));
+    const int k = (int)(ykey[r] >> 56);
+    if (k < K) {
+        const unsigned long long m = (unsigned long long)ymult[r];
+        if (in_l) atomicAdd(&lsz[k], m);
+        if (in_g) atomicAdd(&surv[k], m);
+    }
+}
+
+template <class R, int D>
+static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr) {
+    const MbrArgs &x = a.x, &y = a.y;
+    mbr_build<R, D>((const uint32_t *)x.rows, x.rep_key, x.mr, x.mm, x.code, x.code_alt, x.idx, x.idx_alt,
+                    x.radix_scratch, x.err, x.trows, x.tpart, x.tmin, x.tmax, x.tprange, x.tsub, x.gmin, x.gprange, st,
+                    lerr);
+    const uint32_t *perm = mbr_build<R, D>((const uint32_t *)y.rows, y.rep_key, y.mr, y.mm, y.code, y.code_alt, y.idx,
+                                           y.idx_alt, y.radix_scratch, y.err, y.trows, y.tpart, y.tmin, y.tmax,
+                                           y.tprange, y.tsub, nullptr, nullptr, st, lerr);
+    const uint32_t nyt = (uint32_t)mbr_tiles(y.mr);
+    const unsigned gp = ((nyt + 3) / 4 + 7) / 8 * 8;
+    const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
+    k_mbr_pairs<R, true, true><<<gp, kThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+                                                        x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
+                                                        y.domf, x.pairs);
+    k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,
+                                                                             a.K, a.flags, a.lsz, a.surv);
+}
+
+hipError_t launch_mbr_union(const MbrUnionArgs &a, hipStream_t st) {
+    if (!a.y.mr || !a.x.mr) return hipSuccess;
+    hipError_t lerr = hipSuccess;
+    if (a.x.fmt == 0) {
+        if (a.x.D <= 8) {
+            SKY_DISPATCH_D(a.x.D, (mbr_union_t<RowU16<DD, 4>, DD>(a, st, &lerr)));
+        } else {
+            SKY_DISPATCH_D(a.x.D, (mbr_union_t<RowU16<DD, 8>, DD>(a, st, &lerr)));
+        }
+    } else if (a.x.fmt == 1) {
+        SKY_DISPATCH_D(a.x.D, (mbr_union_t<RowF32<DD>, DD>(a, st, &lerr)));
+    } else {
+        SKY_DISPATCH_D(a.x.D, (mbr_union_t<RowF64<DD>, DD>(a, st, &lerr)));
+    }
+    if (lerr != hipSuccess) return lerr;
+    return hipGetLastError();
 }
 
 hipError_t launch_mbr(const MbrArgs &a, hipStream_t st) {

@@ -251,7 +251,10 @@ __device__ __forceinline__ uint64_t make_sortkey(const T (&tv)[D], uint32_t part
 #pragma unroll
     for (int d = 0; d < D; d++) {
         const double x = (double)tv[d];
-        u16 &= (x >= 0.0) & (x <= 65535.0) & (x == floor(x));
+        // -0.0 is excluded: packed it becomes +0 and would merge with a +0.0 twin of another
+        // partition (MR-Angle keys read the sign bit), which the distinct-row tests assume away
+        u16 &= (x >= 0.0) && (x <= 65535.0) && (x == floor(x)) &&
+               (__double_as_longlong(x) != (long long)0x8000000000000000ull);
     }
     if (!u16) lflags |= kFlagNotU16;
     uint32_t h = 0x9e3779b9u;
@@ -1417,27 +1420,6 @@ __global__ __launch_bounds__(kThreads) void k_out_fused(OutArgs a, unsigned long
     }
 }
 
-template <typename T, int D>
-__global__ __launch_bounds__(kThreads) void k_export_reps(uint32_t mr, const T *__restrict__ rep_rows,
-                                                          const uint64_t *__restrict__ rep_key,
-                                                          const uint8_t *__restrict__ alive_l,
-                                                          const uint32_t *__restrict__ alive_scan,
-                                                          const unsigned long long *__restrict__ mult,
-                                                          double *__restrict__ rows_out,
-                                                          int32_t *__restrict__ keys_out,
-                                                          int64_t *__restrict__ mult_out) {
-    constexpr int DP = padded_dims<T>(D);
-    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
-    if (r >= mr || !alive_l[r]) return;
-    const uint32_t e = alive_scan[r];
-    T v[D];
-    load_trow<T, D>(rep_rows + (size_t)r * DP, v);
-#pragma unroll
-    for (int d = 0; d < D; d++) rows_out[(size_t)e * D + d] = (double)v[d];
-    keys_out[e] = (int32_t)(rep_key[r] >> 56);
-    mult_out[e] = (int64_t)mult[r];
-}
-
 // ---- host launchers -----------------------------------------------------------
 static inline unsigned nblk(size_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
@@ -1577,19 +1559,4 @@ void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, cons
 void launch_out_write(const OutArgs &a, hipStream_t st) {
     if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
 }
-void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
-                        const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,
-                        double *rows_out, int32_t *keys_out, int64_t *mult_out, hipStream_t st) {
-    if (!mr) return;
-    if (f64) {
-        SKY_DISPATCH_D(D, (k_export_reps<double, DD><<<nblk(mr, kThreads), kThreads, 0, st>>>(
-                              mr, (const double *)rep_rows, rep_key, alive_l, alive_scan, mult, rows_out, keys_out,
-                              mult_out)));
-    } else {
-        SKY_DISPATCH_D(D, (k_export_reps<float, DD><<<nblk(mr, kThreads), kThreads, 0, st>>>(
-                              mr, (const float *)rep_rows, rep_key, alive_l, alive_scan, mult, rows_out, keys_out,
-                              mult_out)));
-    }
-}
-
 }  // namespace sky

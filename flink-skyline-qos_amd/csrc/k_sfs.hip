@@ -420,95 +420,6 @@ __global__ __launch_bounds__(kThreads) void k_global_keys(const uint64_t *__rest
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_import_flags(const uint8_t *__restrict__ alive_l,
-                                                           const uint32_t *__restrict__ alive_scan, uint32_t mr,
-                                                           const uint8_t *__restrict__ union_flags,
-                                                           uint32_t self_offset, uint8_t *__restrict__ alive_g) {
-    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
-    if (r >= mr) return;
-    alive_g[r] = alive_l[r] ? ((union_flags[self_offset + alive_scan[r]] & 2u) ? 1 : 0) : 0;
-}
-
-// Multi-GPU import: each rank decides the fate of ITS OWN exported
-// vectors [off, off + n_own) of the all-gathered union only.  A vector v of key k is in L_k
-// iff no union vector of key k dominates it, and in G iff no union vector dominates it (a
-// dominator u outside L_k' is itself dominated by a member of L_k', so testing the whole
-// union is testing the union of the L_k).  Equal vectors never dominate (full test: the
-// same vector may come from several ranks).  Union rows stream through LDS; a wave stops
-// once all its lanes are settled.  Per-rank stats: the multiplicities of the own vectors
-// in L_k / G, summed over ranks by the caller (FlinkSkyline.java:593-608).
-constexpr int kUnionTile = 256;
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_union_fate(const double *__restrict__ urows,
-                                                         const int32_t *__restrict__ ukeys,
-                                                         const int64_t *__restrict__ umult, uint32_t n_union,
-                                                         uint32_t off, uint32_t n_own, int K,
-                                                         uint8_t *__restrict__ flags,
-                                                         unsigned long long *__restrict__ lsz,
-                                                         unsigned long long *__restrict__ surv) {
-    __shared__ double s_x[kUnionTile * D];
-    __shared__ double s_s[kUnionTile];
-    __shared__ int32_t s_k[kUnionTile];
-    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    const bool valid = j < n_own;
-    double y[D];
-#pragma unroll
-    for (int d = 0; d < D; d++) y[d] = valid ? urows[(size_t)(off + j) * D + d] : 0.0;
-    const int32_t ky = valid ? ukeys[off + j] : -1;
-    // x dominates y => sum(x) <= sum(y) (each rounded addition is monotone; values clamped to
-    // +-1e300 so that infinities never meet): the compare is skipped for larger sums
-    auto score = [](const double *v) {
-        double s = 0.0;
-#pragma unroll
-        for (int d = 0; d < D; d++) s += v[d] > 1e300 ? 1e300 : (v[d] < -1e300 ? -1e300 : v[d]);
-        return s;
-    };
-    const double sy = score(y);
-    bool dom_l = false, dom_g = false;
-    for (uint32_t t0 = 0; t0 < n_union; t0 += kUnionTile) {
-        const uint32_t cn = n_union - t0 < (uint32_t)kUnionTile ? n_union - t0 : (uint32_t)kUnionTile;
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < cn * D; q += kThreads) s_x[q] = urows[(size_t)t0 * D + q];
-        for (uint32_t q = threadIdx.x; q < cn; q += kThreads) s_k[q] = ukeys[t0 + q];
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < cn; q += kThreads) s_s[q] = score(s_x + (size_t)q * D);
-        __syncthreads();
-        if (valid && !dom_l) {
-            for (uint32_t i = 0; i < cn; i++) {
-                if (s_s[i] <= sy && dominates_full<D, double>(s_x + (size_t)i * D, y)) {
-                    dom_g = true;
-                    if (s_k[i] == ky) {
-                        dom_l = true;
-                        break;
-                    }
-                }
-            }
-        }
-        if (!__syncthreads_or(valid && !dom_l)) break;
-    }
-    if (!valid) return;
-    flags[off + j] = (uint8_t)((dom_l ? 0u : 1u) | (dom_g ? 0u : 2u));
-    if (ky >= 0 && ky < K) {
-        const unsigned long long m = (unsigned long long)umult[off + j];
-        if (!dom_l) atomicAdd(&lsz[ky], m);
-        if (!dom_g) atomicAdd(&surv[ky], m);
-    }
-}
-
-void launch_union_fate(int D, const double *urows, const int32_t *ukeys, const int64_t *umult, uint32_t n_union,
-                       uint32_t off, uint32_t n_own, int K, uint8_t *flags, unsigned long long *lsz,
-                       unsigned long long *surv, hipStream_t st) {
-    if (!n_own) return;
-    SKY_DISPATCH_D(D, (k_union_fate<DD><<<(n_own + kThreads - 1) / kThreads, kThreads, 0, st>>>(
-                          urows, ukeys, umult, n_union, off, n_own, K, flags, lsz, surv)));
-}
-
-void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
-                         uint32_t self_offset, uint8_t *alive_g, hipStream_t st) {
-    if (mr) k_import_flags<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(alive_l, alive_scan, mr, union_flags,
-                                                                                self_offset, alive_g);
-}
-
 template <typename T, int D>
 __global__ __launch_bounds__(kThreads) void k_gather_rows(const T *__restrict__ src, const uint32_t *__restrict__ idx,
                                                           uint32_t m, T *__restrict__ dst) {

@@ -188,9 +188,6 @@ void launch_out_write(const OutArgs &a, hipStream_t st);
 // *ticket zeroed by the caller; *d_total = selected tuples; writes positions < cap only
 void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket, uint32_t *d_total, uint32_t *err,
                       int64_t cap, hipStream_t st);
-void launch_export_reps(int D, bool f64, uint32_t mr, const void *rep_rows, const uint64_t *rep_key,
-                        const uint8_t *alive_l, const uint32_t *alive_scan, const unsigned long long *mult,
-                        double *rows_out, int32_t *keys_out, int64_t *mult_out, hipStream_t st);
 
 // ---- k_sfs.hip ----
 struct SfsSeg { uint32_t begin, count; };
@@ -225,13 +222,6 @@ struct FillSet : FillRanges {
 };
 // ranges g.p[j] (g.bytes[j] bytes, 4-aligned) copied to pinned_dst + g.val[j] in one launch
 hipError_t launch_gather_words(const FillRanges &g, void *pinned_dst, hipStream_t st);
-void launch_import_flags(const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr, const uint8_t *union_flags,
-                         uint32_t self_offset, uint8_t *alive_g, hipStream_t st);
-// own exported vectors [off, off+n_own) of the gathered union -> flags (bit0 in L_k, bit1 in G)
-// and this rank's multiplicity sums into lsz[K] / surv[K]
-void launch_union_fate(int D, const double *urows, const int32_t *ukeys, const int64_t *umult, uint32_t n_union,
-                       uint32_t off, uint32_t n_own, int K, uint8_t *flags, unsigned long long *lsz,
-                       unsigned long long *surv, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,
                         uint64_t *gkey, uint32_t *gval, unsigned long long *orand, hipStream_t st);
 void launch_sfs_small(int D, bool f64, bool full, bool ties, int B, const void *rows, const uint64_t *key,
@@ -302,6 +292,16 @@ struct MbrArgs {
     unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
 };
+// the multi-GPU merge: own rows (y, a contiguous range of the union) against the whole union
+// (x), FULL test, both levels; x.gmin / x.gprange needed, y's group buffers unused
+struct MbrUnionArgs {
+    MbrArgs x, y;                 // rows / rep_key / mr and the tile buffers of each set; y.domf zeroed
+    const int64_t *ymult = nullptr;
+    int K = 0;
+    uint8_t *flags = nullptr;     // per own row: inL | inG << 1
+    unsigned long long *lsz = nullptr, *surv = nullptr;   // [K] this rank's shares
+};
+hipError_t launch_mbr_union(const MbrUnionArgs &a, hipStream_t st);
 int mbr_row_words(int D, int fmt);
 size_t mbr_tiles(uint32_t mr);
 size_t mbr_groups(uint32_t mr);
@@ -325,6 +325,37 @@ void launch_part_tkeep(uint32_t T, const uint32_t *trep, const uint8_t *ralive, 
 void launch_part_tmove(uint32_t T, const uint32_t *keep, const uint32_t *pos, const uint32_t *rpos, const int64_t *ids,
                        const uint32_t *trep, int64_t *ids2, uint32_t *trep2, hipStream_t st);
 void launch_part_rows_out(int D, uint32_t T, const uint32_t *trep, const double *rrows, double *out, hipStream_t st);
+
+// ---- k_dist.hip (multi-GPU step, device-sized) ----
+// verdict bits of a rank's block header (sky_dist_finish reads them for every rank)
+constexpr uint32_t kDistNaN = 1u;       // a tuple value is NaN: every rank returns SKY_E_NAN
+constexpr uint32_t kDistReplan = 2u;    // the planned local phase missed an assumption: re-run the step
+constexpr uint32_t kDistError = 4u;     // a look-back exceeded its spin bound (internal error)
+struct PlanCheck {                      // pipe_finish's planned-route checks, as kernel arguments
+    int planned = 0;
+    uint32_t cap = 0;                   // candidate slots allocated
+    uint32_t bound[4] = {};             // slots entering round r / the brute pass
+    int rounds = 0;
+    uint32_t brute_max = 0;
+    int k_u16 = 0, k_f32 = 0;           // the brute pass's compare type
+};
+void launch_plan_verdict(const uint32_t *totals, const uint32_t *flags, const PlanCheck &pc, uint32_t *verdict,
+                         hipStream_t st);
+void launch_dist_flags(const uint8_t *alive, uint32_t n, const uint32_t *d_n, uint32_t *out, hipStream_t st);
+void launch_dist_rows(int D, bool f64, const void *rows, const uint64_t *key, const uint32_t *flag, const uint32_t *pos,
+                      uint32_t n, const uint32_t *slot_src, const uint32_t *dup_cnt, const int32_t *pr_entries,
+                      const unsigned long long *mult, int64_t *block, uint32_t cap, hipStream_t st);
+void launch_dist_header(const uint32_t *d_count, const uint32_t *verdict, uint32_t n, int D, int64_t *block,
+                        hipStream_t st);
+void launch_dist_summary(const int64_t *blocks, int world, int rank, uint32_t cap, int D, unsigned long long *sum,
+                         hipStream_t st);
+void launch_dist_compact(int D, const int64_t *blocks, int world, uint32_t cap, unsigned long long *sum, double *urows,
+                         uint64_t *ukey, int64_t *umult, hipStream_t st);
+void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *out, hipStream_t st);
+void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
+                            unsigned long long *lsz, unsigned long long *surv, hipStream_t st);
+void launch_dist_alive_g(const uint32_t *flag, const uint32_t *pos, uint32_t n, const uint8_t *own_flags, uint32_t cap,
+                         uint8_t *alive_g, hipStream_t st);
 
 // ---- k_synth.hip ----
 void launch_synth(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0, int64_t n, double *vals,

@@ -26,6 +26,7 @@ SKY_E_CAPACITY = -3
 SKY_E_NAN = -4
 SKY_E_NOMEM = -5
 SKY_E_NOLIB = -6
+SKY_E_RETRY = -7
 
 SKY_MAX_DIMS = 16
 CSV_OK, CSV_MALFORMED, CSV_BAD_ID, CSV_ARITY = 0, 1, 2, 3
@@ -69,9 +70,11 @@ SIGNATURES = {
     "sky_global_stats_set": [c_p, c_i32, c_p, c_p],
     "sky_query": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64],
     "sky_query_dev": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64],
-    "sky_export_local_dev": [c_p, c_p, c_p, c_i64, P_i64],
-    "sky_export_copy_dev": [c_p, c_p, c_p, c_p, c_i64],
-    "sky_import_union_dev": [c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, P_i64],
+    "sky_dist_export_dev": [c_p, c_p, c_p, c_i64, c_p, c_i64],
+    "sky_dist_reblock_dev": [c_p, c_p, c_i64],
+    "sky_dist_merge_dev": [c_p, c_p, c_i32, c_i32, c_i64, c_p, c_p, c_i64, c_p],
+    "sky_dist_finish": [c_p, c_p, c_i64, P_i64, P_i64],
+    "sky_profile_host_syncs": [c_p, P_i64],
     "sky_parse_csv_dev": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64, c_p],
     "sky_parse_csv": [c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64],
     "sky_format_csv_dev": [c_p, c_p, c_p, c_i64, c_p, c_i64, P_i64],

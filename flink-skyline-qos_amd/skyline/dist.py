@@ -1,118 +1,155 @@
-"""Multi-GPU skyline: one process per GPU, shards of the tuple stream per rank.
+"""Multi-GPU skyline: one process per GPU, one shard of the tuple stream per rank, ONE host
+read per step.
 
-Exactness: SKY(u_k SKY(P_k)) = SKY(u P_k) for ANY split, so:
-  1. each rank reduces its own shard to the distinct vectors of its local skylines, with
-     partition key and multiplicity (sky_export_local_dev);
-  2. the ranks exchange those vectors with ONE all-gather (RCCL over xGMI when the process
-     group is "nccl"; gloo on CPU for tests), counts first;
-  3. each rank decides the fate of ITS OWN vectors against the gathered union
-     (sky_import_union_dev: in L_k iff no union vector of key k dominates it, in G iff no
-     union vector dominates it) -- |own| x |union| pair tests per rank, so the global phase
-     shrinks with the number of ranks instead of being replicated on every rank;
-  4. the per-rank shares of |L_k| and survivors_k are summed with one all-reduce of 2K
-     integers (the optimality inputs, FlinkSkyline.java:593-608).
-Tuple ids never leave their rank: each rank emits its own global-skyline ids.
+The reference scales out by Flink's keyBy shuffle to P keys and one global reducer per query
+(FlinkSkyline.java:138, :171-174; the merge :548-566).  Here every rank owns a shard of the
+stream; SKY(u_r SKY(shard_r)) = SKY(u_r shard_r) makes any split exact.  One step
+(include/skyline_hip.h, "multi-GPU step"):
 
-Wire format of one exported vector (int64 words): D value words (f64 bits),
-1 partition key, 1 multiplicity  ->  [count, D+2] int64 per rank, padded to the
-largest count (counts are all-gathered first).
+  1. sky_dist_export_dev: the shard's local skylines -> this rank's FIXED-SIZE block (its
+     distinct local-skyline vectors with partition key and multiplicity, and a header whose
+     verdict carries the run's checks).  No host read: the planned small-set route replays with
+     device-sized launches, and its assumptions are checked on the device.
+  2. one all-gather of the blocks (RCCL over xGMI with "nccl"; device-resident, no sizes needed
+     on the host because every block has the same capacity);
+  3. sky_dist_merge_dev: each rank decides ITS OWN vectors against the union (in L_k iff no union
+     vector of key k dominates it, in G iff no union vector does), writes its global-skyline ids
+     and its share of |L_k| / survivors_k -- |own| x |union| work, not a replicated merge;
+  4. one all-reduce (sum) of the 2K shares (FlinkSkyline.java:593-608), on the device;
+  5. sky_dist_finish: the step's one host read.  Every rank sees the same gathered headers, so
+     every rank takes the same decision: done, re-run the step (a rank's planned route missed),
+     or re-run the exchange with a larger capacity (some rank exported more than it holds).
+Tuple ids never leave their rank.  With a gloo group (CPU tests, or rehearsing several ranks on
+one GPU) the device blocks are staged through host memory for the transport.
 """
-import time
-
-import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import _abi
 
-def pack_export(rows_f64, keys_i32, mult_i64):
-    """[n,D] f64, [n] i32, [n] i64 -> [n, D+2] i64 (bit-preserving)."""
+_SKY_OK, _SKY_E_RETRY, _SKY_E_CAPACITY = _abi.SKY_OK, _abi.SKY_E_RETRY, _abi.SKY_E_CAPACITY
+
+
+def block_words(cap, dims):
+    """int64 words of one rank's block (SKY_DIST_BLOCK_WORDS)."""
+    return (int(cap) + 1) * (int(dims) + 2)
+
+
+def pack_block(rows_f64, keys, mult, cap, verdict=0, n_tuples=0):
+    """Host mirror of a block (tests, CPU rehearsal): header (count, verdict, shard tuples,
+    dims) + up to cap rows of (value bits, key, multiplicity)."""
+    rows_f64 = torch.as_tensor(rows_f64, dtype=torch.float64)
     n, D = rows_f64.shape
-    out = torch.empty((n, D + 2), dtype=torch.int64, device=rows_f64.device)
-    out[:, :D] = rows_f64.contiguous().view(torch.int64)
-    out[:, D] = keys_i32.to(torch.int64)
-    out[:, D + 1] = mult_i64
+    out = torch.zeros(block_words(cap, D), dtype=torch.int64)
+    b = out.view(cap + 1, D + 2)
+    b[0, 0] = n
+    b[0, 1] = verdict
+    b[0, 2] = n_tuples
+    if D + 2 > 3:
+        b[0, 3] = D
+    m = min(n, cap)
+    if m:
+        b[1:m + 1, :D] = rows_f64[:m].contiguous().view(torch.int64)
+        b[1:m + 1, D] = torch.as_tensor(keys[:m], dtype=torch.int64)
+        b[1:m + 1, D + 1] = torch.as_tensor(mult[:m], dtype=torch.int64)
     return out
 
 
-def unpack_union(packed, counts, D):
-    """all-gathered [W, maxc, D+2] + per-rank counts -> contiguous union tensors."""
-    parts = [packed[r, :int(c)] for r, c in enumerate(counts)]
-    u = torch.cat(parts, 0) if parts else packed.new_empty((0, D + 2))
-    rows = u[:, :D].contiguous().view(torch.float64)
-    keys = u[:, D].to(torch.int32).contiguous()
-    mult = u[:, D + 1].contiguous()
-    return rows, keys, mult
+def unpack_blocks(gathered, world, cap, D):
+    """[world * block] int64 -> per rank (rows f64 [c, D], keys int64 [c], mult int64 [c], count,
+    verdict); rows beyond cap are absent (the count says how many were exported)."""
+    g = gathered.view(world, cap + 1, D + 2)
+    out = []
+    for r in range(world):
+        c = int(g[r, 0, 0])
+        v = int(g[r, 0, 1])
+        m = min(c, cap)
+        body = g[r, 1:m + 1]
+        out.append((body[:, :D].contiguous().view(torch.float64), body[:, D].clone(), body[:, D + 1].clone(), c, v))
+    return out
 
 
-def allgather_varlen(packed, group=None):
-    """Gather a [n, W] int64 tensor of per-rank length n from every rank.
-    Returns (stacked [world, maxn, W], counts list).  With a gloo group (CPU
-    collectives: tests, or rehearsing several ranks on one GPU) device tensors are
-    staged through host memory; with nccl (RCCL) they stay in HBM."""
+def all_gather_blocks(recv, send, group=None):
+    """recv [world * W] <- every rank's send [W] in rank order (device tensors stay in HBM with
+    RCCL; a gloo group stages them through host memory)."""
     world = dist.get_world_size(group)
-    if packed.device.type == "cuda" and dist.get_backend(group) == "gloo":
-        out, counts = allgather_varlen(packed.cpu(), group)
-        return out.to(packed.device), counts
-    dev = packed.device
-    cnt = torch.tensor([packed.shape[0]], dtype=torch.int64, device=dev)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    counts = [int(c.item()) for c in cnts]
-    maxc = max(max(counts), 1)
-    W = packed.shape[1]
-    buf = torch.zeros((maxc, W), dtype=torch.int64, device=dev)
-    buf[:packed.shape[0]] = packed
-    out = torch.empty((world, maxc, W), dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(out.view(world * maxc, W), buf, group=group)
-    return out, counts
+    if dist.get_backend(group) == "gloo":
+        s = send.cpu() if send.is_cuda else send
+        parts = [torch.empty_like(s) for _ in range(world)]
+        dist.all_gather(parts, s, group=group)
+        recv.copy_(torch.cat(parts), non_blocking=False)
+        return
+    dist.all_gather_into_tensor(recv, send, group=group)
 
 
-def allreduce_stats(ls, sv, device, group=None):
-    """Sum the per-rank |L_k| / survivors_k shares over the ranks (one all-reduce)."""
-    K = len(ls)
-    backend = dist.get_backend(group)
-    dev = device if (backend != "gloo" and device.type == "cuda") else torch.device("cpu")
-    t = torch.from_numpy(np.concatenate([ls, sv]).astype(np.int64)).to(dev)
+def all_reduce_sum(t, group=None):
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+        return
     dist.all_reduce(t, group=group)
-    t = t.cpu().numpy()
-    return t[:K], t[K:]
 
 
-def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, cap, group=None):
-    """One query over the union of every rank's shard.  Returns this rank's
-    number of global-skyline ids written to d_ids_out (stream order); afterwards
-    engine.stats() holds the job-wide |L_k| / survivors_k and engine.last_dist_stats
-    the exchange's sizes and phase times."""
-    D = engine.dims
-    dev = d_vals.device
-    t0 = time.perf_counter()
-    ne = engine.export_local_dev(d_ids, d_vals)
-    rows = torch.empty((max(ne, 1), D), dtype=torch.float64, device=dev)
-    keys = torch.empty(max(ne, 1), dtype=torch.int32, device=dev)
-    mult = torch.empty(max(ne, 1), dtype=torch.int64, device=dev)
-    if ne:
-        engine.export_copy_dev(rows, keys, mult, ne)
-    engine.sync()
-    t1 = time.perf_counter()
-    packed = pack_export(rows[:ne], keys[:ne], mult[:ne])
-    gathered, counts = allgather_varlen(packed, group)
-    urows, ukeys, umult = unpack_union(gathered, counts, D)
+class DistExchange:
+    """The fixed-capacity exchange of one engine: this rank's block, the gathered blocks and the
+    stat shares (device tensors), and the capacity every rank uses.  The capacity only grows,
+    and identically on every rank (from the largest count in the gathered headers)."""
+
+    def __init__(self, engine, device, world, cap=4096):
+        self.engine = engine
+        self.device = device
+        self.world = world
+        self.cap = int(cap)
+        self.stats = torch.zeros(2 * engine.K, dtype=torch.int64, device=device)
+        self._alloc()
+        self.retries = 0
+        self.regrows = 0
+
+    def _alloc(self):
+        w = block_words(self.cap, self.engine.dims)
+        self.send = torch.empty(w, dtype=torch.int64, device=self.device)
+        self.recv = torch.empty(w * self.world, dtype=torch.int64, device=self.device)
+
+    def grow(self, need):
+        self.cap = int(need) + int(need) // 4 + 64
+        self._alloc()
+
+
+def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, out_cap, group=None, max_attempts=8):
+    """One query over the union of every rank's shard.  Returns this rank's number of global-
+    skyline ids written to d_ids_out (stream order); afterwards engine.stats() holds the job-wide
+    |L_k| / survivors_k and engine.last_dist_stats the exchange's sizes."""
+    world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    self_off = sum(counts[:rank])
-    if dev.type == "cuda":
-        torch.cuda.synchronize(dev)
-    t2 = time.perf_counter()
-    g = engine.import_union_dev(urows, ukeys, umult, urows.shape[0], self_off, d_ids_out, d_origin_out, cap)
-    ls, sv = engine.stats()                      # this rank's share
-    t3 = time.perf_counter()
-    ls, sv = allreduce_stats(ls, sv, dev, group)
-    engine.set_stats(ls, sv)
-    t4 = time.perf_counter()
-    n_union = int(urows.shape[0])
-    engine.last_dist_stats = {
-        "world": dist.get_world_size(group), "union_vectors": n_union, "own_vectors": ne,
-        "exchange_bytes_per_rank": int(gathered.numel() * 8),
-        "own_x_union_pair_tests": ne * n_union,
-        "ms": {"export": (t1 - t0) * 1e3, "allgather": (t2 - t1) * 1e3, "import": (t3 - t2) * 1e3,
-               "stats_allreduce": (t4 - t3) * 1e3}}
-    return g
+    dev = d_vals.device
+    ex = getattr(engine, "_dist_ex", None)
+    if ex is None or ex.world != world:
+        ex = engine._dist_ex = DistExchange(engine, dev, world)
+    h0 = engine.host_syncs()
+    export = True
+    for attempt in range(max_attempts):
+        if export:
+            engine.dist_export_dev(d_ids, d_vals, ex.send, ex.cap)
+        else:
+            engine.dist_reblock_dev(ex.send, ex.cap)
+        all_gather_blocks(ex.recv, ex.send, group)
+        engine.dist_merge_dev(ex.recv, world, rank, ex.cap, d_ids_out, d_origin_out, out_cap, ex.stats)
+        all_reduce_sum(ex.stats, group)
+        rc, g, need = engine.dist_finish(ex.stats, out_cap)
+        if rc == _SKY_OK:
+            _, cnt = engine.phases()
+            engine.last_dist_stats = {
+                "world": world, "cap": ex.cap, "own_vectors": int(cnt[3]), "union_vectors": int(cnt[5]),
+                "union_route": "pair kernel over the blocks" if int(cnt[6]) == 0 else "bounding-box pass",
+                "exchange_bytes_per_rank": int(ex.send.numel() * 8), "attempts": attempt + 1,
+                "planned_local_phase": bool(int(cnt[7]) & 8), "host_syncs": engine.host_syncs() - h0}
+            return g
+        if rc == _SKY_E_RETRY:
+            ex.retries += 1
+            export = True
+        else:                                       # exchange capacity: same decision on every rank
+            ex.regrows += 1
+            ex.grow(need)
+            export = False
+    raise RuntimeError(f"distributed_query did not converge in {max_attempts} attempts")

@@ -152,24 +152,41 @@ class SkylineEngine:
         g = cnt.value
         return out_ids[:g].copy(), out_org[:g].copy()
 
-    # ---- multi-GPU phases ----------------------------------------------------------------
-    def export_local_dev(self, d_ids, d_values):
+    # ---- multi-GPU step with one host read (sky_dist_*) ------------------------------------
+    def dist_export_dev(self, d_ids, d_values, d_block, cap):
+        """Local skylines of this rank's shard -> its fixed-size exchange block (no host read)."""
         n = d_values.numel() // self.dims
-        cnt = ctypes.c_int64(0)
         with _Ordered(self.h, self.device):
-            check(lib().sky_export_local_dev(self.h, _tptr(d_ids), _tptr(d_values), n, ctypes.byref(cnt)))
-        return cnt.value
+            check(lib().sky_dist_export_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_block), cap))
 
-    def export_copy_dev(self, d_rows, d_keys, d_mult, cap):
+    def dist_reblock_dev(self, d_block, cap):
+        """Rewrite this rank's block with a larger capacity (after SKY_E_CAPACITY with need_cap)."""
         with _Ordered(self.h, self.device):
-            check(lib().sky_export_copy_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), cap))
+            check(lib().sky_dist_reblock_dev(self.h, _tptr(d_block), cap))
 
-    def import_union_dev(self, d_rows, d_keys, d_mult, n_union, self_offset, d_ids_out, d_origin_out, cap):
-        cnt = ctypes.c_int64(0)
+    def dist_merge_dev(self, d_blocks, world, rank, cap, d_ids_out, d_origin_out, out_cap, d_stats):
+        """Own vectors vs the gathered union; output ids and this rank's stat shares (no host read)."""
         with _Ordered(self.h, self.device):
-            check(lib().sky_import_union_dev(self.h, _tptr(d_rows), _tptr(d_keys), _tptr(d_mult), n_union, self_offset,
-                                             _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(cnt)))
-        return cnt.value
+            check(lib().sky_dist_merge_dev(self.h, _tptr(d_blocks), world, rank, cap, _tptr(d_ids_out),
+                                           _tptr(d_origin_out), out_cap, _tptr(d_stats)))
+
+    def dist_finish(self, d_stats_sum, out_cap):
+        """The step's one host read -> (status, this rank's output count, needed exchange capacity);
+        status is SKY_OK or SKY_E_RETRY / SKY_E_CAPACITY (the caller re-runs), other codes raise."""
+        n = ctypes.c_int64(0)
+        need = ctypes.c_int64(0)
+        with _Ordered(self.h, self.device):
+            rc = lib().sky_dist_finish(self.h, _tptr(d_stats_sum), out_cap, ctypes.byref(n), ctypes.byref(need))
+        if rc not in (_abi.SKY_OK, _abi.SKY_E_RETRY, _abi.SKY_E_CAPACITY) or \
+                (rc == _abi.SKY_E_CAPACITY and need.value == 0):
+            check(rc)
+        return rc, n.value, need.value
+
+    def host_syncs(self):
+        """Host synchronisations (device read-backs) this context has made."""
+        n = ctypes.c_int64(0)
+        check(lib().sky_profile_host_syncs(self.h, ctypes.byref(n)))
+        return n.value
 
     # ---- utilities -----------------------------------------------------------------------
     def synth_dev(self, dist, n, d_values, d_ids=None, seed=1234, id0=0, dmin=0, dmax=1000):

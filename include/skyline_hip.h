@@ -47,6 +47,7 @@ extern "C" {
 #define SKY_E_NAN      -4   /* a value is NaN: the reference BNL result is order-dependent for NaN */
 #define SKY_E_NOMEM    -5   /* device allocation failed */
 #define SKY_E_NOLIB    -6   /* no HIP device / code object for gfx950 */
+#define SKY_E_RETRY    -7   /* multi-GPU step: some rank's planned local phase missed, run the step again */
 
 /* partitioners (FlinkSkyline.java:112-134, flag --algo) */
 #define SKY_ALGO_DIM    0   /* "mr-dim"   */
@@ -74,7 +75,7 @@ typedef struct sky_stream sky_stream;
 
 /* ---- context ------------------------------------------------------------ */
 /* devices/ndev: HIP device ordinals; one process drives one device (ndev == 1),
- * multi-GPU runs one process per GPU (see sky_export_local / sky_import_union).
+ * multi-GPU runs one process per GPU (see the sky_dist_* step).
  * dims in [1,16]; num_partitions P in [1,256] (= 2 x Flink parallelism, :76);
  * domain_max = --domain (default 1000.0, :71). */
 int sky_ctx_create(const int *devices, int ndev, int dims, int num_partitions, int algo,
@@ -132,8 +133,8 @@ int sky_global_merge(sky_ctx *ctx, int nparts, const int32_t *part_ids,
  * local_sizes[k] = |L_k|, survivors[k] = |G n L_k| for k < K
  * (K = P, or max(P, 2^D) for MR-Grid with SKY_SEM_COMPLETE). */
 int sky_global_stats(sky_ctx *ctx, int64_t *local_sizes, int64_t *survivors, int32_t *k_out);
-/* records job-wide integers (e.g. the all-reduced per-rank shares after sky_import_union_dev)
- * so that sky_global_stats returns them until the next query */
+/* records job-wide integers (e.g. integers a caller merged itself) so that sky_global_stats
+ * returns them until the next query (sky_dist_finish records the all-reduced shares itself) */
 int sky_global_stats_set(sky_ctx *ctx, int32_t k, const int64_t *local_sizes, const int64_t *survivors);
 
 /* ---- fused whole-stream query --------------------------------------------- */
@@ -165,25 +166,38 @@ int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64
 int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
                          int64_t *n_out);
 
-/* ---- multi-GPU (one process per GPU; the caller moves bytes with RCCL) ------ */
-/* Phase 1 on each rank: local skylines of this rank's shard; export their
- * distinct vectors: rows (f64, dims wide) + origin key + multiplicity.  Returns the
- * count in *n_out; call with cap = 0 first to size the buffers. */
-int sky_export_local_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
-                         int64_t *n_out);
-int sky_export_copy_dev(sky_ctx *ctx, double *d_rows_out, int32_t *d_keys_out,
-                        int64_t *d_mult_out, int64_t cap);
-/* Phase 2: the all-gathered union of every rank's exported vectors (this rank's
- * own export starts at row self_offset).  Each rank decides the fate of ITS OWN
- * vectors only: v (key k) is in L_k iff no union vector of key k
- * dominates it, and in G iff no union vector dominates it; the per-rank work is
- * |own| x |union|, not a re-run over the whole union.  Writes this rank's global-
- * skyline ids (stream order).  sky_global_stats afterwards returns THIS RANK'S SHARE
- * of |L_k| and survivors_k: the caller sums them over the ranks (one all-reduce of
- * 2K integers).  The shard buffers passed to sky_export_local_dev must still be valid. */
-int sky_import_union_dev(sky_ctx *ctx, const double *d_rows, const int32_t *d_keys,
-                         const int64_t *d_mult, int64_t n_union, int64_t self_offset,
-                         int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out);
+/* ---- multi-GPU step with one host read (one process per GPU) --------------------
+ * The reference scales out by Flink's keyBy shuffle and one global reducer per query
+ * (FlinkSkyline.java:138, :171-174, GlobalSkylineAggregator :515-569).  Here every rank owns
+ * a shard of the stream (SKY(u SKY(shard_r)) = SKY(u shard_r) for any split) and exchanges a
+ * FIXED-SIZE block, so the caller's collectives (RCCL over xGMI, device-resident buffers) need
+ * no host-side sizes and one step reads the device back exactly once:
+ *   sky_dist_export_dev  local skylines of this rank's shard -> d_block (this rank's block)
+ *   caller               all-gather the blocks of every rank into d_blocks (rank order)
+ *   sky_dist_merge_dev   this rank's own vectors against the union; this rank's global-skyline
+ *                        ids (stream order) -> d_ids_out / d_origin_out (positions < out_cap);
+ *                        this rank's share of |L_k| / survivors_k -> d_stats (int64[2K])
+ *   caller               all-reduce (sum) d_stats over the ranks
+ *   sky_dist_finish      the one host read: every rank's verdict (from the gathered headers, so
+ *                        every rank returns the same code), *n_out = this rank's output count;
+ *                        sky_global_stats then returns the job-wide |L_k| / survivors_k.
+ * Block: int64[SKY_DIST_BLOCK_WORDS(cap, dims)]: a header row (count, verdict, shard tuples,
+ * dims) and up to cap rows of (dims value bits as f64, partition key, multiplicity).
+ * sky_dist_finish returns, on every rank alike:
+ *   SKY_E_NAN       some shard holds a NaN;
+ *   SKY_E_RETRY     some rank's planned local phase missed: call sky_dist_export_dev again;
+ *   SKY_E_CAPACITY  with *need_cap > cap: some rank exported more than cap vectors: call
+ *                   sky_dist_reblock_dev with a cap >= *need_cap (every rank), then all-gather,
+ *                   merge and finish again (no local re-run);
+ * and on this rank only SKY_E_CAPACITY with *need_cap == 0 when *n_out > out_cap (out_cap >=
+ * the shard's tuple count never overflows).  Output buffers hold unspecified data on error. */
+#define SKY_DIST_BLOCK_WORDS(cap, dims) (((int64_t)(cap) + 1) * ((int64_t)(dims) + 2))
+int sky_dist_export_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n, int64_t *d_block,
+                        int64_t cap);
+int sky_dist_reblock_dev(sky_ctx *ctx, int64_t *d_block, int64_t cap);
+int sky_dist_merge_dev(sky_ctx *ctx, const int64_t *d_blocks, int32_t world, int32_t rank, int64_t cap,
+                       int64_t *d_ids_out, int32_t *d_origin_out, int64_t out_cap, int64_t *d_stats);
+int sky_dist_finish(sky_ctx *ctx, const int64_t *d_stats_sum, int64_t out_cap, int64_t *n_out, int64_t *need_cap);
 
 /* ---- bulk CSV ingest ------------------------------------------------------ */
 /* Decodes '\n'-separated records "id,v1,...,vD" (a non-empty unterminated tail is one
@@ -241,6 +255,8 @@ int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t
  * distinct union of the local skylines; D compares per pair test */
 int sky_profile_dominance(sky_ctx *ctx, int64_t *work_out);
 int sky_profile_reset(sky_ctx *ctx);
+/* host synchronisations (device read-backs) the context has made since it was created */
+int sky_profile_host_syncs(sky_ctx *ctx, int64_t *n_out);
 /* the pipeline's device radix sort (k_radix.hip: onesweep LSD, 8-bit digits over the varying
  * key bits) run alone on n (u64 key, u32 value) pairs in place, for the sort-phase HBM
  * roofline at scale; *passes_out = digit passes, *ms_out = HIP-event time of the sort */

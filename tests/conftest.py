@@ -201,3 +201,60 @@ def gpu_engine_factory():
                 pytest.fail("no HIP device visible for a gpu-marked test: " + str(e))
             raise
     return make
+
+
+def dist_emulate(engs, d_ids, d_vals, cap=4096, steps=1, max_attempts=8):
+    """W ranks of the multi-GPU step emulated on one GPU: one engine (context) per rank, the
+    all-gather = concatenation of the ranks' device blocks, the all-reduce = a device sum
+    (the collectives RCCL performs between processes).  Returns, per step, the per-rank
+    (ids, origins) and the job-wide (|L_k|, survivors_k), plus per-step per-rank host
+    synchronisations and the attempts each step took."""
+    import torch
+    from skyline import _abi
+    from skyline.dist import block_words
+    W = len(engs)
+    D, K = engs[0].dims, engs[0].K
+    dev = d_vals[0].device
+    outs = []
+    for _ in range(steps):
+        h0 = [e.host_syncs() for e in engs]
+        oi = [torch.empty(max(v.shape[0], 1), dtype=torch.int64, device=dev) for v in d_vals]
+        oo = [torch.empty(max(v.shape[0], 1), dtype=torch.int32, device=dev) for v in d_vals]
+        export, attempts = True, 0
+        while True:
+            attempts += 1
+            assert attempts <= max_attempts
+            send = [torch.empty(block_words(cap, D), dtype=torch.int64, device=dev) for _ in range(W)]
+            for r, e in enumerate(engs):
+                if export:
+                    e.dist_export_dev(d_ids[r], d_vals[r], send[r], cap)
+                else:
+                    e.dist_reblock_dev(send[r], cap)
+            recv = torch.cat(send)
+            stats = [torch.empty(2 * K, dtype=torch.int64, device=dev) for _ in range(W)]
+            for r, e in enumerate(engs):
+                e.dist_merge_dev(recv, W, r, cap, oi[r], oo[r], d_vals[r].shape[0], stats[r])
+            tot = torch.stack(stats).sum(0)
+            res = [e.dist_finish(tot, d_vals[r].shape[0]) for r, e in enumerate(engs)]
+            rcs = {x[0] for x in res}
+            assert len(rcs) == 1, f"ranks disagree: {res}"
+            rc = rcs.pop()
+            if rc == _abi.SKY_OK:
+                break
+            if rc == _abi.SKY_E_RETRY:
+                export = True
+            else:
+                need = {x[2] for x in res}
+                assert len(need) == 1
+                cap = need.pop() + 64
+                export = False
+        got = [(oi[r][:res[r][1]].cpu().numpy(), oo[r][:res[r][1]].cpu().numpy()) for r in range(W)]
+        ls, sv = engs[0].stats()
+        for e in engs[1:]:
+            l2, s2 = e.stats()
+            np.testing.assert_array_equal(l2, ls)
+            np.testing.assert_array_equal(s2, sv)
+        outs.append({"ids": np.concatenate([g[0] for g in got]), "org": np.concatenate([g[1] for g in got]),
+                     "ls": ls, "sv": sv, "syncs": [e.host_syncs() - h for e, h in zip(engs, h0)],
+                     "attempts": attempts, "cap": cap})
+    return outs

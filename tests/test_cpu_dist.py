@@ -1,14 +1,17 @@
-"""gloo tests (CPU, world sizes 2 and 4) of the multi-GPU exchange in skyline/dist.py.
+"""gloo tests (CPU, world sizes 2 and 4) of the multi-GPU step's host protocol in skyline/dist.py.
 
-The device phases are stood in for by the oracle (test infrastructure): each rank reduces
-its shard to the distinct vectors of its local skylines with partition + multiplicity
-(sky_export_local_dev), the ranks exchange them with skyline.dist.allgather_varlen /
-pack_export / unpack_union over gloo, each rank decides the fate of ITS OWN vectors
-against the union (sky_import_union_dev's rule: in L_k iff no union vector of key k
-dominates it, in G iff no union vector dominates it), and the per-rank shares of |L_k| /
-survivors_k are summed by skyline.dist.allreduce_stats.  The result must equal the
-single-process answer, and each rank's global-phase work must be its share (|own| x
-|union|, about 1/G of the |union|^2 a replicated merge would cost)."""
+skyline.dist.distributed_query runs unchanged over a gloo group; the device phases behind the
+sky_dist_* contract are stood in for by a CPU model (the oracle is test infrastructure):
+  export  each rank reduces its shard to the distinct vectors of its local skylines with
+          partition + multiplicity, written as a fixed-capacity block (skyline.dist.pack_block);
+  merge   each rank decides the fate of ITS OWN vectors against the gathered union (in L_k iff no
+          union vector of key k dominates it, in G iff no union vector does) and emits its shard's
+          global-skyline ids and its share of |L_k| / survivors_k;
+  finish  every rank reads the same gathered headers: done, re-run the step (a rank's verdict says
+          its planned route missed), or re-run the exchange with a larger capacity.
+The result must equal the single-process answer on every rank, through a forced retry and a
+forced capacity regrow, with one host read per attempt, and each rank's global-phase work must
+be its share (|own| x |union|, about 1/G of the |union|^2 a replicated merge would cost)."""
 import os
 import socket
 import sys
@@ -19,6 +22,7 @@ import torch
 import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "flink-skyline-qos_amd")
 
 
 def _free_port():
@@ -29,97 +33,185 @@ def _free_port():
     return p
 
 
-def _local_export(orc, vals, P):
-    """distinct vectors of the local skylines of one shard, with partition + multiplicity"""
-    _, keys, _, _, inl = orc.query_sfs_chunked("angle", vals, P)
-    inl = inl.astype(bool)
-    rows = vals[inl]
-    ks = keys[inl]
-    uniq, cnt = np.unique(np.column_stack([ks, rows]), axis=0, return_counts=True)
-    return uniq[:, 1:].copy(), uniq[:, 0].astype(np.int32), cnt.astype(np.int64)
-
-
 def _dominates(a, b):
     return bool((a <= b).all() and (a < b).any())
 
 
-def _worker(rank, world, port, shards, P, D, ret):
+class ModelEngine:
+    """CPU model of the sky_dist_* contract (include/skyline_hip.h) with the oracle as the local
+    phase.  replan: verdicts to put into this rank's first exports (2 = planned route missed)."""
+
+    def __init__(self, orc, D, P, replan=0):
+        self.orc, self.dims, self.K, self.P = orc, D, P, P
+        self.replan = replan
+        self.syncs = 0
+        self.pairs = 0
+        self.last = None
+
+    def dist_export_dev(self, d_ids, d_vals, block, cap):
+        from skyline.dist import pack_block
+        vals, ids = d_vals.numpy(), d_ids.numpy()
+        _, keys, _, _, inl = self.orc.query_sfs_chunked("angle", vals, self.P)
+        inl = inl.astype(bool)
+        kv = np.column_stack([keys[inl], vals[inl]])
+        uniq, cnt = np.unique(kv, axis=0, return_counts=True) if len(kv) else (kv, np.zeros(0, np.int64))
+        self.shard = (ids, vals, keys, inl)
+        self.exp = (uniq[:, 1:].copy(), uniq[:, 0].astype(np.int64), cnt.astype(np.int64))
+        verdict = 2 if self.replan > 0 else 0
+        self.replan -= 1
+        block.copy_(pack_block(self.exp[0], self.exp[1], self.exp[2], cap, verdict, len(vals)))
+
+    def dist_reblock_dev(self, block, cap):
+        from skyline.dist import pack_block
+        block.copy_(pack_block(self.exp[0], self.exp[1], self.exp[2], cap, 0, len(self.shard[0])))
+
+    def dist_merge_dev(self, recv, world, rank, cap, oi, oo, out_cap, stats):
+        from skyline.dist import unpack_blocks
+        blocks = unpack_blocks(recv, world, cap, self.dims)
+        self.hdr = [(b[3], b[4]) for b in blocks]
+        self.cap = cap
+        u = np.concatenate([b[0].numpy() for b in blocks]) if blocks else np.zeros((0, self.dims))
+        uk = np.concatenate([b[1].numpy() for b in blocks])
+        own, ok, om = (x.numpy() for x in blocks[rank][:3])
+        ls = np.zeros(self.K, np.int64)
+        sv = np.zeros(self.K, np.int64)
+        in_g = set()
+        for j in range(len(own)):                 # own vectors only, each against the whole union
+            dom_l = dom_g = False
+            for i in range(len(u)):
+                self.pairs += 1
+                if _dominates(u[i], own[j]):
+                    dom_g = True
+                    if uk[i] == ok[j]:
+                        dom_l = True
+                        break
+            if not dom_l:
+                ls[ok[j]] += om[j]
+            if not dom_g:
+                sv[ok[j]] += om[j]
+                in_g.add((int(ok[j]),) + tuple(own[j].tolist()))
+        self.n_union, self.n_own = len(u), len(own)
+        ids, vals, keys, inl = self.shard
+        sel = [t for t in range(len(ids)) if inl[t] and (int(keys[t]),) + tuple(vals[t].tolist()) in in_g]
+        self.g = len(sel)
+        m = min(self.g, out_cap)
+        oi[:m] = torch.from_numpy(ids[sel][:m])
+        oo[:m] = torch.from_numpy(keys[sel][:m].astype(np.int32))
+        stats.copy_(torch.from_numpy(np.concatenate([ls, sv])))
+
+    def dist_finish(self, stats_sum, out_cap):
+        from skyline import _abi
+        self.syncs += 1                           # the one host read
+        maxc = max(c for c, _ in self.hdr)
+        anyv = 0
+        for _, v in self.hdr:
+            anyv |= v
+        if anyv & 2:
+            return _abi.SKY_E_RETRY, 0, 0
+        if maxc > self.cap:
+            return _abi.SKY_E_CAPACITY, 0, maxc
+        s = stats_sum.numpy()
+        self.last = (s[:self.K].copy(), s[self.K:].copy())
+        return _abi.SKY_OK, self.g, 0
+
+    def host_syncs(self):
+        return self.syncs
+
+    def phases(self):
+        return {}, np.array([0, 0, 0, self.n_own, self.g, self.n_union, 0, 8], np.int64)
+
+    def stats(self):
+        return self.last
+
+
+def _worker(rank, world, port, shards, P, D, cap0, replan_rank, ret):
     sys.path.insert(0, HERE)
-    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "flink-skyline-qos_amd"))
+    sys.path.insert(0, PKG)
     import torch.distributed as dist
     from conftest import Oracle
-    from skyline.dist import allgather_varlen, allreduce_stats, pack_export, unpack_union
+    from skyline.dist import DistExchange, distributed_query
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     orc = Oracle()
-    rows, keys, mult = _local_export(orc, shards[rank], P)
-    packed = pack_export(torch.from_numpy(rows), torch.from_numpy(keys), torch.from_numpy(mult))
-    gathered, counts = allgather_varlen(packed)
-    urows, ukeys, umult = unpack_union(gathered, counts, D)
-    assert sum(counts) == urows.shape[0]
-    off = sum(counts[:rank])
-    assert torch.equal(urows[off:off + counts[rank]], torch.from_numpy(rows))
-    u, uk = urows.numpy(), ukeys.numpy()
-    ls = np.zeros(P, np.int64)
-    sv = np.zeros(P, np.int64)
-    gvecs = []
-    pairs = 0
-    for j in range(counts[rank]):               # own vectors only, each against the whole union
-        y, ky = u[off + j], uk[off + j]
-        dom_l = dom_g = False
-        for i in range(len(u)):
-            pairs += 1
-            if _dominates(u[i], y):
-                dom_g = True
-                if uk[i] == ky:
-                    dom_l = True
-                    break
-        if not dom_l:
-            ls[ky] += mult[j]
-        if not dom_g:
-            sv[ky] += mult[j]
-            gvecs.append(tuple(y))
-    tls, tsv = allreduce_stats(ls, sv, torch.device("cpu"))
-    ret[rank] = (sorted(gvecs), tls.tolist(), tsv.tolist(), pairs, len(u))
+    eng = ModelEngine(orc, D, P, replan=1 if rank == replan_rank else 0)
+    eng._dist_ex = DistExchange(eng, torch.device("cpu"), world, cap=cap0)
+    vals = shards[rank]
+    base = sum(len(s) for s in shards[:rank])
+    dv = torch.from_numpy(vals)
+    di = torch.arange(base, base + len(vals), dtype=torch.int64)
+    oi = torch.empty(len(vals), dtype=torch.int64)
+    oo = torch.empty(len(vals), dtype=torch.int32)
+    g = distributed_query(eng, di, dv, oi, oo, len(vals))
+    ls, sv = eng.stats()
+    ex = eng._dist_ex
+    ret[rank] = (oi[:g].tolist(), oo[:g].tolist(), ls.tolist(), sv.tolist(), eng.pairs, eng.n_union,
+                 eng.last_dist_stats, ex.retries, ex.regrows, ex.cap)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_rank_exchange_equals_single_process(world, oracle):
-    n, D, P = 8000, 4, 8
-    vals = oracle.synth(0, D, n, seed=3 + world)
-    bounds = np.linspace(0, n, world + 1).astype(int)
-    shards = [vals[bounds[r]:bounds[r + 1]] for r in range(world)]
+def _run(world, vals, P, D, cap0=4096, replan_rank=-1):
+    bounds = np.linspace(0, len(vals), world + 1).astype(int)
+    shards = [np.ascontiguousarray(vals[bounds[r]:bounds[r + 1]]) for r in range(world)]
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     ret = mgr.dict()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, P, D, ret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, P, D, cap0, replan_rank, ret))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(180)
+        p.join(240)
         assert p.exitcode == 0
+    return [ret[r] for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_exchange_equals_single_process(world, oracle):
+    n, D, P = 6000, 4, 8
+    vals = oracle.synth(0, D, n, seed=3 + world)
+    res = _run(world, vals, P, D)
     exp, keys, els, esv = oracle.query_sfs("angle", vals, P)
-    exp_set = sorted({tuple(r) for r in vals[exp]})
-    got_set = sorted({v for r in range(world) for v in ret[r][0]})
-    assert got_set == exp_set
-    n_union = ret[0][4]
-    for r in range(world):
-        assert ret[r][1] == els.tolist()          # job-wide integers after the all-reduce
-        assert ret[r][2] == esv.tolist()
+    got = sorted(i for r in res for i in r[0])
+    assert got == exp.tolist()
+    org = dict(zip([i for r in res for i in r[0]], [o for r in res for o in r[1]]))
+    assert [org[i] for i in exp.tolist()] == keys[exp].tolist()
+    n_union = res[0][5]
+    for r in res:
+        assert r[2] == els.tolist() and r[3] == esv.tolist()      # job-wide integers on every rank
+        assert r[6]["host_syncs"] == 1 and r[6]["attempts"] == 1  # one host read per step
         # global-phase work of one rank: its own vectors against the union, ~1/G of |U|^2
-        assert ret[r][3] <= 1.6 * n_union * n_union / world
-    assert sum(ret[r][3] for r in range(world)) <= n_union * n_union
+        assert r[4] <= 1.6 * n_union * n_union / world
+    assert sum(r[4] for r in res) <= n_union * n_union
 
 
-def test_pack_unpack_roundtrip():
-    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "flink-skyline-qos_amd"))
-    from skyline.dist import pack_export, unpack_union
+def test_retry_and_capacity_regrow_agree_on_every_rank(oracle):
+    """Rank 1's first verdict says its planned route missed (every rank re-runs the step), and a
+    capacity of 2 vectors forces a regrow (every rank rewrites its block larger)."""
+    n, D, P, world = 4000, 3, 4, 2
+    vals = oracle.synth(3, D, n, seed=12)
+    res = _run(world, vals, P, D, cap0=2, replan_rank=1)
+    exp, keys, els, esv = oracle.query_sfs("angle", vals, P)
+    assert sorted(i for r in res for i in r[0]) == exp.tolist()
+    caps = {r[9] for r in res}
+    assert len(caps) == 1 and caps.pop() > 2                      # the same grown capacity everywhere
+    for r in res:
+        assert r[2] == els.tolist() and r[3] == esv.tolist()
+        assert r[7] == 1 and r[8] >= 1                            # one retry, at least one regrow
+        assert r[6]["host_syncs"] == r[6]["attempts"] == 1 + r[7] + r[8]
+
+
+def test_block_roundtrip():
+    sys.path.insert(0, PKG)
+    from skyline.dist import pack_block, unpack_blocks
     rows = torch.tensor([[0.0, -0.0, 1e300], [float("inf"), 2.5, -3.0]], dtype=torch.float64)
-    keys = torch.tensor([3, 15], dtype=torch.int32)
+    keys = torch.tensor([3, 15], dtype=torch.int64)
     mult = torch.tensor([7, 1], dtype=torch.int64)
-    pk = pack_export(rows, keys, mult)
-    stacked = torch.stack([pk, torch.zeros_like(pk)])
-    r, k, m = unpack_union(stacked, [2, 0], 3)
+    a = pack_block(rows, keys, mult, 4, verdict=2, n_tuples=9)
+    b = pack_block(rows[:0], keys[:0], mult[:0], 4)
+    c = pack_block(rows, keys, mult, 1)                        # overflow: count 2, one row held
+    (r, k, m, cnt, v), (r2, _, _, cnt2, _) = unpack_blocks(torch.cat([a, b]), 2, 4, 3)
     assert torch.equal(r.view(torch.int64), rows.view(torch.int64))   # bit-preserving (keeps -0.0)
-    assert k.tolist() == [3, 15] and m.tolist() == [7, 1]
+    assert k.tolist() == [3, 15] and m.tolist() == [7, 1] and cnt == 2 and v == 2 and cnt2 == 0
+    assert r2.shape == (0, 3)
+    (r3, _, _, cnt3, _), = unpack_blocks(c, 1, 1, 3)
+    assert cnt3 == 2 and r3.shape == (1, 3)

@@ -14,6 +14,7 @@ which equals the oracle's generator bit for bit (test_gpu_engine.py).
 import numpy as np
 import pytest
 import torch
+from conftest import dist_emulate
 
 pytestmark = pytest.mark.gpu
 
@@ -143,6 +144,23 @@ def test_stream_nan_append_is_rejected_and_stream_stays_queryable(gpu_engine_fac
 
 
 # ---- C2 / C3 / C4 at full size -----------------------------------------------------------
+def test_c1_dim_2d_uniform_1m(gpu_engine_factory, oracle):
+    """C1 at its stated size: MR-Dim, 2D independent (uniform), 1M tuples, P = 8 (Flink
+    parallelism 4).  Checked against the chunked oracle AND the literal per-key BNL restatement
+    with 5000-tuple buffers (FlinkSkyline.java:417-444, :548-566), ids and integers."""
+    D, P_, n = 2, 8, 1_000_000
+    eng = gpu_engine_factory(D, P_, "mr-dim")
+    dv, di = device_stream(eng, "uniform", n, seed=1234 + D)
+    got = query_dev(eng, dv, di)
+    eng.close()
+    vals = dv.cpu().numpy()
+    exp = check_full(oracle, "dim", vals, P_, got)
+    g, keys, ls, sv = oracle.query_bnl("dim", vals, np.arange(n, dtype=np.int64), P_)
+    np.testing.assert_array_equal(np.sort(g), exp)
+    np.testing.assert_array_equal(ls, got[2])
+    np.testing.assert_array_equal(sv, got[3])
+
+
 def test_c2_grid_4d_correlated_10m(gpu_engine_factory, oracle, monkeypatch):
     D, P_, n = 4, 8, 10_000_000
     eng = gpu_engine_factory(D, P_, "mr-grid")
@@ -160,7 +178,8 @@ def test_c2_grid_4d_correlated_10m(gpu_engine_factory, oracle, monkeypatch):
 
 def test_c3_angle_4d_anti_50m_one_gpu_and_sharded(gpu_engine_factory, oracle):
     """C3 on one GPU, and the same stream split into 2, 4 and 8 rank shards run through the
-    multi-GPU decomposition (export -> union -> import, one context per emulated rank):
+    multi-GPU step (sky_dist_export -> all-gather -> sky_dist_merge -> all-reduce ->
+    sky_dist_finish, one context per emulated rank):
     every decomposition returns the one-GPU ids, origins, |L_k| and survivors_k."""
     D, P_, n = 4, 8, 50_000_000
     eng = gpu_engine_factory(D, P_, "mr-angle")
@@ -175,38 +194,14 @@ def test_c3_angle_4d_anti_50m_one_gpu_and_sharded(gpu_engine_factory, oracle):
     for W in (2, 4, 8):
         bounds = np.linspace(0, n, W + 1).astype(np.int64)
         engs = [gpu_engine_factory(D, P_, "mr-angle") for _ in range(W)]
-        exports = []
-        for r, e in enumerate(engs):
-            lo, hi = int(bounds[r]), int(bounds[r + 1])
-            ne = e.export_local_dev(di[lo:hi], dv[lo:hi])
-            rows = torch.empty((max(ne, 1), D), dtype=torch.float64, device="cuda")
-            keys = torch.empty(max(ne, 1), dtype=torch.int32, device="cuda")
-            mult = torch.empty(max(ne, 1), dtype=torch.int64, device="cuda")
-            e.export_copy_dev(rows, keys, mult, ne)
-            e.sync()
-            exports.append((rows[:ne], keys[:ne], mult[:ne]))
-        urows = torch.cat([x[0] for x in exports]).contiguous()
-        ukeys = torch.cat([x[1] for x in exports]).contiguous()
-        umult = torch.cat([x[2] for x in exports]).contiguous()
-        off, ids_all, org_all = 0, [], []
-        tot_ls, tot_sv = np.zeros_like(got[2]), np.zeros_like(got[3])
-        for r, e in enumerate(engs):
-            lo, hi = int(bounds[r]), int(bounds[r + 1])
-            oi = torch.empty(hi - lo, dtype=torch.int64, device="cuda")
-            oo = torch.empty(hi - lo, dtype=torch.int32, device="cuda")
-            g = e.import_union_dev(urows, ukeys, umult, urows.shape[0], off, oi, oo, hi - lo)
-            e.sync()
-            ids_all.append(oi[:g].cpu().numpy())
-            org_all.append(oo[:g].cpu().numpy())
-            ls, sv = e.stats()                   # this rank's share of the optimality integers
-            tot_ls += ls
-            tot_sv += sv
-            off += exports[r][0].shape[0]
+        sl = [slice(int(bounds[r]), int(bounds[r + 1])) for r in range(W)]
+        out = dist_emulate(engs, [di[x] for x in sl], [dv[x] for x in sl])[0]
+        for e in engs:
             e.close()
-        np.testing.assert_array_equal(tot_ls, got[2])
-        np.testing.assert_array_equal(tot_sv, got[3])
-        np.testing.assert_array_equal(np.concatenate(ids_all), got[0])
-        np.testing.assert_array_equal(np.concatenate(org_all), got[1])
+        np.testing.assert_array_equal(out["ls"], got[2])
+        np.testing.assert_array_equal(out["sv"], got[3])
+        np.testing.assert_array_equal(out["ids"], got[0])
+        np.testing.assert_array_equal(out["org"], got[1])
     del dv, di
     torch.cuda.empty_cache()
 
@@ -229,6 +224,34 @@ def test_c4_angle_8d_anti_100m(gpu_engine_factory, oracle):
     del dv, di
     torch.cuda.empty_cache()
     check_full(oracle, "angle", vals, P_, (gi, go, ls, sv))
+
+
+def test_c4_8way_decomposition(gpu_engine_factory):
+    """C4 as configured (100M 8D tuples over 8 GPUs): the whole stream split into 8 rank shards
+    run through the multi-GPU step (one context per emulated rank, the collectives as device
+    concatenation / sum) equals the one-GPU query: ids, origins, |L_k|, survivors_k.  Steps
+    after the first replay the planned route: exactly ONE host read per rank per step."""
+    D, P_, n, W = 8, 16, 100_000_000, 8
+    eng = gpu_engine_factory(D, P_, "mr-angle")
+    dv, di = device_stream(eng, "anti_correlated", n, seed=1242)
+    gi, go, ls, sv = query_dev(eng, dv, di)
+    eng.close()
+    bounds = np.linspace(0, n, W + 1).astype(np.int64)
+    sl = [slice(int(bounds[r]), int(bounds[r + 1])) for r in range(W)]
+    engs = [gpu_engine_factory(D, P_, "mr-angle") for _ in range(W)]
+    outs = dist_emulate(engs, [di[x] for x in sl], [dv[x] for x in sl], steps=3)
+    for e in engs:
+        e.close()
+    for out in outs:
+        np.testing.assert_array_equal(out["ids"], gi)
+        np.testing.assert_array_equal(out["org"], go)
+        np.testing.assert_array_equal(out["ls"], ls)
+        np.testing.assert_array_equal(out["sv"], sv)
+    for out in outs[1:]:
+        assert out["attempts"] == 1
+        assert out["syncs"] == [1] * W, out["syncs"]
+    del dv, di
+    torch.cuda.empty_cache()
 
 
 # ---- MR-Grid with no queried tuple (advisor round 1) -------------------------------------

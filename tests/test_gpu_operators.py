@@ -97,7 +97,9 @@ def test_run_job_barrier_triggers(oracle):
 
 
 def test_multi_rank_decomposition(gpu_engine_factory, oracle):
-    """Export/import of 3 shards == one query over the whole stream (ids, stats)."""
+    """The multi-GPU step (sky_dist_*) over 3 emulated ranks == one query over the whole
+    stream (ids, origins, |L_k|, survivors_k)."""
+    from conftest import dist_emulate
     n, D, P, W = 90000, 6, 16, 3
     vals = oracle.synth(2, D, n, seed=31)
     ids = np.arange(n, dtype=np.int64)
@@ -109,38 +111,11 @@ def test_multi_rank_decomposition(gpu_engine_factory, oracle):
     shards = np.array_split(np.arange(n), W)
     dv = [torch.from_numpy(vals[s]).cuda() for s in shards]
     di = [torch.from_numpy(ids[s]).cuda() for s in shards]
-    exports = []
-    for e, v, i in zip(engs, dv, di):
-        ne = e.export_local_dev(i, v)
-        rows = torch.empty((max(ne, 1), D), dtype=torch.float64, device="cuda")
-        keys = torch.empty(max(ne, 1), dtype=torch.int32, device="cuda")
-        mult = torch.empty(max(ne, 1), dtype=torch.int64, device="cuda")
-        e.export_copy_dev(rows, keys, mult, ne)
-        e.sync()
-        exports.append((rows[:ne], keys[:ne], mult[:ne]))
-    urows = torch.cat([x[0] for x in exports]).contiguous()
-    ukeys = torch.cat([x[1] for x in exports]).contiguous()
-    umult = torch.cat([x[2] for x in exports]).contiguous()
-    assert int(umult.sum()) <= n
-    got = []
-    off = 0
-    tot_ls, tot_sv = np.zeros_like(exp_ls), np.zeros_like(exp_sv)
-    for r, (e, s) in enumerate(zip(engs, shards)):
-        oi = torch.empty(len(s), dtype=torch.int64, device="cuda")
-        oo = torch.empty(len(s), dtype=torch.int32, device="cuda")
-        g = e.import_union_dev(urows, ukeys, umult, urows.shape[0], off, oi, oo, len(s))
-        e.sync()
-        got.append((oi[:g].cpu().numpy(), oo[:g].cpu().numpy()))
-        off += exports[r][0].shape[0]
-        ls, sv = e.stats()                       # this rank's share: summed over the ranks
-        tot_ls += ls
-        tot_sv += sv
-    np.testing.assert_array_equal(tot_ls, exp_ls)
-    np.testing.assert_array_equal(tot_sv, exp_sv)
-    gi = np.concatenate([x[0] for x in got])
-    go = np.concatenate([x[1] for x in got])
-    np.testing.assert_array_equal(gi, exp_ids)
-    np.testing.assert_array_equal(go, exp_org)
+    for out in dist_emulate(engs, di, dv, steps=2):
+        np.testing.assert_array_equal(out["ls"], exp_ls)
+        np.testing.assert_array_equal(out["sv"], exp_sv)
+        np.testing.assert_array_equal(out["ids"], exp_ids)
+        np.testing.assert_array_equal(out["org"], exp_org)
     for e in engs:
         e.close()
 

@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-3 GPU pass: STEPS (comma list) of
+#   dist   the multi-GPU step tests (emulated ranks, 2-process gloo, C4 8-way)
+#   tests  the whole gpu suite
+#   bench  bench.py (BENCH_ARGS), its JSON line to gpurun_out/bench_$TAG.json
+#   rehearse  bench.py --gpus 2 --dist-backend gloo (self-launched ranks on one GPU)
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -e
+R=$GRAFT_REPO_ROOT; [ -z "$R" ] && R=$(pwd)
+OUT=$R/gpurun_out; mkdir -p $OUT
+cd $R
+TAG=${TAG:-r03}
+STEPS=${STEPS:-dist}
+export PYTHONUNBUFFERED=1
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+if [[ $STEPS == *dist* ]]; then
+  timeout -k 10 900 $PYT tests/test_gpu_dist_step.py tests/test_gpu_dist.py \
+      "tests/test_gpu_operators.py::test_multi_rank_decomposition" "tests/test_gpu_configs.py::test_c4_8way_decomposition" \
+      ${DIST_EXTRA} > $OUT/pytest_dist_$TAG.log 2>&1 || { tail -60 $OUT/pytest_dist_$TAG.log; exit 1; }
+  tail -4 $OUT/pytest_dist_$TAG.log
+fi
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 1000 $PYT tests -m gpu ${TEST_EXTRA} > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
+  tail -4 $OUT/pytest_gpu_$TAG.log
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 500 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
+  cut -c1-1500 $OUT/bench_$TAG.json
+fi
+if [[ $STEPS == *rehearse* ]]; then
+  timeout -k 10 400 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 2 --tuples ${REH_TUPLES:-50000000} \
+      > $OUT/bench_gloo2_$TAG.json 2> $OUT/bench_gloo2_$TAG.err || { tail -30 $OUT/bench_gloo2_$TAG.err; exit 1; }
+  grep '^{' $OUT/bench_gloo2_$TAG.json | cut -c1-1500
+fi
+if [[ $STEPS == *union* ]]; then
+  timeout -k 10 300 python -u tools/dist_union_bench.py ${UNION_PER:-2000000} ${UNION_W:-4} > $OUT/dist_union_$TAG.json 2> $OUT/dist_union_$TAG.err || { tail -30 $OUT/dist_union_$TAG.err; exit 1; }
+  cat $OUT/dist_union_$TAG.json
+fi
+if [[ $STEPS == *mbrpmc* ]]; then
+  TAG=$TAG NS="${MBR_NS:-2000000 10000000}" bash tools/gpu_mbr_pmc.sh
+fi

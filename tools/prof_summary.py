@@ -116,6 +116,9 @@ def main():
     out = os.path.join(REPO, "profiles", "traffic_filter.json")
     old = json.load(open(out)) if os.path.exists(out) else {}
     old.update({k: v for k, v in res.items() if k != "avg"})
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from src_hash import kernel_src_sha
+    old["kernel_src_sha"] = kernel_src_sha("k_filter")     # bench.py reports it for this build only
     old.setdefault("counters", {}).update(res["avg"])
     c = old["counters"]
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
