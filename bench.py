@@ -453,59 +453,88 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
             "roofline": roof}
 
 
-def operator_run(dev_index, n=10_000_000, buf=5000):
+def operator_run(dev_index, n=10_000_000, buf=5000, micro=80_000):
     """The drop-in operator path (FlinkSkyline.java:265-316, :417-444,
-    :515-569) on the first n tuples of the C4 stream: per-key 5000-tuple flushes through
-    sky_part_insert (host buffers, as the JNI shim passes them) in stream order of their
-    5000th tuple, then at the trigger: the partial buffers flushed, every key's snapshot, and
-    sky_global_merge of the P local skylines.  Per-flush latency = one sky_part_insert call."""
+    :515-569) on the first n tuples of the C4 stream, from host memory as the JNI shim passes
+    it.  Tuples are routed to per-key 5000-tuple buffers in stream order; after every micro-batch
+    of `micro` tuples (Kafka poll granularity) the keys whose buffers are full are flushed in ONE
+    sky_parts_insert call (asynchronous: no host read).  At the trigger: the partial buffers are
+    flushed, every key's snapshot taken (the one synchronisation), and sky_global_merge run over
+    the P local skylines.  Reported: tuples/s end to end, per-call latency (p50 / p99, host time
+    of one sky_parts_insert), and the same stream with one sky_part_insert per full buffer."""
     import numpy as np
     from skyline.operators import _LocalPart
     D, P = 8, 16
     vals, ids = skyline.synth_host(_abi.DISTS["anti_correlated"], D, n, seed=1234 + D)
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
+    eng.warmup()
     keys = eng.partition_keys(vals)
-    events = []                                # (stream position of the flush, key, lo, hi) over order_k
-    per_key = {}
-    for k in range(P):
-        idx = np.flatnonzero(keys == k)
-        per_key[k] = idx
-        for lo in range(0, len(idx) - len(idx) % buf, buf):
-            events.append((int(idx[lo + buf - 1]), k, lo, lo + buf))
-    events.sort()
-    parts = {k: _LocalPart(eng, k) for k in range(P)}
+    order = np.argsort(keys, kind="stable")
+    starts = np.searchsorted(keys[order], np.arange(P + 1))
+    per_key = {k: order[starts[k]:starts[k + 1]] for k in range(P)}    # stream order within a key
     batches = {k: (np.ascontiguousarray(ids[per_key[k]]), np.ascontiguousarray(vals[per_key[k]])) for k in range(P)}
-    lat = []
-    t0 = time.perf_counter()
-    for _, k, lo, hi in events:
-        bi, bv = batches[k]
-        ts = time.perf_counter()
-        parts[k].insert(bi[lo:hi], bv[lo:hi])
-        lat.append((time.perf_counter() - ts) * 1e3)
-    t_ins = time.perf_counter() - t0
-    tq = time.perf_counter()
-    for k in range(P):                         # processQuery: flush the partial buffer (:387)
-        bi, bv = batches[k]
-        rem = len(bi) % buf
-        if rem:
-            parts[k].insert(bi[len(bi) - rem:], bv[len(bv) - rem:])
-    snaps = [parts[k].snapshot() for k in range(P)]
-    gids, _ = eng.global_merge(list(range(P)), [sn[0] for sn in snaps], [sn[1] for sn in snaps])
-    t_q = time.perf_counter() - tq
-    total = time.perf_counter() - t0
-    local_sizes = [len(sn[0]) for sn in snaps]
-    for pt in parts.values():
-        pt.close()
+    # the flush schedule: after micro-batch m, the buffers that filled up during it, one call per
+    # round (a key whose buffer filled r times in the micro-batch appears in the first r calls)
+    sched = []
+    done = {k: 0 for k in range(P)}
+    for m0 in range(0, n, micro):
+        lim = m0 + micro
+        full = {}
+        for k in range(P):
+            nfull = int(np.searchsorted(per_key[k], lim)) // buf
+            full[k] = list(range(done[k], nfull))
+            done[k] = nfull
+        for r in range(max(len(v) for v in full.values())):
+            call = [(k, f[r] * buf, (f[r] + 1) * buf) for k, f in full.items() if r < len(f)]
+            if call:
+                sched.append(call)
+
+    def run(batched):
+        parts = {k: _LocalPart(eng, k) for k in range(P)}
+        lat = []
+        t0 = time.perf_counter()
+        for call in sched:
+            ts = time.perf_counter()
+            if batched:
+                _LocalPart.insert_many([parts[k] for k, _, _ in call],
+                                       [(batches[k][0][lo:hi], batches[k][1][lo:hi]) for k, lo, hi in call])
+            else:
+                for k, lo, hi in call:
+                    parts[k].insert(batches[k][0][lo:hi], batches[k][1][lo:hi])
+            lat.append((time.perf_counter() - ts) * 1e3)
+        t_ins = time.perf_counter() - t0
+        tq = time.perf_counter()
+        rest = [k for k in range(P) if len(batches[k][0]) % buf]
+        _LocalPart.insert_many([parts[k] for k in rest],
+                               [(batches[k][0][done[k] * buf:], batches[k][1][done[k] * buf:]) for k in rest])
+        snaps = [parts[k].snapshot() for k in range(P)]     # processQuery: the one synchronisation
+        gids, _ = eng.global_merge(list(range(P)), [sn[0] for sn in snaps], [sn[1] for sn in snaps])
+        t_q = time.perf_counter() - tq
+        total = time.perf_counter() - t0
+        local_sizes = [len(sn[0]) for sn in snaps]
+        for pt in parts.values():
+            pt.close()
+        lat.sort()
+        nflush = sum(len(cl) for cl in sched)
+        return {"calls": len(lat), "flushes": nflush, "insert_phase_s": t_ins, "query_phase_s": t_q,
+                "tuples_per_s": n / total, "ingest_tuples_per_s": (nflush * buf) / t_ins if t_ins else None,
+                "p50_call_ms": lat[len(lat) // 2] if lat else None,
+                "p99_call_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
+                "max_call_ms": lat[-1] if lat else None,
+                "skyline_size": int(len(gids)), "local_sizes": local_sizes, "skyline_ids": gids}
+
+    run(True)                                          # first launches / allocations
+    b = run(True)
+    s1 = run(False)
+    exp = eng.query(vals, ids)[0]
+    exact = bool(np.array_equal(np.sort(b.pop("skyline_ids")), exp) and
+                 np.array_equal(np.sort(s1.pop("skyline_ids")), exp))
     eng.close()
-    lat.sort()
-    return {"workload": f"C4 stream prefix, {n} tuples, MR-Angle P={P}, per-key {buf}-tuple flushes from host memory "
-                        f"through sky_part_insert, then snapshots + sky_global_merge",
-            "flushes": len(lat), "insert_phase_s": t_ins, "query_phase_s": t_q,
-            "tuples_per_s": n / total, "ingest_tuples_per_s": (len(lat) * buf) / t_ins,
-            "p50_flush_ms": lat[len(lat) // 2] if lat else None,
-            "p99_flush_ms": lat[int(len(lat) * 0.99)] if lat else None,
-            "max_flush_ms": lat[-1] if lat else None,
-            "skyline_size": int(len(gids)), "local_sizes": local_sizes}
+    return {"workload": f"C4 stream prefix, {n} tuples, MR-Angle P={P}, per-key {buf}-tuple buffers from host memory; "
+                        f"the full buffers flushed after every {micro}-tuple micro-batch in one sky_parts_insert "
+                        f"call, then snapshots + sky_global_merge",
+            "exact_vs_whole_stream_query": exact, "batched": b, "one_call_per_buffer": s1,
+            "tuples_per_s": b["tuples_per_s"], "p50_call_ms": b["p50_call_ms"], "p99_call_ms": b["p99_call_ms"]}
 
 
 def sort_run(eng, n, dev, steps=3):

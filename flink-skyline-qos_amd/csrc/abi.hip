@@ -123,6 +123,25 @@ int sky_ctx_signal_stream(sky_ctx *c, void *s) {
     return SKY_OK;
 }
 
+int sky_ctx_info(sky_ctx *c, int32_t *dims, int32_t *num_partitions, int32_t *algo) {
+    ARG_CHECK(c, "ctx is null");
+    if (dims) *dims = c->D;
+    if (num_partitions) *num_partitions = c->P;
+    if (algo) *algo = c->algo;
+    return SKY_OK;
+}
+int sky_part_info(sky_part *p, int32_t *key, int32_t *dims) {
+    ARG_CHECK(p && p->ctx, "part is null");
+    if (key) *key = p->key;
+    if (dims) *dims = p->ctx->D;
+    return SKY_OK;
+}
+int sky_stream_info(sky_stream *s, int32_t *dims) {
+    ARG_CHECK(s && s->ctx, "stream is null");
+    if (dims) *dims = s->ctx->D;
+    return SKY_OK;
+}
+
 int sky_ctx_sync(sky_ctx *c) {
     ARG_CHECK(c, "ctx is null");
     SKY_TRY(bind(c));
@@ -219,6 +238,7 @@ int sky_query_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values, int6
     in.out_ids = d_ids_out;
     in.out_org = d_origin_out;
     in.out_cap = cap;
+    in.planes_ok = true;            // the run's own write pass makes the output
     c->shard_valid = false;
     int r = pipe_run(*c, c->main, in, c->profile >= 2 ? &c->pt : nullptr);
     if (r == SKY_OK) {
@@ -253,6 +273,7 @@ int sky_query(sky_ctx *c, const int64_t *ids, const double *values, int64_t n, i
     in.out_ids = c->h_out_ids.as<int64_t>();
     in.out_org = c->h_out_org.as<int32_t>();
     in.out_cap = n;
+    in.planes_ok = true;
     c->shard_valid = false;
     if (c->profile >= 2) {
         if (!c->pt.ok) c->pt.init();
@@ -369,188 +390,6 @@ int sky_global_merge(sky_ctx *c, int nparts, const int32_t *part_ids, const int6
     HIP_TRY(hipStreamSynchronize(c->st));
     if (origin_out)
         for (int64_t j = 0; j < g; j++) origin_out[j] = part_ids ? part_ids[o[j]] : o[j];
-    return SKY_OK;
-    GUARD_END
-}
-
-// ---- local operator state ----------------------------------------------------------
-int sky_part_open(sky_ctx *c, int32_t key, sky_part **out) {
-    GUARD_BEGIN
-    ARG_CHECK(c && out, "null argument");
-    sky_part *p = new sky_part();
-    p->ctx = c;
-    p->key = key;
-    *out = p;
-    return SKY_OK;
-    GUARD_END
-}
-
-int sky_part_close(sky_part *p) {
-    if (!p) return SKY_OK;
-    hipSetDevice(p->ctx->dev);
-    hipStreamSynchronize(p->ctx->st);
-    delete p;
-    return SKY_OK;
-}
-
-int sky_part_size(sky_part *p, int64_t *n_out) {
-    ARG_CHECK(p && n_out, "null argument");
-    *n_out = (int64_t)p->T - (int64_t)p->Tdead;
-    return SKY_OK;
-}
-
-// grow a state buffer keeping its first `used` bytes (doubling: amortised O(1) per tuple)
-static int grow_keep(DevBuf &b, size_t need, size_t used, hipStream_t st) {
-    if (need <= b.cap && b.p) return SKY_OK;
-    DevBuf nb;
-    SKY_TRY(nb.ensure(std::max(need, b.cap * 2)));
-    if (used) HIP_TRY(hipMemcpyAsync(nb.p, b.p, used, hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipStreamSynchronize(st));       // the old buffer is freed below
-    b = std::move(nb);
-    return SKY_OK;
-}
-
-static int part_read_words(sky_part *p, hipStream_t st, uint32_t nwords) {
-    if (!p->pin && hipHostMalloc(&p->pin, 256, hipHostMallocDefault) != hipSuccess) {
-        p->pin = nullptr;
-        set_error("hipHostMalloc failed");
-        return SKY_E_NOMEM;
-    }
-    HIP_TRY(hipMemcpyAsync(p->pin, p->words.p, (size_t)nwords * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    return SKY_OK;
-}
-
-// drop the dead reps and their tuples (order kept)
-static int part_compact(sky_part *p) {
-    sky_ctx *c = p->ctx;
-    hipStream_t st = c->st;
-    const int D = c->D;
-    const uint32_t R = p->R, T = p->T;
-    SKY_TRY(p->rk.ensure((size_t)R * 4 + 4));
-    SKY_TRY(p->rp.ensure((size_t)R * 4 + 4));
-    SKY_TRY(p->tk.ensure((size_t)T * 4 + 4));
-    SKY_TRY(p->tp.ensure((size_t)T * 4 + 4));
-    SKY_TRY(p->rrows2.ensure(std::max<size_t>(p->rrows.cap, 256)));
-    SKY_TRY(p->ralive2.ensure(std::max<size_t>(p->ralive.cap, 256)));
-    SKY_TRY(p->rcnt2.ensure(std::max<size_t>(p->rcnt.cap, 256)));
-    SKY_TRY(p->tids2.ensure(std::max<size_t>(p->tids.cap, 256)));
-    SKY_TRY(p->trep2.ensure(std::max<size_t>(p->trep.cap, 256)));
-    SKY_TRY(p->scratch.ensure(scan_scratch_words((size_t)std::max(R, T) + 1) * 4 + 64));
-    uint32_t *w = p->words.as<uint32_t>();
-    launch_part_rkeep(R, p->ralive.as<uint8_t>(), p->rk.as<uint32_t>(), st);
-    scan_excl_u32(p->rk.as<uint32_t>(), p->rp.as<uint32_t>(), R, w + 8, p->scratch.as<uint32_t>(), st);
-    launch_part_rmove(D, R, p->rk.as<uint32_t>(), p->rp.as<uint32_t>(), p->rrows.as<double>(), p->rcnt.as<uint32_t>(),
-                      p->rrows2.as<double>(), p->rcnt2.as<uint32_t>(), p->ralive2.as<uint8_t>(), st);
-    launch_part_tkeep(T, p->trep.as<uint32_t>(), p->ralive.as<uint8_t>(), p->tk.as<uint32_t>(), st);
-    scan_excl_u32(p->tk.as<uint32_t>(), p->tp.as<uint32_t>(), T, w + 9, p->scratch.as<uint32_t>(), st);
-    launch_part_tmove(T, p->tk.as<uint32_t>(), p->tp.as<uint32_t>(), p->rp.as<uint32_t>(), p->tids.as<int64_t>(),
-                      p->trep.as<uint32_t>(), p->tids2.as<int64_t>(), p->trep2.as<uint32_t>(), st);
-    HIP_TRY(hipGetLastError());
-    SKY_TRY(part_read_words(p, st, 10));
-    const uint32_t *h = (const uint32_t *)p->pin;
-    std::swap(p->rrows, p->rrows2);
-    std::swap(p->ralive, p->ralive2);
-    std::swap(p->rcnt, p->rcnt2);
-    std::swap(p->tids, p->tids2);
-    std::swap(p->trep, p->trep2);
-    p->R = h[8];
-    p->T = h[9];
-    p->Tdead = 0;
-    return SKY_OK;
-}
-
-// SkylineLocalProcessor.processBuffer (FlinkSkyline.java:417-444): S <- SKY(S u B), with
-// the state held as distinct vectors (k_part.hip) — no re-run over S
-int sky_part_insert(sky_part *p, const int64_t *ids, const double *values, int64_t n) {
-    GUARD_BEGIN
-    ARG_CHECK(p && (n == 0 || (ids && values)), "null argument");
-    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
-    if (n == 0) return SKY_OK;
-    sky_ctx *c = p->ctx;
-    SKY_TRY(bind(c));
-    hipStream_t st = c->st;
-    const int D = c->D;
-    const uint32_t nb = (uint32_t)n, R = p->R, T = p->T;
-    ARG_CHECK((uint64_t)T + nb < 0xffffffffull && (uint64_t)R + nb < 0xffffffffull, "partition state too large");
-    // batch workspace
-    SKY_TRY(p->bids.ensure((size_t)nb * 8));
-    SKY_TRY(p->bvals.ensure((size_t)nb * D * 8));
-    for (DevBuf *b : {&p->dom_b, &p->eq_s, &p->eq_b, &p->keep, &p->keep_pos, &p->fresh, &p->fresh_pos})
-        SKY_TRY(b->ensure((size_t)nb * 4));
-    SKY_TRY(p->dom_s.ensure((size_t)std::max<uint32_t>(R, 1) * 4));
-    SKY_TRY(p->scratch.ensure(scan_scratch_words((size_t)nb + 1) * 4 + 64));
-    SKY_TRY(p->words.ensure(256));
-    // state capacity (contents kept)
-    SKY_TRY(grow_keep(p->rrows, ((size_t)R + nb) * D * 8, (size_t)R * D * 8, st));
-    SKY_TRY(grow_keep(p->ralive, (size_t)R + nb, R, st));
-    SKY_TRY(grow_keep(p->rcnt, ((size_t)R + nb) * 4, (size_t)R * 4, st));
-    SKY_TRY(grow_keep(p->tids, ((size_t)T + nb) * 8, (size_t)T * 8, st));
-    SKY_TRY(grow_keep(p->trep, ((size_t)T + nb) * 4, (size_t)T * 4, st));
-    HIP_TRY(hipMemcpyAsync(p->bids.p, ids, (size_t)nb * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(p->bvals.p, values, (size_t)nb * D * 8, hipMemcpyHostToDevice, st));
-    uint32_t *w = p->words.as<uint32_t>();   // [0] NaN, [1] kept, [2] new reps, [4..5] dead tuples
-    FillSet fill;
-    fill.add(p->dom_b.p, (size_t)nb * 4);
-    fill.add(p->eq_s.p, (size_t)nb * 4, 0xff);
-    fill.add(p->eq_b.p, (size_t)nb * 4, 0xff);
-    if (R) fill.add(p->dom_s.p, (size_t)R * 4);
-    fill.add(p->words.p, 64);
-    fill.add(p->rcnt.as<uint32_t>() + R, (size_t)nb * 4);
-    HIP_TRY(fill.launch(st));
-    launch_nan_any(p->bvals.as<double>(), (size_t)nb * D, w, st);
-    const double *bv = p->bvals.as<double>();
-    launch_part_pairs(D, bv, nb, bv, nb, nullptr, true, w, p->dom_b.as<uint32_t>(), p->eq_b.as<uint32_t>(), st);
-    launch_part_pairs(D, bv, nb, p->rrows.as<double>(), R, p->ralive.as<uint8_t>(), false, w,
-                      p->dom_b.as<uint32_t>(), p->eq_s.as<uint32_t>(), st);
-    launch_part_pairs(D, p->rrows.as<double>(), R, bv, nb, nullptr, false, w, p->dom_s.as<uint32_t>(), nullptr, st);
-    launch_part_flags(nb, p->dom_b.as<uint32_t>(), p->eq_s.as<uint32_t>(), p->eq_b.as<uint32_t>(),
-                      p->keep.as<uint32_t>(), p->fresh.as<uint32_t>(), st);
-    scan_excl_u32(p->keep.as<uint32_t>(), p->keep_pos.as<uint32_t>(), nb, w + 1, p->scratch.as<uint32_t>(), st);
-    scan_excl_u32(p->fresh.as<uint32_t>(), p->fresh_pos.as<uint32_t>(), nb, w + 2, p->scratch.as<uint32_t>(), st);
-    launch_part_write(D, nb, p->bids.as<int64_t>(), bv, p->keep.as<uint32_t>(), p->keep_pos.as<uint32_t>(),
-                      p->fresh.as<uint32_t>(), p->fresh_pos.as<uint32_t>(), p->eq_s.as<uint32_t>(),
-                      p->eq_b.as<uint32_t>(), R, T, w, p->rrows.as<double>(), p->ralive.as<uint8_t>(),
-                      p->rcnt.as<uint32_t>(), p->tids.as<int64_t>(), p->trep.as<uint32_t>(), st);
-    launch_part_kill(R, p->dom_s.as<uint32_t>(), w, p->ralive.as<uint8_t>(), p->rcnt.as<uint32_t>(),
-                     (unsigned long long *)(w + 4), st);
-    HIP_TRY(hipGetLastError());
-    SKY_TRY(part_read_words(p, st, 6));
-    const uint32_t *h = (const uint32_t *)p->pin;
-    if (h[0]) {
-        set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; batch rejected");
-        return SKY_E_NAN;
-    }
-    p->T = T + h[1];
-    p->R = R + h[2];
-    p->Tdead += ((const unsigned long long *)(h + 4))[0];
-    if (p->Tdead && p->Tdead * 2 > p->T) SKY_TRY(part_compact(p));
-    return SKY_OK;
-    GUARD_END
-}
-
-int sky_part_snapshot(sky_part *p, int64_t *ids_out, double *values_out, int64_t cap, int64_t *n_out) {
-    GUARD_BEGIN
-    ARG_CHECK(p, "null part");
-    const int64_t live = (int64_t)p->T - (int64_t)p->Tdead;
-    if (n_out) *n_out = live;
-    if (live > cap) {
-        set_error("snapshot capacity too small");
-        return SKY_E_CAPACITY;
-    }
-    if (live == 0) return SKY_OK;
-    sky_ctx *c = p->ctx;
-    SKY_TRY(bind(c));
-    if (p->Tdead) SKY_TRY(part_compact(p));
-    const int D = c->D;
-    if (ids_out) HIP_TRY(hipMemcpyAsync(ids_out, p->tids.p, (size_t)p->T * 8, hipMemcpyDeviceToHost, c->st));
-    if (values_out) {
-        SKY_TRY(p->out_rows.ensure((size_t)p->T * D * 8));
-        launch_part_rows_out(D, p->T, p->trep.as<uint32_t>(), p->rrows.as<double>(), p->out_rows.as<double>(), c->st);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(values_out, p->out_rows.p, (size_t)p->T * D * 8, hipMemcpyDeviceToHost, c->st));
-    }
-    HIP_TRY(hipStreamSynchronize(c->st));
     return SKY_OK;
     GUARD_END
 }

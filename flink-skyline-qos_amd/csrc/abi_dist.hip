@@ -347,6 +347,8 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
             ow.ids_out = d_ids_out;
             ow.origin_out = d_origin_out;
             ow.out_cap = out_cap;
+            ow.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
+            ow.dom_kj = p.dom_kj;
             launch_out_write(ow, st);
         }
         c->ktimer_end("out", st, p.n);
@@ -372,9 +374,13 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
     unsigned long long sum[16] = {};
     uint32_t tot[16] = {}, flags = 0;
     std::vector<int64_t> st((size_t)K * 2);
+    const int KM = p.Kp * p.M;
+    p.h_dup.assign(KM, 0u);
     SKY_TRY(sync_read(p, c->st,
-                      {{c->dist_sum.p, 128}, {p.totals.p, 64}, {p.flags.p, 4}, {d_stats_sum, (size_t)K * 16}},
-                      {sum, tot, &flags, st.data()}));
+                      {{c->dist_sum.p, 128}, {p.totals.p, 64}, {p.flags.p, 4}, {d_stats_sum, (size_t)K * 16},
+                       {p.dup_cnt.p, p.n ? (size_t)KM * 4 : 0}},
+                      {sum, tot, &flags, st.data(), p.h_dup.data()}));
+    if (p.n) pick_dom_group(p, KM);
     c->dist_merged = false;
     // the next merge's route: |own| x |union| as exported (a capped exchange holds fewer rows)
     c->dist_hist_pairs = (int64_t)(sum[8] * sum[7]);

@@ -76,6 +76,24 @@ struct Ctx {
     // bulk CSV ingest workspace (k_csv.hip)
     DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow;
     DevBuf prof_k, prof_v, prof_scr;   // sky_profile_sort_dev workspace
+    // batched per-key inserts (sky_parts_insert): the call's upload (descriptors, work items,
+    // ids, rows) and work arrays on the device; pinned staging slots, each reusable once its
+    // event (the upload) has completed
+    DevBuf part_batch, part_work;
+    struct Staging {
+        void *h = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        bool used = false;
+    };
+    Staging part_stage[4];
+    int part_stage_next = 0;
+    ~Ctx() {
+        for (Staging &s : part_stage) {
+            if (s.h) (void)hipHostFree(s.h);
+            if (s.ev) (void)hipEventDestroy(s.ev);
+        }
+    }
 
     int Kq() const {
         if (algo == SKY_ALGO_GRID && sem == SKY_SEM_COMPLETE) return std::max(P, 1 << D);
@@ -169,24 +187,31 @@ struct Ctx {
 struct sky_ctx : sky::Ctx {};
 
 // one Flink key's local skyline (SkylineLocalProcessor.localSkylineState, FlinkSkyline.java:243-248)
-// as distinct vectors + the tuples on them (k_part.hip): an insert costs O(|B| (|B| + R))
+// as distinct vectors + the tuples on them (k_part.hip): an insert costs O(|B| (|B| + R)) pair
+// tests and no host read.  The counts live on the device; the host keeps bounds for launch
+// sizes and capacities, tightened from the commit kernel's host-mapped mirror.
+constexpr uint32_t kPartRing = 4096;       // inserts whose cumulative tuple counts the host keeps
 struct sky_part {
     sky_ctx *ctx = nullptr;
     int32_t key = 0;
-    // distinct vectors: rows f64 [R][D], alive flag, tuples per rep
-    sky::DevBuf rrows, ralive, rcnt;
-    uint32_t R = 0;
-    // tuples in insertion order: id, rep; Tdead of them sit on dead reps (compacted lazily)
-    sky::DevBuf tids, trep;
-    uint32_t T = 0;
-    uint64_t Tdead = 0;
-    // batch workspace
-    sky::DevBuf bids, bvals, dom_b, eq_s, eq_b, dom_s, keep, keep_pos, fresh, fresh_pos, scratch, words;
+    // distinct vectors: rows f64 [R][D], alive flag, tuples per rep; tuples: id, rep (insertion order)
+    sky::DevBuf rrows, ralive, rcnt, tids, trep;
+    size_t Rcap = 0, Tcap = 0;              // capacities (elements)
+    sky::DevBuf dcnt;                       // device counts: R, T, dead (u64)
+    uint32_t *mirror = nullptr;             // host-mapped seqlock mirror: begin, R, T, dead lo, hi, end
+    uint32_t *mirror_dev = nullptr;         // its device address
+    uint32_t seq = 0;                       // inserts issued (the mirror's tags)
+    uint64_t issued = 0;                    // tuples issued
+    uint64_t cum[kPartRing] = {};           // tuples issued up to and including insert s (s % kPartRing)
+    uint32_t seq_known = 0;                 // the counts below are those after insert seq_known
+    uint64_t R_known = 0, T_known = 0, dead_known = 0, cum_known = 0;
+    std::vector<sky::DevBuf> grave;         // replaced state buffers, freed at the next synchronisation
     // compaction targets and read-out staging
-    sky::DevBuf rrows2, ralive2, rcnt2, tids2, trep2, rk, rp, tk, tp, out_rows;
-    void *pin = nullptr;        // pinned read-back words
+    sky::DevBuf rrows2, ralive2, rcnt2, tids2, trep2, rk, rp, tk, tp, out_rows, scratch, words;
+    void *pin = nullptr;                    // pinned read-back words
     ~sky_part() {
         if (pin) (void)hipHostFree(pin);
+        if (mirror) (void)hipHostFree(mirror);
     }
 };
 

@@ -43,6 +43,8 @@ struct PipeIn {
     bool single = false;            // one partition (global merge of lists, local state insert)
     bool global = true;             // run the global merge after the local skylines
     bool fate = true;               // per-tuple fate pass (stats, output counts)
+    bool planes_ok = false;         // the output comes from this run's own write pass only (no later
+                                    // recount over the status words): the filter may store status planes
     bool dist = false;              // multi-GPU export (sky_dist_export_dev): local skylines only, the
                                     // small-set / planned routes allowed, the run's checks deferred to a
                                     // device verdict (no host read at the end of the run)
@@ -92,6 +94,11 @@ struct Pipe {
     DevBuf lbuf;
     DevBuf tile_hist, tile_cand;      // per-tile duplicate histograms / surviving candidates (output counts)
     bool hist_count = false;
+    // status planes (k_filter): B / E words per tile instead of a status word per tuple; the
+    // designated duplicate group (B) is the largest group of the last run with the same shape
+    DevBuf planes;
+    bool planes_on = false;
+    int32_t dom_kj = -1, dom_km = 0;
     // the small-set route of the last query (prefilter rounds + brute pair pass), replayed by
     // the next with device-sized launches (bounds from this query's counts)
     struct Plan {
@@ -148,6 +155,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
 // read device ranges into host memory in one synchronisation (one gather launch when they are small)
 int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
               std::vector<void *> dsts);
+// the designated duplicate group of the next run's status planes, from p.h_dup
+void pick_dom_group(Pipe &p, int KM);
 // stream-ordered output of the tuples selected by the last run
 int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d_ids_out, int32_t *d_origin_out,
                 double *d_rows_out, int64_t cap, int64_t *n_out, uint8_t *d_row_flags);

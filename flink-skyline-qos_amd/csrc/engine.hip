@@ -171,6 +171,11 @@ static bool hist_disabled() {   // SKY_HIST_COUNT=0: the status-word count pass 
     const char *e = getenv("SKY_HIST_COUNT");
     return e && e[0] == '0';
 }
+// SKY_PLANES=0: the filter stores every status word (A/B knob, read per query)
+static bool planes_disabled() {
+    const char *e = getenv("SKY_PLANES");
+    return e && e[0] == '0';
+}
 // SKY_PLAN=0: every query takes the host-synchronised route (A/B knob, read per query)
 static bool plan_disabled() {
     const char *e = getenv("SKY_PLAN");
@@ -669,6 +674,19 @@ struct PlanRun {
     const uint32_t *d_cnt = nullptr;  // slots entering the brute pass (device)
     bool k_u16 = false, k_f32 = false;   // the brute pass's compare type
 };
+// the next run's designated duplicate group (status planes): the largest group of this run
+void pick_dom_group(Pipe &p, int KM) {
+    uint32_t best = 0;
+    int32_t kj = -1;
+    for (int q = 0; q < KM && q < (int)p.h_dup.size(); q++)
+        if (p.h_dup[q] > best) {
+            best = p.h_dup[q];
+            kj = q;
+        }
+    p.dom_kj = kj;
+    p.dom_km = KM;
+}
+
 // The end of a multi-GPU export run (in.dist): nothing is read back.  The route's checks (the
 // planned route's assumptions, NaN, a look-back's spin bound) become a device verdict that the
 // export writes into its block header; the fates of this shard's units follow the union merge.
@@ -789,6 +807,8 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         ow.ids_out = in.out_ids;
         ow.origin_out = in.out_org;
         ow.out_cap = in.out_cap;
+        ow.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
+        ow.dom_kj = p.dom_kj;
         c.ktimer_begin("outw", st);
         launch_out_write(ow, st);
         c.ktimer_end("outw", st, n);
@@ -811,10 +831,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     if (brute) {
         uint32_t flags2 = 0, tot[16] = {};
         p.h_seg_n.assign(p.Kp, 0u);
+        p.h_dup.assign(KM, 0u);
         SKY_TRY(sync_read(p, st, {{p.totals.p, 64}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
-                                  {p.flags.p, 4}},
-                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2}));
+                                  {p.flags.p, 4}, {p.dup_cnt.p, (size_t)KM * 4}},
+                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}));
         nout = tot[3];
         if (flags2 & kFlagRadixSpin) {
             set_error("a look-back (output) exceeded its spin bound");
@@ -857,10 +878,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     } else {
         uint32_t flags3 = 0;
         unsigned long long mbr_pairs[2] = {0, 0};
+        p.h_dup.assign(KM, 0u);
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
-                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}},
-                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs}));
+                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}, {p.dup_cnt.p, (size_t)KM * 4}},
+                          {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs, p.h_dup.data()}));
         if (p.used_mbr) {
             p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
             p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
@@ -873,6 +895,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             return SKY_E_HIP;
         }
     }
+    pick_dom_group(p, KM);
     p.dom_w = 0;
     if (have_seg) {
         int64_t sg = 0;
@@ -1096,6 +1119,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(p.tile_cand.ensure((size_t)tiles * 4));
         fill.add(p.tile_cand.p, (size_t)tiles * 4);
     }
+    // status planes: only when this run's own write pass (k_out_write, hist counts) makes the
+    // output, so nothing reads the status words of dropped / designated-group tuples
+    p.planes_on = p.hist_count && (in.planes_ok || in.dist) && !planes_disabled();
+    if (p.planes_on) SKY_TRY(p.planes.ensure((size_t)tiles * 32 * 16));
+    if (p.dom_km != KM) p.dom_kj = -1;
     // the planned route's counters and flags go out with this launch too: one criterion-minima
     // slice per prefilter round, the brute pass's domination bits and partition counts
     if (planned) SKY_TRY(plan_prepare(p, D, fill));
@@ -1128,6 +1156,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.flags = p.flags.as<uint32_t>();
     fa.slot_cap = (uint32_t)cap;
     fa.tile_hist = p.hist_count ? p.tile_hist.as<uint32_t>() : nullptr;
+    fa.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
+    fa.dom_kj = p.dom_kj;
     {
         static const int fdbg = [] { const char *e = getenv("SKY_FILTER_DBG"); return e ? atoi(e) : 0; }();
         fa.dbg = fdbg;
@@ -1465,6 +1495,10 @@ int pipe_output(Ctx &c, Pipe &p, const PipeIn &in, bool select_local, int64_t *d
     // the local skyline of a global run, or other buffers than the single-pass output wrote:
     // a count pass + scan of its own (stats untouched)
     const bool recount = p.n > 0 && ((select_local && in.global) || (p.fused && writes && !fused_done));
+    if (p.planes_on && p.n > 0 && (recount || d_rows_out || d_row_flags || select_local)) {
+        set_error("internal: the run stored status planes, not status words; this output needs the words");
+        return SKY_E_HIP;
+    }
     uint32_t nsel = p.nout;
     OutArgs oa{};
     oa.status = p.status.as<uint16_t>();

@@ -428,6 +428,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     const uint32_t nspans = (a.n + kSpan - 1) / kSpan;
     const int KM = a.Kp * a.M;
+    // status planes (a.planes): per (item, wave) of a tile one 64-bit B word (the tuple is a
+    // duplicate of the designated group a.dom_kj) and one E word (its status word is stored);
+    // every other tuple is dropped and stores nothing
+    const bool planes = a.planes != nullptr;
+    // the designated group's status word (never equal to a stored word when there is none)
+    const uint32_t sg = a.dom_kj >= 0 ? ((uint32_t)(a.dom_kj / a.M) << 8) | (uint32_t)(1 + a.dom_kj % a.M) : 0x10000u;
     double vn[D];                                                // the row of item r+1, in flight
     int32_t kn = 0;
 #define SKY_FILTER_FETCH_TO(I, VN, KN)                                                     \
@@ -463,7 +469,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #pragma unroll
         for (int d = 0; d < D; d++) v[d] = vn[d];
         const int32_t kg = kn;
-        if (r > 0 && i - kThreads < a.n && a.dbg < 2) a.status[i - kThreads] = st_prev;   // item r-1, beside the prefetch
+        if (r > 0 && a.dbg < 2) {                                       // item r-1, beside the prefetch
+            const bool vp = i - kThreads < a.n;
+            if (!planes) {
+                if (vp) a.status[i - kThreads] = st_prev;
+            } else {
+                // planes from the stored word alone (no extra live registers in the loop)
+                const bool dg = vp && (uint32_t)st_prev == sg, ex = vp && (st_prev & 0xffu) != kCodeDropped && !dg;
+                const uint64_t bm = __ballot(dg), em = __ballot(ex);
+                if (ex) a.status[i - kThreads] = st_prev;
+                if (lane == 0)
+                    reinterpret_cast<ulonglong2 *>(a.planes)[((size_t)span * FT + (r - 1) / kItems) * 32 +
+                                                             ((r - 1) % kItems) * (kThreads / 64) + wave] =
+                        make_ulonglong2(bm, em);
+            }
+        }
 #if SKY_FILTER_PF2
 #pragma unroll
         for (int d = 0; d < D; d++) vn[d] = vn2[d];
@@ -489,7 +509,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         if (defer) wlist[kList - 1 - (dcnt + lanes_below(dm))] = i - base;
         dcnt += (uint32_t)__popcll(dm);
         bool cand = false;
-        uint16_t st = 0;                                             // deferred: rewritten by k_filter_deferred
+        // deferred: kCodeDeferred, rewritten by k_filter_deferred (a stored word under planes)
+        uint16_t st = defer ? kCodeDeferred : (uint16_t)0;
         if (valid && !defer) {
             uint16_t code = kCodeCandidate;
             if (nan) { lflags |= kFlagNaN; code = kCodeDropped; k = 0; }
@@ -504,15 +525,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
             cand = code == kCodeCandidate;
             st = (uint16_t)(((uint32_t)k << 8) | code);
         }
-        count_dups((uint16_t)(st & 0xffu), (int32_t)(st >> 8), a.M, s_dup + (FT > 1 ? (r / kItems) * KM : 0));
+        count_dups((uint16_t)(defer ? 0u : (st & 0xffu)), (int32_t)(st >> 8), a.M,
+                   s_dup + (FT > 1 ? (r / kItems) * KM : 0));
         const uint64_t cm = __ballot(cand);
         if (cand) wlist[wcnt + lanes_below(cm)] = ((uint32_t)k << 16) | (i - base);
         wcnt += (uint32_t)__popcll(cm);
         st_prev = st;
     }
-    {
+    if (a.dbg < 2) {
         const uint32_t il = base + (kSpanItems - 1) * kThreads + threadIdx.x;
-        if (il < a.n && a.dbg < 2) a.status[il] = st_prev;
+        const bool vp = il < a.n;
+        if (!planes) {
+            if (vp) a.status[il] = st_prev;
+        } else {
+            const bool dg = vp && (uint32_t)st_prev == sg, ex = vp && (st_prev & 0xffu) != kCodeDropped && !dg;
+            const uint64_t bm = __ballot(dg), em = __ballot(ex);
+            if (ex) a.status[il] = st_prev;
+            if (lane == 0)
+                reinterpret_cast<ulonglong2 *>(a.planes)[((size_t)span * FT + FT - 1) * 32 +
+                                                         (kItems - 1) * (kThreads / 64) + wave] =
+                    make_ulonglong2(bm, em);
+        }
     }
     // the tile's candidates: ONE slot reservation per tile, then rows re-read (cache
     // hot) and appended with their sort keys
@@ -1266,8 +1299,29 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     // (tuples past n are never selected: masked below)
     uint16_t st[kItems];
     int64_t idv[kItems];
+    // status planes: the (item, wave) words are wave-uniform (scalar loads); a status word is
+    // loaded only where the E bit says the filter stored one, the B bit stands for the
+    // designated duplicate group's status
+    uint64_t pb[kItems], pe[kItems];
+    if (a.planes) {
+        const ulonglong2 *pw = reinterpret_cast<const ulonglong2 *>(a.planes) + (size_t)tile * 32 +
+                               __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
-    for (int k = 0; k < kItems; k++) st[k] = a.status[min(i0 + k * kThreads, nl)];
+        for (int k = 0; k < kItems; k++) {
+            const ulonglong2 w = pw[k * (kThreads / 64)];
+            pb[k] = w.x;
+            pe[k] = w.y;
+        }
+        const uint16_t sg = (uint16_t)(a.dom_kj >= 0 ? ((a.dom_kj / a.M) << 8) | (1 + a.dom_kj % a.M) : 0);
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            const bool e = (pe[k] >> lane) & 1ull;
+            st[k] = e ? a.status[min(i0 + k * kThreads, nl)] : (((pb[k] >> lane) & 1ull) ? sg : (uint16_t)0);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) st[k] = a.status[min(i0 + k * kThreads, nl)];
+    }
     if (a.ids) {
 #pragma unroll
         for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];

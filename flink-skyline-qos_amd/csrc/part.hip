@@ -1,0 +1,416 @@
+// part.hip — the per-key operator state behind SkylineLocalProcessor (sky_part_*,
+// sky_parts_insert), FlinkSkyline.java:214-445.
+//
+// processBuffer (:417-444) sets S <- SKY(S u B) for every 5000-tuple buffer B of a key.  An
+// insert here is asynchronous: the batches of one call (one or several keys) are staged into
+// pinned memory (the NaN check rides along), uploaded with their descriptors and work items in
+// ONE copy, and applied by k_parts_pairs + k_parts_commit (k_part.hip) with device-side counts.
+// No host read: launch sizes and capacities come from host bounds (the last counts the commit
+// kernel mirrored into host memory, plus every tuple issued since).  The host synchronises only
+// when it must see the state: sky_part_size / sky_part_snapshot / compaction / close.
+#include "abi_common.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// the newest consistent counts the commit kernel mirrored (seqlock: end, data, begin)
+void refresh_known(sky_part *p) {
+    if (!p->mirror || p->seq_known == p->seq) return;
+    volatile const uint32_t *m = p->mirror;
+    const uint32_t e = m[5];
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint32_t R = m[1], T = m[2], dlo = m[3], dhi = m[4];
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint32_t b = m[0];
+    if (b != e || e == p->seq_known || e == 0) return;
+    if ((int32_t)(e - p->seq_known) < 0 || p->seq - e >= kPartRing) return;   // stale, or the ring moved on
+    p->seq_known = e;
+    p->R_known = R;
+    p->T_known = T;
+    p->dead_known = ((uint64_t)dhi << 32) | dlo;
+    p->cum_known = p->cum[e % kPartRing];
+}
+
+inline uint64_t bound_R(const sky_part *p) { return p->R_known + (p->issued - p->cum_known); }
+inline uint64_t bound_T(const sky_part *p) { return p->T_known + (p->issued - p->cum_known); }
+
+// wait for the part's work, then its exact counts
+int part_sync(sky_part *p) {
+    sky_ctx *c = p->ctx;
+    c->host_syncs++;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    p->grave.clear();
+    if (!p->pin && hipHostMalloc(&p->pin, 256, hipHostMallocDefault) != hipSuccess) {
+        p->pin = nullptr;
+        set_error("hipHostMalloc failed");
+        return SKY_E_NOMEM;
+    }
+    if (!p->dcnt.p) {
+        memset(p->pin, 0, 16);
+    } else {
+        HIP_TRY(hipMemcpy(p->pin, p->dcnt.p, 16, hipMemcpyDeviceToHost));
+    }
+    const uint32_t *h = (const uint32_t *)p->pin;
+    p->R_known = h[0];
+    p->T_known = h[1];
+    p->dead_known = ((uint64_t)h[3] << 32) | h[2];
+    p->seq_known = p->seq;
+    p->cum_known = p->issued;
+    return SKY_OK;
+}
+
+// grow a state buffer keeping its first `used` bytes, stream-ordered (the old buffer waits in
+// the grave until the next synchronisation)
+int grow_async(sky_part *p, DevBuf &b, size_t need, size_t used) {
+    if (need <= b.cap && b.p) return SKY_OK;
+    DevBuf nb;
+    SKY_TRY(nb.ensure(std::max(need, b.cap * 2)));
+    if (used && b.p) HIP_TRY(hipMemcpyAsync(nb.p, b.p, std::min(used, b.cap), hipMemcpyDeviceToDevice, p->ctx->st));
+    if (b.p) p->grave.push_back(std::move(b));
+    b = std::move(nb);
+    return SKY_OK;
+}
+
+// drop the dead reps and their tuples (order kept); after part_sync
+int part_compact(sky_part *p) {
+    sky_ctx *c = p->ctx;
+    hipStream_t st = c->st;
+    const int D = c->D;
+    const uint32_t R = (uint32_t)p->R_known, T = (uint32_t)p->T_known;
+    SKY_TRY(p->rk.ensure((size_t)R * 4 + 4));
+    SKY_TRY(p->rp.ensure((size_t)R * 4 + 4));
+    SKY_TRY(p->tk.ensure((size_t)T * 4 + 4));
+    SKY_TRY(p->tp.ensure((size_t)T * 4 + 4));
+    SKY_TRY(p->rrows2.ensure(std::max<size_t>(p->rrows.cap, 256)));
+    SKY_TRY(p->ralive2.ensure(std::max<size_t>(p->ralive.cap, 256)));
+    SKY_TRY(p->rcnt2.ensure(std::max<size_t>(p->rcnt.cap, 256)));
+    SKY_TRY(p->tids2.ensure(std::max<size_t>(p->tids.cap, 256)));
+    SKY_TRY(p->trep2.ensure(std::max<size_t>(p->trep.cap, 256)));
+    SKY_TRY(p->scratch.ensure(scan_scratch_words((size_t)std::max(R, T) + 1) * 4 + 64));
+    SKY_TRY(p->words.ensure(256));
+    uint32_t *w = p->words.as<uint32_t>();
+    launch_part_rkeep(R, p->ralive.as<uint8_t>(), p->rk.as<uint32_t>(), st);
+    scan_excl_u32(p->rk.as<uint32_t>(), p->rp.as<uint32_t>(), R, w + 8, p->scratch.as<uint32_t>(), st);
+    launch_part_rmove(D, R, p->rk.as<uint32_t>(), p->rp.as<uint32_t>(), p->rrows.as<double>(), p->rcnt.as<uint32_t>(),
+                      p->rrows2.as<double>(), p->rcnt2.as<uint32_t>(), p->ralive2.as<uint8_t>(), st);
+    launch_part_tkeep(T, p->trep.as<uint32_t>(), p->ralive.as<uint8_t>(), p->tk.as<uint32_t>(), st);
+    scan_excl_u32(p->tk.as<uint32_t>(), p->tp.as<uint32_t>(), T, w + 9, p->scratch.as<uint32_t>(), st);
+    launch_part_tmove(T, p->tk.as<uint32_t>(), p->tp.as<uint32_t>(), p->rp.as<uint32_t>(), p->tids.as<int64_t>(),
+                      p->trep.as<uint32_t>(), p->tids2.as<int64_t>(), p->trep2.as<uint32_t>(), st);
+    HIP_TRY(hipGetLastError());
+    uint32_t h[2] = {0, 0};
+    c->host_syncs++;
+    HIP_TRY(hipMemcpyAsync(p->pin, w + 8, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(h, p->pin, 8);
+    std::swap(p->rrows, p->rrows2);
+    std::swap(p->ralive, p->ralive2);
+    std::swap(p->rcnt, p->rcnt2);
+    std::swap(p->tids, p->tids2);
+    std::swap(p->trep, p->trep2);
+    p->Rcap = std::min({p->rcnt.cap / 4, p->ralive.cap, p->rrows.cap / ((size_t)D * 8)});
+    p->Tcap = std::min(p->trep.cap / 4, p->tids.cap / 8);
+    const uint32_t cnt[4] = {h[0], h[1], 0u, 0u};
+    memcpy(p->pin, cnt, 16);
+    HIP_TRY(hipMemcpy(p->dcnt.p, p->pin, 16, hipMemcpyHostToDevice));
+    p->R_known = h[0];
+    p->T_known = h[1];
+    p->dead_known = 0;
+    return SKY_OK;
+}
+
+Ctx::Staging *take_stage(sky_ctx *c, size_t bytes) {
+    Ctx::Staging &s = c->part_stage[c->part_stage_next];
+    c->part_stage_next = (c->part_stage_next + 1) % 4;
+    if (s.used && s.ev) (void)hipEventSynchronize(s.ev);   // its upload has left (normally long ago)
+    s.used = false;
+    if (!s.ev && hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+        s.ev = nullptr;
+        return nullptr;
+    }
+    if (s.cap < bytes) {
+        if (s.h) (void)hipHostFree(s.h);
+        s.h = nullptr;
+        s.cap = std::max(bytes, (size_t)4 << 20);
+        if (hipHostMalloc(&s.h, s.cap, hipHostMallocDefault) != hipSuccess) {
+            s.h = nullptr;
+            s.cap = 0;
+            return nullptr;
+        }
+    }
+    return &s;
+}
+
+int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *ids_all,
+                 const double *const *values_all, const int64_t *counts_all) {
+    sky_ctx *c = parts_all[0]->ctx;
+    hipStream_t st = c->st;
+    const int D = c->D;
+    // the parts with a batch
+    std::vector<sky_part *> parts;
+    std::vector<const int64_t *> ids;
+    std::vector<const double *> values;
+    std::vector<int64_t> counts;
+    uint64_t ntot = 0;
+    for (int g = 0; g < np_all; g++) {
+        if (counts_all[g] == 0) continue;
+        parts.push_back(parts_all[g]);
+        ids.push_back(ids_all[g]);
+        values.push_back(values_all[g]);
+        counts.push_back(counts_all[g]);
+        ntot += (uint64_t)counts_all[g];
+    }
+    const int np = (int)parts.size();
+    if (ntot == 0) return SKY_OK;
+    ARG_CHECK(ntot < 0x7fffffffull, "too many tuples in one call");
+    // ---- bounds, compaction, capacity (per part; no host read unless compaction is due)
+    std::vector<uint64_t> rb(np), tb(np);
+    uint64_t rbtot = 0;
+    for (int g = 0; g < np; g++) {
+        sky_part *p = parts[g];
+        refresh_known(p);
+        if (p->dead_known >= 4096 && p->dead_known * 2 > p->T_known) {   // more than half the tuples dead
+            SKY_TRY(part_sync(p));
+            if (p->dead_known) SKY_TRY(part_compact(p));
+        }
+        const uint64_t nb = (uint64_t)counts[g];
+        rb[g] = bound_R(p);
+        tb[g] = bound_T(p);
+        ARG_CHECK(rb[g] + nb < 0xffffffffull && tb[g] + nb < 0xffffffffull, "partition state too large");
+        if (!p->dcnt.p) {
+            SKY_TRY(p->dcnt.ensure(64));
+            HIP_TRY(hipMemsetAsync(p->dcnt.p, 0, 16, st));
+        }
+        if (!p->mirror) {
+            void *m = nullptr, *dm = nullptr;
+            if (hipHostMalloc(&m, 64, hipHostMallocCoherent) == hipSuccess) {
+                memset(m, 0, 64);
+                if (hipHostGetDevicePointer(&dm, m, 0) == hipSuccess) {
+                    p->mirror = (uint32_t *)m;
+                    p->mirror_dev = (uint32_t *)dm;
+                } else {
+                    (void)hipHostFree(m);
+                }
+            }
+        }
+        const size_t Rn = (size_t)(rb[g] + nb), Tn = (size_t)(tb[g] + nb);
+        if (Rn > p->Rcap) {
+            const size_t want = std::max(Rn, p->Rcap * 2);
+            SKY_TRY(grow_async(p, p->rrows, want * D * 8, (size_t)rb[g] * D * 8));
+            SKY_TRY(grow_async(p, p->ralive, want, (size_t)rb[g]));
+            SKY_TRY(grow_async(p, p->rcnt, want * 4, (size_t)rb[g] * 4));
+            p->Rcap = want;
+        }
+        if (Tn > p->Tcap) {
+            const size_t want = std::max(Tn, p->Tcap * 2);
+            SKY_TRY(grow_async(p, p->tids, want * 8, (size_t)tb[g] * 8));
+            SKY_TRY(grow_async(p, p->trep, want * 4, (size_t)tb[g] * 4));
+            p->Tcap = want;
+        }
+        rbtot += rb[g];
+    }
+    // ---- work items: batch vs batch, batch vs state, state vs batch
+    std::vector<PartItem> items;
+    for (int g = 0; g < np; g++) {
+        const uint32_t nb = (uint32_t)counts[g];
+        for (uint32_t y = 0; y < nb; y += kPartItemY) {
+            for (uint32_t x = 0; x < nb; x += kPartItemX) items.push_back(PartItem{(uint32_t)g, 0u, y, x});
+            for (uint64_t x = 0; x < rb[g]; x += kPartItemX) items.push_back(PartItem{(uint32_t)g, 1u, y, (uint32_t)x});
+        }
+        for (uint64_t y = 0; y < rb[g]; y += kPartItemY)
+            for (uint32_t x = 0; x < nb; x += kPartItemX) items.push_back(PartItem{(uint32_t)g, 2u, (uint32_t)y, x});
+    }
+    // ---- the upload: descriptors, items, ids, rows (one pinned staging slot, one copy)
+    const size_t o_desc = 0, o_items = align_up((size_t)np * sizeof(PartDesc));
+    const size_t o_ids = o_items + align_up(items.size() * sizeof(PartItem));
+    const size_t o_vals = o_ids + align_up((size_t)ntot * 8);
+    const size_t up_bytes = o_vals + (size_t)ntot * D * 8;
+    Ctx::Staging *sg = take_stage(c, up_bytes);
+    if (!sg) {
+        set_error("pinned staging allocation failed");
+        return SKY_E_NOMEM;
+    }
+    char *h = (char *)sg->h;
+    bool nan = false;
+    int nan_part = -1;
+    {
+        uint64_t off = 0;
+        for (int g = 0; g < np; g++) {
+            const size_t nb = (size_t)counts[g];
+            memcpy(h + o_ids + off * 8, ids[g], nb * 8);
+            const double *src = values[g];
+            double *dst = (double *)(h + o_vals) + off * D;
+            bool bad = false;
+            for (size_t q = 0; q < nb * D; q++) {     // staged and checked in one pass
+                const double v = src[q];
+                dst[q] = v;
+                bad |= v != v;
+            }
+            if (bad && !nan) {
+                nan = true;
+                nan_part = g;
+            }
+            off += nb;
+        }
+    }
+    if (nan) {   // the whole call is rejected before any launch: the states never see the batch
+        set_error("a tuple value is NaN (batch of key " + std::to_string(parts[nan_part]->key) +
+                  "): the reference BNL result is order-dependent for NaN; batch rejected");
+        return SKY_E_NAN;
+    }
+    SKY_TRY(c->part_batch.ensure(up_bytes));
+    // work arrays: dom_b | eq_s | eq_b | kpos | fpos (per tuple), dom_s (per bounded rep)
+    const size_t w_nb = (size_t)ntot * 4;
+    SKY_TRY(c->part_work.ensure(5 * w_nb + (size_t)std::max<uint64_t>(rbtot, 1) * 4 + 64));
+    char *dev = c->part_batch.as<char>();
+    uint32_t *w = c->part_work.as<uint32_t>();
+    uint32_t *w_dom_b = w, *w_eq_s = w + ntot, *w_eq_b = w + 2 * ntot, *w_kpos = w + 3 * ntot, *w_fpos = w + 4 * ntot;
+    uint32_t *w_dom_s = w + 5 * ntot;
+    {
+        PartDesc *ds = (PartDesc *)(h + o_desc);
+        uint64_t off = 0, roff = 0;
+        for (int g = 0; g < np; g++) {
+            sky_part *p = parts[g];
+            PartDesc d{};
+            const uint32_t nb = (uint32_t)counts[g];
+            d.bvals = (const double *)(dev + o_vals) + off * D;
+            d.bids = (const int64_t *)(dev + o_ids) + off;
+            d.nb = nb;
+            d.rb = (uint32_t)rb[g];
+            d.dom_b = w_dom_b + off;
+            d.eq_s = w_eq_s + off;
+            d.eq_b = w_eq_b + off;
+            d.kpos = w_kpos + off;
+            d.fpos = w_fpos + off;
+            d.dom_s = w_dom_s + roff;
+            d.rrows = p->rrows.as<double>();
+            d.ralive = p->ralive.as<uint8_t>();
+            d.rcnt = p->rcnt.as<uint32_t>();
+            d.tids = p->tids.as<int64_t>();
+            d.trep = p->trep.as<uint32_t>();
+            d.dcnt = p->dcnt.as<uint32_t>();
+            d.mirror = p->mirror_dev;
+            p->seq++;
+            p->issued += nb;
+            p->cum[p->seq % kPartRing] = p->issued;
+            d.seq = p->seq;
+            ds[g] = d;
+            off += nb;
+            roff += rb[g];
+        }
+        if (!items.empty()) memcpy(h + o_items, items.data(), items.size() * sizeof(PartItem));
+    }
+    HIP_TRY(hipMemcpyAsync(dev, h, up_bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(sg->ev, st));
+    sg->used = true;
+    FillSet fill;
+    fill.add(w_dom_b, w_nb, 0);
+    fill.add(w_eq_s, 2 * w_nb, 0xff);
+    if (rbtot) fill.add(w_dom_s, (size_t)rbtot * 4, 0);
+    HIP_TRY(fill.launch(st));
+    launch_parts_insert(D, (const PartDesc *)(dev + o_desc), np, (const PartItem *)(dev + o_items),
+                        (uint32_t)items.size(), st);
+    HIP_TRY(hipGetLastError());
+    return SKY_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sky_part_open(sky_ctx *c, int32_t key, sky_part **out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && out, "null argument");
+    sky_part *p = new sky_part();
+    p->ctx = c;
+    p->key = key;
+    *out = p;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_part_close(sky_part *p) {
+    if (!p) return SKY_OK;
+    hipSetDevice(p->ctx->dev);
+    hipStreamSynchronize(p->ctx->st);
+    delete p;
+    return SKY_OK;
+}
+
+int sky_part_size(sky_part *p, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(p && n_out, "null argument");
+    SKY_TRY(bind(p->ctx));
+    SKY_TRY(part_sync(p));
+    *n_out = (int64_t)(p->T_known - p->dead_known);
+    return SKY_OK;
+    GUARD_END
+}
+
+// SkylineLocalProcessor.processBuffer (FlinkSkyline.java:417-444) for one key
+int sky_part_insert(sky_part *p, const int64_t *ids, const double *values, int64_t n) {
+    GUARD_BEGIN
+    ARG_CHECK(p && (n == 0 || (ids && values)), "null argument");
+    ARG_CHECK(n >= 0 && n < (int64_t)0x7fffffffLL, "n out of range");
+    if (n == 0) return SKY_OK;
+    SKY_TRY(bind(p->ctx));
+    return parts_insert(1, &p, &ids, &values, &n);
+    GUARD_END
+}
+
+// processBuffer for the full buffers of several keys of one context in one launch set
+int sky_parts_insert(int nparts, sky_part *const *parts, const int64_t *const *ids, const double *const *values,
+                     const int64_t *counts) {
+    GUARD_BEGIN
+    ARG_CHECK(nparts >= 0 && nparts <= 65536, "nparts out of range");
+    if (nparts == 0) return SKY_OK;
+    ARG_CHECK(parts && ids && values && counts, "null argument");
+    for (int g = 0; g < nparts; g++) {
+        ARG_CHECK(parts[g] && parts[g]->ctx == parts[0]->ctx, "every part must belong to one context");
+        ARG_CHECK(counts[g] >= 0 && counts[g] < (int64_t)0x7fffffffLL, "count out of range");
+        ARG_CHECK(counts[g] == 0 || (ids[g] && values[g]), "null batch");
+        for (int h = 0; h < g; h++) ARG_CHECK(parts[h] != parts[g], "a part appears twice in one call");
+    }
+    SKY_TRY(bind(parts[0]->ctx));
+    return parts_insert(nparts, parts, ids, values, counts);
+    GUARD_END
+}
+
+int sky_part_snapshot(sky_part *p, int64_t *ids_out, double *values_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(p, "null part");
+    sky_ctx *c = p->ctx;
+    SKY_TRY(bind(c));
+    SKY_TRY(part_sync(p));
+    const int64_t live = (int64_t)(p->T_known - p->dead_known);
+    if (n_out) *n_out = live;
+    if (live > cap) {
+        set_error("snapshot capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    if (live == 0) return SKY_OK;
+    if (p->dead_known) SKY_TRY(part_compact(p));
+    const int D = c->D;
+    const size_t T = (size_t)p->T_known;
+    if (ids_out) HIP_TRY(hipMemcpyAsync(ids_out, p->tids.p, T * 8, hipMemcpyDeviceToHost, c->st));
+    if (values_out) {
+        SKY_TRY(p->out_rows.ensure(T * D * 8));
+        launch_part_rows_out(D, (uint32_t)T, p->trep.as<uint32_t>(), p->rrows.as<double>(), p->out_rows.as<double>(),
+                             c->st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(values_out, p->out_rows.p, T * D * 8, hipMemcpyDeviceToHost, c->st));
+    }
+    c->host_syncs++;
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
+}  // extern "C"

@@ -16,6 +16,7 @@ constexpr int kStatShards = 1024;             // |L_k| / survivors_k accumulator
 constexpr uint16_t kCodeDropped = 0;          // dominated by a pruner / key never queried
 constexpr uint16_t kCodeCandidate = 255;      // goes to sort + SFS
 constexpr uint16_t kCodeFate0 = 251;          // candidate after the fate pass: 251 + (inL | inG << 1)
+constexpr uint16_t kCodeDeferred = 250;       // MR-Angle key left to k_filter_deferred (rewritten there)
 // codes 1..254: exact duplicate of pruner (code-1) of its partition
 
 // flag bits (device u32)

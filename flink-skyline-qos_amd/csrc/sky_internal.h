@@ -76,6 +76,11 @@ struct FilterArgs {
     uint32_t slot_cap;            // slots allocated: appends past it are counted, not written
     uint32_t *tile_hist;          // [tiles][Kp*M] duplicates per tile (nullptr: not kept; Kp*M <= kHistMaxKM)
     int dbg;                      // SKY_FILTER_DBG (measurement only, results invalid): 1 = loads + status only
+    // status planes (nullptr: every status word is stored): per tile 32 (item, wave) pairs of
+    // 64-bit words, B = duplicate of the designated group dom_kj (k * M + j), E = the status
+    // word is stored (candidates, other duplicate groups, deferred keys); else dropped
+    uint64_t *planes = nullptr;
+    int32_t dom_kj = -1;
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
@@ -176,6 +181,8 @@ struct OutArgs {
     uint8_t *row_flags;           // optional per tuple: bit0 inL, bit1 inG
     int64_t out_cap = INT64_MAX;  // write pass: output positions >= out_cap are not written
     int select_local;             // output tuples in L instead of G
+    const uint64_t *planes = nullptr;   // the filter's status planes (k_out_write only)
+    int32_t dom_kj = -1;
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);
 // per-tile counts of the global level from the filter's duplicate histograms + k_fate_tables'
@@ -308,16 +315,31 @@ size_t mbr_groups(uint32_t mr);
 hipError_t launch_mbr(const MbrArgs &a, hipStream_t st);
 
 // ---- k_part.hip (per-key operator state, incremental) ----
-void launch_part_pairs(int D, const double *y, uint32_t ny, const double *x, uint32_t nx, const uint8_t *x_alive,
-                       bool same_set, const uint32_t *nanflag, uint32_t *dom, uint32_t *eq, hipStream_t st);
-void launch_part_flags(uint32_t nb, const uint32_t *dom_b, const uint32_t *eq_s, const uint32_t *eq_b, uint32_t *keep,
-                       uint32_t *fresh, hipStream_t st);
-void launch_part_write(int D, uint32_t nb, const int64_t *bids, const double *bvals, const uint32_t *keep,
-                       const uint32_t *keep_pos, const uint32_t *fresh, const uint32_t *fresh_pos, const uint32_t *eq_s,
-                       const uint32_t *eq_b, uint32_t R, uint32_t T, const uint32_t *nanflag, double *rrows,
-                       uint8_t *ralive, uint32_t *rcnt, int64_t *tids, uint32_t *trep, hipStream_t st);
-void launch_part_kill(uint32_t R, const uint32_t *dom_s, const uint32_t *nanflag, uint8_t *ralive, const uint32_t *rcnt,
-                      unsigned long long *dead, hipStream_t st);
+// one part's share of a batched insert (device memory, uploaded with the batch)
+struct PartDesc {
+    const double *bvals;          // [nb][D] this part's batch
+    const int64_t *bids;          // [nb]
+    uint32_t nb;
+    uint32_t rb;                  // bound of the state's rep count (launch sizes; the device count decides)
+    uint32_t *dom_b, *eq_s, *eq_b, *kpos, *fpos;   // [nb] work (dom_b 0, eq_* ~0 on entry)
+    uint32_t *dom_s;              // [rb] work (0 on entry)
+    double *rrows;                // state: reps [R][D], alive, tuples per rep
+    uint8_t *ralive;
+    uint32_t *rcnt;
+    int64_t *tids;                // state: tuples (id, rep) in insertion order
+    uint32_t *trep;
+    uint32_t *dcnt;               // device counts: R, T, dead (u64 lo, hi)
+    uint32_t *mirror;             // host-mapped seqlock mirror of the counts (nullptr: none)
+    uint32_t seq;                 // this insert's sequence number (the mirror's tag)
+};
+struct PartItem {
+    uint32_t part;
+    uint32_t mode;                // 0: batch vs batch, 1: batch vs state reps, 2: state reps vs batch
+    uint32_t y0, x0;              // 256 y rows from y0, kPartChunk x rows from x0
+};
+constexpr uint32_t kPartItemY = 256, kPartItemX = 256;
+void launch_parts_insert(int D, const PartDesc *descs, int nparts, const PartItem *items, uint32_t nitems,
+                         hipStream_t st);
 void launch_part_rkeep(uint32_t R, const uint8_t *ralive, uint32_t *keep, hipStream_t st);
 void launch_part_rmove(int D, uint32_t R, const uint32_t *keep, const uint32_t *pos, const double *rows,
                        const uint32_t *cnt, double *rows2, uint32_t *cnt2, uint8_t *alive2, hipStream_t st);

@@ -55,6 +55,9 @@ SIGNATURES = {
     "sky_ctx_set_stream": [c_p, c_p],
     "sky_ctx_set_grid_filter": [c_p, c_int],
     "sky_ctx_sync": [c_p],
+    "sky_ctx_info": [c_p, P_i32, P_i32, P_i32],
+    "sky_part_info": [c_p, P_i32, P_i32],
+    "sky_stream_info": [c_p, P_i32],
     "sky_ctx_warmup": [c_p],
     "sky_ctx_wait_stream": [c_p, c_p],
     "sky_ctx_signal_stream": [c_p, c_p],
@@ -63,6 +66,7 @@ SIGNATURES = {
     "sky_part_open": [c_p, c_i32, ctypes.POINTER(c_p)],
     "sky_part_close": [c_p],
     "sky_part_insert": [c_p, c_p, c_p, c_i64],
+    "sky_parts_insert": [c_int, c_p, c_p, c_p, c_p],
     "sky_part_size": [c_p, P_i64],
     "sky_part_snapshot": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_global_merge": [c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, P_i64],

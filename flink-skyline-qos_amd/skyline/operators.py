@@ -29,6 +29,22 @@ def now_ms():
     return int(time.time() * 1000)
 
 
+_JAVA_LONG_MAX = (1 << 63) - 1
+
+
+def java_parse_long(s):
+    """Long.parseLong(s): an optional sign and ASCII digits only -- no whitespace, no '_', no
+    other digit scripts (Python's int() accepts all three) -- within the long range; anything
+    else is a NumberFormatException (raised here as ValueError)."""
+    t = s[1:] if s[:1] in ("+", "-") else s
+    if not t or any(c not in "0123456789" for c in t):
+        raise ValueError('NumberFormatException: For input string: "%s"' % s)
+    v = int(s)
+    if v > _JAVA_LONG_MAX or v < -_JAVA_LONG_MAX - 1:
+        raise ValueError('NumberFormatException: For input string: "%s"' % s)
+    return v
+
+
 def java_format_4f(x):
     """String.format(Locale.US, "%.4f", x): Java rounds HALF_UP on the shortest
     decimal representation of the double (FormattedFloatingDecimal)."""
@@ -38,6 +54,16 @@ def java_format_4f(x):
         return "Infinity" if x > 0 else "-Infinity"
     d = decimal.Decimal(repr(float(x)))
     return str(d.quantize(decimal.Decimal("0.0001"), rounding=decimal.ROUND_HALF_UP))
+
+
+def java_split(s, sep=","):
+    """String.split(sep) for a one-character separator: trailing empty strings removed."""
+    parts = s.split(sep)
+    while len(parts) > 1 and parts[-1] == "":
+        parts.pop()
+    if parts == [""] and s != "":
+        return []
+    return parts
 
 
 class ServiceTuple:
@@ -168,6 +194,26 @@ class _LocalPart:
         check(lib().sky_part_insert(self.h, ids.ctypes.data_as(ctypes.c_void_p),
                                     vals.ctypes.data_as(ctypes.c_void_p), len(ids)))
 
+    @staticmethod
+    def insert_many(parts, batches):
+        """One sky_parts_insert call: batches[g] = (ids, values) for parts[g] (parts of one engine):
+        the full buffers of several keys flushed in one launch set, asynchronously."""
+        n = len(parts)
+        if n == 0:
+            return
+        ids = [np.ascontiguousarray(b[0], np.int64) for b in batches]
+        vals = [np.ascontiguousarray(b[1], np.float64) for b in batches]
+        ph = (ctypes.c_void_p * n)(*[p.h.value for p in parts])
+        ip = (ctypes.c_void_p * n)(*[a.ctypes.data for a in ids])
+        vp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in vals])
+        cnt = np.array([len(a) for a in ids], np.int64)
+        check(lib().sky_parts_insert(n, ph, ip, vp, cnt.ctypes.data_as(ctypes.c_void_p)))
+
+    def size(self):
+        n = ctypes.c_int64(0)
+        check(lib().sky_part_size(self.h, ctypes.byref(n)))
+        return n.value
+
     def snapshot(self):
         n = ctypes.c_int64(0)
         check(lib().sky_part_size(self.h, ctypes.byref(n)))
@@ -226,8 +272,29 @@ class SkylineLocalProcessor:
 
     @staticmethod
     def _required(q):
-        parts = q[1].split(",")
-        return int(parts[1]) if len(parts) > 1 else 0
+        """requiredCount of a trigger payload "q,R" (FlinkSkyline.java:303-305, :333-334):
+        split(",") and Long.parseLong with no trim, so "q, 1000" fails as it does there."""
+        parts = java_split(q[1])
+        return java_parse_long(parts[1]) if len(parts) > 1 else 0
+
+    # ---- checkpoints (the reference's localSkylineState is Flink keyed state, :243-248) ----
+    def snapshot_state(self):
+        """What a checkpoint stores: every key's local skyline (ids, values), its buffered
+        tuples flushed into the device state first (HipSkylineOperators.snapshotState)."""
+        out = {}
+        for key in list(self.localSkylineState):
+            if self.inputBuffer.get(key):
+                self.processBuffer(key)
+            out[key] = self.localSkylineState[key].snapshot()
+        return out
+
+    def restore_state(self, state):
+        """Restore by insert into fresh device state: SKY(empty u S) = S, insertion order kept
+        (HipSkylineOperators.initializeState + open)."""
+        for key, (ids, vals) in state.items():
+            part = self._state(key)
+            if len(ids):
+                part.insert(ids, vals)
 
     def _release_global(self, out):
         """Answer every pending query whose ids < R are all in, then replay held tuples."""
@@ -297,8 +364,7 @@ class SkylineLocalProcessor:
             remaining = []
             processed = False
             for q in pending:
-                parts = q[1].split(",")
-                required = int(parts[1]) if len(parts) > 1 else 0
+                required = self._required(q)
                 if max_id >= required:
                     self.processQuery(q, key, out)
                     processed = True
@@ -309,8 +375,7 @@ class SkylineLocalProcessor:
 
     def processElement2(self, trigger, out):
         key = trigger[0]
-        parts = trigger[1].split(",")
-        required = int(parts[1]) if len(parts) > 1 else 0
+        required = self._required(trigger)
         if self.barrier == "global":
             if self.watermark >= required:
                 self.processQuery(trigger, key, out)
@@ -396,7 +461,7 @@ class GlobalSkylineAggregator:
                 if i in sizes and sizes[i] > 0:
                     s += surv.get(i, 0) / sizes[i]
             optimality = s / self.totalPartitions
-            parts = payload.split(",")
+            parts = java_split(payload)
             qid = parts[0]
             rec = parts[1] if len(parts) > 1 else "unknown"
             js = ('{"query_id": "%s", "record_count": %s, "skyline_size": %d, "optimality": %s, '

@@ -91,6 +91,10 @@ int sky_ctx_set_grid_filter(sky_ctx *ctx, int on);
  * NULL returns to the context's own stream. */
 int sky_ctx_set_stream(sky_ctx *ctx, void *hip_stream);
 int sky_ctx_sync(sky_ctx *ctx);
+/* the shape a handle was created with (any pointer may be NULL): FFI shims size arrays by it */
+int sky_ctx_info(sky_ctx *ctx, int32_t *dims, int32_t *num_partitions, int32_t *algo);
+int sky_part_info(sky_part *part, int32_t *key, int32_t *dims);
+int sky_stream_info(sky_stream *s, int32_t *dims);
 /* One-time warm-up: a small device-generated query down each pipeline branch, so that no later
  * query pays for first kernel launches / first allocations inside its latency.  Optional; call
  * once after sky_ctx_create (e.g. in the operator's open()), never on a timed path. */
@@ -114,8 +118,15 @@ int sky_partition_keys_dev(sky_ctx *ctx, const double *d_values, int64_t n, int3
 /* ---- local operator state (one per Flink key) ----------------------------- */
 int sky_part_open(sky_ctx *ctx, int32_t key, sky_part **out);
 int sky_part_close(sky_part *part);
-/* S <- SKY(S u batch)  (processBuffer, FlinkSkyline.java:417-444); duplicates kept */
+/* S <- SKY(S u batch)  (processBuffer, FlinkSkyline.java:417-444); duplicates kept.
+ * Asynchronous: the batch is copied before the call returns and applied on the device without
+ * a host read; size / snapshot wait for every earlier insert.  A batch holding a NaN is
+ * rejected before anything is launched (SKY_E_NAN) and the state is unchanged. */
 int sky_part_insert(sky_part *part, const int64_t *ids, const double *values, int64_t n);
+/* the same for the batches of several keys (parts of ONE context) in one launch set: the
+ * full buffers of a subtask's keys flushed together.  A NaN anywhere rejects the whole call. */
+int sky_parts_insert(int nparts, sky_part *const *parts, const int64_t *const *ids,
+                     const double *const *values, const int64_t *counts);
 int sky_part_size(sky_part *part, int64_t *n_out);
 /* copy of the current local skyline (ids + values), order = ascending insertion order;
  * SKY_E_CAPACITY with *n_out set if cap is too small */

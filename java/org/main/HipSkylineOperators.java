@@ -9,6 +9,10 @@ import org.apache.flink.api.common.typeinfo.TypeInformation;
 import org.apache.flink.api.java.tuple.Tuple3;
 import org.apache.flink.api.java.tuple.Tuple6;
 import org.apache.flink.configuration.Configuration;
+import org.apache.flink.runtime.state.FunctionInitializationContext;
+import org.apache.flink.runtime.state.FunctionSnapshotContext;
+import org.apache.flink.runtime.state.KeyGroupRangeAssignment;
+import org.apache.flink.streaming.api.checkpoint.CheckpointedFunction;
 import org.apache.flink.streaming.api.functions.KeyedProcessFunction;
 import org.apache.flink.streaming.api.functions.co.KeyedCoProcessFunction;
 import org.apache.flink.util.Collector;
@@ -33,6 +37,11 @@ import java.util.Map;
  * Deliberate differences from the reference (DESIGN.md §5): the input buffer is per key (the
  * reference's is shared by a subtask's keys, :223,244); NaN values fail the task
  * (ArithmeticException); the JSON adds "query_latency_ms" (computed at :588, never emitted).
+ * Trigger payloads are parsed exactly as the reference does (split(","), Long.parseLong without
+ * trim, :303-305, :333-334, :627-629): "q, 1000" throws NumberFormatException in both.
+ * Checkpoints: the reference keeps localSkylineState in Flink keyed state (:243-248); the device
+ * state is written into union operator state at every checkpoint (snapshotState) and re-inserted
+ * into fresh device state on restore (initializeState + open), each subtask taking its keys.
  */
 public final class HipSkylineOperators {
     private HipSkylineOperators() {}
@@ -60,11 +69,13 @@ public final class HipSkylineOperators {
 
     /**
      * SkylineLocalProcessor (FlinkSkyline.java:214-445) with the per-key skyline held on the
-     * device: processBuffer's BNL (:417-444) is sky_part_insert on a micro-batch; processQuery's
-     * snapshot (:387-392) is sky_part_snapshot.  The id barrier (:276-356) is unchanged.
+     * device: processBuffer's BNL (:417-444) is an asynchronous sky_parts_insert of the full
+     * buffers of up to FLUSH_GROUP keys; processQuery's snapshot (:387-392) is sky_part_snapshot
+     * (after every waiting buffer).  The id barrier (:276-356) is unchanged.
      */
     public static class LocalProcessor extends KeyedCoProcessFunction<Integer, ServiceTuple,
-            Tuple3<Integer, String, Long>, Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> {
+            Tuple3<Integer, String, Long>, Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>
+            implements CheckpointedFunction {
         private final int dims, partitions, algo;
         private final double domain;
         private transient long ctx;
@@ -74,6 +85,9 @@ public final class HipSkylineOperators {
         private transient ListState<Tuple3<Integer, String, Long>> pendingQueriesState;
         private transient ValueState<Long> startTimeState;
         private transient ValueState<Long> accumulatedCpuNanosState;
+        // the device skylines at the last checkpoint: (key, ids, values row-major), union-redistributed
+        private transient ListState<Tuple3<Integer, long[], double[]>> checkpointedSkylines;
+        private transient List<Tuple3<Integer, long[], double[]>> restored;
 
         public LocalProcessor(int dims, int partitions, String algo, double domain) {
             this.dims = dims;
@@ -93,10 +107,52 @@ public final class HipSkylineOperators {
                     TypeInformation.of(new TypeHint<Tuple3<Integer, String, Long>>() {})));
             startTimeState = getRuntimeContext().getState(new ValueStateDescriptor<>("jobStartTime", Long.class));
             accumulatedCpuNanosState = getRuntimeContext().getState(new ValueStateDescriptor<>("cpuTime", Long.class));
+            restoreInto();
+        }
+
+        /** Checkpoint: every key's device skyline (its buffered tuples flushed first, so nothing
+         *  that arrived before the barrier is lost) into union operator state. */
+        @Override
+        public void snapshotState(FunctionSnapshotContext fc) throws Exception {
+            checkpointedSkylines.clear();
+            drainFull();
+            for (int key : new ArrayList<>(buffers.keySet())) flush(key);
+            for (Map.Entry<Integer, Long> e : parts.entrySet()) {
+                final long p = e.getValue();
+                int n = (int) SkylineHip.partSize(p);
+                long[] ids = new long[n];
+                double[] vals = new double[n * dims];
+                n = SkylineHip.partSnapshot(p, ids, vals);
+                checkpointedSkylines.add(Tuple3.of(e.getKey(), ids, vals));
+            }
+        }
+
+        @Override
+        public void initializeState(FunctionInitializationContext fc) throws Exception {
+            checkpointedSkylines = fc.getOperatorStateStore().getUnionListState(new ListStateDescriptor<>(
+                    "hipLocalSky", TypeInformation.of(new TypeHint<Tuple3<Integer, long[], double[]>>() {})));
+            restored = new ArrayList<>();
+            if (fc.isRestored())
+                for (Tuple3<Integer, long[], double[]> t : checkpointedSkylines.get()) restored.add(t);
+        }
+
+        /** Restore by insert: SKY(empty u S) = S for a skyline S, insertion order kept; each
+         *  subtask takes the keys of its key-group range (the state is union-redistributed). */
+        private void restoreInto() {
+            if (restored == null || restored.isEmpty()) return;
+            final int maxPar = getRuntimeContext().getMaxNumberOfParallelSubtasks();
+            final int par = getRuntimeContext().getNumberOfParallelSubtasks();
+            final int idx = getRuntimeContext().getIndexOfThisSubtask();
+            for (Tuple3<Integer, long[], double[]> t : restored) {
+                if (KeyGroupRangeAssignment.assignKeyToParallelOperator(t.f0, maxPar, par) != idx) continue;
+                if (t.f1.length > 0) SkylineHip.partInsert(part(t.f0), t.f1, t.f2, t.f1.length);
+            }
+            restored.clear();
         }
 
         @Override
         public void close() {   // the reference has no close(); device state is released here
+            full = null;
             for (long p : parts.values()) SkylineHip.partClose(p);
             parts.clear();
             if (ctx != 0) SkylineHip.ctxDestroy(ctx);
@@ -107,7 +163,36 @@ public final class HipSkylineOperators {
             return parts.computeIfAbsent(key, k -> SkylineHip.partOpen(ctx, k));
         }
 
+        // full buffers waiting to go to the device together (one partsInsert per round of keys)
+        private static final int FLUSH_GROUP = 8;
+        private transient List<Tuple3<Integer, KeyBuffer, Integer>> full;
+
+        /** processBuffer for every full buffer waiting: S <- SKY(S u buffer) per key, in one
+         *  asynchronous launch set per round (a key appears once per round, in arrival order). */
+        private void drainFull() {
+            if (full == null || full.isEmpty()) return;
+            while (!full.isEmpty()) {
+                List<Tuple3<Integer, KeyBuffer, Integer>> round = new ArrayList<>(), later = new ArrayList<>();
+                java.util.Set<Integer> seen = new java.util.HashSet<>();
+                for (Tuple3<Integer, KeyBuffer, Integer> t : full) (seen.add(t.f0) ? round : later).add(t);
+                long[] ps = new long[round.size()];
+                long[][] is = new long[round.size()][];
+                double[][] vs = new double[round.size()][];
+                int[] cs = new int[round.size()];
+                for (int g = 0; g < round.size(); g++) {
+                    Tuple3<Integer, KeyBuffer, Integer> t = round.get(g);
+                    ps[g] = part(t.f0);
+                    is[g] = t.f1.ids;
+                    vs[g] = t.f1.values;
+                    cs[g] = t.f2;
+                }
+                SkylineHip.partsInsert(ps, is, vs, cs);    // copied before it returns
+                full = later;
+            }
+        }
+
         private void flush(int key) {
+            drainFull();
             KeyBuffer b = buffers.get(key);
             if (b != null && b.n > 0) {
                 SkylineHip.partInsert(part(key), b.ids, b.values, b.n);   // S <- SKY(S u buffer)
@@ -115,9 +200,9 @@ public final class HipSkylineOperators {
             }
         }
 
-        private static long required(Tuple3<Integer, String, Long> q) {
+        private static long required(Tuple3<Integer, String, Long> q) {   // :303-305, :333-334
             String[] parts = q.f1.split(",");
-            return parts.length > 1 ? Long.parseLong(parts[1].trim()) : 0L;
+            return parts.length > 1 ? Long.parseLong(parts[1]) : 0L;
         }
 
         private void addCpu(long startNano) throws Exception {
@@ -138,7 +223,13 @@ public final class HipSkylineOperators {
                 maxSeenIdState.update(id);
                 maxId = id;
             }
-            if (buffers.computeIfAbsent(key, k -> new KeyBuffer(dims)).add(id, point.values)) flush(key);
+            if (buffers.computeIfAbsent(key, k -> new KeyBuffer(dims)).add(id, point.values)) {
+                // the full buffer waits for FLUSH_GROUP of them; the key continues in a fresh one
+                if (full == null) full = new ArrayList<>();
+                full.add(Tuple3.of(key, buffers.get(key), BUFFER_SIZE));
+                buffers.put(key, new KeyBuffer(dims));
+                if (full.size() >= FLUSH_GROUP) drainFull();
+            }
             addCpu(startNano);
             List<Tuple3<Integer, String, Long>> remaining = new ArrayList<>();
             boolean released = false;
@@ -269,9 +360,9 @@ public final class HipSkylineOperators {
             final long jobStart = minStartTimeState.value();
             final long mapWall = lastArrival - jobStart;
             final long ingest = Math.max(0, mapWall - maxCpu);
-            String[] payload = in.f1.split(",");
-            String records = payload.length > 1 ? payload[1].trim() : "unknown";
-            out.collect("{\"query_id\": \"" + payload[0].trim() + "\", \"record_count\": " + records
+            String[] payload = in.f1.split(",");                       // :627-629
+            String records = payload.length > 1 ? payload[1] : "unknown";
+            out.collect("{\"query_id\": \"" + payload[0] + "\", \"record_count\": " + records
                     + ", \"skyline_size\": " + g
                     + ", \"optimality\": " + String.format(Locale.US, "%.4f", optimality)
                     + ", \"ingestion_time_ms\": " + ingest

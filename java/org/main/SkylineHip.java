@@ -7,7 +7,8 @@ package org.main;
  * tests/operator_replay.c (C) and by the Python binding (flink-skyline-qos_amd/skyline/).
  *
  * Handles are opaque longs.  Arrays: ids long[n], values double[n * dims] row-major.
- * Failures throw RuntimeException(sky_last_error()); a NaN value throws ArithmeticException.
+ * Failures throw RuntimeException(sky_last_error()); a NaN value throws ArithmeticException;
+ * arrays shorter than the call needs throw IllegalArgumentException.
  * Methods returning an int count return -required when an output array is too small.
  */
 public final class SkylineHip {
@@ -41,6 +42,8 @@ public final class SkylineHip {
     public static native long partOpen(long ctx, int key);
     public static native void partClose(long part);
     public static native void partInsert(long part, long[] ids, double[] values, int n);
+    /** the full buffers of several keys (parts of one context) in one launch set */
+    public static native void partsInsert(long[] parts, long[][] ids, double[][] values, int[] counts);
     public static native long partSize(long part);
     public static native int partSnapshot(long part, long[] idsOut, double[] valuesOut);
 

@@ -11,9 +11,11 @@
  *       -Wl,-rpath,'$ORIGIN' -o libskyline_hip_jni.so
  *
  * Arrays cross as Java primitive arrays: ids long[n], values double[n*dims] (row-major, the
- * layout of ServiceTuple.values concatenated).  The library copies host buffers before it
- * returns, so arrays are pinned only for the duration of one call (GetPrimitiveArrayCritical,
- * no JNI calls in between).  Handles are jlong (uintptr_t) values of the C pointers.
+ * layout of ServiceTuple.values concatenated).  Every array is checked against what the C call
+ * reads or writes (IllegalArgumentException otherwise), and a NULL from Get*Critical leaves the
+ * pending OutOfMemoryError.  The library copies host buffers before it returns, so arrays are
+ * pinned only for the duration of one call (GetPrimitiveArrayCritical, no JNI calls in
+ * between).  Handles are jlong (uintptr_t) values of the C pointers.
  *
  * The C call sequence these natives produce is replayed by tests/operator_replay.c, which the
  * GPU test tests/test_gpu_replay.py runs on the golden streams.
@@ -31,9 +33,35 @@ static jboolean fail(JNIEnv *env, int rc) {
     return JNI_TRUE;
 }
 
+static jboolean throw_arg(JNIEnv *env, const char *msg) {
+    (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/IllegalArgumentException"), msg);
+    return JNI_TRUE;
+}
+
+/* every array a native reads or writes is checked against what the C call will touch: a
+ * misuse from Java is an IllegalArgumentException, never an out-of-bounds native access */
+static jboolean bad_len(JNIEnv *env, jarray a, jlong need, const char *what) {
+    if (!a) return throw_arg(env, what);
+    if ((jlong)(*env)->GetArrayLength(env, a) < need) return throw_arg(env, what);
+    return JNI_FALSE;
+}
+
+/* GetPrimitiveArrayCritical may return NULL (out of memory): an OutOfMemoryError is pending */
+#define CRIT(arr) ((*env)->GetPrimitiveArrayCritical(env, (arr), NULL))
+#define UNCRIT(arr, p, mode) do { if (p) (*env)->ReleasePrimitiveArrayCritical(env, (arr), (p), (mode)); } while (0)
+
 #define CTX(h) ((sky_ctx *)(uintptr_t)(h))
 #define PART(h) ((sky_part *)(uintptr_t)(h))
 #define STREAM(h) ((sky_stream *)(uintptr_t)(h))
+
+static int ctx_dims(sky_ctx *c) {
+    int32_t d = 0;
+    return sky_ctx_info(c, &d, NULL, NULL) == SKY_OK ? d : -1;
+}
+static int part_dims(sky_part *p) {
+    int32_t d = 0;
+    return sky_part_info(p, NULL, &d) == SKY_OK ? d : -1;
+}
 
 /* ---- context: SkylineLocalProcessor.open() / GlobalSkylineAggregator.open() ---- */
 JNIEXPORT jlong JNICALL Java_org_main_SkylineHip_ctxCreate(JNIEnv *env, jclass cls, jint device, jint dims,
@@ -63,12 +91,17 @@ JNIEXPORT void JNICALL Java_org_main_SkylineHip_ctxSetGridFilter(JNIEnv *env, jc
 /* ---- partitioners: SkylinePartitioner.getKey over a batch (FlinkSkyline.java:675) ---- */
 JNIEXPORT void JNICALL Java_org_main_SkylineHip_partitionKeys(JNIEnv *env, jclass cls, jlong ctx,
                                                                jdoubleArray values, jint n, jintArray keys_out) {
-    jdouble *v = (*env)->GetPrimitiveArrayCritical(env, values, NULL);
-    jint *k = (*env)->GetPrimitiveArrayCritical(env, keys_out, NULL);
-    const int rc = sky_partition_keys(CTX(ctx), v, n, (int32_t *)k);
-    (*env)->ReleasePrimitiveArrayCritical(env, keys_out, k, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, values, v, JNI_ABORT);
-    fail(env, rc);
+    const int D = ctx_dims(CTX(ctx));
+    if (n < 0 || D < 1) { throw_arg(env, "partitionKeys: bad n or context"); return; }
+    if (bad_len(env, values, (jlong)n * D, "partitionKeys: values shorter than n * dims") ||
+        bad_len(env, keys_out, n, "partitionKeys: keysOut shorter than n"))
+        return;
+    jdouble *v = CRIT(values);
+    jint *k = CRIT(keys_out);
+    const int rc = v && k ? sky_partition_keys(CTX(ctx), v, n, (int32_t *)k) : SKY_E_NOMEM;
+    UNCRIT(keys_out, k, 0);
+    UNCRIT(values, v, JNI_ABORT);
+    if (v && k) fail(env, rc);
 }
 
 /* ---- local operator state: localSkylineState + processBuffer (FlinkSkyline.java:221, :417-444) ---- */
@@ -84,12 +117,82 @@ JNIEXPORT void JNICALL Java_org_main_SkylineHip_partClose(JNIEnv *env, jclass cl
 
 JNIEXPORT void JNICALL Java_org_main_SkylineHip_partInsert(JNIEnv *env, jclass cls, jlong part, jlongArray ids,
                                                             jdoubleArray values, jint n) {
-    jlong *pi = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
-    jdouble *pv = (*env)->GetPrimitiveArrayCritical(env, values, NULL);
-    const int rc = sky_part_insert(PART(part), (const int64_t *)pi, pv, n);   /* copies before return */
-    (*env)->ReleasePrimitiveArrayCritical(env, values, pv, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids, pi, JNI_ABORT);
-    fail(env, rc);
+    const int D = part_dims(PART(part));
+    if (n < 0 || D < 1) { throw_arg(env, "partInsert: bad n or part"); return; }
+    if (n == 0) return;
+    if (bad_len(env, ids, n, "partInsert: ids shorter than n") ||
+        bad_len(env, values, (jlong)n * D, "partInsert: values shorter than n * dims"))
+        return;
+    jlong *pi = CRIT(ids);
+    jdouble *pv = CRIT(values);
+    const int rc = pi && pv ? sky_part_insert(PART(part), (const int64_t *)pi, pv, n) : SKY_E_NOMEM;   /* copies */
+    UNCRIT(values, pv, JNI_ABORT);
+    UNCRIT(ids, pi, JNI_ABORT);
+    if (pi && pv) fail(env, rc);
+}
+
+/* the full buffers of several keys in one call (sky_parts_insert): parts[g] gets
+ * ids[g][0..counts[g]) / values[g][0..counts[g] * dims) */
+JNIEXPORT void JNICALL Java_org_main_SkylineHip_partsInsert(JNIEnv *env, jclass cls, jlongArray parts,
+                                                             jobjectArray ids, jobjectArray values, jintArray counts) {
+    if (!parts || !ids || !values || !counts) { throw_arg(env, "partsInsert: null argument"); return; }
+    const jsize np = (*env)->GetArrayLength(env, parts);
+    if ((*env)->GetArrayLength(env, ids) != np || (*env)->GetArrayLength(env, values) != np ||
+        (*env)->GetArrayLength(env, counts) != np) {
+        throw_arg(env, "partsInsert: arrays of different lengths");
+        return;
+    }
+    if (np == 0) return;
+    sky_part **pp = calloc((size_t)np, sizeof(sky_part *));
+    const int64_t **pids = calloc((size_t)np, sizeof(int64_t *));
+    const double **pvals = calloc((size_t)np, sizeof(double *));
+    int64_t *cnt = calloc((size_t)np, sizeof(int64_t));
+    jlongArray *ja = calloc((size_t)np, sizeof(jlongArray));
+    jdoubleArray *jv = calloc((size_t)np, sizeof(jdoubleArray));
+    jsize got = 0;
+    if (!pp || !pids || !pvals || !cnt || !ja || !jv) {
+        (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/OutOfMemoryError"), "partsInsert");
+        goto out;
+    }
+    {
+        jlong *ph = (*env)->GetLongArrayElements(env, parts, NULL);
+        jint *pc = (*env)->GetIntArrayElements(env, counts, NULL);
+        if (!ph || !pc) goto out;
+        for (jsize g = 0; g < np; g++) { pp[g] = PART(ph[g]); cnt[g] = pc[g]; }
+        (*env)->ReleaseIntArrayElements(env, counts, pc, JNI_ABORT);
+        (*env)->ReleaseLongArrayElements(env, parts, ph, JNI_ABORT);
+    }
+    for (jsize g = 0; g < np; g++) {   /* Get*ArrayElements: several arrays stay pinned/copied at once */
+        const int D = part_dims(pp[g]);
+        ja[g] = (jlongArray)(*env)->GetObjectArrayElement(env, ids, g);
+        jv[g] = (jdoubleArray)(*env)->GetObjectArrayElement(env, values, g);
+        if (D < 1 || cnt[g] < 0 || bad_len(env, ja[g], cnt[g], "partsInsert: ids[g] shorter than counts[g]") ||
+            bad_len(env, jv[g], cnt[g] * D, "partsInsert: values[g] shorter than counts[g] * dims")) {
+            if (!(*env)->ExceptionCheck(env)) throw_arg(env, "partsInsert: bad part or count");
+            goto release;
+        }
+        pids[g] = (const int64_t *)(*env)->GetLongArrayElements(env, ja[g], NULL);
+        pvals[g] = (*env)->GetDoubleArrayElements(env, jv[g], NULL);
+        got = g + 1;
+        if (!pids[g] || !pvals[g]) goto release;
+    }
+    fail(env, sky_parts_insert(np, pp, pids, pvals, cnt));   /* copies before it returns */
+release:
+    for (jsize g = 0; g < np; g++) {
+        if (g < got) {
+            if (pvals[g]) (*env)->ReleaseDoubleArrayElements(env, jv[g], (jdouble *)pvals[g], JNI_ABORT);
+            if (pids[g]) (*env)->ReleaseLongArrayElements(env, ja[g], (jlong *)pids[g], JNI_ABORT);
+        }
+        if (jv[g]) (*env)->DeleteLocalRef(env, jv[g]);
+        if (ja[g]) (*env)->DeleteLocalRef(env, ja[g]);
+    }
+out:
+    free(pp);
+    free(pids);
+    free(pvals);
+    free(cnt);
+    free(ja);
+    free(jv);
 }
 
 JNIEXPORT jlong JNICALL Java_org_main_SkylineHip_partSize(JNIEnv *env, jclass cls, jlong part) {
@@ -101,13 +204,18 @@ JNIEXPORT jlong JNICALL Java_org_main_SkylineHip_partSize(JNIEnv *env, jclass cl
 /* processQuery's snapshot (:387-392): returns n, or -required if the arrays are too small */
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partSnapshot(JNIEnv *env, jclass cls, jlong part,
                                                               jlongArray ids_out, jdoubleArray values_out) {
-    const jsize cap = (*env)->GetArrayLength(env, ids_out);
-    jlong *pi = (*env)->GetPrimitiveArrayCritical(env, ids_out, NULL);
-    jdouble *pv = (*env)->GetPrimitiveArrayCritical(env, values_out, NULL);
+    const int D = part_dims(PART(part));
+    if (D < 1 || !ids_out || !values_out) { throw_arg(env, "partSnapshot: bad part or null array"); return 0; }
+    jsize cap = (*env)->GetArrayLength(env, ids_out);
+    const jsize vcap = (*env)->GetArrayLength(env, values_out) / D;
+    if (vcap < cap) cap = vcap;            /* both arrays must hold the snapshot */
+    jlong *pi = CRIT(ids_out);
+    jdouble *pv = CRIT(values_out);
     int64_t n = 0;
-    const int rc = sky_part_snapshot(PART(part), (int64_t *)pi, pv, cap, &n);
-    (*env)->ReleasePrimitiveArrayCritical(env, values_out, pv, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids_out, pi, 0);
+    const int rc = pi && pv ? sky_part_snapshot(PART(part), (int64_t *)pi, pv, cap, &n) : SKY_E_NOMEM;
+    UNCRIT(values_out, pv, 0);
+    UNCRIT(ids_out, pi, 0);
+    if (!pi || !pv) return 0;
     if (rc == SKY_E_CAPACITY) return (jint)-n;
     if (fail(env, rc)) return 0;
     return (jint)n;
@@ -128,32 +236,50 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalMerge(JNIEnv *env, jclass 
         (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/OutOfMemoryError"), "globalMerge");
         goto out;
     }
+    const int D = ctx_dims(CTX(ctx));
+    jsize got = 0;
+    if (D < 1 || !ids || !values || !ids_out || !origin_out || (*env)->GetArrayLength(env, ids) != np ||
+        (*env)->GetArrayLength(env, values) != np) {
+        throw_arg(env, "globalMerge: bad context or arrays");
+        goto out;
+    }
     for (jsize k = 0; k < np; k++) {   /* Get*ArrayElements: several arrays stay pinned/copied at once */
         ja[k] = (jlongArray)(*env)->GetObjectArrayElement(env, ids, k);
         jv[k] = (jdoubleArray)(*env)->GetObjectArrayElement(env, values, k);
+        if (!ja[k] || bad_len(env, jv[k], (jlong)(*env)->GetArrayLength(env, ja[k]) * D,
+                               "globalMerge: values[k] shorter than ids[k].length * dims"))
+            goto release;
         counts[k] = (*env)->GetArrayLength(env, ja[k]);
         pids[k] = (const int64_t *)(*env)->GetLongArrayElements(env, ja[k], NULL);
         pvals[k] = (*env)->GetDoubleArrayElements(env, jv[k], NULL);
+        got = k + 1;
+        if (!pids[k] || !pvals[k]) goto release;
     }
     {
+        const jsize cap = (*env)->GetArrayLength(env, ids_out);
+        if ((*env)->GetArrayLength(env, origin_out) < cap) { throw_arg(env, "globalMerge: originOut shorter than idsOut"); goto release; }
         jint *pk = (*env)->GetIntArrayElements(env, part_ids, NULL);
         jlong *oi = (*env)->GetLongArrayElements(env, ids_out, NULL);
         jint *oo = (*env)->GetIntArrayElements(env, origin_out, NULL);
-        const jsize cap = (*env)->GetArrayLength(env, ids_out);
-        int64_t n = 0;
-        const int rc = sky_global_merge(CTX(ctx), np, (const int32_t *)pk, pids, pvals, counts, (int64_t *)oi,
-                                        (int32_t *)oo, cap, &n);
-        (*env)->ReleaseIntArrayElements(env, origin_out, oo, 0);
-        (*env)->ReleaseLongArrayElements(env, ids_out, oi, 0);
-        (*env)->ReleaseIntArrayElements(env, part_ids, pk, JNI_ABORT);
-        if (rc == SKY_E_CAPACITY) g = (jint)-n;
-        else if (!fail(env, rc)) g = (jint)n;
+        if (pk && oi && oo) {
+            int64_t n = 0;
+            const int rc = sky_global_merge(CTX(ctx), np, (const int32_t *)pk, pids, pvals, counts, (int64_t *)oi,
+                                            (int32_t *)oo, cap, &n);
+            if (rc == SKY_E_CAPACITY) g = (jint)-n;
+            else if (!fail(env, rc)) g = (jint)n;
+        }
+        if (oo) (*env)->ReleaseIntArrayElements(env, origin_out, oo, 0);
+        if (oi) (*env)->ReleaseLongArrayElements(env, ids_out, oi, 0);
+        if (pk) (*env)->ReleaseIntArrayElements(env, part_ids, pk, JNI_ABORT);
     }
+release:
     for (jsize k = 0; k < np; k++) {
-        (*env)->ReleaseDoubleArrayElements(env, jv[k], (jdouble *)pvals[k], JNI_ABORT);
-        (*env)->ReleaseLongArrayElements(env, ja[k], (jlong *)pids[k], JNI_ABORT);
-        (*env)->DeleteLocalRef(env, jv[k]);
-        (*env)->DeleteLocalRef(env, ja[k]);
+        if (k < got) {
+            if (pvals[k]) (*env)->ReleaseDoubleArrayElements(env, jv[k], (jdouble *)pvals[k], JNI_ABORT);
+            if (pids[k]) (*env)->ReleaseLongArrayElements(env, ja[k], (jlong *)pids[k], JNI_ABORT);
+        }
+        if (jv[k]) (*env)->DeleteLocalRef(env, jv[k]);
+        if (ja[k]) (*env)->DeleteLocalRef(env, ja[k]);
     }
 out:
     free(pids);
@@ -169,13 +295,14 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalStats(JNIEnv *env, jclass 
                                                              jlongArray local_sizes, jlongArray survivors) {
     int32_t K = 0;
     if (fail(env, sky_global_stats(CTX(ctx), NULL, NULL, &K))) return 0;
+    if (!local_sizes || !survivors) { throw_arg(env, "globalStats: null array"); return 0; }
     if ((*env)->GetArrayLength(env, local_sizes) < K || (*env)->GetArrayLength(env, survivors) < K) return -K;
     jlong *ls = (*env)->GetLongArrayElements(env, local_sizes, NULL);
     jlong *sv = (*env)->GetLongArrayElements(env, survivors, NULL);
-    const int rc = sky_global_stats(CTX(ctx), (int64_t *)ls, (int64_t *)sv, &K);
-    (*env)->ReleaseLongArrayElements(env, survivors, sv, 0);
-    (*env)->ReleaseLongArrayElements(env, local_sizes, ls, 0);
-    fail(env, rc);
+    const int rc = ls && sv ? sky_global_stats(CTX(ctx), (int64_t *)ls, (int64_t *)sv, &K) : SKY_E_NOMEM;
+    if (sv) (*env)->ReleaseLongArrayElements(env, survivors, sv, 0);
+    if (ls) (*env)->ReleaseLongArrayElements(env, local_sizes, ls, 0);
+    if (ls && sv) fail(env, rc);
     return K;
 }
 
@@ -183,17 +310,28 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalStats(JNIEnv *env, jclass 
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_query(JNIEnv *env, jclass cls, jlong ctx, jlongArray ids,
                                                        jdoubleArray values, jint n, jlongArray ids_out,
                                                        jintArray origin_out) {
-    const jsize cap = (*env)->GetArrayLength(env, ids_out);
-    jlong *pi = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
-    jdouble *pv = (*env)->GetPrimitiveArrayCritical(env, values, NULL);
-    jlong *oi = (*env)->GetPrimitiveArrayCritical(env, ids_out, NULL);
-    jint *oo = (*env)->GetPrimitiveArrayCritical(env, origin_out, NULL);
+    const int D = ctx_dims(CTX(ctx));
+    if (n < 0 || D < 1 || bad_len(env, ids, n, "query: ids shorter than n") ||
+        bad_len(env, values, (jlong)n * D, "query: values shorter than n * dims") ||
+        bad_len(env, ids_out, 0, "query: null idsOut") || bad_len(env, origin_out, 0, "query: null originOut")) {
+        if (!(*env)->ExceptionCheck(env)) throw_arg(env, "query: bad n or context");
+        return 0;
+    }
+    jsize cap = (*env)->GetArrayLength(env, ids_out);
+    if ((*env)->GetArrayLength(env, origin_out) < cap) cap = (*env)->GetArrayLength(env, origin_out);
+    jlong *pi = CRIT(ids);
+    jdouble *pv = CRIT(values);
+    jlong *oi = CRIT(ids_out);
+    jint *oo = CRIT(origin_out);
     int64_t g = 0;
-    const int rc = sky_query(CTX(ctx), (const int64_t *)pi, pv, n, (int64_t *)oi, (int32_t *)oo, cap, &g);
-    (*env)->ReleasePrimitiveArrayCritical(env, origin_out, oo, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids_out, oi, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, values, pv, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids, pi, JNI_ABORT);
+    const int ok = pi && pv && oi && oo;
+    const int rc = ok ? sky_query(CTX(ctx), (const int64_t *)pi, pv, n, (int64_t *)oi, (int32_t *)oo, cap, &g)
+                      : SKY_E_NOMEM;
+    UNCRIT(origin_out, oo, 0);
+    UNCRIT(ids_out, oi, 0);
+    UNCRIT(values, pv, JNI_ABORT);
+    UNCRIT(ids, pi, JNI_ABORT);
+    if (!ok) return 0;
     if (rc == SKY_E_CAPACITY) return (jint)-g;
     if (fail(env, rc)) return 0;
     return (jint)g;
@@ -205,17 +343,28 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_query(JNIEnv *env, jclass cls, j
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_parseCsv(JNIEnv *env, jclass cls, jlong ctx, jbyteArray text,
                                                           jint nbytes, jlongArray ids_out, jdoubleArray values_out,
                                                           jlongArray counts_out) {
-    const jsize cap = (*env)->GetArrayLength(env, ids_out);
-    jbyte *t = (*env)->GetPrimitiveArrayCritical(env, text, NULL);
-    jlong *oi = (*env)->GetPrimitiveArrayCritical(env, ids_out, NULL);
-    jdouble *ov = (*env)->GetPrimitiveArrayCritical(env, values_out, NULL);
-    jlong *oc = (*env)->GetPrimitiveArrayCritical(env, counts_out, NULL);
+    const int D = ctx_dims(CTX(ctx));
+    if (nbytes < 0 || D < 1 || bad_len(env, text, nbytes, "parseCsv: text shorter than nbytes") ||
+        bad_len(env, counts_out, 4, "parseCsv: countsOut shorter than 4") ||
+        bad_len(env, ids_out, 0, "parseCsv: null idsOut") || bad_len(env, values_out, 0, "parseCsv: null valuesOut")) {
+        if (!(*env)->ExceptionCheck(env)) throw_arg(env, "parseCsv: bad nbytes or context");
+        return 0;
+    }
+    jsize cap = (*env)->GetArrayLength(env, ids_out);
+    if ((*env)->GetArrayLength(env, values_out) / D < cap) cap = (*env)->GetArrayLength(env, values_out) / D;
+    jbyte *t = CRIT(text);
+    jlong *oi = CRIT(ids_out);
+    jdouble *ov = CRIT(values_out);
+    jlong *oc = CRIT(counts_out);
     int64_t n = 0;
-    const int rc = sky_parse_csv(CTX(ctx), (const char *)t, nbytes, (int64_t *)oi, ov, cap, &n, (int64_t *)oc);
-    (*env)->ReleasePrimitiveArrayCritical(env, counts_out, oc, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, values_out, ov, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids_out, oi, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, text, t, JNI_ABORT);
+    const int ok = t && oi && ov && oc;
+    const int rc = ok ? sky_parse_csv(CTX(ctx), (const char *)t, nbytes, (int64_t *)oi, ov, cap, &n, (int64_t *)oc)
+                      : SKY_E_NOMEM;
+    UNCRIT(counts_out, oc, 0);
+    UNCRIT(values_out, ov, 0);
+    UNCRIT(ids_out, oi, 0);
+    UNCRIT(text, t, JNI_ABORT);
+    if (!ok) return 0;
     if (rc == SKY_E_CAPACITY) return (jint)-n;
     if (fail(env, rc)) return 0;
     return (jint)n;
@@ -234,23 +383,32 @@ JNIEXPORT void JNICALL Java_org_main_SkylineHip_streamDestroy(JNIEnv *env, jclas
 
 JNIEXPORT void JNICALL Java_org_main_SkylineHip_streamAppend(JNIEnv *env, jclass cls, jlong s, jlongArray ids,
                                                               jdoubleArray values, jint n) {
-    jlong *pi = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
-    jdouble *pv = (*env)->GetPrimitiveArrayCritical(env, values, NULL);
-    const int rc = sky_stream_append(STREAM(s), (const int64_t *)pi, pv, n);
-    (*env)->ReleasePrimitiveArrayCritical(env, values, pv, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids, pi, JNI_ABORT);
-    fail(env, rc);
+    int32_t D = 0;
+    if (n < 0 || sky_stream_info(STREAM(s), &D) != SKY_OK || D < 1) { throw_arg(env, "streamAppend: bad n or stream"); return; }
+    if (n == 0) return;
+    if (bad_len(env, ids, n, "streamAppend: ids shorter than n") ||
+        bad_len(env, values, (jlong)n * D, "streamAppend: values shorter than n * dims"))
+        return;
+    jlong *pi = CRIT(ids);
+    jdouble *pv = CRIT(values);
+    const int rc = pi && pv ? sky_stream_append(STREAM(s), (const int64_t *)pi, pv, n) : SKY_E_NOMEM;
+    UNCRIT(values, pv, JNI_ABORT);
+    UNCRIT(ids, pi, JNI_ABORT);
+    if (pi && pv) fail(env, rc);
 }
 
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_streamQuery(JNIEnv *env, jclass cls, jlong s, jlongArray ids_out,
                                                              jintArray origin_out) {
-    const jsize cap = (*env)->GetArrayLength(env, ids_out);
-    jlong *oi = (*env)->GetPrimitiveArrayCritical(env, ids_out, NULL);
-    jint *oo = (*env)->GetPrimitiveArrayCritical(env, origin_out, NULL);
+    if (!ids_out || !origin_out) { throw_arg(env, "streamQuery: null array"); return 0; }
+    jsize cap = (*env)->GetArrayLength(env, ids_out);
+    if ((*env)->GetArrayLength(env, origin_out) < cap) cap = (*env)->GetArrayLength(env, origin_out);
+    jlong *oi = CRIT(ids_out);
+    jint *oo = CRIT(origin_out);
     int64_t g = 0;
-    const int rc = sky_stream_query(STREAM(s), (int64_t *)oi, (int32_t *)oo, cap, &g);
-    (*env)->ReleasePrimitiveArrayCritical(env, origin_out, oo, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, ids_out, oi, 0);
+    const int rc = oi && oo ? sky_stream_query(STREAM(s), (int64_t *)oi, (int32_t *)oo, cap, &g) : SKY_E_NOMEM;
+    UNCRIT(origin_out, oo, 0);
+    UNCRIT(ids_out, oi, 0);
+    if (!oi || !oo) return 0;
     if (rc == SKY_E_CAPACITY) return (jint)-g;
     if (fail(env, rc)) return 0;
     return (jint)g;

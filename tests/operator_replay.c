@@ -13,7 +13,14 @@
  *   global    GlobalSkylineAggregator: sky_global_merge over the P lists + sky_global_stats
  *             (:515-608), then the JSON payload of :631-648 plus "query_latency_ms"
  *
- * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain]
+ *   batching  full buffers wait in groups of G keys (default 8, as HipSkylineOperators'
+ *             FLUSH_GROUP) and go to the device in one sky_parts_insert per round of keys
+ *   checkpoint after C tuples (optional): every key's buffer flushed and its skyline snapshot
+ *             taken (snapshotState), every part and the context closed (a failure), a fresh
+ *             context opened and each snapshot re-inserted (initializeState + open); the stream
+ *             then continues, and the answer must not change
+ *
+ * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain] [checkpoint C | -1] [G]
  * stdout: the JSON line, then "ids" and the sorted global skyline ids, then "lsz" / "surv".
  */
 #include <stdint.h>
@@ -80,7 +87,41 @@ typedef struct {
     int64_t *ids;
     double *vals;
     int64_t n;
+    int64_t *fids[64];   /* full buffers waiting for their group (a key fills at most 64 meanwhile) */
+    double *fvals[64];
+    int nfull;
 } keyed_state;
+
+/* every waiting full buffer, one sky_parts_insert per round (each key at most once a round) */
+static void drain_full(keyed_state *ks, int kmax, int D) {
+    for (;;) {
+        sky_part *pp[256];
+        const int64_t *pi[256];
+        const double *pv[256];
+        int64_t cnt[256];
+        int np = 0;
+        for (int k = 0; k < kmax && np < 256; k++) {
+            if (!ks[k].nfull) continue;
+            pp[np] = ks[k].part;
+            pi[np] = ks[k].fids[0];
+            pv[np] = ks[k].fvals[0];
+            cnt[np] = BUFFER_SIZE;
+            np++;
+        }
+        if (!np) return;
+        CHECK(sky_parts_insert(np, pp, pi, pv, cnt));   /* copied before it returns */
+        for (int k = 0, g = 0; k < kmax && g < np; k++) {
+            if (!ks[k].nfull) continue;
+            free(ks[k].fids[0]);
+            free(ks[k].fvals[0]);
+            memmove(ks[k].fids, ks[k].fids + 1, (size_t)(ks[k].nfull - 1) * sizeof(int64_t *));
+            memmove(ks[k].fvals, ks[k].fvals + 1, (size_t)(ks[k].nfull - 1) * sizeof(double *));
+            ks[k].nfull--;
+            g++;
+        }
+        (void)D;
+    }
+}
 
 int main(int argc, char **argv) {
     if (argc >= 2 && strcmp(argv[1], "--fmt") == 0) {   /* formatter self-check (no device) */
@@ -97,6 +138,8 @@ int main(int argc, char **argv) {
     }
     const int D = atoi(argv[2]), par = atoi(argv[3]), algo = atoi(argv[4]);
     const double domain = argc > 5 ? atof(argv[5]) : 1000.0;
+    const int64_t ckpt_at = argc > 6 ? atoll(argv[6]) : -1;
+    const int group = argc > 7 ? atoi(argv[7]) : 8;
     const int P = 2 * par;   /* FlinkSkyline.java:76 */
     FILE *f = fopen(argv[1], "rb");
     if (!f) { perror("open"); return 2; }
@@ -130,18 +173,67 @@ int main(int argc, char **argv) {
         ks[k].vals = (double *)malloc((size_t)BUFFER_SIZE * D * 8);
         CHECK(sky_part_open(ctx, k, &ks[k].part));
     }
-    /* processElement1: buffer, flush through processBuffer at BUFFER_SIZE */
+    /* processElement1: buffer; a full buffer waits for its group, then processBuffer */
+    int waiting = 0;
     for (int64_t i = 0; i < n; i++) {
+        if (i == ckpt_at) {
+            /* snapshotState: the waiting and partial buffers flushed, every key's skyline saved */
+            drain_full(ks, kmax, D);
+            waiting = 0;
+            int64_t *sn = (int64_t *)calloc((size_t)kmax, 8);
+            int64_t **sid = (int64_t **)calloc((size_t)kmax, sizeof(int64_t *));
+            double **sval = (double **)calloc((size_t)kmax, sizeof(double *));
+            for (int k = 0; k < kmax; k++) {
+                keyed_state *s = &ks[k];
+                if (s->n) CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
+                s->n = 0;
+                int64_t m = 0;
+                int rc = sky_part_snapshot(s->part, NULL, NULL, 0, &m);
+                if (rc != SKY_OK && rc != SKY_E_CAPACITY) die("sky_part_snapshot (size)", rc);
+                sid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+                sval[k] = (double *)malloc((size_t)(m > 0 ? m : 1) * D * 8);
+                CHECK(sky_part_snapshot(s->part, sid[k], sval[k], m, &m));
+                sn[k] = m;
+            }
+            /* the failure: every handle gone */
+            for (int k = 0; k < kmax; k++) CHECK(sky_part_close(ks[k].part));
+            CHECK(sky_ctx_destroy(ctx));
+            /* restore: a fresh context, each key's skyline re-inserted (SKY(empty u S) = S) */
+            CHECK(sky_ctx_create(&dev, 1, D, P, algo, domain, &ctx));
+            for (int k = 0; k < kmax; k++) {
+                CHECK(sky_part_open(ctx, k, &ks[k].part));
+                if (sn[k]) CHECK(sky_part_insert(ks[k].part, sid[k], sval[k], sn[k]));
+                free(sid[k]);
+                free(sval[k]);
+            }
+            free(sn);
+            free(sid);
+            free(sval);
+        }
         const int k = keys[i];
         if (k < 0) continue;   /* removed by the (optional) grid dominance filter */
         keyed_state *s = &ks[k];
         s->ids[s->n] = ids[i];
         memcpy(s->vals + s->n * D, vals + i * D, (size_t)D * 8);
         if (++s->n == BUFFER_SIZE) {
-            CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
+            if (group <= 1) {
+                CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
+            } else {
+                if (s->nfull == 64) drain_full(ks, kmax, D), waiting = 0;
+                s->fids[s->nfull] = (int64_t *)malloc(BUFFER_SIZE * 8);
+                s->fvals[s->nfull] = (double *)malloc((size_t)BUFFER_SIZE * D * 8);
+                memcpy(s->fids[s->nfull], s->ids, BUFFER_SIZE * 8);
+                memcpy(s->fvals[s->nfull], s->vals, (size_t)BUFFER_SIZE * D * 8);
+                s->nfull++;
+                if (++waiting >= group) {
+                    drain_full(ks, kmax, D);
+                    waiting = 0;
+                }
+            }
             s->n = 0;
         }
     }
+    drain_full(ks, kmax, D);
     /* trigger "1,N" after the last tuple, broadcast to keys 0..P-1 (:145-157) */
     const int64_t dispatch = now_ms();
     int32_t *part_ids = (int32_t *)malloc((size_t)P * 4);

@@ -96,3 +96,92 @@ def test_part_state_nan_batch_rejected(gpu_engine_factory, oracle):
     np.testing.assert_array_equal(got_ids, ids[keep][exp])
     part.close()
     eng.close()
+
+
+def test_part_async_inserts_without_sync(gpu_engine_factory, oracle):
+    """Hundreds of inserts issued back to back with no synchronisation in between (bounds from
+    the host mirror, capacities grown on the stream, in-insert compaction of a kill-heavy
+    stream): the one snapshot at the end equals the oracle."""
+    from skyline.operators import _LocalPart
+    rng = np.random.default_rng(31)
+    n, D = 60000, 3
+    base = np.repeat(np.arange(n // 500)[::-1], 500)[:, None] * 25.0
+    vals = base + rng.integers(0, 40, size=(n, D)).astype(np.float64)
+    vals[::7] = vals[::7].round(-1)
+    ids = np.arange(n, dtype=np.int64) * 5 + 1
+    eng = gpu_engine_factory(D, 8)
+    part = _LocalPart(eng, 3)
+    s = 0
+    while s < n:
+        f = int(min(n - s, rng.integers(1, 700)))
+        part.insert(ids[s:s + f], vals[s:s + f])
+        s += f
+    got_ids, got_vals = part.snapshot()
+    exp, _, _, _ = oracle.query_sfs("dim", vals, 1)
+    np.testing.assert_array_equal(got_ids, ids[exp])
+    np.testing.assert_array_equal(got_vals, vals[exp])
+    part.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("dist,D", [(2, 8), (3, 4), (4, 6)])
+def test_parts_insert_batched_keys_vs_oracle(dist, D, gpu_engine_factory, oracle):
+    """sky_parts_insert: the full buffers of several keys per call (each key at most once per
+    call), no synchronisation until the trigger; every key's snapshot equals the oracle's local
+    skyline of its tuples, and equals one sky_part_insert per buffer."""
+    from skyline.operators import _LocalPart
+    n, P, buf = 120000, 8, 5000
+    vals = oracle.synth(dist, D, n, seed=90 + D)
+    ids = np.arange(n, dtype=np.int64)
+    eng = gpu_engine_factory(D, P)
+    keys = eng.partition_keys(vals)
+    rng = np.random.default_rng(D)
+    per = {k: np.flatnonzero(keys == k) for k in range(P)}
+    a = {k: _LocalPart(eng, k) for k in range(P)}
+    b = {k: _LocalPart(eng, k) for k in range(P)}
+    pos = {k: 0 for k in range(P)}
+    while any(pos[k] < len(per[k]) for k in range(P)):
+        call = [k for k in range(P) if pos[k] < len(per[k]) and rng.random() < 0.6]
+        batches = []
+        for k in call:
+            f = int(min(len(per[k]) - pos[k], rng.integers(1, 2 * buf)))
+            sel = per[k][pos[k]:pos[k] + f]
+            batches.append((ids[sel], vals[sel]))
+            pos[k] += f
+            b[k].insert(ids[sel], vals[sel])
+        _LocalPart.insert_many([a[k] for k in call], batches)
+    for k in range(P):
+        got_ids, got_vals = a[k].snapshot()
+        ref_ids, _ = b[k].snapshot()
+        exp, _, _, _ = oracle.query_sfs("dim", vals[per[k]], 1)
+        np.testing.assert_array_equal(got_ids, ids[per[k]][exp])
+        np.testing.assert_array_equal(got_vals, vals[per[k]][exp])
+        np.testing.assert_array_equal(ref_ids, got_ids)
+    for x in list(a.values()) + list(b.values()):
+        x.close()
+    eng.close()
+
+
+def test_parts_insert_nan_rejects_the_whole_call(gpu_engine_factory, oracle):
+    from skyline.operators import _LocalPart
+    D = 4
+    vals = oracle.synth(3, D, 20000, seed=2)
+    ids = np.arange(len(vals), dtype=np.int64)
+    eng = gpu_engine_factory(D, 8)
+    p0, p1 = _LocalPart(eng, 0), _LocalPart(eng, 1)
+    _LocalPart.insert_many([p0, p1], [(ids[:5000], vals[:5000]), (ids[5000:10000], vals[5000:10000])])
+    before = [p0.snapshot(), p1.snapshot()]
+    bad = vals[15000:20000].copy()
+    bad[4999, 0] = np.nan
+    with pytest.raises(SkylineError) as e:
+        _LocalPart.insert_many([p0, p1], [(ids[10000:15000], vals[10000:15000]), (ids[15000:], bad)])
+    assert e.value.code == SKY_E_NAN
+    after = [p0.snapshot(), p1.snapshot()]
+    for x, y in zip(before, after):
+        np.testing.assert_array_equal(x[0], y[0])
+        np.testing.assert_array_equal(x[1], y[1])
+    with pytest.raises(SkylineError):                     # one part twice in one call
+        _LocalPart.insert_many([p0, p0], [(ids[:10], vals[:10]), (ids[10:20], vals[10:20])])
+    p0.close()
+    p1.close()
+    eng.close()

@@ -3,7 +3,9 @@ build/operator_replay) replays the reference operators' call sequence -- device 
 getKey, per-key 5000-tuple buffers flushed through sky_part_insert, a trigger after the last
 tuple answered by sky_part_snapshot per key, sky_global_merge + sky_global_stats, the JSON of
 FlinkSkyline.java:631-648 -- exactly as the JNI shim (jni/skyline_hip_jni.c) drives the
-library from the Java operators.  Its output must equal the golden results."""
+library from the Java operators (full buffers grouped into sky_parts_insert calls, as
+HipSkylineOperators does).  Its output must equal the golden results, also with single-buffer
+inserts, and across a checkpoint -> close -> reopen -> restore-by-insert in mid-stream."""
 import json
 import os
 import subprocess
@@ -36,20 +38,24 @@ def test_c_caller_replays_operator_sequence(path, tmp_path):
     with open(csv, "w") as f:   # the producers' payload, python/unified_producer.py:174
         for i, row in zip(ids, vals):
             f.write(f"{int(i)}," + ",".join(str(int(x)) for x in row) + "\n")
+    n = len(ids)
+    # (domain, checkpoint position or -1, buffers per sky_parts_insert group)
+    modes = [[], ["1000.0", str(n // 2), "8"], ["1000.0", "-1", "1"], ["1000.0", str(n // 3), "3"]]
     for algo in ("dim", "grid", "angle"):
         for P in (4, 8, 16):
-            r = subprocess.run([BIN, str(csv), str(D), str(P // 2), str(ALGO[algo])], capture_output=True,
-                               text=True, timeout=120)
-            assert r.returncode == 0, r.stderr
-            lines = r.stdout.strip().split("\n")
-            js = json.loads(lines[0])
-            got_ids = np.array([int(x) for x in lines[1].split()[1:]], np.int64)
-            lsz = np.array([int(x) for x in lines[2].split()[1:]], np.int64)
-            surv = np.array([int(x) for x in lines[3].split()[1:]], np.int64)
-            np.testing.assert_array_equal(got_ids, np.sort(ids[g[f"gsky_{algo}_{P}"]]))
-            np.testing.assert_array_equal(lsz, g[f"lsz_{algo}_{P}"])
-            np.testing.assert_array_equal(surv, g[f"surv_{algo}_{P}"])
-            assert js["skyline_size"] == len(got_ids) and js["record_count"] == len(ids)
-            opt = sum(surv[i] / lsz[i] for i in range(P) if lsz[i] > 0) / P
-            assert lines[0].split('"optimality": ')[1].split(",")[0] == java_format_4f(opt)
-            assert "query_latency_ms" in js
+            for extra in modes:
+                r = subprocess.run([BIN, str(csv), str(D), str(P // 2), str(ALGO[algo])] + extra,
+                                   capture_output=True, text=True, timeout=120)
+                assert r.returncode == 0, r.stderr
+                lines = r.stdout.strip().split("\n")
+                js = json.loads(lines[0])
+                got_ids = np.array([int(x) for x in lines[1].split()[1:]], np.int64)
+                lsz = np.array([int(x) for x in lines[2].split()[1:]], np.int64)
+                surv = np.array([int(x) for x in lines[3].split()[1:]], np.int64)
+                np.testing.assert_array_equal(got_ids, np.sort(ids[g[f"gsky_{algo}_{P}"]]))
+                np.testing.assert_array_equal(lsz, g[f"lsz_{algo}_{P}"])
+                np.testing.assert_array_equal(surv, g[f"surv_{algo}_{P}"])
+                assert js["skyline_size"] == len(got_ids) and js["record_count"] == len(ids)
+                opt = sum(surv[i] / lsz[i] for i in range(P) if lsz[i] > 0) / P
+                assert lines[0].split('"optimality": ')[1].split(",")[0] == java_format_4f(opt)
+                assert "query_latency_ms" in js

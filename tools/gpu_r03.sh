@@ -19,6 +19,11 @@ if [[ $STEPS == *dist* ]]; then
       ${DIST_EXTRA} > $OUT/pytest_dist_$TAG.log 2>&1 || { tail -60 $OUT/pytest_dist_$TAG.log; exit 1; }
   tail -4 $OUT/pytest_dist_$TAG.log
 fi
+if [[ $STEPS == *parts* ]]; then
+  timeout -k 10 600 $PYT tests/test_gpu_part.py tests/test_gpu_operators.py tests/test_gpu_replay.py \
+      > $OUT/pytest_parts_$TAG.log 2>&1 || { tail -60 $OUT/pytest_parts_$TAG.log; exit 1; }
+  tail -4 $OUT/pytest_parts_$TAG.log
+fi
 if [[ $STEPS == *tests* ]]; then
   timeout -k 10 1000 $PYT tests -m gpu ${TEST_EXTRA} > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
   tail -4 $OUT/pytest_gpu_$TAG.log
@@ -38,4 +43,14 @@ if [[ $STEPS == *union* ]]; then
 fi
 if [[ $STEPS == *mbrpmc* ]]; then
   TAG=$TAG NS="${MBR_NS:-2000000 10000000}" bash tools/gpu_mbr_pmc.sh
+fi
+if [[ $STEPS == *c4ab* ]]; then
+  # C4 alone, the round's default path and the A/B knobs in KNOBS (e.g. "SKY_PLANES=0")
+  C4ARGS="--steps 10 --warmup 3 --no-cpu-baseline --no-dominance --no-csv --no-stream --no-sort --no-configs --no-e2e --no-operator"
+  timeout -k 10 200 python -u bench.py $C4ARGS > $OUT/c4_$TAG.json 2> $OUT/c4_$TAG.err || { tail -30 $OUT/c4_$TAG.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/c4_$TAG.json'));print('default', d['ms_per_step'], d['p50_query_latency_ms'], d['roofline']['avg_launch_ms'])"
+  for K in ${KNOBS}; do
+    env $K timeout -k 10 200 python -u bench.py $C4ARGS > $OUT/c4_${TAG}_$K.json 2> $OUT/c4_${TAG}_$K.err || { tail -30 $OUT/c4_${TAG}_$K.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/c4_${TAG}_$K.json'));print('$K', d['ms_per_step'], d['p50_query_latency_ms'], d['roofline']['avg_launch_ms'])"
+  done
 fi
