@@ -193,6 +193,17 @@ static uint32_t mbr_min() {
     const char *e = getenv("SKY_MBR_MIN");
     return e ? (uint32_t)atoi(e) : 16384u;
 }
+// Up to 32768 slots the brute pair pass (one 64 x 64 block pair per workgroup, no sort or
+// dedup) beats the sorted bounding-box route, whose 64-row y tiles leave a small rep set at a
+// few hundred waves on 1024 SIMDs (C5 sliding window: 21-25k reps took 0.6-0.85 ms there).
+uint32_t brute_max() {
+    static const uint32_t v = [] {
+        const char *e = getenv("SKY_BRUTE_MAX");
+        const long x = e ? atol(e) : 32768;
+        return (uint32_t)std::min<long>(std::max<long>(x, 64), 1 << 20);
+    }();
+    return v;
+}
 static bool brute_disabled() {
     const char *e = getenv("SKY_BRUTE");
     return e && atoi(e) == 0;
@@ -615,12 +626,12 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_gmin.ensure(mbr_groups(mr) * NW * 4));
     SKY_TRY(p.mbr_gpr.ensure(mbr_groups(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
-    SKY_TRY(p.mbr_pairs.ensure(16));
+    SKY_TRY(p.mbr_pairs.ensure(64));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
     FillSet fill;
     fill.add(p.mbr_mm.p, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
-    fill.add(p.mbr_pairs.p, 16, 0);
+    fill.add(p.mbr_pairs.p, 64, 0);
     fill.add(p.mbr_domf.p, (size_t)mr * 4, 0);
     HIP_TRY(fill.launch(st));
     MbrArgs a;
@@ -634,8 +645,13 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     {
         const char *e = getenv("SKY_MBR_DBG");
         a.dbg = e ? atoi(e) : 0;
-        const char *sp = getenv("SKY_MBR_SPLIT");   // x-tile ranges per y tile (A/B knob)
-        a.nsplit = sp ? std::max(1, atoi(sp)) : 1;
+        // x-tile ranges per y tile: a small rep set has few 64-row y tiles (20k reps: ~330 waves
+        // on 1024 SIMDs), so its groups are split over more waves (domf is OR-ed atomically);
+        // SKY_MBR_SPLIT overrides (A/B knob)
+        const char *sp = getenv("SKY_MBR_SPLIT");
+        const uint32_t nt = (uint32_t)mbr_tiles(mr), ng = (uint32_t)mbr_groups(mr);
+        const uint32_t auto_split = std::min<uint32_t>(ng, std::max<uint32_t>(1u, (4096u + nt - 1) / nt));
+        a.nsplit = sp ? std::max(1, atoi(sp)) : (int)auto_split;
     }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
@@ -699,7 +715,7 @@ static int dist_finish_run(Ctx &c, Pipe &p, PhaseTimer *tm, bool brute, uint32_t
         pc.cap = (uint32_t)pr->cap;
         pc.rounds = p.plan.rounds;
         for (int r = 0; r <= p.plan.rounds && r < 4; r++) pc.bound[r] = p.plan.bound[r];
-        pc.brute_max = kBruteMax;
+        pc.brute_max = brute_max();
         pc.k_u16 = pr->k_u16 ? 1 : 0;
         pc.k_f32 = pr->k_f32 ? 1 : 0;
     }
@@ -857,7 +873,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             bool ok = tot[10] <= p.plan.bound[0];
             for (int r = 0; r < p.plan.rounds; r++) ok &= tot[11 + r] <= p.plan.bound[r + 1];
             const uint32_t fin = p.plan.rounds ? tot[10 + p.plan.rounds] : tot[10];
-            ok &= fin <= kBruteMax;
+            ok &= fin <= brute_max();
             const bool f64 = (flags2 & kFlagNotF32) != 0, ints = !f64 && (flags2 & kFlagNotU16) == 0;
             ok &= pr->k_u16 ? ints : (pr->k_f32 ? !f64 : true);
             if (!ok) return kPlanMiss;
@@ -877,15 +893,18 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         p.mg = in.global && !in.single ? alive_sum : 0;
     } else {
         uint32_t flags3 = 0;
-        unsigned long long mbr_pairs[2] = {0, 0};
+        unsigned long long mbr_pairs[5] = {0, 0, 0, 0, 0};
         p.h_dup.assign(KM, 0u);
         SKY_TRY(sync_read(p, st, {{p.totals.as<uint32_t>() + 3, 4}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, have_seg ? (size_t)p.Kp * 4 : 0}, {p.flags.p, 4},
-                                  {p.mbr_pairs.p, p.used_mbr ? 16u : 0u}, {p.dup_cnt.p, (size_t)KM * 4}},
+                                  {p.mbr_pairs.p, p.used_mbr ? 40u : 0u}, {p.dup_cnt.p, (size_t)KM * 4}},
                           {&nout, sk2.data(), p.h_seg_s.data(), &flags3, mbr_pairs, p.h_dup.data()}));
         if (p.used_mbr) {
             p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
             p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
+            if (mbr_pairs[3])                             // SKY_MBR_DBG bit 4: the scan's funnel
+                fprintf(stderr, "[mbr] reps %u groups %llu box %llu listed %llu tested %llu pairs %llu\n", p.mr,
+                        mbr_pairs[2], mbr_pairs[3], mbr_pairs[4], mbr_pairs[1], mbr_pairs[0]);
             uint32_t alive_sum = 0;
             for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
             p.mg = in.global && !in.single ? alive_sum : 0;
@@ -1274,12 +1293,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         plan_live[plan_rounds++] = live_n;
         if (debug_level() >= 3)
             fprintf(stderr, "[sky] prefilter round %d: %u -> %u slots (M2=%d)\n", round, mt0, live_n, M2);
-        if (live_n <= kBruteMax || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
+        if (live_n <= brute_max() || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
     }
     const uint32_t mt = p.mt;
     // small candidate sets (typical after the prefilter): both skyline levels by one
     // brute-force launch instead of the round-based SFS (SKY_BRUTE=0: A/B knob)
-    const bool brute = (in.fate || in.dist) && mt > 0 && mt <= kBruteMax && !brute_disabled() && c.warm_mode == 0;
+    const bool brute = (in.fate || in.dist) && mt > 0 && mt <= brute_max() && !brute_disabled() && c.warm_mode == 0;
     // the route for the next queries' planned replay: this one's, if it was the small-set one
     p.plan.valid = brute && plan_rounds <= Pipe::Plan::kMaxRounds;
     if (p.plan.valid) {

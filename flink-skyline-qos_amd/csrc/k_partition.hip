@@ -1299,6 +1299,15 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     // (tuples past n are never selected: masked below)
     uint16_t st[kItems];
     int64_t idv[kItems];
+    // the id loads first: the status words are widened / packed as soon as they arrive, and
+    // vmcnt waits in issue order, so ids issued after them would wait behind that
+    if (a.ids) {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k * kThreads);
+    }
     // status planes: the (item, wave) words are wave-uniform (scalar loads); a status word is
     // loaded only where the E bit says the filter stored one, the B bit stands for the
     // designated duplicate group's status
@@ -1313,21 +1322,20 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
             pe[k] = w.y;
         }
         const uint16_t sg = (uint16_t)(a.dom_kj >= 0 ? ((a.dom_kj / a.M) << 8) | (1 + a.dom_kj % a.M) : 0);
+        // a wave's 64 status words are loaded only if the filter stored one of them (pe is
+        // wave-uniform: a scalar branch, and the load itself unconditional per lane — a per-lane
+        // conditional load made the compiler wait on each one)
+        uint16_t raw[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; k++) raw[k] = pe[k] ? a.status[min(i0 + k * kThreads, nl)] : (uint16_t)0;
 #pragma unroll
         for (int k = 0; k < kItems; k++) {
             const bool e = (pe[k] >> lane) & 1ull;
-            st[k] = e ? a.status[min(i0 + k * kThreads, nl)] : (((pb[k] >> lane) & 1ull) ? sg : (uint16_t)0);
+            st[k] = e ? raw[k] : (((pb[k] >> lane) & 1ull) ? sg : (uint16_t)0);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < kItems; k++) st[k] = a.status[min(i0 + k * kThreads, nl)];
-    }
-    if (a.ids) {
-#pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];
-    } else {
-#pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k * kThreads);
     }
     for (int q = threadIdx.x; q < a.KM; q += kThreads) s_pf[q] = a.pruner_fate[q];
     __syncthreads();                                   // s_pf ready

@@ -241,7 +241,8 @@ void launch_scatter_alive(const uint32_t *gval, const uint8_t *galive, uint32_t 
 void launch_stat_reduce(const unsigned long long *lsz, const unsigned long long *surv, int K, unsigned long long *out,
                         hipStream_t st);
 // both skyline levels of a small rep set in one launch (alive_l, alive_g, segalive counts)
-constexpr uint32_t kBruteMax = 16384;
+// the largest slot count the brute pass takes (SKY_BRUTE_MAX, default 32768; engine.hip)
+uint32_t brute_max();
 // over f64 candidate slots (rows [mr][pad(D)], sort keys): domf / segalive / segn zeroed by
 // the caller; writes alive_l / alive_g / slot_rep (identity) per slot
 // f32: compare in f32 (every candidate value exactly an f32), else f64; u16: every candidate

@@ -13,6 +13,22 @@ TAG=${TAG:-r03}
 STEPS=${STEPS:-dist}
 export PYTHONUNBUFFERED=1
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+if [[ $STEPS == *funnel* ]]; then
+  # the bounding-box scan's funnel (groups / tiles passing / listed / tested / pair tests)
+  for V in "SKY_MBR_ORDER=hilbert" "SKY_MBR_ORDER=morton" "SKY_MBR_PIPE=0" "SKY_MBR_ORDER=morton SKY_MBR_PIPE=0"; do
+    T=$(echo $V | tr ' =' '__')
+    env $V SKY_MBR_DBG=4 timeout -k 10 200 python -u tools/dom_bench.py ${MBR_N:-2000000} 3 > $OUT/funnel_${TAG}_$T.log 2>&1 || { tail -30 $OUT/funnel_${TAG}_$T.log; exit 1; }
+    echo "$V"; grep -v "^\[mbr\]" $OUT/funnel_${TAG}_$T.log; grep "^\[mbr\]" $OUT/funnel_${TAG}_$T.log | tail -1
+  done
+fi
+if [[ $STEPS == *c5probe* ]]; then
+  for K in default ${C5KNOBS}; do
+    for W in 0 10000000; do
+      env ${K/default/SKY_X=0} SKY_MBR_DBG=4 timeout -k 10 200 python -u tools/c5_probe.py $W --phases > $OUT/c5probe_${TAG}_${K}_$W.log 2>&1 || { tail -30 $OUT/c5probe_${TAG}_${K}_$W.log; exit 1; }
+      echo "$K W=$W"; grep pass $OUT/c5probe_${TAG}_${K}_$W.log
+    done
+  done
+fi
 if [[ $STEPS == *dist* ]]; then
   timeout -k 10 900 $PYT tests/test_gpu_dist_step.py tests/test_gpu_dist.py \
       "tests/test_gpu_operators.py::test_multi_rank_decomposition" "tests/test_gpu_configs.py::test_c4_8way_decomposition" \
