@@ -150,7 +150,9 @@ int sky_global_stats_set(sky_ctx *ctx, int32_t k, const int64_t *local_sizes, co
 
 /* ---- fused whole-stream query --------------------------------------------- */
 /* keyBy -> per-key local skylines -> global merge, the trigger arriving after
- * the last tuple.  ids_out/origin_out: the global skyline in stream order. */
+ * the last tuple.  ids_out/origin_out: the global skyline in stream order.
+ * On any error (e.g. SKY_E_NAN found at the final verification of a planned query) the
+ * output buffers hold unspecified data; only *n_out of a SKY_E_CAPACITY return is defined. */
 int sky_query(sky_ctx *ctx, const int64_t *ids, const double *values, int64_t n,
               int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
 int sky_query_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n,
