@@ -813,6 +813,26 @@ int sky_stream_append(sky_stream *s, const int64_t *ids, const double *values, i
 int sky_stream_append_dev(sky_stream *s, const int64_t *d_ids, const double *d_values, int64_t n) {
     return stream_append(s, d_ids, d_values, n, hipMemcpyDeviceToDevice);
 }
+int sky_stream_reserve(sky_stream *s, int64_t tuples) {
+    GUARD_BEGIN
+    ARG_CHECK(s, "null stream");
+    ARG_CHECK(tuples >= 0 && tuples < (int64_t)0x3fffffffLL, "tuples out of range");
+    sky_ctx *c = s->ctx;
+    SKY_TRY(bind(c));
+    if (tuples > s->n) SKY_TRY(stream_reserve(s, tuples - s->n));
+    const size_t m = (size_t)std::max<int64_t>(tuples, 1);
+    // the landmark compaction's target buffer, the host-view query's output, the run's buffers
+    SKY_TRY(s->ids[1 - s->cur].ensure((size_t)std::max<int64_t>(s->cap, 1) * 8));
+    SKY_TRY(s->rows[1 - s->cur].ensure((size_t)std::max<int64_t>(s->cap, 1) * c->D * 8));
+    SKY_TRY(s->out_ids.ensure(m * 8));
+    SKY_TRY(s->out_org.ensure(m * 4));
+    SKY_TRY(s->nanflag.ensure(64));
+    if (!s->nan_host) HIP_TRY(hipHostMalloc(&s->nan_host, 64, hipHostMallocDefault));
+    SKY_TRY(pipe_reserve(*c, c->main, (uint32_t)m));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
 int sky_stream_size(sky_stream *s, int64_t *resident, int64_t *appended) {
     ARG_CHECK(s, "null stream");
     if (resident) *resident = s->n;

@@ -1056,6 +1056,24 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     return r2;
 }
 
+// every buffer of a whole-stream run whose size follows the tuple count, sized for n tuples
+// (sky_stream_reserve: a continuous query's resident set grows trigger by trigger, and each
+// regrowth's hipFree synchronises the device inside that trigger's latency)
+int pipe_reserve(Ctx &c, Pipe &p, uint32_t n) {
+    const uint32_t tiles = (n + kTile - 1) / kTile;
+    const int Kp = c.Kq();
+    const int M = std::max(1, std::min(8, 49152 / (Kp * c.D * 8)));
+    SKY_TRY(p.status.ensure((size_t)tiles * kTile * 2));
+    SKY_TRY(p.planes.ensure((size_t)tiles * 32 * 16));
+    if (Kp * M <= kHistMaxKM) SKY_TRY(p.tile_hist.ensure((size_t)tiles * Kp * M * 4));
+    SKY_TRY(p.tile_cand.ensure((size_t)tiles * 4));
+    SKY_TRY(p.defer.ensure((size_t)n * 4));
+    SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
+    SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
+    SKY_TRY(p.scratch.ensure(scan_scratch_words(tiles + 1) * 4 + 64));
+    return SKY_OK;
+}
+
 int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     hipStream_t st = c.st;
     const int D = c.D;

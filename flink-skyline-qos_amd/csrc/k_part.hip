@@ -31,39 +31,192 @@ constexpr uint32_t kPartChunk = 256;    // x rows per workgroup (grid.y): many s
 // the new counts into host-mapped memory (seqlock) so that the host tightens its bounds
 // without synchronising.
 
+// ---- batch pruners (k_parts_prune) --------------------------------------------------------
+// Before any pair test, each part's batch is reduced to its UNDECIDED tuples U: kPartPruners
+// batch tuples p_c minimise positive-weight linear criteria (a dominator never has a larger
+// criterion value: rounding is monotone), and every batch tuple is classified against them in
+// order c = 0, 1, ...: dominated by p_c (dropped: dom_b = 1), equal to p_c (class c: shares the
+// fate of p_c, the class's first index is its equal-earlier tuple), or neither (undecided).  U =
+// the undecided tuples plus each non-empty class's pruner.  Then
+//   - a dominator of y in U is a pruned tuple t (its pruner, or a pruner before it, dominates y
+//     and reaches U as a class pruner), a class member (its pruner is in U, same vector) or in U;
+//   - an equal batch tuple of an undecided y is undecided too (a pruner dominating or equal to
+//     it would dominate or equal y);
+//   - a state rep dominated by a batch tuple is dominated by a member of U (same argument);
+// so B x B and the state tests run over U only: O(|U| (|U| + R)) pair tests instead of
+// O(|B| (|B| + R)).  On the reference streams a 5000-tuple buffer keeps a few hundred tuples.
+template <int D>
+__device__ __forceinline__ double part_crit(const double (&v)[D], int c) {
+    // c = 0: the sum; c >= 1: the sum plus 3 x dimension (c - 1) * D / (kPartPruners - 1)
+    double s = 0.0;
+    const int dk = c == 0 ? -1 : ((c - 1) * D) / (kPartPruners - 1);
+#pragma unroll
+    for (int q = 0; q < D; q++) s += q == dk ? 4.0 * v[q] : v[q];
+    return s;
+}
+
+template <int D>
+__global__ __launch_bounds__(1024) void k_parts_prune(const PartDesc *__restrict__ descs) {
+    __shared__ double s_bv[16][kPartPruners];
+    __shared__ uint32_t s_bi[16][kPartPruners];
+    __shared__ double s_pr[kPartPruners][D];
+    __shared__ uint32_t s_pi[kPartPruners], s_fe[kPartPruners], s_u;
+    const PartDesc &d = descs[blockIdx.x];
+    const uint32_t nb = d.nb;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double bv[kPartPruners];
+    uint32_t bi[kPartPruners];
+#pragma unroll
+    for (int c = 0; c < kPartPruners; c++) {
+        bv[c] = __longlong_as_double(0x7ff0000000000000ll);
+        bi[c] = 0xffffffffu;
+    }
+    // per thread: increasing b, so the first minimum is kept (ties -> the smallest index)
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        double v[D];
+#pragma unroll
+        for (int q = 0; q < D; q++) v[q] = d.bvals[(size_t)b * D + q];
+#pragma unroll
+        for (int c = 0; c < kPartPruners; c++) {
+            const double s = part_crit<D>(v, c);
+            if (s < bv[c] || bi[c] == 0xffffffffu) {
+                bv[c] = s;
+                bi[c] = b;
+            }
+        }
+    }
+    // (value, index) minimum over the block: waves, then the 16 wave results
+#pragma unroll
+    for (int c = 0; c < kPartPruners; c++) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double ov = __shfl_xor(bv[c], o, 64);
+            const uint32_t oi = (uint32_t)__shfl_xor((int)bi[c], o, 64);
+            if (oi != 0xffffffffu && (bi[c] == 0xffffffffu || ov < bv[c] || (ov == bv[c] && oi < bi[c]))) {
+                bv[c] = ov;
+                bi[c] = oi;
+            }
+        }
+        if (lane == 0) {
+            s_bv[wave][c] = bv[c];
+            s_bi[wave][c] = bi[c];
+        }
+    }
+    if (threadIdx.x == 0) s_u = 0;
+    __syncthreads();
+    if (threadIdx.x < kPartPruners) {
+        const int c = threadIdx.x;
+        double v = s_bv[0][c];
+        uint32_t i = s_bi[0][c];
+        for (int w = 1; w < 16; w++) {
+            const double ov = s_bv[w][c];
+            const uint32_t oi = s_bi[w][c];
+            if (oi != 0xffffffffu && (i == 0xffffffffu || ov < v || (ov == v && oi < i))) {
+                v = ov;
+                i = oi;
+            }
+        }
+        s_pi[c] = i;
+        s_fe[c] = 0xffffffffu;
+    }
+    __syncthreads();
+    if (threadIdx.x < kPartPruners * D) {
+        const int c = threadIdx.x / D, q = threadIdx.x % D;
+        s_pr[c][q] = s_pi[c] != 0xffffffffu ? d.bvals[(size_t)s_pi[c] * D + q] : 0.0;
+    }
+    __syncthreads();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
+        const uint32_t b = c0 + threadIdx.x;
+        const bool valid = b < nb;
+        uint32_t cls = 0xffffffffu;
+        bool dom = false;
+        if (valid) {
+            double v[D];
+#pragma unroll
+            for (int q = 0; q < D; q++) v[q] = d.bvals[(size_t)b * D + q];
+            for (int c = 0; c < kPartPruners; c++) {
+                if (s_pi[c] == 0xffffffffu) break;
+                bool le = true, ge = true;
+#pragma unroll
+                for (int q = 0; q < D; q++) {
+                    le &= s_pr[c][q] <= v[q];
+                    ge &= s_pr[c][q] >= v[q];
+                }
+                if (le && !ge) {
+                    dom = true;
+                    break;
+                }
+                if (le) {
+                    cls = (uint32_t)c;
+                    break;
+                }
+            }
+            if (dom) d.dom_b[b] = 1u;
+            d.eqp[b] = cls;
+            if (cls != 0xffffffffu) atomicMin(&s_fe[cls], b);
+        }
+        const bool inU = valid && !dom && (cls == 0xffffffffu || b == s_pi[cls]);
+        const uint64_t um = __ballot(inU);
+        uint32_t base = 0;
+        if (lane == 0 && um) base = atomicAdd(&s_u, (uint32_t)__popcll(um));
+        base = (uint32_t)__shfl((int)base, 0, 64);
+        if (inU) d.uidx[base + (uint32_t)__popcll(um & lt)] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) d.meta[0] = s_u;
+    if (threadIdx.x < kPartPruners) {
+        d.meta[1 + threadIdx.x] = s_pi[threadIdx.x];
+        d.meta[1 + kPartPruners + threadIdx.x] = s_fe[threadIdx.x];
+    }
+}
+
 // dominance as ServiceTuple.dominates (ServiceTuple.java:67-77): <= everywhere, < somewhere
-// mode 0: batch y vs batch x (dom_b, eq_b: first EARLIER equal batch tuple)
-// mode 1: batch y vs alive state reps x (dom_b, eq_s: first equal rep)
-// mode 2: state reps y vs batch x (dom_s)
+// mode 0: undecided y vs undecided x (dom_b, eq_b: first EARLIER equal batch tuple)
+// mode 1: undecided y vs alive state reps x (dom_b, eq_s: first equal rep)
+// mode 2: state reps y vs undecided x (dom_s)
+// Launch sizes come from the batch size (a bound of |U|, which lives on the device): work items
+// past |U| return at once.
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__restrict__ descs,
                                                           const PartItem *__restrict__ items) {
     __shared__ double s_x[kPartX * D];
+    __shared__ uint32_t s_xi[kPartX];
     const PartItem it = items[blockIdx.x];
     const PartDesc &d = descs[it.part];
     const uint32_t R0 = d.dcnt[0];
+    const uint32_t nu = min(d.meta[0], d.nb);
     const int mode = (int)it.mode;
-    const double *y = mode == 2 ? d.rrows : d.bvals;
-    const uint32_t ny = mode == 2 ? min(R0, d.rb) : d.nb;
-    const double *x = mode == 1 ? d.rrows : d.bvals;
-    const uint32_t nx = mode == 1 ? min(R0, d.rb) : d.nb;
-    const uint32_t j = it.y0 + threadIdx.x;
-    const bool valid = j < ny;
+    const uint32_t ny = mode == 2 ? min(R0, d.rb) : nu;
+    const uint32_t nx = mode == 1 ? min(R0, d.rb) : nu;
     if (it.y0 >= ny || it.x0 >= nx) return;
+    const uint32_t yi = it.y0 + threadIdx.x;
+    const bool valid = yi < ny;
+    // y: its row and its index (batch index for modes 0 / 1, rep index for mode 2)
+    const uint32_t j = valid ? (mode == 2 ? yi : d.uidx[yi]) : 0u;
+    const double *ysrc = mode == 2 ? d.rrows : d.bvals;
     double v[D];
 #pragma unroll
-    for (int q = 0; q < D; q++) v[q] = valid ? y[(size_t)j * D + q] : 0.0;
+    for (int q = 0; q < D; q++) v[q] = valid ? ysrc[(size_t)j * D + q] : 0.0;
     const uint32_t c1 = min(nx, it.x0 + kPartChunk);
     bool dm = false;
     uint32_t emin = 0xffffffffu;
     for (uint32_t t0 = it.x0; t0 < c1; t0 += kPartX) {
         const uint32_t cn = min((uint32_t)kPartX, c1 - t0);
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < cn * D; q += kThreads) s_x[q] = x[(size_t)t0 * D + q];
+        if (mode == 1) {
+            for (uint32_t q = threadIdx.x; q < cn * D; q += kThreads) s_x[q] = d.rrows[(size_t)t0 * D + q];
+            if (threadIdx.x < cn) s_xi[threadIdx.x] = d.ralive[t0 + threadIdx.x] ? t0 + threadIdx.x : 0xffffffffu;
+        } else {
+            if (threadIdx.x < cn) s_xi[threadIdx.x] = d.uidx[t0 + threadIdx.x];
+            __syncthreads();
+            for (uint32_t q = threadIdx.x; q < cn * D; q += kThreads)
+                s_x[q] = d.bvals[(size_t)s_xi[q / D] * D + q % D];
+        }
         __syncthreads();
         if (!valid) continue;
         for (uint32_t i = 0; i < cn; i++) {
-            const uint32_t xi = t0 + i;
+            const uint32_t xo = s_xi[i];
             bool le = true, ge = true;
 #pragma unroll
             for (int q = 0; q < D; q++) {
@@ -71,9 +224,9 @@ __global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__rest
                 le &= a <= v[q];
                 ge &= a >= v[q];
             }
-            const bool skip = (mode == 0 && xi == j) || (mode == 1 && !d.ralive[xi]);
+            const bool skip = (mode == 0 && xo == j) || (mode == 1 && xo == 0xffffffffu);
             dm |= !skip && le && !ge;
-            if (!skip && le && ge && xi < emin && (mode != 0 || xi < j)) emin = xi;
+            if (!skip && le && ge && xo < emin && (mode != 0 || xo < j)) emin = xo;
         }
     }
     if (!valid) return;
@@ -114,6 +267,19 @@ __global__ __launch_bounds__(1024) void k_parts_commit(const PartDesc *__restric
     const uint32_t R0 = d.dcnt[0], T0 = d.dcnt[1];
     const uint32_t nb = d.nb;
     if (threadIdx.x == 0) s_dead = 0;
+    // the members of a pruner class take the fate of its pruner (same vector); the class's
+    // first index is their first equal batch tuple
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        const uint32_t c = d.eqp[b];
+        if (c == 0xffffffffu) continue;
+        const uint32_t r = d.meta[1 + c], fe = d.meta[1 + kPartPruners + c];
+        if (b != r) {
+            d.dom_b[b] = d.dom_b[r];
+            d.eq_s[b] = d.eq_s[r];
+        }
+        d.eq_b[b] = fe < b ? fe : 0xffffffffu;
+    }
+    __syncthreads();
     uint32_t kbase = 0, fbase = 0;
     for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
         const uint32_t b = c0 + threadIdx.x;
@@ -251,6 +417,7 @@ static inline unsigned nbk(size_t n) { return (unsigned)((n + kThreads - 1) / kT
 
 void launch_parts_insert(int D, const PartDesc *descs, int nparts, const PartItem *items, uint32_t nitems,
                          hipStream_t st) {
+    if (nparts) SKY_DISPATCH_D(D, (k_parts_prune<DD><<<nparts, 1024, 0, st>>>(descs)));
     if (nitems) SKY_DISPATCH_D(D, (k_parts_pairs<DD><<<nitems, kThreads, 0, st>>>(descs, items)));
     if (nparts) SKY_DISPATCH_D(D, (k_parts_commit<DD><<<nparts, 1024, 0, st>>>(descs)));
 }

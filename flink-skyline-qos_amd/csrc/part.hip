@@ -216,7 +216,8 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
         }
         rbtot += rb[g];
     }
-    // ---- work items: batch vs batch, batch vs state, state vs batch
+    // ---- work items: batch vs batch, batch vs state, state vs batch (over the undecided tuples
+    //      k_parts_prune leaves; their count lives on the device, the batch size bounds it)
     std::vector<PartItem> items;
     for (int g = 0; g < np; g++) {
         const uint32_t nb = (uint32_t)counts[g];
@@ -266,13 +267,16 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
         return SKY_E_NAN;
     }
     SKY_TRY(c->part_batch.ensure(up_bytes));
-    // work arrays: dom_b | eq_s | eq_b | kpos | fpos (per tuple), dom_s (per bounded rep)
+    // work arrays: dom_b | eq_s | eq_b | kpos | fpos | eqp | uidx (per tuple), meta (per part),
+    // dom_s (per bounded rep)
     const size_t w_nb = (size_t)ntot * 4;
-    SKY_TRY(c->part_work.ensure(5 * w_nb + (size_t)std::max<uint64_t>(rbtot, 1) * 4 + 64));
+    SKY_TRY(c->part_work.ensure(7 * w_nb + (size_t)np * kPartMeta * 4 + (size_t)std::max<uint64_t>(rbtot, 1) * 4 +
+                                64));
     char *dev = c->part_batch.as<char>();
     uint32_t *w = c->part_work.as<uint32_t>();
     uint32_t *w_dom_b = w, *w_eq_s = w + ntot, *w_eq_b = w + 2 * ntot, *w_kpos = w + 3 * ntot, *w_fpos = w + 4 * ntot;
-    uint32_t *w_dom_s = w + 5 * ntot;
+    uint32_t *w_eqp = w + 5 * ntot, *w_uidx = w + 6 * ntot, *w_meta = w + 7 * ntot;
+    uint32_t *w_dom_s = w_meta + (size_t)np * kPartMeta;
     {
         PartDesc *ds = (PartDesc *)(h + o_desc);
         uint64_t off = 0, roff = 0;
@@ -290,6 +294,9 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
             d.kpos = w_kpos + off;
             d.fpos = w_fpos + off;
             d.dom_s = w_dom_s + roff;
+            d.eqp = w_eqp + off;
+            d.uidx = w_uidx + off;
+            d.meta = w_meta + (size_t)g * kPartMeta;
             d.rrows = p->rrows.as<double>();
             d.ralive = p->ralive.as<uint8_t>();
             d.rcnt = p->rcnt.as<uint32_t>();

@@ -324,6 +324,9 @@ struct PartDesc {
     uint32_t rb;                  // bound of the state's rep count (launch sizes; the device count decides)
     uint32_t *dom_b, *eq_s, *eq_b, *kpos, *fpos;   // [nb] work (dom_b 0, eq_* ~0 on entry)
     uint32_t *dom_s;              // [rb] work (0 on entry)
+    uint32_t *eqp;                // [nb] pruner class of the tuple (~0: none), written by k_parts_prune
+    uint32_t *uidx;               // [nb] the undecided tuples (batch indices), written by k_parts_prune
+    uint32_t *meta;               // [16] |U|, pruner index per class, first index per class (k_parts_prune)
     double *rrows;                // state: reps [R][D], alive, tuples per rep
     uint8_t *ralive;
     uint32_t *rcnt;
@@ -339,6 +342,8 @@ struct PartItem {
     uint32_t y0, x0;              // 256 y rows from y0, kPartChunk x rows from x0
 };
 constexpr uint32_t kPartItemY = 256, kPartItemX = 256;
+constexpr int kPartPruners = 4;   // batch pruners per insert (k_parts_prune)
+constexpr int kPartMeta = 16;     // words of PartDesc::meta
 void launch_parts_insert(int D, const PartDesc *descs, int nparts, const PartItem *items, uint32_t nitems,
                          hipStream_t st);
 void launch_part_rkeep(uint32_t R, const uint8_t *ralive, uint32_t *keep, hipStream_t st);

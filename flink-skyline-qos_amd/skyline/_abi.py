@@ -87,6 +87,7 @@ SIGNATURES = {
     "sky_stream_append": [c_p, c_p, c_p, c_i64],
     "sky_stream_append_dev": [c_p, c_p, c_p, c_i64],
     "sky_stream_size": [c_p, P_i64, P_i64],
+    "sky_stream_reserve": [c_p, c_i64],
     "sky_stream_query": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_stream_query_dev": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_synth_dev": [c_p, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],

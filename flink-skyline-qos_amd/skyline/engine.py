@@ -347,9 +347,11 @@ class SkylineStream:
         return ids[:g.value].copy(), org[:g.value].copy()
 
     def reserve(self, cap):
-        """Size the page-locked result buffers once (pinning hundreds of MB takes tens of ms:
-        not something a trigger should pay)."""
+        """Size the page-locked result buffers and the device state once, for up to `cap`
+        resident tuples (pinning hundreds of MB takes tens of ms, and every device regrowth
+        synchronises the GPU: not something a trigger should pay)."""
         self._out(max(int(cap), 1))
+        check(lib().sky_stream_reserve(self.h, max(int(cap), 1)))
 
     def query_host_view(self):
         """Query into the reusable page-locked buffers; returns g (results in view()[:g])."""

@@ -173,6 +173,11 @@ int sky_stream_create(sky_ctx *ctx, int64_t window, sky_stream **out);
 int sky_stream_destroy(sky_stream *s);
 int sky_stream_append(sky_stream *s, const int64_t *ids, const double *values, int64_t n);
 int sky_stream_append_dev(sky_stream *s, const int64_t *d_ids, const double *d_values, int64_t n);
+/* pre-sizes the device state for up to `tuples` resident tuples plus one appended batch (the
+ * resident buffers, the query's working buffers, the host-view output), so that no trigger
+ * pays a device allocation (each regrowth synchronises the device).  Optional; call before
+ * the stream starts (e.g. in the operator's open()), never on a timed path. */
+int sky_stream_reserve(sky_stream *s, int64_t tuples);
 /* resident tuples and tuples appended since creation */
 int sky_stream_size(sky_stream *s, int64_t *resident, int64_t *appended);
 int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);

@@ -60,5 +60,6 @@ public final class SkylineHip {
     public static native void streamDestroy(long stream);
     public static native void streamAppend(long stream, long[] ids, double[] values, int n);
     public static native int streamQuery(long stream, long[] idsOut, int[] originOut);
+    public static native void streamReserve(long stream, long tuples);
     public static native long streamResident(long stream);
 }

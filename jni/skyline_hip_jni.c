@@ -414,6 +414,15 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_streamQuery(JNIEnv *env, jclass 
     return (jint)g;
 }
 
+JNIEXPORT void JNICALL Java_org_main_SkylineHip_streamReserve(JNIEnv *env, jclass cls, jlong s, jlong tuples) {
+    (void)cls;
+    if (tuples < 0) {
+        throw_arg(env, "tuples must be >= 0");
+        return;
+    }
+    (void)fail(env, sky_stream_reserve(STREAM(s), (int64_t)tuples));
+}
+
 JNIEXPORT jlong JNICALL Java_org_main_SkylineHip_streamResident(JNIEnv *env, jclass cls, jlong s) {
     int64_t r = 0, a = 0;
     if (fail(env, sky_stream_size(STREAM(s), &r, &a))) return -1;

@@ -61,6 +61,24 @@ def test_part_state_special_values(gpu_engine_factory, oracle):
     replay(gpu_engine_factory, oracle, v, [777] * 25 + [20000 - 777 * 25], 3)
 
 
+def test_part_state_pruner_classes(gpu_engine_factory, oracle):
+    """k_parts_prune's corner cases: many tuples equal to a pruner (classes sharing its fate, the
+    first of them the equal-earlier tuple), criterion ties where the chosen pruner (the smaller
+    index) is dominated by a later tuple with the same rounded criterion, pruners equal to each
+    other, -0.0 / +0.0 twins, and rows whose criterion is NaN (+inf and -inf in one row)."""
+    rng = np.random.default_rng(21)
+    n, D = 24000, 3
+    v = rng.integers(0, 4, size=(n, D)).astype(np.float64)
+    v[::3] = [1.0, 1.0, 1.0]                        # a big class of one vector
+    v[5::97] = [1.0, 1e-17, 0.0]                     # same f64 sum as (1, 0, 0) ...
+    v[6::97] = [1.0, 0.0, 0.0]                       # ... which dominates it
+    v[40::211] = [-0.0, 2.0, 2.0]
+    v[41::211] = [0.0, 2.0, 2.0]
+    v[77::509] = [np.inf, -np.inf, 1.0]              # criterion NaN
+    v[78::509] = [-np.inf, 5.0, 5.0]
+    replay(gpu_engine_factory, oracle, v, [5000, 1, 2, 4000, 997, 3000] + [2000] * 4 + [n - 17000], D)
+
+
 def test_part_state_kills_and_compaction(gpu_engine_factory, oracle):
     """Every batch dominates most of the state before it: reps die, their tuples are dropped
     by the lazy compaction, and the survivors keep their insertion order."""

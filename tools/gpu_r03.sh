@@ -70,3 +70,23 @@ if [[ $STEPS == *c4ab* ]]; then
     python -c "import json;d=json.load(open('$OUT/c4_${TAG}_$K.json'));print('$K', d['ms_per_step'], d['p50_query_latency_ms'], d['roofline']['avg_launch_ms'])"
   done
 fi
+if [[ $STEPS == *optrace* ]]; then
+  # the operator path (sky_parts_insert flushes) under the kernel trace: GPU time per call vs host time
+  export TMPDIR=/tmp
+  rm -rf $OUT/optrace_$TAG
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/optrace_$TAG -o run -- python3 -u tools/op_bench.py ${OP_N:-10000000} \
+      > $OUT/optrace_$TAG.json 2> $OUT/optrace_$TAG.err || { tail -30 $OUT/optrace_$TAG.err; exit 1; }
+  python3 tools/prof_summary.py trace $OUT/optrace_$TAG > $OUT/optrace_${TAG}_summary.txt
+  head -16 $OUT/optrace_${TAG}_summary.txt
+  cut -c1-600 $OUT/optrace_$TAG.json
+fi
+if [[ $STEPS == *filterpmc* ]]; then
+  bash tools/gpu_pmc.sh $TAG
+fi
+if [[ $STEPS == *c5bench* ]]; then
+  timeout -k 10 300 python -u bench.py --config C5 > $OUT/c5_$TAG.json 2> $OUT/c5_$TAG.err || { tail -30 $OUT/c5_$TAG.err; exit 1; }
+  python3 -c "
+import json; d=json.load(open('$OUT/c5_$TAG.json'))
+for k in ('landmark','sliding_10M'):
+    x=d[k]; print(k, 'p50', round(x['p50_query_latency_ms'],3), 'p90', round(x['p90_query_latency_ms'],3), 'max', round(x['max_query_latency_ms'],3), x['latencies_ms'])"
+fi
