@@ -136,6 +136,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     SKY_TRY(p.mbr_gpr.ensure(mbr_groups(n_union) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)n_own * 4));
     SKY_TRY(p.mbr_pairs.ensure(16));
+    SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(yt) * 4));
     // one radix scratch for both sorts (they run one after the other on the stream)
     SKY_TRY(p.scratch.ensure(radix_scratch_words(std::max(n_union, n_own)) * 4 + 64));
     FillSet fill;
@@ -144,6 +145,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     fill.add(p.mbr_mm.as<uint32_t>() + 2 * D, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + 3 * D, (size_t)D * 4, 0);
     fill.add(p.mbr_pairs.p, 16, 0);
+    fill.add(p.mbr_lpt.p, kMbrLptHead * 4, 0);
     fill.add(p.mbr_domf.p, (size_t)n_own * 4, 0);
     HIP_TRY(fill.launch(st));
     MbrUnionArgs a;
@@ -178,6 +180,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     set(a.y, (const char *)rows + (size_t)own_off * rb, c->dist_ukey.as<uint64_t>() + own_off, n_own, xt, n_union,
         2 * D, p.scratch.as<uint32_t>());
     a.y.domf = p.mbr_domf.as<uint32_t>();
+    a.y.lpt = mbr_lpt_enabled() ? p.mbr_lpt.as<uint32_t>() : nullptr;
     a.ymult = c->dist_umult.as<int64_t>() + own_off;
     a.K = K;
     a.flags = c->main.dist_own.as<uint8_t>();

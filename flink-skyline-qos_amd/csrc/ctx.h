@@ -79,7 +79,15 @@ struct Ctx {
     // batched per-key inserts (sky_parts_insert): the call's upload (descriptors, work items,
     // ids, rows) and work arrays on the device; pinned staging slots, each reusable once its
     // event (the upload) has completed
-    DevBuf part_batch, part_work;
+    // the upload goes out on a copy stream into one of two device buffers, so that a call's
+    // upload overlaps the previous call's kernels; part_done[b]: the kernels that read buffer b
+    DevBuf part_batch[2], part_work;
+    // sky_parts_global_merge work buffers
+    DevBuf pgm_w, pgm_flag, pgm_tsel, pgm_tpos, pgm_scr, pgm_lists, pgm_surv, pgm_sorg, pgm_ids, pgm_org;
+    hipStream_t part_copy_st = nullptr;
+    hipEvent_t part_done[2] = {nullptr, nullptr};
+    bool part_done_rec[2] = {false, false};
+    int part_buf_next = 0;
     struct Staging {
         void *h = nullptr;
         size_t cap = 0;
@@ -92,6 +100,12 @@ struct Ctx {
         for (Staging &s : part_stage) {
             if (s.h) (void)hipHostFree(s.h);
             if (s.ev) (void)hipEventDestroy(s.ev);
+        }
+        for (hipEvent_t &e : part_done)
+            if (e) (void)hipEventDestroy(e);
+        if (part_copy_st) {
+            (void)hipStreamSynchronize(part_copy_st);
+            (void)hipStreamDestroy(part_copy_st);
         }
     }
 

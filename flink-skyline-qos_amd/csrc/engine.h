@@ -81,7 +81,7 @@ struct Pipe {
     DevBuf cmin, pr2, npr2, live, livepos, rows2, sortkey2, slot_src2, rows3, sortkey3, slot_src3;
     // bounding-box pruned all-pairs pass over large rep sets (k_mbr.hip)
     DevBuf mbr_mm, mbr_code, mbr_code2, mbr_idx, mbr_idx2, mbr_rows, mbr_part, mbr_min, mbr_max, mbr_pr, mbr_sub, mbr_domf,
-        mbr_pairs, mbr_gmin, mbr_gpr;
+        mbr_pairs, mbr_gmin, mbr_gpr, mbr_lpt;
     bool used_mbr = false;
     size_t slot_hint = 0;       // candidate slots the next run allocates (grown on overflow)
     int64_t slot_reruns = 0;    // runs repeated because the slots overflowed
@@ -154,6 +154,8 @@ struct Ctx;
 int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
 // pre-size the tuple-count-proportional buffers of a run over n tuples
 int pipe_reserve(Ctx &c, Pipe &p, uint32_t n);
+// SKY_MBR_LPT=0 turns the bounding-box pass's cost-ordered work queue off (A/B knob)
+bool mbr_lpt_enabled();
 // read device ranges into host memory in one synchronisation (one gather launch when they are small)
 int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
               std::vector<void *> dsts);

@@ -599,6 +599,12 @@ int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *,
     return SKY_OK;
 }
 
+// SKY_MBR_LPT=0: the pair pass takes its y tiles in blockIdx order (A/B knob, read per query)
+bool mbr_lpt_enabled() {
+    const char *e = getenv("SKY_MBR_LPT");
+    return !(e && e[0] == '0');
+}
+
 // both skyline levels of the rep set in one bounding-box pruned all-pairs pass (k_mbr.hip)
 static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) {
     hipStream_t st = c.st;
@@ -627,8 +633,10 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_gpr.ensure(mbr_groups(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
     SKY_TRY(p.mbr_pairs.ensure(64));
+    SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(ntiles) * 4));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
     FillSet fill;
+    fill.add(p.mbr_lpt.p, kMbrLptHead * 4, 0);
     fill.add(p.mbr_mm.p, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
     fill.add(p.mbr_pairs.p, 64, 0);
@@ -670,6 +678,7 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.gprange = p.mbr_gpr.as<uint32_t>();
     a.domf = p.mbr_domf.as<uint32_t>();
     a.pairs = p.mbr_pairs.as<unsigned long long>();
+    a.lpt = mbr_lpt_enabled() ? p.mbr_lpt.as<uint32_t>() : nullptr;
     a.alive_l = p.alive_l.as<uint8_t>();
     a.alive_g = p.alive_g.as<uint8_t>();
     c.ktimer_begin("mbr", st);

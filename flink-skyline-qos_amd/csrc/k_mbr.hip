@@ -336,6 +336,67 @@ __global__ __launch_bounds__(kThreads) void k_mbr_groups(const uint32_t *__restr
     }
 }
 
+// threads per workgroup of the pair pass: ONE wave.  A workgroup's resources are held until its
+// last wave exits, and the y tiles' work varies by orders of magnitude, so 4-wave workgroups kept
+// slots occupied by finished waves (measured: ~2 resident waves per SIMD of the 6 the registers
+// allow)
+constexpr int kMbrPairThreads = 64;
+
+// the y tiles of the pair pass (the x tiles' set, or another: the multi-GPU merge's own rows)
+struct MbrYSet {
+    const uint32_t *trows, *tpart, *tmax, *tprange;
+    uint32_t mr, ntiles;
+};
+
+// ---- the y tiles' work queue ---------------------------------------------------------------
+// The work of a y tile varies by orders of magnitude (a loose box reaches many x tiles; PMC on
+// std-anti 8D 2M: ~2 resident waves per SIMD on average against 6 possible, i.e. the launch
+// waits for its slowest waves).  So the y tiles are handed out heaviest first (longest
+// processing time first): the cost estimate is the number of x groups the tile's box reaches,
+// the order a counting sort over 32 log2 buckets, and every wave of the pair pass takes the
+// next tile of that order from a ticket counter.
+template <class R>
+__global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restrict__ gmin, uint32_t ngroups,
+                                                       MbrYSet ys, uint32_t *__restrict__ lpt) {
+    constexpr int NW = R::NW;
+    const uint32_t yt = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
+    if (yt >= ys.ntiles) return;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t ymax[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
+    uint32_t cnt = 0;
+    for (uint32_t g0 = 0; g0 < ngroups; g0 += 64) {
+        const uint32_t q = min(g0 + lane, ngroups - 1u);
+        uint32_t gc[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
+        cnt += (uint32_t)__popcll(__ballot(g0 + lane < ngroups && R::le(gc, ymax)));
+    }
+    if (lane == 0) {
+        lpt[kMbrLptHead + yt] = cnt;
+        atomicAdd(&lpt[31 - __clz(cnt | 1u)], 1u);          // bucket = floor(log2(cnt)), 0..31
+    }
+}
+
+// one workgroup: bucket offsets (heaviest bucket first), then every y tile to its slot
+__global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__restrict__ lpt) {
+    __shared__ uint32_t s_off[32];
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (int b = 31; b >= 0; b--) {
+            s_off[b] = o;
+            o += lpt[b];
+        }
+    }
+    __syncthreads();
+    uint32_t *order = lpt + kMbrLptHead + nyt;
+    for (uint32_t yt = threadIdx.x; yt < nyt; yt += 1024) {
+        const uint32_t c = lpt[kMbrLptHead + yt];
+        order[atomicAdd(&s_off[31 - __clz(c | 1u)], 1u)] = yt;
+    }
+}
+
 // ---- the pair pass -------------------------------------------------------------------
 // FULL: the complete test (x <= y and not y <= x) — given partition keys may repeat a
 // vector across partitions, and f32/f64 rows may hold -0.0 / +0.0 twins; otherwise the rows
@@ -349,12 +410,8 @@ __global__ __launch_bounds__(kThreads) void k_mbr_groups(const uint32_t *__restr
 // The y tiles (ytrows / ytpart / ytmax / ytprange, ymr rows) may be another set than the x
 // tiles (the multi-GPU merge: own vectors against the union, FULL only); for one set they are
 // the same arrays.
-struct MbrYSet {
-    const uint32_t *trows, *tpart, *tmax, *tprange;
-    uint32_t mr, ntiles;
-};
-template <class R, bool FULL, bool GM, bool PIPE>
-__global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+template <class R, bool FULL, bool GM, bool PIPE, bool BC = false>
+__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tprange,
@@ -363,19 +420,29 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                                                         const uint32_t *__restrict__ gprange, uint32_t mr,
                                                         uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
                                                         uint32_t *__restrict__ domf,
-                                                        unsigned long long *__restrict__ pairs) {
+                                                        unsigned long long *__restrict__ pairs,
+                                                        uint32_t *__restrict__ lpt) {
     constexpr int NW = R::NW;
-    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
-    // XCD b % 8; give each XCD a contiguous run of y tiles, whose reachable x tiles then
-    // overlap and stay in that XCD's L2 (the grid is padded to a multiple of 8)
-    const uint32_t per_xcd = gridDim.x / 8u;
-    const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
-    // the x tiles are split into nsplit ranges, one work item each: the work of a y tile
-    // varies by orders of magnitude (a loose box reaches many tiles), and one wave per y
-    // tile left the launch waiting for its slowest waves
-    const uint32_t split = blk % nsplit;
-    const uint32_t yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kThreads / 64) + (threadIdx.x >> 6));
-    if (yt >= ys.ntiles) return;
+    uint32_t split, yt;
+    if (lpt) {
+        // the next (y tile, x range) work item of the cost order, heaviest tiles first
+        uint32_t item = 0;
+        if ((threadIdx.x & 63) == 0) item = atomicAdd(&lpt[32], 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl((int)item, 0, 64));
+        if (item >= ys.ntiles * nsplit) return;
+        split = item % nsplit;
+        yt = __builtin_amdgcn_readfirstlane(lpt[kMbrLptHead + ys.ntiles + item / nsplit]);
+    } else {
+        // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
+        // XCD b % 8; give each XCD a contiguous run of y tiles, whose reachable x tiles then
+        // overlap and stay in that XCD's L2 (the grid is padded to a multiple of 8)
+        const uint32_t per_xcd = gridDim.x / 8u;
+        const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+        // the x tiles are split into nsplit ranges, one work item each
+        split = blk % nsplit;
+        yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kMbrPairThreads / 64) + (threadIdx.x >> 6));
+        if (yt >= ys.ntiles) return;
+    }
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
     const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
     const uint32_t lane = threadIdx.x & 63;
@@ -399,8 +466,8 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
     const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
     // this wave's y rows and partitions in LDS for the broadcast reads of the tests
-    __shared__ uint32_t s_y[kThreads / 64][64 * NW];
-    __shared__ uint32_t s_py[kThreads / 64][64];
+    __shared__ uint32_t s_y[kMbrPairThreads / 64][64 * NW];
+    __shared__ uint32_t s_py[kMbrPairThreads / 64][64];
     uint32_t *sy = s_y[threadIdx.x >> 6], *spy = s_py[threadIdx.x >> 6];
 #pragma unroll
     for (int w = 0; w < NW; w++) sy[lane * NW + w] = y[w];
@@ -411,14 +478,14 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
     uint64_t npairs = 0, ntested = 0;
     uint32_t ngrp = 0, nbox = 0, nlist = 0;    // diagnostics (dbg & 4): groups / tiles passing, listed
     // per wave: the reachable x tiles of the current group of 64 (tile index, lane mask)
-    __shared__ uint32_t s_lx[kThreads / 64][64];
-    __shared__ uint64_t s_lm[kThreads / 64][64];
+    __shared__ uint32_t s_lx[kMbrPairThreads / 64][64];
+    __shared__ uint64_t s_lm[kMbrPairThreads / 64][64];
     uint32_t *lx = s_lx[threadIdx.x >> 6];
     uint64_t *lmq = s_lm[threadIdx.x >> 6];
     // the x tile under test (rows, partitions) and its (y, sub-box) entries
-    __shared__ uint32_t s_x[kThreads / 64][64 * NW];
-    __shared__ uint32_t s_px[kThreads / 64][64];
-    __shared__ uint8_t s_e[kThreads / 64][256];
+    __shared__ uint32_t s_x[kMbrPairThreads / 64][64 * NW];
+    __shared__ uint32_t s_px[kMbrPairThreads / 64][64];
+    __shared__ uint8_t s_e[kMbrPairThreads / 64][256];
     uint32_t *sx = s_x[threadIdx.x >> 6], *spx = s_px[threadIdx.x >> 6];
     uint8_t *se = s_e[threadIdx.x >> 6];
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -461,6 +528,34 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
         if (!lm) return;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         ntested++;
+        if constexpr (BC) {
+            // lane = x row (in registers since load_tile); each reachable y is broadcast from its
+            // lane (readlane -> scalar operands) and compared with all 64 rows at once: no LDS
+            // staging, no barrier, and the y's are independent of each other
+            const bool xvalid = (uint32_t)lane < nx;
+            uint64_t h_any = 0, h_same = 0, m = lm;
+            npairs += 64ull * (uint64_t)__popcll(m);
+            if (dbg & 1) return;
+            while (m) {
+                const uint32_t yb = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                uint32_t yv[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) yv[w] = (uint32_t)__builtin_amdgcn_readlane((int)y[w], (int)yb);
+                const uint32_t pyv = (uint32_t)__builtin_amdgcn_readlane((int)py, (int)yb);
+                bool dom = xvalid & R::le(xv, yv);
+                if constexpr (FULL) dom = dom & !R::le(yv, xv);
+                else dom = dom & !(xt == yt && (uint32_t)lane == yb);
+                const uint64_t hm = __ballot(dom);
+                if (hm) {
+                    h_any |= 1ull << yb;
+                    if (__ballot(dom & (px == pyv))) h_same |= 1ull << yb;
+                }
+            }
+            f |= ((h_same >> lane) & 1ull) ? 3u : (((h_any >> lane) & 1ull) ? 2u : 0u);
+            live &= __ballot(!(f & 1u));
+            return;
+        }
         uint64_t ms[4];
         uint32_t E = 0;
 #pragma unroll
@@ -640,7 +735,7 @@ __global__ __launch_bounds__(kThreads) void k_mbr_pairs(const uint32_t *__restri
                 load_group(tg, tr, gn);
             }
             if constexpr (PIPE) process2(cnt);
-            else process(cnt);                         // A/B: single-buffered (round 2)
+            else process(cnt);                         // single-buffered (round 2; not instantiated)
             if (!more || !live) break;
             g = gn;
         }
@@ -675,10 +770,12 @@ int mbr_row_words(int D, int fmt) {
     return 2 * padded_dims<double>(D);
 }
 
-// SKY_MBR_PIPE=0: the single-buffered tile loads of round 2 (A/B knob)
-static bool mbr_pipe() {
-    const char *e = getenv("SKY_MBR_PIPE");
-    return !(e && atoi(e) == 0);
+// SKY_MBR_BCAST=1: each reachable y broadcast (readlane) against the whole x tile instead of the
+// 16-row sub-box entries staged in LDS (A/B knob; measured slower: std-anti 8D 2M 9.2 vs 7.4 ms,
+// 10M 58 vs 30 ms -- 6x the pair tests outweigh the saved LDS staging)
+static bool mbr_bcast() {
+    const char *e = getenv("SKY_MBR_BCAST");
+    return e && atoi(e) == 1;
 }
 // SKY_MBR_ORDER=morton: the Morton order of round 2 (A/B knob, read per build)
 static bool mbr_hilbert() {
@@ -719,6 +816,13 @@ static const uint32_t *mbr_build(const uint32_t *rows, const uint64_t *rep_key, 
     return perm;
 }
 
+// the cost order of the y tiles (lpt: kMbrLptHead words zeroed by the caller)
+template <class R>
+static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, hipStream_t st) {
+    k_mbr_cost<R><<<(ys.ntiles + 3) / 4, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
+    k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, lpt);
+}
+
 template <class R, int D>
 static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t mr = a.mr;
@@ -727,14 +831,15 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t *perm = mbr_build<R, D>((const uint32_t *)a.rows, a.rep_key, mr, a.mm, a.code, a.code_alt, a.idx,
                                            a.idx_alt, a.radix_scratch, a.err, a.trows, a.tpart, a.tmin, a.tmax,
                                            a.tprange, a.tsub, a.gmin, a.gprange, st, lerr);
-    const unsigned gt = (ntiles + 3) / 4;
+    const unsigned gt = (ntiles + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64);
     const uint32_t nsplit = a.nsplit < 1 ? 1u : (uint32_t)a.nsplit;
     const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
+    if (a.lpt) mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    (mbr_pipe() ? k_mbr_pairs<R, F, G, true> : k_mbr_pairs<R, F, G, false>)                                  \
-        <<<gp, kThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
-                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs)
+    (mbr_bcast() ? k_mbr_pairs<R, F, G, true, true> : k_mbr_pairs<R, F, G, true>)                              \
+        <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
+                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt)
     if (a.full) {
         if (a.gmerge) SKY_MBR_PAIRS(true, true);
         else SKY_MBR_PAIRS(true, false);
@@ -778,11 +883,12 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
                                            y.idx_alt, y.radix_scratch, y.err, y.trows, y.tpart, y.tmin, y.tmax,
                                            y.tprange, y.tsub, nullptr, nullptr, st, lerr);
     const uint32_t nyt = (uint32_t)mbr_tiles(y.mr);
-    const unsigned gp = ((nyt + 3) / 4 + 7) / 8 * 8;
+    const unsigned gp = ((nyt + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64) + 7) / 8 * 8;
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
-    k_mbr_pairs<R, true, true, true><<<gp, kThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+    if (y.lpt) mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
+    (mbr_bcast() ? k_mbr_pairs<R, true, true, true, true> : k_mbr_pairs<R, true, true, true>)<<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
-                                                        y.domf, x.pairs);
+                                                        y.domf, x.pairs, y.lpt);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,
                                                                              a.K, a.flags, a.lsz, a.surv);
 }

@@ -4,13 +4,16 @@
 // every 5000-tuple buffer B.  The state is held as
 //   reps     distinct vectors (f64 [R][D]), alive flag, number of tuples per rep
 //   tuples   ids and rep index in insertion order (T entries, Tdead of them on dead reps)
-// and an insert costs O(|B| (|B| + R)) pair tests plus O(|B|) writes, independent of the
-// number of (duplicate) tuples in S:
-//   k_parts_pairs  B vs B, B vs alive S reps  -> dom_b (any dominator), eq_s (equal S rep),
-//                  eq_b (first equal earlier batch tuple);  S reps vs B -> dom_s
-//   k_parts_commit per batch tuple: kept (not dominated), new rep (kept, first of its vector, no
-//                  equal S rep); kept tuples appended (ids, rep), new reps appended, joined reps
-//                  counted; dominated S reps die, their tuples count as dead (compacted lazily)
+// and an insert costs O(|U| (|U| + R)) pair tests (U: the batch tuples its pruners leave
+// undecided) plus O(|B|) work, independent of the number of (duplicate) tuples in S:
+//   k_parts_crit / k_parts_classify  batch pruners: every batch tuple dropped (dominated by a
+//                  pruner), in a pruner's class (equal to it) or undecided (U)
+//   k_parts_pairs  U vs U, U vs alive S reps  -> dom_b (any dominator), eq_s (equal S rep),
+//                  eq_b (first equal earlier batch tuple);  S reps vs U -> dom_s
+//   k_parts_count / k_parts_place / k_parts_join  per batch tuple: kept (not dominated), new rep
+//                  (kept, first of its vector, no equal S rep); kept tuples appended (ids, rep),
+//                  new reps appended, joined reps counted; dominated S reps die, their tuples
+//                  count as dead (compacted lazily)
 // S reps are never dominated by each other, a tuple equal to a rep shares its fate (equal
 // vectors never dominate each other), and a rep killed by b kills every batch tuple equal to
 // it too (b dominates them), so no surviving tuple joins a dying rep.
@@ -25,13 +28,12 @@ constexpr uint32_t kPartChunk = 256;    // x rows per workgroup (grid.y): many s
 
 // ---- batched, asynchronous insert (sky_parts_insert) ---------------------------------------
 // One call inserts one batch into each of G parts (the full buffers of several Flink keys) with
-// four launches and no host read: k_fill_multi (flags), k_parts_pairs (work items over every
-// part), k_parts_commit (one workgroup per part).  Counts live on the device (PartDesc::dcnt);
-// launches are sized by host-side bounds and clamp to the device counts; the commit mirrors
-// the new counts into host-mapped memory (seqlock) so that the host tightens its bounds
-// without synchronising.
+// six launches and no host read (grid = batch slice x part, except the pair pass: one
+// workgroup per work item).  Counts live on the device (PartDesc::dcnt); launches are sized by
+// host-side bounds and clamp to the device counts; the part's last slice mirrors the new counts
+// into host-mapped memory (seqlock) so that the host tightens its bounds without synchronising.
 
-// ---- batch pruners (k_parts_prune) --------------------------------------------------------
+// ---- batch pruners (k_parts_crit, k_parts_classify) ----------------------------------------
 // Before any pair test, each part's batch is reduced to its UNDECIDED tuples U: kPartPruners
 // batch tuples p_c minimise positive-weight linear criteria (a dominator never has a larger
 // criterion value: rounding is monotone), and every batch tuple is classified against them in
@@ -55,93 +57,125 @@ __device__ __forceinline__ double part_crit(const double (&v)[D], int c) {
     return s;
 }
 
+// The insert's kernels work on SLICES of kPartSlice batch tuples (grid.x = slice, grid.y =
+// part; 256 threads, 4 tuples each, b = slice * 1024 + k * 256 + thread): a 5000-tuple buffer
+// spreads over 5 workgroups per part instead of one 1024-thread workgroup, whose dependent
+// chain of loads, reductions and barriers (one CU) took 20-30 us per call.
+constexpr int kSliceIt = kPartSlice / kThreads;    // tuples per thread
+
+// (value, index) lexicographic minimum: the smaller criterion, then the smaller index
+__device__ __forceinline__ void vi_min(double &v, uint32_t &i, double ov, uint32_t oi) {
+    if (oi != 0xffffffffu && (i == 0xffffffffu || ov < v || (ov == v && oi < i))) {
+        v = ov;
+        i = oi;
+    }
+}
+
+// K1: per slice, the (criterion, index) minimum of each criterion; slice 0 also resets the
+// part's insert words (|U|, first indices, killed tuples, tickets)
 template <int D>
-__global__ __launch_bounds__(1024) void k_parts_prune(const PartDesc *__restrict__ descs) {
-    __shared__ double s_bv[16][kPartPruners];
-    __shared__ uint32_t s_bi[16][kPartPruners];
-    __shared__ double s_pr[kPartPruners][D];
-    __shared__ uint32_t s_pi[kPartPruners], s_fe[kPartPruners], s_u;
-    const PartDesc &d = descs[blockIdx.x];
-    const uint32_t nb = d.nb;
+__global__ __launch_bounds__(kThreads) void k_parts_crit(const PartDesc *__restrict__ descs) {
+    __shared__ double s_bv[kThreads / 64][kPartPruners];
+    __shared__ uint32_t s_bi[kThreads / 64][kPartPruners];
+    const PartDesc &d = descs[blockIdx.y];
+    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    if (s0 >= nb) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x < kPartMeta) d.meta[threadIdx.x] = threadIdx.x >= 1 + kPartPruners &&
+                                                                          threadIdx.x < 1 + 2 * kPartPruners
+                                                                          ? 0xffffffffu : 0u;
+    double rv[kSliceIt][D];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = min(s0 + k * kThreads + threadIdx.x, nb - 1u);
+#pragma unroll
+        for (int q = 0; q < D; q++) rv[k][q] = d.bvals[(size_t)b * D + q];
+    }
     double bv[kPartPruners];
     uint32_t bi[kPartPruners];
 #pragma unroll
     for (int c = 0; c < kPartPruners; c++) {
-        bv[c] = __longlong_as_double(0x7ff0000000000000ll);
+        bv[c] = 0.0;
         bi[c] = 0xffffffffu;
     }
-    // per thread: increasing b, so the first minimum is kept (ties -> the smallest index)
-    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
-        double v[D];
 #pragma unroll
-        for (int q = 0; q < D; q++) v[q] = d.bvals[(size_t)b * D + q];
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = s0 + k * kThreads + threadIdx.x;
+        if (b >= nb) continue;
 #pragma unroll
-        for (int c = 0; c < kPartPruners; c++) {
-            const double s = part_crit<D>(v, c);
-            if (s < bv[c] || bi[c] == 0xffffffffu) {
-                bv[c] = s;
-                bi[c] = b;
-            }
-        }
+        for (int c = 0; c < kPartPruners; c++) vi_min(bv[c], bi[c], part_crit<D>(rv[k], c), b);
     }
-    // (value, index) minimum over the block: waves, then the 16 wave results
 #pragma unroll
     for (int c = 0; c < kPartPruners; c++) {
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const double ov = __shfl_xor(bv[c], o, 64);
-            const uint32_t oi = (uint32_t)__shfl_xor((int)bi[c], o, 64);
-            if (oi != 0xffffffffu && (bi[c] == 0xffffffffu || ov < bv[c] || (ov == bv[c] && oi < bi[c]))) {
-                bv[c] = ov;
-                bi[c] = oi;
-            }
-        }
+        for (int o = 32; o >= 1; o >>= 1)
+            vi_min(bv[c], bi[c], __shfl_xor(bv[c], o, 64), (uint32_t)__shfl_xor((int)bi[c], o, 64));
         if (lane == 0) {
             s_bv[wave][c] = bv[c];
             s_bi[wave][c] = bi[c];
         }
     }
-    if (threadIdx.x == 0) s_u = 0;
     __syncthreads();
     if (threadIdx.x < kPartPruners) {
         const int c = threadIdx.x;
         double v = s_bv[0][c];
         uint32_t i = s_bi[0][c];
-        for (int w = 1; w < 16; w++) {
-            const double ov = s_bv[w][c];
-            const uint32_t oi = s_bi[w][c];
-            if (oi != 0xffffffffu && (i == 0xffffffffu || ov < v || (ov == v && oi < i))) {
-                v = ov;
-                i = oi;
-            }
-        }
+        for (int w = 1; w < kThreads / 64; w++) vi_min(v, i, s_bv[w][c], s_bi[w][c]);
+        d.sl_v[blockIdx.x * kPartPruners + c] = v;
+        d.sl_i[blockIdx.x * kPartPruners + c] = i;
+    }
+}
+
+// K2: the pruners (the minima over the part's slices, reduced by every workgroup itself), then
+// each tuple of the slice classified: dropped / pruner class / undecided (appended to U)
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__restrict__ descs) {
+    __shared__ double s_pr[kPartPruners][D];
+    __shared__ uint32_t s_pi[kPartPruners], s_fe[kPartPruners];
+    const PartDesc &d = descs[blockIdx.y];
+    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    // the insert's dom_s (per bounded rep) starts here, spread over the part's workgroups
+    for (uint32_t r = blockIdx.x * kThreads + threadIdx.x; r < d.rb; r += gridDim.x * kThreads) d.dom_s[r] = 0u;
+    if (s0 >= nb) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t nsl = (nb + kPartSlice - 1) / kPartSlice;
+    if (threadIdx.x < kPartPruners) {
+        const int c = threadIdx.x;
+        double v = 0.0;
+        uint32_t i = 0xffffffffu;
+        for (uint32_t q = 0; q < nsl; q++) vi_min(v, i, d.sl_v[q * kPartPruners + c], d.sl_i[q * kPartPruners + c]);
         s_pi[c] = i;
         s_fe[c] = 0xffffffffu;
+        if (blockIdx.x == 0) d.meta[1 + c] = i;
     }
     __syncthreads();
     if (threadIdx.x < kPartPruners * D) {
         const int c = threadIdx.x / D, q = threadIdx.x % D;
         s_pr[c][q] = s_pi[c] != 0xffffffffu ? d.bvals[(size_t)s_pi[c] * D + q] : 0.0;
     }
+    double rv[kSliceIt][D];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = min(s0 + k * kThreads + threadIdx.x, nb - 1u);
+#pragma unroll
+        for (int q = 0; q < D; q++) rv[k][q] = d.bvals[(size_t)b * D + q];
+    }
     __syncthreads();
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
-        const uint32_t b = c0 + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = s0 + k * kThreads + threadIdx.x;
         const bool valid = b < nb;
         uint32_t cls = 0xffffffffu;
         bool dom = false;
         if (valid) {
-            double v[D];
-#pragma unroll
-            for (int q = 0; q < D; q++) v[q] = d.bvals[(size_t)b * D + q];
             for (int c = 0; c < kPartPruners; c++) {
                 if (s_pi[c] == 0xffffffffu) break;
                 bool le = true, ge = true;
 #pragma unroll
                 for (int q = 0; q < D; q++) {
-                    le &= s_pr[c][q] <= v[q];
-                    ge &= s_pr[c][q] >= v[q];
+                    le &= s_pr[c][q] <= rv[k][q];
+                    ge &= s_pr[c][q] >= rv[k][q];
                 }
                 if (le && !ge) {
                     dom = true;
@@ -152,23 +186,22 @@ __global__ __launch_bounds__(1024) void k_parts_prune(const PartDesc *__restrict
                     break;
                 }
             }
-            if (dom) d.dom_b[b] = 1u;
+            d.dom_b[b] = dom ? 1u : 0u;
+            d.eq_s[b] = 0xffffffffu;
+            d.eq_b[b] = 0xffffffffu;
             d.eqp[b] = cls;
             if (cls != 0xffffffffu) atomicMin(&s_fe[cls], b);
         }
         const bool inU = valid && !dom && (cls == 0xffffffffu || b == s_pi[cls]);
         const uint64_t um = __ballot(inU);
         uint32_t base = 0;
-        if (lane == 0 && um) base = atomicAdd(&s_u, (uint32_t)__popcll(um));
+        if (lane == 0 && um) base = atomicAdd(&d.meta[0], (uint32_t)__popcll(um));
         base = (uint32_t)__shfl((int)base, 0, 64);
         if (inU) d.uidx[base + (uint32_t)__popcll(um & lt)] = b;
     }
     __syncthreads();
-    if (threadIdx.x == 0) d.meta[0] = s_u;
-    if (threadIdx.x < kPartPruners) {
-        d.meta[1 + threadIdx.x] = s_pi[threadIdx.x];
-        d.meta[1 + kPartPruners + threadIdx.x] = s_fe[threadIdx.x];
-    }
+    if (threadIdx.x < kPartPruners && s_fe[threadIdx.x] != 0xffffffffu)
+        atomicMin(&d.meta[1 + kPartPruners + threadIdx.x], s_fe[threadIdx.x]);
 }
 
 // dominance as ServiceTuple.dominates (ServiceTuple.java:67-77): <= everywhere, < somewhere
@@ -238,127 +271,209 @@ __global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__rest
     if (emin != 0xffffffffu) atomicMin(mode == 0 ? &d.eq_b[j] : &d.eq_s[j], emin);
 }
 
-// exclusive rank of a 0/1 flag over the 1024 threads, and the block total
-__device__ __forceinline__ uint32_t rank1024(bool f, uint32_t *s_w, uint32_t &total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t m = __ballot(f);
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    __syncthreads();
-    if (lane == 0) s_w[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int w = 0; w < 16; w++) {
-        const uint32_t c = s_w[w];
-        off += w < wave ? c : 0u;
-        tot += c;
+// Ka: per slice, the pruner classes resolved (a class member takes the fate of its pruner, same
+// vector; the class's first index is its equal-earlier tuple), kept / new-rep counts; and the
+// state reps the batch dominates die (no kept tuple joins a dying rep: its dominator dominates
+// every tuple equal to it), their tuples counted dead
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_count(const PartDesc *__restrict__ descs) {
+    __shared__ uint32_t s_k[kThreads / 64], s_f[kThreads / 64];
+    const PartDesc &d = descs[blockIdx.y];
+    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const uint32_t R0 = d.dcnt[0];
+    {
+        uint32_t killed = 0;
+        const uint32_t rs = min(R0, d.rb);
+        for (uint32_t r = blockIdx.x * kThreads + threadIdx.x; r < rs; r += gridDim.x * kThreads)
+            if (d.dom_s[r] && d.ralive[r]) {
+                d.ralive[r] = 0;
+                killed += d.rcnt[r];
+            }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) killed += (uint32_t)__shfl_xor((int)killed, o, 64);
+        if ((threadIdx.x & 63) == 0 && killed) atomicAdd(&d.meta[2 + 2 * kPartPruners], killed);
     }
-    total = tot;
-    return off + (uint32_t)__popcll(m & lt);
+    if (s0 >= nb) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t db[kSliceIt], es[kSliceIt], eb[kSliceIt], cp[kSliceIt];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = min(s0 + k * kThreads + threadIdx.x, nb - 1u);
+        db[k] = d.dom_b[b];
+        es[k] = d.eq_s[b];
+        eb[k] = d.eq_b[b];
+        cp[k] = d.eqp[b];
+    }
+    uint32_t nk = 0, nf = 0;
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = s0 + k * kThreads + threadIdx.x;
+        if (b >= nb) continue;
+        if (cp[k] != 0xffffffffu) {
+            const uint32_t r = d.meta[1 + cp[k]], fe = d.meta[1 + kPartPruners + cp[k]];
+            if (b != r) {
+                db[k] = d.dom_b[r];
+                es[k] = d.eq_s[r];
+                d.dom_b[b] = db[k];
+                d.eq_s[b] = es[k];
+            }
+            eb[k] = fe < b ? fe : 0xffffffffu;
+            d.eq_b[b] = eb[k];
+        }
+        const bool keep = db[k] == 0u;
+        nk += keep ? 1u : 0u;
+        nf += keep && es[k] == 0xffffffffu && eb[k] == 0xffffffffu ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        nk += (uint32_t)__shfl_xor((int)nk, o, 64);
+        nf += (uint32_t)__shfl_xor((int)nf, o, 64);
+    }
+    if (lane == 0) {
+        s_k[wave] = nk;
+        s_f[wave] = nf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tk = 0, tf = 0;
+        for (int w = 0; w < kThreads / 64; w++) {
+            tk += s_k[w];
+            tf += s_f[w];
+        }
+        d.sl_k[blockIdx.x] = tk;
+        d.sl_k[blockIdx.x + ((nb + kPartSlice - 1) / kPartSlice)] = tf;
+    }
 }
 
-// one workgroup per part: kept batch tuples appended (insertion order), new reps appended,
-// tuples joining an existing rep counted, dominated reps killed; the new counts to the device
-// and to the host mirror
+// Kb: positions (the slices before this one, then ballots) of the kept tuples and the new reps;
+// the new reps' rows appended
 template <int D>
-__global__ __launch_bounds__(1024) void k_parts_commit(const PartDesc *__restrict__ descs) {
-    __shared__ uint32_t s_w[16];
-    __shared__ unsigned long long s_dead;
-    const PartDesc &d = descs[blockIdx.x];
-    const uint32_t R0 = d.dcnt[0], T0 = d.dcnt[1];
-    const uint32_t nb = d.nb;
-    if (threadIdx.x == 0) s_dead = 0;
-    // the members of a pruner class take the fate of its pruner (same vector); the class's
-    // first index is their first equal batch tuple
-    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
-        const uint32_t c = d.eqp[b];
-        if (c == 0xffffffffu) continue;
-        const uint32_t r = d.meta[1 + c], fe = d.meta[1 + kPartPruners + c];
-        if (b != r) {
-            d.dom_b[b] = d.dom_b[r];
-            d.eq_s[b] = d.eq_s[r];
-        }
-        d.eq_b[b] = fe < b ? fe : 0xffffffffu;
+__global__ __launch_bounds__(kThreads) void k_parts_place(const PartDesc *__restrict__ descs) {
+    __shared__ uint32_t s_kc[kSliceIt][kThreads / 64], s_fc[kSliceIt][kThreads / 64];
+    const PartDesc &d = descs[blockIdx.y];
+    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    if (s0 >= nb) return;
+    const uint32_t R0 = d.dcnt[0];
+    const uint32_t nsl = (nb + kPartSlice - 1) / kPartSlice;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint32_t ko = 0, fo = 0;
+    for (uint32_t q = 0; q < blockIdx.x; q++) {
+        ko += d.sl_k[q];
+        fo += d.sl_k[nsl + q];
     }
-    __syncthreads();
-    uint32_t kbase = 0, fbase = 0;
-    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
-        const uint32_t b = c0 + threadIdx.x;
-        const bool valid = b < nb;
+    uint64_t km[kSliceIt], fm[kSliceIt];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = min(s0 + k * kThreads + threadIdx.x, nb - 1u);
+        const bool valid = s0 + k * kThreads + threadIdx.x < nb;
         const bool keep = valid && d.dom_b[b] == 0u;
         const bool fresh = keep && d.eq_s[b] == 0xffffffffu && d.eq_b[b] == 0xffffffffu;
-        uint32_t kt, ft;
-        const uint32_t kp = kbase + rank1024(keep, s_w, kt);
-        const uint32_t fp = fbase + rank1024(fresh, s_w, ft);
-        if (valid) {
-            d.kpos[b] = kp;
-            d.fpos[b] = fp;
+        km[k] = __ballot(keep);
+        fm[k] = __ballot(fresh);
+        if (lane == 0) {
+            s_kc[k][wave] = (uint32_t)__popcll(km[k]);
+            s_fc[k][wave] = (uint32_t)__popcll(fm[k]);
         }
-        if (fresh) {
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        uint32_t kw = 0, fw = 0, kt = 0, ft = 0;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; w++) {
+            kw += w < wave ? s_kc[k][w] : 0u;
+            fw += w < wave ? s_fc[k][w] : 0u;
+            kt += s_kc[k][w];
+            ft += s_fc[k][w];
+        }
+        const uint32_t b = s0 + k * kThreads + threadIdx.x;
+        if ((km[k] >> lane) & 1ull) d.kpos[b] = ko + kw + (uint32_t)__popcll(km[k] & lt);
+        if ((fm[k] >> lane) & 1ull) {
+            const uint32_t fp = fo + fw + (uint32_t)__popcll(fm[k] & lt);
+            d.fpos[b] = fp;
             const uint32_t r = R0 + fp;
 #pragma unroll
             for (int q = 0; q < D; q++) d.rrows[(size_t)r * D + q] = d.bvals[(size_t)b * D + q];
             d.ralive[r] = 1;
             d.rcnt[r] = 0;
         }
-        kbase += kt;
-        fbase += ft;
+        ko += kt;
+        fo += ft;
     }
-    __syncthreads();                           // the new reps and positions are visible
-    for (uint32_t c0 = 0; c0 < nb; c0 += 1024) {
-        const uint32_t b = c0 + threadIdx.x;
-        const bool act = b < nb && d.dom_b[b] == 0u;
+}
+
+// Kc: the kept tuples appended (id, rep) at their positions, the tuples joining a rep counted
+// (duplicate-heavy keys: one atomic per wave); the part's last slice to finish (a ticket)
+// writes the new counts to the device and to the host mirror
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_join(const PartDesc *__restrict__ descs) {
+    __shared__ bool s_last;
+    const PartDesc &d = descs[blockIdx.y];
+    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    if (s0 >= nb) return;
+    const uint32_t R0 = d.dcnt[0], T0 = d.dcnt[1];
+    const int lane = threadIdx.x & 63;
+    uint32_t db[kSliceIt], es[kSliceIt], eb[kSliceIt], kp[kSliceIt];
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = min(s0 + k * kThreads + threadIdx.x, nb - 1u);
+        db[k] = s0 + k * kThreads + threadIdx.x < nb ? d.dom_b[b] : 1u;
+        es[k] = d.eq_s[b];
+        eb[k] = d.eq_b[b];
+        kp[k] = d.kpos[b];
+    }
+#pragma unroll
+    for (int k = 0; k < kSliceIt; k++) {
+        const uint32_t b = s0 + k * kThreads + threadIdx.x;
+        const bool act = db[k] == 0u;
         uint32_t rep = 0xffffffffu;
         if (act) {
-            const uint32_t e = d.eq_s[b];
-            rep = e != 0xffffffffu ? e : R0 + d.fpos[d.eq_b[b] != 0xffffffffu ? d.eq_b[b] : b];
-            const uint32_t t = T0 + d.kpos[b];
+            rep = es[k] != 0xffffffffu ? es[k] : R0 + d.fpos[eb[k] != 0xffffffffu ? eb[k] : b];
+            const uint32_t t = T0 + kp[k];
             d.tids[t] = d.bids[b];
             d.trep[t] = rep;
         }
-        // the tuples of a batch mostly join one rep (duplicate-heavy keys): one atomic per wave
         const uint64_t am = __ballot(act);
         if (am) {
             const int leader = __ffsll((unsigned long long)am) - 1;
-            const uint32_t r0 = __shfl(rep, leader, 64);
+            const uint32_t r0 = (uint32_t)__shfl((int)rep, leader, 64);
             const bool uni = __ballot(act && rep != r0) == 0ull;
             if (uni) {
-                if ((int)(threadIdx.x & 63) == leader) atomicAdd(&d.rcnt[r0], (uint32_t)__popcll(am));
+                if (lane == leader) atomicAdd(&d.rcnt[r0], (uint32_t)__popcll(am));
             } else if (act) {
                 atomicAdd(&d.rcnt[rep], 1u);
             }
         }
     }
-    __syncthreads();                           // joins done before the kills read rcnt
-    unsigned long long killed = 0;
-    const uint32_t rs = min(R0, d.rb);
-    for (uint32_t s = threadIdx.x; s < rs; s += 1024) {
-        if (d.dom_s[s] && d.ralive[s]) {
-            d.ralive[s] = 0;
-            killed += d.rcnt[s];
-        }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) killed += __shfl_xor(killed, o, 64);
-    if ((threadIdx.x & 63) == 0 && killed) atomicAdd(&s_dead, killed);
+    // the last slice of the part: every slice has read the old counts by now
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t R1 = R0 + fbase, T1 = T0 + kbase;
-        const unsigned long long dead = ((unsigned long long)d.dcnt[3] << 32 | d.dcnt[2]) + s_dead;
-        d.dcnt[0] = R1;
-        d.dcnt[1] = T1;
-        d.dcnt[2] = (uint32_t)dead;
-        d.dcnt[3] = (uint32_t)(dead >> 32);
-        if (d.mirror) {                        // seqlock: begin, data, end (the host checks begin == end)
-            volatile uint32_t *m = d.mirror;
-            m[0] = d.seq;
-            __threadfence_system();
-            m[1] = R1;
-            m[2] = T1;
-            m[3] = (uint32_t)dead;
-            m[4] = (uint32_t)(dead >> 32);
-            __threadfence_system();
-            m[5] = d.seq;
-        }
+    const uint32_t nsl = (nb + kPartSlice - 1) / kPartSlice;
+    if (threadIdx.x == 0) s_last = atomicAdd(&d.meta[3 + 2 * kPartPruners], 1u) == nsl - 1u;
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    uint32_t tk = 0, tf = 0;
+    for (uint32_t q = 0; q < nsl; q++) {
+        tk += d.sl_k[q];
+        tf += d.sl_k[nsl + q];
+    }
+    const uint32_t R1 = R0 + tf, T1 = T0 + tk;
+    const unsigned long long dead = ((unsigned long long)d.dcnt[3] << 32 | d.dcnt[2]) +
+                                    d.meta[2 + 2 * kPartPruners];
+    d.dcnt[0] = R1;
+    d.dcnt[1] = T1;
+    d.dcnt[2] = (uint32_t)dead;
+    d.dcnt[3] = (uint32_t)(dead >> 32);
+    if (d.mirror) {                        // seqlock: begin, data, end (the host checks begin == end)
+        volatile uint32_t *m = d.mirror;
+        m[0] = d.seq;
+        __threadfence_system();
+        m[1] = R1;
+        m[2] = T1;
+        m[3] = (uint32_t)dead;
+        m[4] = (uint32_t)(dead >> 32);
+        __threadfence_system();
+        m[5] = d.seq;
     }
 }
 
@@ -415,11 +530,83 @@ __global__ __launch_bounds__(kThreads) void k_part_rows_out(uint32_t T, const ui
 // ---- launchers ---------------------------------------------------------------------------
 static inline unsigned nbk(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
-void launch_parts_insert(int D, const PartDesc *descs, int nparts, const PartItem *items, uint32_t nitems,
-                         hipStream_t st) {
-    if (nparts) SKY_DISPATCH_D(D, (k_parts_prune<DD><<<nparts, 1024, 0, st>>>(descs)));
+// ---- the global merge of device-resident per-key states (sky_parts_global_merge) -----------
+// GlobalSkylineAggregator (FlinkSkyline.java:515-569) over the keys' local skylines without
+// moving them through host memory: the alive reps of every part (origin = list index, weight =
+// tuples on the rep) run through the single-partition pipeline; the surviving reps are flagged,
+// and every part's tuples (list order, then insertion order) whose rep survives are written.
+__global__ __launch_bounds__(kThreads) void k_pgm_prep(uint32_t R, const uint32_t *__restrict__ rcnt, int32_t k,
+                                                       int32_t *__restrict__ origin, int64_t *__restrict__ w) {
+    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+    if (r >= R) return;
+    origin[r] = k;
+    w[r] = (int64_t)rcnt[r];
+}
+__global__ __launch_bounds__(kThreads) void k_pgm_flags(uint32_t n, const int64_t *__restrict__ surv_idx,
+                                                        uint8_t *__restrict__ flag) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    flag[surv_idx[i]] = 1;
+}
+// per tuple of the concatenated lists: its rep survives?
+__global__ __launch_bounds__(kThreads) void k_pgm_tflag(const PgmList *__restrict__ lists, int nl, uint32_t ttot,
+                                                        const uint8_t *__restrict__ flag,
+                                                        uint32_t *__restrict__ tsel) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= ttot) return;
+    int lo = 0, hi = nl - 1;                   // the list holding tuple i (toff ascending)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (lists[mid].toff <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const PgmList &L = lists[lo];
+    tsel[i] = flag[L.roff + L.trep[i - L.toff]] ? 1u : 0u;
+}
+__global__ __launch_bounds__(kThreads) void k_pgm_write(const PgmList *__restrict__ lists, int nl, uint32_t ttot,
+                                                        const uint32_t *__restrict__ tsel,
+                                                        const uint32_t *__restrict__ tpos, int64_t *__restrict__ ids_out,
+                                                        int32_t *__restrict__ org_out) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= ttot || !tsel[i]) return;
+    int lo = 0, hi = nl - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (lists[mid].toff <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const PgmList &L = lists[lo];
+    const uint32_t o = tpos[i];
+    ids_out[o] = L.tids[i - L.toff];
+    org_out[o] = L.part_id;
+}
+
+void launch_pgm_prep(uint32_t R, const uint32_t *rcnt, int32_t k, int32_t *origin, int64_t *w, hipStream_t st) {
+    if (R) k_pgm_prep<<<(R + kThreads - 1) / kThreads, kThreads, 0, st>>>(R, rcnt, k, origin, w);
+}
+void launch_pgm_flags(uint32_t n, const int64_t *surv_idx, uint8_t *flag, hipStream_t st) {
+    if (n) k_pgm_flags<<<(n + kThreads - 1) / kThreads, kThreads, 0, st>>>(n, surv_idx, flag);
+}
+void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_t *flag, uint32_t *tsel,
+                       uint32_t *tpos, uint32_t *d_total, uint32_t *scratch, int64_t *ids_out, int32_t *org_out,
+                       hipStream_t st) {
+    if (!ttot) return;
+    const unsigned g = (ttot + kThreads - 1) / kThreads;
+    k_pgm_tflag<<<g, kThreads, 0, st>>>(lists, nl, ttot, flag, tsel);
+    scan_excl_u32(tsel, tpos, ttot, d_total, scratch, st);
+    k_pgm_write<<<g, kThreads, 0, st>>>(lists, nl, ttot, tsel, tpos, ids_out, org_out);
+}
+
+void launch_parts_insert(int D, const PartDesc *descs, int nparts, uint32_t max_slices, const PartItem *items,
+                         uint32_t nitems, hipStream_t st) {
+    if (!nparts || !max_slices) return;
+    const dim3 g(max_slices, (unsigned)nparts);
+    SKY_DISPATCH_D(D, (k_parts_crit<DD><<<g, kThreads, 0, st>>>(descs)));
+    SKY_DISPATCH_D(D, (k_parts_classify<DD><<<g, kThreads, 0, st>>>(descs)));
     if (nitems) SKY_DISPATCH_D(D, (k_parts_pairs<DD><<<nitems, kThreads, 0, st>>>(descs, items)));
-    if (nparts) SKY_DISPATCH_D(D, (k_parts_commit<DD><<<nparts, 1024, 0, st>>>(descs)));
+    SKY_DISPATCH_D(D, (k_parts_count<DD><<<g, kThreads, 0, st>>>(descs)));
+    SKY_DISPATCH_D(D, (k_parts_place<DD><<<g, kThreads, 0, st>>>(descs)));
+    SKY_DISPATCH_D(D, (k_parts_join<DD><<<g, kThreads, 0, st>>>(descs)));
 }
 
 void launch_part_rkeep(uint32_t R, const uint8_t *ralive, uint32_t *keep, hipStream_t st) {

@@ -11,14 +11,135 @@
 #include "abi_common.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 namespace {
 
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// ---- the staging pool: a call's batches copied into pinned memory (and checked for NaN) by the
+// caller plus a few persistent threads
+struct StageChunk {
+    const int64_t *ids;
+    const double *vals;
+    int64_t *ids_dst;
+    double *vals_dst;
+    size_t n;                 // tuples
+    int part;
+    bool nan;
+};
+constexpr size_t kStageChunkTuples = 2048;
+
+// copy + NaN check on the bits (NaN <=> |bits| > +inf's bits; the wrapping subtraction sets bit
+// 63 exactly then): a loop the compiler vectorises
+void stage_one(StageChunk &k, int D) {
+    memcpy(k.ids_dst, k.ids, k.n * 8);
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(k.vals);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(k.vals_dst);
+    uint64_t acc = 0;
+    const size_t nq = k.n * (size_t)D;
+    for (size_t q = 0; q < nq; q++) {
+        const uint64_t u = src[q];
+        dst[q] = u;
+        acc |= 0x7ff0000000000000ull - (u & 0x7fffffffffffffffull);
+    }
+    k.nan = (acc >> 63) != 0;
+}
+
+class StagePool {
+  public:
+    static StagePool &get() {
+        static StagePool pool;
+        return pool;
+    }
+    // f(i) for every i < n, on the pool's threads and the caller; returns when all are done
+    void run(size_t n, const std::function<void(size_t)> &f) {
+        if (workers_.empty() || n < 2) {
+            for (size_t i = 0; i < n; i++) f(i);
+            return;
+        }
+        std::unique_lock<std::mutex> call(call_m_);          // one job at a time
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &f;
+            n_ = n;
+            next_.store(0);
+            done_.store(0);
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return done_.load() == n_; });
+        fn_ = nullptr;
+    }
+    ~StagePool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread &t : workers_) t.join();
+    }
+
+  private:
+    StagePool() {
+        const char *e = getenv("SKY_STAGE_THREADS");
+        int nt = e ? atoi(e) : 4;
+        const int hw = (int)std::thread::hardware_concurrency();
+        nt = std::max(1, std::min(nt, std::max(1, hw)));
+        for (int i = 0; i < nt - 1; i++) workers_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    void work() {
+        for (;;) {
+            const size_t i = next_.fetch_add(1);
+            if (i >= n_) return;
+            (*fn_)(i);
+            if (done_.fetch_add(1) + 1 == n_) {
+                std::lock_guard<std::mutex> lk(m_);
+                done_cv_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_, call_m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0}, done_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+void stage_chunks(std::vector<StageChunk> &ch, int D) {
+    size_t bytes = 0;
+    for (const StageChunk &k : ch) bytes += k.n * (8 + 8 * (size_t)D);
+    if (bytes < (256u << 10)) {                              // small: not worth a wake-up
+        for (StageChunk &k : ch) stage_one(k, D);
+        return;
+    }
+    StagePool::get().run(ch.size(), [&](size_t i) { stage_one(ch[i], D); });
+}
 
 // the newest consistent counts the commit kernel mirrored (seqlock: end, data, begin)
 void refresh_known(sky_part *p) {
@@ -242,44 +363,70 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
     bool nan = false;
     int nan_part = -1;
     {
+        // staged and checked in one pass, in chunks spread over the staging pool (the caller and
+        // SKY_STAGE_THREADS - 1 persistent threads): one thread copies ~10 GB/s, and a call's
+        // 0.8 MB was most of the host side of the operator path
+        std::vector<StageChunk> ch;
         uint64_t off = 0;
         for (int g = 0; g < np; g++) {
             const size_t nb = (size_t)counts[g];
-            memcpy(h + o_ids + off * 8, ids[g], nb * 8);
-            const double *src = values[g];
-            double *dst = (double *)(h + o_vals) + off * D;
-            bool bad = false;
-            for (size_t q = 0; q < nb * D; q++) {     // staged and checked in one pass
-                const double v = src[q];
-                dst[q] = v;
-                bad |= v != v;
-            }
-            if (bad && !nan) {
-                nan = true;
-                nan_part = g;
+            for (size_t t0 = 0; t0 < nb; t0 += kStageChunkTuples) {
+                const size_t t1 = std::min(nb, t0 + kStageChunkTuples);
+                ch.push_back(StageChunk{ids[g] + t0, values[g] + t0 * D, (int64_t *)(h + o_ids) + off + t0,
+                                        (double *)(h + o_vals) + (off + t0) * D, t1 - t0, g, false});
             }
             off += nb;
         }
+        stage_chunks(ch, D);
+        for (const StageChunk &k : ch)
+            if (k.nan && (!nan || k.part < nan_part)) {
+                nan = true;
+                nan_part = k.part;
+            }
     }
     if (nan) {   // the whole call is rejected before any launch: the states never see the batch
         set_error("a tuple value is NaN (batch of key " + std::to_string(parts[nan_part]->key) +
                   "): the reference BNL result is order-dependent for NaN; batch rejected");
         return SKY_E_NAN;
     }
-    SKY_TRY(c->part_batch.ensure(up_bytes));
+    // double-buffered upload target: this call's copy may run while the previous call's kernels
+    // still read the other buffer; a buffer is overwritten only after the kernels that read it
+    if (!c->part_copy_st) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->part_copy_st, hipStreamNonBlocking));
+        for (hipEvent_t &e : c->part_done) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    const int bsel = c->part_buf_next;
+    c->part_buf_next ^= 1;
+    DevBuf &pbuf = c->part_batch[bsel];
+    if (up_bytes > pbuf.cap && c->part_done_rec[bsel]) HIP_TRY(hipEventSynchronize(c->part_done[bsel]));
+    SKY_TRY(pbuf.ensure(up_bytes));
     // work arrays: dom_b | eq_s | eq_b | kpos | fpos | eqp | uidx (per tuple), meta (per part),
     // dom_s (per bounded rep)
     const size_t w_nb = (size_t)ntot * 4;
-    SKY_TRY(c->part_work.ensure(7 * w_nb + (size_t)np * kPartMeta * 4 + (size_t)std::max<uint64_t>(rbtot, 1) * 4 +
-                                64));
-    char *dev = c->part_batch.as<char>();
+    // per-slice words: criterion minima (f64 + index per criterion), kept / new-rep counts
+    uint64_t sltot = 0;
+    uint32_t max_sl = 0;
+    for (int g = 0; g < np; g++) {
+        const uint32_t ns = (uint32_t)(((uint64_t)counts[g] + kPartSlice - 1) / kPartSlice);
+        sltot += ns;
+        max_sl = std::max(max_sl, ns);
+    }
+    const size_t sl_bytes = (size_t)sltot * (kPartPruners * 12 + 8);
+    SKY_TRY(c->part_work.ensure(7 * w_nb + (size_t)np * kPartMeta * 4 + sl_bytes + 16 +
+                                (size_t)std::max<uint64_t>(rbtot, 1) * 4 + 64));
+    char *dev = pbuf.as<char>();
     uint32_t *w = c->part_work.as<uint32_t>();
     uint32_t *w_dom_b = w, *w_eq_s = w + ntot, *w_eq_b = w + 2 * ntot, *w_kpos = w + 3 * ntot, *w_fpos = w + 4 * ntot;
     uint32_t *w_eqp = w + 5 * ntot, *w_uidx = w + 6 * ntot, *w_meta = w + 7 * ntot;
-    uint32_t *w_dom_s = w_meta + (size_t)np * kPartMeta;
+    // the f64 slice minima 8-byte aligned
+    double *w_slv = reinterpret_cast<double *>(
+        (reinterpret_cast<uintptr_t>(w_meta + (size_t)np * kPartMeta) + 7) & ~uintptr_t(7));
+    uint32_t *w_sli = reinterpret_cast<uint32_t *>(w_slv + (size_t)sltot * kPartPruners);
+    uint32_t *w_slk = w_sli + (size_t)sltot * kPartPruners;
+    uint32_t *w_dom_s = w_slk + 2 * (size_t)sltot;
     {
         PartDesc *ds = (PartDesc *)(h + o_desc);
-        uint64_t off = 0, roff = 0;
+        uint64_t off = 0, roff = 0, sloff = 0;
         for (int g = 0; g < np; g++) {
             sky_part *p = parts[g];
             PartDesc d{};
@@ -297,6 +444,10 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
             d.eqp = w_eqp + off;
             d.uidx = w_uidx + off;
             d.meta = w_meta + (size_t)g * kPartMeta;
+            d.sl_v = w_slv + (size_t)sloff * kPartPruners;
+            d.sl_i = w_sli + (size_t)sloff * kPartPruners;
+            d.sl_k = w_slk + 2 * (size_t)sloff;
+            sloff += ((uint64_t)nb + kPartSlice - 1) / kPartSlice;
             d.rrows = p->rrows.as<double>();
             d.ralive = p->ralive.as<uint8_t>();
             d.rcnt = p->rcnt.as<uint32_t>();
@@ -314,17 +465,17 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
         }
         if (!items.empty()) memcpy(h + o_items, items.data(), items.size() * sizeof(PartItem));
     }
-    HIP_TRY(hipMemcpyAsync(dev, h, up_bytes, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipEventRecord(sg->ev, st));
+    if (c->part_done_rec[bsel]) HIP_TRY(hipStreamWaitEvent(c->part_copy_st, c->part_done[bsel], 0));
+    HIP_TRY(hipMemcpyAsync(dev, h, up_bytes, hipMemcpyHostToDevice, c->part_copy_st));
+    HIP_TRY(hipEventRecord(sg->ev, c->part_copy_st));
     sg->used = true;
-    FillSet fill;
-    fill.add(w_dom_b, w_nb, 0);
-    fill.add(w_eq_s, 2 * w_nb, 0xff);
-    if (rbtot) fill.add(w_dom_s, (size_t)rbtot * 4, 0);
-    HIP_TRY(fill.launch(st));
-    launch_parts_insert(D, (const PartDesc *)(dev + o_desc), np, (const PartItem *)(dev + o_items),
+    HIP_TRY(hipStreamWaitEvent(st, sg->ev, 0));      // the kernels wait for their upload
+    // (the work arrays are initialised by k_parts_prune: no fill launch)
+    launch_parts_insert(D, (const PartDesc *)(dev + o_desc), np, max_sl, (const PartItem *)(dev + o_items),
                         (uint32_t)items.size(), st);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->part_done[bsel], st));
+    c->part_done_rec[bsel] = true;
     return SKY_OK;
 }
 
@@ -387,6 +538,118 @@ int sky_parts_insert(int nparts, sky_part *const *parts, const int64_t *const *i
     }
     SKY_TRY(bind(parts[0]->ctx));
     return parts_insert(nparts, parts, ids, values, counts);
+    GUARD_END
+}
+
+// GlobalSkylineAggregator (FlinkSkyline.java:515-569) over the keys' device-resident states:
+// the same result and stats as sky_global_merge over the parts' snapshots, without moving the
+// local skylines through host memory (see skyline_hip.h)
+int sky_parts_global_merge(sky_ctx *c, int nparts, sky_part *const *parts, const int32_t *part_ids,
+                           int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && nparts >= 0 && nparts <= SKY_MAX_PARTITIONS, "bad nparts (<= 256 parts)");
+    ARG_CHECK(nparts == 0 || parts, "null parts");
+    for (int g = 0; g < nparts; g++) {
+        ARG_CHECK(parts[g] && parts[g]->ctx == c, "every part must belong to this context");
+        for (int h = 0; h < g; h++) ARG_CHECK(parts[h] != parts[g], "a part appears twice");
+    }
+    SKY_TRY(bind(c));
+    hipStream_t st = c->st;
+    const int D = c->D;
+    // exact counts; dead reps and their tuples dropped (insertion order kept)
+    std::vector<uint32_t> R(nparts), T(nparts);
+    uint64_t rtot = 0, ttot = 0;
+    for (int g = 0; g < nparts; g++) {
+        sky_part *p = parts[g];
+        SKY_TRY(part_sync(p));
+        if (p->dead_known) SKY_TRY(part_compact(p));
+        R[g] = (uint32_t)p->R_known;
+        T[g] = (uint32_t)p->T_known;
+        rtot += R[g];
+        ttot += T[g];
+    }
+    ARG_CHECK(rtot < 0x7fffffffull && ttot < 0x7fffffffull, "too many tuples");
+    const size_t rr = (size_t)std::max<uint64_t>(rtot, 1), tt = (size_t)std::max<uint64_t>(ttot, 1);
+    SKY_TRY(c->h_vals.ensure(rr * D * 8));
+    SKY_TRY(c->h_origin.ensure(rr * 4));
+    SKY_TRY(c->pgm_w.ensure(rr * 8));
+    SKY_TRY(c->pgm_surv.ensure(rr * 8));
+    SKY_TRY(c->pgm_sorg.ensure(rr * 4));
+    SKY_TRY(c->pgm_flag.ensure(rr));
+    // the alive reps of every part as one single-partition run (origin = list, weight = tuples)
+    uint64_t off = 0;
+    for (int g = 0; g < nparts; g++) {
+        if (!R[g]) continue;
+        HIP_TRY(hipMemcpyAsync(c->h_vals.as<double>() + off * D, parts[g]->rrows.p, (size_t)R[g] * D * 8,
+                               hipMemcpyDeviceToDevice, st));
+        launch_pgm_prep(R[g], parts[g]->rcnt.as<uint32_t>(), g, c->h_origin.as<int32_t>() + off,
+                        c->pgm_w.as<int64_t>() + off, st);
+        off += R[g];
+    }
+    HIP_TRY(hipGetLastError());
+    PipeIn in;
+    in.vals = c->h_vals.as<double>();
+    in.n = (uint32_t)rtot;
+    in.ids = nullptr;                           // the rep's index in the concatenation
+    in.origin = c->h_origin.as<int32_t>();
+    in.weights = c->pgm_w.as<int64_t>();
+    in.single = true;
+    in.global = false;
+    in.K = std::max(nparts, 1);
+    c->shard_valid = false;
+    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
+    // GlobalSkylineAggregator: localSkylineSizes[k] = incoming list size (:544); survivors by
+    // originPartition (:593-596), weighted by the tuples on each rep
+    c->K_last = nparts;
+    c->lsz.assign(nparts, 0);
+    c->surv.assign(nparts, 0);
+    uint64_t gtot = 0;
+    for (int g = 0; g < nparts; g++) {
+        c->lsz[g] = T[g];
+        c->surv[g] = (int64_t)c->main.h_lsz[g];
+        gtot += (uint64_t)c->main.h_lsz[g];
+    }
+    if (n_out) *n_out = (int64_t)gtot;
+    if ((int64_t)gtot > cap && (ids_out || origin_out)) {
+        set_error("output capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    const uint32_t greps = (uint32_t)c->main.nout;
+    int64_t gr = 0;
+    SKY_TRY(pipe_output(*c, c->main, in, false, c->pgm_surv.as<int64_t>(), c->pgm_sorg.as<int32_t>(), nullptr,
+                        (int64_t)rr, &gr, nullptr));
+    HIP_TRY(hipMemsetAsync(c->pgm_flag.p, 0, rr, st));
+    launch_pgm_flags(greps, c->pgm_surv.as<int64_t>(), c->pgm_flag.as<uint8_t>(), st);
+    // every list's tuples whose rep survives, list order then insertion order
+    std::vector<PgmList> lists((size_t)std::max(nparts, 1));
+    uint64_t toff = 0, roff = 0;
+    for (int g = 0; g < nparts; g++) {
+        PgmList &L = lists[g];
+        L.tids = parts[g]->tids.as<int64_t>();
+        L.trep = parts[g]->trep.as<uint32_t>();
+        L.toff = (uint32_t)toff;
+        L.roff = (uint32_t)roff;
+        L.part_id = part_ids ? part_ids[g] : g;
+        L.pad = 0;
+        toff += T[g];
+        roff += R[g];
+    }
+    SKY_TRY(c->pgm_lists.ensure(lists.size() * sizeof(PgmList)));
+    SKY_TRY(c->pgm_tsel.ensure(tt * 4));
+    SKY_TRY(c->pgm_tpos.ensure(tt * 4 + 64));
+    SKY_TRY(c->pgm_scr.ensure(scan_scratch_words(tt) * 4 + 64));
+    SKY_TRY(c->pgm_ids.ensure((size_t)std::max<uint64_t>(gtot, 1) * 8));
+    SKY_TRY(c->pgm_org.ensure((size_t)std::max<uint64_t>(gtot, 1) * 4));
+    HIP_TRY(hipMemcpyAsync(c->pgm_lists.p, lists.data(), lists.size() * sizeof(PgmList), hipMemcpyHostToDevice, st));
+    launch_pgm_tuples(c->pgm_lists.as<PgmList>(), nparts, (uint32_t)ttot, c->pgm_flag.as<uint8_t>(),
+                      c->pgm_tsel.as<uint32_t>(), c->pgm_tpos.as<uint32_t>(), c->pgm_tpos.as<uint32_t>() + tt,
+                      c->pgm_scr.as<uint32_t>(), c->pgm_ids.as<int64_t>(), c->pgm_org.as<int32_t>(), st);
+    HIP_TRY(hipGetLastError());
+    if (gtot && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->pgm_ids.p, gtot * 8, hipMemcpyDeviceToHost, st));
+    if (gtot && origin_out) HIP_TRY(hipMemcpyAsync(origin_out, c->pgm_org.p, gtot * 4, hipMemcpyDeviceToHost, st));
+    c->host_syncs++;
+    HIP_TRY(hipStreamSynchronize(st));
+    return SKY_OK;
     GUARD_END
 }
 

@@ -274,6 +274,8 @@ void launch_move16(int W, const uint32_t *keep, const uint32_t *scan, uint32_t n
 void launch_gather_u32(const uint32_t *src, const uint32_t *at, uint32_t n, uint32_t *out, hipStream_t st);
 
 // ---- k_mbr.hip (both skyline levels of a large rep set, bounding-box pruned all-pairs) ----
+constexpr int kMbrLptHead = 64;   // head words of MbrArgs::lpt
+inline size_t mbr_lpt_words(size_t ytiles) { return kMbrLptHead + 2 * ytiles; }
 struct MbrArgs {
     int D = 0;
     int fmt = 0;                  // 0: packed u16 rows (dom16 layout), 1: f32 rows, 2: f64 rows
@@ -298,6 +300,10 @@ struct MbrArgs {
     uint32_t *gprange = nullptr;  // [ngroups]: their partition ranges
     uint32_t *domf = nullptr;     // [mr], zeroed by the caller
     unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
+    // the y tiles' work queue (k_mbr_cost / k_mbr_order): [kMbrLptHead] words zeroed by the
+    // caller (bucket counts, the ticket), then a cost and an order word per y tile; nullptr:
+    // the y tiles go in blockIdx order
+    uint32_t *lpt = nullptr;
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
 };
 // the multi-GPU merge: own rows (y, a contiguous range of the union) against the whole union
@@ -322,11 +328,14 @@ struct PartDesc {
     const int64_t *bids;          // [nb]
     uint32_t nb;
     uint32_t rb;                  // bound of the state's rep count (launch sizes; the device count decides)
-    uint32_t *dom_b, *eq_s, *eq_b, *kpos, *fpos;   // [nb] work (dom_b 0, eq_* ~0 on entry)
-    uint32_t *dom_s;              // [rb] work (0 on entry)
+    uint32_t *dom_b, *eq_s, *eq_b, *kpos, *fpos;   // [nb] work (dom_b, eq_* initialised by k_parts_prune)
+    uint32_t *dom_s;              // [rb] work (zeroed by k_parts_prune)
     uint32_t *eqp;                // [nb] pruner class of the tuple (~0: none), written by k_parts_prune
     uint32_t *uidx;               // [nb] the undecided tuples (batch indices), written by k_parts_prune
-    uint32_t *meta;               // [16] |U|, pruner index per class, first index per class (k_parts_prune)
+    uint32_t *meta;               // [kPartMeta] |U|, pruner index / first index per class, killed, ticket
+    double *sl_v;                 // [slices][kPartPruners] per slice: criterion minima (k_parts_crit)
+    uint32_t *sl_i;               // [slices][kPartPruners] ... and their indices
+    uint32_t *sl_k;               // [2][slices] per slice: kept tuples, new reps (k_parts_count)
     double *rrows;                // state: reps [R][D], alive, tuples per rep
     uint8_t *ralive;
     uint32_t *rcnt;
@@ -341,11 +350,26 @@ struct PartItem {
     uint32_t mode;                // 0: batch vs batch, 1: batch vs state reps, 2: state reps vs batch
     uint32_t y0, x0;              // 256 y rows from y0, kPartChunk x rows from x0
 };
+// one key's tuples in sky_parts_global_merge: ids / rep of its T alive tuples (insertion
+// order), where they start in the concatenation (toff) and its reps (roff), the output origin
+struct PgmList {
+    const int64_t *tids;
+    const uint32_t *trep;
+    uint32_t toff, roff;
+    int32_t part_id;
+    uint32_t pad;
+};
+void launch_pgm_prep(uint32_t R, const uint32_t *rcnt, int32_t k, int32_t *origin, int64_t *w, hipStream_t st);
+void launch_pgm_flags(uint32_t n, const int64_t *surv_idx, uint8_t *flag, hipStream_t st);
+void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_t *flag, uint32_t *tsel,
+                       uint32_t *tpos, uint32_t *d_total, uint32_t *scratch, int64_t *ids_out, int32_t *org_out,
+                       hipStream_t st);
 constexpr uint32_t kPartItemY = 256, kPartItemX = 256;
-constexpr int kPartPruners = 4;   // batch pruners per insert (k_parts_prune)
+constexpr int kPartPruners = 4;   // batch pruners per insert (k_parts_crit / k_parts_classify)
 constexpr int kPartMeta = 16;     // words of PartDesc::meta
-void launch_parts_insert(int D, const PartDesc *descs, int nparts, const PartItem *items, uint32_t nitems,
-                         hipStream_t st);
+constexpr uint32_t kPartSlice = 1024;   // batch tuples per workgroup of the insert kernels
+void launch_parts_insert(int D, const PartDesc *descs, int nparts, uint32_t max_slices, const PartItem *items,
+                         uint32_t nitems, hipStream_t st);
 void launch_part_rkeep(uint32_t R, const uint8_t *ralive, uint32_t *keep, hipStream_t st);
 void launch_part_rmove(int D, uint32_t R, const uint32_t *keep, const uint32_t *pos, const double *rows,
                        const uint32_t *cnt, double *rows2, uint32_t *cnt2, uint8_t *alive2, hipStream_t st);

@@ -70,6 +70,7 @@ SIGNATURES = {
     "sky_part_size": [c_p, P_i64],
     "sky_part_snapshot": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_global_merge": [c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, P_i64],
+    "sky_parts_global_merge": [c_p, c_int, c_p, c_p, c_p, c_p, c_i64, P_i64],
     "sky_global_stats": [c_p, c_p, c_p, P_i32],
     "sky_global_stats_set": [c_p, c_i32, c_p, c_p],
     "sky_query": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64],

@@ -209,6 +209,23 @@ class _LocalPart:
         cnt = np.array([len(a) for a in ids], np.int64)
         check(lib().sky_parts_insert(n, ph, ip, vp, cnt.ctypes.data_as(ctypes.c_void_p)))
 
+    @staticmethod
+    def global_merge_many(engine, parts, part_ids=None):
+        """sky_parts_global_merge: GlobalSkylineAggregator over the parts' device-resident local
+        skylines (no snapshot through host memory) -> (ids, origins), part order then insertion
+        order; engine.stats() then holds |L_k| / survivors_k as after engine.global_merge."""
+        n = len(parts)
+        ph = (ctypes.c_void_p * max(n, 1))(*[p.h.value for p in parts])
+        pids = np.ascontiguousarray(part_ids if part_ids is not None else np.arange(n), np.int32)
+        g = sum(p.size() for p in parts)          # a bound: every part's local skyline
+        out_ids = np.empty(max(g, 1), np.int64)
+        out_org = np.empty(max(g, 1), np.int32)
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_parts_global_merge(engine.h, n, ph, pids.ctypes.data_as(ctypes.c_void_p),
+                                           out_ids.ctypes.data_as(ctypes.c_void_p),
+                                           out_org.ctypes.data_as(ctypes.c_void_p), g, ctypes.byref(cnt)))
+        return out_ids[:cnt.value].copy(), out_org[:cnt.value].copy()
+
     def size(self):
         n = ctypes.c_int64(0)
         check(lib().sky_part_size(self.h, ctypes.byref(n)))

@@ -140,6 +140,12 @@ int sky_global_merge(sky_ctx *ctx, int nparts, const int32_t *part_ids,
                      const int64_t *const *ids, const double *const *values,
                      const int64_t *counts, int64_t *ids_out, int32_t *origin_out,
                      int64_t cap, int64_t *n_out);
+/* the same merge over the keys' device-resident states (no snapshot through host memory): the
+ * result, its order (part order, then insertion order), origin_out (= part_ids[k], or k when
+ * part_ids is NULL) and sky_global_stats equal sky_global_merge over the parts' snapshots.
+ * For an aggregator co-located with the local processors (one process drives the device). */
+int sky_parts_global_merge(sky_ctx *ctx, int nparts, sky_part *const *parts, const int32_t *part_ids,
+                           int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
 /* integers behind the optimality metric of the last merge / query:
  * local_sizes[k] = |L_k|, survivors[k] = |G n L_k| for k < K
  * (K = P, or max(P, 2^D) for MR-Grid with SKY_SEM_COMPLETE). */

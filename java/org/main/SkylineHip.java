@@ -47,6 +47,9 @@ public final class SkylineHip {
     public static native long partSize(long part);
     public static native int partSnapshot(long part, long[] idsOut, double[] valuesOut);
 
+    /** GlobalSkylineAggregator over the parts' device-resident states (co-located aggregator):
+     *  the skyline size, or -(needed) when idsOut is too short. */
+    public static native int partsGlobalMerge(long ctx, long[] parts, int[] partIds, long[] idsOut, int[] originOut);
     public static native int globalMerge(long ctx, int[] partIds, long[][] ids, double[][] values,
                                          long[] idsOut, int[] originOut);
     public static native int globalStats(long ctx, long[] localSizes, long[] survivors);

@@ -222,6 +222,46 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partSnapshot(JNIEnv *env, jclass
 }
 
 /* ---- global merge: GlobalSkylineAggregator.processElement (:515-569), on the last arrival ---- */
+/* the co-located aggregator's merge over the parts' device-resident states (no snapshot through
+ * the JVM heap); returns the skyline size, or -(needed) when idsOut is too short */
+JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partsGlobalMerge(JNIEnv *env, jclass cls, jlong ctx, jlongArray parts,
+                                                                  jintArray part_ids, jlongArray ids_out,
+                                                                  jintArray origin_out) {
+    (void)cls;
+    if (!parts || !part_ids || !ids_out || !origin_out) {
+        throw_arg(env, "partsGlobalMerge: null array");
+        return 0;
+    }
+    const jsize np = (*env)->GetArrayLength(env, parts);
+    if (bad_len(env, part_ids, np, "partsGlobalMerge: partIds shorter than parts")) return 0;
+    const jsize cap = (*env)->GetArrayLength(env, ids_out);
+    if (bad_len(env, origin_out, cap, "partsGlobalMerge: originOut shorter than idsOut")) return 0;
+    jlong *ph = (*env)->GetLongArrayElements(env, parts, NULL);
+    jint *pk = (*env)->GetIntArrayElements(env, part_ids, NULL);
+    jlong *oi = (*env)->GetLongArrayElements(env, ids_out, NULL);
+    jint *oo = (*env)->GetIntArrayElements(env, origin_out, NULL);
+    jint g = 0;
+    if (ph && pk && oi && oo) {
+        sky_part **pp = calloc(np ? np : 1, sizeof(sky_part *));
+        if (!pp) {
+            (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/OutOfMemoryError"), "partsGlobalMerge");
+        } else {
+            for (jsize k = 0; k < np; k++) pp[k] = PART(ph[k]);
+            int64_t n = 0;
+            const int rc = sky_parts_global_merge(CTX(ctx), np, pp, (const int32_t *)pk, (int64_t *)oi,
+                                                  (int32_t *)oo, cap, &n);
+            if (rc == SKY_E_CAPACITY) g = (jint)-n;
+            else if (!fail(env, rc)) g = (jint)n;
+            free(pp);
+        }
+    }
+    if (oo) (*env)->ReleaseIntArrayElements(env, origin_out, oo, 0);
+    if (oi) (*env)->ReleaseLongArrayElements(env, ids_out, oi, 0);
+    if (pk) (*env)->ReleaseIntArrayElements(env, part_ids, pk, JNI_ABORT);
+    if (ph) (*env)->ReleaseLongArrayElements(env, parts, ph, JNI_ABORT);
+    return g;
+}
+
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalMerge(JNIEnv *env, jclass cls, jlong ctx, jintArray part_ids,
                                                              jobjectArray ids, jobjectArray values,
                                                              jlongArray ids_out, jintArray origin_out) {

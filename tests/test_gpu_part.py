@@ -203,3 +203,37 @@ def test_parts_insert_nan_rejects_the_whole_call(gpu_engine_factory, oracle):
     p0.close()
     p1.close()
     eng.close()
+
+
+@pytest.mark.parametrize("dist,D,n", [(2, 8, 80000), (3, 4, 40000), (0, 3, 30000)])
+def test_parts_global_merge_equals_snapshot_merge(dist, D, n, gpu_engine_factory, oracle):
+    """sky_parts_global_merge over device-resident states == sky_global_merge over their
+    snapshots (ids, origins, order, |L_k|, survivors_k), and == the oracle's two-level skyline."""
+    from skyline.operators import _LocalPart
+    P = 8
+    eng = gpu_engine_factory(D, P)
+    vals = oracle.synth(dist, D, n, seed=90 + D)
+    vals[5::101] = vals[7]                          # the same vector in several keys
+    ids = np.arange(n, dtype=np.int64) * 5 + 3
+    keys = eng.partition_keys(vals)
+    parts = {k: _LocalPart(eng, k) for k in range(P)}
+    for k in range(P):
+        sel = np.nonzero(keys == k)[0]
+        for s0 in range(0, len(sel), 5000):
+            parts[k].insert(ids[sel[s0:s0 + 5000]], vals[sel[s0:s0 + 5000]])
+    order = [3, 0, 7, 1, 5, 2, 6, 4]                # any list order: the output follows it
+    plist = [parts[k] for k in order]
+    g_ids, g_org = _LocalPart.global_merge_many(eng, plist, order)
+    ls_dev, sv_dev = eng.stats()
+    snaps = [p.snapshot() for p in plist]
+    e_ids, e_org = eng.global_merge(order, [s[0] for s in snaps], [s[1] for s in snaps])
+    ls_ref, sv_ref = eng.stats()
+    np.testing.assert_array_equal(g_ids, e_ids)
+    np.testing.assert_array_equal(g_org, e_org)
+    np.testing.assert_array_equal(ls_dev, ls_ref)
+    np.testing.assert_array_equal(sv_dev, sv_ref)
+    exp, _, _, _ = oracle.query_bnl("angle", vals, ids, P)
+    assert sorted(g_ids.tolist()) == sorted(exp.tolist())
+    for p in parts.values():
+        p.close()
+    eng.close()

@@ -15,7 +15,7 @@ export PYTHONUNBUFFERED=1
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 if [[ $STEPS == *funnel* ]]; then
   # the bounding-box scan's funnel (groups / tiles passing / listed / tested / pair tests)
-  for V in "SKY_MBR_ORDER=hilbert" "SKY_MBR_ORDER=morton" "SKY_MBR_PIPE=0" "SKY_MBR_ORDER=morton SKY_MBR_PIPE=0"; do
+  for V in ${FUNNEL_KNOBS:-"SKY_MBR_ORDER=hilbert" "SKY_MBR_ORDER=morton"}; do
     T=$(echo $V | tr ' =' '__')
     env $V SKY_MBR_DBG=4 timeout -k 10 200 python -u tools/dom_bench.py ${MBR_N:-2000000} 3 > $OUT/funnel_${TAG}_$T.log 2>&1 || { tail -30 $OUT/funnel_${TAG}_$T.log; exit 1; }
     echo "$V"; grep -v "^\[mbr\]" $OUT/funnel_${TAG}_$T.log; grep "^\[mbr\]" $OUT/funnel_${TAG}_$T.log | tail -1
@@ -40,11 +40,11 @@ if [[ $STEPS == *parts* ]]; then
       > $OUT/pytest_parts_$TAG.log 2>&1 || { tail -60 $OUT/pytest_parts_$TAG.log; exit 1; }
   tail -4 $OUT/pytest_parts_$TAG.log
 fi
-if [[ $STEPS == *tests* ]]; then
+if [[ ,$STEPS, == *,tests,* ]]; then
   timeout -k 10 1000 $PYT tests -m gpu ${TEST_EXTRA} > $OUT/pytest_gpu_$TAG.log 2>&1 || { tail -60 $OUT/pytest_gpu_$TAG.log; exit 1; }
   tail -4 $OUT/pytest_gpu_$TAG.log
 fi
-if [[ $STEPS == *bench* ]]; then
+if [[ ,$STEPS, == *,bench,* ]]; then
   timeout -k 10 500 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
   cut -c1-1500 $OUT/bench_$TAG.json
 fi
@@ -89,4 +89,18 @@ if [[ $STEPS == *c5bench* ]]; then
 import json; d=json.load(open('$OUT/c5_$TAG.json'))
 for k in ('landmark','sliding_10M'):
     x=d[k]; print(k, 'p50', round(x['p50_query_latency_ms'],3), 'p90', round(x['p90_query_latency_ms'],3), 'max', round(x['max_query_latency_ms'],3), x['latencies_ms'])"
+fi
+if [[ $STEPS == *mbrtests* ]]; then
+  timeout -k 10 600 $PYT tests/test_gpu_mbr.py tests/test_gpu_dist_step.py > $OUT/pytest_mbr_$TAG.log 2>&1 || { tail -60 $OUT/pytest_mbr_$TAG.log; exit 1; }
+  tail -3 $OUT/pytest_mbr_$TAG.log
+fi
+if [[ $STEPS == *domab* ]]; then
+  # the dominance companion (std-anti 8D) under the A/B knobs in DOMKNOBS, at each N in DOM_NS
+  for N in ${DOM_NS:-2000000}; do
+    for K in default ${DOMKNOBS}; do
+      env ${K/default/SKY_X=0} timeout -k 10 300 python3 -u tools/dom_bench.py $N 2 > $OUT/domab_${TAG}_${K}_$N.json 2> $OUT/domab_${TAG}_${K}_$N.err \
+          || { tail -20 $OUT/domab_${TAG}_${K}_$N.err; exit 1; }
+      echo "$K N=$N $(cat $OUT/domab_${TAG}_${K}_$N.json)"
+    done
+  done
 fi
