@@ -50,6 +50,12 @@ def test_mbr_generic_rows(force_mbr, gpu_engine_factory, oracle):
     v = rng.integers(-3, 3, size=(20000, 3)).astype(np.float64) * 0.5   # negatives, +-0
     v[v == 0] = np.where(rng.random((v == 0).sum()) < 0.5, -0.0, 0.0)
     cases.append(v)
+    # integer data (the packed-u16 candidate) with -0.0 / +0.0 twins: MR-Angle keys read the sign
+    # bit, so the twins land in different partitions; -0.0 must keep the rows off the u16 path,
+    # whose distinct-vector test would make the twins dominate each other
+    v = rng.integers(0, 6, size=(30000, 4)).astype(np.float64)
+    v[v == 0] = np.where(rng.random((v == 0).sum()) < 0.5, -0.0, 0.0)
+    cases.append(v)
     v = rng.integers(0, 100, size=(20000, 3)).astype(np.float64)
     v[::97, 1] = np.inf
     v[5::89, 2] = -np.inf
