@@ -21,6 +21,10 @@
 // any launch (SKY_E_NAN), so the state never sees it.
 #include "sky_internal.h"
 
+#include <hip/hip_cooperative_groups.h>
+
+#include <algorithm>
+
 namespace sky {
 
 constexpr int kPartX = 128;          // x rows per LDS tile
@@ -74,14 +78,15 @@ __device__ __forceinline__ void vi_min(double &v, uint32_t &i, double ov, uint32
 // K1: per slice, the (criterion, index) minimum of each criterion; slice 0 also resets the
 // part's insert words (|U|, first indices, killed tuples, tickets)
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_crit(const PartDesc *__restrict__ descs) {
+__device__ __forceinline__ void parts_crit(const PartDesc *__restrict__ descs, uint32_t slice, uint32_t part,
+                                               uint32_t nsl_grid) {
     __shared__ double s_bv[kThreads / 64][kPartPruners];
     __shared__ uint32_t s_bi[kThreads / 64][kPartPruners];
-    const PartDesc &d = descs[blockIdx.y];
-    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const PartDesc &d = descs[part];
+    const uint32_t nb = d.nb, s0 = slice * kPartSlice;
     if (s0 >= nb) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (blockIdx.x == 0 && threadIdx.x < kPartMeta) d.meta[threadIdx.x] = threadIdx.x >= 1 + kPartPruners &&
+    if (slice == 0 && threadIdx.x < kPartMeta) d.meta[threadIdx.x] = threadIdx.x >= 1 + kPartPruners &&
                                                                           threadIdx.x < 1 + 2 * kPartPruners
                                                                           ? 0xffffffffu : 0u;
     double rv[kSliceIt][D];
@@ -121,21 +126,26 @@ __global__ __launch_bounds__(kThreads) void k_parts_crit(const PartDesc *__restr
         double v = s_bv[0][c];
         uint32_t i = s_bi[0][c];
         for (int w = 1; w < kThreads / 64; w++) vi_min(v, i, s_bv[w][c], s_bi[w][c]);
-        d.sl_v[blockIdx.x * kPartPruners + c] = v;
-        d.sl_i[blockIdx.x * kPartPruners + c] = i;
+        d.sl_v[slice * kPartPruners + c] = v;
+        d.sl_i[slice * kPartPruners + c] = i;
     }
+}
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_crit(const PartDesc *__restrict__ descs) {
+    parts_crit<D>(descs, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // K2: the pruners (the minima over the part's slices, reduced by every workgroup itself), then
 // each tuple of the slice classified: dropped / pruner class / undecided (appended to U)
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__restrict__ descs) {
+__device__ __forceinline__ void parts_classify(const PartDesc *__restrict__ descs, uint32_t slice, uint32_t part,
+                                               uint32_t nsl_grid) {
     __shared__ double s_pr[kPartPruners][D];
     __shared__ uint32_t s_pi[kPartPruners], s_fe[kPartPruners];
-    const PartDesc &d = descs[blockIdx.y];
-    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const PartDesc &d = descs[part];
+    const uint32_t nb = d.nb, s0 = slice * kPartSlice;
     // the insert's dom_s (per bounded rep) starts here, spread over the part's workgroups
-    for (uint32_t r = blockIdx.x * kThreads + threadIdx.x; r < d.rb; r += gridDim.x * kThreads) d.dom_s[r] = 0u;
+    for (uint32_t r = slice * kThreads + threadIdx.x; r < d.rb; r += nsl_grid * kThreads) d.dom_s[r] = 0u;
     if (s0 >= nb) return;
     const int lane = threadIdx.x & 63;
     const uint32_t nsl = (nb + kPartSlice - 1) / kPartSlice;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__r
         for (uint32_t q = 0; q < nsl; q++) vi_min(v, i, d.sl_v[q * kPartPruners + c], d.sl_i[q * kPartPruners + c]);
         s_pi[c] = i;
         s_fe[c] = 0xffffffffu;
-        if (blockIdx.x == 0) d.meta[1 + c] = i;
+        if (slice == 0) d.meta[1 + c] = i;
     }
     __syncthreads();
     if (threadIdx.x < kPartPruners * D) {
@@ -203,6 +213,10 @@ __global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__r
     if (threadIdx.x < kPartPruners && s_fe[threadIdx.x] != 0xffffffffu)
         atomicMin(&d.meta[1 + kPartPruners + threadIdx.x], s_fe[threadIdx.x]);
 }
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__restrict__ descs) {
+    parts_classify<D>(descs, blockIdx.x, blockIdx.y, gridDim.x);
+}
 
 // dominance as ServiceTuple.dominates (ServiceTuple.java:67-77): <= everywhere, < somewhere
 // mode 0: undecided y vs undecided x (dom_b, eq_b: first EARLIER equal batch tuple)
@@ -211,11 +225,11 @@ __global__ __launch_bounds__(kThreads) void k_parts_classify(const PartDesc *__r
 // Launch sizes come from the batch size (a bound of |U|, which lives on the device): work items
 // past |U| return at once.
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__restrict__ descs,
-                                                          const PartItem *__restrict__ items) {
+__device__ __forceinline__ void parts_pairs(const PartDesc *__restrict__ descs, const PartItem *__restrict__ items,
+                                            uint32_t item) {
     __shared__ double s_x[kPartX * D];
     __shared__ uint32_t s_xi[kPartX];
-    const PartItem it = items[blockIdx.x];
+    const PartItem it = items[item];
     const PartDesc &d = descs[it.part];
     const uint32_t R0 = d.dcnt[0];
     const uint32_t nu = min(d.meta[0], d.nb);
@@ -270,21 +284,27 @@ __global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__rest
     if (dm) d.dom_b[j] = 1u;
     if (emin != 0xffffffffu) atomicMin(mode == 0 ? &d.eq_b[j] : &d.eq_s[j], emin);
 }
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_pairs(const PartDesc *__restrict__ descs,
+                                                          const PartItem *__restrict__ items) {
+    parts_pairs<D>(descs, items, blockIdx.x);
+}
 
 // Ka: per slice, the pruner classes resolved (a class member takes the fate of its pruner, same
 // vector; the class's first index is its equal-earlier tuple), kept / new-rep counts; and the
 // state reps the batch dominates die (no kept tuple joins a dying rep: its dominator dominates
 // every tuple equal to it), their tuples counted dead
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_count(const PartDesc *__restrict__ descs) {
+__device__ __forceinline__ void parts_count(const PartDesc *__restrict__ descs, uint32_t slice, uint32_t part,
+                                               uint32_t nsl_grid) {
     __shared__ uint32_t s_k[kThreads / 64], s_f[kThreads / 64];
-    const PartDesc &d = descs[blockIdx.y];
-    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const PartDesc &d = descs[part];
+    const uint32_t nb = d.nb, s0 = slice * kPartSlice;
     const uint32_t R0 = d.dcnt[0];
     {
         uint32_t killed = 0;
         const uint32_t rs = min(R0, d.rb);
-        for (uint32_t r = blockIdx.x * kThreads + threadIdx.x; r < rs; r += gridDim.x * kThreads)
+        for (uint32_t r = slice * kThreads + threadIdx.x; r < rs; r += nsl_grid * kThreads)
             if (d.dom_s[r] && d.ralive[r]) {
                 d.ralive[r] = 0;
                 killed += d.rcnt[r];
@@ -340,25 +360,30 @@ __global__ __launch_bounds__(kThreads) void k_parts_count(const PartDesc *__rest
             tk += s_k[w];
             tf += s_f[w];
         }
-        d.sl_k[blockIdx.x] = tk;
-        d.sl_k[blockIdx.x + ((nb + kPartSlice - 1) / kPartSlice)] = tf;
+        d.sl_k[slice] = tk;
+        d.sl_k[slice + ((nb + kPartSlice - 1) / kPartSlice)] = tf;
     }
+}
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_count(const PartDesc *__restrict__ descs) {
+    parts_count<D>(descs, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // Kb: positions (the slices before this one, then ballots) of the kept tuples and the new reps;
 // the new reps' rows appended
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_place(const PartDesc *__restrict__ descs) {
+__device__ __forceinline__ void parts_place(const PartDesc *__restrict__ descs, uint32_t slice, uint32_t part,
+                                               uint32_t nsl_grid) {
     __shared__ uint32_t s_kc[kSliceIt][kThreads / 64], s_fc[kSliceIt][kThreads / 64];
-    const PartDesc &d = descs[blockIdx.y];
-    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const PartDesc &d = descs[part];
+    const uint32_t nb = d.nb, s0 = slice * kPartSlice;
     if (s0 >= nb) return;
     const uint32_t R0 = d.dcnt[0];
     const uint32_t nsl = (nb + kPartSlice - 1) / kPartSlice;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint32_t ko = 0, fo = 0;
-    for (uint32_t q = 0; q < blockIdx.x; q++) {
+    for (uint32_t q = 0; q < slice; q++) {
         ko += d.sl_k[q];
         fo += d.sl_k[nsl + q];
     }
@@ -402,15 +427,20 @@ __global__ __launch_bounds__(kThreads) void k_parts_place(const PartDesc *__rest
         fo += ft;
     }
 }
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_place(const PartDesc *__restrict__ descs) {
+    parts_place<D>(descs, blockIdx.x, blockIdx.y, gridDim.x);
+}
 
 // Kc: the kept tuples appended (id, rep) at their positions, the tuples joining a rep counted
 // (duplicate-heavy keys: one atomic per wave); the part's last slice to finish (a ticket)
 // writes the new counts to the device and to the host mirror
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_join(const PartDesc *__restrict__ descs) {
+__device__ __forceinline__ void parts_join(const PartDesc *__restrict__ descs, uint32_t slice, uint32_t part,
+                                               uint32_t nsl_grid) {
     __shared__ bool s_last;
-    const PartDesc &d = descs[blockIdx.y];
-    const uint32_t nb = d.nb, s0 = blockIdx.x * kPartSlice;
+    const PartDesc &d = descs[part];
+    const uint32_t nb = d.nb, s0 = slice * kPartSlice;
     if (s0 >= nb) return;
     const uint32_t R0 = d.dcnt[0], T0 = d.dcnt[1];
     const int lane = threadIdx.x & 63;
@@ -475,6 +505,10 @@ __global__ __launch_bounds__(kThreads) void k_parts_join(const PartDesc *__restr
         __threadfence_system();
         m[5] = d.seq;
     }
+}
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_join(const PartDesc *__restrict__ descs) {
+    parts_join<D>(descs, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // ---- compaction (dead reps and their tuples) and read-out -------------------------------
@@ -597,9 +631,91 @@ void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_
     k_pgm_write<<<g, kThreads, 0, st>>>(lists, nl, ttot, tsel, tpos, ids_out, org_out);
 }
 
+// The whole insert as ONE cooperative launch: the six phases above, separated by grid-wide
+// barriers, each workgroup looping over the phase's (slice, part) tasks / pair work items.
+// SKY_PART_COOP=1 (A/B knob, off by default): measured on the C4 10M prefix it saved ~8 us of the
+// ~40 us of API calls per insert call, but the five grid barriers made the GPU side ~3x longer
+// (the host then waited ~100 us per call for a staging slot): 61M vs 110M tuples/s.
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_parts_all(const PartDesc *__restrict__ descs, uint32_t nparts,
+                                                        uint32_t max_sl, const PartItem *__restrict__ items,
+                                                        uint32_t nitems) {
+    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    const uint32_t ntask = nparts * max_sl, G = gridDim.x;
+    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
+        parts_crit<D>(descs, t % max_sl, t / max_sl, max_sl);
+        __syncthreads();
+    }
+    grid.sync();
+    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
+        parts_classify<D>(descs, t % max_sl, t / max_sl, max_sl);
+        __syncthreads();
+    }
+    grid.sync();
+    for (uint32_t i = blockIdx.x; i < nitems; i += G) {
+        parts_pairs<D>(descs, items, i);
+        __syncthreads();
+    }
+    grid.sync();
+    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
+        parts_count<D>(descs, t % max_sl, t / max_sl, max_sl);
+        __syncthreads();
+    }
+    grid.sync();
+    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
+        parts_place<D>(descs, t % max_sl, t / max_sl, max_sl);
+        __syncthreads();
+    }
+    grid.sync();
+    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
+        parts_join<D>(descs, t % max_sl, t / max_sl, max_sl);
+        __syncthreads();
+    }
+}
+
+template <int D>
+static hipError_t launch_parts_coop(const PartDesc *descs, uint32_t nparts, uint32_t max_sl, const PartItem *items,
+                                    uint32_t nitems, hipStream_t st) {
+    static int max_blocks = -1;                // co-resident workgroups of k_parts_all<D> on this device
+    if (max_blocks < 0) {
+        int per_cu = 0, cus = 0, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_parts_all<D>, kThreads, 0) !=
+                hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+            (void)hipGetLastError();
+            max_blocks = 0;
+        } else {
+            max_blocks = per_cu * cus;
+        }
+    }
+    if (max_blocks <= 0) return hipErrorNotSupported;
+    // the slice tasks, and up to 256 workgroups for the pair items (most return at once: their
+    // bound is the batch size, |U| is far smaller on the reference streams); fewer workgroups
+    // make the grid barriers cheaper
+    const uint32_t want = std::max<uint32_t>(1u, std::max(nparts * max_sl, std::min(nitems, 256u)));
+    const unsigned g = (unsigned)std::min<uint32_t>(want, (uint32_t)std::min(max_blocks, 1024));
+    void *args[] = {(void *)&descs, (void *)&nparts, (void *)&max_sl, (void *)&items, (void *)&nitems};
+    return hipLaunchCooperativeKernel((const void *)k_parts_all<D>, dim3(g), dim3(kThreads), args, 0, st);
+}
+
+static bool parts_coop_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("SKY_PART_COOP");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 void launch_parts_insert(int D, const PartDesc *descs, int nparts, uint32_t max_slices, const PartItem *items,
                          uint32_t nitems, hipStream_t st) {
     if (!nparts || !max_slices) return;
+    if (parts_coop_enabled()) {
+        hipError_t e = hipErrorNotSupported;
+        SKY_DISPATCH_D(D, (e = launch_parts_coop<DD>(descs, (uint32_t)nparts, max_slices, items, nitems, st)));
+        if (e == hipSuccess) return;
+        (void)hipGetLastError();                   // not available: the six launches
+    }
     const dim3 g(max_slices, (unsigned)nparts);
     SKY_DISPATCH_D(D, (k_parts_crit<DD><<<g, kThreads, 0, st>>>(descs)));
     SKY_DISPATCH_D(D, (k_parts_classify<DD><<<g, kThreads, 0, st>>>(descs)));

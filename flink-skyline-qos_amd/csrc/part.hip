@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -269,6 +271,24 @@ Ctx::Staging *take_stage(sky_ctx *c, size_t bytes) {
     return &s;
 }
 
+// SKY_PART_HOSTPROF=1 (measurement only): host time of the insert calls split into the bounds /
+// work items, the staging copy, and the copy + launches; printed at process exit
+struct HostProf {
+    double pre = 0, wait = 0, stage = 0, launch = 0;
+    uint64_t calls = 0;
+    bool on = getenv("SKY_PART_HOSTPROF") != nullptr;
+    ~HostProf() {
+        if (on && calls)
+            fprintf(stderr, "[part] %llu calls, host us/call: bounds+items %.2f slot wait %.2f staging %.2f "
+                    "copy+launch %.2f\n", (unsigned long long)calls, pre / calls, wait / calls, stage / calls,
+                    launch / calls);
+    }
+};
+HostProf g_hprof;
+inline double us_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count();
+}
+
 int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *ids_all,
                  const double *const *values_all, const int64_t *counts_all) {
     sky_ctx *c = parts_all[0]->ctx;
@@ -289,6 +309,7 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
         ntot += (uint64_t)counts_all[g];
     }
     const int np = (int)parts.size();
+    const auto t_pre = std::chrono::steady_clock::now();
     if (ntot == 0) return SKY_OK;
     ARG_CHECK(ntot < 0x7fffffffull, "too many tuples in one call");
     // ---- bounds, compaction, capacity (per part; no host read unless compaction is due)
@@ -354,7 +375,11 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
     const size_t o_ids = o_items + align_up(items.size() * sizeof(PartItem));
     const size_t o_vals = o_ids + align_up((size_t)ntot * 8);
     const size_t up_bytes = o_vals + (size_t)ntot * D * 8;
+    if (g_hprof.on) g_hprof.pre += us_since(t_pre);
+    const auto t_wait = std::chrono::steady_clock::now();
     Ctx::Staging *sg = take_stage(c, up_bytes);
+    if (g_hprof.on) g_hprof.wait += us_since(t_wait);
+    const auto t_stage = std::chrono::steady_clock::now();
     if (!sg) {
         set_error("pinned staging allocation failed");
         return SKY_E_NOMEM;
@@ -378,6 +403,7 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
             off += nb;
         }
         stage_chunks(ch, D);
+        if (g_hprof.on) g_hprof.stage += us_since(t_stage);
         for (const StageChunk &k : ch)
             if (k.nan && (!nan || k.part < nan_part)) {
                 nan = true;
@@ -389,6 +415,7 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
                   "): the reference BNL result is order-dependent for NaN; batch rejected");
         return SKY_E_NAN;
     }
+    const auto t_launch = std::chrono::steady_clock::now();
     // double-buffered upload target: this call's copy may run while the previous call's kernels
     // still read the other buffer; a buffer is overwritten only after the kernels that read it
     if (!c->part_copy_st) {
@@ -476,6 +503,10 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->part_done[bsel], st));
     c->part_done_rec[bsel] = true;
+    if (g_hprof.on) {
+        g_hprof.launch += us_since(t_launch);
+        g_hprof.calls++;
+    }
     return SKY_OK;
 }
 

@@ -104,3 +104,13 @@ if [[ $STEPS == *domab* ]]; then
     done
   done
 fi
+if [[ $STEPS == *ophost* ]]; then
+  # the operator path with the host-side split of every insert call (SKY_PART_HOSTPROF)
+  SKY_PART_HOSTPROF=1 timeout -k 10 300 python3 -u tools/op_bench.py ${OP_N:-10000000} > $OUT/ophost_$TAG.json 2> $OUT/ophost_$TAG.err || { tail -30 $OUT/ophost_$TAG.err; exit 1; }
+  grep "^\[part\]" $OUT/ophost_$TAG.err
+  python3 -c "import json; d=json.load(open('$OUT/ophost_$TAG.json')); b=d['batched']; print('batched', b['insert_phase_s'], b['query_phase_s'], d['tuples_per_s'], b['p50_call_ms'])"
+  for T in 1 2 8; do
+    SKY_STAGE_THREADS=$T SKY_PART_HOSTPROF=1 timeout -k 10 300 python3 -u tools/op_bench.py ${OP_N:-10000000} > $OUT/ophost_${TAG}_t$T.json 2> $OUT/ophost_${TAG}_t$T.err || { tail -30 $OUT/ophost_${TAG}_t$T.err; exit 1; }
+    echo "threads $T: $(grep '^\[part\]' $OUT/ophost_${TAG}_t$T.err | tail -1)"
+  done
+fi
