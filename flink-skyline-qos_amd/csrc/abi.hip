@@ -480,6 +480,18 @@ int sky_profile_reset(sky_ctx *c) {
 }  // extern "C"
 
 // ---- bulk CSV ingest (k_csv.hip) ---------------------------------------------
+namespace sky {
+void launch_csv_nl_index(const uint8_t *text, int64_t nbytes, unsigned long long *lb, uint32_t *ticket_err,
+                         uint32_t *blk_off, uint32_t *d_nl, unsigned long long *ncomma, int R, int64_t *line_g,
+                         hipStream_t st);
+}
+// SKY_CSV_ONEPASS=1: the one-pass newline index (k_csv_nl_index) instead of the count, scan and
+// group passes (A/B knob, read per call; measured slower on the C4 text: 1.77 ms for the pass
+// with 64 KB super-chunks, 11 ms with 4 KB chunks, against 0.73 + 0.86 ms for the two passes)
+static bool csv_onepass() {
+    const char *e = getenv("SKY_CSV_ONEPASS");
+    return e && e[0] == '1';
+}
 // ServiceTuple.fromString (ServiceTuple.java:89-104) + filter(nonNull) (FlinkSkyline.java:103)
 // + Long.parseLong(id) (FlinkSkyline.java:276), over a whole device-resident buffer of records.
 int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d_ids_out, double *d_values_out,
@@ -501,7 +513,48 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
     unsigned long long h_commas = 0;
     std::vector<unsigned long long> h_shards(256, 0);
-    if (nb) {
+    // one pass (k_csv_nl_index: newline index by decoupled look-back + the group ends for R0, the
+    // records per group estimated from a sample of the text) with SKY_CSV_ONEPASS=1, unless the
+    // pass's look-back gave up; by default count -> scan -> groups
+    int R0 = 0;
+    bool onepass = false;
+    if (nb && csv_onepass()) {
+        const int64_t ns = std::min<int64_t>(nbytes, 64 << 10);
+        std::vector<uint8_t> smp((size_t)ns);
+        HIP_TRY(hipMemcpyAsync(smp.data(), text, (size_t)ns, hipMemcpyDeviceToHost, c->st));
+        HIP_TRY(hipStreamSynchronize(c->st));
+        int64_t snl = 0, scm = 0, send = 0;
+        for (int64_t i = 0; i < ns; i++) {
+            if (smp[i] == '\n') {
+                snl++;
+                send = i + 1;
+            } else if (smp[i] == ',') {
+                scm++;
+            }
+        }
+        if (snl > 0) {
+            R0 = csv_records_per_block(send, snl, scm + snl);
+            SKY_TRY(c->csv_lines.ensure((size_t)(nbytes / R0 + 2) * 8));
+            SKY_TRY(c->csv_lb.ensure((size_t)nb * 8 + 64));
+            unsigned long long *lb = c->csv_lb.as<unsigned long long>();
+            uint32_t *tick = reinterpret_cast<uint32_t *>(lb + nb);
+            HIP_TRY(hipMemsetAsync(lb, 0, (size_t)nb * 8 + 16, c->st));
+            HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
+            c->ktimer_begin("csv_count", c->st);
+            launch_csv_nl_index(text, nbytes, lb, tick, blk_off, d_nl, d_cnt + 8, R0, c->csv_lines.as<int64_t>(),
+                                c->st);
+            c->ktimer_end("csv_count", c->st, nbytes);
+            uint32_t h_err = 0;
+            HIP_TRY(hipMemcpyAsync(h_shards.data(), d_cnt + 8, 256 * 8, hipMemcpyDeviceToHost, c->st));
+            HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
+            HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
+            HIP_TRY(hipMemcpyAsync(&h_err, tick + 1, 4, hipMemcpyDeviceToHost, c->st));
+            HIP_TRY(hipStreamSynchronize(c->st));
+            onepass = h_err == 0;
+        }
+    }
+    if (nb && !onepass) {
+        std::fill(h_shards.begin(), h_shards.end(), 0ull);
         HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
         c->ktimer_begin("csv_count", c->st);
         launch_csv_nl_count(text, nbytes, blk, d_cnt + 8, c->st);
@@ -517,13 +570,18 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const int64_t nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
     // group boundaries only (R records per parse workgroup; R >= 8, and the exact path's groups of
-    // 256 need fewer): 8 bytes per group instead of per record
-    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
-    SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
+    // 256 need fewer): 8 bytes per group instead of per record.  The one pass's groups of R0 serve
+    // when R0 <= R (the sample did not overestimate the records that fit a workgroup's window)
+    int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
     SKY_TRY(c->csv_status.ensure(nr1));
-    c->ktimer_begin("csv_lines", c->st);
-    if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);
-    c->ktimer_end("csv_lines", c->st, nbytes);
+    if (onepass && R0 <= R) {
+        R = R0;
+    } else {
+        SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
+        c->ktimer_begin("csv_lines", c->st);
+        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);
+        c->ktimer_end("csv_lines", c->st, nbytes);
+    }
     const bool direct = cap >= nrec && d_ids_out && d_values_out;
     int64_t *pid = d_ids_out;
     double *pval = d_values_out;

@@ -114,3 +114,14 @@ if [[ $STEPS == *ophost* ]]; then
     echo "threads $T: $(grep '^\[part\]' $OUT/ophost_${TAG}_t$T.err | tail -1)"
   done
 fi
+if [[ $STEPS == *csvtests* ]]; then
+  timeout -k 10 600 $PYT tests/test_gpu_csv.py tests/test_gpu_replay.py > $OUT/pytest_csv_$TAG.log 2>&1 || { tail -60 $OUT/pytest_csv_$TAG.log; exit 1; }
+  tail -3 $OUT/pytest_csv_$TAG.log
+fi
+if [[ $STEPS == *csvab* ]]; then
+  # the CSV companion (C4 stream as producer text) with the one-pass newline index and without
+  for K in default SKY_CSV_ONEPASS=0; do
+    env ${K/default/SKY_X=0} timeout -k 10 300 python3 -u tools/csv_bench.py > $OUT/csvab_${TAG}_$K.json 2> $OUT/csvab_${TAG}_$K.err || { tail -20 $OUT/csvab_${TAG}_$K.err; exit 1; }
+    echo "$K $(cut -c1-600 $OUT/csvab_${TAG}_$K.json)"
+  done
+fi
