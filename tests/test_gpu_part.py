@@ -237,3 +237,32 @@ def test_parts_global_merge_equals_snapshot_merge(dist, D, n, gpu_engine_factory
     for p in parts.values():
         p.close()
     eng.close()
+
+
+def test_parts_global_merge_edge_cases(gpu_engine_factory, oracle):
+    """Empty parts (never inserted into), a single part, a state with dead vectors (compacted by the
+    merge), and no parts at all: sky_parts_global_merge equals the snapshot-based merge."""
+    from skyline.operators import _LocalPart
+    D = 4
+    eng = gpu_engine_factory(D, 8)
+    rng = np.random.default_rng(33)
+    a = _LocalPart(eng, 0)
+    b = _LocalPart(eng, 1)                          # stays empty
+    c = _LocalPart(eng, 2)
+    base = rng.integers(20, 60, size=(3000, D)).astype(np.float64)
+    a.insert(np.arange(3000, dtype=np.int64), base)
+    a.insert(np.arange(3000, 4000, dtype=np.int64), base[:1000] - 15.0)   # kills most of a's vectors
+    c.insert(np.arange(5000, 5500, dtype=np.int64), rng.integers(0, 80, size=(500, D)).astype(np.float64))
+    for plist, pids in (([a, b, c], [0, 1, 2]), ([b], [1]), ([c], [7]), ([], [])):
+        g_ids, g_org = _LocalPart.global_merge_many(eng, plist, pids)
+        ls_dev, sv_dev = eng.stats()
+        snaps = [p.snapshot() for p in plist]
+        e_ids, e_org = eng.global_merge(pids, [s[0] for s in snaps], [s[1] for s in snaps])
+        ls_ref, sv_ref = eng.stats()
+        np.testing.assert_array_equal(g_ids, e_ids)
+        np.testing.assert_array_equal(g_org, e_org)
+        np.testing.assert_array_equal(ls_dev, ls_ref)
+        np.testing.assert_array_equal(sv_dev, sv_ref)
+    for p in (a, b, c):
+        p.close()
+    eng.close()

@@ -99,3 +99,30 @@ def test_stream_device_appends_match_whole_query(gpu_engine_factory):
             assert (ls == ls2).all() and (sv == sv2).all()
     st.close()
     eng.close()
+
+
+@pytest.mark.parametrize("W", [0, 5000])
+def test_stream_reserve_then_queries(gpu_engine_factory, oracle, W):
+    """sky_stream_reserve (SkylineStream.reserve) before the stream, again mid-stream with tuples
+    resident, and a stream that outgrows its reservation: every host-view query still equals the
+    oracle over the window (landmark: every tuple so far)."""
+    import skyline
+    g = load_golden([p for p in golden_streams() if "anti_correlated_4d" in p][0])
+    vals, ids = g["values"], g["ids"].astype(np.int64)
+    n, D = vals.shape
+    eng = gpu_engine_factory(D, 8, "mr-angle")
+    st = skyline.SkylineStream(eng, W)
+    st.reserve(max(64, n // 4))                     # smaller than the stream: it has to grow
+    pos, step = 0, max(1, n // 10)
+    while pos < n:
+        b = min(step, n - pos)
+        st.append(ids[pos:pos + b], vals[pos:pos + b])
+        pos += b
+        if pos >= n // 2 and pos - b < n // 2:
+            st.reserve(n)                           # again, with tuples resident
+        k = st.query_host_view()
+        got_ids, _ = st.view()
+        lo = max(0, pos - W) if W else 0
+        _check(oracle, "angle", vals[lo:pos], ids[lo:pos], 8, got_ids[:k].copy(), eng)
+    st.close()
+    eng.close()
