@@ -698,16 +698,34 @@ __device__ __forceinline__ bool swar_digits(const uint32_t *__restrict__ buf, in
     return ok;
 }
 
-// the same for len <= 8 (one window, three LDS words): the producer's ids (< 10^8 for 100M
-// records) and values (<= 4 digits) all take it; chosen per wave, so the branch is uniform
-__device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, int s, int len, uint64_t &v) {
-    const int k = s >> 2, sh = (s & 3) * 8;
-    const uint64_t A = (uint64_t)buf[k] | ((uint64_t)buf[k + 1] << 32);
-    const uint64_t C = buf[k + 2];
-    const uint64_t x0 = sh ? (A >> sh) | (C << (64 - sh)) : A;
-    const uint64_t y0 = swar_pad(x0, len);
-    v = swar_value(y0);
-    return len >= 1 && len <= 8 && swar_is_digits(y0);
+// the same for len <= 8, in 32-bit operations only (the 64-bit shifts and multiplies of the
+// general path issue at a fraction of the rate): the producer's ids (< 10^8 for 100M records)
+// and values (<= 4 digits) all take it; chosen per wave, so the branch is uniform.  The
+// window is the 8 bytes [e - 8, e) that END at the field's delimiter (two v_alignbyte from
+// three LDS words; buf must be readable 8 bytes before its start), with the bytes before s
+// replaced by '0' — right-aligned, so the digit weights are fixed.
+__device__ __forceinline__ uint32_t swar4_value(uint32_t d) {      // 4 digit bytes (0..9), first = most significant
+    // bytes 0 / 2 of 10 d + (d >> 8): two-digit values.  A 24-bit multiply-add (byte 3 of 10 d is
+    // not needed); written out because the compiler otherwise picks v_mad_u64_u32 for it
+    uint32_t t;
+    asm("v_mad_u32_u24 %0, %1, 10, %2" : "=v"(t) : "v"(d), "v"(d >> 8));
+    return (t & 0xffu) * 100u + ((t >> 16) & 0xffu);
+}
+__device__ __forceinline__ uint32_t swar4_bad(uint32_t w) {        // 0 iff every byte is an ASCII digit
+    return ((w & 0xF0F0F0F0u) ^ 0x30303030u) | (((w + 0x06060606u) & 0xF0F0F0F0u) ^ 0x30303030u);
+}
+__device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, int s, int e, uint32_t &v) {
+    const int b = e - 8;
+    const int k = b >> 2;                                           // >= -2
+    const uint32_t sh = (uint32_t)b & 3u;
+    const uint32_t x0 = buf[k], x1 = buf[k + 1], x2 = buf[k + 2];
+    const uint32_t len = (uint32_t)(e - s);
+    const uint64_t m = (1ull << (8u * (8u - min(max(len, 1u), 8u)))) - 1ull;   // the bytes before s
+    const uint32_t m0 = (uint32_t)m, m1 = (uint32_t)(m >> 32);
+    const uint32_t w0 = (__builtin_amdgcn_alignbyte(x1, x0, sh) & ~m0) | (0x30303030u & m0);
+    const uint32_t w1 = (__builtin_amdgcn_alignbyte(x2, x1, sh) & ~m1) | (0x30303030u & m1);
+    v = swar4_value(w0 - 0x30303030u) * 10000u + swar4_value(w1 - 0x30303030u);
+    return ((swar4_bad(w0) | swar4_bad(w1)) == 0u) & (len - 1u < 8u);   // no short circuit: no branch
 }
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
@@ -719,9 +737,13 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                                                             longlong3 *__restrict__ slow,
                                                             unsigned long long *__restrict__ slow_n,
                                                             unsigned long long slow_cap, int R, int stop) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kFieldText / 4 + 8];
-    __shared__ uint32_t s_dl[kFieldsMax];                // delimiter f: staged byte offset | record << 16
-    __shared__ uint16_t s_rfirst[kCsvThreads + 1];
+    // s_buf[-4, 0): readable front pad for swar_digits8's window (masked bytes)
+    __shared__ __attribute__((aligned(16))) uint32_t s_bufp[4 + kFieldText / 4 + 8];
+    uint32_t *const s_buf = s_bufp + 4;
+    // delimiter f: staged byte offset | record << 16; s_dl[-1] closes the field before the first
+    __shared__ uint32_t s_dlp[1 + kFieldsMax + kCsvThreads];   // + one dummy slot per lane
+    uint32_t *const s_dl = s_dlp + 1;
+    __shared__ uint16_t s_rfirst[kCsvThreads + 1 + kCsvThreads];   // + one dummy slot per lane
     __shared__ int s_fempty[kCsvThreads];
     __shared__ uint8_t s_bad[kCsvThreads], s_idok[kCsvThreads];
     __shared__ uint32_t s_w[8], s_cnt[4];
@@ -772,8 +794,13 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     if (tid < 4) s_cnt[tid] = 0;
     s_fempty[tid] = 0x7fffffff;
     s_bad[tid] = 0;
-    uint32_t mcs[kUnits * 4], mns[kUnits * 4];
-    uint32_t nd = 0, nn = 0;
+    s_idok[tid] = 1;                                       // cleared by a failed id parse
+    // the lane's delimiters as bit masks over its <= 48 staged bytes (bit b = byte b of its
+    // range, bytes 0-31 in md0 / mnl0, 32-47 in md1 / mnl1): ',' or '\n' in md, '\n' in mnl.
+    // Each word's four 0x80 flags are gathered into a nibble by one multiply (bits 7 / 15 /
+    // 23 / 31 -> 28..31, no carries)
+    static_assert(kUnits * 16 <= 64, "two 32-bit masks per lane");
+    uint32_t md0 = 0, mnl0 = 0, md1 = 0, mnl1 = 0;
 #pragma unroll
     for (int k = 0; k < kUnits * 4; k++) {
         const int b0 = 16 * (tid * per) + 4 * k;
@@ -787,11 +814,11 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
             mc &= keep;
             mn &= keep;
         }
-        mcs[k] = mc;
-        mns[k] = mn;
-        nd += __popc(mc | mn);
-        nn += __popc(mn);
+        const uint32_t nd4 = ((mc | mn) * 0x00204081u) >> 28, nn4 = (mn * 0x00204081u) >> 28;
+        if (k < 8) { md0 |= nd4 << (4 * k); mnl0 |= nn4 << (4 * k); }
+        else { md1 |= nd4 << (4 * (k - 8)); mnl1 |= nn4 << (4 * (k - 8)); }
     }
+    const uint32_t nd = __popc(md0) + __popc(md1), nn = __popc(mnl0) + __popc(mnl1);
     // block exclusive scans of (nd, nn)
     const int lane = tid & 63, wv = tid >> 6;
     uint32_t id_ = nd, in_ = nn;
@@ -814,46 +841,72 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     }
     if (tid == 0) {
         s_rfirst[0] = 0;
+        s_dl[-1] = (uint32_t)(lo - 1) & 0xffffu;           // field 0 starts at lo
         if (tail_open) {                                   // virtual delimiter closing the tail record
             s_dl[nf - 1] = (uint32_t)hi | ((uint32_t)(nr - 1) << 16);
             s_rfirst[nr] = (uint16_t)nf;
         }
     }
     {
+        // per half, one pass over the lane's set bits, as many steps as the wave's busiest lane
+        // has delimiters there; the stores of a lane that has run out (or of a ',') go to its
+        // own dummy slot instead of being branched around
         uint32_t f = fbase, rec = rbase;
 #pragma unroll
-        for (int k = 0; k < kUnits * 4; k++) {
-            const int b0 = 16 * (tid * per) + 4 * k;
-            const uint32_t mn = mns[k];
-            uint32_t m = mcs[k] | mn;
-            while (m) {
-                const int bit = __ffs(m) - 1;
-                m &= m - 1;
-                s_dl[f] = (uint32_t)(b0 + (bit >> 3)) | (rec << 16);
-                if ((mn >> bit) & 1u) {
-                    rec++;
-                    s_rfirst[rec] = (uint16_t)(f + 1);
-                }
-                f++;
+        for (int h = 0; h < 2; h++) {
+            const uint32_t b0 = 16u * (uint32_t)(tid * per) + 32u * h;
+            uint32_t m = h ? md1 : md0;
+            const uint32_t mnl = h ? mnl1 : mnl0;
+            while (__ballot(m != 0u)) {
+                const bool has = m != 0u;
+                const uint32_t low = m & (0u - m);
+                const uint32_t bit = __builtin_ctz(m | 0x80000000u);   // 31 past the last: unused
+                m ^= low;
+                const uint32_t isn = (mnl & low) ? 1u : 0u;
+                s_dl[has ? f : (uint32_t)(kFieldsMax + tid)] = (b0 + bit) | (rec << 16);
+                rec += isn;
+                s_rfirst[isn ? rec : (uint32_t)(kCsvThreads + 1 + tid)] = (uint16_t)(f + 1);
+                f += has ? 1u : 0u;
             }
         }
     }
     __syncthreads();
     if (stop == 2) { if (s_dl[tid] == 0x1234u) status[0] = 9; return; }
-    // 3. fields
+    // 3. fields.  Common case, straight-line: a plain digit field (the SWAR path) that is an
+    // id or an in-range value of <= 15 digits -> one 8-byte store, its address and bits
+    // selected (ids and values interleave in every wave; exec-masked branches per kind cost
+    // more than the selects).  Everything else (empty, signs, decimals, exponents, NaN /
+    // Infinity, long digit strings, extra fields) takes the full grammar below.
     const LdsSrc src{reinterpret_cast<const uint8_t *>(s_buf), 0};
+    int64_t *const ids_b = ids + r0;
+    double *const vals_b = vals + r0 * D - 1;              // + j * D + col, col >= 1
     for (int f = tid; f < nf; f += kCsvThreads) {
-        const uint32_t dl = s_dl[f];
-        const int s = f == 0 ? lo : (int)(s_dl[f - 1] & 0xffffu) + 1;
+        const uint32_t dp = s_dl[f - 1], dl = s_dl[f];
+        const int s = (int)(((dp & 0xffffu) + 1u) & 0xffffu);
         const int e = (int)(dl & 0xffffu);
         const int j = (int)(dl >> 16);
         const int col = f - (int)s_rfirst[j];
+        const bool is_id = col == 0;
         uint64_t u = 0;
-        const bool fast = __ballot(e - s > 8) == 0ull ? swar_digits8(s_buf, s, e - s, u)
-                                                       : swar_digits(s_buf, s, e - s, u);
-        const bool is_id = col == 0, empty = s == e;
-        int64_t idv = (int64_t)u;                          // < 10^16
-        double v = (double)u;                              // exact when len <= 15
+        double v;
+        bool fast;
+        if (__ballot(e - s > 8) == 0ull) {
+            uint32_t u32;
+            fast = swar_digits8(s_buf, s, e, u32);
+            u = u32;
+            v = (double)u32;
+        } else {
+            fast = swar_digits(s_buf, s, e - s, u);
+            v = (double)u;                                 // exact when len <= 15
+        }
+        if (fast & (is_id | ((e - s <= 15) & (col <= D)))) {
+            const uint32_t off = is_id ? (uint32_t)j : __umul24((uint32_t)j, (uint32_t)D) + (uint32_t)col;
+            int64_t *const p = (is_id ? ids_b : reinterpret_cast<int64_t *>(vals_b)) + off;
+            *p = is_id ? (int64_t)u : __double_as_longlong(v);   // id < 10^16
+            continue;
+        }
+        const bool empty = s == e;
+        int64_t idv = (int64_t)u;
         bool idok = fast;
         int pr = 1;
         if (!(fast && (is_id || e - s <= 15)) && !empty) {   // rare: the full Java grammar
@@ -861,7 +914,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
             else pr = java_parse_double<false>(src, s, e, v);
         }
         if (is_id) {
-            ids[r0 + j] = idv;
+            ids_b[j] = idv;
             s_idok[j] = idok;
         } else if (empty) {
             atomicMin(&s_fempty[j], col);

@@ -118,9 +118,17 @@ if [[ $STEPS == *csvtests* ]]; then
   timeout -k 10 600 $PYT tests/test_gpu_csv.py tests/test_gpu_replay.py > $OUT/pytest_csv_$TAG.log 2>&1 || { tail -60 $OUT/pytest_csv_$TAG.log; exit 1; }
   tail -3 $OUT/pytest_csv_$TAG.log
 fi
+if [[ $STEPS == *csvpmc* ]]; then
+  # instruction mix of k_csv_fields (one counter pass, kernel trace only), 20M records
+  export TMPDIR=/tmp
+  rm -rf $OUT/csvpmc_$TAG
+  timeout -k 10 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+    --kernel-include-regex k_csv_fields -f csv -d $OUT/csvpmc_$TAG -o run -- python3 -u $R/tools/csv_bench.py 20000000 > $OUT/csvpmc_$TAG.log 2>&1 || { tail -20 $OUT/csvpmc_$TAG.log; exit 1; }
+  python tools/prof_summary.py pmcshow $OUT/csvpmc_$TAG k_csv_fields | tee $OUT/csvpmc_${TAG}_summary.txt
+fi
 if [[ $STEPS == *csvab* ]]; then
   # the CSV companion (C4 stream as producer text) with the one-pass newline index and without
-  for K in default SKY_CSV_ONEPASS=0; do
+  for K in ${CSVKNOBS:-default}; do
     env ${K/default/SKY_X=0} timeout -k 10 300 python3 -u tools/csv_bench.py > $OUT/csvab_${TAG}_$K.json 2> $OUT/csvab_${TAG}_$K.err || { tail -20 $OUT/csvab_${TAG}_$K.err; exit 1; }
     echo "$K $(cut -c1-600 $OUT/csvab_${TAG}_$K.json)"
   done
