@@ -484,6 +484,20 @@ namespace sky {
 void launch_csv_nl_index(const uint8_t *text, int64_t nbytes, unsigned long long *lb, uint32_t *ticket_err,
                          uint32_t *blk_off, uint32_t *d_nl, unsigned long long *ncomma, int R, int64_t *line_g,
                          hipStream_t st);
+int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int *tail);
+int64_t csv_chunk_count(int64_t nbytes, int chunk);
+void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
+                             int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
+                             longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
+                             unsigned long long slow_cap, hipStream_t st);
+}
+// SKY_CSV_CHUNKS=1: byte chunks that find their own records and take their first record index from
+// the count pass's prefix, instead of the group pass (every R-th newline) + R records per parse
+// workgroup (A/B knob, read per call; measured slower on the C4 text: parse 4.89 ms against
+// 0.86 + 3.79 ms for groups + parse, profiles/r03_csv_parse_ab.txt)
+static bool csv_chunk_mode() {
+    const char *e = getenv("SKY_CSV_CHUNKS");
+    return e && e[0] == '1';
 }
 // SKY_CSV_ONEPASS=1: the one-pass newline index (k_csv_nl_index) instead of the count, scan and
 // group passes (A/B knob, read per call; measured slower on the C4 text: 1.77 ms for the pass
@@ -513,6 +527,17 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
     unsigned long long h_commas = 0;
     std::vector<unsigned long long> h_shards(256, 0);
+    // exact-conversion queue (SKY_CSV_SLOW_CAP: tests force the re-parse-everything path)
+    static const unsigned long long slow_cap = [] {
+        const char *e = getenv("SKY_CSV_SLOW_CAP");
+        return e ? (unsigned long long)std::max(1, atoi(e)) : (1ull << 20);
+    }();
+    SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
+    unsigned long long h_cnt[5] = {};
+    int64_t nrec = 0;
+    bool direct = false;
+    int64_t *pid = d_ids_out;
+    double *pval = d_values_out;
     // one pass (k_csv_nl_index: newline index by decoupled look-back + the group ends for R0, the
     // records per group estimated from a sample of the text) with SKY_CSV_ONEPASS=1, unless the
     // pass's look-back gave up; by default count -> scan -> groups
@@ -567,14 +592,20 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     }
     for (unsigned long long x : h_shards) h_commas += x;
     const int64_t nl = h_nl;
-    const int64_t nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
+    nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
     // group boundaries only (R records per parse workgroup; R >= 8, and the exact path's groups of
     // 256 need fewer): 8 bytes per group instead of per record.  The one pass's groups of R0 serve
     // when R0 <= R (the sample did not overestimate the records that fit a workgroup's window)
     int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
     SKY_TRY(c->csv_status.ensure(nr1));
-    if (onepass && R0 <= R) {
+    // byte chunks (SKY_CSV_CHUNKS=1): each parse workgroup finds its records itself and takes the
+    // index of its first one from the count pass's prefix, so no group pass
+    int ctail = 0;
+    const int chunk =
+        csv_chunk_mode() && !onepass ? csv_chunk_bytes(nbytes, nrec, (int64_t)h_commas + nrec, &ctail) : 0;
+    if (chunk > 0) {
+    } else if (onepass && R0 <= R) {
         R = R0;
     } else {
         SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
@@ -582,9 +613,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);
         c->ktimer_end("csv_lines", c->st, nbytes);
     }
-    const bool direct = cap >= nrec && d_ids_out && d_values_out;
-    int64_t *pid = d_ids_out;
-    double *pval = d_values_out;
+    direct = cap >= nrec && d_ids_out && d_values_out;
     if (!direct) {
         SKY_TRY(c->csv_ids.ensure(nr1 * 8));
         SKY_TRY(c->csv_vals.ensure(nr1 * D * 8));
@@ -592,24 +621,29 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         pval = c->csv_vals.as<double>();
     }
     HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));   // [1..3] rejected per cause, [4] queued exact conversions
-    // exact-conversion queue (SKY_CSV_SLOW_CAP: tests force the re-parse-everything path)
-    static const unsigned long long slow_cap = [] {
-        const char *e = getenv("SKY_CSV_SLOW_CAP");
-        return e ? (unsigned long long)std::max(1, atoi(e)) : (1ull << 20);
-    }();
-    SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
-    SKY_TRY(c->csv_keep.ensure((size_t)((nrec + R - 1) / R + 1) * 4));   // spill list of k_csv_fields
-    HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
-    c->ktimer_begin("csv_parse", c->st);
-    launch_csv_parse(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval, c->csv_status.as<uint8_t>(),
-                     d_cnt, c->csv_keep.as<uint32_t>(), c->csv_slow.as<longlong3>(), d_cnt + 4, slow_cap, R, c->st);
-    c->ktimer_end("csv_parse", c->st, nrec);
+    if (chunk > 0) {
+        SKY_TRY(c->csv_keep.ensure(16));                                   // [0]: listed spans
+        SKY_TRY(c->csv_spans.ensure((size_t)csv_chunk_count(nbytes, chunk) * sizeof(longlong4)));
+        HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
+        c->ktimer_begin("csv_parse", c->st);
+        launch_csv_parse_chunks(text, nbytes, chunk, ctail, blk_off, D, pid, pval, c->csv_status.as<uint8_t>(), d_cnt,
+                                c->csv_keep.as<uint32_t>(), c->csv_spans.as<longlong4>(), c->csv_slow.as<longlong3>(),
+                                d_cnt + 4, slow_cap, c->st);
+        c->ktimer_end("csv_parse", c->st, nrec);
+    } else {
+        SKY_TRY(c->csv_keep.ensure((size_t)((nrec + R - 1) / R + 1) * 4));   // spill list of k_csv_fields
+        HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
+        c->ktimer_begin("csv_parse", c->st);
+        launch_csv_parse(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval, c->csv_status.as<uint8_t>(),
+                         d_cnt, c->csv_keep.as<uint32_t>(), c->csv_slow.as<longlong3>(), d_cnt + 4, slow_cap, R, c->st);
+        c->ktimer_end("csv_parse", c->st, nrec);
+    }
     HIP_TRY(hipGetLastError());
-    unsigned long long h_cnt[5] = {};
     HIP_TRY(hipMemcpyAsync(h_cnt, d_cnt, 40, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     if (h_cnt[4] > slow_cap) {   // more exact conversions than the queue holds: re-parse every record exactly
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));
+        SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / 256 + 2) * 8));   // unsized on the chunk path
         if (nl) launch_csv_nl_groups(text, nbytes, blk_off, 256, c->csv_lines.as<int64_t>(), c->st);
         launch_csv_parse_exact(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval,
                                c->csv_status.as<uint8_t>(), d_cnt, c->st);

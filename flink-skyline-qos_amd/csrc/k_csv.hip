@@ -728,6 +728,20 @@ __device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, i
     return ((swar4_bad(w0) | swar4_bad(w1)) == 0u) & (len - 1u < 8u);   // no short circuit: no branch
 }
 
+// CHUNK = false: workgroup b parses records [b R, b R + R) (group boundaries from k_csv_nl_groups).
+// CHUNK = true (no group pass): workgroup c parses the records that START in the byte chunk
+// [c C, c C + C): it stages the chunk plus a tail for its last record, finds its first record
+// start and its last record's end itself, and takes its first record's index from the count
+// pass's prefix at the 4 KB block holding byte c C - 1 plus its own count of the newlines between
+// that block's start and c C - 1.  Chunks that do not fit (a record past the staged tail, > 256
+// records, > kFieldsMax fields) are listed as spans for k_csv_records.
+struct CsvChunkArgs {
+    const uint32_t *blk_off;     // exclusive newline counts per 4 KB count chunk
+    longlong4 *spans;            // (start, end or -1, first record, records) of listed chunks
+    int chunk;                   // C, bytes (multiple of 16)
+    int tail;                    // bytes staged past the chunk (C + 16 + tail <= kFieldText)
+};
+template <bool CHUNK>
 __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__restrict__ text, int64_t nbytes,
                                                             const int64_t *__restrict__ line_g, int64_t nl,
                                                             int64_t nrec, int D, int64_t *__restrict__ ids,
@@ -736,7 +750,8 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
                                                             uint32_t *__restrict__ spill,
                                                             longlong3 *__restrict__ slow,
                                                             unsigned long long *__restrict__ slow_n,
-                                                            unsigned long long slow_cap, int R, int stop) {
+                                                            unsigned long long slow_cap, int R, int stop,
+                                                            CsvChunkArgs ca) {
     // s_buf[-4, 0): readable front pad for swar_digits8's window (masked bytes)
     __shared__ __attribute__((aligned(16))) uint32_t s_bufp[4 + kFieldText / 4 + 8];
     uint32_t *const s_buf = s_bufp + 4;
@@ -748,47 +763,143 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     __shared__ uint8_t s_bad[kCsvThreads], s_idok[kCsvThreads];
     __shared__ uint32_t s_w[8], s_cnt[4];
     const int tid = threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.x * R;             // R <= 256 records per workgroup (host-chosen)
-    const int nr = (int)(nrec - r0 < R ? nrec - r0 : R);
-    const int64_t rl = r0 + nr - 1;
-    // group boundaries (k_csv_nl_groups): the last group ends at the end of the text (its last
-    // record has no '\n', or its '\n' is the last byte)
-    const int64_t span_s = r0 == 0 ? 0 : line_g[blockIdx.x - 1] + 1;
-    const bool tail_open = rl >= nl;                       // last record has no '\n'
-    const int64_t span_e = tail_open || nr < R ? nbytes : line_g[blockIdx.x] + 1;   // includes the final '\n'
-    const int64_t a0 = span_s & ~15ll;
-    if (span_e - a0 > kFieldText) {                        // uniform per block
-        if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
-        return;
-    }
-    if (stop == 4) return;
-    // 1+2. lane tid owns the 16-byte units [tid*per, tid*per + per) of the staged span: it loads
-    // them (into registers and LDS) and numbers its delimiters without re-reading LDS
     constexpr int kUnits = (kFieldText / 16 + kCsvThreads - 1) / kCsvThreads;   // 3
-    const int nq = (int)((span_e - a0 + 15) >> 4);
-    const int per = (nq + kCsvThreads - 1) / kCsvThreads;
-    const int lo = (int)(span_s - a0), hi = (int)(span_e - a0);   // staged byte range of the records
     const bool aligned = ((uintptr_t)text & 15) == 0;
+    int64_t r0, a0;
+    int nr, nq, lo, hi;
+    bool tail_open;
     uint32_t dw[kUnits * 4];
+    // stage the 16-byte units [a0 + 16 q, ...) for q < nq: lane tid owns [tid*per, tid*per + per)
+    // (registers + LDS), and numbers its delimiters later without re-reading LDS
+    auto stage = [&](int per) {
 #pragma unroll
-    for (int u = 0; u < kUnits; u++) {
-        const int q = tid * per + u;
-        uint4 x = make_uint4(0, 0, 0, 0);
-        if (u < per && q < nq) {
-            const int64_t o = a0 + 16 * (int64_t)q;
-            if (aligned && o + 16 <= nbytes) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(text + o));
-                x = make_uint4(y.x, y.y, y.z, y.w);
-            } else {
-                uint32_t t[4] = {0, 0, 0, 0};
-                for (int k = 0; k < 16; k++)
-                    if (o + k < nbytes) t[k >> 2] |= (uint32_t)text[o + k] << (8 * (k & 3));
-                x = make_uint4(t[0], t[1], t[2], t[3]);
+        for (int u = 0; u < kUnits; u++) {
+            const int q = tid * per + u;
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (u < per && q < nq) {
+                const int64_t o = a0 + 16 * (int64_t)q;
+                if (aligned && o + 16 <= nbytes) {
+                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(text + o));
+                    x = make_uint4(y.x, y.y, y.z, y.w);
+                } else {
+                    uint32_t t[4] = {0, 0, 0, 0};
+                    for (int k = 0; k < 16; k++)
+                        if (o + k < nbytes) t[k >> 2] |= (uint32_t)text[o + k] << (8 * (k & 3));
+                    x = make_uint4(t[0], t[1], t[2], t[3]);
+                }
+                reinterpret_cast<uint4 *>(s_buf)[q] = x;
             }
-            reinterpret_cast<uint4 *>(s_buf)[q] = x;
+            dw[4 * u] = x.x; dw[4 * u + 1] = x.y; dw[4 * u + 2] = x.z; dw[4 * u + 3] = x.w;
         }
-        dw[4 * u] = x.x; dw[4 * u + 1] = x.y; dw[4 * u + 2] = x.z; dw[4 * u + 3] = x.w;
+    };
+    int per;
+    if constexpr (!CHUNK) {
+        r0 = (int64_t)blockIdx.x * R;                       // R <= 256 records per workgroup (host-chosen)
+        nr = (int)(nrec - r0 < R ? nrec - r0 : R);
+        const int64_t rl = r0 + nr - 1;
+        // group boundaries (k_csv_nl_groups): the last group ends at the end of the text (its last
+        // record has no '\n', or its '\n' is the last byte)
+        const int64_t span_s = r0 == 0 ? 0 : line_g[blockIdx.x - 1] + 1;
+        tail_open = rl >= nl;                               // last record has no '\n'
+        const int64_t span_e = tail_open || nr < R ? nbytes : line_g[blockIdx.x] + 1;   // includes the final '\n'
+        a0 = span_s & ~15ll;
+        if (span_e - a0 > kFieldText) {                     // uniform per block
+            if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+            return;
+        }
+        if (stop == 4) return;
+        nq = (int)((span_e - a0 + 15) >> 4);
+        per = (nq + kCsvThreads - 1) / kCsvThreads;
+        lo = (int)(span_s - a0);
+        hi = (int)(span_e - a0);                            // staged byte range of the records
+        stage(per);
+    } else {
+        __shared__ uint32_t s_nlw, s_nlb;
+        __shared__ int s_first, s_end;
+        if (tid == 0) {
+            s_nlw = 0;
+            s_nlb = 0;
+            s_first = 0x7fffffff;
+            s_end = 0x7fffffff;
+        }
+        const int64_t c = blockIdx.x;
+        const int64_t cs = c * ca.chunk, ce = min(cs + ca.chunk, nbytes);
+        a0 = c ? cs - 16 : 0;                               // byte cs - 1 tells whether a record starts at cs
+        const int64_t wend = min(a0 + 16 + ca.chunk + ca.tail, nbytes);
+        nq = (int)((wend - a0 + 15) >> 4);
+        per = (nq + kCsvThreads - 1) / kCsvThreads;
+        // the newlines in [b_s, cs - 1), b_s = the start of the count block holding byte cs - 1
+        // (< 4 KB, one 16-byte load per lane; the previous chunk staged most of them: L2-hot)
+        const int64_t blk0 = c ? (cs - 1) / kCsvChunk : 0;
+        uint32_t nlb = 0;
+        if (c) {
+            const int64_t bs = blk0 * kCsvChunk, base = bs + 16 * tid;
+            if (base < cs - 1) {
+                uint32_t w[4];
+                load16(text, nbytes, base, aligned, w);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int64_t v = min<int64_t>(max<int64_t>(cs - 1 - (base + 4 * k), 0), 4);   // bytes before cs - 1
+                    const uint32_t keep = v >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * v)) - 1u));
+                    nlb += __popc(nl_in_word(w[k]) & keep);
+                }
+            }
+        }
+        stage(per);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nlb += __shfl_xor(nlb, o, 64);
+        __syncthreads();                                    // s_nlw / s_nlb / s_first / s_end initialised
+        if ((tid & 63) == 0 && nlb) atomicAdd(&s_nlb, nlb);
+        // newlines in [wlo, whi) start this chunk's records; the first one at or after whi ends its last
+        const int wlo = c ? (int)(cs - 1 - a0) : 0, whi = (int)(ce - 1 - a0);
+        // the lane's newlines as one bit per staged byte (as in the delimiter pass below), then the
+        // window's count / first and the first at or after whi by popcount / ctz, no bit loops
+        const int L0 = 16 * (tid * per);
+        uint64_t nlm = 0;
+#pragma unroll
+        for (int k = 0; k < kUnits * 4; k++) {
+            const uint32_t mn = k < per * 4 ? byte_eq_mask(dw[k], 0x0a0a0a0au) : 0u;   // unstaged bytes are 0
+            nlm |= (uint64_t)((mn * 0x00204081u) >> 28) << (4 * k);
+        }
+        auto below = [](int b) -> uint64_t {                // bits [0, b), b clamped to [0, 64]
+            return b <= 0 ? 0ull : (b >= 64 ? ~0ull : (1ull << b) - 1ull);
+        };
+        const uint64_t inw = nlm & below(whi - L0) & ~below(wlo - L0), aft = nlm & ~below(whi - L0);
+        uint32_t cnt = (uint32_t)__popcll(inw);
+        int first = inw ? L0 + (int)__builtin_ctzll(inw) : 0x7fffffff;
+        int endp = aft ? L0 + (int)__builtin_ctzll(aft) : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            cnt += __shfl_xor(cnt, o, 64);
+            first = min(first, __shfl_xor(first, o, 64));
+            endp = min(endp, __shfl_xor(endp, o, 64));
+        }
+        if ((tid & 63) == 0) {
+            atomicAdd(&s_nlw, cnt);
+            atomicMin(&s_first, first);
+            atomicMin(&s_end, endp);
+        }
+        __syncthreads();
+        nr = (int)s_nlw + (c == 0 ? 1 : 0);
+        if (nr == 0 || stop == 4) return;
+        // records before the chunk: record 0 + one per newline in [0, cs - 1)
+        r0 = c == 0 ? 0 : 1 + (int64_t)ca.blk_off[blk0] + (int64_t)s_nlb;
+        lo = c ? s_first + 1 : 0;
+        tail_open = false;
+        if (s_end != 0x7fffffff) {
+            hi = s_end + 1;
+        } else if (wend == nbytes) {
+            hi = (int)(nbytes - a0);                        // the text's last record, without '\n'
+            tail_open = true;
+        } else {
+            hi = -1;                                        // the last record runs past the staged tail
+        }
+        if (hi < 0 || nr > kCsvThreads) {
+            if (tid == 0)
+                ca.spans[atomicAdd(&spill[0], 1u)] = make_longlong4(a0 + lo, hi < 0 ? -1ll : a0 + hi, r0, nr);
+            return;
+        }
     }
     if (stop == 1) { __syncthreads(); if (s_buf[tid] == 0x12345678u) status[0] = 9; return; }
     if (tid < 4) s_cnt[tid] = 0;
@@ -836,7 +947,10 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     }
     const int nf = (int)ftot + (tail_open ? 1 : 0);
     if (nf > kFieldsMax) {                                 // uniform per block
-        if (tid == 0) spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+        if (tid == 0) {
+            if constexpr (CHUNK) ca.spans[atomicAdd(&spill[0], 1u)] = make_longlong4(a0 + lo, a0 + hi, r0, nr);
+            else spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+        }
         return;
     }
     if (tid == 0) {
@@ -976,26 +1090,38 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_slow(const uint8_t *__restr
 
 // ---- fallback: the workgroups k_csv_fields listed (very long records), lane per record from HBM.
 // The group's records are found here: the workgroup scans its span (group boundaries from
-// k_csv_nl_groups) 4 KB at a time for newlines, numbering them by a block scan.
+// k_csv_nl_groups, or a listed chunk's span: its first record, and its end when known) 4 KB at
+// a time for newlines, numbering them by a block scan; a chunk's records go in rounds of 256.
 __global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__restrict__ text, int64_t nbytes,
                                                              const int64_t *__restrict__ line_g, int64_t nl,
                                                              int64_t nrec, int D, int64_t *__restrict__ ids,
                                                              double *__restrict__ vals, uint8_t *__restrict__ status,
                                                              unsigned long long *__restrict__ counts,
                                                              const uint32_t *__restrict__ spill, int64_t all_blocks,
-                                                             int R) {
+                                                             int R, const longlong4 *__restrict__ spans) {
     __shared__ int64_t s_end[kCsvThreads];                 // record j of the group ends at s_end[j] ('\n')
     __shared__ uint32_t s_w[kCsvThreads / 64];
     const int64_t nlist = all_blocks ? all_blocks : (int64_t)spill[0];
     const bool aligned = ((uintptr_t)text & 15) == 0;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int64_t li = blockIdx.x; li < nlist; li += gridDim.x) {
-        const int64_t b = all_blocks ? li : (int64_t)spill[1 + li];
-        const int64_t r0 = b * R;
-        const int nr = (int)(nrec - r0 < R ? nrec - r0 : R);
-        const int64_t span_s = r0 == 0 ? 0 : line_g[b - 1] + 1;
-        const bool tail_open = r0 + nr - 1 >= nl;
-        const int64_t span_e = tail_open || nr < R ? nbytes : line_g[b] + 1;
+      int64_t r0, span_s, span_e, left;
+      if (spans) {
+          const longlong4 sp = spans[li];
+          span_s = sp.x;
+          span_e = sp.y < 0 ? nbytes : sp.y;
+          r0 = sp.z;
+          left = sp.w;
+      } else {
+          const int64_t b = all_blocks ? li : (int64_t)spill[1 + li];
+          r0 = b * R;
+          left = nrec - r0 < R ? nrec - r0 : R;
+          span_s = r0 == 0 ? 0 : line_g[b - 1] + 1;
+          const bool tail_open = r0 + left - 1 >= nl;
+          span_e = tail_open || left < R ? nbytes : line_g[b] + 1;
+      }
+      while (left > 0) {                                   // workgroup-uniform
+        const int nr = (int)(left < kCsvThreads ? left : kCsvThreads);
         uint32_t found = 0;                                // workgroup-uniform
         for (int64_t a = span_s & ~15ll; a < span_e && found < (uint32_t)nr; a += kCsvChunk) {
             const int64_t base = a + threadIdx.x * 16;
@@ -1047,7 +1173,12 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__re
             status[r] = st;
             if (st != SKY_CSV_OK) atomicAdd(&counts[st], 1ull);
         }
-        __syncthreads();                                   // s_end reused by the next group
+        const int64_t next = nr <= (int)found ? s_end[nr - 1] + 1 : nbytes;
+        __syncthreads();                                   // s_end reused by the next round / group
+        r0 += nr;
+        left -= nr;
+        span_s = next;
+      }
     }
 }
 
@@ -1182,11 +1313,45 @@ void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g
                       hipStream_t st) {
     if (nrec == 0) return;
     const int64_t nb = (nrec + R - 1) / R;
-    k_csv_fields<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts,
-                                                      spill, slow, slow_n, slow_cap, R, csv_stop());
+    k_csv_fields<false><<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status,
+                                                             counts, spill, slow, slow_n, slow_cap, R, csv_stop(),
+                                                             CsvChunkArgs{});
     const unsigned g = (unsigned)(nb < 1024 ? nb : 1024);
     k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts, spill, 0,
-                                             R);
+                                             R, nullptr);
+    k_csv_slow<<<1024, kCsvThreads, 0, st>>>(text, slow, slow_n, slow_cap, vals);
+}
+// Chunk mode: bytes per chunk from the average record length and field count, so that a chunk's
+// records fit one workgroup (<= 0.8 x 256 records, 0.8 x kFieldsMax fields), and the staged tail
+// past it (*tail: >= 256 bytes and 4 average records); 0 when the chunk would be under 512 bytes
+int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int *tail) {
+    if (nrec <= 0 || nbytes <= 0) return 0;
+    const double len = (double)nbytes / (double)nrec, nf = (double)nfields / (double)nrec;
+    const double fit = std::min(0.8 * kCsvThreads * len, 0.8 * kFieldsMax / std::max(nf, 1.0) * len);
+    const int t = ((int)std::min(std::max(256.0, 4.0 * len), (double)kFieldText / 2) + 15) & ~15;
+    const int64_t cb = std::min<int64_t>((int64_t)fit, kFieldText - 16 - t) & ~15ll;
+    *tail = t;
+    return cb >= 512 ? (int)cb : 0;
+}
+int64_t csv_chunk_count(int64_t nbytes, int chunk) { return (nbytes + chunk - 1) / chunk; }
+// blk_off: the count pass's exclusive newline counts per 4 KB; spill[0] zeroed (listed spans:
+// spans[0 .. spill[0])), slow_n zeroed
+void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
+                             int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
+                             longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
+                             unsigned long long slow_cap, hipStream_t st) {
+    const int64_t nc = csv_chunk_count(nbytes, chunk);
+    if (nc == 0) return;
+    CsvChunkArgs ca;
+    ca.blk_off = blk_off;
+    ca.spans = spans;
+    ca.chunk = chunk;
+    ca.tail = tail;
+    k_csv_fields<true><<<(unsigned)nc, kCsvThreads, 0, st>>>(text, nbytes, nullptr, 0, 0, D, ids, vals, status, counts,
+                                                            spill, slow, slow_n, slow_cap, 0, csv_stop(), ca);
+    const unsigned g = (unsigned)(nc < 1024 ? nc : 1024);
+    k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, nullptr, 0, 0, D, ids, vals, status, counts, spill, 0, 0,
+                                             spans);
     k_csv_slow<<<1024, kCsvThreads, 0, st>>>(text, slow, slow_n, slow_cap, vals);
 }
 void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec,
@@ -1196,7 +1361,7 @@ void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *
     const int64_t nb = (nrec + kCsvThreads - 1) / kCsvThreads;
     const unsigned g = (unsigned)(nb < 4096 ? nb : 4096);
     k_csv_records<<<g, kCsvThreads, 0, st>>>(text, nbytes, line_g, nl, nrec, D, ids, vals, status, counts, nullptr,
-                                             nb, kCsvThreads);
+                                             nb, kCsvThreads, nullptr);
 }
 // records per k_csv_fields workgroup: as many as fit the LDS windows at the stream's average
 // record length and field count (outliers spill to k_csv_records)

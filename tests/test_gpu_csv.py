@@ -153,6 +153,33 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_csv_chunks_listed_spans(gpu_engine_factory, oracle, monkeypatch):
+    """Byte-chunk parse (SKY_CSV_CHUNKS=1): chunks sized from the text's average record, each
+    workgroup finding its own records; chunks that do not fit go to the fallback as spans: > 256
+    record starts (tiny records), a record running past the staged tail (mid-text and the text's
+    last, with and without a newline), > 2048 fields.  Same results as the default group-pass
+    parse."""
+    rng = random.Random(21)
+    D = 3
+    head = [f"{10 ** 6 + i}," + ",".join(str(rng.randrange(10 ** 5, 10 ** 6)) for _ in range(3)) for i in range(8000)]
+    tiny = ["7"] * 2000 + ["1,2,3,4"] * 1500
+    # > 10 KB (past any chunk's staged tail), every field < 8 KB (the oracle's field limit)
+    longrec = ["5," + ",".join(str(rng.randrange(10 ** 9)) for _ in range(3)) + "," + "1" * 7000 + ",2" + "0" * 4000]
+    wide = ["9," + ",".join(["1"] * 3000)] * 3
+    tail = [f"{i},{i % 7}00000,{i % 5}00000,{i % 3}00000" for i in range(3000)]
+    for body in (head + tiny + longrec + head + wide + tail, head + longrec, head + wide):
+        for end in ("", "\n"):
+            text = ("\n".join(body) + end).encode()
+            assert len(text) / len(body) >= 512 / (0.8 * 256)       # chunk mode is chosen
+            eng = gpu_engine_factory(D, 8)
+            monkeypatch.setenv("SKY_CSV_CHUNKS", "1")
+            n1 = _check(eng, oracle, text, D)
+            monkeypatch.delenv("SKY_CSV_CHUNKS")
+            n0 = _check(eng, oracle, text, D)
+            assert n1 == n0
+            eng.close()
+
+
 def test_csv_halfway_values(gpu_engine_factory, oracle):
     from fractions import Fraction
     rng = random.Random(9)
