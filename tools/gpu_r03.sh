@@ -121,10 +121,15 @@ fi
 if [[ $STEPS == *csvpmc* ]]; then
   # instruction mix of k_csv_fields (one counter pass, kernel trace only), 20M records
   export TMPDIR=/tmp
-  rm -rf $OUT/csvpmc_$TAG
+  rm -rf $OUT/csvpmc_$TAG $OUT/csvpmc2_$TAG
   timeout -k 10 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     --kernel-include-regex k_csv_fields -f csv -d $OUT/csvpmc_$TAG -o run -- python3 -u $R/tools/csv_bench.py 20000000 > $OUT/csvpmc_$TAG.log 2>&1 || { tail -20 $OUT/csvpmc_$TAG.log; exit 1; }
   python tools/prof_summary.py pmcshow $OUT/csvpmc_$TAG k_csv_fields | tee $OUT/csvpmc_${TAG}_summary.txt
+  if [ -n "$CSVPMC2" ]; then
+    timeout -k 10 180 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_ACTIVE_INST_ANY \
+      --kernel-include-regex k_csv_fields -f csv -d $OUT/csvpmc2_$TAG -o run -- python3 -u $R/tools/csv_bench.py 20000000 > $OUT/csvpmc2_$TAG.log 2>&1 || { tail -20 $OUT/csvpmc2_$TAG.log; exit 1; }
+    python tools/prof_summary.py pmcshow $OUT/csvpmc2_$TAG k_csv_fields | tee -a $OUT/csvpmc_${TAG}_summary.txt
+  fi
 fi
 if [[ $STEPS == *csvab* ]]; then
   # the CSV companion (C4 stream as producer text) with the one-pass newline index and without
