@@ -794,6 +794,10 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         }
     };
     int per;
+    uint64_t cm64 = 0, nl64 = 0;                            // CHUNK: the lane's ',' / '\n' bits, unclipped
+    auto below = [](int b) -> uint64_t {                    // bits [0, b), b clamped to [0, 64]
+        return b <= 0 ? 0ull : (b >= 64 ? ~0ull : (1ull << b) - 1ull);
+    };
     if constexpr (!CHUNK) {
         r0 = (int64_t)blockIdx.x * R;                       // R <= 256 records per workgroup (host-chosen)
         nr = (int)(nrec - r0 < R ? nrec - r0 : R);
@@ -855,16 +859,16 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         const int wlo = c ? (int)(cs - 1 - a0) : 0, whi = (int)(ce - 1 - a0);
         // the lane's newlines as one bit per staged byte (as in the delimiter pass below), then the
         // window's count / first and the first at or after whi by popcount / ctz, no bit loops
+        // (the ',' masks too: the delimiter pass below only clips them to [lo, hi))
         const int L0 = 16 * (tid * per);
-        uint64_t nlm = 0;
 #pragma unroll
         for (int k = 0; k < kUnits * 4; k++) {
             const uint32_t mn = k < per * 4 ? byte_eq_mask(dw[k], 0x0a0a0a0au) : 0u;   // unstaged bytes are 0
-            nlm |= (uint64_t)((mn * 0x00204081u) >> 28) << (4 * k);
+            const uint32_t mc = k < per * 4 ? byte_eq_mask(dw[k], 0x2c2c2c2cu) : 0u;
+            nl64 |= (uint64_t)((mn * 0x00204081u) >> 28) << (4 * k);
+            cm64 |= (uint64_t)((mc * 0x00204081u) >> 28) << (4 * k);
         }
-        auto below = [](int b) -> uint64_t {                // bits [0, b), b clamped to [0, 64]
-            return b <= 0 ? 0ull : (b >= 64 ? ~0ull : (1ull << b) - 1ull);
-        };
+        const uint64_t nlm = nl64;
         const uint64_t inw = nlm & below(whi - L0) & ~below(wlo - L0), aft = nlm & ~below(whi - L0);
         uint32_t cnt = (uint32_t)__popcll(inw);
         int first = inw ? L0 + (int)__builtin_ctzll(inw) : 0x7fffffff;
@@ -912,6 +916,15 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     // 23 / 31 -> 28..31, no carries)
     static_assert(kUnits * 16 <= 64, "two 32-bit masks per lane");
     uint32_t md0 = 0, mnl0 = 0, md1 = 0, mnl1 = 0;
+    if constexpr (CHUNK) {                                  // the prologue's masks, clipped to [lo, hi)
+        const int L0 = 16 * (tid * per);
+        const uint64_t clip = below(hi - L0) & ~below(lo - L0);
+        const uint64_t d = (cm64 | nl64) & clip, n = nl64 & clip;
+        md0 = (uint32_t)d;
+        md1 = (uint32_t)(d >> 32);
+        mnl0 = (uint32_t)n;
+        mnl1 = (uint32_t)(n >> 32);
+    } else {
 #pragma unroll
     for (int k = 0; k < kUnits * 4; k++) {
         const int b0 = 16 * (tid * per) + 4 * k;
@@ -928,6 +941,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         const uint32_t nd4 = ((mc | mn) * 0x00204081u) >> 28, nn4 = (mn * 0x00204081u) >> 28;
         if (k < 8) { md0 |= nd4 << (4 * k); mnl0 |= nn4 << (4 * k); }
         else { md1 |= nd4 << (4 * (k - 8)); mnl1 |= nn4 << (4 * (k - 8)); }
+    }
     }
     const uint32_t nd = __popc(md0) + __popc(md1), nn = __popc(mnl0) + __popc(mnl1);
     // block exclusive scans of (nd, nn)
