@@ -493,8 +493,8 @@ void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int
 }
 // SKY_CSV_CHUNKS=1: byte chunks that find their own records and take their first record index from
 // the count pass's prefix, instead of the group pass (every R-th newline) + R records per parse
-// workgroup (A/B knob, read per call; measured slower on the C4 text: parse 4.89 ms against
-// 0.86 + 3.79 ms for groups + parse, profiles/r03_csv_parse_ab.txt)
+// workgroup (A/B knob, read per call; on the C4 text parse 4.55-4.61 ms against 0.86 + 3.81 ms for
+// groups + parse, 2 % less in all, profiles/r03_csv_parse_ab.txt; not yet the default)
 static bool csv_chunk_mode() {
     const char *e = getenv("SKY_CSV_CHUNKS");
     return e && e[0] == '1';
