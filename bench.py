@@ -689,9 +689,13 @@ def main():
     out_ids = torch.empty(n, dtype=torch.int64, device=dev)
     out_org = torch.empty(n, dtype=torch.int32, device=dev)
 
+    dist_phase_log = []
+
     def step():
         if distributed:
-            return distributed_query(eng, ids, vals, out_ids, out_org, n)
+            g = distributed_query(eng, ids, vals, out_ids, out_org, n)
+            dist_phase_log.append(eng.last_dist_phases)     # export / all-gather / merge / finish split
+            return g
         return eng.query_dev(ids, vals, out_ids, out_org, n)
 
     elapsed, step_ms, g, kt = time_steps(step, eng, args.steps, args.warmup, distributed)
@@ -706,6 +710,9 @@ def main():
     phases, counters = eng.phases()
     roof = filter_roofline(eng, D, kt)
     dist_stats = getattr(eng, "last_dist_stats", None) if distributed else None
+    if dist_stats is not None:
+        # the timed steps' phase split (warm-up steps come first, the profiled step last)
+        dist_stats = dict(dist_stats, phases_per_step=dist_phase_log[args.warmup:args.warmup + args.steps])
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps

@@ -1,6 +1,7 @@
 // abi.hip — extern "C" entry points of libskyline_hip.so (include/skyline_hip.h).
 // Status codes only; no exception crosses the boundary.
 #include "abi_common.h"
+#include "knobs.h"
 
 #include <cstring>
 #include <new>
@@ -481,9 +482,6 @@ int sky_profile_reset(sky_ctx *c) {
 
 // ---- bulk CSV ingest (k_csv.hip) ---------------------------------------------
 namespace sky {
-void launch_csv_nl_index(const uint8_t *text, int64_t nbytes, unsigned long long *lb, uint32_t *ticket_err,
-                         uint32_t *blk_off, uint32_t *d_nl, unsigned long long *ncomma, int R, int64_t *line_g,
-                         hipStream_t st);
 int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int *tail);
 int64_t csv_chunk_count(int64_t nbytes, int chunk);
 void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
@@ -496,14 +494,7 @@ void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int
 // workgroup (A/B knob, read per call; on the C4 text parse 4.55-4.61 ms against 0.86 + 3.81 ms for
 // groups + parse, 2 % less in all, profiles/r03_csv_parse_ab.txt; not yet the default)
 static bool csv_chunk_mode() {
-    const char *e = getenv("SKY_CSV_CHUNKS");
-    return e && e[0] == '1';
-}
-// SKY_CSV_ONEPASS=1: the one-pass newline index (k_csv_nl_index) instead of the count, scan and
-// group passes (A/B knob, read per call; measured slower on the C4 text: 1.77 ms for the pass
-// with 64 KB super-chunks, 11 ms with 4 KB chunks, against 0.73 + 0.86 ms for the two passes)
-static bool csv_onepass() {
-    const char *e = getenv("SKY_CSV_ONEPASS");
+    const char *e = SKY_ENV("SKY_CSV_CHUNKS");
     return e && e[0] == '1';
 }
 // ServiceTuple.fromString (ServiceTuple.java:89-104) + filter(nonNull) (FlinkSkyline.java:103)
@@ -529,7 +520,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     std::vector<unsigned long long> h_shards(256, 0);
     // exact-conversion queue (SKY_CSV_SLOW_CAP: tests force the re-parse-everything path)
     static const unsigned long long slow_cap = [] {
-        const char *e = getenv("SKY_CSV_SLOW_CAP");
+        const char *e = SKY_ENV("SKY_CSV_SLOW_CAP");
         return e ? (unsigned long long)std::max(1, atoi(e)) : (1ull << 20);
     }();
     SKY_TRY(c->csv_slow.ensure(slow_cap * sizeof(longlong3)));
@@ -538,48 +529,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     bool direct = false;
     int64_t *pid = d_ids_out;
     double *pval = d_values_out;
-    // one pass (k_csv_nl_index: newline index by decoupled look-back + the group ends for R0, the
-    // records per group estimated from a sample of the text) with SKY_CSV_ONEPASS=1, unless the
-    // pass's look-back gave up; by default count -> scan -> groups
-    int R0 = 0;
-    bool onepass = false;
-    if (nb && csv_onepass()) {
-        const int64_t ns = std::min<int64_t>(nbytes, 64 << 10);
-        std::vector<uint8_t> smp((size_t)ns);
-        HIP_TRY(hipMemcpyAsync(smp.data(), text, (size_t)ns, hipMemcpyDeviceToHost, c->st));
-        HIP_TRY(hipStreamSynchronize(c->st));
-        int64_t snl = 0, scm = 0, send = 0;
-        for (int64_t i = 0; i < ns; i++) {
-            if (smp[i] == '\n') {
-                snl++;
-                send = i + 1;
-            } else if (smp[i] == ',') {
-                scm++;
-            }
-        }
-        if (snl > 0) {
-            R0 = csv_records_per_block(send, snl, scm + snl);
-            SKY_TRY(c->csv_lines.ensure((size_t)(nbytes / R0 + 2) * 8));
-            SKY_TRY(c->csv_lb.ensure((size_t)nb * 8 + 64));
-            unsigned long long *lb = c->csv_lb.as<unsigned long long>();
-            uint32_t *tick = reinterpret_cast<uint32_t *>(lb + nb);
-            HIP_TRY(hipMemsetAsync(lb, 0, (size_t)nb * 8 + 16, c->st));
-            HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
-            c->ktimer_begin("csv_count", c->st);
-            launch_csv_nl_index(text, nbytes, lb, tick, blk_off, d_nl, d_cnt + 8, R0, c->csv_lines.as<int64_t>(),
-                                c->st);
-            c->ktimer_end("csv_count", c->st, nbytes);
-            uint32_t h_err = 0;
-            HIP_TRY(hipMemcpyAsync(h_shards.data(), d_cnt + 8, 256 * 8, hipMemcpyDeviceToHost, c->st));
-            HIP_TRY(hipMemcpyAsync(&h_nl, d_nl, 4, hipMemcpyDeviceToHost, c->st));
-            HIP_TRY(hipMemcpyAsync(&last, text + nbytes - 1, 1, hipMemcpyDeviceToHost, c->st));
-            HIP_TRY(hipMemcpyAsync(&h_err, tick + 1, 4, hipMemcpyDeviceToHost, c->st));
-            HIP_TRY(hipStreamSynchronize(c->st));
-            onepass = h_err == 0;
-        }
-    }
-    if (nb && !onepass) {
-        std::fill(h_shards.begin(), h_shards.end(), 0ull);
+    if (nb) {
         HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
         c->ktimer_begin("csv_count", c->st);
         launch_csv_nl_count(text, nbytes, blk, d_cnt + 8, c->st);
@@ -595,19 +545,15 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     nrec = nl + (nbytes > 0 && last != '\n' ? 1 : 0);
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
     // group boundaries only (R records per parse workgroup; R >= 8, and the exact path's groups of
-    // 256 need fewer): 8 bytes per group instead of per record.  The one pass's groups of R0 serve
-    // when R0 <= R (the sample did not overestimate the records that fit a workgroup's window)
-    int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
+    // 256 need fewer): 8 bytes per group instead of per record
+    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
     SKY_TRY(c->csv_status.ensure(nr1));
     // byte chunks (SKY_CSV_CHUNKS=1): each parse workgroup finds its records itself and takes the
     // index of its first one from the count pass's prefix, so no group pass
     int ctail = 0;
     const int chunk =
-        csv_chunk_mode() && !onepass ? csv_chunk_bytes(nbytes, nrec, (int64_t)h_commas + nrec, &ctail) : 0;
-    if (chunk > 0) {
-    } else if (onepass && R0 <= R) {
-        R = R0;
-    } else {
+        csv_chunk_mode() ? csv_chunk_bytes(nbytes, nrec, (int64_t)h_commas + nrec, &ctail) : 0;
+    if (chunk == 0) {
         SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
         c->ktimer_begin("csv_lines", c->st);
         if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);

@@ -18,6 +18,7 @@
 //                        reach the same decision from the same gathered headers), the output
 //                        count, the summed integers behind the optimality (:593-608)
 #include "abi_common.h"
+#include "knobs.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -28,7 +29,7 @@ namespace {
 // pair tests below which the own-vs-union fates run as one pair kernel over the blocks
 // (SKY_DIST_BRUTE_PAIRS overrides, read per call: tests force the bounding-box route)
 uint64_t dist_brute_pairs() {
-    const char *e = getenv("SKY_DIST_BRUTE_PAIRS");
+    const char *e = SKY_ENV("SKY_DIST_BRUTE_PAIRS");
     return e ? strtoull(e, nullptr, 10) : (1ull << 28);
 }
 
@@ -108,7 +109,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     if (!n_own || h[0] > (unsigned long long)cap) return SKY_OK;   // overflow: sky_dist_finish re-runs
     if ((uint64_t)n_own * n_union <= dist_brute_pairs()) {
         launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, c->main.dist_own.as<uint8_t>(), lsz, surv,
-                               st);
+                               sum, ~0ull, nullptr, st);
         return SKY_OK;
     }
     const uint32_t fl = (uint32_t)h[5];
@@ -272,13 +273,14 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
     const int D = c->D;
     const int K = c->Kq();
     SKY_TRY(c->dist_sum.ensure((size_t)(16 + world) * 8));   // [0..15] summary, [16..] offsets
-    SKY_TRY(p.statk.ensure((size_t)K * 16));
+    SKY_TRY(p.statk.ensure((size_t)SKY_DIST_STATS_WORDS(K) * 8));
     SKY_TRY(p.dist_own.ensure((size_t)std::max<int64_t>(cap, 1)));
     unsigned long long *sum = c->dist_sum.as<unsigned long long>();
     unsigned long long *lsz = p.statk.as<unsigned long long>(), *surv = lsz + K;
+    unsigned long long *w_miss = lsz + 2 * K, *w_err = lsz + 2 * K + 1;   // summed over the ranks
     const uint32_t tiles = (p.n + kTile - 1) / kTile;
     FillSet fill;
-    fill.add(p.statk.p, (size_t)K * 16);
+    fill.add(p.statk.p, (size_t)SKY_DIST_STATS_WORDS(K) * 8);
     fill.add(c->dist_sum.p, 128);
     if (p.hist_count && c->dist_state == 1 && tiles) fill.add(p.tile_cand.p, (size_t)tiles * 4);
     HIP_TRY(fill.launch(st));
@@ -288,10 +290,18 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
     if (c->dist_state == 1 && p.n) {
         // ---- own vectors against the union: one pair kernel over the blocks while the last
         //      step's |own| x |union| was small, else (and on the first step) the sized route
-        const bool brute = c->dist_hist_pairs >= 0 && (uint64_t)c->dist_hist_pairs <= dist_brute_pairs();
+        //      (the capacity only grows: if cap x world x cap could exceed the route's bound, the
+        //      kernel checks this step's sizes on the device and, when they are too large, writes
+        //      no fate and raises the route-miss word: every rank returns SKY_E_RETRY, this one
+        //      then takes the sized route)
+        const uint64_t bp = dist_brute_pairs();
+        const bool brute = c->dist_hist_pairs >= 0 && (uint64_t)c->dist_hist_pairs <= bp;
         if (brute) {
+            const unsigned __int128 worst = (unsigned __int128)(uint64_t)cap * (uint64_t)cap * (uint64_t)world;
+            const unsigned long long limit = worst <= bp ? ~0ull : (unsigned long long)bp;
             c->ktimer_begin("union_fate", st);
-            launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, p.dist_own.as<uint8_t>(), lsz, surv, st);
+            launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, p.dist_own.as<uint8_t>(), lsz, surv, sum,
+                                   limit, w_miss, st);
             c->ktimer_end("union_fate", st, 0);
             c->dist_last_route = 0;
         } else {
@@ -356,8 +366,10 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
         }
         c->ktimer_end("out", st, p.n);
     }
-    // this rank's shares for the caller's all-reduce
-    HIP_TRY(hipMemcpyAsync(d_stats, p.statk.p, (size_t)K * 16, hipMemcpyDeviceToDevice, st));
+    // merge-time errors (the union pass's look-backs) into the summed words, then this rank's
+    // shares for the caller's all-reduce
+    launch_dist_merge_err(p.flags.as<uint32_t>(), w_err, st);
+    HIP_TRY(hipMemcpyAsync(d_stats, p.statk.p, (size_t)SKY_DIST_STATS_WORDS(K) * 8, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipGetLastError());
     c->dist_world = world;
     c->dist_merged = true;
@@ -376,11 +388,11 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
     if (need_cap) *need_cap = 0;
     unsigned long long sum[16] = {};
     uint32_t tot[16] = {}, flags = 0;
-    std::vector<int64_t> st((size_t)K * 2);
+    std::vector<int64_t> st((size_t)SKY_DIST_STATS_WORDS(K));
     const int KM = p.Kp * p.M;
     p.h_dup.assign(KM, 0u);
     SKY_TRY(sync_read(p, c->st,
-                      {{c->dist_sum.p, 128}, {p.totals.p, 64}, {p.flags.p, 4}, {d_stats_sum, (size_t)K * 16},
+                      {{c->dist_sum.p, 128}, {p.totals.p, 64}, {p.flags.p, 4}, {d_stats_sum, (size_t)SKY_DIST_STATS_WORDS(K) * 8},
                        {p.dup_cnt.p, p.n ? (size_t)KM * 4 : 0}},
                       {sum, tot, &flags, st.data(), p.h_dup.data()}));
     if (p.n) pick_dom_group(p, KM);
@@ -407,7 +419,10 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
         if ((size_t)tot[0] + tot[5] > p.dist_pc.cap)
             p.slot_hint = std::min<size_t>((size_t)p.n + KM, ((size_t)tot[0] + tot[5]) * 5 / 4 + KM);
     }
-    if ((any & kDistError) || (flags & kFlagRadixSpin)) {
+    // every code below comes from data identical on every rank (the gathered headers, the
+    // all-reduced words), so every rank returns the same one
+    const int64_t route_miss = st[2 * K], merge_err = st[2 * K + 1];
+    if ((any & kDistError) || merge_err > 0) {
         set_error("a look-back exceeded its spin bound on some rank");
         return SKY_E_HIP;
     }
@@ -419,6 +434,11 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
         set_error("a rank's planned local phase missed its assumptions: run the step again");
         return SKY_E_RETRY;
     }
+    if (route_miss > 0 && (int64_t)sum[0] <= c->dist_cap) {
+        set_error("a rank's union was too large for the pair-kernel route it took from the last step: run the step "
+                  "again");
+        return SKY_E_RETRY;
+    }
     if ((int64_t)sum[0] > c->dist_cap) {
         if (need_cap) *need_cap = (int64_t)sum[0];
         set_error("exchange capacity " + std::to_string(c->dist_cap) + " < exported vectors " + std::to_string(sum[0]));
@@ -428,7 +448,7 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
     if (n_out) *n_out = g;
     c->K_last = K;
     c->lsz.assign(st.begin(), st.begin() + K);
-    c->surv.assign(st.begin() + K, st.end());
+    c->surv.assign(st.begin() + K, st.begin() + 2 * K);
     c->counters[0] = p.n;
     c->counters[1] = p.m;
     c->counters[2] = p.mr;

@@ -74,7 +74,7 @@ struct Ctx {
     DevBuf dist_sum;            // the merge's summary of every block header (u64 words)
     DevBuf dist_union, dist_ukey, dist_umult, dist_uflags;   // the compacted union (bounding-box path)
     // bulk CSV ingest workspace (k_csv.hip)
-    DevBuf csv_blk, csv_lb, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow,
+    DevBuf csv_blk, csv_scr, csv_lines, csv_status, csv_counts, csv_ids, csv_vals, csv_keep, csv_pos, csv_text, csv_slow,
         csv_spans;
     DevBuf prof_k, prof_v, prof_scr;   // sky_profile_sort_dev workspace
     // batched per-key inserts (sky_parts_insert): the call's upload (descriptors, work items,

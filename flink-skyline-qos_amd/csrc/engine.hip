@@ -8,6 +8,7 @@
 // Host synchronisations happen only where the host must size the next launch
 // (candidate count, representative count, per-round SFS segment counts).
 #include "engine.h"
+#include "knobs.h"
 #include "ctx.h"
 
 #include <algorithm>
@@ -42,7 +43,7 @@ int DevBuf::ensure(size_t bytes) {
     size_t want = std::max<size_t>(bytes, 256);
     if (regrow) want = std::max(want, bytes + bytes / 2);
     want = (want + 4095) & ~size_t(4095);
-    static const bool trace_alloc = getenv("SKY_TRACE_ALLOC") != nullptr;   // measurement only
+    static const bool trace_alloc = SKY_MEASURE_ENV("SKY_TRACE_ALLOC") != nullptr;   // measurement only
     auto t0 = std::chrono::steady_clock::now();
     const hipError_t me = hipMalloc(&p, want);
     if (trace_alloc)
@@ -60,7 +61,7 @@ int DevBuf::ensure(size_t bytes) {
 }
 
 void DevBuf::release() {
-    static const bool trace_alloc = getenv("SKY_TRACE_ALLOC") != nullptr;   // measurement only
+    static const bool trace_alloc = SKY_MEASURE_ENV("SKY_TRACE_ALLOC") != nullptr;   // measurement only
     if (p) {
         auto t0 = std::chrono::steady_clock::now();
         (void)hipFree(p);
@@ -128,7 +129,7 @@ int Pipe::pinned(size_t bytes) {
 // SKY_DEBUG=1: synchronise and check after every stage, naming the stage
 static int debug_level() {
     static int lvl = [] {
-        const char *e = getenv("SKY_DEBUG");
+        const char *e = SKY_MEASURE_ENV("SKY_DEBUG");
         return e ? atoi(e) : 0;
     }();
     return lvl;
@@ -136,17 +137,17 @@ static int debug_level() {
 // SKY_SFS16=0 forces the generic f32/f64 SFS (read per query: the tests compare the
 // two paths in one process)
 static bool sfs16_disabled() {
-    const char *e = getenv("SKY_SFS16");
+    const char *e = SKY_ENV("SKY_SFS16");
     return e && atoi(e) == 0;
 }
 // SKY_PREFILTER=0 skips the candidate prefilter (A/B knob; read per query)
 static bool prefilter_disabled() {
-    const char *e = getenv("SKY_PREFILTER");
+    const char *e = SKY_ENV("SKY_PREFILTER");
     return e && atoi(e) == 0;
 }
 static int prefilter_m2() {   // second-level pruners per partition (SKY_PREFILTER_M2, default 16)
     static const int m = [] {
-        const char *e = getenv("SKY_PREFILTER_M2");
+        const char *e = SKY_MEASURE_ENV("SKY_PREFILTER_M2");
         const int v = e ? atoi(e) : 16;
         return v < 1 ? 1 : (v > 64 ? 64 : v);
     }();
@@ -155,30 +156,30 @@ static int prefilter_m2() {   // second-level pruners per partition (SKY_PREFILT
 constexpr uint32_t kPrefilterMin = 4096;
 // candidate slots of a first run (SKY_SLOT_MIN overrides: tests force the overflow re-run)
 static size_t slot_min() {
-    const char *e = getenv("SKY_SLOT_MIN");
+    const char *e = SKY_ENV("SKY_SLOT_MIN");
     return e ? (size_t)std::max(1, atoi(e)) : (size_t(1) << 20);
 }
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
-    const char *e = getenv("SKY_FUSED_OUT");
+    const char *e = SKY_ENV("SKY_FUSED_OUT");
     return e && atoi(e) == 0;
 }
 static bool fused_onepass() {   // SKY_FUSED_OUT=2: the one-pass look-back output kernel
-    const char *e = getenv("SKY_FUSED_OUT");
+    const char *e = SKY_ENV("SKY_FUSED_OUT");
     return e && atoi(e) == 2;
 }
 static bool hist_disabled() {   // SKY_HIST_COUNT=0: the status-word count pass (A/B knob)
-    const char *e = getenv("SKY_HIST_COUNT");
+    const char *e = SKY_MEASURE_ENV("SKY_HIST_COUNT");
     return e && e[0] == '0';
 }
 // SKY_PLANES=0: the filter stores every status word (A/B knob, read per query)
 static bool planes_disabled() {
-    const char *e = getenv("SKY_PLANES");
+    const char *e = SKY_MEASURE_ENV("SKY_PLANES");
     return e && e[0] == '0';
 }
 // SKY_PLAN=0: every query takes the host-synchronised route (A/B knob, read per query)
 static bool plan_disabled() {
-    const char *e = getenv("SKY_PLAN");
+    const char *e = SKY_ENV("SKY_PLAN");
     return e && e[0] == '0';
 }
 // a device-sized launch's bound for a count the last query saw
@@ -186,11 +187,11 @@ static uint32_t plan_bound(uint32_t x) { return x + x / 4 + 1024u; }
 // SKY_MBR=0 keeps the round-based SFS for large rep sets (A/B knob, read per query);
 // SKY_MBR_MIN: smallest rep count for the bounding-box pruned all-pairs pass
 static bool mbr_disabled() {
-    const char *e = getenv("SKY_MBR");
+    const char *e = SKY_ENV("SKY_MBR");
     return e && atoi(e) == 0;
 }
 static uint32_t mbr_min() {
-    const char *e = getenv("SKY_MBR_MIN");
+    const char *e = SKY_ENV("SKY_MBR_MIN");
     return e ? (uint32_t)atoi(e) : 16384u;
 }
 // Up to 32768 slots the brute pair pass (one 64 x 64 block pair per workgroup, no sort or
@@ -198,24 +199,24 @@ static uint32_t mbr_min() {
 // few hundred waves on 1024 SIMDs (C5 sliding window: 21-25k reps took 0.6-0.85 ms there).
 uint32_t brute_max() {
     static const uint32_t v = [] {
-        const char *e = getenv("SKY_BRUTE_MAX");
+        const char *e = SKY_MEASURE_ENV("SKY_BRUTE_MAX");
         const long x = e ? atol(e) : 32768;
         return (uint32_t)std::min<long>(std::max<long>(x, 64), 1 << 20);
     }();
     return v;
 }
 static bool brute_disabled() {
-    const char *e = getenv("SKY_BRUTE");
+    const char *e = SKY_ENV("SKY_BRUTE");
     return e && atoi(e) == 0;
 }
 // SKY_BRUTE16=0: the small-set pair pass compares f32 even for integer rows (A/B knob)
 static bool brute16_disabled() {
-    const char *e = getenv("SKY_BRUTE16");
+    const char *e = SKY_ENV("SKY_BRUTE16");
     return e && atoi(e) == 0;
 }
 // SKY_GATHER=0 reads counters back by one hipMemcpyAsync per range (A/B knob)
 static bool gather_disabled() {
-    const char *e = getenv("SKY_GATHER");
+    const char *e = SKY_ENV("SKY_GATHER");
     return e && atoi(e) == 0;
 }
 static int stage_check(hipStream_t st, const char *where) {
@@ -601,7 +602,7 @@ int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *,
 
 // SKY_MBR_LPT=0: the pair pass takes its y tiles in blockIdx order (A/B knob, read per query)
 bool mbr_lpt_enabled() {
-    const char *e = getenv("SKY_MBR_LPT");
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_LPT");
     return !(e && e[0] == '0');
 }
 
@@ -651,15 +652,12 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.gmerge = gmerge;
     a.full = fmt != 0 || in.keys != nullptr;   // ±0 twins (f32/f64) or vectors repeated across given keys
     {
-        const char *e = getenv("SKY_MBR_DBG");
+        const char *e = SKY_MEASURE_ENV("SKY_MBR_DBG");
         a.dbg = e ? atoi(e) : 0;
         // x-tile ranges per y tile: a small rep set has few 64-row y tiles (20k reps: ~330 waves
-        // on 1024 SIMDs), so its groups are split over more waves (domf is OR-ed atomically);
-        // SKY_MBR_SPLIT overrides (A/B knob)
-        const char *sp = getenv("SKY_MBR_SPLIT");
+        // on 1024 SIMDs), so its groups are split over more waves (domf is OR-ed atomically)
         const uint32_t nt = (uint32_t)mbr_tiles(mr), ng = (uint32_t)mbr_groups(mr);
-        const uint32_t auto_split = std::min<uint32_t>(ng, std::max<uint32_t>(1u, (4096u + nt - 1) / nt));
-        a.nsplit = sp ? std::max(1, atoi(sp)) : (int)auto_split;
+        a.nsplit = (int)std::min<uint32_t>(ng, std::max<uint32_t>(1u, (4096u + nt - 1) / nt));
     }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
@@ -1205,7 +1203,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
     fa.dom_kj = p.dom_kj;
     {
-        static const int fdbg = [] { const char *e = getenv("SKY_FILTER_DBG"); return e ? atoi(e) : 0; }();
+        static const int fdbg = [] { const char *e = SKY_MEASURE_ENV("SKY_FILTER_DBG"); return e ? atoi(e) : 0; }();
         fa.dbg = fdbg;
     }
     const bool angle_keys = !in.single && !in.keys && c.algo == SKY_ALGO_ANGLE;

@@ -7,9 +7,6 @@
 // Records are '\n'-separated "id,v1,...,vD" (one Kafka value each in the reference).
 //
 // Passes (all HBM-streaming byte work, no MFMA):
-//   k_csv_nl_index  (SKY_CSV_ONEPASS=1, measured slower) one pass: newline index by decoupled
-//                   look-back over 64 KB super-chunks + the group ends for an R from a sample of
-//                   the text; by default the two passes:
 //   k_csv_nl_count  per 4 KB chunk: number of '\n' (16 B per lane, one vector load)
 //   scan            chunk offsets (k_scan.hip)
 //   k_csv_nl_groups positions of every R-th '\n' -> line_g[] (group boundaries, R records per
@@ -22,6 +19,7 @@
 //                   against the halfway points, __noinline__ and rare), Long.parseLong.
 //   k_csv_compact   only if some record was rejected: stable compaction of the rows.
 #include "sky_internal.h"
+#include "knobs.h"
 #include <algorithm>
 #include <cstdlib>
 
@@ -130,145 +128,6 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_groups(const uint8_t *__
                 break;
             }
             t -= ck;
-        }
-    }
-}
-
-// ONE pass instead of count -> scan -> groups (each a full read of the text): super-chunks of
-// kNlSub 4 KB chunks are taken in launch order from a ticket; each counts its newlines, publishes
-// the count and looks back over its predecessors for its exclusive newline index (decoupled
-// look-back: wave 0 reads a window of 64 predecessors' status words at once, bounded spin), then
-// re-reads its text (L2-hot) and writes the group ends for a record count per group R chosen from a
-// sample of the text before the pass.  Also writes every 4 KB chunk's exclusive offset (blk_off)
-// and the total (d_nl), so that a different R can still be served by k_csv_nl_groups.
-// (With one 4 KB chunk per workgroup and a one-predecessor look-back the chain of 892k links took
-// 11 ms for 3.65 GB of text, against 1.6 ms for the two passes.)
-constexpr unsigned long long kNlAgg = 1ull << 62, kNlInc = 2ull << 62, kNlVal = (1ull << 62) - 1;
-constexpr int kNlSub = 16;                              // 4 KB chunks per super-chunk (64 KB)
-__global__ __launch_bounds__(kCsvThreads) void k_csv_nl_index(const uint8_t *__restrict__ text, int64_t nbytes,
-                                                              bool aligned, int64_t nb, int64_t nsup,
-                                                              unsigned long long *__restrict__ lb,
-                                                              uint32_t *__restrict__ ticket_err,
-                                                              uint32_t *__restrict__ blk_off, uint32_t *__restrict__ d_nl,
-                                                              unsigned long long *__restrict__ ncomma, uint32_t R,
-                                                              int64_t *__restrict__ line_g) {
-    __shared__ uint32_t s_w[kNlSub][kCsvThreads / 64];    // newlines per (sub-chunk, wave)
-    __shared__ uint32_t s_c[kCsvThreads / 64];
-    __shared__ uint32_t s_sup;
-    __shared__ unsigned long long s_pre;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) s_sup = atomicAdd(&ticket_err[0], 1u);
-    __syncthreads();
-    const int64_t sup = s_sup;
-    // 1. count
-    uint32_t cm = 0;
-#pragma unroll 4
-    for (int k = 0; k < kNlSub; k++) {
-        const int64_t base = (sup * kNlSub + k) * kCsvChunk + tid * 16;
-        uint32_t w[4];
-        load16(text, nbytes, base, aligned, w);
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            c += __popc(nl_in_word(w[q]));
-            cm += __popc(byte_eq_mask(w[q], 0x2c2c2c2cu));
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) s_w[k][wv] = c;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cm += __shfl_xor(cm, o, 64);
-    if (lane == 0) s_c[wv] = cm;
-    __syncthreads();
-    // 2. publish + look back (wave 0)
-    if (wv == 0) {
-        unsigned long long agg = 0;
-        for (int k = 0; k < kNlSub; k++) agg += s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
-        unsigned long long *mine = lb + sup;
-        unsigned long long excl = 0;
-        if (sup == 0) {
-            if (lane == 0) __hip_atomic_store(mine, kNlInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(mine, kNlAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t end = sup;                             // the window is [end - 64, end)
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t pc = end - 1 - lane;
-                const unsigned long long sv =
-                    pc >= 0 ? __hip_atomic_load(lb + pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kNlInc;
-                const unsigned long long f = sv & ~kNlVal;
-                const uint64_t incm = __ballot(f == kNlInc), zerom = __ballot(f == 0ull);
-                const int first = incm ? __ffsll((long long)incm) - 1 : 63;   // nearest inclusive (or the window)
-                const uint64_t upto = first == 63 ? ~0ull : ((2ull << first) - 1ull);
-                if (zerom & upto) {                        // a predecessor has not published yet
-                    if (++spins > (1u << 22)) {
-                        if (lane == 0) atomicOr(&ticket_err[1], 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                unsigned long long v = ((upto >> lane) & 1ull) ? (sv & kNlVal) : 0ull;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-                    v += ((unsigned long long)hi << 32) | lo;
-                }
-                excl += v;
-                if (incm) break;
-                end -= 64;
-            }
-            if (lane == 0) __hip_atomic_store(mine, kNlInc | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_pre = excl;
-            unsigned long long o = excl;
-            for (int k = 0; k < kNlSub; k++) {             // every 4 KB chunk's exclusive offset
-                const int64_t ch = sup * kNlSub + k;
-                if (ch < nb) blk_off[ch] = (uint32_t)o;
-                o += s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
-            }
-            if (sup == nsup - 1) *d_nl = (uint32_t)(excl + agg);
-            const uint32_t tc = s_c[0] + s_c[1] + s_c[2] + s_c[3];
-            if (tc) atomicAdd(&ncomma[sup & (kCommaShards - 1)], (unsigned long long)tc);
-        }
-    }
-    __syncthreads();
-    if (R == 0) return;
-    // 3. group ends (the text again, from L2)
-    uint32_t run = (uint32_t)s_pre;
-    for (int k = 0; k < kNlSub; k++) {
-        const int64_t base = (sup * kNlSub + k) * kCsvChunk + tid * 16;
-        uint32_t wbase = run;
-        for (int i = 0; i < wv; i++) wbase += s_w[k][i];
-        run += s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
-        uint32_t w[4], m[4];
-        load16(text, nbytes, base, aligned, w);
-        uint32_t c = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) { m[q] = nl_in_word(w[q]); c += __popc(m[q]); }
-        uint32_t inc = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += t;
-        }
-        if (!c) continue;
-        const uint32_t g0 = wbase + inc - c;               // index of this thread's first newline
-        for (uint32_t q = (g0 / R + 1) * R - 1; q < g0 + c; q += R) {
-            uint32_t t = q - g0;
-#pragma unroll
-            for (int k2 = 0; k2 < 4; k2++) {
-                const uint32_t ck = __popc(m[k2]);
-                if (t < ck) {
-                    uint32_t mk = m[k2];
-                    for (uint32_t u = 0; u < t; u++) mk &= mk - 1;
-                    line_g[(q + 1) / R - 1] = base + k2 * 4 + ((__ffs(mk) - 1) >> 3);
-                    break;
-                }
-                t -= ck;
-            }
         }
     }
 }
@@ -1304,18 +1163,8 @@ void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *b
     const bool aligned = ((uintptr_t)text & 15) == 0;
     k_csv_nl_groups<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_off, (uint32_t)R, line_g);
 }
-void launch_csv_nl_index(const uint8_t *text, int64_t nbytes, unsigned long long *lb, uint32_t *ticket_err,
-                         uint32_t *blk_off, uint32_t *d_nl, unsigned long long *ncomma, int R, int64_t *line_g,
-                         hipStream_t st) {
-    const int64_t nb = csv_chunks(nbytes);
-    if (nb == 0) return;
-    const int64_t nsup = (nb + kNlSub - 1) / kNlSub;
-    const bool aligned = ((uintptr_t)text & 15) == 0;
-    k_csv_nl_index<<<(unsigned)nsup, kCsvThreads, 0, st>>>(text, nbytes, aligned, nb, nsup, lb, ticket_err, blk_off,
-                                                          d_nl, ncomma, (uint32_t)R, line_g);
-}
 static int csv_stop() {
-    const char *e = getenv("SKY_CSV_STOP");
+    const char *e = SKY_MEASURE_ENV("SKY_CSV_STOP");
     return e ? atoi(e) : 0;
 }
 // spill: device u32 [1 + blocks], spill[0] zeroed by the caller; slow: queue of exact

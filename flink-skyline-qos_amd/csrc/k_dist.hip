@@ -222,11 +222,21 @@ __global__ __launch_bounds__(kThreads) void k_dist_pack(const double *__restrict
 // in L_k / G (FlinkSkyline.java:593-608), summed over the ranks by the caller's all-reduce.
 constexpr int kDistTile = 256;
 template <int D>
+// limit: the route was chosen from the previous step's sizes; if this step's |own| x |union|
+// (k_dist_summary's sum[4] x sum[3]) exceeds it, no fate is written and *miss = 1 (the caller's
+// all-reduce carries it: every rank returns SKY_E_RETRY and this rank re-runs on the sized route).
 __global__ __launch_bounds__(kThreads) void k_dist_union_fate(const int64_t *__restrict__ blocks, int world, int rank,
                                                               uint32_t cap, int K, uint8_t *__restrict__ flags,
                                                               unsigned long long *__restrict__ lsz,
-                                                              unsigned long long *__restrict__ surv) {
+                                                              unsigned long long *__restrict__ surv,
+                                                              const unsigned long long *__restrict__ sum,
+                                                              unsigned long long limit,
+                                                              unsigned long long *__restrict__ miss) {
     constexpr int RW = D + 2;
+    if (sum[4] * sum[3] > limit) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *miss = 1ull;
+        return;
+    }
     __shared__ double s_x[kDistTile * D];
     __shared__ double s_s[kDistTile];
     __shared__ int32_t s_k[kDistTile];
@@ -349,10 +359,20 @@ void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *
 }
 
 void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
-                            unsigned long long *lsz, unsigned long long *surv, hipStream_t st) {
+                            unsigned long long *lsz, unsigned long long *surv, const unsigned long long *sum,
+                            unsigned long long limit, unsigned long long *miss, hipStream_t st) {
     if (!cap) return;
-    SKY_DISPATCH_D(D, (k_dist_union_fate<DD><<<nblk_d(cap, kThreads), kThreads, 0, st>>>(blocks, world, rank, cap, K,
-                                                                                        flags, lsz, surv)));
+    SKY_DISPATCH_D(D, (k_dist_union_fate<DD><<<nblk_d(cap, kThreads), kThreads, 0, st>>>(
+                          blocks, world, rank, cap, K, flags, lsz, surv, sum, limit, miss)));
+}
+
+// merge-time errors into the all-reduced stat words: a look-back that exceeded its spin bound in
+// the union pass (flags, kFlagRadixSpin) -> err = 1 (every rank then returns SKY_E_HIP)
+__global__ void k_dist_merge_err(const uint32_t *__restrict__ flags, unsigned long long *__restrict__ err) {
+    if (threadIdx.x == 0) *err = (flags[0] & kFlagRadixSpin) ? 1ull : 0ull;
+}
+void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st) {
+    k_dist_merge_err<<<1, 64, 0, st>>>(flags, err);
 }
 
 void launch_dist_alive_g(const uint32_t *flag, const uint32_t *pos, uint32_t n, const uint8_t *own_flags, uint32_t cap,

@@ -22,6 +22,7 @@
 // Work items are (segment, 64*PPT y, <= kDomTx x) tiles, one wave each; a tile
 // whose y are all dead skips its remaining x.
 #include <cstdlib>
+#include "knobs.h"
 
 #include "sky_internal.h"
 
@@ -353,23 +354,22 @@ void launch_pack16(int D, const float *rows, uint32_t m, const uint32_t *idx, ui
 
 // SKY_DOM_PPT in {4, 8} (y rows per lane of the rest tiles; tri tiles use 1), SKY_DOM_R in {2, 4} (x rows per
 // scalar-load batch) or 64 (vector batches + v_readlane): tuning knobs, defaults measured on the MI355X
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
+static int env_int(const char *e, int dflt) {
     return e ? atoi(e) : dflt;
 }
 int dom16_ppt() {
     static int v = [] {
-        const int p = env_int("SKY_DOM_PPT", 4);
+        const int p = env_int(SKY_MEASURE_ENV("SKY_DOM_PPT"), 4);
         return p == 8 ? 8 : 4;
     }();
     return v;
 }
 uint32_t dom16_tx() {                          // 0: adaptive (sfs_run16)
-    const int t = env_int("SKY_DOM_TX", 0);
+    const int t = env_int(SKY_MEASURE_ENV("SKY_DOM_TX"), 0);
     return t >= 64 && t <= 4096 ? (uint32_t)t : 0u;
 }
 static int dom16_r() {
-    const int r = env_int("SKY_DOM_R", 4);
+    const int r = env_int(SKY_MEASURE_ENV("SKY_DOM_R"), 4);
     return r == 2 || r == 64 ? r : 4;
 }
 

@@ -25,6 +25,7 @@
 // its rows, so a skipped tile holds no dominator.  On the labelled std-anti 8D stream about
 // 2 % of the tile pairs survive the box test (tools/mbr_sim note in DESIGN.md §2.2).
 #include "sky_internal.h"
+#include "knobs.h"
 
 namespace sky {
 
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__re
 // The y tiles (ytrows / ytpart / ytmax / ytprange, ymr rows) may be another set than the x
 // tiles (the multi-GPU merge: own vectors against the union, FULL only); for one set they are
 // the same arrays.
-template <class R, bool FULL, bool GM, bool PIPE, bool BC = false>
+template <class R, bool FULL, bool GM, bool PIPE>
 __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
@@ -528,34 +529,6 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         if (!lm) return;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         ntested++;
-        if constexpr (BC) {
-            // lane = x row (in registers since load_tile); each reachable y is broadcast from its
-            // lane (readlane -> scalar operands) and compared with all 64 rows at once: no LDS
-            // staging, no barrier, and the y's are independent of each other
-            const bool xvalid = (uint32_t)lane < nx;
-            uint64_t h_any = 0, h_same = 0, m = lm;
-            npairs += 64ull * (uint64_t)__popcll(m);
-            if (dbg & 1) return;
-            while (m) {
-                const uint32_t yb = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
-                uint32_t yv[NW];
-#pragma unroll
-                for (int w = 0; w < NW; w++) yv[w] = (uint32_t)__builtin_amdgcn_readlane((int)y[w], (int)yb);
-                const uint32_t pyv = (uint32_t)__builtin_amdgcn_readlane((int)py, (int)yb);
-                bool dom = xvalid & R::le(xv, yv);
-                if constexpr (FULL) dom = dom & !R::le(yv, xv);
-                else dom = dom & !(xt == yt && (uint32_t)lane == yb);
-                const uint64_t hm = __ballot(dom);
-                if (hm) {
-                    h_any |= 1ull << yb;
-                    if (__ballot(dom & (px == pyv))) h_same |= 1ull << yb;
-                }
-            }
-            f |= ((h_same >> lane) & 1ull) ? 3u : (((h_any >> lane) & 1ull) ? 2u : 0u);
-            live &= __ballot(!(f & 1u));
-            return;
-        }
         uint64_t ms[4];
         uint32_t E = 0;
 #pragma unroll
@@ -770,16 +743,9 @@ int mbr_row_words(int D, int fmt) {
     return 2 * padded_dims<double>(D);
 }
 
-// SKY_MBR_BCAST=1: each reachable y broadcast (readlane) against the whole x tile instead of the
-// 16-row sub-box entries staged in LDS (A/B knob; measured slower: std-anti 8D 2M 9.2 vs 7.4 ms,
-// 10M 58 vs 30 ms -- 6x the pair tests outweigh the saved LDS staging)
-static bool mbr_bcast() {
-    const char *e = getenv("SKY_MBR_BCAST");
-    return e && atoi(e) == 1;
-}
 // SKY_MBR_ORDER=morton: the Morton order of round 2 (A/B knob, read per build)
 static bool mbr_hilbert() {
-    const char *e = getenv("SKY_MBR_ORDER");
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_ORDER");
     return !(e && e[0] == 'm');
 }
 
@@ -837,7 +803,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
     if (a.lpt) mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    (mbr_bcast() ? k_mbr_pairs<R, F, G, true, true> : k_mbr_pairs<R, F, G, true>)                              \
+    k_mbr_pairs<R, F, G, true>                              \
         <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
                                                   a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt)
     if (a.full) {
@@ -886,7 +852,7 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     const unsigned gp = ((nyt + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64) + 7) / 8 * 8;
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
     if (y.lpt) mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
-    (mbr_bcast() ? k_mbr_pairs<R, true, true, true, true> : k_mbr_pairs<R, true, true, true>)<<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+    k_mbr_pairs<R, true, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
                                                         y.domf, x.pairs, y.lpt);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,

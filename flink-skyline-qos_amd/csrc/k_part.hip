@@ -21,7 +21,6 @@
 // any launch (SKY_E_NAN), so the state never sees it.
 #include "sky_internal.h"
 
-#include <hip/hip_cooperative_groups.h>
 
 #include <algorithm>
 
@@ -631,91 +630,9 @@ void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_
     k_pgm_write<<<g, kThreads, 0, st>>>(lists, nl, ttot, tsel, tpos, ids_out, org_out);
 }
 
-// The whole insert as ONE cooperative launch: the six phases above, separated by grid-wide
-// barriers, each workgroup looping over the phase's (slice, part) tasks / pair work items.
-// SKY_PART_COOP=1 (A/B knob, off by default): measured on the C4 10M prefix it saved ~8 us of the
-// ~40 us of API calls per insert call, but the five grid barriers made the GPU side ~3x longer
-// (the host then waited ~100 us per call for a staging slot): 61M vs 110M tuples/s.
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_parts_all(const PartDesc *__restrict__ descs, uint32_t nparts,
-                                                        uint32_t max_sl, const PartItem *__restrict__ items,
-                                                        uint32_t nitems) {
-    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-    const uint32_t ntask = nparts * max_sl, G = gridDim.x;
-    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
-        parts_crit<D>(descs, t % max_sl, t / max_sl, max_sl);
-        __syncthreads();
-    }
-    grid.sync();
-    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
-        parts_classify<D>(descs, t % max_sl, t / max_sl, max_sl);
-        __syncthreads();
-    }
-    grid.sync();
-    for (uint32_t i = blockIdx.x; i < nitems; i += G) {
-        parts_pairs<D>(descs, items, i);
-        __syncthreads();
-    }
-    grid.sync();
-    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
-        parts_count<D>(descs, t % max_sl, t / max_sl, max_sl);
-        __syncthreads();
-    }
-    grid.sync();
-    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
-        parts_place<D>(descs, t % max_sl, t / max_sl, max_sl);
-        __syncthreads();
-    }
-    grid.sync();
-    for (uint32_t t = blockIdx.x; t < ntask; t += G) {
-        parts_join<D>(descs, t % max_sl, t / max_sl, max_sl);
-        __syncthreads();
-    }
-}
-
-template <int D>
-static hipError_t launch_parts_coop(const PartDesc *descs, uint32_t nparts, uint32_t max_sl, const PartItem *items,
-                                    uint32_t nitems, hipStream_t st) {
-    static int max_blocks = -1;                // co-resident workgroups of k_parts_all<D> on this device
-    if (max_blocks < 0) {
-        int per_cu = 0, cus = 0, dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_parts_all<D>, kThreads, 0) !=
-                hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-            (void)hipGetLastError();
-            max_blocks = 0;
-        } else {
-            max_blocks = per_cu * cus;
-        }
-    }
-    if (max_blocks <= 0) return hipErrorNotSupported;
-    // the slice tasks, and up to 256 workgroups for the pair items (most return at once: their
-    // bound is the batch size, |U| is far smaller on the reference streams); fewer workgroups
-    // make the grid barriers cheaper
-    const uint32_t want = std::max<uint32_t>(1u, std::max(nparts * max_sl, std::min(nitems, 256u)));
-    const unsigned g = (unsigned)std::min<uint32_t>(want, (uint32_t)std::min(max_blocks, 1024));
-    void *args[] = {(void *)&descs, (void *)&nparts, (void *)&max_sl, (void *)&items, (void *)&nitems};
-    return hipLaunchCooperativeKernel((const void *)k_parts_all<D>, dim3(g), dim3(kThreads), args, 0, st);
-}
-
-static bool parts_coop_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("SKY_PART_COOP");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 void launch_parts_insert(int D, const PartDesc *descs, int nparts, uint32_t max_slices, const PartItem *items,
                          uint32_t nitems, hipStream_t st) {
     if (!nparts || !max_slices) return;
-    if (parts_coop_enabled()) {
-        hipError_t e = hipErrorNotSupported;
-        SKY_DISPATCH_D(D, (e = launch_parts_coop<DD>(descs, (uint32_t)nparts, max_slices, items, nitems, st)));
-        if (e == hipSuccess) return;
-        (void)hipGetLastError();                   // not available: the six launches
-    }
     const dim3 g(max_slices, (unsigned)nparts);
     SKY_DISPATCH_D(D, (k_parts_crit<DD><<<g, kThreads, 0, st>>>(descs)));
     SKY_DISPATCH_D(D, (k_parts_classify<DD><<<g, kThreads, 0, st>>>(descs)));

@@ -17,6 +17,7 @@
 //                    per tuple: is it in its local / the global skyline? -> stats
 //                    (|L_k|, survivors_k) and the stream-ordered output ids
 #include <algorithm>
+#include "knobs.h"
 #include <cstdlib>
 
 #include "sky_internal.h"
@@ -1497,7 +1498,7 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
                            double *pruners, int32_t *npr, hipStream_t st) {
     if (S == 0) return;                               // gmin: all-ones on entry (the caller's fill)
     static const unsigned sgrid = [] {        // SKY_SAMPLE_WG: workgroups of the sample pass (A/B knob)
-        const char *e = getenv("SKY_SAMPLE_WG");
+        const char *e = SKY_MEASURE_ENV("SKY_SAMPLE_WG");
         return e ? (unsigned)std::max(1, atoi(e)) : 256u;   // 32: +20 us, 64: +2 us (latency-bound per row)
     }();
     const unsigned g = std::min<unsigned>(nblk(S, kThreads), sgrid);
@@ -1509,7 +1510,7 @@ void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = (D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4) +
                        (size_t)(kFilterFT - 1) * a.Kp * a.M * 4;   // one duplicate-count array per output tile of a span
     static const unsigned tpb = [] {           // tiles per workgroup (SKY_FILTER_TPB, A/B knob)
-        const char *e = getenv("SKY_FILTER_TPB");   // 4: -4 % filter time vs 1 (2: -3 %, 8: -3 %)
+        const char *e = SKY_MEASURE_ENV("SKY_FILTER_TPB");   // 4: -4 % filter time vs 1 (2: -3 %, 8: -3 %)
         const int v = e ? atoi(e) : 4;
         return (unsigned)std::max(1, std::min(v, 64));
     }();
@@ -1523,7 +1524,7 @@ void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4;
     static const unsigned dgrid = [] {        // SKY_DEFER_WG: workgroups of the deferred-key pass (A/B knob)
-        const char *e = getenv("SKY_DEFER_WG");
+        const char *e = SKY_MEASURE_ENV("SKY_DEFER_WG");
         return e ? (unsigned)std::max(1, atoi(e)) : 256u;
     }();
     SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<dgrid, kThreads, lds, st>>>(a)));
@@ -1584,7 +1585,7 @@ void launch_rep_mult(uint32_t mt, const uint32_t *perm, const uint32_t *slot_src
 // SKY_OUT_TPB in {4, 8, 16}: tiles per count-pass workgroup (A/B knob)
 static int out_tpb() {
     static const int v = [] {
-        const char *e = getenv("SKY_OUT_TPB");
+        const char *e = SKY_MEASURE_ENV("SKY_OUT_TPB");
         const int t = e ? atoi(e) : 4;
         return t == 8 || t == 16 ? t : 4;
     }();

@@ -11,6 +11,7 @@
 //                   in LDS in digit order as contiguous runs (coalesced)
 // Only bytes that differ between keys are sorted (OR/AND reduction first).
 #include <cstdlib>
+#include "knobs.h"
 
 #include "sky_internal.h"
 
@@ -325,7 +326,7 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     // 7.43), 1024 for the query's candidates
     const bool big = m >= (1u << 22);
     static const int big_items = [] {   // SKY_RADIX_ITEMS: keys per thread of the large-sort tiles (A/B knob)
-        const char *e = getenv("SKY_RADIX_ITEMS");
+        const char *e = SKY_MEASURE_ENV("SKY_RADIX_ITEMS");
         const int v = e ? atoi(e) : 24;
         return v == 8 || v == 12 || v == 16 || v == 24 || v == 32 ? v : 24;
     }();
@@ -349,7 +350,7 @@ bool radix_sort_pairs(uint64_t *keys, uint32_t *vals, uint64_t *keys_alt, uint32
     for (int byte = 0; byte < 8; byte++) byte_passes += ((varying_bits >> (8 * byte)) & 0xffull) ? 1 : 0;
     const int dense_passes = (nbits + 7) / 8;
     static const int comp_mode = [] {            // SKY_RADIX_COMPRESS=0 disables (debug)
-        const char *e = getenv("SKY_RADIX_COMPRESS");
+        const char *e = SKY_MEASURE_ENV("SKY_RADIX_COMPRESS");
         return e ? atoi(e) : 1;
     }();
     const bool compress = comp_mode && !too_many_runs && dense_passes < byte_passes;

@@ -9,6 +9,8 @@
 // kernel mirrored into host memory, plus every tuple issued since).  The host synchronises only
 // when it must see the state: sky_part_size / sky_part_snapshot / compaction / close.
 #include "abi_common.h"
+#include "knobs.h"
+#include "stage_pool.h"
 
 #include <algorithm>
 #include <atomic>
@@ -56,82 +58,14 @@ void stage_one(StageChunk &k, int D) {
     k.nan = (acc >> 63) != 0;
 }
 
-class StagePool {
-  public:
-    static StagePool &get() {
-        static StagePool pool;
-        return pool;
-    }
-    // f(i) for every i < n, on the pool's threads and the caller; returns when all are done
-    void run(size_t n, const std::function<void(size_t)> &f) {
-        if (workers_.empty() || n < 2) {
-            for (size_t i = 0; i < n; i++) f(i);
-            return;
-        }
-        std::unique_lock<std::mutex> call(call_m_);          // one job at a time
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            fn_ = &f;
-            n_ = n;
-            next_.store(0);
-            done_.store(0);
-            gen_++;
-        }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return done_.load() == n_; });
-        fn_ = nullptr;
-    }
-    ~StagePool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (std::thread &t : workers_) t.join();
-    }
-
-  private:
-    StagePool() {
-        const char *e = getenv("SKY_STAGE_THREADS");
-        int nt = e ? atoi(e) : 4;
-        const int hw = (int)std::thread::hardware_concurrency();
-        nt = std::max(1, std::min(nt, std::max(1, hw)));
-        for (int i = 0; i < nt - 1; i++) workers_.emplace_back([this] { loop(); });
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-            }
-            work();
-        }
-    }
-    void work() {
-        for (;;) {
-            const size_t i = next_.fetch_add(1);
-            if (i >= n_) return;
-            (*fn_)(i);
-            if (done_.fetch_add(1) + 1 == n_) {
-                std::lock_guard<std::mutex> lk(m_);
-                done_cv_.notify_all();
-            }
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex m_, call_m_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(size_t)> *fn_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0}, done_{0};
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
+StagePool &stage_pool() {
+    // the caller + 3 workers (SKY_STAGE_THREADS in a measurement build)
+    static StagePool pool([] {
+        const char *e = SKY_MEASURE_ENV("SKY_STAGE_THREADS");
+        return e ? atoi(e) : 4;
+    }());
+    return pool;
+}
 
 void stage_chunks(std::vector<StageChunk> &ch, int D) {
     size_t bytes = 0;
@@ -140,7 +74,7 @@ void stage_chunks(std::vector<StageChunk> &ch, int D) {
         for (StageChunk &k : ch) stage_one(k, D);
         return;
     }
-    StagePool::get().run(ch.size(), [&](size_t i) { stage_one(ch[i], D); });
+    stage_pool().run(ch.size(), [&](size_t i) { stage_one(ch[i], D); });
 }
 
 // the newest consistent counts the commit kernel mirrored (seqlock: end, data, begin)
@@ -276,7 +210,7 @@ Ctx::Staging *take_stage(sky_ctx *c, size_t bytes) {
 struct HostProf {
     double pre = 0, wait = 0, stage = 0, launch = 0;
     uint64_t calls = 0;
-    bool on = getenv("SKY_PART_HOSTPROF") != nullptr;
+    bool on = SKY_MEASURE_ENV("SKY_PART_HOSTPROF") != nullptr;
     ~HostProf() {
         if (on && calls)
             fprintf(stderr, "[part] %llu calls, host us/call: bounds+items %.2f slot wait %.2f staging %.2f "

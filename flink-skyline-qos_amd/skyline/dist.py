@@ -15,7 +15,8 @@ stream; SKY(u_r SKY(shard_r)) = SKY(u_r shard_r) makes any split exact.  One ste
   3. sky_dist_merge_dev: each rank decides ITS OWN vectors against the union (in L_k iff no union
      vector of key k dominates it, in G iff no union vector does), writes its global-skyline ids
      and its share of |L_k| / survivors_k -- |own| x |union| work, not a replicated merge;
-  4. one all-reduce (sum) of the 2K shares (FlinkSkyline.java:593-608), on the device;
+  4. one all-reduce (sum) of the 2K shares (FlinkSkyline.java:593-608) and two verdict words
+     (route misses, merge errors), on the device;
   5. sky_dist_finish: the step's one host read.  Every rank sees the same gathered headers, so
      every rank takes the same decision: done, re-run the step (a rank's planned route missed),
      or re-run the exchange with a larger capacity (some rank exported more than it holds).
@@ -33,6 +34,12 @@ _SKY_OK, _SKY_E_RETRY, _SKY_E_CAPACITY = _abi.SKY_OK, _abi.SKY_E_RETRY, _abi.SKY
 def block_words(cap, dims):
     """int64 words of one rank's block (SKY_DIST_BLOCK_WORDS)."""
     return (int(cap) + 1) * (int(dims) + 2)
+
+
+def stats_words(K):
+    """int64 words of the all-reduced stat shares (SKY_DIST_STATS_WORDS): |L_k|, survivors_k,
+    then the route-miss and merge-error verdict words."""
+    return 2 * int(K) + 2
 
 
 def pack_block(rows_f64, keys, mult, cap, verdict=0, n_tuples=0):
@@ -101,7 +108,7 @@ class DistExchange:
         self.device = device
         self.world = world
         self.cap = int(cap)
-        self.stats = torch.zeros(2 * engine.K, dtype=torch.int64, device=device)
+        self.stats = torch.zeros(stats_words(engine.K), dtype=torch.int64, device=device)
         self._alloc()
         self.retries = 0
         self.regrows = 0
@@ -116,6 +123,37 @@ class DistExchange:
         self._alloc()
 
 
+class _PhaseClock:
+    """Where a step's time went: host wall time between the phase marks and, on a GPU, the device
+    time between the same marks (events on the current stream, which every *_dev call orders
+    itself with; read after sky_dist_finish has synchronised).  Wall time of a phase includes
+    waiting for earlier device work when the phase blocks (gloo staging, the finish read)."""
+
+    def __init__(self, cuda):
+        import time
+        self._now = time.perf_counter
+        self.cuda = cuda
+        self.marks = []
+
+    def mark(self, name):
+        if name == "start":
+            self.marks = []
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        self.marks.append((name, self._now(), ev))
+
+    def split(self, attempts):
+        out = {"attempts": attempts, "wall_ms": {}, "device_ms": {}}
+        for (_, t0, e0), (name, t1, e1) in zip(self.marks, self.marks[1:]):
+            out["wall_ms"][name] = round((t1 - t0) * 1e3, 4)
+            if e0 is not None and e1 is not None:
+                e1.synchronize()
+                out["device_ms"][name] = round(e0.elapsed_time(e1), 4)
+        return out
+
+
 def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, out_cap, group=None, max_attempts=8):
     """One query over the union of every rank's shard.  Returns this rank's number of global-
     skyline ids written to d_ids_out (stream order); afterwards engine.stats() holds the job-wide
@@ -128,15 +166,23 @@ def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, out_cap, g
         ex = engine._dist_ex = DistExchange(engine, dev, world)
     h0 = engine.host_syncs()
     export = True
+    clock = _PhaseClock(d_vals.is_cuda)
     for attempt in range(max_attempts):
+        clock.mark("start")
         if export:
             engine.dist_export_dev(d_ids, d_vals, ex.send, ex.cap)
         else:
             engine.dist_reblock_dev(ex.send, ex.cap)
+        clock.mark("export")
         all_gather_blocks(ex.recv, ex.send, group)
+        clock.mark("all_gather")
         engine.dist_merge_dev(ex.recv, world, rank, ex.cap, d_ids_out, d_origin_out, out_cap, ex.stats)
+        clock.mark("merge")
         all_reduce_sum(ex.stats, group)
+        clock.mark("all_reduce")
         rc, g, need = engine.dist_finish(ex.stats, out_cap)
+        clock.mark("finish")
+        engine.last_dist_phases = clock.split(attempt + 1)
         if rc == _SKY_OK:
             _, cnt = engine.phases()
             engine.last_dist_stats = {

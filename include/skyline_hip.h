@@ -200,7 +200,10 @@ int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_ou
  *   caller               all-gather the blocks of every rank into d_blocks (rank order)
  *   sky_dist_merge_dev   this rank's own vectors against the union; this rank's global-skyline
  *                        ids (stream order) -> d_ids_out / d_origin_out (positions < out_cap);
- *                        this rank's share of |L_k| / survivors_k -> d_stats (int64[2K])
+ *                        this rank's share of |L_k| / survivors_k -> d_stats
+ *                        (int64[SKY_DIST_STATS_WORDS(K)]: [0, K) |L_k|, [K, 2K) survivors_k,
+ *                        [2K] route misses, [2K+1] merge errors -- the last two are verdict
+ *                        words, summed so that every rank sees every rank's)
  *   caller               all-reduce (sum) d_stats over the ranks
  *   sky_dist_finish      the one host read: every rank's verdict (from the gathered headers, so
  *                        every rank returns the same code), *n_out = this rank's output count;
@@ -209,13 +212,17 @@ int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_ou
  * dims) and up to cap rows of (dims value bits as f64, partition key, multiplicity).
  * sky_dist_finish returns, on every rank alike:
  *   SKY_E_NAN       some shard holds a NaN;
- *   SKY_E_RETRY     some rank's planned local phase missed: call sky_dist_export_dev again;
+ *   SKY_E_HIP       a look-back ran out of its spin bound on some rank (export or merge);
+ *   SKY_E_RETRY     some rank's planned local phase missed, or some rank's union outgrew the
+ *                   pair-kernel route it chose from the previous step's sizes: call
+ *                   sky_dist_export_dev again (the next attempt takes the sized route);
  *   SKY_E_CAPACITY  with *need_cap > cap: some rank exported more than cap vectors: call
  *                   sky_dist_reblock_dev with a cap >= *need_cap (every rank), then all-gather,
  *                   merge and finish again (no local re-run);
  * and on this rank only SKY_E_CAPACITY with *need_cap == 0 when *n_out > out_cap (out_cap >=
  * the shard's tuple count never overflows).  Output buffers hold unspecified data on error. */
 #define SKY_DIST_BLOCK_WORDS(cap, dims) (((int64_t)(cap) + 1) * ((int64_t)(dims) + 2))
+#define SKY_DIST_STATS_WORDS(K) (2 * (int64_t)(K) + 2)
 int sky_dist_export_dev(sky_ctx *ctx, const int64_t *d_ids, const double *d_values, int64_t n, int64_t *d_block,
                         int64_t cap);
 int sky_dist_reblock_dev(sky_ctx *ctx, int64_t *d_block, int64_t cap);

@@ -211,7 +211,7 @@ def dist_emulate(engs, d_ids, d_vals, cap=4096, steps=1, max_attempts=8):
     synchronisations and the attempts each step took."""
     import torch
     from skyline import _abi
-    from skyline.dist import block_words
+    from skyline.dist import block_words, stats_words
     W = len(engs)
     D, K = engs[0].dims, engs[0].K
     dev = d_vals[0].device
@@ -231,7 +231,7 @@ def dist_emulate(engs, d_ids, d_vals, cap=4096, steps=1, max_attempts=8):
                 else:
                     e.dist_reblock_dev(send[r], cap)
             recv = torch.cat(send)
-            stats = [torch.empty(2 * K, dtype=torch.int64, device=dev) for _ in range(W)]
+            stats = [torch.empty(stats_words(K), dtype=torch.int64, device=dev) for _ in range(W)]
             for r, e in enumerate(engs):
                 e.dist_merge_dev(recv, W, r, cap, oi[r], oo[r], d_vals[r].shape[0], stats[r])
             tot = torch.stack(stats).sum(0)

@@ -97,7 +97,7 @@ class ModelEngine:
         m = min(self.g, out_cap)
         oi[:m] = torch.from_numpy(ids[sel][:m])
         oo[:m] = torch.from_numpy(keys[sel][:m].astype(np.int32))
-        stats.copy_(torch.from_numpy(np.concatenate([ls, sv])))
+        stats.copy_(torch.from_numpy(np.concatenate([ls, sv, np.zeros(2, np.int64)])))
 
     def dist_finish(self, stats_sum, out_cap):
         from skyline import _abi
@@ -111,7 +111,7 @@ class ModelEngine:
         if maxc > self.cap:
             return _abi.SKY_E_CAPACITY, 0, maxc
         s = stats_sum.numpy()
-        self.last = (s[:self.K].copy(), s[self.K:].copy())
+        self.last = (s[:self.K].copy(), s[self.K:2 * self.K].copy())
         return _abi.SKY_OK, self.g, 0
 
     def host_syncs(self):

@@ -137,7 +137,7 @@ def test_dist_retry_after_planned_miss(gpu_engine_factory, oracle):
 
 def test_dist_nan_every_rank_reports_it(gpu_engine_factory, oracle):
     from skyline._abi import SkylineError
-    from skyline.dist import block_words
+    from skyline.dist import block_words, stats_words
     n, D, P, W = 30000, 4, 8, 3
     vals = oracle.synth(0, D, n, seed=4)
     vals[n - 7, 2] = np.nan                               # only the last rank's shard
@@ -149,7 +149,7 @@ def test_dist_nan_every_rank_reports_it(gpu_engine_factory, oracle):
     for r, e in enumerate(engs):
         e.dist_export_dev(di[r], dv[r], send[r], cap)
     recv = torch.cat(send)
-    st = [torch.zeros(2 * P, dtype=torch.int64, device="cuda") for _ in range(W)]
+    st = [torch.zeros(stats_words(P), dtype=torch.int64, device="cuda") for _ in range(W)]
     oi = torch.empty(n, dtype=torch.int64, device="cuda")
     oo = torch.empty(n, dtype=torch.int32, device="cuda")
     for r, e in enumerate(engs):
@@ -179,5 +179,33 @@ def test_dist_empty_shard(gpu_engine_factory, oracle):
           torch.from_numpy(ids[20000:]).cuda()]
     for out in dist_emulate(engs, di, dv, steps=2):
         _check(out, exp)
+    for e in engs:
+        e.close()
+
+
+def test_dist_route_large_small_large(gpu_engine_factory, oracle, monkeypatch):
+    """A merge picks its union route from the previous step's |own| x |union|.  After a small step
+    a large one on the same engines must not run the pair kernel over the large union: the kernel
+    checks this step's sizes on the device, every rank gets SKY_E_RETRY through the all-reduced
+    route-miss word, and the retry takes the bounding-box route (counters[6] = 1), exact."""
+    monkeypatch.setenv("SKY_DIST_BRUTE_PAIRS", str(1 << 20))
+    monkeypatch.setenv("SKY_PLAN", "0")                # no planned-route misses: a retry is the route's
+    D, P, W = 6, 8, 3
+    big = oracle.synth(3, D, 150000, seed=31)          # std-anti: large local skylines
+    small = oracle.synth(1, D, 30000, seed=32)         # correlated: a handful of vectors
+    engs = [gpu_engine_factory(D, P) for _ in range(W)]
+    routes, cap = [], 4096
+    for step, vals in enumerate((big, small, big)):
+        ids = np.arange(len(vals), dtype=np.int64) + 1000 * step
+        dv, di = _split(vals, ids, W)
+        out = dist_emulate(engs, di, dv, cap=cap)[0]
+        cap = out["cap"]
+        _check(out, _expect(gpu_engine_factory, vals, ids, D, P))
+        routes.append(int(engs[0].phases()[1][6]))
+        if step == 2:
+            assert out["attempts"] == 2                 # the route miss, then the sized route
+        own, union = int(engs[0].phases()[1][3]), int(engs[0].phases()[1][5])
+        assert (own * union > (1 << 20)) == (step != 1)
+    assert routes == [1, 0, 1]
     for e in engs:
         e.close()
