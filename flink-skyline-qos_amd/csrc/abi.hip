@@ -35,6 +35,27 @@ extern "C" {
 const char *sky_last_error(void) { return g_err.c_str(); }
 const char *sky_version(void) { return "skyline_hip 0.1 (gfx950)"; }
 
+// devices this process sees (0 without a GPU: no error), for the operators' subtask -> device map
+int sky_device_count(int32_t *n_out) {
+    ARG_CHECK(n_out != nullptr, "null argument");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        count = 0;
+    }
+    *n_out = count;
+    return SKY_OK;
+}
+
+// the device of a subtask: subtasks round-robin over the node's GPUs (a TaskManager per node
+// runs subtasks 0..parallelism-1 of an operator; each keeps its context on one GPU)
+int sky_device_for_subtask(int32_t subtask, int32_t ndev, int32_t *dev_out) {
+    ARG_CHECK(dev_out != nullptr, "null argument");
+    ARG_CHECK(subtask >= 0 && ndev >= 1, "subtask must be >= 0 and ndev >= 1");
+    *dev_out = subtask % ndev;
+    return SKY_OK;
+}
+
 int sky_ctx_create(const int *devices, int ndev, int dims, int num_partitions, int algo, double domain_max,
                    sky_ctx **out) {
     GUARD_BEGIN

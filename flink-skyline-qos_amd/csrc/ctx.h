@@ -84,7 +84,7 @@ struct Ctx {
     // upload overlaps the previous call's kernels; part_done[b]: the kernels that read buffer b
     DevBuf part_batch[2], part_work;
     // sky_parts_global_merge work buffers
-    DevBuf pgm_w, pgm_flag, pgm_tsel, pgm_tpos, pgm_scr, pgm_lists, pgm_surv, pgm_sorg, pgm_ids, pgm_org;
+    DevBuf pgm_w, pgm_flag, pgm_tsel, pgm_tpos, pgm_scr, pgm_lists, pgm_surv, pgm_sorg, pgm_ids, pgm_org, pgm_up, pgm_err;
     hipStream_t part_copy_st = nullptr;
     hipEvent_t part_done[2] = {nullptr, nullptr};
     bool part_done_rec[2] = {false, false};

@@ -606,6 +606,49 @@ bool mbr_lpt_enabled() {
     return !(e && e[0] == '0');
 }
 
+#ifdef SKY_MEASURE
+// SKY_MBR_DBG & 8 (measurement builds): how the pair pass's work items spread over time --
+// duration percentiles, the share of the pass the longest items cover, and the number of items
+// in flight per twentieth of the pass (the occupancy the pass actually reaches)
+static void mbr_trace_report(const unsigned long long *d, size_t n, hipStream_t st) {
+    std::vector<unsigned long long> h(n * 4);
+    if (hipMemcpyAsync(h.data(), d, n * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess || !n)
+        return;
+    unsigned long long t0 = ~0ull, t1 = 0, tt = 0, tp = 0;
+    std::vector<double> dur(n);
+    for (size_t i = 0; i < n; i++) {
+        t0 = std::min(t0, h[4 * i]);
+        t1 = std::max(t1, h[4 * i + 1]);
+        dur[i] = (double)(h[4 * i + 1] - h[4 * i]) * 0.01;   // us (100 MHz)
+        tt += h[4 * i + 2];
+        tp += h[4 * i + 3];
+    }
+    const double span = (double)(t1 - t0) * 0.01;
+    std::vector<double> sd(dur);
+    std::sort(sd.begin(), sd.end());
+    double busy = 0;
+    for (double x : dur) busy += x;
+    auto pct = [&](double q) { return sd[std::min(n - 1, (size_t)(q * (double)(n - 1)))]; };
+    fprintf(stderr, "[mbr-trace] items %zu span %.1f us, item us p50 %.1f p90 %.1f p99 %.1f max %.1f, mean in flight %.0f, "
+            "tested tiles %llu pair tests %llu\n", n, span, pct(0.5), pct(0.9), pct(0.99), sd[n - 1], busy / span,
+            tt, tp);
+    const int B = 20;
+    std::vector<double> occ(B, 0.0);
+    for (size_t i = 0; i < n; i++) {
+        const double a = (double)(h[4 * i] - t0) * 0.01, b = (double)(h[4 * i + 1] - t0) * 0.01;
+        for (int k = 0; k < B; k++) {
+            const double lo = span * k / B, hi = span * (k + 1) / B;
+            const double ov = std::min(b, hi) - std::max(a, lo);
+            if (ov > 0) occ[k] += ov / (hi - lo);
+        }
+    }
+    fprintf(stderr, "[mbr-trace] in flight per 5%% of the span:");
+    for (int k = 0; k < B; k++) fprintf(stderr, " %.0f", occ[k]);
+    fprintf(stderr, "\n");
+}
+#endif
+
 // both skyline levels of the rep set in one bounding-box pruned all-pairs pass (k_mbr.hip)
 static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) {
     hipStream_t st = c.st;
@@ -679,9 +722,21 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.lpt = mbr_lpt_enabled() ? p.mbr_lpt.as<uint32_t>() : nullptr;
     a.alive_l = p.alive_l.as<uint8_t>();
     a.alive_g = p.alive_g.as<uint8_t>();
+#ifdef SKY_MEASURE
+    DevBuf trace;
+    const size_t nitems = mbr_tiles(mr) * (size_t)std::max(a.nsplit, 1);
+    if (a.dbg & 8) {
+        SKY_TRY(trace.ensure(nitems * 32));
+        HIP_TRY(hipMemsetAsync(trace.p, 0, nitems * 32, st));
+        a.trace = trace.as<unsigned long long>();
+    }
+#endif
     c.ktimer_begin("mbr", st);
     HIP_TRY(launch_mbr(a, st));
     c.ktimer_end("mbr", st, mr);
+#ifdef SKY_MEASURE
+    if (a.dbg & 8) mbr_trace_report(trace.as<unsigned long long>(), nitems, st);
+#endif
     STAGE(st, "mbr");
     p.used_mbr = true;
     p.sfs_rounds++;

@@ -422,9 +422,11 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
                                                         uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
                                                         uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs,
-                                                        uint32_t *__restrict__ lpt) {
+                                                        uint32_t *__restrict__ lpt,
+                                                        unsigned long long *__restrict__ trace) {
     constexpr int NW = R::NW;
-    uint32_t split, yt;
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t split, yt, witem;
     if (lpt) {
         // the next (y tile, x range) work item of the cost order, heaviest tiles first
         uint32_t item = 0;
@@ -432,6 +434,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         item = __builtin_amdgcn_readfirstlane(__shfl((int)item, 0, 64));
         if (item >= ys.ntiles * nsplit) return;
         split = item % nsplit;
+        witem = item;
         yt = __builtin_amdgcn_readfirstlane(lpt[kMbrLptHead + ys.ntiles + item / nsplit]);
     } else {
         // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
@@ -441,6 +444,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
         // the x tiles are split into nsplit ranges, one work item each
         split = blk % nsplit;
+        witem = blk;
         yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kMbrPairThreads / 64) + (threadIdx.x >> 6));
         if (yt >= ys.ntiles) return;
     }
@@ -714,6 +718,12 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         }
     }
     if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
+    if (trace && lane == 0) {
+        trace[4 * (size_t)witem] = t_start;
+        trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[4 * (size_t)witem + 2] = ntested;
+        trace[4 * (size_t)witem + 3] = npairs;
+    }
     if (lane == 0 && pairs) {
         atomicAdd(pairs, (unsigned long long)npairs);
         atomicAdd(pairs + 1, (unsigned long long)ntested);
@@ -805,7 +815,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
     k_mbr_pairs<R, F, G, true>                              \
         <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
-                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt)
+                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
     if (a.full) {
         if (a.gmerge) SKY_MBR_PAIRS(true, true);
         else SKY_MBR_PAIRS(true, false);
@@ -854,7 +864,7 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     if (y.lpt) mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
     k_mbr_pairs<R, true, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
-                                                        y.domf, x.pairs, y.lpt);
+                                                        y.domf, x.pairs, y.lpt, nullptr);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,
                                                                              a.K, a.flags, a.lsz, a.surv);
 }

@@ -582,9 +582,11 @@ __global__ __launch_bounds__(kThreads) void k_pgm_flags(uint32_t n, const int64_
     flag[surv_idx[i]] = 1;
 }
 // per tuple of the concatenated lists: its rep survives?
+// (a caller-given rep index past its list's rep count -- sky_global_merge_reps -- selects nothing
+// and sets *err)
 __global__ __launch_bounds__(kThreads) void k_pgm_tflag(const PgmList *__restrict__ lists, int nl, uint32_t ttot,
                                                         const uint8_t *__restrict__ flag,
-                                                        uint32_t *__restrict__ tsel) {
+                                                        uint32_t *__restrict__ tsel, uint32_t *__restrict__ err) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= ttot) return;
     int lo = 0, hi = nl - 1;                   // the list holding tuple i (toff ascending)
@@ -594,7 +596,13 @@ __global__ __launch_bounds__(kThreads) void k_pgm_tflag(const PgmList *__restric
         else hi = mid - 1;
     }
     const PgmList &L = lists[lo];
-    tsel[i] = flag[L.roff + L.trep[i - L.toff]] ? 1u : 0u;
+    const uint32_t r = L.trep[i - L.toff];
+    if (r >= L.nrep) {
+        tsel[i] = 0u;
+        *err = 1u;
+        return;
+    }
+    tsel[i] = flag[L.roff + r] ? 1u : 0u;
 }
 __global__ __launch_bounds__(kThreads) void k_pgm_write(const PgmList *__restrict__ lists, int nl, uint32_t ttot,
                                                         const uint32_t *__restrict__ tsel,
@@ -622,10 +630,10 @@ void launch_pgm_flags(uint32_t n, const int64_t *surv_idx, uint8_t *flag, hipStr
 }
 void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_t *flag, uint32_t *tsel,
                        uint32_t *tpos, uint32_t *d_total, uint32_t *scratch, int64_t *ids_out, int32_t *org_out,
-                       hipStream_t st) {
+                       uint32_t *err, hipStream_t st) {
     if (!ttot) return;
     const unsigned g = (ttot + kThreads - 1) / kThreads;
-    k_pgm_tflag<<<g, kThreads, 0, st>>>(lists, nl, ttot, flag, tsel);
+    k_pgm_tflag<<<g, kThreads, 0, st>>>(lists, nl, ttot, flag, tsel, err);
     scan_excl_u32(tsel, tpos, ttot, d_total, scratch, st);
     k_pgm_write<<<g, kThreads, 0, st>>>(lists, nl, ttot, tsel, tpos, ids_out, org_out);
 }

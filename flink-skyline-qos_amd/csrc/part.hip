@@ -444,6 +444,102 @@ int parts_insert(int np_all, sky_part *const *parts_all, const int64_t *const *i
     return SKY_OK;
 }
 
+// GlobalSkylineAggregator (FlinkSkyline.java:515-569) over lists held as distinct vectors: list g
+// has R[g] reps (rows already concatenated into c->h_vals, weights = tuples on each rep in
+// c->pgm_w, origins in c->h_origin) and T[g] tuples (id, rep index) at src[g].  The alive reps
+// run through the single-partition pipeline, the surviving reps are flagged, and every list's
+// tuples whose rep survives are written in list order, then insertion order: the result, its
+// order, the origins and sky_global_stats equal sky_global_merge over the expanded lists.
+struct PgmSrc {
+    const int64_t *tids;
+    const uint32_t *trep;
+};
+int pgm_core(sky_ctx *c, int nparts, const uint32_t *R, const uint32_t *T, const PgmSrc *src, const int32_t *part_ids,
+             int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out) {
+    hipStream_t st = c->st;
+    uint64_t rtot = 0, ttot = 0;
+    for (int g = 0; g < nparts; g++) {
+        rtot += R[g];
+        ttot += T[g];
+    }
+    const size_t rr = (size_t)std::max<uint64_t>(rtot, 1), tt = (size_t)std::max<uint64_t>(ttot, 1);
+    SKY_TRY(c->pgm_surv.ensure(rr * 8));
+    SKY_TRY(c->pgm_sorg.ensure(rr * 4));
+    SKY_TRY(c->pgm_flag.ensure(rr));
+    PipeIn in;
+    in.vals = c->h_vals.as<double>();
+    in.n = (uint32_t)rtot;
+    in.ids = nullptr;                           // the rep's index in the concatenation
+    in.origin = c->h_origin.as<int32_t>();
+    in.weights = c->pgm_w.as<int64_t>();
+    in.single = true;
+    in.global = false;
+    in.K = std::max(nparts, 1);
+    c->shard_valid = false;
+    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
+    // GlobalSkylineAggregator: localSkylineSizes[k] = incoming list size (:544); survivors by
+    // originPartition (:593-596), weighted by the tuples on each rep
+    c->K_last = nparts;
+    c->lsz.assign(nparts, 0);
+    c->surv.assign(nparts, 0);
+    uint64_t gtot = 0;
+    for (int g = 0; g < nparts; g++) {
+        c->lsz[g] = T[g];
+        c->surv[g] = (int64_t)c->main.h_lsz[g];
+        gtot += (uint64_t)c->main.h_lsz[g];
+    }
+    if (n_out) *n_out = (int64_t)gtot;
+    if ((int64_t)gtot > cap && (ids_out || origin_out)) {
+        set_error("output capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    const uint32_t greps = (uint32_t)c->main.nout;
+    int64_t gr = 0;
+    SKY_TRY(pipe_output(*c, c->main, in, false, c->pgm_surv.as<int64_t>(), c->pgm_sorg.as<int32_t>(), nullptr,
+                        (int64_t)rr, &gr, nullptr));
+    HIP_TRY(hipMemsetAsync(c->pgm_flag.p, 0, rr, st));
+    launch_pgm_flags(greps, c->pgm_surv.as<int64_t>(), c->pgm_flag.as<uint8_t>(), st);
+    // every list's tuples whose rep survives, list order then insertion order
+    std::vector<PgmList> lists((size_t)std::max(nparts, 1));
+    uint64_t toff = 0, roff = 0;
+    for (int g = 0; g < nparts; g++) {
+        PgmList &L = lists[g];
+        L.tids = src[g].tids;
+        L.trep = src[g].trep;
+        L.toff = (uint32_t)toff;
+        L.roff = (uint32_t)roff;
+        L.part_id = part_ids ? part_ids[g] : g;
+        L.nrep = R[g];
+        toff += T[g];
+        roff += R[g];
+    }
+    SKY_TRY(c->pgm_lists.ensure(lists.size() * sizeof(PgmList)));
+    SKY_TRY(c->pgm_tsel.ensure(tt * 4));
+    SKY_TRY(c->pgm_tpos.ensure(tt * 4 + 64));
+    SKY_TRY(c->pgm_scr.ensure(scan_scratch_words(tt) * 4 + 64));
+    SKY_TRY(c->pgm_ids.ensure((size_t)std::max<uint64_t>(gtot, 1) * 8));
+    SKY_TRY(c->pgm_org.ensure((size_t)std::max<uint64_t>(gtot, 1) * 4));
+    SKY_TRY(c->pgm_err.ensure(64));
+    HIP_TRY(hipMemsetAsync(c->pgm_err.p, 0, 4, st));
+    HIP_TRY(hipMemcpyAsync(c->pgm_lists.p, lists.data(), lists.size() * sizeof(PgmList), hipMemcpyHostToDevice, st));
+    launch_pgm_tuples(c->pgm_lists.as<PgmList>(), nparts, (uint32_t)ttot, c->pgm_flag.as<uint8_t>(),
+                      c->pgm_tsel.as<uint32_t>(), c->pgm_tpos.as<uint32_t>(), c->pgm_tpos.as<uint32_t>() + tt,
+                      c->pgm_scr.as<uint32_t>(), c->pgm_ids.as<int64_t>(), c->pgm_org.as<int32_t>(),
+                      c->pgm_err.as<uint32_t>(), st);
+    HIP_TRY(hipGetLastError());
+    uint32_t herr = 0;
+    if (gtot && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->pgm_ids.p, gtot * 8, hipMemcpyDeviceToHost, st));
+    if (gtot && origin_out) HIP_TRY(hipMemcpyAsync(origin_out, c->pgm_org.p, gtot * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&herr, c->pgm_err.p, 4, hipMemcpyDeviceToHost, st));
+    c->host_syncs++;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (herr) {
+        set_error("a tuple's rep index is not below its list's rep count");
+        return SKY_E_ARG;
+    }
+    return SKY_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -506,9 +602,9 @@ int sky_parts_insert(int nparts, sky_part *const *parts, const int64_t *const *i
     GUARD_END
 }
 
-// GlobalSkylineAggregator (FlinkSkyline.java:515-569) over the keys' device-resident states:
-// the same result and stats as sky_global_merge over the parts' snapshots, without moving the
-// local skylines through host memory (see skyline_hip.h)
+// GlobalSkylineAggregator over the keys' device-resident states (co-located aggregator): the
+// same result and stats as sky_global_merge over the parts' snapshots, without moving the local
+// skylines through host memory (see skyline_hip.h)
 int sky_parts_global_merge(sky_ctx *c, int nparts, sky_part *const *parts, const int32_t *part_ids,
                            int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out) {
     GUARD_BEGIN
@@ -523,6 +619,7 @@ int sky_parts_global_merge(sky_ctx *c, int nparts, sky_part *const *parts, const
     const int D = c->D;
     // exact counts; dead reps and their tuples dropped (insertion order kept)
     std::vector<uint32_t> R(nparts), T(nparts);
+    std::vector<PgmSrc> src(nparts);
     uint64_t rtot = 0, ttot = 0;
     for (int g = 0; g < nparts; g++) {
         sky_part *p = parts[g];
@@ -530,17 +627,15 @@ int sky_parts_global_merge(sky_ctx *c, int nparts, sky_part *const *parts, const
         if (p->dead_known) SKY_TRY(part_compact(p));
         R[g] = (uint32_t)p->R_known;
         T[g] = (uint32_t)p->T_known;
+        src[g] = PgmSrc{p->tids.as<int64_t>(), p->trep.as<uint32_t>()};
         rtot += R[g];
         ttot += T[g];
     }
     ARG_CHECK(rtot < 0x7fffffffull && ttot < 0x7fffffffull, "too many tuples");
-    const size_t rr = (size_t)std::max<uint64_t>(rtot, 1), tt = (size_t)std::max<uint64_t>(ttot, 1);
+    const size_t rr = (size_t)std::max<uint64_t>(rtot, 1);
     SKY_TRY(c->h_vals.ensure(rr * D * 8));
     SKY_TRY(c->h_origin.ensure(rr * 4));
     SKY_TRY(c->pgm_w.ensure(rr * 8));
-    SKY_TRY(c->pgm_surv.ensure(rr * 8));
-    SKY_TRY(c->pgm_sorg.ensure(rr * 4));
-    SKY_TRY(c->pgm_flag.ensure(rr));
     // the alive reps of every part as one single-partition run (origin = list, weight = tuples)
     uint64_t off = 0;
     for (int g = 0; g < nparts; g++) {
@@ -552,68 +647,108 @@ int sky_parts_global_merge(sky_ctx *c, int nparts, sky_part *const *parts, const
         off += R[g];
     }
     HIP_TRY(hipGetLastError());
-    PipeIn in;
-    in.vals = c->h_vals.as<double>();
-    in.n = (uint32_t)rtot;
-    in.ids = nullptr;                           // the rep's index in the concatenation
-    in.origin = c->h_origin.as<int32_t>();
-    in.weights = c->pgm_w.as<int64_t>();
-    in.single = true;
-    in.global = false;
-    in.K = std::max(nparts, 1);
-    c->shard_valid = false;
-    SKY_TRY(pipe_run(*c, c->main, in, nullptr));
-    // GlobalSkylineAggregator: localSkylineSizes[k] = incoming list size (:544); survivors by
-    // originPartition (:593-596), weighted by the tuples on each rep
-    c->K_last = nparts;
-    c->lsz.assign(nparts, 0);
-    c->surv.assign(nparts, 0);
-    uint64_t gtot = 0;
-    for (int g = 0; g < nparts; g++) {
-        c->lsz[g] = T[g];
-        c->surv[g] = (int64_t)c->main.h_lsz[g];
-        gtot += (uint64_t)c->main.h_lsz[g];
+    return pgm_core(c, nparts, R.data(), T.data(), src.data(), part_ids, ids_out, origin_out, cap, n_out);
+    GUARD_END
+}
+
+// GlobalSkylineAggregator over local skylines shipped as distinct vectors (sky_part_snapshot_reps):
+// the aggregator of a job whose local processors run elsewhere (see skyline_hip.h)
+int sky_global_merge_reps(sky_ctx *c, int nlists, const int32_t *part_ids, const int64_t *const *ids,
+                          const int32_t *const *rep_idx, const int64_t *counts, const double *const *reps,
+                          const int32_t *const *rep_counts, const int64_t *nreps, int64_t *ids_out,
+                          int32_t *origin_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && nlists >= 0 && nlists <= SKY_MAX_PARTITIONS, "bad nlists (<= 256 lists)");
+    ARG_CHECK(nlists == 0 || (ids && rep_idx && counts && reps && rep_counts && nreps), "null argument");
+    uint64_t rtot = 0, ttot = 0;
+    for (int g = 0; g < nlists; g++) {
+        ARG_CHECK(counts[g] >= 0 && nreps[g] >= 0, "negative count");
+        ARG_CHECK(counts[g] == 0 || (ids[g] && rep_idx[g]), "null tuple list");
+        ARG_CHECK(nreps[g] == 0 || (reps[g] && rep_counts[g]), "null rep list");
+        ARG_CHECK(counts[g] == 0 || nreps[g] > 0, "tuples without reps");
+        rtot += (uint64_t)nreps[g];
+        ttot += (uint64_t)counts[g];
     }
-    if (n_out) *n_out = (int64_t)gtot;
-    if ((int64_t)gtot > cap && (ids_out || origin_out)) {
-        set_error("output capacity too small");
+    ARG_CHECK(rtot < 0x7fffffffull && ttot < 0x7fffffffull, "too many tuples");
+    SKY_TRY(bind(c));
+    hipStream_t st = c->st;
+    const int D = c->D;
+    const size_t rr = (size_t)std::max<uint64_t>(rtot, 1), tt = (size_t)std::max<uint64_t>(ttot, 1);
+    SKY_TRY(c->h_vals.ensure(rr * D * 8));
+    SKY_TRY(c->h_origin.ensure(rr * 4));
+    SKY_TRY(c->pgm_w.ensure(rr * 8));
+    // the lists' tuples: ids [tt] then rep indices [tt] (weights and origins built here)
+    SKY_TRY(c->pgm_up.ensure(tt * 12 + 256));
+    std::vector<int64_t> w((size_t)rtot);
+    std::vector<int32_t> org((size_t)rtot);
+    std::vector<uint32_t> R(nlists), T(nlists);
+    std::vector<PgmSrc> src(nlists);
+    uint64_t roff = 0, toff = 0;
+    for (int g = 0; g < nlists; g++) {
+        R[g] = (uint32_t)nreps[g];
+        T[g] = (uint32_t)counts[g];
+        for (uint32_t r = 0; r < R[g]; r++) {
+            w[roff + r] = rep_counts[g][r];
+            org[roff + r] = g;
+        }
+        if (R[g]) HIP_TRY(hipMemcpyAsync(c->h_vals.as<double>() + roff * D, reps[g], (size_t)R[g] * D * 8,
+                                         hipMemcpyHostToDevice, st));
+        int64_t *d_ids = c->pgm_up.as<int64_t>() + toff;
+        uint32_t *d_rep = reinterpret_cast<uint32_t *>(c->pgm_up.as<int64_t>() + tt) + toff;
+        if (T[g]) {
+            HIP_TRY(hipMemcpyAsync(d_ids, ids[g], (size_t)T[g] * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(d_rep, rep_idx[g], (size_t)T[g] * 4, hipMemcpyHostToDevice, st));
+        }
+        src[g] = PgmSrc{d_ids, d_rep};
+        roff += R[g];
+        toff += T[g];
+    }
+    if (rtot) {
+        HIP_TRY(hipMemcpyAsync(c->pgm_w.p, w.data(), (size_t)rtot * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(c->h_origin.p, org.data(), (size_t)rtot * 4, hipMemcpyHostToDevice, st));
+    }
+    return pgm_core(c, nlists, R.data(), T.data(), src.data(), part_ids, ids_out, origin_out, cap, n_out);
+    GUARD_END
+}
+
+// exact tuple and distinct-vector counts of a part (after its pending work)
+int sky_part_sizes(sky_part *p, int64_t *n_tuples, int64_t *n_reps) {
+    GUARD_BEGIN
+    ARG_CHECK(p && n_tuples && n_reps, "null argument");
+    SKY_TRY(bind(p->ctx));
+    SKY_TRY(part_sync(p));
+    if (p->dead_known) SKY_TRY(part_compact(p));
+    *n_tuples = (int64_t)p->T_known;
+    *n_reps = (int64_t)p->R_known;
+    return SKY_OK;
+    GUARD_END
+}
+
+// the state as distinct vectors: tuples (id, rep index) in insertion order, reps (values, tuples
+// on each) -- what a local processor ships to an aggregator elsewhere (sky_global_merge_reps)
+int sky_part_snapshot_reps(sky_part *p, int64_t *ids_out, int32_t *rep_out, int64_t cap, double *reps_out,
+                           int32_t *rep_count_out, int64_t rep_cap, int64_t *n_out, int64_t *nrep_out) {
+    GUARD_BEGIN
+    ARG_CHECK(p, "null part");
+    sky_ctx *c = p->ctx;
+    SKY_TRY(bind(c));
+    SKY_TRY(part_sync(p));
+    if (p->dead_known) SKY_TRY(part_compact(p));
+    const int64_t T = (int64_t)p->T_known, R = (int64_t)p->R_known;
+    if (n_out) *n_out = T;
+    if (nrep_out) *nrep_out = R;
+    if (T > cap || R > rep_cap) {
+        set_error("snapshot capacity too small");
         return SKY_E_CAPACITY;
     }
-    const uint32_t greps = (uint32_t)c->main.nout;
-    int64_t gr = 0;
-    SKY_TRY(pipe_output(*c, c->main, in, false, c->pgm_surv.as<int64_t>(), c->pgm_sorg.as<int32_t>(), nullptr,
-                        (int64_t)rr, &gr, nullptr));
-    HIP_TRY(hipMemsetAsync(c->pgm_flag.p, 0, rr, st));
-    launch_pgm_flags(greps, c->pgm_surv.as<int64_t>(), c->pgm_flag.as<uint8_t>(), st);
-    // every list's tuples whose rep survives, list order then insertion order
-    std::vector<PgmList> lists((size_t)std::max(nparts, 1));
-    uint64_t toff = 0, roff = 0;
-    for (int g = 0; g < nparts; g++) {
-        PgmList &L = lists[g];
-        L.tids = parts[g]->tids.as<int64_t>();
-        L.trep = parts[g]->trep.as<uint32_t>();
-        L.toff = (uint32_t)toff;
-        L.roff = (uint32_t)roff;
-        L.part_id = part_ids ? part_ids[g] : g;
-        L.pad = 0;
-        toff += T[g];
-        roff += R[g];
-    }
-    SKY_TRY(c->pgm_lists.ensure(lists.size() * sizeof(PgmList)));
-    SKY_TRY(c->pgm_tsel.ensure(tt * 4));
-    SKY_TRY(c->pgm_tpos.ensure(tt * 4 + 64));
-    SKY_TRY(c->pgm_scr.ensure(scan_scratch_words(tt) * 4 + 64));
-    SKY_TRY(c->pgm_ids.ensure((size_t)std::max<uint64_t>(gtot, 1) * 8));
-    SKY_TRY(c->pgm_org.ensure((size_t)std::max<uint64_t>(gtot, 1) * 4));
-    HIP_TRY(hipMemcpyAsync(c->pgm_lists.p, lists.data(), lists.size() * sizeof(PgmList), hipMemcpyHostToDevice, st));
-    launch_pgm_tuples(c->pgm_lists.as<PgmList>(), nparts, (uint32_t)ttot, c->pgm_flag.as<uint8_t>(),
-                      c->pgm_tsel.as<uint32_t>(), c->pgm_tpos.as<uint32_t>(), c->pgm_tpos.as<uint32_t>() + tt,
-                      c->pgm_scr.as<uint32_t>(), c->pgm_ids.as<int64_t>(), c->pgm_org.as<int32_t>(), st);
-    HIP_TRY(hipGetLastError());
-    if (gtot && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, c->pgm_ids.p, gtot * 8, hipMemcpyDeviceToHost, st));
-    if (gtot && origin_out) HIP_TRY(hipMemcpyAsync(origin_out, c->pgm_org.p, gtot * 4, hipMemcpyDeviceToHost, st));
+    if (T && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, p->tids.p, (size_t)T * 8, hipMemcpyDeviceToHost, c->st));
+    if (T && rep_out) HIP_TRY(hipMemcpyAsync(rep_out, p->trep.p, (size_t)T * 4, hipMemcpyDeviceToHost, c->st));
+    if (R && reps_out)
+        HIP_TRY(hipMemcpyAsync(reps_out, p->rrows.p, (size_t)R * c->D * 8, hipMemcpyDeviceToHost, c->st));
+    if (R && rep_count_out)
+        HIP_TRY(hipMemcpyAsync(rep_count_out, p->rcnt.p, (size_t)R * 4, hipMemcpyDeviceToHost, c->st));
     c->host_syncs++;
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipStreamSynchronize(c->st));
     return SKY_OK;
     GUARD_END
 }

@@ -305,6 +305,9 @@ struct MbrArgs {
     // the y tiles go in blockIdx order
     uint32_t *lpt = nullptr;
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
+    // measurement builds only (SKY_MBR_DBG & 8): per work item of the pair pass {start, end,
+    // tested tiles, pair tests} (s_memrealtime ticks, 100 MHz)
+    unsigned long long *trace = nullptr;
 };
 // the multi-GPU merge: own rows (y, a contiguous range of the union) against the whole union
 // (x), FULL test, both levels; x.gmin / x.gprange needed, y's group buffers unused
@@ -357,13 +360,13 @@ struct PgmList {
     const uint32_t *trep;
     uint32_t toff, roff;
     int32_t part_id;
-    uint32_t pad;
+    uint32_t nrep;                // reps of the list (bound of its trep entries)
 };
 void launch_pgm_prep(uint32_t R, const uint32_t *rcnt, int32_t k, int32_t *origin, int64_t *w, hipStream_t st);
 void launch_pgm_flags(uint32_t n, const int64_t *surv_idx, uint8_t *flag, hipStream_t st);
 void launch_pgm_tuples(const PgmList *lists, int nl, uint32_t ttot, const uint8_t *flag, uint32_t *tsel,
                        uint32_t *tpos, uint32_t *d_total, uint32_t *scratch, int64_t *ids_out, int32_t *org_out,
-                       hipStream_t st);
+                       uint32_t *err, hipStream_t st);
 constexpr uint32_t kPartItemY = 256, kPartItemX = 256;
 constexpr int kPartPruners = 4;   // batch pruners per insert (k_parts_crit / k_parts_classify)
 constexpr int kPartMeta = 16;     // words of PartDesc::meta

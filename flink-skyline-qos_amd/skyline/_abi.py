@@ -69,8 +69,11 @@ SIGNATURES = {
     "sky_parts_insert": [c_int, c_p, c_p, c_p, c_p],
     "sky_part_size": [c_p, P_i64],
     "sky_part_snapshot": [c_p, c_p, c_p, c_i64, P_i64],
+    "sky_part_sizes": [c_p, P_i64, P_i64],
+    "sky_part_snapshot_reps": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64, P_i64],
     "sky_global_merge": [c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, P_i64],
     "sky_parts_global_merge": [c_p, c_int, c_p, c_p, c_p, c_p, c_i64, P_i64],
+    "sky_global_merge_reps": [c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, P_i64],
     "sky_global_stats": [c_p, c_p, c_p, P_i32],
     "sky_global_stats_set": [c_p, c_i32, c_p, c_p],
     "sky_query": [c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, P_i64],
@@ -105,6 +108,8 @@ SIGNATURES = {
     "sky_profile_sort_dev": [c_p, c_p, c_p, c_i64, P_i32, P_dbl],
     "sky_last_error": [],
     "sky_version": [],
+    "sky_device_count": [P_i32],
+    "sky_device_for_subtask": [c_i32, c_i32, P_i32],
 }
 
 

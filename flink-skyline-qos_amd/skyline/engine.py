@@ -152,6 +152,30 @@ class SkylineEngine:
         g = cnt.value
         return out_ids[:g].copy(), out_org[:g].copy()
 
+    def global_merge_reps(self, part_ids, lists):
+        """sky_global_merge_reps: the merge over local skylines shipped as distinct vectors;
+        lists[g] = (ids int64 [T], rep_idx int32 [T], reps f64 [R, dims], rep_counts int32 [R]).
+        Same (ids, origins) and stats as global_merge over the expanded lists."""
+        n = len(part_ids)
+        idl = [np.ascontiguousarray(l[0], np.int64) for l in lists]
+        rpi = [np.ascontiguousarray(l[1], np.int32) for l in lists]
+        rps = [np.ascontiguousarray(l[2], np.float64).reshape(-1, self.dims) for l in lists]
+        rpc = [np.ascontiguousarray(l[3], np.int32) for l in lists]
+        counts = np.array([len(a) for a in idl], np.int64)
+        nreps = np.array([len(a) for a in rps], np.int64)
+        pids = np.ascontiguousarray(part_ids, dtype=np.int32)
+
+        def arr(xs):
+            return (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in xs])
+        tot = int(counts.sum())
+        out_ids = np.empty(max(tot, 1), np.int64)
+        out_org = np.empty(max(tot, 1), np.int32)
+        cnt = ctypes.c_int64(0)
+        check(lib().sky_global_merge_reps(self.h, n, _ptr(pids), arr(idl), arr(rpi), _ptr(counts), arr(rps), arr(rpc),
+                                          _ptr(nreps), _ptr(out_ids), _ptr(out_org), tot, ctypes.byref(cnt)))
+        g = cnt.value
+        return out_ids[:g].copy(), out_org[:g].copy()
+
     # ---- multi-GPU step with one host read (sky_dist_*) ------------------------------------
     def dist_export_dev(self, d_ids, d_values, d_block, cap):
         """Local skylines of this rank's shard -> its fixed-size exchange block (no host read)."""

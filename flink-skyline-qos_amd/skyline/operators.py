@@ -181,6 +181,22 @@ def make_partitioner(algo, num_partitions, domain, dims, device=0):
     return PartitioningLogic.AnglePartitioner(num_partitions, dims, device)
 
 
+def device_count():
+    """HIP devices this process sees (sky_device_count; 0 without a GPU)."""
+    n = ctypes.c_int32(0)
+    check(lib().sky_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def device_for_subtask(subtask, ndev=None):
+    """The device of a Flink subtask's context (sky_device_for_subtask): subtask % ndev, as
+    HipSkylineOperators.open() maps getIndexOfThisSubtask() over the node's GPUs."""
+    ndev = device_count() if ndev is None else ndev
+    d = ctypes.c_int32(0)
+    check(lib().sky_device_for_subtask(int(subtask), int(ndev), ctypes.byref(d)))
+    return d.value
+
+
 class _LocalPart:
     def __init__(self, engine, key):
         h = ctypes.c_void_p()
@@ -240,10 +256,44 @@ class _LocalPart:
                                       vals.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n)))
         return ids[:n.value].copy(), vals[:n.value].copy()
 
+    def snapshot_reps(self):
+        """sky_part_sizes + sky_part_snapshot_reps: the local skyline as distinct vectors."""
+        n, r = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().sky_part_sizes(self.h, ctypes.byref(n), ctypes.byref(r)))
+        ids = np.empty(max(n.value, 1), np.int64)
+        rep = np.empty(max(n.value, 1), np.int32)
+        reps = np.empty((max(r.value, 1), self.dims), np.float64)
+        rcnt = np.empty(max(r.value, 1), np.int32)
+        check(lib().sky_part_snapshot_reps(self.h, ids.ctypes.data_as(ctypes.c_void_p),
+                                           rep.ctypes.data_as(ctypes.c_void_p), n.value,
+                                           reps.ctypes.data_as(ctypes.c_void_p),
+                                           rcnt.ctypes.data_as(ctypes.c_void_p), r.value,
+                                           ctypes.byref(n), ctypes.byref(r)))
+        return LocalSkyline(ids[:n.value].copy(), rep[:n.value].copy(), reps[:r.value].copy(), rcnt[:r.value].copy())
+
     def close(self):
         if self.h:
             lib().sky_part_close(self.h)
             self.h = None
+
+
+class LocalSkyline:
+    """The message LocalProcessor.processQuery sends to the aggregator (field 4 of the Tuple6 of
+    FlinkSkyline.java:396-403, there a List<ServiceTuple>): the tuples (ids, rep index) in
+    insertion order and their distinct vectors with tuple counts -- on the reference streams
+    key 0's local skyline is millions of copies of one vector."""
+
+    __slots__ = ("ids", "rep_idx", "reps", "rep_counts")
+
+    def __init__(self, ids, rep_idx, reps, rep_counts):
+        self.ids, self.rep_idx, self.reps, self.rep_counts = ids, rep_idx, reps, rep_counts
+
+    def __len__(self):
+        return len(self.ids)
+
+    def values(self):
+        """The expanded rows (the reference's List<ServiceTuple> values), n x dims."""
+        return self.reps[self.rep_idx] if len(self.ids) else self.reps[:0]
 
 
 class SkylineLocalProcessor:
@@ -413,8 +463,8 @@ class SkylineLocalProcessor:
         total = self.accumulatedCpuNanosState.get(key, 0) + (time.perf_counter_ns() - start)
         self.accumulatedCpuNanosState[key] = total
         part_start = self.startTimeState.get(key, now_ms())
-        ids, vals = self.localSkylineState[key].snapshot()
-        out.append((trigger[0], trigger[1], trigger[2], part_start, (ids, vals), total // 1_000_000))
+        sky = self.localSkylineState[key].snapshot_reps()
+        out.append((trigger[0], trigger[1], trigger[2], part_start, sky, total // 1_000_000))
 
     def processBuffer(self, key):
         """S <- SKY(S u buffer) on the device (the BNL of :417-444)."""
@@ -435,7 +485,8 @@ class SkylineLocalProcessor:
 class GlobalSkylineAggregator:
     """FlinkSkyline.GlobalSkylineAggregator (:460-660).  Collects the P local
     skylines of one query key and, on the last arrival, merges them on the
-    device (sky_global_merge) and emits the JSON payload (:631-648)."""
+    device (sky_global_merge_reps over the distinct-vector messages) and emits the JSON
+    payload (:631-648)."""
 
     def __init__(self, engine, totalPartitions):
         self.engine = engine
@@ -443,7 +494,7 @@ class GlobalSkylineAggregator:
         self.state = {}
 
     def processElement(self, inp, out):
-        pid, payload, dispatch_ms, pstart, (ids, vals), cpu_ms = inp
+        pid, payload, dispatch_ms, pstart, sky, cpu_ms = inp
         st = self.state.setdefault(payload, {"lists": [], "count": 0, "minStart": None, "lastArr": None,
                                              "maxCpu": None})
         if st["minStart"] is None or (pstart is not None and pstart < st["minStart"]):
@@ -451,12 +502,12 @@ class GlobalSkylineAggregator:
         st["lastArr"] = now_ms()
         if st["maxCpu"] is None or cpu_ms > st["maxCpu"]:
             st["maxCpu"] = cpu_ms
-        st["lists"].append((pid, ids, vals))
+        st["lists"].append((pid, sky))
         st["count"] += 1
         if st["count"] >= self.totalPartitions:
             lists = st["lists"]
-            gids, gorg = self.engine.global_merge([l[0] for l in lists], [l[1] for l in lists],
-                                                  [l[2] for l in lists])
+            gids, gorg = self.engine.global_merge_reps(
+                [l[0] for l in lists], [(l[1].ids, l[1].rep_idx, l[1].reps, l[1].rep_counts) for l in lists])
             finish = now_ms()
             job_start = st["minStart"]
             map_finish = st["lastArr"]
@@ -469,7 +520,7 @@ class GlobalSkylineAggregator:
             # optimality (:593-608): the local size of partition i is its list size
             sizes = {}
             for l in lists:
-                sizes[l[0]] = len(l[1])
+                sizes[l[0]] = len(l[1])      # the list's tuple count
             surv = {}
             for o in gorg.tolist():
                 surv[o] = surv.get(o, 0) + 1

@@ -108,6 +108,12 @@ int sky_ctx_wait_stream(sky_ctx *ctx, void *hip_stream);
 int sky_ctx_signal_stream(sky_ctx *ctx, void *hip_stream);
 const char *sky_last_error(void);
 const char *sky_version(void);
+/* HIP devices this process sees (*n_out = 0 without a GPU, not an error), and the device a
+ * Flink subtask's context goes on: subtask % ndev.  The reference runs `parallelism` subtasks
+ * over 2p keys (FlinkSkyline.java:66,76,138); HipSkylineOperators creates each subtask's
+ * context on sky_device_for_subtask(getIndexOfThisSubtask(), sky_device_count()). */
+int sky_device_count(int32_t *n_out);
+int sky_device_for_subtask(int32_t subtask, int32_t ndev, int32_t *dev_out);
 
 /* ---- partitioners --------------------------------------------------------- */
 /* keys_out[i] = getKey(tuple i), bit-exact with Java (fdlibm atan2, no FMA);
@@ -132,6 +138,16 @@ int sky_part_size(sky_part *part, int64_t *n_out);
  * SKY_E_CAPACITY with *n_out set if cap is too small */
 int sky_part_snapshot(sky_part *part, int64_t *ids_out, double *values_out, int64_t cap,
                       int64_t *n_out);
+/* the local skyline as the state holds it: T tuples (ids_out[i], rep_out[i] = index of its
+ * vector) in insertion order, and R distinct vectors (reps_out: R x dims row-major, and
+ * rep_count_out[r] = tuples on vector r).  What LocalProcessor.processQuery ships to the
+ * aggregator: on the reference streams key 0's 4.4M skyline tuples are ONE vector, so the
+ * message is its ids and rep indices (12 bytes per tuple) instead of 8 + 8 dims.
+ * sky_part_sizes gives T and R; SKY_E_CAPACITY with both counts set if a cap is too small. */
+int sky_part_sizes(sky_part *part, int64_t *n_tuples, int64_t *n_reps);
+int sky_part_snapshot_reps(sky_part *part, int64_t *ids_out, int32_t *rep_out, int64_t cap,
+                           double *reps_out, int32_t *rep_count_out, int64_t rep_cap,
+                           int64_t *n_out, int64_t *nrep_out);
 
 /* ---- global merge ---------------------------------------------------------- */
 /* G = SKY(u_k list_k) for the nparts local skylines; origin_out[j] = part_ids[k] of
@@ -146,6 +162,14 @@ int sky_global_merge(sky_ctx *ctx, int nparts, const int32_t *part_ids,
  * For an aggregator co-located with the local processors (one process drives the device). */
 int sky_parts_global_merge(sky_ctx *ctx, int nparts, sky_part *const *parts, const int32_t *part_ids,
                            int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
+/* sky_global_merge over lists shipped as sky_part_snapshot_reps output (list g: counts[g]
+ * tuples ids[g] / rep_idx[g], nreps[g] vectors reps[g] with rep_counts[g] tuples each): same
+ * result, order, origins and sky_global_stats as sky_global_merge over the expanded lists.
+ * A rep index outside [0, nreps[g]) is SKY_E_ARG. */
+int sky_global_merge_reps(sky_ctx *ctx, int nlists, const int32_t *part_ids, const int64_t *const *ids,
+                          const int32_t *const *rep_idx, const int64_t *counts, const double *const *reps,
+                          const int32_t *const *rep_counts, const int64_t *nreps, int64_t *ids_out,
+                          int32_t *origin_out, int64_t cap, int64_t *n_out);
 /* integers behind the optimality metric of the last merge / query:
  * local_sizes[k] = |L_k|, survivors[k] = |G n L_k| for k < K
  * (K = P, or max(P, 2^D) for MR-Grid with SKY_SEM_COMPLETE). */

@@ -149,6 +149,33 @@ def test_ctx_create_without_gpu_fails_loudly():
     assert e.value.code == -6
 
 
+def test_subtask_device_map():
+    """HipSkylineOperators puts subtask i's context on sky_device_for_subtask(i, sky_device_count()):
+    round-robin over the node's GPUs (the reference runs `parallelism` subtasks over 2p keys,
+    FlinkSkyline.java:66,76,138).  No GPU here: zero devices, not an error."""
+    import ctypes
+    import torch
+    import skyline
+    from skyline._abi import SKY_E_ARG, SKY_OK
+    L = skyline.lib()
+    n = ctypes.c_int32(-1)
+    assert L.sky_device_count(ctypes.byref(n)) == SKY_OK
+    if not torch.cuda.is_available():
+        assert n.value == 0
+    dev = ctypes.c_int32(-1)
+    got = []
+    for sub in range(12):
+        assert L.sky_device_for_subtask(sub, 8, ctypes.byref(dev)) == SKY_OK
+        got.append(dev.value)
+    assert got == [0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3]
+    for sub in range(5):                                 # one GPU: every subtask on device 0
+        assert L.sky_device_for_subtask(sub, 1, ctypes.byref(dev)) == SKY_OK and dev.value == 0
+    assert L.sky_device_for_subtask(3, 0, ctypes.byref(dev)) == SKY_E_ARG    # no device: the caller must not create
+    assert L.sky_device_for_subtask(-1, 8, ctypes.byref(dev)) == SKY_E_ARG
+    from skyline.operators import device_for_subtask
+    assert [device_for_subtask(s, 3) for s in range(7)] == [0, 1, 2, 0, 1, 2, 0]
+
+
 def test_host_generator_matches_oracle(oracle):
     import skyline
     for dist in range(5):

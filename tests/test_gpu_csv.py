@@ -119,10 +119,13 @@ def test_csv_long_records_and_numbers(gpu_engine_factory, oracle):
     eng.close()
 
 
-def test_csv_exact_reparse_path():
+@pytest.mark.parametrize("chunks", ["0", "1"])
+def test_csv_exact_reparse_path(chunks):
     """More exact conversions than the queue holds: every record is re-parsed on the exact
     path (groups of 256 records, boundaries found by the fallback workgroups).  The queue
-    size is read once per process, so this runs in a child process with a 4-entry queue."""
+    size is read once per process, so this runs in a child process with a 4-entry queue.
+    chunks=1: the byte-chunk route, which never sizes the group array itself -- the exact
+    re-parse must size it (round 3 faulted here: an illegal address in the re-parse)."""
     import os
     import subprocess
     import sys
@@ -148,7 +151,7 @@ _check(eng, Oracle(), text, 2)
 _check(eng, Oracle(), text[:-1], 2)          # tail record without a newline
 print("ok")
 """ % (os.path.join(os.path.dirname(here), "flink-skyline-qos_amd"), here)
-    env = dict(os.environ, SKY_CSV_SLOW_CAP="4")
+    env = dict(os.environ, SKY_CSV_SLOW_CAP="4", SKY_CSV_CHUNKS=chunks)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 

@@ -171,7 +171,7 @@ def test_local_processor_checkpoint_restore(oracle):
         out = []
         for k in range(P):
             proc.processElement2((k, "q", 0), out)          # requiredCount 0: answered now (:305)
-        return {t[0]: (np.sort(t[4][0]), t[4][1][np.argsort(t[4][0])]) for t in out}
+        return {t[0]: (np.sort(t[4].ids), t[4].values()[np.argsort(t[4].ids)]) for t in out}
 
     e1 = skyline.SkylineEngine(D, P, "mr-angle")
     ref = SkylineLocalProcessor(e1)

@@ -232,6 +232,19 @@ def test_parts_global_merge_equals_snapshot_merge(dist, D, n, gpu_engine_factory
     np.testing.assert_array_equal(g_org, e_org)
     np.testing.assert_array_equal(ls_dev, ls_ref)
     np.testing.assert_array_equal(sv_dev, sv_ref)
+    # the distinct-vector messages (what the Java LocalProcessor ships): same expansion, same merge
+    reps = [p.snapshot_reps() for p in plist]
+    for r, sn in zip(reps, snaps):
+        np.testing.assert_array_equal(r.ids, sn[0])
+        np.testing.assert_array_equal(r.values(), sn[1])
+        np.testing.assert_array_equal(r.rep_counts, np.bincount(r.rep_idx, minlength=len(r.reps)))
+        assert len(np.unique(r.reps, axis=0)) == len(r.reps)
+    r_ids, r_org = eng.global_merge_reps(order, [(r.ids, r.rep_idx, r.reps, r.rep_counts) for r in reps])
+    ls_r, sv_r = eng.stats()
+    np.testing.assert_array_equal(r_ids, e_ids)
+    np.testing.assert_array_equal(r_org, e_org)
+    np.testing.assert_array_equal(ls_r, ls_ref)
+    np.testing.assert_array_equal(sv_r, sv_ref)
     exp, _, _, _ = oracle.query_bnl("angle", vals, ids, P)
     assert sorted(g_ids.tolist()) == sorted(exp.tolist())
     for p in parts.values():
@@ -263,6 +276,19 @@ def test_parts_global_merge_edge_cases(gpu_engine_factory, oracle):
         np.testing.assert_array_equal(g_org, e_org)
         np.testing.assert_array_equal(ls_dev, ls_ref)
         np.testing.assert_array_equal(sv_dev, sv_ref)
+        reps = [p.snapshot_reps() for p in plist]
+        r_ids, r_org = eng.global_merge_reps(pids, [(r.ids, r.rep_idx, r.reps, r.rep_counts) for r in reps])
+        np.testing.assert_array_equal(r_ids, e_ids)
+        np.testing.assert_array_equal(r_org, e_org)
+        for x, y in zip(eng.stats(), (ls_ref, sv_ref)):
+            np.testing.assert_array_equal(x, y)
+    # a rep index outside its list's reps is an argument error, not an out-of-range read
+    r = a.snapshot_reps()
+    bad = r.rep_idx.copy()
+    bad[len(bad) // 2] = len(r.reps)
+    with pytest.raises(SkylineError) as e:
+        eng.global_merge_reps([0], [(r.ids, bad, r.reps, r.rep_counts)])
+    assert e.value.code == -1
     for p in (a, b, c):
         p.close()
     eng.close()

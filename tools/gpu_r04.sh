@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-4 GPU pass: STEPS (comma list) of
+#   tests   the whole gpu suite (PYTEST_ARGS narrows it)
+#   bench   bench.py (BENCH_ARGS) -> gpurun_out/bench_$TAG.json
+#   dom     tools/dom_bench.py at 2M and 10M std-anti (DOM_ARGS)
+#   trace   rocprofv3 kernel-trace of bench.py (BENCH_ARGS)
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -e
+R=$GRAFT_REPO_ROOT; [ -z "$R" ] && R=$(pwd)
+OUT=$R/gpurun_out; mkdir -p $OUT
+cd $R
+TAG=${TAG:-r04}
+STEPS=${STEPS:-tests}
+export PYTHONUNBUFFERED=1
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 900 $PYT -m gpu ${PYTEST_ARGS:-tests} > $OUT/pytest_$TAG.log 2>&1 || { tail -60 $OUT/pytest_$TAG.log; exit 1; }
+  tail -3 $OUT/pytest_$TAG.log
+fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || { tail -30 $OUT/smoke_$TAG.log; exit 1; }
+  tail -2 $OUT/smoke_$TAG.log
+fi
+if [[ $STEPS == *dom* ]]; then
+  for N in ${DOM_NS:-2000000 10000000}; do
+    timeout -k 10 300 python -u tools/dom_bench.py $N 3 ${DOM_ARGS} > $OUT/dom_${TAG}_$N.log 2>&1 || { tail -30 $OUT/dom_${TAG}_$N.log; exit 1; }
+    tail -3 $OUT/dom_${TAG}_$N.log
+  done
+fi
+if [[ $STEPS == *mtrace* ]]; then
+  # measurement build: the pair pass's per-work-item timeline (SKY_MBR_DBG=8)
+  for N in ${DOM_NS:-2000000 10000000}; do
+    SKYLINE_HIP_LIB=$R/flink-skyline-qos_amd/build_measure/libskyline_hip.so SKY_MBR_DBG=${MBR_DBG:-8} \
+      timeout -k 10 300 python -u tools/dom_bench.py $N 2 > $OUT/mtrace_${TAG}_$N.log 2>&1 || { tail -30 $OUT/mtrace_${TAG}_$N.log; exit 1; }
+    grep "mbr-trace" $OUT/mtrace_${TAG}_$N.log | tail -4
+  done
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
+  cut -c1-1500 $OUT/bench_$TAG.json
+fi
+if [[ $STEPS == *trace* ]]; then
+  export TMPDIR=/tmp
+  rm -rf $OUT/trace_$TAG
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$TAG -o run -- python3 -u $R/bench.py ${BENCH_ARGS} > $OUT/trace_$TAG.log 2>&1 || { tail -30 $OUT/trace_$TAG.log; exit 1; }
+  python tools/prof_summary.py trace $OUT/trace_$TAG > $OUT/trace_${TAG}_summary.txt
+  head -30 $OUT/trace_${TAG}_summary.txt
+fi
