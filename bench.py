@@ -543,19 +543,92 @@ def operator_run(dev_index, n=10_000_000, buf=5000, micro=80_000):
                 "max_call_ms": lat[-1] if lat else None,
                 "skyline_size": int(len(gids)), "local_sizes": local_sizes, "skyline_ids": gids}
 
+    # ---- the Java operators' exact call sequence (HipSkylineOperators, java/org/main): full buffers
+    #      in arrival order wait until FLUSH_GROUP = 8 are pending, then drainFull issues rounds (the
+    #      first waiting buffer of every key, one sky_parts_insert per round); the trigger: per key
+    #      drainFull + the partial buffer's sky_part_insert + sky_part_sizes + sky_part_snapshot_reps
+    #      (the LocalSkyline message), then sky_global_merge_reps over the P messages
+    done_pos = []
+    for k in range(P):
+        for j in range(len(per_key[k]) // buf):
+            done_pos.append((int(per_key[k][(j + 1) * buf - 1]), k, j))
+    done_pos.sort()
+    jsched, fifo = [], []
+
+    def drain():
+        nonlocal fifo
+        while fifo:
+            seen, rnd, later = set(), [], []
+            for kj in fifo:
+                (later if kj[0] in seen else rnd).append(kj)
+                seen.add(kj[0])
+            jsched.append(rnd)
+            fifo = later
+    for _, k, j in done_pos:
+        fifo.append((k, j))
+        if len(fifo) >= 8:
+            drain()
+    drain()
+
+    def java_sequence():
+        parts = {k: _LocalPart(eng, k) for k in range(P)}
+        args = []
+        for rnd in jsched:
+            nc = len(rnd)
+            args.append((nc, (ctypes.c_void_p * nc)(*[parts[k].h.value for k, _ in rnd]),
+                         (ctypes.c_void_p * nc)(*[batches[k][0].ctypes.data + j * buf * 8 for k, j in rnd]),
+                         (ctypes.c_void_p * nc)(*[batches[k][1].ctypes.data + j * buf * D * 8 for k, j in rnd]),
+                         (ctypes.c_int64 * nc)(*([buf] * nc))))
+        f_ins = lib().sky_parts_insert
+        lat = []
+        t0 = time.perf_counter()
+        for a in args:
+            ts = time.perf_counter()
+            check(f_ins(*a))
+            lat.append((time.perf_counter() - ts) * 1e3)
+        t_ins = time.perf_counter() - t0
+        tq = time.perf_counter()
+        msgs = []
+        for k in range(P):                       # processQuery on every key (the trigger's broadcast)
+            nf = len(per_key[k]) // buf
+            if len(per_key[k]) > nf * buf:
+                parts[k].insert(batches[k][0][nf * buf:], batches[k][1][nf * buf:])
+            m = parts[k].snapshot_reps()
+            msgs.append((m.ids, m.rep_idx, m.reps, m.rep_counts))
+        t_snap = time.perf_counter() - tq
+        gids, _ = eng.global_merge_reps(list(range(P)), msgs)   # GlobalAggregator, last arrival
+        t_q = time.perf_counter() - tq
+        total = time.perf_counter() - t0
+        for pt in parts.values():
+            pt.close()
+        lat.sort()
+        return {"calls": len(lat), "flushes": sum(len(r) for r in jsched), "insert_phase_s": t_ins,
+                "query_phase_s": t_q, "snapshot_s": t_snap, "merge_s": t_q - t_snap, "tuples_per_s": n / total,
+                "p50_call_ms": lat[len(lat) // 2] if lat else None,
+                "p99_call_ms": lat[min(len(lat) - 1, int(len(lat) * 0.99))] if lat else None,
+                "message_bytes": int(sum(m[0].nbytes + m[1].nbytes + m[2].nbytes + m[3].nbytes for m in msgs)),
+                "message_tuples": int(sum(len(m[0]) for m in msgs)), "message_vectors": int(sum(len(m[2]) for m in msgs)),
+                "skyline_size": int(len(gids)), "skyline_ids": gids}
+
     run(True)                                          # first launches / allocations
     b = run(True)
     s1 = run(False, device_merge=False)
+    java_sequence()
+    js = java_sequence()
     exp = eng.query(vals, ids)[0]
     exact = bool(np.array_equal(np.sort(b.pop("skyline_ids")), exp) and
-                 np.array_equal(np.sort(s1.pop("skyline_ids")), exp))
+                 np.array_equal(np.sort(s1.pop("skyline_ids")), exp) and
+                 np.array_equal(np.sort(js.pop("skyline_ids")), exp))
     eng.close()
     return {"workload": f"C4 stream prefix, {n} tuples, MR-Angle P={P}, per-key {buf}-tuple buffers from host memory; "
                         f"the full buffers flushed after every {micro}-tuple micro-batch in one sky_parts_insert "
                         f"call, then the co-located global merge of the device-resident states "
                         f"(sky_parts_global_merge); 'one_call_per_buffer': one sky_part_insert per buffer, then "
                         f"snapshots through host memory + sky_global_merge",
-            "exact_vs_whole_stream_query": exact, "batched": b, "one_call_per_buffer": s1,
+            "java_sequence_workload": "the Java operators' calls exactly (HipSkylineOperators): drainFull rounds of "
+                                      "sky_parts_insert every 8 full buffers, per key sky_part_sizes + "
+                                      "sky_part_snapshot_reps at the trigger, sky_global_merge_reps",
+            "exact_vs_whole_stream_query": exact, "batched": b, "one_call_per_buffer": s1, "java_sequence": js,
             "tuples_per_s": b["tuples_per_s"], "p50_call_ms": b["p50_call_ms"], "p99_call_ms": b["p99_call_ms"]}
 
 

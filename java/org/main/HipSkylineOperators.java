@@ -27,6 +27,16 @@ import java.util.Map;
  * Drop-in replacements for the two hot-path operators of FlinkSkyline.java, running their
  * dominance work in libskyline_hip.so on the MI355X (through SkylineHip / JNI).
  *
+ * Devices: every subtask creates its context on SkylineHip.deviceForSubtask(getIndexOfThisSubtask(),
+ * deviceCount()), so the `parallelism` subtasks of an operator (FlinkSkyline.java:66,76,138)
+ * spread round-robin over the node's GPUs; a TaskManager without a GPU fails in open().
+ *
+ * The local skylines travel between the two operators as LocalSkyline messages (field 4 of the
+ * Tuple6, a List<ServiceTuple> in the reference, :396-403): the tuples as (id, index of their
+ * vector) and the distinct vectors with their tuple counts -- on the reference streams key 0's
+ * 4.4M skyline tuples are one all-zero vector, so the message is 12 bytes per tuple and no
+ * ServiceTuple objects are built on either side.
+ *
  * Topology change in FlinkSkyline.main (:162-176):
  *   keyedData.connect(keyedTriggers).process(new HipSkylineOperators.LocalProcessor(dims, P, algo, domain))
  *   ...keyBy(t -> t.f1).process(new HipSkylineOperators.GlobalAggregator(P, dims, algo, domain))
@@ -67,14 +77,50 @@ public final class HipSkylineOperators {
         }
     }
 
+    /** A local skyline as distinct vectors (sky_part_snapshot_reps): tuple i is ids[i] with the
+     *  values reps[repIdx[i] * dims ..]; repCounts[r] = tuples on vector r.  A Flink POJO. */
+    public static final class LocalSkyline {
+        public long[] ids;
+        public int[] repIdx;
+        public double[] reps;
+        public int[] repCounts;
+
+        public LocalSkyline() {}
+
+        LocalSkyline(long[] ids, int[] repIdx, double[] reps, int[] repCounts) {
+            this.ids = ids;
+            this.repIdx = repIdx;
+            this.reps = reps;
+            this.repCounts = repCounts;
+        }
+
+        public int size() {
+            return ids.length;
+        }
+    }
+
+    /** The context of this subtask, on its GPU (see the class comment). */
+    static long openContext(org.apache.flink.api.common.functions.RuntimeContext rc, int dims, int partitions,
+                            int algo, double domain) {
+        final int ndev = SkylineHip.deviceCount();
+        if (ndev < 1) throw new IllegalStateException("no HIP device visible to this TaskManager");
+        final long ctx = SkylineHip.ctxCreate(SkylineHip.deviceForSubtask(rc.getIndexOfThisSubtask(), ndev), dims,
+                partitions, algo, domain);
+        SkylineHip.ctxWarmup(ctx);                     // first kernel launches off the query path
+        return ctx;
+    }
+
     /**
      * SkylineLocalProcessor (FlinkSkyline.java:214-445) with the per-key skyline held on the
      * device: processBuffer's BNL (:417-444) is an asynchronous sky_parts_insert of the full
-     * buffers of up to FLUSH_GROUP keys; processQuery's snapshot (:387-392) is sky_part_snapshot
-     * (after every waiting buffer).  The id barrier (:276-356) is unchanged.
+     * buffers of up to FLUSH_GROUP keys; processQuery's snapshot (:387-392) is
+     * sky_part_snapshot_reps (after every waiting buffer).  The id barrier (:276-356) is unchanged.
+     * A device error or NaN in a buffer held back for its flush group surfaces at the flush, from
+     * whichever element, query or checkpoint triggers it; its message names the key whose batch
+     * failed ("batch of key k").
      */
     public static class LocalProcessor extends KeyedCoProcessFunction<Integer, ServiceTuple,
-            Tuple3<Integer, String, Long>, Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>
+            Tuple3<Integer, String, Long>, Tuple6<Integer, String, Long, Long, LocalSkyline, Long>>
             implements CheckpointedFunction {
         private final int dims, partitions, algo;
         private final double domain;
@@ -98,8 +144,7 @@ public final class HipSkylineOperators {
 
         @Override
         public void open(Configuration config) {
-            ctx = SkylineHip.ctxCreate(0, dims, partitions, algo, domain);
-            SkylineHip.ctxWarmup(ctx);                 // first kernel launches off the query path
+            ctx = openContext(getRuntimeContext(), dims, partitions, algo, domain);
             parts = new HashMap<>();
             buffers = new HashMap<>();
             maxSeenIdState = getRuntimeContext().getState(new ValueStateDescriptor<>("maxId", Long.class));
@@ -212,7 +257,7 @@ public final class HipSkylineOperators {
 
         @Override
         public void processElement1(ServiceTuple point, Context c,
-                                    Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                                    Collector<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>> out)
                 throws Exception {
             final long startNano = System.nanoTime();
             final int key = c.getCurrentKey();
@@ -246,7 +291,7 @@ public final class HipSkylineOperators {
 
         @Override
         public void processElement2(Tuple3<Integer, String, Long> trigger, Context c,
-                                    Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                                    Collector<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>> out)
                 throws Exception {
             Long current = maxSeenIdState.value();
             long cur = current == null ? -1L : current;
@@ -255,24 +300,17 @@ public final class HipSkylineOperators {
         }
 
         private void processQuery(Tuple3<Integer, String, Long> trigger, int key,
-                                  Collector<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> out)
+                                  Collector<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>> out)
                 throws Exception {
             final long startNano = System.nanoTime();
             flush(key);
             final long p = part(key);
-            int n = (int) SkylineHip.partSize(p);
-            long[] ids = new long[n];
-            double[] vals = new double[n * dims];
-            n = SkylineHip.partSnapshot(p, ids, vals);
+            final long[] sizes = new long[2];
+            SkylineHip.partSizes(p, sizes);                // the one synchronisation of the query
+            final int n = (int) sizes[0], r = (int) sizes[1];
+            final LocalSkyline sky = new LocalSkyline(new long[n], new int[n], new double[r * dims], new int[r]);
+            SkylineHip.partSnapshotReps(p, sky.ids, sky.repIdx, sky.reps, sky.repCounts);
             addCpu(startNano);
-            List<ServiceTuple> sky = new ArrayList<>(n);
-            for (int i = 0; i < n; i++) {
-                double[] v = new double[dims];
-                System.arraycopy(vals, i * dims, v, 0, dims);
-                ServiceTuple t = new ServiceTuple(Long.toString(ids[i]), v);
-                t.originPartition = key;
-                sky.add(t);
-            }
             Long start = startTimeState.value();
             Long cpu = accumulatedCpuNanosState.value();
             out.collect(new Tuple6<>(trigger.f0, trigger.f1, trigger.f2,
@@ -282,15 +320,16 @@ public final class HipSkylineOperators {
 
     /**
      * GlobalSkylineAggregator (FlinkSkyline.java:460-660): collects the P local skylines of one
-     * query, then ONE sky_global_merge (the BNL merge of :548-566) and sky_global_stats (the
-     * optimality integers of :593-608) on the last arrival, and the JSON payload of :631-648.
+     * query, then ONE sky_global_merge_reps (the BNL merge of :548-566 over the distinct-vector
+     * messages) and sky_global_stats (the optimality integers of :593-608) on the last arrival,
+     * and the JSON payload of :631-648.
      */
     public static class GlobalAggregator extends KeyedProcessFunction<String,
-            Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>, String> {
+            Tuple6<Integer, String, Long, Long, LocalSkyline, Long>, String> {
         private final int totalPartitions, dims, algo;
         private final double domain;
         private transient long ctx;
-        private transient ValueState<List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>> arrived;
+        private transient ValueState<List<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>>> arrived;
         private transient ValueState<Long> minStartTimeState;
 
         public GlobalAggregator(int totalPartitions, int dims, String algo, double domain) {
@@ -302,10 +341,9 @@ public final class HipSkylineOperators {
 
         @Override
         public void open(Configuration config) {
-            ctx = SkylineHip.ctxCreate(0, dims, totalPartitions, algo, domain);
-            SkylineHip.ctxWarmup(ctx);
+            ctx = openContext(getRuntimeContext(), dims, totalPartitions, algo, domain);
             arrived = getRuntimeContext().getState(new ValueStateDescriptor<>("arrived",
-                    TypeInformation.of(new TypeHint<List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>>>() {})));
+                    TypeInformation.of(new TypeHint<List<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>>>() {})));
             minStartTimeState = getRuntimeContext().getState(new ValueStateDescriptor<>("minStart", Long.class));
         }
 
@@ -316,11 +354,11 @@ public final class HipSkylineOperators {
         }
 
         @Override
-        public void processElement(Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long> in, Context c,
+        public void processElement(Tuple6<Integer, String, Long, Long, LocalSkyline, Long> in, Context c,
                                    Collector<String> out) throws Exception {
             Long minStart = minStartTimeState.value();
             if (minStart == null || in.f3 < minStart) minStartTimeState.update(in.f3);
-            List<Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long>> lists = arrived.value();
+            List<Tuple6<Integer, String, Long, Long, LocalSkyline, Long>> lists = arrived.value();
             if (lists == null) lists = new ArrayList<>();
             lists.add(in);
             if (lists.size() < totalPartitions) {
@@ -331,25 +369,24 @@ public final class HipSkylineOperators {
             final int np = lists.size();
             int[] partIds = new int[np];
             long[][] ids = new long[np][];
-            double[][] vals = new double[np][];
+            int[][] repIdx = new int[np][];
+            double[][] reps = new double[np][];
+            int[][] repCounts = new int[np][];
             long maxCpu = 0;
             int total = 0;
             for (int k = 0; k < np; k++) {
-                Tuple6<Integer, String, Long, Long, List<ServiceTuple>, Long> t = lists.get(k);
+                Tuple6<Integer, String, Long, Long, LocalSkyline, Long> t = lists.get(k);
                 partIds[k] = t.f0;
-                List<ServiceTuple> l = t.f4;
-                ids[k] = new long[l.size()];
-                vals[k] = new double[l.size() * dims];
-                for (int i = 0; i < l.size(); i++) {
-                    ids[k][i] = Long.parseLong(l.get(i).id);
-                    System.arraycopy(l.get(i).values, 0, vals[k], i * dims, dims);
-                }
-                total += l.size();
+                ids[k] = t.f4.ids;
+                repIdx[k] = t.f4.repIdx;
+                reps[k] = t.f4.reps;
+                repCounts[k] = t.f4.repCounts;
+                total += t.f4.size();
                 maxCpu = Math.max(maxCpu, t.f5);
             }
             long[] gids = new long[Math.max(total, 1)];
             int[] gorg = new int[Math.max(total, 1)];
-            final int g = SkylineHip.globalMerge(ctx, partIds, ids, vals, gids, gorg);
+            final int g = SkylineHip.globalMergeReps(ctx, partIds, ids, repIdx, reps, repCounts, gids, gorg);
             long[] lsz = new long[np], surv = new long[np];
             SkylineHip.globalStats(ctx, lsz, surv);           // indexed by list, like partIds
             double sum = 0.0;

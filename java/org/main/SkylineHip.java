@@ -31,6 +31,11 @@ public final class SkylineHip {
         }
     }
 
+    /** HIP devices this TaskManager process sees (0 without a GPU). */
+    public static native int deviceCount();
+    /** The device of subtask `subtask`: subtask % ndev (sky_device_for_subtask). */
+    public static native int deviceForSubtask(int subtask, int ndev);
+
     public static native long ctxCreate(int device, int dims, int partitions, int algo, double domain);
     public static native void ctxDestroy(long ctx);
     public static native void ctxWarmup(long ctx);            // once in open(): first launches off the query path
@@ -46,12 +51,21 @@ public final class SkylineHip {
     public static native void partsInsert(long[] parts, long[][] ids, double[][] values, int[] counts);
     public static native long partSize(long part);
     public static native int partSnapshot(long part, long[] idsOut, double[] valuesOut);
+    /** sizesOut[0] = tuples T, sizesOut[1] = distinct vectors R of the local skyline. */
+    public static native void partSizes(long part, long[] sizesOut);
+    /** The local skyline as distinct vectors: ids[T], repIdx[T], reps[R * dims], repCounts[R];
+     *  returns T, or -T when an array is too small. */
+    public static native int partSnapshotReps(long part, long[] idsOut, int[] repIdxOut, double[] repsOut,
+                                              int[] repCountsOut);
 
     /** GlobalSkylineAggregator over the parts' device-resident states (co-located aggregator):
      *  the skyline size, or -(needed) when idsOut is too short. */
     public static native int partsGlobalMerge(long ctx, long[] parts, int[] partIds, long[] idsOut, int[] originOut);
     public static native int globalMerge(long ctx, int[] partIds, long[][] ids, double[][] values,
                                          long[] idsOut, int[] originOut);
+    /** globalMerge over partSnapshotReps messages: same ids, order, origins and stats. */
+    public static native int globalMergeReps(long ctx, int[] partIds, long[][] ids, int[][] repIdx, double[][] reps,
+                                             int[][] repCounts, long[] idsOut, int[] originOut);
     public static native int globalStats(long ctx, long[] localSizes, long[] survivors);
 
     public static native int query(long ctx, long[] ids, double[] values, int n, long[] idsOut, int[] originOut);

@@ -63,6 +63,19 @@ static int part_dims(sky_part *p) {
     return sky_part_info(p, NULL, &d) == SKY_OK ? d : -1;
 }
 
+/* ---- device map: which GPU a subtask's context goes on (FlinkSkyline.java:66,76,138) ---- */
+JNIEXPORT jint JNICALL Java_org_main_SkylineHip_deviceCount(JNIEnv *env, jclass cls) {
+    int32_t n = 0;
+    if (fail(env, sky_device_count(&n))) return 0;
+    return n;
+}
+
+JNIEXPORT jint JNICALL Java_org_main_SkylineHip_deviceForSubtask(JNIEnv *env, jclass cls, jint subtask, jint ndev) {
+    int32_t d = 0;
+    if (fail(env, sky_device_for_subtask(subtask, ndev, &d))) return 0;
+    return d;
+}
+
 /* ---- context: SkylineLocalProcessor.open() / GlobalSkylineAggregator.open() ---- */
 JNIEXPORT jlong JNICALL Java_org_main_SkylineHip_ctxCreate(JNIEnv *env, jclass cls, jint device, jint dims,
                                                             jint partitions, jint algo, jdouble domain) {
@@ -157,10 +170,12 @@ JNIEXPORT void JNICALL Java_org_main_SkylineHip_partsInsert(JNIEnv *env, jclass 
     {
         jlong *ph = (*env)->GetLongArrayElements(env, parts, NULL);
         jint *pc = (*env)->GetIntArrayElements(env, counts, NULL);
+        if (ph && pc)
+            for (jsize g = 0; g < np; g++) { pp[g] = PART(ph[g]); cnt[g] = pc[g]; }
+        /* each released on its own: one of them may have failed (OutOfMemoryError pending) */
+        if (pc) (*env)->ReleaseIntArrayElements(env, counts, pc, JNI_ABORT);
+        if (ph) (*env)->ReleaseLongArrayElements(env, parts, ph, JNI_ABORT);
         if (!ph || !pc) goto out;
-        for (jsize g = 0; g < np; g++) { pp[g] = PART(ph[g]); cnt[g] = pc[g]; }
-        (*env)->ReleaseIntArrayElements(env, counts, pc, JNI_ABORT);
-        (*env)->ReleaseLongArrayElements(env, parts, ph, JNI_ABORT);
     }
     for (jsize g = 0; g < np; g++) {   /* Get*ArrayElements: several arrays stay pinned/copied at once */
         const int D = part_dims(pp[g]);
@@ -221,7 +236,140 @@ JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partSnapshot(JNIEnv *env, jclass
     return (jint)n;
 }
 
+/* exact tuple and distinct-vector counts: sizes_out[0] = T, sizes_out[1] = R */
+JNIEXPORT void JNICALL Java_org_main_SkylineHip_partSizes(JNIEnv *env, jclass cls, jlong part, jlongArray sizes_out) {
+    if (bad_len(env, sizes_out, 2, "partSizes: sizesOut shorter than 2")) return;
+    int64_t t = 0, r = 0;
+    if (fail(env, sky_part_sizes(PART(part), &t, &r))) return;
+    const jlong v[2] = {(jlong)t, (jlong)r};
+    (*env)->SetLongArrayRegion(env, sizes_out, 0, 2, v);
+}
+
+/* processQuery's message as distinct vectors: ids[T], repIdx[T], reps[R * dims], repCounts[R];
+ * returns T, or -T when an array is too small (partSizes gives T and R) */
+JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partSnapshotReps(JNIEnv *env, jclass cls, jlong part,
+                                                                  jlongArray ids_out, jintArray rep_out,
+                                                                  jdoubleArray reps_out, jintArray rep_count_out) {
+    const int D = part_dims(PART(part));
+    if (D < 1 || !ids_out || !rep_out || !reps_out || !rep_count_out) {
+        throw_arg(env, "partSnapshotReps: bad part or null array");
+        return 0;
+    }
+    jsize cap = (*env)->GetArrayLength(env, ids_out);
+    if ((*env)->GetArrayLength(env, rep_out) < cap) cap = (*env)->GetArrayLength(env, rep_out);
+    jsize rcap = (*env)->GetArrayLength(env, rep_count_out);
+    if ((*env)->GetArrayLength(env, reps_out) / D < rcap) rcap = (*env)->GetArrayLength(env, reps_out) / D;
+    jlong *pi = CRIT(ids_out);
+    jint *pr = CRIT(rep_out);
+    jdouble *pv = CRIT(reps_out);
+    jint *pc = CRIT(rep_count_out);
+    int64_t n = 0, r = 0;
+    const int ok = pi && pr && pv && pc;
+    const int rc = ok ? sky_part_snapshot_reps(PART(part), (int64_t *)pi, (int32_t *)pr, cap, pv, (int32_t *)pc, rcap,
+                                               &n, &r)
+                      : SKY_E_NOMEM;
+    UNCRIT(rep_count_out, pc, 0);
+    UNCRIT(reps_out, pv, 0);
+    UNCRIT(rep_out, pr, 0);
+    UNCRIT(ids_out, pi, 0);
+    if (!ok) return 0;
+    if (rc == SKY_E_CAPACITY) return (jint)-n;
+    if (fail(env, rc)) return 0;
+    return (jint)n;
+}
+
 /* ---- global merge: GlobalSkylineAggregator.processElement (:515-569), on the last arrival ---- */
+/* over the distinct-vector messages (partSnapshotReps output of each local processor):
+ * returns the skyline size, or -(needed) when idsOut is too short */
+JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalMergeReps(JNIEnv *env, jclass cls, jlong ctx, jintArray part_ids,
+                                                                 jobjectArray ids, jobjectArray rep_idx,
+                                                                 jobjectArray reps, jobjectArray rep_counts,
+                                                                 jlongArray ids_out, jintArray origin_out) {
+    (void)cls;
+    const int D = ctx_dims(CTX(ctx));
+    if (D < 1 || !part_ids || !ids || !rep_idx || !reps || !rep_counts || !ids_out || !origin_out) {
+        throw_arg(env, "globalMergeReps: bad context or null array");
+        return 0;
+    }
+    const jsize np = (*env)->GetArrayLength(env, part_ids);
+    if ((*env)->GetArrayLength(env, ids) != np || (*env)->GetArrayLength(env, rep_idx) != np ||
+        (*env)->GetArrayLength(env, reps) != np || (*env)->GetArrayLength(env, rep_counts) != np) {
+        throw_arg(env, "globalMergeReps: arrays of different lengths");
+        return 0;
+    }
+    const size_t m = np ? (size_t)np : 1;
+    const int64_t **pid = calloc(m, sizeof(int64_t *));
+    const int32_t **prx = calloc(m, sizeof(int32_t *));
+    const double **prp = calloc(m, sizeof(double *));
+    const int32_t **prc = calloc(m, sizeof(int32_t *));
+    int64_t *cnt = calloc(m, sizeof(int64_t)), *nrep = calloc(m, sizeof(int64_t));
+    jarray *jo = calloc(4 * m, sizeof(jarray));          /* [4k + 0..3]: ids, repIdx, reps, repCounts of list k */
+    jint g = 0;
+    jsize got = 0;
+    if (!pid || !prx || !prp || !prc || !cnt || !nrep || !jo) {
+        (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/OutOfMemoryError"), "globalMergeReps");
+        goto out;
+    }
+    for (jsize k = 0; k < np; k++) {    /* Get*ArrayElements: several arrays stay pinned/copied at once */
+        jo[4 * k] = (*env)->GetObjectArrayElement(env, ids, k);
+        jo[4 * k + 1] = (*env)->GetObjectArrayElement(env, rep_idx, k);
+        jo[4 * k + 2] = (*env)->GetObjectArrayElement(env, reps, k);
+        jo[4 * k + 3] = (*env)->GetObjectArrayElement(env, rep_counts, k);
+        if (!jo[4 * k] || !jo[4 * k + 3]) { throw_arg(env, "globalMergeReps: null list"); goto release; }
+        cnt[k] = (*env)->GetArrayLength(env, jo[4 * k]);
+        nrep[k] = (*env)->GetArrayLength(env, jo[4 * k + 3]);
+        if (bad_len(env, jo[4 * k + 1], cnt[k], "globalMergeReps: repIdx[k] shorter than ids[k]") ||
+            bad_len(env, jo[4 * k + 2], nrep[k] * D, "globalMergeReps: reps[k] shorter than repCounts[k] * dims"))
+            goto release;
+        pid[k] = (const int64_t *)(*env)->GetLongArrayElements(env, (jlongArray)jo[4 * k], NULL);
+        prx[k] = (const int32_t *)(*env)->GetIntArrayElements(env, (jintArray)jo[4 * k + 1], NULL);
+        prp[k] = (*env)->GetDoubleArrayElements(env, (jdoubleArray)jo[4 * k + 2], NULL);
+        prc[k] = (const int32_t *)(*env)->GetIntArrayElements(env, (jintArray)jo[4 * k + 3], NULL);
+        got = k + 1;
+        if (!pid[k] || !prx[k] || !prp[k] || !prc[k]) goto release;
+    }
+    {
+        const jsize cap = (*env)->GetArrayLength(env, ids_out);
+        if ((*env)->GetArrayLength(env, origin_out) < cap) {
+            throw_arg(env, "globalMergeReps: originOut shorter than idsOut");
+            goto release;
+        }
+        jint *pk = (*env)->GetIntArrayElements(env, part_ids, NULL);
+        jlong *oi = (*env)->GetLongArrayElements(env, ids_out, NULL);
+        jint *oo = (*env)->GetIntArrayElements(env, origin_out, NULL);
+        if (pk && oi && oo) {
+            int64_t n = 0;
+            const int rc = sky_global_merge_reps(CTX(ctx), np, (const int32_t *)pk, pid, prx, cnt, prp, prc, nrep,
+                                                 (int64_t *)oi, (int32_t *)oo, cap, &n);
+            if (rc == SKY_E_CAPACITY) g = (jint)-n;
+            else if (!fail(env, rc)) g = (jint)n;
+        }
+        if (oo) (*env)->ReleaseIntArrayElements(env, origin_out, oo, 0);
+        if (oi) (*env)->ReleaseLongArrayElements(env, ids_out, oi, 0);
+        if (pk) (*env)->ReleaseIntArrayElements(env, part_ids, pk, JNI_ABORT);
+    }
+release:
+    for (jsize k = 0; k < np; k++) {
+        if (k < got) {
+            if (prc[k]) (*env)->ReleaseIntArrayElements(env, (jintArray)jo[4 * k + 3], (jint *)prc[k], JNI_ABORT);
+            if (prp[k]) (*env)->ReleaseDoubleArrayElements(env, (jdoubleArray)jo[4 * k + 2], (jdouble *)prp[k], JNI_ABORT);
+            if (prx[k]) (*env)->ReleaseIntArrayElements(env, (jintArray)jo[4 * k + 1], (jint *)prx[k], JNI_ABORT);
+            if (pid[k]) (*env)->ReleaseLongArrayElements(env, (jlongArray)jo[4 * k], (jlong *)pid[k], JNI_ABORT);
+        }
+        for (int q = 0; q < 4; q++)
+            if (jo[4 * k + q]) (*env)->DeleteLocalRef(env, jo[4 * k + q]);
+    }
+out:
+    free(pid);
+    free(prx);
+    free(prp);
+    free(prc);
+    free(cnt);
+    free(nrep);
+    free(jo);
+    return g;
+}
+
 /* the co-located aggregator's merge over the parts' device-resident states (no snapshot through
  * the JVM heap); returns the skyline size, or -(needed) when idsOut is too short */
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_partsGlobalMerge(JNIEnv *env, jclass cls, jlong ctx, jlongArray parts,

@@ -7,21 +7,27 @@
  *             from a file and decoded on the device: sky_parse_csv
  *             (.map(ServiceTuple::fromString).filter(nonNull), FlinkSkyline.java:102-104)
  *   keyBy     sky_partition_keys (getKey, FlinkSkyline.java:138, :707-712/:774-789/:827-875)
+ *   device    sky_device_count + sky_device_for_subtask (the subtask's GPU, HipSkylineOperators.open)
  *   local     SkylineLocalProcessor: per key, buffer 5000 tuples then sky_part_insert
  *             (processElement1 + processBuffer, :265-316, :417-444); a trigger "q,N" after the
- *             last tuple: per key 0..P-1 flush + sky_part_snapshot (processQuery, :367-404)
- *   global    GlobalSkylineAggregator: sky_global_merge over the P lists + sky_global_stats
- *             (:515-608), then the JSON payload of :631-648 plus "query_latency_ms"
+ *             last tuple: per key 0..P-1 flush + sky_part_sizes + sky_part_snapshot_reps
+ *             (processQuery, :367-404: the LocalSkyline message, distinct vectors)
+ *   global    GlobalSkylineAggregator: sky_global_merge_reps over the P messages +
+ *             sky_global_stats (:515-608), then the JSON payload of :631-648 plus
+ *             "query_latency_ms".  proto 1: the round-3 messages instead (sky_part_snapshot of
+ *             ids + values, sky_global_merge)
  *
- *   batching  full buffers wait in groups of G keys (default 8, as HipSkylineOperators'
- *             FLUSH_GROUP) and go to the device in one sky_parts_insert per round of keys
+ *   batching  full buffers wait until G of them are pending (default 8, as HipSkylineOperators'
+ *             FLUSH_GROUP) and go to the device as drainFull does: rounds in arrival order,
+ *             each round the first waiting buffer of every key, one sky_parts_insert per round
  *   checkpoint after C tuples (optional): every key's buffer flushed and its skyline snapshot
  *             taken (snapshotState), every part and the context closed (a failure), a fresh
  *             context opened and each snapshot re-inserted (initializeState + open); the stream
  *             then continues, and the answer must not change
  *
- * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain] [checkpoint C | -1] [G]
- * stdout: the JSON line, then "ids" and the sorted global skyline ids, then "lsz" / "surv".
+ * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain] [checkpoint C | -1] [G] [proto]
+ * stdout: the JSON line, then "ids" and the sorted global skyline ids, then "lsz" / "surv";
+ * stderr: "calls" -- the sky_parts_insert calls and their part counts (the call sequence).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -87,40 +93,68 @@ typedef struct {
     int64_t *ids;
     double *vals;
     int64_t n;
-    int64_t *fids[64];   /* full buffers waiting for their group (a key fills at most 64 meanwhile) */
-    double *fvals[64];
-    int nfull;
 } keyed_state;
 
-/* every waiting full buffer, one sky_parts_insert per round (each key at most once a round) */
-static void drain_full(keyed_state *ks, int kmax, int D) {
-    for (;;) {
+/* the full buffers waiting for drainFull, in arrival order (HipSkylineOperators.LocalProcessor.full) */
+typedef struct {
+    int key;
+    int64_t *ids;
+    double *vals;
+} full_buf;
+static full_buf *g_full;
+static int g_nfull, g_capfull;
+static long g_calls, g_call_parts;
+
+/* drainFull: while buffers wait, one round = the first waiting buffer of every key in arrival
+ * order (a key appears once per round), one sky_parts_insert per round, the rest keep their order */
+static void drain_full(keyed_state *ks) {
+    while (g_nfull) {
         sky_part *pp[256];
         const int64_t *pi[256];
         const double *pv[256];
         int64_t cnt[256];
-        int np = 0;
-        for (int k = 0; k < kmax && np < 256; k++) {
-            if (!ks[k].nfull) continue;
-            pp[np] = ks[k].part;
-            pi[np] = ks[k].fids[0];
-            pv[np] = ks[k].fvals[0];
-            cnt[np] = BUFFER_SIZE;
-            np++;
+        char seen[256] = {0};
+        int np = 0, nlater = 0;
+        full_buf *later = (full_buf *)malloc((size_t)g_nfull * sizeof(full_buf));
+        full_buf *round = (full_buf *)malloc((size_t)g_nfull * sizeof(full_buf));
+        for (int i = 0; i < g_nfull; i++) {
+            const int k = g_full[i].key;
+            if (k < 256 && !seen[k] && np < 256) {
+                seen[k] = 1;
+                pp[np] = ks[k].part;
+                pi[np] = g_full[i].ids;
+                pv[np] = g_full[i].vals;
+                cnt[np] = BUFFER_SIZE;
+                round[np++] = g_full[i];
+            } else {
+                later[nlater++] = g_full[i];
+            }
         }
-        if (!np) return;
         CHECK(sky_parts_insert(np, pp, pi, pv, cnt));   /* copied before it returns */
-        for (int k = 0, g = 0; k < kmax && g < np; k++) {
-            if (!ks[k].nfull) continue;
-            free(ks[k].fids[0]);
-            free(ks[k].fvals[0]);
-            memmove(ks[k].fids, ks[k].fids + 1, (size_t)(ks[k].nfull - 1) * sizeof(int64_t *));
-            memmove(ks[k].fvals, ks[k].fvals + 1, (size_t)(ks[k].nfull - 1) * sizeof(double *));
-            ks[k].nfull--;
-            g++;
+        g_calls++;
+        g_call_parts += np;
+        for (int g = 0; g < np; g++) {
+            free(round[g].ids);
+            free(round[g].vals);
         }
-        (void)D;
+        memcpy(g_full, later, (size_t)nlater * sizeof(full_buf));
+        g_nfull = nlater;
+        free(later);
+        free(round);
     }
+}
+
+static void push_full(keyed_state *s, int D) {
+    if (g_nfull == g_capfull) {
+        g_capfull = g_capfull ? 2 * g_capfull : 64;
+        g_full = (full_buf *)realloc(g_full, (size_t)g_capfull * sizeof(full_buf));
+    }
+    full_buf *b = &g_full[g_nfull++];
+    b->key = s->key;
+    b->ids = (int64_t *)malloc(BUFFER_SIZE * 8);
+    b->vals = (double *)malloc((size_t)BUFFER_SIZE * D * 8);
+    memcpy(b->ids, s->ids, BUFFER_SIZE * 8);
+    memcpy(b->vals, s->vals, (size_t)BUFFER_SIZE * D * 8);
 }
 
 int main(int argc, char **argv) {
@@ -140,6 +174,7 @@ int main(int argc, char **argv) {
     const double domain = argc > 5 ? atof(argv[5]) : 1000.0;
     const int64_t ckpt_at = argc > 6 ? atoll(argv[6]) : -1;
     const int group = argc > 7 ? atoi(argv[7]) : 8;
+    const int proto = argc > 8 ? atoi(argv[8]) : 0;
     const int P = 2 * par;   /* FlinkSkyline.java:76 */
     FILE *f = fopen(argv[1], "rb");
     if (!f) { perror("open"); return 2; }
@@ -150,7 +185,11 @@ int main(int argc, char **argv) {
     if (fread(text, 1, (size_t)nbytes, f) != (size_t)nbytes) { perror("read"); return 2; }
     fclose(f);
 
-    int dev = 0;
+    int32_t ndev = 0, dev32 = 0;
+    CHECK(sky_device_count(&ndev));
+    if (ndev < 1) { fprintf(stderr, "no HIP device\n"); return 4; }
+    CHECK(sky_device_for_subtask(0, ndev, &dev32));   /* the one subtask of this replay */
+    int dev = dev32;
     sky_ctx *ctx = NULL;
     CHECK(sky_ctx_create(&dev, 1, D, P, algo, domain, &ctx));
     const int64_t rmax = nbytes / 2 + 1;
@@ -174,12 +213,10 @@ int main(int argc, char **argv) {
         CHECK(sky_part_open(ctx, k, &ks[k].part));
     }
     /* processElement1: buffer; a full buffer waits for its group, then processBuffer */
-    int waiting = 0;
     for (int64_t i = 0; i < n; i++) {
         if (i == ckpt_at) {
             /* snapshotState: the waiting and partial buffers flushed, every key's skyline saved */
-            drain_full(ks, kmax, D);
-            waiting = 0;
+            drain_full(ks);
             int64_t *sn = (int64_t *)calloc((size_t)kmax, 8);
             int64_t **sid = (int64_t **)calloc((size_t)kmax, sizeof(int64_t *));
             double **sval = (double **)calloc((size_t)kmax, sizeof(double *));
@@ -219,50 +256,60 @@ int main(int argc, char **argv) {
             if (group <= 1) {
                 CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
             } else {
-                if (s->nfull == 64) drain_full(ks, kmax, D), waiting = 0;
-                s->fids[s->nfull] = (int64_t *)malloc(BUFFER_SIZE * 8);
-                s->fvals[s->nfull] = (double *)malloc((size_t)BUFFER_SIZE * D * 8);
-                memcpy(s->fids[s->nfull], s->ids, BUFFER_SIZE * 8);
-                memcpy(s->fvals[s->nfull], s->vals, (size_t)BUFFER_SIZE * D * 8);
-                s->nfull++;
-                if (++waiting >= group) {
-                    drain_full(ks, kmax, D);
-                    waiting = 0;
-                }
+                push_full(s, D);
+                if (g_nfull >= group) drain_full(ks);
             }
             s->n = 0;
         }
     }
-    drain_full(ks, kmax, D);
     /* trigger "1,N" after the last tuple, broadcast to keys 0..P-1 (:145-157) */
     const int64_t dispatch = now_ms();
     int32_t *part_ids = (int32_t *)malloc((size_t)P * 4);
     int64_t **lid = (int64_t **)malloc((size_t)P * sizeof(int64_t *));
     double **lval = (double **)malloc((size_t)P * sizeof(double *));
-    int64_t *lcnt = (int64_t *)malloc((size_t)P * 8);
+    int32_t **lrep = (int32_t **)malloc((size_t)P * sizeof(int32_t *));
+    int32_t **lrc = (int32_t **)malloc((size_t)P * sizeof(int32_t *));
+    int64_t *lcnt = (int64_t *)malloc((size_t)P * 8), *lnr = (int64_t *)malloc((size_t)P * 8);
     int64_t total = 0;
-    for (int k = 0; k < P; k++) {   /* processQuery: flush, then the local skyline snapshot */
+    for (int k = 0; k < P; k++) {   /* processQuery: flush (drainFull first), then the local skyline message */
         keyed_state *s = &ks[k];
+        drain_full(ks);
         if (s->n) {
             CHECK(sky_part_insert(s->part, s->ids, s->vals, s->n));
             s->n = 0;
         }
-        int64_t m = 0;
-        int rc = sky_part_snapshot(s->part, NULL, NULL, 0, &m);
-        if (rc != SKY_OK && rc != SKY_E_CAPACITY) die("sky_part_snapshot (size)", rc);
-        lid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
-        lval[k] = (double *)malloc((size_t)(m > 0 ? m : 1) * D * 8);
-        CHECK(sky_part_snapshot(s->part, lid[k], lval[k], m, &m));
+        int64_t m = 0, r = 0;
+        if (proto == 0) {
+            CHECK(sky_part_sizes(s->part, &m, &r));
+            lid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+            lrep[k] = (int32_t *)malloc((size_t)(m > 0 ? m : 1) * 4);
+            lval[k] = (double *)malloc((size_t)(r > 0 ? r : 1) * D * 8);
+            lrc[k] = (int32_t *)malloc((size_t)(r > 0 ? r : 1) * 4);
+            CHECK(sky_part_snapshot_reps(s->part, lid[k], lrep[k], m, lval[k], lrc[k], r, &m, &r));
+        } else {
+            CHECK(sky_part_size(s->part, &m));
+            lid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
+            lval[k] = (double *)malloc((size_t)(m > 0 ? m : 1) * D * 8);
+            lrep[k] = lrc[k] = NULL;
+            CHECK(sky_part_snapshot(s->part, lid[k], lval[k], m, &m));
+        }
         part_ids[k] = k;
         lcnt[k] = m;
+        lnr[k] = r;
         total += m;
     }
+    fprintf(stderr, "calls %ld parts %ld\n", g_calls, g_call_parts);
     /* GlobalSkylineAggregator: merge on the last arrival, optimality integers */
     int64_t *gids = (int64_t *)malloc((size_t)(total > 0 ? total : 1) * 8);
     int32_t *gorg = (int32_t *)malloc((size_t)(total > 0 ? total : 1) * 4);
     int64_t g = 0;
-    CHECK(sky_global_merge(ctx, P, part_ids, (const int64_t *const *)lid, (const double *const *)lval, lcnt, gids,
-                           gorg, total, &g));
+    if (proto == 0)
+        CHECK(sky_global_merge_reps(ctx, P, part_ids, (const int64_t *const *)lid, (const int32_t *const *)lrep, lcnt,
+                                    (const double *const *)lval, (const int32_t *const *)lrc, lnr, gids, gorg, total,
+                                    &g));
+    else
+        CHECK(sky_global_merge(ctx, P, part_ids, (const int64_t *const *)lid, (const double *const *)lval, lcnt, gids,
+                               gorg, total, &g));
     int64_t *lsz = (int64_t *)malloc((size_t)P * 8), *surv = (int64_t *)malloc((size_t)P * 8);
     int32_t K = 0;
     CHECK(sky_global_stats(ctx, lsz, surv, &K));
@@ -293,9 +340,9 @@ int main(int argc, char **argv) {
         free(ks[k].ids);
         free(ks[k].vals);
     }
-    for (int k = 0; k < P; k++) { free(lid[k]); free(lval[k]); }
+    for (int k = 0; k < P; k++) { free(lid[k]); free(lval[k]); free(lrep[k]); free(lrc[k]); }
     CHECK(sky_ctx_destroy(ctx));
-    free(ks); free(lid); free(lval); free(lcnt); free(part_ids); free(gids); free(gorg); free(lsz); free(surv);
+    free(ks); free(lid); free(lval); free(lrep); free(lrc); free(lcnt); free(lnr); free(part_ids); free(g_full); free(gids); free(gorg); free(lsz); free(surv);
     free(keys); free(ids); free(vals); free(text);
     return 0;
 }

@@ -59,3 +59,62 @@ def test_c_caller_replays_operator_sequence(path, tmp_path):
                 opt = sum(surv[i] / lsz[i] for i in range(P) if lsz[i] > 0) / P
                 assert lines[0].split('"optimality": ')[1].split(",")[0] == java_format_4f(opt)
                 assert "query_latency_ms" in js
+
+
+def _drain_model(keys, P, group, buf=5000):
+    """HipSkylineOperators.drainFull's call sequence: (calls, parts over all calls)."""
+    fill = {}
+    full = []
+    calls = parts = 0
+
+    def drain():
+        nonlocal full, calls, parts
+        while full:
+            seen, rnd, later = set(), [], []
+            for k in full:
+                (later if k in seen else rnd).append(k)
+                seen.add(k)
+            calls += 1
+            parts += len(rnd)
+            full = later
+    for k in keys.tolist():
+        fill[k] = fill.get(k, 0) + 1
+        if fill[k] == buf:
+            fill[k] = 0
+            full.append(k)
+            if len(full) >= group:
+                drain()
+    drain()
+    return calls, parts
+
+
+@pytest.mark.parametrize("dist,D,algo,proto", [(2, 8, "angle", 0), (2, 8, "angle", 1), (3, 4, "angle", 0),
+                                               (1, 4, "grid", 0), (0, 2, "dim", 0)])
+def test_c_caller_java_sequence_large(dist, D, algo, proto, tmp_path, oracle):
+    """The operators' exact call sequence at a size where buffers fill: drainFull rounds of
+    sky_parts_insert (arrival order, one buffer per key per round, every 8 full buffers), then per
+    key flush + sky_part_sizes + sky_part_snapshot_reps and sky_global_merge_reps (proto 0, the
+    Java operators' LocalSkyline messages) or the round-3 ids + values messages (proto 1).  The
+    answer equals the oracle's two-level skyline, and the calls equal the drainFull model's."""
+    n, P = 240_000, 8
+    vals = oracle.synth(dist, D, n, seed=300 + D)
+    ids = np.arange(n, dtype=np.int64) + 7
+    csv = tmp_path / "stream.csv"
+    with open(csv, "w") as f:
+        for i, row in zip(ids, vals):
+            f.write(f"{int(i)}," + ",".join(str(int(x)) for x in row) + "\n")
+    r = subprocess.run([BIN, str(csv), str(D), str(P // 2), str(ALGO[algo]), "1000.0", "-1", "8", str(proto)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().split("\n")
+    got_ids = np.array([int(x) for x in lines[1].split()[1:]], np.int64)
+    lsz = np.array([int(x) for x in lines[2].split()[1:]], np.int64)
+    surv = np.array([int(x) for x in lines[3].split()[1:]], np.int64)
+    e_or, _, e_ls, e_sv = oracle.query_sfs(algo, vals, P)
+    np.testing.assert_array_equal(got_ids, np.sort(ids[e_or]))
+    np.testing.assert_array_equal(lsz, e_ls)
+    np.testing.assert_array_equal(surv, e_sv)
+    calls = [ln for ln in r.stderr.split("\n") if ln.startswith("calls ")][-1].split()
+    keys = oracle.keys(algo, vals, P)
+    assert (int(calls[1]), int(calls[3])) == _drain_model(keys, P, 8)
+    assert int(calls[1]) > 0
