@@ -132,7 +132,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     SKY_TRY(p.mbr_min.ensure((xt + yt) * NW * 4));
     SKY_TRY(p.mbr_max.ensure((xt + yt) * NW * 4));
     SKY_TRY(p.mbr_pr.ensure((xt + yt) * 4));
-    SKY_TRY(p.mbr_sub.ensure((xt + yt) * 4 * NW * 4));
+    SKY_TRY(p.mbr_sub.ensure((xt + yt) * kMbrSubMax * NW * 4));
     SKY_TRY(p.mbr_gmin.ensure(mbr_groups(n_union) * NW * 4));
     SKY_TRY(p.mbr_gpr.ensure(mbr_groups(n_union) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)n_own * 4));
@@ -171,7 +171,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
         s.tmin = p.mbr_min.as<uint32_t>() + t0 * NW;
         s.tmax = p.mbr_max.as<uint32_t>() + t0 * NW;
         s.tprange = p.mbr_pr.as<uint32_t>() + t0;
-        s.tsub = p.mbr_sub.as<uint32_t>() + t0 * 4 * NW;
+        s.tsub = p.mbr_sub.as<uint32_t>() + t0 * kMbrSubMax * NW;
         s.pairs = p.mbr_pairs.as<unsigned long long>();
     };
     const size_t rb = (size_t)NW * 4;

@@ -672,7 +672,7 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_min.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
-    SKY_TRY(p.mbr_sub.ensure(ntiles * 4 * NW * 4));
+    SKY_TRY(p.mbr_sub.ensure(ntiles * kMbrSubMax * NW * 4));
     SKY_TRY(p.mbr_gmin.ensure(mbr_groups(mr) * NW * 4));
     SKY_TRY(p.mbr_gpr.ensure(mbr_groups(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));

@@ -236,6 +236,11 @@ __global__ __launch_bounds__(kThreads) void k_mbr_code(const uint32_t *__restric
 
 // ---- tiles: rows in sorted order, bounding boxes, partition ranges ---------------------
 constexpr int kMbrT = 64;   // rows per tile (= one wave)
+// sub-boxes per tile whose min corners the pair pass tests each y against before comparing rows:
+// 8 boxes of 8 rows for packed u16 rows (the corners of a tile are 32 words: one pair of scalar
+// loads), 4 of 16 rows for f32 / f64 rows (32 / 64 words).  tsub holds kMbrSubMax corners per tile.
+template <class R>
+constexpr int mbr_subs() { return R::NW <= 4 ? 8 : 4; }
 
 template <class R>
 __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restrict__ rows,
@@ -270,8 +275,9 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
         pl = 0xffffffffu;
         ph = 0u;
     }
-    // offsets 1..8 first: the 16-row sub-boxes' min corners (k_mbr_pairs tests a y against
-    // them before comparing rows), then 16, 32: the whole tile
+    // offsets below the sub-box size first: the sub-boxes' min corners (k_mbr_pairs tests a y
+    // against them before comparing rows), then the rest: the whole tile
+    constexpr int S = mbr_subs<R>(), RS = kMbrT / S;
 #pragma unroll
     for (int o = 1; o <= 32; o <<= 1) {
         uint32_t a[NW], b[NW];
@@ -284,9 +290,9 @@ __global__ __launch_bounds__(kThreads) void k_mbr_tiles(const uint32_t *__restri
         R::cmax(mx, b);
         pl = min(pl, (uint32_t)__shfl_xor((int)pl, o, 64));
         ph = max(ph, (uint32_t)__shfl_xor((int)ph, o, 64));
-        if (o == 8 && (threadIdx.x & 15) == 0) {
+        if (o == RS / 2 && (threadIdx.x & (RS - 1)) == 0) {
 #pragma unroll
-            for (int w = 0; w < NW; w++) tsub[((size_t)tile * 4 + ((threadIdx.x & 63) >> 4)) * NW + w] = mn[w];
+            for (int w = 0; w < NW; w++) tsub[((size_t)tile * S + ((threadIdx.x & 63) / RS)) * NW + w] = mn[w];
         }
     }
     if ((threadIdx.x & 63) == 0) {
@@ -508,7 +514,9 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     auto load_tile = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px, uint32_t (&xs)[NW]) {
         const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);      // rows past mr: masked by xvalid
         const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
-        const uint4 *sb = reinterpret_cast<const uint4 *>(tsub + ((size_t)xt * 4 + (lane >> 4)) * NW);
+        // the 16-row box of this lane: one stored corner, or the min of two 8-row ones
+        constexpr int S = mbr_subs<R>(), H = S / 4;
+        const uint4 *sb = reinterpret_cast<const uint4 *>(tsub + ((size_t)xt * S + (lane >> 4) * H) * NW);
 #pragma unroll
         for (int q = 0; q < NW / 4; q++) {
             const uint4 v = src[q];
@@ -521,6 +529,18 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             xs[4 * q + 1] = c.y;
             xs[4 * q + 2] = c.z;
             xs[4 * q + 3] = c.w;
+        }
+        if constexpr (H == 2) {
+            uint32_t x2[NW];
+#pragma unroll
+            for (int q = 0; q < NW / 4; q++) {
+                const uint4 c = sb[NW / 4 + q];
+                x2[4 * q] = c.x;
+                x2[4 * q + 1] = c.y;
+                x2[4 * q + 2] = c.z;
+                x2[4 * q + 3] = c.w;
+            }
+            R::cmin(xs, x2);
         }
         px = tpart[xi];
     };
@@ -735,6 +755,240 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     }
 }
 
+// ---- the pair pass, round 4 ------------------------------------------------------------
+// Per y tile (one wave, lane = y), for every x tile whose min corner is <= the y tile's max
+// corner (found 64 tiles at a time per reachable group, as above):
+//  * the tile's S sub-box min corners are wave-uniform loads (SGPRs), each tested against
+//    every live y at once: S ballots give the (y, sub-box) entries -- no per-tile listing pass
+//    in LDS and no readlane of corners;
+//  * the tile's rows (loaded one tile ahead, two register sets used alternately) are staged in
+//    LDS, the entries packed into an LDS list, and compared S entries per wave instruction
+//    (RS = 64 / S lanes per entry: lane r of entry g compares row r of its sub-box with its y);
+//  * a hit is one LDS atomic OR into the y's fate word (no per-group scalar loop); the fates are
+//    read back once per tile to retire the y's a rep of their own partition dominates.
+// With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
+template <class R, bool FULL, bool GM>
+__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *__restrict__ trows,
+                                                         const uint32_t *__restrict__ tpart,
+                                                         const uint32_t *__restrict__ tmin,
+                                                         const uint32_t *__restrict__ tprange,
+                                                         const uint32_t *__restrict__ tsub,
+                                                         const uint32_t *__restrict__ gmin,
+                                                         const uint32_t *__restrict__ gprange, uint32_t mr,
+                                                         uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
+                                                         uint32_t *__restrict__ domf,
+                                                         unsigned long long *__restrict__ pairs,
+                                                         uint32_t *__restrict__ lpt,
+                                                         unsigned long long *__restrict__ trace) {
+    constexpr int NW = R::NW;
+    constexpr int S = mbr_subs<R>(), RS = kMbrT / S;
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint32_t split, yt, witem;
+    if (lpt) {
+        uint32_t item = 0;
+        if ((threadIdx.x & 63) == 0) item = atomicAdd(&lpt[32], 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl((int)item, 0, 64));
+        if (item >= ys.ntiles * nsplit) return;
+        split = item % nsplit;
+        witem = item;
+        yt = __builtin_amdgcn_readfirstlane(lpt[kMbrLptHead + ys.ntiles + item / nsplit]);
+    } else {
+        const uint32_t per_xcd = gridDim.x / 8u;
+        const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+        split = blk % nsplit;
+        witem = blk;
+        yt = __builtin_amdgcn_readfirstlane(blk / nsplit);
+        if (yt >= ys.ntiles) return;
+    }
+    const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
+    const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t j = yt * kMbrT + lane;
+    const bool valid = j < ys.mr;
+    uint32_t y[NW], ymax[NW];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(ys.trows + (size_t)min(j, ys.mr - 1u) * NW);
+#pragma unroll
+        for (int q = 0; q < NW / 4; q++) {
+            const uint4 v = src[q];
+            y[4 * q] = v.x;
+            y[4 * q + 1] = v.y;
+            y[4 * q + 2] = v.z;
+            y[4 * q + 3] = v.w;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
+    const uint32_t yr = ys.tprange[yt];
+    const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
+    const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
+    __shared__ uint4 s_y[64 * NW / 4];            // this wave's y rows (compare operands)
+    __shared__ uint32_t s_py[64], s_hit[64];       // y partitions; y fate words (bit 1 any, bit 0 same)
+    __shared__ uint4 s_x[64 * NW / 4];            // the x tile under test
+    __shared__ uint32_t s_px[64];
+    __shared__ uint16_t s_e[64 * S];              // (y << 3 | sub-box) entries
+    uint32_t *sy = reinterpret_cast<uint32_t *>(s_y), *sx = reinterpret_cast<uint32_t *>(s_x);
+#pragma unroll
+    for (int w = 0; w < NW; w++) sy[lane * NW + w] = y[w];
+    s_py[lane] = py;
+    s_hit[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t f = 0;
+    uint64_t live = __ballot(valid);
+    uint64_t npairs = 0, ntested = 0;
+    uint32_t ngrp = 0, nbox = 0;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
+
+    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx)
+    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
+        const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);
+        const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
+#pragma unroll
+        for (int q = 0; q < NW / 4; q++) {
+            const uint4 v = src[q];
+            xv[4 * q] = v.x;
+            xv[4 * q + 1] = v.y;
+            xv[4 * q + 2] = v.z;
+            xv[4 * q + 3] = v.w;
+        }
+        px = tpart[xi];
+    };
+    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px) {
+        const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
+        // the S corners: wave-uniform, all loaded before the first test (scalar loads in flight
+        // together); the tests are unconditional (a branch per box would wait per load) and a
+        // box past the last row is masked afterwards
+        const uint32_t *cs = tsub + (size_t)xt * S * NW;
+        uint32_t c[S][NW];
+#pragma unroll
+        for (int b = 0; b < S; b++)
+#pragma unroll
+            for (int w = 0; w < NW; w++) c[b][w] = cs[b * NW + w];
+        uint64_t ms[S];
+        uint32_t E = 0;
+#pragma unroll
+        for (int b = 0; b < S; b++) {
+            const uint64_t bal = __ballot(R::le(c[b], y));
+            ms[b] = bal & live & ((uint32_t)(b * RS) < nx ? ~0ull : 0ull);
+            E += (uint32_t)__popcll(ms[b]);
+        }
+        npairs += (uint64_t)RS * E;
+        if ((dbg & 1) || !E) return;
+        ntested++;
+#pragma unroll
+        for (int w = 0; w < NW; w++) sx[lane * NW + w] = xv[w];
+        s_px[lane] = px;
+        {
+            uint32_t eb = 0;
+#pragma unroll
+            for (int b = 0; b < S; b++) {
+                if ((ms[b] >> lane) & 1ull) s_e[eb + (uint32_t)__popcll(ms[b] & lt)] = (uint16_t)((lane << 3) | b);
+                eb += (uint32_t)__popcll(ms[b]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        bool any = false;
+        for (uint32_t e0 = 0; e0 < E; e0 += S) {
+            const bool ev = e0 + eg < E;
+            const uint32_t ent = s_e[min(e0 + eg, E - 1u)];
+            const uint32_t yb = ent >> 3, xr = (ent & 7u) * RS + er;
+            uint32_t xw[NW], yw[NW];
+#pragma unroll
+            for (int q = 0; q < NW / 4; q++) {
+                const uint4 a = s_x[xr * (NW / 4) + q], b = s_y[yb * (NW / 4) + q];
+                xw[4 * q] = a.x; xw[4 * q + 1] = a.y; xw[4 * q + 2] = a.z; xw[4 * q + 3] = a.w;
+                yw[4 * q] = b.x; yw[4 * q + 1] = b.y; yw[4 * q + 2] = b.z; yw[4 * q + 3] = b.w;
+            }
+            // bitwise, not short-circuit: no exec-masked branches per test
+            bool dom = ev & (xr < nx) & R::le(xw, yw);
+            if constexpr (FULL) dom = dom & !R::le(yw, xw);
+            else dom = dom & !(xt == yt && xr == yb);
+            if (dom) {
+                atomicOr(&s_hit[yb], s_px[xr] == s_py[yb] ? 3u : 2u);
+                any = true;
+            }
+        }
+        if (__ballot(any)) {
+            __builtin_amdgcn_wave_barrier();
+            f |= s_hit[lane];
+            live &= __ballot(!(f & 1u));
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+
+    for (uint32_t s0 = gs_lo; s0 < gs_hi && live; s0 += 64) {
+        uint64_t gm;
+        {
+            const uint32_t q = min(s0 + lane, ngroups - 1u);
+            uint32_t gc[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
+            const uint32_t gr = gprange[q];
+            const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
+            bool cand = s0 + lane < gs_hi && R::le(gc, ymax);
+            if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
+            gm = __ballot(cand);
+        }
+        ngrp += (uint32_t)__popcll(gm);
+        while (gm && live) {
+            const uint32_t g = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
+            gm &= gm - 1;
+            uint64_t tm;
+            {
+                const uint32_t t = min(g + lane, ntiles - 1u);
+                uint32_t tg[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
+                const uint32_t tr = tprange[t];
+                const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
+                bool cand = g + lane < ntiles && R::le(tg, ymax);
+                if (cand && !need_any) cand = (tr & 0xffffu) <= yph && (tr >> 16) >= ypl;
+                tm = __ballot(cand);
+            }
+            if (dbg & 2) tm = 0;
+            nbox += (uint32_t)__popcll(tm);
+            if (!tm) continue;
+            // the tiles of the group, the next one's rows in flight while one is tested (two
+            // register sets used alternately: no copy at the back-edge that would wait for them)
+            uint32_t xa = g + (uint32_t)__builtin_ctzll(tm), xb;
+            tm &= tm - 1;
+            uint32_t va[NW], vb[NW], pa, pb;
+            load_x(xa, va, pa);
+            for (;;) {
+                const bool hb = tm != 0ull;
+                xb = hb ? g + (uint32_t)__builtin_ctzll(tm) : xa;
+                tm &= tm - 1;
+                load_x(xb, vb, pb);
+                test_tile(xa, va, pa);
+                if (!hb || !live) break;
+                const bool ha = tm != 0ull;
+                xa = ha ? g + (uint32_t)__builtin_ctzll(tm) : xb;
+                tm &= tm - 1;
+                load_x(xa, va, pa);
+                test_tile(xb, vb, pb);
+                if (!ha || !live) break;
+            }
+        }
+    }
+    if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
+    if (lane == 0 && pairs) {
+        atomicAdd(pairs, (unsigned long long)npairs);
+        atomicAdd(pairs + 1, (unsigned long long)ntested);
+        if (dbg & 4) {
+            atomicAdd(pairs + 2, (unsigned long long)ngrp);
+            atomicAdd(pairs + 3, (unsigned long long)nbox);
+            atomicAdd(pairs + 4, (unsigned long long)ntested);
+        }
+    }
+    if (trace && lane == 0) {
+        trace[4 * (size_t)witem] = t_start;
+        trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[4 * (size_t)witem + 2] = ntested;
+        trace[4 * (size_t)witem + 3] = npairs;
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_mbr_finish(const uint32_t *__restrict__ perm,
                                                          const uint32_t *__restrict__ domf, uint32_t mr, int gmerge,
                                                          uint8_t *__restrict__ alive_l, uint8_t *__restrict__ alive_g) {
@@ -753,6 +1007,11 @@ int mbr_row_words(int D, int fmt) {
     return 2 * padded_dims<double>(D);
 }
 
+// SKY_MBR_V1=1: the round-3 pair pass (16-row boxes, LDS tile list; measurement builds, A/B)
+static bool mbr_v1() {
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_V1");
+    return e && e[0] == '1';
+}
 // SKY_MBR_ORDER=morton: the Morton order of round 2 (A/B knob, read per build)
 static bool mbr_hilbert() {
     const char *e = SKY_MEASURE_ENV("SKY_MBR_ORDER");
@@ -813,7 +1072,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
     if (a.lpt) mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    k_mbr_pairs<R, F, G, true>                              \
+    (mbr_v1() ? k_mbr_pairs<R, F, G, true> : k_mbr_pairs2<R, F, G>)                                         \
         <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
                                                   a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
     if (a.full) {
@@ -862,7 +1121,7 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     const unsigned gp = ((nyt + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64) + 7) / 8 * 8;
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
     if (y.lpt) mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
-    k_mbr_pairs<R, true, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+    (mbr_v1() ? k_mbr_pairs<R, true, true, true> : k_mbr_pairs2<R, true, true>)<<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
                                                         y.domf, x.pairs, y.lpt, nullptr);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,

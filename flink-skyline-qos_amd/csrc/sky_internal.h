@@ -275,6 +275,7 @@ void launch_gather_u32(const uint32_t *src, const uint32_t *at, uint32_t n, uint
 
 // ---- k_mbr.hip (both skyline levels of a large rep set, bounding-box pruned all-pairs) ----
 constexpr int kMbrLptHead = 64;   // head words of MbrArgs::lpt
+constexpr int kMbrSubMax = 8;     // sub-box corners per 64-row tile (k_mbr.hip mbr_subs)
 inline size_t mbr_lpt_words(size_t ytiles) { return kMbrLptHead + 2 * ytiles; }
 struct MbrArgs {
     int D = 0;
@@ -295,7 +296,7 @@ struct MbrArgs {
     uint32_t *tpart = nullptr;    // [mr]
     uint32_t *tmin = nullptr, *tmax = nullptr;       // [NW][ntiles]
     uint32_t *tprange = nullptr;  // [ntiles]
-    uint32_t *tsub = nullptr;     // [ntiles][4][NW]: min corners of the 16-row sub-boxes
+    uint32_t *tsub = nullptr;     // [ntiles][S][NW] (room for kMbrSubMax): min corners of the sub-boxes
     uint32_t *gmin = nullptr;     // [NW][ngroups]: min corners of the groups of 64 tiles
     uint32_t *gprange = nullptr;  // [ngroups]: their partition ranges
     uint32_t *domf = nullptr;     // [mr], zeroed by the caller
