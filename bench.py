@@ -439,6 +439,7 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     eng.profile(False)
     roof = filter_roofline(eng, D)
     resident, _ = st.size()
+    vectors = st.vectors()
     st.close()
     eng.close()
     rate = n / total
@@ -450,6 +451,9 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
             "p50_query_latency_ms": statistics.median(lat), "p90_query_latency_ms": sorted(lat)[int(0.9 * len(lat))],
             "max_query_latency_ms": max(lat), "latencies_ms": [round(x, 3) for x in lat],
             "skyline_size_last": sizes[-1], "resident_tuples_last": resident,
+            "resident_vectors_last": vectors,
+            "resident_note": ("landmark: the local-skyline tuples kept (ids, arrival order) and the distinct "
+                              "vectors the next query runs over" if window == 0 else "the window's tuples"),
             "roofline": roof}
 
 
@@ -693,6 +697,8 @@ def main():
     ap.add_argument("--dist", default=None, help="override the config's distribution (e.g. std_anti)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
+    ap.add_argument("--dom-n-large", type=int, default=10_000_000,
+                    help="tuples of the second dominance-bound companion run (0: skip)")
     ap.add_argument("--no-dominance", action="store_true")
     ap.add_argument("--no-csv", action="store_true", help="skip the CSV-ingest companion measurement")
     ap.add_argument("--no-stream", action="store_true", help="skip the C5 continuous-query companion measurement")
@@ -817,6 +823,8 @@ def main():
                                               "sliding_10M": stream_run(dev_index, 1234 + 6, window=10_000_000)}
             if not args.no_dominance:
                 extra["dominance_roofline"] = dominance_run(dev, D, P, args.dom_n, seed, 2, 1)
+                if args.dom_n_large:
+                    extra["dominance_roofline_large"] = dominance_run(dev, D, P, args.dom_n_large, seed, 2, 1)
         line = {
             "metric": METRIC,
             "value": value,

@@ -14,21 +14,6 @@ void set_error(const std::string &m) { g_err = m; }
 
 using namespace sky;
 
-static void store_stats(sky_ctx *c, const Pipe &p) {
-    c->K_last = p.K;
-    c->lsz.assign(p.h_lsz.begin(), p.h_lsz.end());
-    c->surv.assign(p.h_surv.begin(), p.h_surv.end());
-    c->counters[0] = p.n;
-    c->counters[1] = p.m;
-    c->counters[2] = p.mr;
-    c->counters[3] = p.mg;
-    c->counters[4] = p.nout;
-    c->counters[5] = p.sfs_rounds;
-    c->counters[6] = p.sfs_pairs_upper;
-    c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0) | (p.u16 ? 4 : 0) | (p.last_planned ? 8 : 0) |
-                     (p.last_plan_miss ? 16 : 0) | (p.mbr_tiles << 8);
-    c->dom_w = p.dom_w;
-}
 
 extern "C" {
 
@@ -720,212 +705,6 @@ int sky_format_csv_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values,
     launch_csv_fmt_write(d_ids, d_values, n, c->D, c->csv_pos.as<uint32_t>(), reinterpret_cast<uint8_t *>(d_text),
                          c->st);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->st));
-    return SKY_OK;
-    GUARD_END
-}
-
-// ---- continuous queries (sky_stream) ----------------------------------------
-// Landmark window: the resident tuples are the last query's local-skyline tuples followed by the
-// tuples appended since, always in arrival order; a query runs the whole pipeline over them and then
-// keeps only its local-skyline tuples (pipe_output select_local), which is exact because
-// SKY_k(L_k ∪ new) = SKY_k(every tuple of key k) (FlinkSkyline.java:417-444 applied batch-wise).
-// Sliding window: the last `window` tuples stay resident; each query runs over all of them.
-static int stream_reserve(sky_stream *s, int64_t extra) {
-    sky_ctx *c = s->ctx;
-    const int D = c->D;
-    if (s->off + s->n + extra <= s->cap) return SKY_OK;
-    // compact the live range to the front of the other buffer, growing both if needed
-    int64_t want = s->n + extra;
-    int64_t cap = std::max<int64_t>(s->cap, 1024);
-    while (cap < want) cap *= 2;
-    if (s->window > 0) cap = std::max<int64_t>(cap, std::min<int64_t>(2 * s->window + extra, (int64_t)0x7ffffffe));
-    ARG_CHECK(cap < (int64_t)0x7fffffffLL, "stream state too large");
-    const int o = 1 - s->cur;
-    if (cap > s->cap) {
-        // both buffers must hold `cap`: grow the other, move, then grow the first on the next swap
-        SKY_TRY(s->ids[o].ensure((size_t)cap * 8));
-        SKY_TRY(s->rows[o].ensure((size_t)cap * D * 8));
-    }
-    if (s->n) {
-        HIP_TRY(hipMemcpyAsync(s->ids[o].p, s->ids[s->cur].as<int64_t>() + s->off, (size_t)s->n * 8,
-                               hipMemcpyDeviceToDevice, c->st));
-        HIP_TRY(hipMemcpyAsync(s->rows[o].p, s->rows[s->cur].as<double>() + s->off * D, (size_t)s->n * D * 8,
-                               hipMemcpyDeviceToDevice, c->st));
-    }
-    HIP_TRY(hipStreamSynchronize(c->st));
-    if (cap > s->cap) {
-        SKY_TRY(s->ids[s->cur].ensure((size_t)cap * 8));
-        SKY_TRY(s->rows[s->cur].ensure((size_t)cap * D * 8));
-        s->cap = cap;
-    }
-    s->cur = o;
-    s->off = 0;
-    return SKY_OK;
-}
-
-static int stream_append(sky_stream *s, const int64_t *ids, const double *values, int64_t n, hipMemcpyKind kind) {
-    GUARD_BEGIN
-    ARG_CHECK(s && (n == 0 || (ids && values)), "null argument");
-    ARG_CHECK(n >= 0, "negative n");
-    if (n == 0) return SKY_OK;
-    sky_ctx *c = s->ctx;
-    SKY_TRY(bind(c));
-    const int D = c->D;
-    const int64_t n_all = n;
-    bool drop_resident = false;
-    if (s->window > 0 && n >= s->window) {   // only the newest `window` tuples of this batch can stay
-        ids += n - s->window;
-        values += (n - s->window) * D;
-        n = s->window;
-        drop_resident = true;
-    }
-    SKY_TRY(stream_reserve(s, n));
-    const int64_t at = s->off + s->n;
-    HIP_TRY(hipMemcpyAsync(s->ids[s->cur].as<int64_t>() + at, ids, (size_t)n * 8, kind, c->st));
-    HIP_TRY(hipMemcpyAsync(s->rows[s->cur].as<double>() + at * D, values, (size_t)n * D * 8, kind, c->st));
-    // admission: a NaN row never becomes resident (the state stays queryable); the
-    // batch is rejected whole, as sky_part_insert rejects it
-    SKY_TRY(s->nanflag.ensure(64));
-    if (!s->nan_host) HIP_TRY(hipHostMalloc(&s->nan_host, 64, hipHostMallocDefault));
-    HIP_TRY(hipMemsetAsync(s->nanflag.p, 0, 4, c->st));
-    launch_nan_any(s->rows[s->cur].as<double>() + at * D, (size_t)n * D, s->nanflag.as<uint32_t>(), c->st);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(s->nan_host, s->nanflag.p, 4, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipStreamSynchronize(c->st));   // also: the caller's host buffer is free
-    if (*(volatile uint32_t *)s->nan_host) {
-        set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; batch rejected");
-        return SKY_E_NAN;
-    }
-    if (drop_resident) {
-        s->off = at;
-        s->n = 0;
-    }
-    s->n += n;
-    s->appended += n_all;
-    if (s->window > 0 && s->n > s->window) {   // expire the oldest tuples
-        s->off += s->n - s->window;
-        s->n = s->window;
-    }
-    return SKY_OK;
-    GUARD_END
-}
-
-static int stream_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out) {
-    sky_ctx *c = s->ctx;
-    const int D = c->D;
-    PipeIn in;
-    in.vals = s->rows[s->cur].as<double>() + s->off * D;
-    in.ids = s->ids[s->cur].as<int64_t>() + s->off;
-    in.n = (uint32_t)s->n;
-    in.global = true;
-    in.K = c->Kq();
-    in.out_ids = d_ids_out;
-    in.out_org = d_origin_out;
-    in.out_cap = cap;
-    c->shard_valid = false;
-    if (c->profile >= 2) {
-        if (!c->pt.ok) c->pt.init();
-        c->pt.reset();
-    }
-    SKY_TRY(pipe_run(*c, c->main, in, c->profile >= 2 ? &c->pt : nullptr));
-    store_stats(c, c->main);
-    SKY_TRY(pipe_output(*c, c->main, in, false, d_ids_out, d_origin_out, nullptr, cap, n_out, nullptr));
-    if (s->window == 0 && s->n) {   // landmark: keep only the local-skyline tuples, in arrival order
-        const int o = 1 - s->cur;
-        int64_t nl = 0;
-        SKY_TRY(s->ids[o].ensure((size_t)std::max<int64_t>(s->cap, 1) * 8));
-        SKY_TRY(s->rows[o].ensure((size_t)std::max<int64_t>(s->cap, 1) * D * 8));
-        SKY_TRY(pipe_output(*c, c->main, in, true, s->ids[o].as<int64_t>(), nullptr, s->rows[o].as<double>(),
-                            s->cap, &nl, nullptr));
-        s->cur = o;
-        s->off = 0;
-        s->n = nl;
-    }
-    HIP_TRY(hipGetLastError());
-    finish_profile(c);
-    return SKY_OK;
-}
-
-int sky_stream_create(sky_ctx *c, int64_t window, sky_stream **out) {
-    GUARD_BEGIN
-    ARG_CHECK(c && out, "null argument");
-    ARG_CHECK(window >= 0 && window < (int64_t)0x3fffffffLL, "window out of range");
-    sky_stream *s = new sky_stream();
-    s->ctx = c;
-    s->window = window;
-    *out = s;
-    return SKY_OK;
-    GUARD_END
-}
-int sky_stream_destroy(sky_stream *s) {
-    if (!s) return SKY_OK;
-    hipSetDevice(s->ctx->dev);
-    hipStreamSynchronize(s->ctx->st);
-    if (s->nan_host) hipHostFree(s->nan_host);
-    delete s;
-    return SKY_OK;
-}
-int sky_stream_append(sky_stream *s, const int64_t *ids, const double *values, int64_t n) {
-    return stream_append(s, ids, values, n, hipMemcpyHostToDevice);
-}
-int sky_stream_append_dev(sky_stream *s, const int64_t *d_ids, const double *d_values, int64_t n) {
-    return stream_append(s, d_ids, d_values, n, hipMemcpyDeviceToDevice);
-}
-int sky_stream_reserve(sky_stream *s, int64_t tuples) {
-    GUARD_BEGIN
-    ARG_CHECK(s, "null stream");
-    ARG_CHECK(tuples >= 0 && tuples < (int64_t)0x3fffffffLL, "tuples out of range");
-    sky_ctx *c = s->ctx;
-    SKY_TRY(bind(c));
-    if (tuples > s->n) SKY_TRY(stream_reserve(s, tuples - s->n));
-    const size_t m = (size_t)std::max<int64_t>(tuples, 1);
-    // the landmark compaction's target buffer, the host-view query's output, the run's buffers
-    SKY_TRY(s->ids[1 - s->cur].ensure((size_t)std::max<int64_t>(s->cap, 1) * 8));
-    SKY_TRY(s->rows[1 - s->cur].ensure((size_t)std::max<int64_t>(s->cap, 1) * c->D * 8));
-    SKY_TRY(s->out_ids.ensure(m * 8));
-    SKY_TRY(s->out_org.ensure(m * 4));
-    SKY_TRY(s->nanflag.ensure(64));
-    if (!s->nan_host) HIP_TRY(hipHostMalloc(&s->nan_host, 64, hipHostMallocDefault));
-    SKY_TRY(pipe_reserve(*c, c->main, (uint32_t)m));
-    HIP_TRY(hipStreamSynchronize(c->st));
-    return SKY_OK;
-    GUARD_END
-}
-int sky_stream_size(sky_stream *s, int64_t *resident, int64_t *appended) {
-    ARG_CHECK(s, "null stream");
-    if (resident) *resident = s->n;
-    if (appended) *appended = s->appended;
-    return SKY_OK;
-}
-int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap, int64_t *n_out) {
-    GUARD_BEGIN
-    ARG_CHECK(s && n_out, "null argument");
-    SKY_TRY(bind(s->ctx));
-    SKY_TRY(stream_query(s, d_ids_out, d_origin_out, cap, n_out));
-    HIP_TRY(hipStreamSynchronize(s->ctx->st));
-    return SKY_OK;
-    GUARD_END
-}
-int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out) {
-    GUARD_BEGIN
-    ARG_CHECK(s && n_out, "null argument");
-    sky_ctx *c = s->ctx;
-    SKY_TRY(bind(c));
-    const size_t m = (size_t)std::max<int64_t>(s->n, 1);
-    SKY_TRY(s->out_ids.ensure(m * 8));
-    SKY_TRY(s->out_org.ensure(m * 4));
-    int64_t g = 0;
-    SKY_TRY(stream_query(s, s->out_ids.as<int64_t>(), s->out_org.as<int32_t>(), (int64_t)m, &g));
-    *n_out = g;
-    if (g > cap && (ids_out || origin_out)) {
-        HIP_TRY(hipStreamSynchronize(c->st));
-        set_error("output capacity too small");
-        return SKY_E_CAPACITY;
-    }
-    if (g && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, s->out_ids.p, (size_t)g * 8, hipMemcpyDeviceToHost, c->st));
-    if (g && origin_out)
-        HIP_TRY(hipMemcpyAsync(origin_out, s->out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return SKY_OK;
     GUARD_END

@@ -48,6 +48,22 @@ static inline int bind(sky_ctx *c) {
 }
 
 
+static inline void store_stats(sky_ctx *c, const Pipe &p) {
+    c->K_last = p.K;
+    c->lsz.assign(p.h_lsz.begin(), p.h_lsz.end());
+    c->surv.assign(p.h_surv.begin(), p.h_surv.end());
+    c->counters[0] = p.n;
+    c->counters[1] = p.m;
+    c->counters[2] = p.mr;
+    c->counters[3] = p.mg;
+    c->counters[4] = p.nout;
+    c->counters[5] = p.sfs_rounds;
+    c->counters[6] = p.sfs_pairs_upper;
+    c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0) | (p.u16 ? 4 : 0) | (p.last_planned ? 8 : 0) |
+                     (p.last_plan_miss ? 16 : 0) | (p.mbr_tiles << 8);
+    c->dom_w = p.dom_w;
+}
+
 static inline void finish_profile(sky_ctx *c) {
     if (!c->profile) return;
     hipStreamSynchronize(c->st);

@@ -230,14 +230,20 @@ struct sky_part {
     }
 };
 
+struct sky_stream_landmark;     // stream.hip: the landmark window's distinct-vector state
 struct sky_stream {
     sky_ctx *ctx = nullptr;
     int64_t window = 0;         // 0: landmark
-    sky::DevBuf ids[2], rows[2];
+    sky_stream_landmark *lm = nullptr;
+    sky::DevBuf ids[2], rows[2];   // sliding window: a ring of two buffers
     int cur = 0;
-    int64_t off = 0, n = 0;     // resident tuples: [off, off + n) of buffer `cur`
-    int64_t cap = 0;            // capacity (tuples) of both buffers
+    int64_t off = 0, n = 0;     // resident tuples (sliding window: [off, off + n) of buffer `cur`)
+    int64_t cap = 0;            // capacity (tuples) of both ring buffers
     int64_t appended = 0;
     sky::DevBuf out_ids, out_org, nanflag;
     void *nan_host = nullptr;   // pinned word: the append's NaN admission flag
+    sky_stream() = default;
+    sky_stream(const sky_stream &) = delete;
+    sky_stream &operator=(const sky_stream &) = delete;
+    ~sky_stream();
 };

@@ -91,6 +91,7 @@ SIGNATURES = {
     "sky_stream_append": [c_p, c_p, c_p, c_i64],
     "sky_stream_append_dev": [c_p, c_p, c_p, c_i64],
     "sky_stream_size": [c_p, P_i64, P_i64],
+    "sky_stream_vectors": [c_p, P_i64],
     "sky_stream_reserve": [c_p, c_i64],
     "sky_stream_query": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_stream_query_dev": [c_p, c_p, c_p, c_i64, P_i64],

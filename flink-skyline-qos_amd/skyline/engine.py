@@ -347,6 +347,13 @@ class SkylineStream:
         check(lib().sky_stream_size(self.h, ctypes.byref(r), ctypes.byref(a)))
         return r.value, a.value
 
+    def vectors(self):
+        """Rows the next query runs over (sky_stream_vectors): a landmark stream's distinct
+        local-skyline vectors + the tuples appended since its last query."""
+        v = ctypes.c_int64(0)
+        check(lib().sky_stream_vectors(self.h, ctypes.byref(v)))
+        return v.value
+
     def _out(self, cap):
         """Reusable page-locked result buffers (D2H at full PCIe rate), numpy views."""
         if getattr(self, "_cap", 0) < cap:

@@ -210,6 +210,11 @@ int sky_stream_append_dev(sky_stream *s, const int64_t *d_ids, const double *d_v
 int sky_stream_reserve(sky_stream *s, int64_t tuples);
 /* resident tuples and tuples appended since creation */
 int sky_stream_size(sky_stream *s, int64_t *resident, int64_t *appended);
+/* the rows the next query runs over: a landmark stream holds its local-skyline tuples as
+ * distinct vectors (rep + tuple count, tuples as (id, rep) in arrival order), so this is the
+ * distinct local-skyline vectors plus the tuples appended since the last query; a sliding
+ * window: its resident tuples */
+int sky_stream_vectors(sky_stream *s, int64_t *vectors);
 int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
 int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
                          int64_t *n_out);

@@ -37,6 +37,10 @@ if [[ $STEPS == *mtrace* ]]; then
   done
   done
 fi
+if [[ $STEPS == *probe* ]]; then
+  timeout -k 10 120 ./tools/probe/filter_probe > $OUT/filter_probe_$TAG.log 2>&1 || { tail -20 $OUT/filter_probe_$TAG.log; exit 1; }
+  cat $OUT/filter_probe_$TAG.log
+fi
 if [[ $STEPS == *bench* ]]; then
   timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
   cut -c1-1500 $OUT/bench_$TAG.json
