@@ -181,7 +181,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     set(a.y, (const char *)rows + (size_t)own_off * rb, c->dist_ukey.as<uint64_t>() + own_off, n_own, xt, n_union,
         2 * D, p.scratch.as<uint32_t>());
     a.y.domf = p.mbr_domf.as<uint32_t>();
-    a.y.lpt = mbr_lpt_enabled() ? p.mbr_lpt.as<uint32_t>() : nullptr;
+    a.y.lpt = p.mbr_lpt.as<uint32_t>();
     a.ymult = c->dist_umult.as<int64_t>() + own_off;
     a.K = K;
     a.flags = c->main.dist_own.as<uint8_t>();

@@ -155,7 +155,6 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
 // pre-size the tuple-count-proportional buffers of a run over n tuples
 int pipe_reserve(Ctx &c, Pipe &p, uint32_t n);
 // SKY_MBR_LPT=0 turns the bounding-box pass's cost-ordered work queue off (A/B knob)
-bool mbr_lpt_enabled();
 // read device ranges into host memory in one synchronisation (one gather launch when they are small)
 int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
               std::vector<void *> dsts);

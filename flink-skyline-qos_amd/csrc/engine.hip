@@ -600,11 +600,6 @@ int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *,
     return SKY_OK;
 }
 
-// SKY_MBR_LPT=0: the pair pass takes its y tiles in blockIdx order (A/B knob, read per query)
-bool mbr_lpt_enabled() {
-    const char *e = SKY_MEASURE_ENV("SKY_MBR_LPT");
-    return !(e && e[0] == '0');
-}
 
 #ifdef SKY_MEASURE
 // SKY_MBR_DBG & 8 (measurement builds): how the pair pass's work items spread over time --
@@ -615,6 +610,16 @@ static void mbr_trace_report(const unsigned long long *d, size_t n, hipStream_t 
     if (hipMemcpyAsync(h.data(), d, n * 32, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess || !n)
         return;
+    {   // the items that ran (the buffer holds room for the most items the split can make)
+        size_t m = 0;
+        for (size_t i = 0; i < n; i++)
+            if (h[4 * i + 1]) {
+                for (int q = 0; q < 4; q++) h[4 * m + q] = h[4 * i + q];
+                m++;
+            }
+        n = m;
+        if (!n) return;
+    }
     unsigned long long t0 = ~0ull, t1 = 0, tt = 0, tp = 0;
     std::vector<double> dur(n);
     for (size_t i = 0; i < n; i++) {
@@ -697,10 +702,6 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     {
         const char *e = SKY_MEASURE_ENV("SKY_MBR_DBG");
         a.dbg = e ? atoi(e) : 0;
-        // x-tile ranges per y tile: a small rep set has few 64-row y tiles (20k reps: ~330 waves
-        // on 1024 SIMDs), so its groups are split over more waves (domf is OR-ed atomically)
-        const uint32_t nt = (uint32_t)mbr_tiles(mr), ng = (uint32_t)mbr_groups(mr);
-        a.nsplit = (int)std::min<uint32_t>(ng, std::max<uint32_t>(1u, (4096u + nt - 1) / nt));
     }
     a.mm = p.mbr_mm.as<uint32_t>();
     a.code = p.mbr_code.as<uint64_t>();
@@ -719,12 +720,12 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     a.gprange = p.mbr_gpr.as<uint32_t>();
     a.domf = p.mbr_domf.as<uint32_t>();
     a.pairs = p.mbr_pairs.as<unsigned long long>();
-    a.lpt = mbr_lpt_enabled() ? p.mbr_lpt.as<uint32_t>() : nullptr;
+    a.lpt = p.mbr_lpt.as<uint32_t>();
     a.alive_l = p.alive_l.as<uint8_t>();
     a.alive_g = p.alive_g.as<uint8_t>();
 #ifdef SKY_MEASURE
     DevBuf trace;
-    const size_t nitems = mbr_tiles(mr) * (size_t)std::max(a.nsplit, 1);
+    const size_t nitems = mbr_items_max(mbr_tiles(mr));
     if (a.dbg & 8) {
         SKY_TRY(trace.ensure(nitems * 32));
         HIP_TRY(hipMemsetAsync(trace.p, 0, nitems * 32, st));

@@ -355,13 +355,15 @@ struct MbrYSet {
     uint32_t mr, ntiles;
 };
 
-// ---- the y tiles' work queue ---------------------------------------------------------------
-// The work of a y tile varies by orders of magnitude (a loose box reaches many x tiles; PMC on
-// std-anti 8D 2M: ~2 resident waves per SIMD on average against 6 possible, i.e. the launch
-// waits for its slowest waves).  So the y tiles are handed out heaviest first (longest
-// processing time first): the cost estimate is the number of x groups the tile's box reaches,
-// the order a counting sort over 32 log2 buckets, and every wave of the pair pass takes the
-// next tile of that order from a ticket counter.
+// ---- the pair pass's work queue ----------------------------------------------------------
+// The work of a y tile varies by orders of magnitude (a loose box reaches many x tiles), and a
+// launch waits for its slowest wave: on std-anti 8D 2M one y tile took the whole 6.6 ms pass
+// while the rest of the chip idled for its second half (SKY_MBR_DBG=8 work-item timeline,
+// DESIGN.md §2.2).  So the work is cut into items and handed out heaviest first: a y tile's
+// cost is the number of x groups its box reaches (k_mbr_cost); a tile above the average cost
+// is split into up to kMbrSplitMax items that take every s-th reachable group (the reachable
+// groups cluster, so interleaving balances the parts), and every wave of the pair pass takes
+// items from a ticket counter until none is left.
 template <class R>
 __global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restrict__ gmin, uint32_t ngroups,
                                                        MbrYSet ys, uint32_t *__restrict__ lpt) {
@@ -382,26 +384,78 @@ __global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restric
     }
     if (lane == 0) {
         lpt[kMbrLptHead + yt] = cnt;
-        atomicAdd(&lpt[31 - __clz(cnt | 1u)], 1u);          // bucket = floor(log2(cnt)), 0..31
+        if (cnt) atomicAdd(reinterpret_cast<unsigned long long *>(lpt + 36), (unsigned long long)cnt);
     }
 }
 
-// one workgroup: bucket offsets (heaviest bucket first), then every y tile to its slot
+// one workgroup: the split of every y tile, bucket counts of the items' costs (log2), offsets
+// heaviest bucket first, then every item to its slot; lpt[33] = the number of items
 __global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__restrict__ lpt) {
-    __shared__ uint32_t s_off[32];
+    __shared__ uint32_t s_cnt[32], s_off[32];
+    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    // average cost per item slot: at least every y tile, and at least 4096 items to fill the chip
+    const unsigned long long total = *reinterpret_cast<const unsigned long long *>(lpt + 36);
+    const unsigned long long c0 = max(1ull, total / (unsigned long long)max(nyt, 4096u));
+    const uint32_t *cost = lpt + kMbrLptHead;
+    auto split = [&](uint32_t c) -> uint32_t {
+        return c == 0 ? 0u : (uint32_t)min((unsigned long long)min(c, (uint32_t)kMbrSplitMax), (c + c0 - 1) / c0);
+    };
+    for (uint32_t yt = threadIdx.x; yt < nyt; yt += 1024) {
+        const uint32_t c = cost[yt], s = split(c);
+        if (s) atomicAdd(&s_cnt[31 - __clz((c + s - 1) / s)], s);   // bucket = floor(log2(item cost))
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t o = 0;
         for (int b = 31; b >= 0; b--) {
             s_off[b] = o;
-            o += lpt[b];
+            o += s_cnt[b];
         }
+        lpt[33] = o;
     }
     __syncthreads();
-    uint32_t *order = lpt + kMbrLptHead + nyt;
+    uint32_t *items = lpt + kMbrLptHead + nyt;
     for (uint32_t yt = threadIdx.x; yt < nyt; yt += 1024) {
-        const uint32_t c = lpt[kMbrLptHead + yt];
-        order[atomicAdd(&s_off[31 - __clz(c | 1u)], 1u)] = yt;
+        const uint32_t c = cost[yt], s = split(c);
+        if (!s) continue;                          // no reachable group: nothing dominates its rows
+        const uint32_t o = atomicAdd(&s_off[31 - __clz((c + s - 1) / s)], s);
+        for (uint32_t i = 0; i < s; i++) {
+            items[2 * (o + i)] = yt;
+            items[2 * (o + i) + 1] = i | (s << 16);
+        }
     }
+}
+
+// the next work item of this wave (wave-uniform); false when the queue is empty
+__device__ __forceinline__ bool mbr_next_item(uint32_t *__restrict__ lpt, uint32_t nyt, uint32_t &item, uint32_t &yt,
+                                              uint32_t &part, uint32_t &parts) {
+    uint32_t t = 0;
+    if ((threadIdx.x & 63) == 0) t = atomicAdd(&lpt[32], 1u);
+    item = __builtin_amdgcn_readfirstlane(__shfl((int)t, 0, 64));
+    if (item >= __builtin_amdgcn_readfirstlane(lpt[33])) return false;
+    const uint32_t *it = lpt + kMbrLptHead + nyt + 2 * (size_t)item;
+    yt = __builtin_amdgcn_readfirstlane(it[0]);
+    const uint32_t ps = __builtin_amdgcn_readfirstlane(it[1]);
+    part = ps & 0xffffu;
+    parts = ps >> 16;
+    return true;
+}
+
+// this item's share of a chunk of reachable groups m (wave-uniform): the groups whose ordinal
+// among the y tile's reachable groups is = part (mod parts); ord carries the ordinal mod parts.
+// Reachability here is the box test alone (the static set k_mbr_cost counted): every reachable
+// group belongs to exactly one item whatever the items' live lanes do.
+__device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_t part, uint32_t parts) {
+    if (parts == 1) return ~0ull;
+    uint64_t keep = 0;
+    while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        if (ord == part) keep |= 1ull << b;
+        ord = ord + 1 == parts ? 0u : ord + 1;
+    }
+    return keep;
 }
 
 // ---- the pair pass -------------------------------------------------------------------
@@ -425,37 +479,21 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
                                                         const uint32_t *__restrict__ tsub,
                                                         const uint32_t *__restrict__ gmin,
                                                         const uint32_t *__restrict__ gprange, uint32_t mr,
-                                                        uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
+                                                        uint32_t ntiles, MbrYSet ys, int dbg,
                                                         uint32_t *__restrict__ domf,
                                                         unsigned long long *__restrict__ pairs,
                                                         uint32_t *__restrict__ lpt,
                                                         unsigned long long *__restrict__ trace) {
     constexpr int NW = R::NW;
-    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t split, yt, witem;
-    if (lpt) {
-        // the next (y tile, x range) work item of the cost order, heaviest tiles first
-        uint32_t item = 0;
-        if ((threadIdx.x & 63) == 0) item = atomicAdd(&lpt[32], 1u);
-        item = __builtin_amdgcn_readfirstlane(__shfl((int)item, 0, 64));
-        if (item >= ys.ntiles * nsplit) return;
-        split = item % nsplit;
-        witem = item;
-        yt = __builtin_amdgcn_readfirstlane(lpt[kMbrLptHead + ys.ntiles + item / nsplit]);
-    } else {
-        // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so block b runs on
-        // XCD b % 8; give each XCD a contiguous run of y tiles, whose reachable x tiles then
-        // overlap and stay in that XCD's L2 (the grid is padded to a multiple of 8)
-        const uint32_t per_xcd = gridDim.x / 8u;
-        const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
-        // the x tiles are split into nsplit ranges, one work item each
-        split = blk % nsplit;
-        witem = blk;
-        yt = __builtin_amdgcn_readfirstlane((blk / nsplit) * (kMbrPairThreads / 64) + (threadIdx.x >> 6));
-        if (yt >= ys.ntiles) return;
-    }
+    uint64_t npairs = 0, ntested = 0;
+    uint32_t ngrp = 0, nbox = 0, nlist = 0;    // diagnostics (dbg & 4): groups / tiles passing, listed
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
-    const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
+    uint32_t witem, yt, part, parts;
+    while (mbr_next_item(lpt, ys.ntiles, witem, yt, part, parts)) {
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t np0 = npairs, nt0 = ntested;
+    uint32_t gord = 0;                         // this y tile's reachable groups so far, mod parts
+    const uint32_t gs_lo = 0, gs_hi = ngroups;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
     const bool valid = j < ys.mr;
@@ -486,8 +524,6 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     __builtin_amdgcn_wave_barrier();
     uint32_t f = 0;
     uint64_t live = __ballot(valid);
-    uint64_t npairs = 0, ntested = 0;
-    uint32_t ngrp = 0, nbox = 0, nlist = 0;    // diagnostics (dbg & 4): groups / tiles passing, listed
     // per wave: the reachable x tiles of the current group of 64 (tile index, lane mask)
     __shared__ uint32_t s_lx[kMbrPairThreads / 64][64];
     __shared__ uint64_t s_lm[kMbrPairThreads / 64][64];
@@ -713,9 +749,10 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
             const uint32_t gr = gprange[q];
             const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-            bool cand = s0 + lane < gs_hi && R::le(gc, ymax);
+            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax);
+            bool cand = reach;
             if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
-            gm = __ballot(cand);
+            gm = __ballot(cand) & mbr_share(__ballot(reach), gord, part, parts);
         }
         if (!gm) continue;
         ngrp += (uint32_t)__popcll(gm);
@@ -741,10 +778,11 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     if (trace && lane == 0) {
         trace[4 * (size_t)witem] = t_start;
         trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
-        trace[4 * (size_t)witem + 2] = ntested;
-        trace[4 * (size_t)witem + 3] = npairs;
+        trace[4 * (size_t)witem + 2] = ntested - nt0;
+        trace[4 * (size_t)witem + 3] = npairs - np0;
     }
-    if (lane == 0 && pairs) {
+    }                                               // the next work item
+    if ((threadIdx.x & 63) == 0 && pairs) {
         atomicAdd(pairs, (unsigned long long)npairs);
         atomicAdd(pairs + 1, (unsigned long long)ntested);
         if (dbg & 4) {
@@ -775,33 +813,22 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
                                                          const uint32_t *__restrict__ tsub,
                                                          const uint32_t *__restrict__ gmin,
                                                          const uint32_t *__restrict__ gprange, uint32_t mr,
-                                                         uint32_t ntiles, MbrYSet ys, uint32_t nsplit, int dbg,
+                                                         uint32_t ntiles, MbrYSet ys, int dbg,
                                                          uint32_t *__restrict__ domf,
                                                          unsigned long long *__restrict__ pairs,
                                                          uint32_t *__restrict__ lpt,
                                                          unsigned long long *__restrict__ trace) {
     constexpr int NW = R::NW;
     constexpr int S = mbr_subs<R>(), RS = kMbrT / S;
-    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t split, yt, witem;
-    if (lpt) {
-        uint32_t item = 0;
-        if ((threadIdx.x & 63) == 0) item = atomicAdd(&lpt[32], 1u);
-        item = __builtin_amdgcn_readfirstlane(__shfl((int)item, 0, 64));
-        if (item >= ys.ntiles * nsplit) return;
-        split = item % nsplit;
-        witem = item;
-        yt = __builtin_amdgcn_readfirstlane(lpt[kMbrLptHead + ys.ntiles + item / nsplit]);
-    } else {
-        const uint32_t per_xcd = gridDim.x / 8u;
-        const uint32_t blk = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
-        split = blk % nsplit;
-        witem = blk;
-        yt = __builtin_amdgcn_readfirstlane(blk / nsplit);
-        if (yt >= ys.ntiles) return;
-    }
+    uint64_t npairs = 0, ntested = 0;
+    uint32_t ngrp = 0, nbox = 0;
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
-    const uint32_t gs_lo = split * ngroups / nsplit, gs_hi = (split + 1) * ngroups / nsplit;
+    uint32_t witem, yt, part, parts;
+    while (mbr_next_item(lpt, ys.ntiles, witem, yt, part, parts)) {
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t np0 = npairs, nt0 = ntested;
+    uint32_t gord = 0;
+    const uint32_t gs_lo = 0, gs_hi = ngroups;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t j = yt * kMbrT + lane;
     const bool valid = j < ys.mr;
@@ -835,8 +862,6 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
     __builtin_amdgcn_wave_barrier();
     uint32_t f = 0;
     uint64_t live = __ballot(valid);
-    uint64_t npairs = 0, ntested = 0;
-    uint32_t ngrp = 0, nbox = 0;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
 
@@ -926,9 +951,10 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
             for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
             const uint32_t gr = gprange[q];
             const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-            bool cand = s0 + lane < gs_hi && R::le(gc, ymax);
+            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax);
+            bool cand = reach;
             if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
-            gm = __ballot(cand);
+            gm = __ballot(cand) & mbr_share(__ballot(reach), gord, part, parts);
         }
         ngrp += (uint32_t)__popcll(gm);
         while (gm && live) {
@@ -972,7 +998,14 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
         }
     }
     if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
-    if (lane == 0 && pairs) {
+    if (trace && lane == 0) {
+        trace[4 * (size_t)witem] = t_start;
+        trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[4 * (size_t)witem + 2] = ntested - nt0;
+        trace[4 * (size_t)witem + 3] = npairs - np0;
+    }
+    }                                               // the next work item
+    if ((threadIdx.x & 63) == 0 && pairs) {
         atomicAdd(pairs, (unsigned long long)npairs);
         atomicAdd(pairs + 1, (unsigned long long)ntested);
         if (dbg & 4) {
@@ -980,12 +1013,6 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
             atomicAdd(pairs + 3, (unsigned long long)nbox);
             atomicAdd(pairs + 4, (unsigned long long)ntested);
         }
-    }
-    if (trace && lane == 0) {
-        trace[4 * (size_t)witem] = t_start;
-        trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
-        trace[4 * (size_t)witem + 2] = ntested;
-        trace[4 * (size_t)witem + 3] = npairs;
     }
 }
 
@@ -1051,7 +1078,13 @@ static const uint32_t *mbr_build(const uint32_t *rows, const uint64_t *rep_key, 
     return perm;
 }
 
-// the cost order of the y tiles (lpt: kMbrLptHead words zeroed by the caller)
+// one-wave workgroups of the pair pass: each takes work items until the queue is empty; more
+// than stay resident at once (8 per SIMD on 1024 SIMDs), fewer when there are fewer items
+static unsigned mbr_pair_waves(uint32_t ytiles) {
+    return (unsigned)std::min<size_t>(mbr_items_max(ytiles), 8192);
+}
+
+// the work items of the pair pass, heaviest first (lpt: kMbrLptHead words zeroed by the caller)
 template <class R>
 static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, hipStream_t st) {
     k_mbr_cost<R><<<(ys.ntiles + 3) / 4, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
@@ -1066,15 +1099,13 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const uint32_t *perm = mbr_build<R, D>((const uint32_t *)a.rows, a.rep_key, mr, a.mm, a.code, a.code_alt, a.idx,
                                            a.idx_alt, a.radix_scratch, a.err, a.trows, a.tpart, a.tmin, a.tmax,
                                            a.tprange, a.tsub, a.gmin, a.gprange, st, lerr);
-    const unsigned gt = (ntiles + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64);
-    const uint32_t nsplit = a.nsplit < 1 ? 1u : (uint32_t)a.nsplit;
-    const unsigned gp = (gt * nsplit + 7) / 8 * 8;  // the pair pass: a multiple of the 8 XCDs
+    const unsigned gp = mbr_pair_waves(ntiles);
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
-    if (a.lpt) mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
+    mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
     (mbr_v1() ? k_mbr_pairs<R, F, G, true> : k_mbr_pairs2<R, F, G>)                                         \
         <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
-                                                  a.gprange, mr, ntiles, ys, nsplit, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
+                                                  a.gprange, mr, ntiles, ys, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
     if (a.full) {
         if (a.gmerge) SKY_MBR_PAIRS(true, true);
         else SKY_MBR_PAIRS(true, false);
@@ -1118,11 +1149,11 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
                                            y.idx_alt, y.radix_scratch, y.err, y.trows, y.tpart, y.tmin, y.tmax,
                                            y.tprange, y.tsub, nullptr, nullptr, st, lerr);
     const uint32_t nyt = (uint32_t)mbr_tiles(y.mr);
-    const unsigned gp = ((nyt + kMbrPairThreads / 64 - 1) / (kMbrPairThreads / 64) + 7) / 8 * 8;
+    const unsigned gp = mbr_pair_waves(nyt);
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
-    if (y.lpt) mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
+    mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
     (mbr_v1() ? k_mbr_pairs<R, true, true, true> : k_mbr_pairs2<R, true, true>)<<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
-                                                        x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, 1u, x.dbg,
+                                                        x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, x.dbg,
                                                         y.domf, x.pairs, y.lpt, nullptr);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,
                                                                              a.K, a.flags, a.lsz, a.surv);

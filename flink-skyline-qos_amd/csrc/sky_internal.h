@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <algorithm>
 #include <utility>
 #include <vector>
 #include "sky_common.h"
@@ -274,9 +275,13 @@ void launch_move16(int W, const uint32_t *keep, const uint32_t *scan, uint32_t n
 void launch_gather_u32(const uint32_t *src, const uint32_t *at, uint32_t n, uint32_t *out, hipStream_t st);
 
 // ---- k_mbr.hip (both skyline levels of a large rep set, bounding-box pruned all-pairs) ----
-constexpr int kMbrLptHead = 64;   // head words of MbrArgs::lpt
+constexpr int kMbrLptHead = 64;   // head words of MbrArgs::lpt: [0, 32) bucket counts, [32] ticket,
+                                  // [33] work items, [36..37] total cost (u64)
+constexpr int kMbrSplitMax = 64;  // work items per y tile at most (its reachable groups split between them)
 constexpr int kMbrSubMax = 8;     // sub-box corners per 64-row tile (k_mbr.hip mbr_subs)
-inline size_t mbr_lpt_words(size_t ytiles) { return kMbrLptHead + 2 * ytiles; }
+// work items <= ytiles + max(ytiles, 4096) (k_mbr_order's split rule); 2 words per item
+inline size_t mbr_items_max(size_t ytiles) { return ytiles + std::max<size_t>(ytiles, 4096); }
+inline size_t mbr_lpt_words(size_t ytiles) { return kMbrLptHead + ytiles + 2 * mbr_items_max(ytiles); }
 struct MbrArgs {
     int D = 0;
     int fmt = 0;                  // 0: packed u16 rows (dom16 layout), 1: f32 rows, 2: f64 rows
@@ -286,7 +291,6 @@ struct MbrArgs {
     bool gmerge = false;          // the global level (alive_g) too
     bool full = false;            // complete dominance test (rows may repeat a vector)
     int row_min = 24;
-    int nsplit = 1;               // x-tile ranges per y tile (work items of the pair pass)
     int dbg = 0;                  // SKY_MBR_DBG (measurement only): 1 skip the pair tests, 2 also the lane tests
     uint32_t *mm = nullptr;       // [2D]: {0xffffffff} x D, {0} x D on entry
     uint64_t *code = nullptr, *code_alt = nullptr;   // [mr]
@@ -301,9 +305,9 @@ struct MbrArgs {
     uint32_t *gprange = nullptr;  // [ngroups]: their partition ranges
     uint32_t *domf = nullptr;     // [mr], zeroed by the caller
     unsigned long long *pairs = nullptr;             // executed pair tests (optional, zeroed)
-    // the y tiles' work queue (k_mbr_cost / k_mbr_order): [kMbrLptHead] words zeroed by the
-    // caller (bucket counts, the ticket), then a cost and an order word per y tile; nullptr:
-    // the y tiles go in blockIdx order
+    // the pair pass's work queue (k_mbr_cost / k_mbr_order, mbr_lpt_words): [kMbrLptHead] head
+    // words zeroed by the caller, a cost word per y tile, then the work items (y tile, part |
+    // parts << 16), heaviest first
     uint32_t *lpt = nullptr;
     uint8_t *alive_l = nullptr, *alive_g = nullptr;  // [mr] by rep
     // measurement builds only (SKY_MBR_DBG & 8): per work item of the pair pass {start, end,

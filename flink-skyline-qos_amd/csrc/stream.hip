@@ -37,9 +37,14 @@ __device__ __forceinline__ uint32_t row_hash(const double *r, int D, int32_t key
     }
     return (uint32_t)(h ^ (h >> 32));
 }
-__device__ __forceinline__ bool same_row(const double *a, const double *b, int D) {
+// a published rep's row, read past this CU's L1 (another workgroup wrote it during this kernel;
+// a line cached here earlier for a neighbouring rep would be stale)
+__device__ __forceinline__ bool same_row(const double *pub, const double *b, int D) {
     bool eq = true;
-    for (int d = 0; d < D; d++) eq &= __double_as_longlong(a[d]) == __double_as_longlong(b[d]);
+    const unsigned long long *a = reinterpret_cast<const unsigned long long *>(pub);
+    for (int d = 0; d < D; d++)
+        eq &= __hip_atomic_load(a + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              (unsigned long long)__double_as_longlong(b[d]);
     return eq;
 }
 
@@ -137,8 +142,8 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
             }
             if ((uint32_t)(cur >> 32) == h) {
                 const uint32_t r2 = (uint32_t)cur;
-                if (r2 != mine) __threadfence();         // (the publisher fenced its row)
-                if (key2[r2] == k && same_row(rows2 + (size_t)r2 * D, src, D)) {
+                if (__hip_atomic_load(key2 + r2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k &&
+                    same_row(rows2 + (size_t)r2 * D, src, D)) {
                     rep = r2;
                     break;
                 }
@@ -193,7 +198,7 @@ inline unsigned nblk(size_t n) { return (unsigned)((n + kThreads - 1) / kThreads
 struct sky_stream_landmark {
     sky::DevBuf qrows, qids, qkey, qw;      // [reps ; new rows]: capacity qcap rows
     sky::DevBuf tid, trep;                  // resident tuples (arrival order): capacity tcap
-    sky::DevBuf rows2, key2, w2, tid2, trep2, qids2;   // the next state, swapped in after a query
+    sky::DevBuf rows2, key2, w2, tid2, trep2;   // the next state, swapped in after a query
     sky::DevBuf rowf, flag, pos, rflag, rpos, newrep, table, words, scratch;
     int64_t R = 0, N = 0, T = 0, holes = 0;
     int64_t qcap = 0, tcap = 0;
@@ -234,7 +239,6 @@ int lm_reserve(sky_stream *s, int64_t rows, int64_t tuples) {
         SKY_TRY(L.rows2.ensure((size_t)cap * D * 8));
         SKY_TRY(L.key2.ensure((size_t)cap * 4));
         SKY_TRY(L.w2.ensure((size_t)cap * 8));
-        SKY_TRY(L.qids2.ensure((size_t)cap * 8));
         SKY_TRY(L.rowf.ensure((size_t)cap));
         SKY_TRY(L.rflag.ensure((size_t)cap * 4));
         SKY_TRY(L.rpos.ensure((size_t)cap * 4 + 64));

@@ -45,7 +45,7 @@ if [[ $STEPS == *bench* ]]; then
   timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
   cut -c1-1500 $OUT/bench_$TAG.json
 fi
-if [[ $STEPS == *trace* ]]; then
+if [[ $STEPS == *ktrace* ]]; then
   export TMPDIR=/tmp
   rm -rf $OUT/trace_$TAG
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$TAG -o run -- python3 -u $R/bench.py ${BENCH_ARGS} > $OUT/trace_$TAG.log 2>&1 || { tail -30 $OUT/trace_$TAG.log; exit 1; }
