@@ -495,13 +495,15 @@ void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int
                              longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
                              unsigned long long slow_cap, hipStream_t st);
 }
-// SKY_CSV_CHUNKS=1: byte chunks that find their own records and take their first record index from
-// the count pass's prefix, instead of the group pass (every R-th newline) + R records per parse
-// workgroup (A/B knob, read per call; on the C4 text parse 4.55-4.61 ms against 0.86 + 3.81 ms for
-// groups + parse, 2 % less in all, profiles/r03_csv_parse_ab.txt; not yet the default)
+// Byte chunks that find their own records and take their first record index from the count
+// pass's prefix (the default), or SKY_CSV_CHUNKS=0: the group pass (every R-th newline) + R
+// records per parse workgroup (route knob, read per call; the tests run both).  On the C4 text the
+// chunk parse takes 4.55-4.61 ms against 0.86 + 3.81 ms for groups + parse, 2 % less in all
+// (profiles/r03_csv_parse_ab.txt).  Texts of very short records (chunks under 512 bytes) take the
+// group route either way.
 static bool csv_chunk_mode() {
     const char *e = SKY_ENV("SKY_CSV_CHUNKS");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 // ServiceTuple.fromString (ServiceTuple.java:89-104) + filter(nonNull) (FlinkSkyline.java:103)
 // + Long.parseLong(id) (FlinkSkyline.java:276), over a whole device-resident buffer of records.

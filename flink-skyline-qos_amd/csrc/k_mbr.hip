@@ -471,8 +471,9 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 // The y tiles (ytrows / ytpart / ytmax / ytprange, ymr rows) may be another set than the x
 // tiles (the multi-GPU merge: own vectors against the union, FULL only); for one set they are
 // the same arrays.
-template <class R, bool FULL, bool GM, bool PIPE>
-__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+template <class R, bool FULL, bool GM, bool PIPE, int WPE = 0>
+__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
+void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                         const uint32_t *__restrict__ tpart,
                                                         const uint32_t *__restrict__ tmin,
                                                         const uint32_t *__restrict__ tprange,
@@ -805,7 +806,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
 //  * a hit is one LDS atomic OR into the y's fate word (no per-group scalar loop); the fates are
 //    read back once per tile to retire the y's a rep of their own partition dominates.
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
-template <class R, bool FULL, bool GM>
+template <class R, bool FULL, bool GM, bool CPF = false>
 __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
@@ -865,8 +866,18 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
 
-    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx)
-    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
+    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx); CPF:
+    // also its S sub-box corners, 16 bytes per lane in the first S NW / 4 lanes (read back by
+    // readlane: they are in flight with the rows instead of a scalar load per tile)
+    constexpr int CL = S * NW / 4;
+    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px, uint32_t (&cq)[4]) {
+        if constexpr (CPF) {
+            const uint4 c = reinterpret_cast<const uint4 *>(tsub + (size_t)xt * S * NW)[min(lane, (uint32_t)CL - 1u)];
+            cq[0] = c.x;
+            cq[1] = c.y;
+            cq[2] = c.z;
+            cq[3] = c.w;
+        }
         const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);
         const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
 #pragma unroll
@@ -879,7 +890,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
         }
         px = tpart[xi];
     };
-    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px) {
+    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px, const uint32_t (&cq)[4]) {
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         // the S corners: wave-uniform, all loaded before the first test (scalar loads in flight
         // together); the tests are unconditional (a branch per box would wait per load) and a
@@ -889,7 +900,10 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
 #pragma unroll
         for (int b = 0; b < S; b++)
 #pragma unroll
-            for (int w = 0; w < NW; w++) c[b][w] = cs[b * NW + w];
+            for (int w = 0; w < NW; w++) {
+                if constexpr (CPF) c[b][w] = (uint32_t)__builtin_amdgcn_readlane((int)cq[(b * NW + w) & 3], (b * NW + w) >> 2);
+                else c[b][w] = cs[b * NW + w];
+            }
         uint64_t ms[S];
         uint32_t E = 0;
 #pragma unroll
@@ -979,20 +993,20 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
             // register sets used alternately: no copy at the back-edge that would wait for them)
             uint32_t xa = g + (uint32_t)__builtin_ctzll(tm), xb;
             tm &= tm - 1;
-            uint32_t va[NW], vb[NW], pa, pb;
-            load_x(xa, va, pa);
+            uint32_t va[NW], vb[NW], pa, pb, ca[4] = {0, 0, 0, 0}, cb[4] = {0, 0, 0, 0};
+            load_x(xa, va, pa, ca);
             for (;;) {
                 const bool hb = tm != 0ull;
                 xb = hb ? g + (uint32_t)__builtin_ctzll(tm) : xa;
                 tm &= tm - 1;
-                load_x(xb, vb, pb);
-                test_tile(xa, va, pa);
+                load_x(xb, vb, pb, cb);
+                test_tile(xa, va, pa, ca);
                 if (!hb || !live) break;
                 const bool ha = tm != 0ull;
                 xa = ha ? g + (uint32_t)__builtin_ctzll(tm) : xb;
                 tm &= tm - 1;
-                load_x(xa, va, pa);
-                test_tile(xb, vb, pb);
+                load_x(xa, va, pa, ca);
+                test_tile(xb, vb, pb, cb);
                 if (!ha || !live) break;
             }
         }
@@ -1038,6 +1052,16 @@ int mbr_row_words(int D, int fmt) {
 static bool mbr_v1() {
     const char *e = SKY_MEASURE_ENV("SKY_MBR_V1");
     return e && e[0] == '1';
+}
+// SKY_MBR_CPF=1: the round-4 pass with the sub-box corners loaded a tile ahead (A/B)
+static bool mbr_cpf() {
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_CPF");
+    return e && e[0] == '1';
+}
+// SKY_MBR_WPE=6: the round-3 pass with a register budget for 6 waves per SIMD (A/B)
+static int mbr_wpe() {
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_WPE");
+    return e ? atoi(e) : 0;
 }
 // SKY_MBR_ORDER=morton: the Morton order of round 2 (A/B knob, read per build)
 static bool mbr_hilbert() {
@@ -1103,7 +1127,8 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
     mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    (mbr_v1() ? k_mbr_pairs<R, F, G, true> : k_mbr_pairs2<R, F, G>)                                         \
+    (mbr_v1() ? (mbr_wpe() == 6 ? k_mbr_pairs<R, F, G, true, 6> : k_mbr_pairs<R, F, G, true>)               \
+              : (mbr_cpf() ? k_mbr_pairs2<R, F, G, true> : k_mbr_pairs2<R, F, G>))                           \
         <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
                                                   a.gprange, mr, ntiles, ys, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
     if (a.full) {

@@ -81,8 +81,11 @@ def _check(eng, oracle, text, D, offset=0):
     return n
 
 
+@pytest.mark.parametrize("route", ["chunks", "groups"])
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
-def test_csv_fuzz_matches_oracle(gpu_engine_factory, oracle, D):
+def test_csv_fuzz_matches_oracle(gpu_engine_factory, oracle, monkeypatch, D, route):
+    """Both parse routes: byte chunks (the default) and the group pass (SKY_CSV_CHUNKS=0)."""
+    monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
     rng = random.Random(100 + D)
     text = ("\n".join(_record(rng, D) for _ in range(20000))).encode()
     eng = gpu_engine_factory(D, 8)
@@ -91,8 +94,10 @@ def test_csv_fuzz_matches_oracle(gpu_engine_factory, oracle, D):
     eng.close()
 
 
+@pytest.mark.parametrize("route", ["chunks", "groups"])
 @pytest.mark.parametrize("offset", [1, 2, 3, 5])
-def test_csv_unaligned_buffer(gpu_engine_factory, oracle, offset):
+def test_csv_unaligned_buffer(gpu_engine_factory, oracle, monkeypatch, offset, route):
+    monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
     rng = random.Random(offset)
     text = ("\n".join(_record(rng, 3) for _ in range(3000)) + "\n").encode()
     eng = gpu_engine_factory(3, 8)
@@ -157,11 +162,10 @@ print("ok")
 
 
 def test_csv_chunks_listed_spans(gpu_engine_factory, oracle, monkeypatch):
-    """Byte-chunk parse (SKY_CSV_CHUNKS=1): chunks sized from the text's average record, each
+    """Byte-chunk parse (the default; SKY_CSV_CHUNKS=0 is the group route): chunks sized from the text's average record, each
     workgroup finding its own records; chunks that do not fit go to the fallback as spans: > 256
     record starts (tiny records), a record running past the staged tail (mid-text and the text's
-    last, with and without a newline), > 2048 fields.  Same results as the default group-pass
-    parse."""
+    last, with and without a newline), > 2048 fields.  Same results as the group-pass parse."""
     rng = random.Random(21)
     D = 3
     head = [f"{10 ** 6 + i}," + ",".join(str(rng.randrange(10 ** 5, 10 ** 6)) for _ in range(3)) for i in range(8000)]
@@ -177,8 +181,9 @@ def test_csv_chunks_listed_spans(gpu_engine_factory, oracle, monkeypatch):
             eng = gpu_engine_factory(D, 8)
             monkeypatch.setenv("SKY_CSV_CHUNKS", "1")
             n1 = _check(eng, oracle, text, D)
-            monkeypatch.delenv("SKY_CSV_CHUNKS")
+            monkeypatch.setenv("SKY_CSV_CHUNKS", "0")
             n0 = _check(eng, oracle, text, D)
+            monkeypatch.delenv("SKY_CSV_CHUNKS")
             assert n1 == n0
             eng.close()
 

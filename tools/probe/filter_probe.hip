@@ -48,6 +48,76 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
     }
 }
 
+// the box's stream ceilings for the same bytes: rows read one per lane (no work, no store), and
+// 16 B per lane lane-contiguous (1 KB per wave instruction)
+__global__ __launch_bounds__(kThreads) void k_rows_only(const double *__restrict__ p, uint32_t n, double *out) {
+    const uint32_t nl = n - 1;
+    const uint32_t base = blockIdx.x * kThreads * kItems;
+    double acc = 0;
+#pragma unroll 4
+    for (int r = 0; r < kItems; r++) {
+        const double2 *q = reinterpret_cast<const double2 *>(p + (size_t)min(base + r * kThreads + threadIdx.x, nl) * 8);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const double2 x = q[k];
+            acc += x.x + x.y;
+        }
+    }
+    if (acc == 1234.5) out[0] = acc;
+}
+__global__ __launch_bounds__(kThreads) void k_coal_only(const double2 *__restrict__ p, uint32_t n, double *out) {
+    const size_t base = (size_t)blockIdx.x * kThreads * kItems * 4;    // double2 units
+    const size_t lim = (size_t)n * 4;
+    double acc = 0;
+#pragma unroll 4
+    for (int r = 0; r < kItems * 4; r++) {
+        const size_t j = min(base + (size_t)r * kThreads + threadIdx.x, lim - 1);
+        const double2 a = p[j];
+        acc += a.x + a.y;
+    }
+    if (acc == 1234.5) out[0] = acc;
+}
+// coalesced 1 KB wave loads (lane-contiguous 16 B), transposed through a swizzled LDS image into
+// one row per lane, W work and the status store per row (a register-staged k_filter shape)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_coal_lds(const double *__restrict__ p, uint32_t n, int W,
+                                                                    uint16_t *__restrict__ st) {
+    __shared__ double2 s[kThreads / 64][64 * 4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t base = blockIdx.x * kThreads * kItems;
+    const size_t lim = (size_t)n * 4;
+    const double2 *p2 = reinterpret_cast<const double2 *>(p);
+    double2 c[4];
+    auto fetch = [&](int r) {          // wave w's 64 rows of item r: rows base + r*256 + 64w ..
+        const size_t row0 = (size_t)base + (size_t)r * kThreads + 64 * w;
+#pragma unroll
+        for (int k = 0; k < 4; k++) c[k] = p2[min(row0 * 4 + (size_t)k * 64 + lane, lim - 1)];
+    };
+    fetch(0);
+#pragma unroll 1
+    for (int r = 0; r < kItems; r++) {
+        double2 *buf = s[w];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int e = k * 64 + lane, row = e >> 2, q = e & 3;
+            buf[row * 4 + (q ^ ((row >> 2) & 3))] = c[k];
+        }
+        if (r + 1 < kItems) fetch(r + 1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double2 x = buf[lane * 4 + (q ^ ((lane >> 2) & 3))];
+            v[2 * q] = x.x;
+            v[2 * q + 1] = x.y;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint16_t sv = work(v, W);
+        const uint32_t i = base + r * kThreads + 64 * w + lane;
+        if (i < n) st[i] = sv;
+    }
+}
+
 // waitcnt immediates (gfx9 encoding): vmcnt(N) only, N < 64
 #define VMCNT(N) (0x3f70 | ((N) & 15) | (((N) >> 4) << 14))
 
@@ -114,6 +184,24 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
+    double *out;
+    hipMalloc(&out, 64);
+    {
+        auto run0 = [&](const char *name, auto launch, double bytes) {
+            launch();
+            hipEventRecord(a);
+            for (int k = 0; k < 5; k++) launch();
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, a, b);
+            ms /= 5;
+            printf("read-only %-10s %.3f ms  %.2f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12);
+        };
+        run0("rows", [&] { k_rows_only<<<g, kThreads>>>(p, n, out); }, (double)n * 64);
+        run0("coalesced", [&] { k_coal_only<<<g, kThreads>>>(reinterpret_cast<const double2 *>(p), n, out); },
+             (double)n * 64);
+    }
     for (int W : {0, 16, 48, 96}) {
         auto run = [&](const char *name, auto launch) {
             launch();
@@ -127,6 +215,7 @@ int main(int argc, char **argv) {
             printf("W=%3d %-6s %.3f ms  %.2f TB/s\n", W, name, ms, (double)n * 66 / (ms * 1e-3) / 1e12);
         };
         run("reg", [&] { k_reg<<<g, kThreads>>>(p, n, W, st); });
+        run("coal+lds", [&] { k_coal_lds<<<g, kThreads>>>(p, n, W, st); });
         run("lds3", [&] { k_lds<3><<<g, kThreads>>>(p, n, W, st); });
         run("lds4", [&] { k_lds<4><<<g, kThreads>>>(p, n, W, st); });
     }
