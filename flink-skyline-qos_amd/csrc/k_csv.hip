@@ -513,6 +513,7 @@ __device__ __forceinline__ uint8_t parse_record(const Src b, int64_t s, int64_t 
 // A workgroup whose records exceed the LDS window or kFieldsMax fields is listed for
 // k_csv_records (lane per record, reading HBM).
 constexpr int kFieldsMax = 2048;
+constexpr int kCsvFastDims = 8;           // lane-per-record fast path: records of D <= 8 values
 constexpr int kFieldText = 10 * 1024;   // ~19 KB of LDS per workgroup in all: 8 workgroups (32 waves) per CU
 
 
@@ -819,12 +820,86 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         ftot += s_w[i];
     }
     const int nf = (int)ftot + (tail_open ? 1 : 0);
+    const int nnl = (int)(s_w[4] + s_w[5] + s_w[6] + s_w[7]);
     if (nf > kFieldsMax) {                                 // uniform per block
         if (tid == 0) {
             if constexpr (CHUNK) ca.spans[atomicAdd(&spill[0], 1u)] = make_longlong4(a0 + lo, a0 + hi, r0, nr);
             else spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
         }
         return;
+    }
+    // 2b. the producer's shape, one lane per RECORD: when the workgroup holds exactly D + 1 fields
+    // per record (D <= 8), every lane walks its own record's fields left to right, each one an
+    // 8-byte window at its start (its delimiter = the first ',' / '\n' there) and the 32-bit SWAR
+    // conversion, values in registers.  Straight-line for every lane (a field count fixed by D,
+    // no grammar branches), so the divergence that sank lane-per-record parsing in round 1 (the
+    // general grammar, from HBM) does not arise.  Only the newlines are numbered (~1 per lane, not
+    // every delimiter), and there is no per-field LDS traffic beyond the windows.  If ANY record
+    // of the workgroup is not plain digit fields of 1..8 characters, nothing has been stored and
+    // the workgroup takes the general path below on the same staged text.
+    if (D <= kCsvFastDims && nf == nr * (D + 1) && nnl + (tail_open ? 1 : 0) == nr) {          // uniform per block
+        uint16_t *const s_nl = s_rfirst;                    // newline k closes record k (rewritten below)
+        {
+            uint64_t m = (uint64_t)mnl0 | ((uint64_t)mnl1 << 32);
+            uint32_t r = rbase;
+            const uint32_t b0 = 16u * (uint32_t)(tid * per);
+            while (m) {
+                s_nl[r++] = (uint16_t)(b0 + (uint32_t)__builtin_ctzll(m));
+                m &= m - 1ull;
+            }
+        }
+        if (tail_open && tid == 0) s_nl[nr - 1] = (uint16_t)hi;   // the tail record ends at the text's end
+        __syncthreads();
+        bool ok = true;
+        uint32_t idv = 0;
+        double v[kCsvFastDims];
+        if (tid < nr) {
+            const int e = s_nl[tid];
+            int p = tid ? (int)s_nl[tid - 1] + 1 : lo;
+#pragma unroll
+            for (int f = 0; f <= kCsvFastDims; f++) {
+                if (f > D) continue;                        // uniform
+                const int k = p >> 2;
+                const uint32_t sh = (uint32_t)p & 3u;
+                const uint32_t x0 = s_buf[k], x1 = s_buf[k + 1], x2 = s_buf[k + 2];
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, sh), w1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+                const uint64_t cm = (uint64_t)byte_eq_mask(w0, 0x2c2c2c2cu) | ((uint64_t)byte_eq_mask(w1, 0x2c2c2c2cu) << 32);
+                const uint64_t nm = (uint64_t)byte_eq_mask(w0, 0x0a0a0a0au) | ((uint64_t)byte_eq_mask(w1, 0x0a0a0a0au) << 32);
+                int end;
+                if (f < D) {                                // ends at a ',' before any '\n'
+                    const int cf = cm ? (int)(__builtin_ctzll(cm) >> 3) : 8;
+                    const int nf1 = nm ? (int)(__builtin_ctzll(nm) >> 3) : 8;
+                    ok &= cf < nf1;
+                    end = p + cf;
+                } else {                                    // the last field ends at the record's end
+                    end = e;
+                    const int len = min(max(e - p, 0), 8);
+                    ok &= ((cm | nm) & (len >= 8 ? ~0ull : (1ull << (8 * len)) - 1ull)) == 0ull;
+                }
+                uint32_t u;
+                ok &= swar_digits8(s_buf, p, end, u);       // 1..8 digits
+                if (f == 0) idv = u;
+                else v[f - 1] = (double)u;
+                p = min(end + 1, e);
+            }
+        }
+        if (__syncthreads_and(ok ? 1 : 0)) {
+            if (tid < nr) {
+                ids[r0 + tid] = (int64_t)idv;
+                double *const row = vals + (r0 + tid) * D;
+                if ((D & 1) == 0 && ((uintptr_t)vals & 15) == 0) {
+#pragma unroll
+                    for (int c = 0; c < kCsvFastDims; c += 2)
+                        if (c < D) *reinterpret_cast<double2 *>(row + c) = make_double2(v[c], v[c + 1]);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < kCsvFastDims; c++)
+                        if (c < D) row[c] = v[c];
+                }
+                status[r0 + tid] = SKY_CSV_OK;
+            }
+            return;
+        }
     }
     if (tid == 0) {
         s_rfirst[0] = 0;

@@ -394,9 +394,12 @@ __global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__re
     __shared__ uint32_t s_cnt[32], s_off[32];
     if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0;
     __syncthreads();
-    // average cost per item slot: at least every y tile, and at least 4096 items to fill the chip
+    // the cost per item: total / max(nyt, 4096), rounded UP, so that the items
+    // sum_t ceil(c_t / c0) <= nyt + total / c0 <= nyt + max(nyt, 4096) = mbr_items_max(nyt) fit the
+    // queue (rounding down overflowed it: c0 = 1 split every tile into c_t items)
     const unsigned long long total = *reinterpret_cast<const unsigned long long *>(lpt + 36);
-    const unsigned long long c0 = max(1ull, total / (unsigned long long)max(nyt, 4096u));
+    const unsigned long long M = (unsigned long long)max(nyt, 4096u);
+    const unsigned long long c0 = max(1ull, (total + M - 1) / M);
     const uint32_t *cost = lpt + kMbrLptHead;
     auto split = [&](uint32_t c) -> uint32_t {
         return c == 0 ? 0u : (uint32_t)min((unsigned long long)min(c, (uint32_t)kMbrSplitMax), (c + c0 - 1) / c0);

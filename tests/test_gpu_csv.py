@@ -94,6 +94,55 @@ def test_csv_fuzz_matches_oracle(gpu_engine_factory, oracle, monkeypatch, D, rou
     eng.close()
 
 
+def _plain_record(rng, D, i, rate):
+    """The producer's shape (ids and values as plain digit strings, unified_producer.py:174),
+    with a rare perturbation that the lane-per-record fast path must hand to the general path:
+    9-digit fields, decimals, signs, empty / missing / extra fields, '\\r', a trailing comma."""
+    vals = [str(rng.randrange(0, 10 ** rng.choice([1, 4, 8]))) for _ in range(D)]
+    rec = [str(i % 10 ** 8)] + vals
+    if rng.random() < rate:
+        k = rng.randrange(10)
+        c = rng.randrange(D + 1)
+        if k == 0:
+            rec[c] = "123456789"                    # 9 digits: the 64-bit SWAR path
+        elif k == 1:
+            rec[c] = "99999999"                     # 8 digits: still the fast path
+        elif k == 2:
+            rec[c] = "1.5"
+        elif k == 3:
+            rec[c] = "-7" if c else "+7"
+        elif k == 4:
+            rec[c] = ""
+        elif k == 5:
+            rec.pop()
+        elif k == 6:
+            rec.append("3")
+        elif k == 7:
+            rec[-1] += "\r"
+        elif k == 8:
+            rec[-1] += ","
+        else:
+            rec[c] = "00000042"
+    return ",".join(rec)
+
+
+@pytest.mark.parametrize("route", ["chunks", "groups"])
+@pytest.mark.parametrize("D,rate,tail", [(1, 0.001, True), (2, 0.0005, False), (3, 0.002, True), (4, 0.0, False),
+                                         (7, 0.001, False), (8, 0.0005, True), (8, 0.0, False), (9, 0.001, True)])
+def test_csv_producer_shape_mixed(gpu_engine_factory, oracle, monkeypatch, D, rate, tail, route):
+    """Workgroups of plain records take the lane-per-record fast path (D <= 8), a workgroup with
+    one perturbed record takes the general path on the same staged text; both against the oracle,
+    with and without a final newline."""
+    monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
+    rng = random.Random(7 * D + int(rate * 10000))
+    text = "\n".join(_plain_record(rng, D, i, rate) for i in range(60000))
+    text = (text + ("" if tail else "\n")).encode()
+    eng = gpu_engine_factory(D, 8)
+    n = _check(eng, oracle, text, D)
+    assert n >= 60000 * (1 - 2 * rate) - 50
+    eng.close()
+
+
 @pytest.mark.parametrize("route", ["chunks", "groups"])
 @pytest.mark.parametrize("offset", [1, 2, 3, 5])
 def test_csv_unaligned_buffer(gpu_engine_factory, oracle, monkeypatch, offset, route):

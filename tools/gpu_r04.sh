@@ -29,12 +29,19 @@ if [[ $STEPS == *dom* ]]; then
 fi
 if [[ $STEPS == *mtrace* ]]; then
   # measurement build: the pair pass's per-work-item timeline (SKY_MBR_DBG=8)
+  # MBR_VARIANTS: space-separated variants, each a comma-separated list of NAME=VALUE
   for V in ${MBR_VARIANTS:-SKY_MBR_V1=0}; do
   for N in ${DOM_NS:-2000000 10000000}; do
-    env $V SKYLINE_HIP_LIB=$R/flink-skyline-qos_amd/build_measure/libskyline_hip.so SKY_MBR_DBG=${MBR_DBG:-8} \
+    env ${V//,/ } SKYLINE_HIP_LIB=$R/flink-skyline-qos_amd/build_measure/libskyline_hip.so SKY_MBR_DBG=${MBR_DBG:-8} \
       timeout -k 10 300 python -u tools/dom_bench.py $N 2 > $OUT/mtrace_${TAG}_${V}_$N.log 2>&1 || { tail -30 $OUT/mtrace_${TAG}_${V}_$N.log; exit 1; }
     echo "$V $N"; grep "mbr-trace" $OUT/mtrace_${TAG}_${V}_$N.log | tail -2; tail -1 $OUT/mtrace_${TAG}_${V}_$N.log | cut -c1-200
   done
+  done
+fi
+if [[ $STEPS == *csv* ]]; then
+  for C in 1 0; do
+    SKY_CSV_CHUNKS=$C timeout -k 10 240 python -u tools/csv_bench.py > $OUT/csv_${TAG}_$C.log 2>&1 || { tail -30 $OUT/csv_${TAG}_$C.log; exit 1; }
+    echo "chunks=$C $(tail -1 $OUT/csv_${TAG}_$C.log)"
   done
 fi
 if [[ $STEPS == *probe* ]]; then
