@@ -488,7 +488,7 @@ int sky_profile_reset(sky_ctx *c) {
 
 // ---- bulk CSV ingest (k_csv.hip) ---------------------------------------------
 namespace sky {
-int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int *tail);
+int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int D, int *tail);
 int64_t csv_chunk_count(int64_t nbytes, int chunk);
 void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
                              int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
@@ -554,13 +554,13 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const size_t nr1 = (size_t)std::max<int64_t>(nrec, 1);
     // group boundaries only (R records per parse workgroup; R >= 8, and the exact path's groups of
     // 256 need fewer): 8 bytes per group instead of per record
-    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec);
+    const int R = csv_records_per_block(nbytes, nrec, (int64_t)h_commas + nrec, D);
     SKY_TRY(c->csv_status.ensure(nr1));
     // byte chunks (SKY_CSV_CHUNKS=1): each parse workgroup finds its records itself and takes the
     // index of its first one from the count pass's prefix, so no group pass
     int ctail = 0;
     const int chunk =
-        csv_chunk_mode() ? csv_chunk_bytes(nbytes, nrec, (int64_t)h_commas + nrec, &ctail) : 0;
+        csv_chunk_mode() ? csv_chunk_bytes(nbytes, nrec, (int64_t)h_commas + nrec, D, &ctail) : 0;
     if (chunk == 0) {
         SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
         c->ktimer_begin("csv_lines", c->st);

@@ -767,6 +767,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     }
     if (stop == 1) { __syncthreads(); if (s_buf[tid] == 0x12345678u) status[0] = 9; return; }
     if (tid < 4) s_cnt[tid] = 0;
+    for (int i = tid; i < kFieldText / 32 + 4; i += kCsvThreads) s_dlp[i] = 0;   // 2b's bitmap
     s_fempty[tid] = 0x7fffffff;
     s_bad[tid] = 0;
     s_idok[tid] = 1;                                       // cleared by a failed id parse
@@ -775,74 +776,64 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     // Each word's four 0x80 flags are gathered into a nibble by one multiply (bits 7 / 15 /
     // 23 / 31 -> 28..31, no carries)
     static_assert(kUnits * 16 <= 64, "two 32-bit masks per lane");
-    uint32_t md0 = 0, mnl0 = 0, md1 = 0, mnl1 = 0;
-    if constexpr (CHUNK) {                                  // the prologue's masks, clipped to [lo, hi)
-        const int L0 = 16 * (tid * per);
+    uint32_t md0, mnl0, md1, mnl1;
+    {
+        if constexpr (!CHUNK) {                             // (CHUNK: the prologue's masks)
+#pragma unroll
+            for (int k = 0; k < kUnits * 4; k++) {          // unstaged words are 0: no flags
+                const uint32_t mn = byte_eq_mask(dw[k], 0x0a0a0a0au), mc = byte_eq_mask(dw[k], 0x2c2c2c2cu);
+                nl64 |= (uint64_t)((mn * 0x00204081u) >> 28) << (4 * k);
+                cm64 |= (uint64_t)((mc * 0x00204081u) >> 28) << (4 * k);
+            }
+        }
+        const int L0 = 16 * (tid * per);                    // clipped to [lo, hi)
         const uint64_t clip = below(hi - L0) & ~below(lo - L0);
         const uint64_t d = (cm64 | nl64) & clip, n = nl64 & clip;
         md0 = (uint32_t)d;
         md1 = (uint32_t)(d >> 32);
         mnl0 = (uint32_t)n;
         mnl1 = (uint32_t)(n >> 32);
-    } else {
-#pragma unroll
-    for (int k = 0; k < kUnits * 4; k++) {
-        const int b0 = 16 * (tid * per) + 4 * k;
-        uint32_t mc = byte_eq_mask(dw[k], 0x2c2c2c2cu), mn = byte_eq_mask(dw[k], 0x0a0a0a0au);
-        if (k >= per * 4 || b0 + 4 <= lo || b0 >= hi) {
-            mc = mn = 0;
-        } else if (b0 < lo || b0 + 4 > hi) {               // clip to [lo, hi)
-            uint32_t keep = 0;
-            for (int t = 0; t < 4; t++)
-                if (b0 + t >= lo && b0 + t < hi) keep |= 0x80u << (8 * t);
-            mc &= keep;
-            mn &= keep;
-        }
-        const uint32_t nd4 = ((mc | mn) * 0x00204081u) >> 28, nn4 = (mn * 0x00204081u) >> 28;
-        if (k < 8) { md0 |= nd4 << (4 * k); mnl0 |= nn4 << (4 * k); }
-        else { md1 |= nd4 << (4 * (k - 8)); mnl1 |= nn4 << (4 * (k - 8)); }
-    }
     }
     const uint32_t nd = __popc(md0) + __popc(md1), nn = __popc(mnl0) + __popc(mnl1);
-    // block exclusive scans of (nd, nn)
+    // block exclusive scan of (nd, nn), packed in 16-bit halves (a workgroup stages <= 12 KB)
     const int lane = tid & 63, wv = tid >> 6;
-    uint32_t id_ = nd, in_ = nn;
+    const uint32_t x0 = nd | (nn << 16);
+    uint32_t x = x0;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t a = __shfl_up(id_, o, 64), b = __shfl_up(in_, o, 64);
-        if (lane >= o) { id_ += a; in_ += b; }
+        const uint32_t a = __shfl_up(x, o, 64);
+        if (lane >= o) x += a;
     }
-    if (lane == 63) { s_w[wv] = id_; s_w[4 + wv] = in_; }
+    if (lane == 63) s_w[wv] = x;
     __syncthreads();
-    uint32_t fbase = id_ - nd, rbase = in_ - nn, ftot = 0;
+    uint32_t base = x - x0, tot = 0;
     for (int i = 0; i < 4; i++) {
-        if (i < wv) { fbase += s_w[i]; rbase += s_w[4 + i]; }
-        ftot += s_w[i];
+        if (i < wv) base += s_w[i];
+        tot += s_w[i];
     }
+    const uint32_t fbase = base & 0xffffu, rbase = base >> 16, ftot = tot & 0xffffu;
     const int nf = (int)ftot + (tail_open ? 1 : 0);
-    const int nnl = (int)(s_w[4] + s_w[5] + s_w[6] + s_w[7]);
-    if (nf > kFieldsMax) {                                 // uniform per block
-        if (tid == 0) {
-            if constexpr (CHUNK) ca.spans[atomicAdd(&spill[0], 1u)] = make_longlong4(a0 + lo, a0 + hi, r0, nr);
-            else spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
-        }
-        return;
-    }
+    const int nnl = (int)(tot >> 16);
     // 2b. the producer's shape, one lane per RECORD: when the workgroup holds exactly D + 1 fields
-    // per record (D <= 8), every lane walks its own record's fields left to right, each one an
-    // 8-byte window at its start (its delimiter = the first ',' / '\n' there) and the 32-bit SWAR
-    // conversion, values in registers.  Straight-line for every lane (a field count fixed by D,
-    // no grammar branches), so the divergence that sank lane-per-record parsing in round 1 (the
-    // general grammar, from HBM) does not arise.  Only the newlines are numbered (~1 per lane, not
-    // every delimiter), and there is no per-field LDS traffic beyond the windows.  If ANY record
-    // of the workgroup is not plain digit fields of 1..8 characters, nothing has been stored and
-    // the workgroup takes the general path below on the same staged text.
-    if (D <= kCsvFastDims && nf == nr * (D + 1) && nnl + (tail_open ? 1 : 0) == nr) {          // uniform per block
+    // per record (D <= 8), every lane walks its own record: the delimiter masks the lanes already
+    // hold go to an LDS bitmap (one bit per staged byte, two ds_or per lane), a lane reads its
+    // record's 64 bits of it (records < 64 bytes; inside a record every delimiter is a ','), and
+    // each field is one ctz + the 32-bit SWAR conversion, values in registers.  Straight-line for
+    // every lane (a field count fixed by D, no grammar branches), so the divergence that sank
+    // lane-per-record parsing in round 1 (the general grammar, from HBM) does not arise, and only
+    // the newlines are numbered (~1 per lane, not every delimiter).  If ANY record of the
+    // workgroup is not plain digit fields of 1..8 characters, nothing has been stored and the
+    // workgroup takes the general path below on the same staged text.
+    if (D <= kCsvFastDims && nf == nr * (D + 1) && nnl + (tail_open ? 1 : 0) == nr) {   // uniform per block
         uint16_t *const s_nl = s_rfirst;                    // newline k closes record k (rewritten below)
+        uint32_t *const s_bits = s_dlp;                     // delimiter bitmap (zeroed above, rewritten below)
         {
+            const uint32_t b0 = 16u * (uint32_t)(tid * per);
+            const uint64_t x = ((uint64_t)md0 | ((uint64_t)md1 << 32)) << (b0 & 31u);   // <= 48 bits, shift 0 / 16
+            if ((uint32_t)x) atomicOr(&s_bits[b0 >> 5], (uint32_t)x);
+            if ((uint32_t)(x >> 32)) atomicOr(&s_bits[(b0 >> 5) + 1], (uint32_t)(x >> 32));
             uint64_t m = (uint64_t)mnl0 | ((uint64_t)mnl1 << 32);
             uint32_t r = rbase;
-            const uint32_t b0 = 16u * (uint32_t)(tid * per);
             while (m) {
                 s_nl[r++] = (uint16_t)(b0 + (uint32_t)__builtin_ctzll(m));
                 m &= m - 1ull;
@@ -850,40 +841,35 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         }
         if (tail_open && tid == 0) s_nl[nr - 1] = (uint16_t)hi;   // the tail record ends at the text's end
         __syncthreads();
+        if (stop == 6) { if (s_nl[tid] == 0x1234u) status[0] = 9; return; }
         bool ok = true;
         uint32_t idv = 0;
         double v[kCsvFastDims];
         if (tid < nr) {
             const int e = s_nl[tid];
-            int p = tid ? (int)s_nl[tid - 1] + 1 : lo;
+            const int s0 = tid ? (int)s_nl[tid - 1] + 1 : lo;
+            const int len = e - s0;
+            int p = s0;
+            const uint32_t w = (uint32_t)s0 >> 5, o = (uint32_t)s0 & 31u;
+            const uint32_t y0 = s_bits[w], y1 = s_bits[w + 1], y2 = s_bits[w + 2];
+            uint64_t m = (uint64_t)__builtin_amdgcn_alignbit(y1, y0, o) | ((uint64_t)__builtin_amdgcn_alignbit(y2, y1, o) << 32);
+            m &= (1ull << (len & 63)) - 1ull;               // the record's bytes [p, e): its ','s
+            ok = (len < 64) & (__popcll(m) == D);
 #pragma unroll
             for (int f = 0; f <= kCsvFastDims; f++) {
                 if (f > D) continue;                        // uniform
-                const int k = p >> 2;
-                const uint32_t sh = (uint32_t)p & 3u;
-                const uint32_t x0 = s_buf[k], x1 = s_buf[k + 1], x2 = s_buf[k + 2];
-                const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, sh), w1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-                const uint64_t cm = (uint64_t)byte_eq_mask(w0, 0x2c2c2c2cu) | ((uint64_t)byte_eq_mask(w1, 0x2c2c2c2cu) << 32);
-                const uint64_t nm = (uint64_t)byte_eq_mask(w0, 0x0a0a0a0au) | ((uint64_t)byte_eq_mask(w1, 0x0a0a0a0au) << 32);
-                int end;
-                if (f < D) {                                // ends at a ',' before any '\n'
-                    const int cf = cm ? (int)(__builtin_ctzll(cm) >> 3) : 8;
-                    const int nf1 = nm ? (int)(__builtin_ctzll(nm) >> 3) : 8;
-                    ok &= cf < nf1;
-                    end = p + cf;
-                } else {                                    // the last field ends at the record's end
-                    end = e;
-                    const int len = min(max(e - p, 0), 8);
-                    ok &= ((cm | nm) & (len >= 8 ? ~0ull : (1ull << (8 * len)) - 1ull)) == 0ull;
-                }
+                const int end = f < D ? min(s0 + (int)__builtin_ctzll(m | (1ull << 63)), e) : e;
+                m &= m - 1ull;
                 uint32_t u;
                 ok &= swar_digits8(s_buf, p, end, u);       // 1..8 digits
                 if (f == 0) idv = u;
                 else v[f - 1] = (double)u;
-                p = min(end + 1, e);
+                p = end + 1;
             }
         }
-        if (__syncthreads_and(ok ? 1 : 0)) {
+        const int all_ok = __syncthreads_and(ok ? 1 : 0);
+        if (stop == 5) { if (!all_ok && tid == 0) atomicAdd(&counts[0], 1ull); if (idv == 0x12345u) status[0] = (uint8_t)v[0]; return; }
+        if (all_ok) {
             if (tid < nr) {
                 ids[r0 + tid] = (int64_t)idv;
                 double *const row = vals + (r0 + tid) * D;
@@ -900,6 +886,13 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
             }
             return;
         }
+    }
+    if (nf > kFieldsMax) {                                 // uniform per block
+        if (tid == 0) {
+            if constexpr (CHUNK) ca.spans[atomicAdd(&spill[0], 1u)] = make_longlong4(a0 + lo, a0 + hi, r0, nr);
+            else spill[1 + atomicAdd(&spill[0], 1u)] = blockIdx.x;
+        }
+        return;
     }
     if (tid == 0) {
         s_rfirst[0] = 0;
@@ -1262,10 +1255,17 @@ void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g
 // Chunk mode: bytes per chunk from the average record length and field count, so that a chunk's
 // records fit one workgroup (<= 0.8 x 256 records, 0.8 x kFieldsMax fields), and the staged tail
 // past it (*tail: >= 256 bytes and 4 average records); 0 when the chunk would be under 512 bytes
-int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int *tail) {
+// The producer's shape (every record D + 1 fields, D <= 8: the lane-per-record path, which has no
+// field limit) packs 0.9 x 256 records per workgroup; anything else keeps the general path's margins.
+static bool csv_fast_shape(int64_t nrec, int64_t nfields, int D) {
+    return D >= 1 && D <= kCsvFastDims && nfields == nrec * (D + 1);
+}
+int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int D, int *tail) {
     if (nrec <= 0 || nbytes <= 0) return 0;
     const double len = (double)nbytes / (double)nrec, nf = (double)nfields / (double)nrec;
-    const double fit = std::min(0.8 * kCsvThreads * len, 0.8 * kFieldsMax / std::max(nf, 1.0) * len);
+    const double fit = csv_fast_shape(nrec, nfields, D)
+                           ? 0.9 * kCsvThreads * len
+                           : std::min(0.8 * kCsvThreads * len, 0.8 * kFieldsMax / std::max(nf, 1.0) * len);
     const int t = ((int)std::min(std::max(256.0, 4.0 * len), (double)kFieldText / 2) + 15) & ~15;
     const int64_t cb = std::min<int64_t>((int64_t)fit, kFieldText - 16 - t) & ~15ll;
     *tail = t;
@@ -1303,12 +1303,13 @@ void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *
 }
 // records per k_csv_fields workgroup: as many as fit the LDS windows at the stream's average
 // record length and field count (outliers spill to k_csv_records)
-int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields) {
+int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields, int D) {
     if (nrec <= 0) return kCsvThreads;
     const double len = (double)nbytes / (double)nrec, nf = (double)nfields / (double)nrec;
+    const bool fast = csv_fast_shape(nrec, nfields, D);
     int R = kCsvThreads;
-    R = std::min<int>(R, (int)(0.8 * kFieldText / std::max(len, 1.0)));
-    R = std::min<int>(R, (int)(0.8 * kFieldsMax / std::max(nf, 1.0)));
+    R = std::min<int>(R, (int)((fast ? 0.9 : 0.8) * kFieldText / std::max(len, 1.0)));
+    if (!fast) R = std::min<int>(R, (int)(0.8 * kFieldsMax / std::max(nf, 1.0)));
     return std::max(R, 8);
 }
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st) {

@@ -11,14 +11,18 @@
 //                  b bits per dimension (nearby vectors -> nearby positions)
 //   radix sort     (k_radix.hip) of the keys, rep index as value
 //   k_mbr_tiles    one wave per tile of 64 consecutive positions: rows gathered into tile
-//                  order, the tile's bounding box (per-dimension min and max) and partition
-//                  range
-//   k_mbr_pairs    one wave per y tile (lane = y).  The x tiles are scanned 64 at a time
-//                  (lane = x tile): an x tile can hold a dominator of some y of the y tile
-//                  only if its min corner <= the y tile's max corner.  A candidate tile is
-//                  then tested per lane (min corner <= y), and only if some live lane passes
-//                  are its 64 rows compared (scalar row loads, y in VGPRs).  A lane is done
-//                  once a rep of its own partition dominates it.
+//                  order, the tile's bounding box (per-dimension min and max), partition
+//                  range and its sub-box min corners (8 rows each for packed u16 rows)
+//   k_mbr_groups   min corner + partition range of 64 consecutive tiles
+//   k_mbr_cost /   the work queue: per y tile the number of x groups its box reaches, split
+//   k_mbr_order    above the average into items, heaviest first
+//   k_mbr_pairs    persistent one-wave workgroups take items (a y tile, lane = y, or a share
+//                  of its reachable groups).  The x groups' and tiles' min corners are scanned
+//                  64 at a time (lane = group / tile) against the y tile's max corner; for a
+//                  passing tile every live y is tested against the sub-box corners (scalar
+//                  loads, one ballot per sub-box), the surviving (y, sub-box) entries are
+//                  compared 8 per wave instruction from LDS, hits are LDS atomic ORs into the
+//                  y's fate word.  A lane is done once a rep of its own partition dominates it.
 //   k_mbr_finish   alive_l / alive_g per rep
 //
 // The order only decides how much is pruned, never the result: any bounding box contains
@@ -53,6 +57,7 @@ __device__ __forceinline__ uint32_t ord_f32(float f) {       // order-preserving
 template <int D, int W>
 struct RowU16 {
     static constexpr int NW = W;
+    using Pair = RowU16<2 * W, W>;                 // the pair pass reads only the W words
     static __device__ __forceinline__ bool le(const uint32_t *x, const uint32_t *y) {
         uint32_t r = 0;
 #pragma unroll
@@ -84,6 +89,7 @@ struct RowU16 {
 template <int D>
 struct RowF32 {
     static constexpr int NW = padded_dims<float>(D);
+    using Pair = RowF32<D>;
     static __device__ __forceinline__ bool le(const uint32_t *x, const uint32_t *y) {
         bool r = true;
 #pragma unroll
@@ -113,6 +119,7 @@ struct RowF32 {
 template <int D>
 struct RowF64 {
     static constexpr int NW = 2 * padded_dims<double>(D);
+    using Pair = RowF64<D>;
     static __device__ __forceinline__ double get(const uint32_t *r, int d) {
         return __hiloint2double((int)r[2 * d + 1], (int)r[2 * d]);
     }
@@ -466,338 +473,9 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 // vector across partitions, and f32/f64 rows may hold -0.0 / +0.0 twins; otherwise the rows
 // are distinct vectors and "x <= y, x at another position" is dominance.
 // GM: the global level is wanted (bit 1); else only the same-partition bit matters.
+// The y tiles (ys) may be another set than the x tiles (the multi-GPU merge: own vectors against
+// the union, FULL only); for one set they are the same arrays.
 //
-// Software pipeline: the scan finds the next reachable x tile and issues the load of its
-// rows (one row per lane) before the current tile is tested, so a wave keeps a tile load in
-// flight while it computes (8 waves per SIMD alone do not hide the HBM / L2 latency of
-// ~250 dependent tile loads per y tile).
-// The y tiles (ytrows / ytpart / ytmax / ytprange, ymr rows) may be another set than the x
-// tiles (the multi-GPU merge: own vectors against the union, FULL only); for one set they are
-// the same arrays.
-template <class R, bool FULL, bool GM, bool PIPE, int WPE = 0>
-__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
-void k_mbr_pairs(const uint32_t *__restrict__ trows,
-                                                        const uint32_t *__restrict__ tpart,
-                                                        const uint32_t *__restrict__ tmin,
-                                                        const uint32_t *__restrict__ tprange,
-                                                        const uint32_t *__restrict__ tsub,
-                                                        const uint32_t *__restrict__ gmin,
-                                                        const uint32_t *__restrict__ gprange, uint32_t mr,
-                                                        uint32_t ntiles, MbrYSet ys, int dbg,
-                                                        uint32_t *__restrict__ domf,
-                                                        unsigned long long *__restrict__ pairs,
-                                                        uint32_t *__restrict__ lpt,
-                                                        unsigned long long *__restrict__ trace) {
-    constexpr int NW = R::NW;
-    uint64_t npairs = 0, ntested = 0;
-    uint32_t ngrp = 0, nbox = 0, nlist = 0;    // diagnostics (dbg & 4): groups / tiles passing, listed
-    const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
-    uint32_t witem, yt, part, parts;
-    while (mbr_next_item(lpt, ys.ntiles, witem, yt, part, parts)) {
-    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    const uint64_t np0 = npairs, nt0 = ntested;
-    uint32_t gord = 0;                         // this y tile's reachable groups so far, mod parts
-    const uint32_t gs_lo = 0, gs_hi = ngroups;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t j = yt * kMbrT + lane;
-    const bool valid = j < ys.mr;
-    uint32_t y[NW], ymax[NW];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(ys.trows + (size_t)min(j, ys.mr - 1u) * NW);
-#pragma unroll
-        for (int q = 0; q < NW / 4; q++) {
-            const uint4 v = src[q];
-            y[4 * q] = v.x;
-            y[4 * q + 1] = v.y;
-            y[4 * q + 2] = v.z;
-            y[4 * q + 3] = v.w;
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
-    const uint32_t yr = ys.tprange[yt];
-    const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
-    const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
-    // this wave's y rows and partitions in LDS for the broadcast reads of the tests
-    __shared__ uint32_t s_y[kMbrPairThreads / 64][64 * NW];
-    __shared__ uint32_t s_py[kMbrPairThreads / 64][64];
-    uint32_t *sy = s_y[threadIdx.x >> 6], *spy = s_py[threadIdx.x >> 6];
-#pragma unroll
-    for (int w = 0; w < NW; w++) sy[lane * NW + w] = y[w];
-    spy[lane] = py;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t f = 0;
-    uint64_t live = __ballot(valid);
-    // per wave: the reachable x tiles of the current group of 64 (tile index, lane mask)
-    __shared__ uint32_t s_lx[kMbrPairThreads / 64][64];
-    __shared__ uint64_t s_lm[kMbrPairThreads / 64][64];
-    uint32_t *lx = s_lx[threadIdx.x >> 6];
-    uint64_t *lmq = s_lm[threadIdx.x >> 6];
-    // the x tile under test (rows, partitions) and its (y, sub-box) entries
-    __shared__ uint32_t s_x[kMbrPairThreads / 64][64 * NW];
-    __shared__ uint32_t s_px[kMbrPairThreads / 64][64];
-    __shared__ uint8_t s_e[kMbrPairThreads / 64][256];
-    uint32_t *sx = s_x[threadIdx.x >> 6], *spx = s_px[threadIdx.x >> 6];
-    uint8_t *se = s_e[threadIdx.x >> 6];
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    constexpr int BT = 2;                      // x tiles loaded together (independent loads in flight)
-
-    // loads are unconditional (clamped index; flags mask the values): conditional loads make
-    // the compiler wait for every load in flight
-    auto load_group = [&](uint32_t (&tg)[NW], uint32_t &tr, uint32_t g) {
-        const uint32_t t = min(g + lane, ntiles - 1u);
-#pragma unroll
-        for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
-        tr = tprange[t];
-    };
-    // lane l: row l of the tile and the min corner of its sub-box l / 16
-    auto load_tile = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px, uint32_t (&xs)[NW]) {
-        const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);      // rows past mr: masked by xvalid
-        const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
-        // the 16-row box of this lane: one stored corner, or the min of two 8-row ones
-        constexpr int S = mbr_subs<R>(), H = S / 4;
-        const uint4 *sb = reinterpret_cast<const uint4 *>(tsub + ((size_t)xt * S + (lane >> 4) * H) * NW);
-#pragma unroll
-        for (int q = 0; q < NW / 4; q++) {
-            const uint4 v = src[q];
-            xv[4 * q] = v.x;
-            xv[4 * q + 1] = v.y;
-            xv[4 * q + 2] = v.z;
-            xv[4 * q + 3] = v.w;
-            const uint4 c = sb[q];
-            xs[4 * q] = c.x;
-            xs[4 * q + 1] = c.y;
-            xs[4 * q + 2] = c.z;
-            xs[4 * q + 3] = c.w;
-        }
-        if constexpr (H == 2) {
-            uint32_t x2[NW];
-#pragma unroll
-            for (int q = 0; q < NW / 4; q++) {
-                const uint4 c = sb[NW / 4 + q];
-                x2[4 * q] = c.x;
-                x2[4 * q + 1] = c.y;
-                x2[4 * q + 2] = c.z;
-                x2[4 * q + 3] = c.w;
-            }
-            R::cmin(xs, x2);
-        }
-        px = tpart[xi];
-    };
-    // one x tile against its reachable y: each y is first tested against the min corners of
-    // the tile's four 16-row sub-boxes; the surviving (y, sub-box) entries are then compared
-    // four per wave instruction (lanes 16g..16g+15: entry g's 16 rows vs its y, rows and y
-    // read from LDS).  Hits collect in two wave masks, applied to the lanes afterwards.
-    auto test_tile = [&](uint32_t xt, uint64_t lm, const uint32_t (&xv)[NW], uint32_t px, const uint32_t (&xs)[NW]) {
-        lm &= live;
-        if (!lm) return;
-        const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
-        ntested++;
-        uint64_t ms[4];
-        uint32_t E = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t c[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) c[w] = (uint32_t)__builtin_amdgcn_readlane((int)xs[w], 16 * b);
-            ms[b] = (uint32_t)(16 * b) < nx ? lm & __ballot(R::le(c, y)) : 0ull;
-            E += (uint32_t)__popcll(ms[b]);
-        }
-        npairs += 16ull * E;
-        if ((dbg & 1) || !E) return;
-        // stage the tile and the entries (y << 2 | sub-box) in LDS
-#pragma unroll
-        for (int w = 0; w < NW; w++) sx[lane * NW + w] = xv[w];
-        spx[lane] = px;
-        {
-            uint32_t eb = 0;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                if ((ms[b] >> lane) & 1ull) se[eb + (uint32_t)__popcll(ms[b] & lt)] = (uint8_t)((lane << 2) | b);
-                eb += (uint32_t)__popcll(ms[b]);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t g = lane >> 4, r = lane & 15;
-        uint64_t h_any = 0, h_same = 0;
-        for (uint32_t e0 = 0; e0 < E; e0 += 4) {
-            const bool ev = e0 + g < E;
-            const uint32_t ent = se[min(e0 + g, E - 1u)];
-            const uint32_t yb = ent >> 2, xr = (ent & 3u) * 16u + r;
-            uint32_t xw[NW], yw[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) {
-                xw[w] = sx[xr * NW + w];
-                yw[w] = sy[yb * NW + w];
-            }
-            const uint32_t pxl = spx[xr], pyl = spy[yb];
-            // bitwise, not short-circuit: no exec-masked branches per test
-            bool dom = ev & (xr < nx) & R::le(xw, yw);
-            if constexpr (FULL) dom = dom & !R::le(yw, xw);
-            else dom = dom & !(xt == yt && xr == yb);
-            const uint64_t hm = __ballot(dom);
-            if (hm) {
-                const uint64_t hs = __ballot(dom & (pxl == pyl));
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if ((hm >> (16 * q)) & 0xffffull) {
-                        const uint32_t yq = (uint32_t)__builtin_amdgcn_readlane((int)yb, 16 * q);
-                        h_any |= 1ull << yq;
-                        if ((hs >> (16 * q)) & 0xffffull) h_same |= 1ull << yq;
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        f |= ((h_same >> lane) & 1ull) ? 3u : (((h_any >> lane) & 1ull) ? 2u : 0u);
-        live &= __ballot(!(f & 1u));
-    };
-    // one group of 64 x tiles: box tests -> LDS list of reachable tiles (returns its length)
-    auto candidates = [&](const uint32_t (&tg)[NW], uint32_t tr, uint32_t g) -> uint32_t {
-        // some live lane not yet dominated by any rep (global level only): every tile
-        // counts; otherwise only tiles holding rows of the y tile's partitions do
-        const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-        bool cand = g + lane < ntiles && R::le(tg, ymax);
-        if (cand && !need_any) cand = (tr & 0xffffu) <= yph && (tr >> 16) >= ypl;
-        uint64_t gm = __ballot(cand);
-        if (dbg & 2) gm = 0;
-        nbox += (uint32_t)__popcll(gm);
-        uint32_t cnt = 0;
-        while (gm) {
-            const uint32_t b = (uint32_t)__builtin_ctzll(gm);
-            gm &= gm - 1;
-            uint32_t xm[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) xm[w] = (uint32_t)__builtin_amdgcn_readlane((int)tg[w], (int)b);
-            const uint64_t lm = live & __ballot(R::le(xm, y));
-            if (lm) {
-                if (lane == 0) {
-                    lx[cnt] = g + b;
-                    lmq[cnt] = lm;
-                }
-                cnt++;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        nlist += cnt;
-        return cnt;
-    };
-    // list entry k (clamped) as wave-uniform values: LDS reads are per-lane to the compiler;
-    // readfirstlane makes them scalar (bit loops and branches instead of exec-masked VALU ones)
-    auto entry = [&](uint32_t i, uint32_t cnt, uint32_t &xt, uint64_t &lm) {
-        const uint32_t k = min(i, cnt - 1u);
-        xt = __builtin_amdgcn_readfirstlane(lx[k]);
-        const uint64_t e = lmq[k];
-        const uint64_t eu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) << 32) |
-                            (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
-        lm = i < cnt ? eu : 0ull;
-    };
-    // the listed tiles, BT at a time (their loads in flight together)
-    auto process = [&](uint32_t cnt) {
-        for (uint32_t i = 0; i < cnt && live; i += BT) {
-            uint32_t xt[BT], xv[BT][NW], px[BT], xs[BT][NW];
-            uint64_t lmb[BT];
-#pragma unroll
-            for (int u = 0; u < BT; u++) entry(i + u, cnt, xt[u], lmb[u]);
-#pragma unroll
-            for (int u = 0; u < BT; u++) load_tile(xt[u], xv[u], px[u], xs[u]);
-#pragma unroll
-            for (int u = 0; u < BT; u++) test_tile(xt[u], lmb[u], xv[u], px[u], xs[u]);
-        }
-        __builtin_amdgcn_wave_barrier();
-    };
-    // double-buffered: the loads of the next BT listed tiles are issued before the current BT
-    // are tested, so a wave keeps 2 BT tile loads in flight through its compares (two register
-    // sets used alternately: no copy at the back-edge, which would wait for the loads)
-    auto process2 = [&](uint32_t cnt) {
-        uint32_t xa[BT], va[BT][NW], pa[BT], sa[BT][NW], xb[BT], vb[BT][NW], pb[BT], sb[BT][NW];
-        uint64_t la[BT], lb[BT];
-#pragma unroll
-        for (int u = 0; u < BT; u++) {
-            entry(u, cnt, xa[u], la[u]);
-            load_tile(xa[u], va[u], pa[u], sa[u]);
-        }
-        for (uint32_t i = 0; i < cnt && live;) {
-#pragma unroll
-            for (int u = 0; u < BT; u++) {
-                entry(i + BT + u, cnt, xb[u], lb[u]);
-                load_tile(xb[u], vb[u], pb[u], sb[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < BT; u++) test_tile(xa[u], la[u], va[u], pa[u], sa[u]);
-            i += BT;
-            if (i >= cnt || !live) break;
-#pragma unroll
-            for (int u = 0; u < BT; u++) {
-                entry(i + BT + u, cnt, xa[u], la[u]);
-                load_tile(xa[u], va[u], pa[u], sa[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < BT; u++) test_tile(xb[u], lb[u], vb[u], pb[u], sb[u]);
-            i += BT;
-        }
-        __builtin_amdgcn_wave_barrier();
-    };
-
-    // groups 64 at a time (lane = group): the reachable ones as a wave mask; within it the
-    // next group's tile corners load into the same registers right after the current
-    // group's list is built, so they are in flight while its tiles are tested (no
-    // loop-carried copy of registers still being loaded)
-    uint32_t tg[NW], tr = 0;
-    for (uint32_t s0 = gs_lo; s0 < gs_hi && live; s0 += 64) {
-        uint64_t gm;
-        {
-            const uint32_t q = min(s0 + lane, ngroups - 1u);
-            uint32_t gc[NW];
-#pragma unroll
-            for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
-            const uint32_t gr = gprange[q];
-            const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax);
-            bool cand = reach;
-            if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
-            gm = __ballot(cand) & mbr_share(__ballot(reach), gord, part, parts);
-        }
-        if (!gm) continue;
-        ngrp += (uint32_t)__popcll(gm);
-        uint32_t g = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
-        gm &= gm - 1;
-        load_group(tg, tr, g);
-        for (;;) {
-            const uint32_t cnt = candidates(tg, tr, g);
-            const bool more = gm != 0ull;
-            uint32_t gn = 0;
-            if (more) {
-                gn = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
-                gm &= gm - 1;
-                load_group(tg, tr, gn);
-            }
-            if constexpr (PIPE) process2(cnt);
-            else process(cnt);                         // single-buffered (round 2; not instantiated)
-            if (!more || !live) break;
-            g = gn;
-        }
-    }
-    if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
-    if (trace && lane == 0) {
-        trace[4 * (size_t)witem] = t_start;
-        trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
-        trace[4 * (size_t)witem + 2] = ntested - nt0;
-        trace[4 * (size_t)witem + 3] = npairs - np0;
-    }
-    }                                               // the next work item
-    if ((threadIdx.x & 63) == 0 && pairs) {
-        atomicAdd(pairs, (unsigned long long)npairs);
-        atomicAdd(pairs + 1, (unsigned long long)ntested);
-        if (dbg & 4) {
-            atomicAdd(pairs + 2, (unsigned long long)ngrp);
-            atomicAdd(pairs + 3, (unsigned long long)nbox);
-            atomicAdd(pairs + 4, (unsigned long long)nlist);
-        }
-    }
-}
-
-// ---- the pair pass, round 4 ------------------------------------------------------------
 // Per y tile (one wave, lane = y), for every x tile whose min corner is <= the y tile's max
 // corner (found 64 tiles at a time per reachable group, as above):
 //  * the tile's S sub-box min corners are wave-uniform loads (SGPRs), each tested against
@@ -809,8 +487,8 @@ void k_mbr_pairs(const uint32_t *__restrict__ trows,
 //  * a hit is one LDS atomic OR into the y's fate word (no per-group scalar loop); the fates are
 //    read back once per tile to retire the y's a rep of their own partition dominates.
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
-template <class R, bool FULL, bool GM, bool CPF = false>
-__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *__restrict__ trows,
+template <class R, bool FULL, bool GM>
+__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
                                                          const uint32_t *__restrict__ tprange,
@@ -869,18 +547,8 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
 
-    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx); CPF:
-    // also its S sub-box corners, 16 bytes per lane in the first S NW / 4 lanes (read back by
-    // readlane: they are in flight with the rows instead of a scalar load per tile)
-    constexpr int CL = S * NW / 4;
-    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px, uint32_t (&cq)[4]) {
-        if constexpr (CPF) {
-            const uint4 c = reinterpret_cast<const uint4 *>(tsub + (size_t)xt * S * NW)[min(lane, (uint32_t)CL - 1u)];
-            cq[0] = c.x;
-            cq[1] = c.y;
-            cq[2] = c.z;
-            cq[3] = c.w;
-        }
+    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx)
+    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
         const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);
         const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
 #pragma unroll
@@ -893,7 +561,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
         }
         px = tpart[xi];
     };
-    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px, const uint32_t (&cq)[4]) {
+    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px) {
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         // the S corners: wave-uniform, all loaded before the first test (scalar loads in flight
         // together); the tests are unconditional (a branch per box would wait per load) and a
@@ -904,8 +572,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
         for (int b = 0; b < S; b++)
 #pragma unroll
             for (int w = 0; w < NW; w++) {
-                if constexpr (CPF) c[b][w] = (uint32_t)__builtin_amdgcn_readlane((int)cq[(b * NW + w) & 3], (b * NW + w) >> 2);
-                else c[b][w] = cs[b * NW + w];
+                c[b][w] = cs[b * NW + w];
             }
         uint64_t ms[S];
         uint32_t E = 0;
@@ -996,20 +663,20 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs2(const uint32_t *
             // register sets used alternately: no copy at the back-edge that would wait for them)
             uint32_t xa = g + (uint32_t)__builtin_ctzll(tm), xb;
             tm &= tm - 1;
-            uint32_t va[NW], vb[NW], pa, pb, ca[4] = {0, 0, 0, 0}, cb[4] = {0, 0, 0, 0};
-            load_x(xa, va, pa, ca);
+            uint32_t va[NW], vb[NW], pa, pb;
+            load_x(xa, va, pa);
             for (;;) {
                 const bool hb = tm != 0ull;
                 xb = hb ? g + (uint32_t)__builtin_ctzll(tm) : xa;
                 tm &= tm - 1;
-                load_x(xb, vb, pb, cb);
-                test_tile(xa, va, pa, ca);
+                load_x(xb, vb, pb);
+                test_tile(xa, va, pa);
                 if (!hb || !live) break;
                 const bool ha = tm != 0ull;
                 xa = ha ? g + (uint32_t)__builtin_ctzll(tm) : xb;
                 tm &= tm - 1;
-                load_x(xa, va, pa, ca);
-                test_tile(xb, vb, pb, cb);
+                load_x(xa, va, pa);
+                test_tile(xb, vb, pb);
                 if (!ha || !live) break;
             }
         }
@@ -1051,21 +718,6 @@ int mbr_row_words(int D, int fmt) {
     return 2 * padded_dims<double>(D);
 }
 
-// SKY_MBR_V1=1: the round-3 pair pass (16-row boxes, LDS tile list; measurement builds, A/B)
-static bool mbr_v1() {
-    const char *e = SKY_MEASURE_ENV("SKY_MBR_V1");
-    return e && e[0] == '1';
-}
-// SKY_MBR_CPF=1: the round-4 pass with the sub-box corners loaded a tile ahead (A/B)
-static bool mbr_cpf() {
-    const char *e = SKY_MEASURE_ENV("SKY_MBR_CPF");
-    return e && e[0] == '1';
-}
-// SKY_MBR_WPE=6: the round-3 pass with a register budget for 6 waves per SIMD (A/B)
-static int mbr_wpe() {
-    const char *e = SKY_MEASURE_ENV("SKY_MBR_WPE");
-    return e ? atoi(e) : 0;
-}
 // SKY_MBR_ORDER=morton: the Morton order of round 2 (A/B knob, read per build)
 static bool mbr_hilbert() {
     const char *e = SKY_MEASURE_ENV("SKY_MBR_ORDER");
@@ -1114,7 +766,7 @@ static unsigned mbr_pair_waves(uint32_t ytiles) {
 // the work items of the pair pass, heaviest first (lpt: kMbrLptHead words zeroed by the caller)
 template <class R>
 static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, hipStream_t st) {
-    k_mbr_cost<R><<<(ys.ntiles + 3) / 4, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
+    k_mbr_cost<typename R::Pair><<<(ys.ntiles + 3) / 4, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
     k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, lpt);
 }
 
@@ -1130,9 +782,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
     mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
-    (mbr_v1() ? (mbr_wpe() == 6 ? k_mbr_pairs<R, F, G, true, 6> : k_mbr_pairs<R, F, G, true>)               \
-              : (mbr_cpf() ? k_mbr_pairs2<R, F, G, true> : k_mbr_pairs2<R, F, G>))                           \
-        <<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
+    k_mbr_pairs<typename R::Pair, F, G><<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
                                                   a.gprange, mr, ntiles, ys, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
     if (a.full) {
         if (a.gmerge) SKY_MBR_PAIRS(true, true);
@@ -1180,7 +830,7 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     const unsigned gp = mbr_pair_waves(nyt);
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
     mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
-    (mbr_v1() ? k_mbr_pairs<R, true, true, true> : k_mbr_pairs2<R, true, true>)<<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+    k_mbr_pairs<typename R::Pair, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, x.dbg,
                                                         y.domf, x.pairs, y.lpt, nullptr);
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,

@@ -440,7 +440,7 @@ void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g
 void launch_csv_parse_exact(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec,
                             int D, int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts,
                             hipStream_t st);
-int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields);
+int csv_records_per_block(int64_t nbytes, int64_t nrec, int64_t nfields, int D);
 void launch_csv_keep(const uint8_t *status, int64_t n, uint32_t *keep, hipStream_t st);
 void launch_csv_compact(const uint8_t *status, const uint32_t *pos, int64_t n, int D, const int64_t *ids_in,
                         const double *vals_in, int64_t *ids_out, double *vals_out, hipStream_t st);

@@ -14,7 +14,8 @@ eng.format_csv_dev(ids, vals, n, text, nb)
 pi = torch.empty_like(ids); pv = torch.empty_like(vals)
 for mode in os.environ.get("MODES", "0,1,2,3,0").split(","):
     os.environ["SKY_CSV_STOP"] = mode
-    eng.parse_csv_dev(text, nb, pi, pv, n)
+    _, cnt = eng.parse_csv_dev(text, nb, pi, pv, n)
+    print(f"stop={mode} counts {list(cnt)}", flush=True)
     eng.profile(True); eng.profile_reset()
     for _ in range(3):
         eng.parse_csv_dev(text, nb, pi, pv, n)

@@ -30,7 +30,7 @@ fi
 if [[ $STEPS == *mtrace* ]]; then
   # measurement build: the pair pass's per-work-item timeline (SKY_MBR_DBG=8)
   # MBR_VARIANTS: space-separated variants, each a comma-separated list of NAME=VALUE
-  for V in ${MBR_VARIANTS:-SKY_MBR_V1=0}; do
+  for V in ${MBR_VARIANTS:-SKY_MBR_ORDER=hilbert}; do
   for N in ${DOM_NS:-2000000 10000000}; do
     env ${V//,/ } SKYLINE_HIP_LIB=$R/flink-skyline-qos_amd/build_measure/libskyline_hip.so SKY_MBR_DBG=${MBR_DBG:-8} \
       timeout -k 10 300 python -u tools/dom_bench.py $N 2 > $OUT/mtrace_${TAG}_${V}_$N.log 2>&1 || { tail -30 $OUT/mtrace_${TAG}_${V}_$N.log; exit 1; }
