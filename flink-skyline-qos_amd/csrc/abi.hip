@@ -489,8 +489,10 @@ int sky_profile_reset(sky_ctx *c) {
 // ---- bulk CSV ingest (k_csv.hip) ---------------------------------------------
 namespace sky {
 int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int D, int *tail);
+int64_t csv_count_blocks(int64_t nbytes);
 int64_t csv_chunk_count(int64_t nbytes, int chunk);
-void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
+void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off,
+                             const uint32_t *cnt1k, int D,
                              int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
                              longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
                              unsigned long long slow_cap, hipStream_t st);
@@ -515,12 +517,13 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     ARG_CHECK(cap >= 0, "cap out of range");
     SKY_TRY(bind(c));
     const uint8_t *text = reinterpret_cast<const uint8_t *>(d_text);
-    const int64_t nb = csv_chunks(nbytes);
+    const int64_t nb = csv_chunks(nbytes), nbc = csv_count_blocks(nbytes);   // 4 KB passes, 1 KB counts
     const int D = c->D;
-    SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 16));
+    SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 16 + (size_t)nbc * 4));
     SKY_TRY(c->csv_scr.ensure(scan_scratch_words((size_t)std::max<int64_t>(nb, 1)) * 4));
     SKY_TRY(c->csv_counts.ensure(64 + 256 * 8));
-    uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1);
+    uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1),
+             *cnt1k = d_nl + 4;
     uint32_t h_nl = 0;
     uint8_t last = '\n';
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();
@@ -540,7 +543,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     if (nb) {
         HIP_TRY(hipMemsetAsync(d_cnt + 8, 0, 256 * 8, c->st));
         c->ktimer_begin("csv_count", c->st);
-        launch_csv_nl_count(text, nbytes, blk, d_cnt + 8, c->st);
+        launch_csv_nl_count(text, nbytes, blk, cnt1k, d_cnt + 8, c->st);
         scan_excl_u32(blk, blk_off, (size_t)nb, d_nl, c->csv_scr.as<uint32_t>(), c->st);
         c->ktimer_end("csv_count", c->st, nbytes);
         HIP_TRY(hipMemcpyAsync(h_shards.data(), d_cnt + 8, 256 * 8, hipMemcpyDeviceToHost, c->st));
@@ -580,7 +583,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
         SKY_TRY(c->csv_spans.ensure((size_t)csv_chunk_count(nbytes, chunk) * sizeof(longlong4)));
         HIP_TRY(hipMemsetAsync(c->csv_keep.p, 0, 4, c->st));
         c->ktimer_begin("csv_parse", c->st);
-        launch_csv_parse_chunks(text, nbytes, chunk, ctail, blk_off, D, pid, pval, c->csv_status.as<uint8_t>(), d_cnt,
+        launch_csv_parse_chunks(text, nbytes, chunk, ctail, blk_off, cnt1k, D, pid, pval, c->csv_status.as<uint8_t>(), d_cnt,
                                 c->csv_keep.as<uint32_t>(), c->csv_spans.as<longlong4>(), c->csv_slow.as<longlong3>(),
                                 d_cnt + 4, slow_cap, c->st);
         c->ktimer_end("csv_parse", c->st, nrec);

@@ -27,6 +27,7 @@ namespace sky {
 
 constexpr int kCsvThreads = 256;
 constexpr int kCsvChunk = kCsvThreads * 16;   // bytes per workgroup in the newline passes
+constexpr int kCsvCountBlk = 64 * 16;         // bytes per newline count (one per wave of the count pass)
 constexpr int kCommaShards = 256;             // comma-count accumulators (one global atomic per workgroup)
 
 // ---------------------------------------------------------------- newline index
@@ -65,6 +66,7 @@ __device__ __forceinline__ void load16(const uint8_t *__restrict__ text, int64_t
 
 __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__restrict__ text, int64_t nbytes,
                                                               bool aligned, uint32_t *__restrict__ blk_cnt,
+                                                              uint32_t *__restrict__ cnt1k,
                                                               unsigned long long *__restrict__ ncomma) {
     __shared__ uint32_t s_w[kCsvThreads / 64], s_c[kCsvThreads / 64];
     const int64_t base = (int64_t)blockIdx.x * kCsvChunk + threadIdx.x * 16;
@@ -78,7 +80,11 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__r
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o, 64); cm += __shfl_xor(cm, o, 64); }
-    if ((threadIdx.x & 63) == 0) { s_w[threadIdx.x >> 6] = c; s_c[threadIdx.x >> 6] = cm; }
+    if ((threadIdx.x & 63) == 0) {
+        cnt1k[(int64_t)blockIdx.x * (kCsvChunk / kCsvCountBlk) + (threadIdx.x >> 6)] = c;   // per 1 KB (unscanned)
+        s_w[threadIdx.x >> 6] = c;
+        s_c[threadIdx.x >> 6] = cm;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         blk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
@@ -597,6 +603,7 @@ __device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, i
 // records, > kFieldsMax fields) are listed as spans for k_csv_records.
 struct CsvChunkArgs {
     const uint32_t *blk_off;     // exclusive newline counts per 4 KB count chunk
+    const uint32_t *cnt1k;       // newline counts per 1 KB
     longlong4 *spans;            // (start, end or -1, first record, records) of listed chunks
     int chunk;                   // C, bytes (multiple of 16)
     int tail;                    // bytes staged past the chunk (C + 16 + tail <= kFieldText)
@@ -616,7 +623,9 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
     __shared__ __attribute__((aligned(16))) uint32_t s_bufp[4 + kFieldText / 4 + 8];
     uint32_t *const s_buf = s_bufp + 4;
     // delimiter f: staged byte offset | record << 16; s_dl[-1] closes the field before the first
-    __shared__ uint32_t s_dlp[1 + kFieldsMax + kCsvThreads];   // + one dummy slot per lane
+    __shared__ __attribute__((aligned(16))) uint32_t s_dlp[1 + kFieldsMax + kCsvThreads];   // + one dummy slot per lane
+    static_assert(2 * 64 * (kCsvFastDims + 1) * 8 <= (1 + kFieldsMax + kCsvThreads) * 4 &&
+                      2 * 64 * (kCsvFastDims + 1) * 8 <= kFieldText, "two waves' row images per array");
     uint32_t *const s_dl = s_dlp + 1;
     __shared__ uint16_t s_rfirst[kCsvThreads + 1 + kCsvThreads];   // + one dummy slot per lane
     __shared__ int s_fempty[kCsvThreads];
@@ -679,14 +688,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         hi = (int)(span_e - a0);                            // staged byte range of the records
         stage(per);
     } else {
-        __shared__ uint32_t s_nlw, s_nlb;
-        __shared__ int s_first, s_end;
-        if (tid == 0) {
-            s_nlw = 0;
-            s_nlb = 0;
-            s_first = 0x7fffffff;
-            s_end = 0x7fffffff;
-        }
+        __shared__ int s_red[kCsvThreads / 64][4];          // per wave: newlines, first, end, prefix newlines
         const int64_t c = blockIdx.x;
         const int64_t cs = c * ca.chunk, ce = min(cs + ca.chunk, nbytes);
         a0 = c ? cs - 16 : 0;                               // byte cs - 1 tells whether a record starts at cs
@@ -694,10 +696,14 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         nq = (int)((wend - a0 + 15) >> 4);
         per = (nq + kCsvThreads - 1) / kCsvThreads;
         // the newlines in [b_s, cs - 1), b_s = the start of the count block holding byte cs - 1
-        // (< 4 KB, one 16-byte load per lane; the previous chunk staged most of them: L2-hot)
-        const int64_t blk0 = c ? (cs - 1) / kCsvChunk : 0;
+        // (< 4 KB, one 16-byte load per lane; the previous chunk staged most of them: L2-hot).
+        // Chunks of whole count blocks start at a block boundary: then only byte cs - 1 (staged
+        // here) is between the block's prefix and cs - 1, and nothing is loaded
+        const bool blk_aligned = (ca.chunk & (kCsvCountBlk - 1)) == 0;
+        const int64_t blk0 = c ? (blk_aligned ? cs / kCsvCountBlk : (cs - 1) / kCsvChunk) : 0;
         uint32_t nlb = 0;
-        if (c) {
+        if (c && blk_aligned && tid < (int)(blk0 & 3)) nlb = ca.cnt1k[(blk0 & ~3ll) + tid];   // the 4 KB block's earlier KBs
+        if (c && !blk_aligned) {
             const int64_t bs = blk0 * kCsvChunk, base = bs + 16 * tid;
             if (base < cs - 1) {
                 uint32_t w[4];
@@ -713,8 +719,6 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         stage(per);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) nlb += __shfl_xor(nlb, o, 64);
-        __syncthreads();                                    // s_nlw / s_nlb / s_first / s_end initialised
-        if ((tid & 63) == 0 && nlb) atomicAdd(&s_nlb, nlb);
         // newlines in [wlo, whi) start this chunk's records; the first one at or after whi ends its last
         const int wlo = c ? (int)(cs - 1 - a0) : 0, whi = (int)(ce - 1 - a0);
         // the lane's newlines as one bit per staged byte (as in the delimiter pass below), then the
@@ -740,15 +744,26 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
             endp = min(endp, __shfl_xor(endp, o, 64));
         }
         if ((tid & 63) == 0) {
-            atomicAdd(&s_nlw, cnt);
-            atomicMin(&s_first, first);
-            atomicMin(&s_end, endp);
+            s_red[tid >> 6][0] = (int)cnt;
+            s_red[tid >> 6][1] = first;
+            s_red[tid >> 6][2] = endp;
+            s_red[tid >> 6][3] = (int)nlb;
         }
-        __syncthreads();
-        nr = (int)s_nlw + (c == 0 ? 1 : 0);
+        __syncthreads();                                    // (also: the staged text)
+        int s_nlw = 0, s_nlb = 0, s_first = 0x7fffffff, s_end = 0x7fffffff;
+#pragma unroll
+        for (int i = 0; i < kCsvThreads / 64; i++) {
+            s_nlw += s_red[i][0];
+            s_first = min(s_first, s_red[i][1]);
+            s_end = min(s_end, s_red[i][2]);
+            s_nlb += s_red[i][3];
+        }
+        nr = s_nlw + (c == 0 ? 1 : 0);
         if (nr == 0 || stop == 4) return;
         // records before the chunk: record 0 + one per newline in [0, cs - 1)
-        r0 = c == 0 ? 0 : 1 + (int64_t)ca.blk_off[blk0] + (int64_t)s_nlb;
+        r0 = c == 0 ? 0
+                    : 1 + (int64_t)ca.blk_off[blk_aligned ? blk0 >> 2 : blk0] + (int64_t)s_nlb -
+                          (blk_aligned && (s_buf[3] >> 24) == 0x0au ? 1 : 0);   // byte cs - 1 = staged byte 15
         lo = c ? s_first + 1 : 0;
         tail_open = false;
         if (s_end != 0x7fffffff) {
@@ -870,18 +885,26 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         const int all_ok = __syncthreads_and(ok ? 1 : 0);
         if (stop == 5) { if (!all_ok && tid == 0) atomicAdd(&counts[0], 1ull); if (idv == 0x12345u) status[0] = (uint8_t)v[0]; return; }
         if (all_ok) {
+            // each wave's <= 64 rows through its own LDS image (row stride D + 1 doubles: 2-way
+            // banks at most), then D lane-contiguous 8-byte stores per wave; the text and the
+            // bitmap are dead now (the barrier above)
+            const int w = tid >> 6, l = tid & 63;
+            double *const img = reinterpret_cast<double *>(w < 2 ? reinterpret_cast<uint32_t *>(s_buf) : s_dlp) +
+                                (w & 1) * 64 * (kCsvFastDims + 1);
+            const int nw = min(max(nr - 64 * w, 0), 64);
+#pragma unroll
+            for (int c = 0; c < kCsvFastDims; c++)
+                if (c < D) img[l * (D + 1) + c] = v[c];
+            __builtin_amdgcn_wave_barrier();
+            double *const out = vals + (r0 + 64 * w) * D;
+            const uint32_t mD = (65536u + (uint32_t)D - 1u) / (uint32_t)D;   // i / D = (i mD) >> 16 for i < 512
+#pragma unroll
+            for (int k = 0; k < kCsvFastDims; k++) {
+                const uint32_t i = (uint32_t)(k * 64 + l), row = (i * mD) >> 16;
+                if (k < D && (int)i < nw * D) out[i] = img[row * (D + 1) + (i - row * D)];
+            }
             if (tid < nr) {
                 ids[r0 + tid] = (int64_t)idv;
-                double *const row = vals + (r0 + tid) * D;
-                if ((D & 1) == 0 && ((uintptr_t)vals & 15) == 0) {
-#pragma unroll
-                    for (int c = 0; c < kCsvFastDims; c += 2)
-                        if (c < D) *reinterpret_cast<double2 *>(row + c) = make_double2(v[c], v[c + 1]);
-                } else {
-#pragma unroll
-                    for (int c = 0; c < kCsvFastDims; c++)
-                        if (c < D) row[c] = v[c];
-                }
                 status[r0 + tid] = SKY_CSV_OK;
             }
             return;
@@ -1216,13 +1239,14 @@ void launch_csv_fmt_write(const int64_t *ids, const double *vals, int64_t n, int
 }
 
 int64_t csv_chunks(int64_t nbytes) { return (nbytes + kCsvChunk - 1) / kCsvChunk; }
+int64_t csv_count_blocks(int64_t nbytes) { return csv_chunks(nbytes) * (kCsvChunk / kCsvCountBlk); }
 
-void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, unsigned long long *ncomma,
-                         hipStream_t st) {
+void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, uint32_t *cnt1k,
+                         unsigned long long *ncomma, hipStream_t st) {
     const int64_t nb = csv_chunks(nbytes);
     if (nb == 0) return;
     const bool aligned = ((uintptr_t)text & 15) == 0;
-    k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt, ncomma);
+    k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt, cnt1k, ncomma);
 }
 void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
                           hipStream_t st) {
@@ -1267,14 +1291,21 @@ int csv_chunk_bytes(int64_t nbytes, int64_t nrec, int64_t nfields, int D, int *t
                            ? 0.9 * kCsvThreads * len
                            : std::min(0.8 * kCsvThreads * len, 0.8 * kFieldsMax / std::max(nf, 1.0) * len);
     const int t = ((int)std::min(std::max(256.0, 4.0 * len), (double)kFieldText / 2) + 15) & ~15;
-    const int64_t cb = std::min<int64_t>((int64_t)fit, kFieldText - 16 - t) & ~15ll;
+    int64_t cb = std::min<int64_t>((int64_t)fit, kFieldText - 16 - t) & ~15ll;
+    // whole 1 KB count blocks (no newline scan per chunk for its first record's index), and a
+    // staged window of <= 8 KB (two 16-byte units per lane: a third of the mask work less) when
+    // that keeps >= 3/4 of the records per workgroup
+    const int64_t c2 = (int64_t)(8192 - 16 - t) & ~(int64_t)(kCsvCountBlk - 1);
+    if (cb >= kCsvCountBlk) cb = (cb >= c2 && 4 * c2 >= 3 * cb) ? c2 : (cb & ~(int64_t)(kCsvCountBlk - 1));
+    if (const char *e = SKY_MEASURE_ENV("SKY_CSV_CHUNK_BYTES")) cb = atoi(e) & ~15;   // A/B
     *tail = t;
     return cb >= 512 ? (int)cb : 0;
 }
 int64_t csv_chunk_count(int64_t nbytes, int chunk) { return (nbytes + chunk - 1) / chunk; }
-// blk_off: the count pass's exclusive newline counts per 4 KB; spill[0] zeroed (listed spans:
+// blk_off: the count pass's exclusive newline counts per 1 KB; spill[0] zeroed (listed spans:
 // spans[0 .. spill[0])), slow_n zeroed
-void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off, int D,
+void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int tail, const uint32_t *blk_off,
+                             const uint32_t *cnt1k, int D,
                              int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
                              longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
                              unsigned long long slow_cap, hipStream_t st) {
@@ -1282,6 +1313,7 @@ void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int
     if (nc == 0) return;
     CsvChunkArgs ca;
     ca.blk_off = blk_off;
+    ca.cnt1k = cnt1k;
     ca.spans = spans;
     ca.chunk = chunk;
     ca.tail = tail;

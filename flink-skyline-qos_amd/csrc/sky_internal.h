@@ -427,8 +427,8 @@ void synth_host(int dist, int D, int dmin, int dmax, uint64_t seed, int64_t id0,
 
 // ---- k_csv.hip ----
 int64_t csv_chunks(int64_t nbytes);
-void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, unsigned long long *ncomma,
-                         hipStream_t st);
+void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, uint32_t *cnt1k,
+                         unsigned long long *ncomma, hipStream_t st);
 // positions of the newlines that end groups of R records: line_g[g] = end of group g
 void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
                           hipStream_t st);

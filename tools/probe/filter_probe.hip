@@ -48,6 +48,48 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
     }
 }
 
+// reg, but the status words of 8 items staged per wave in LDS and written as one 16-byte store
+// per lane every 8 items (gfx9 counts stores in vmcnt: a short store per item sits in front of
+// the next prefetch's wait)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void k_reg_st8(const double *__restrict__ p, uint32_t n, int W,
+                                                                   uint16_t *__restrict__ st) {
+    __shared__ uint16_t s_st[kThreads / 64][8][64];
+    const uint32_t nl = n - 1;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double vn[8];
+    auto fetch = [&](uint32_t i) {
+        const double2 *q = reinterpret_cast<const double2 *>(p + (size_t)min(i, nl) * 8);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const double2 x = q[k];
+            vn[2 * k] = x.x;
+            vn[2 * k + 1] = x.y;
+        }
+    };
+    const uint32_t base = blockIdx.x * kThreads * kItems;
+    fetch(base + threadIdx.x);
+#pragma unroll 1
+    for (int r0 = 0; r0 < kItems; r0 += 8) {
+#pragma unroll
+        for (int r = r0; r < r0 + 8; r++) {
+            const uint32_t i = base + r * kThreads + threadIdx.x;
+            double v[8];
+#pragma unroll
+            for (int d = 0; d < 8; d++) v[d] = vn[d];
+            fetch(i + kThreads);
+            s_st[w][r - r0][lane] = work(v, W);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        // segment g = item r0 + g: rows base + (r0 + g) * 256 + 64 w .. + 64, 128 bytes
+        const int g = lane >> 3, part = lane & 7;
+        const uint4 x = reinterpret_cast<const uint4 *>(&s_st[w][g][0])[part];
+        const uint32_t row0 = base + (r0 + g) * kThreads + 64 * w + 8 * part;
+        if (row0 + 8 <= n) *reinterpret_cast<uint4 *>(st + row0) = x;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // the box's stream ceilings for the same bytes: rows read one per lane (no work, no store), and
 // 16 B per lane lane-contiguous (1 KB per wave instruction)
 __global__ __launch_bounds__(kThreads) void k_rows_only(const double *__restrict__ p, uint32_t n, double *out) {
@@ -215,6 +257,7 @@ int main(int argc, char **argv) {
             printf("W=%3d %-6s %.3f ms  %.2f TB/s\n", W, name, ms, (double)n * 66 / (ms * 1e-3) / 1e12);
         };
         run("reg", [&] { k_reg<<<g, kThreads>>>(p, n, W, st); });
+        run("reg+st8", [&] { k_reg_st8<<<g, kThreads>>>(p, n, W, st); });
         run("coal+lds", [&] { k_coal_lds<<<g, kThreads>>>(p, n, W, st); });
         run("lds3", [&] { k_lds<3><<<g, kThreads>>>(p, n, W, st); });
         run("lds4", [&] { k_lds<4><<<g, kThreads>>>(p, n, W, st); });
