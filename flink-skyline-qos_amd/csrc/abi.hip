@@ -519,11 +519,11 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     const uint8_t *text = reinterpret_cast<const uint8_t *>(d_text);
     const int64_t nb = csv_chunks(nbytes), nbc = csv_count_blocks(nbytes);   // 4 KB passes, 1 KB counts
     const int D = c->D;
-    SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 16 + (size_t)nbc * 4));
+    SKY_TRY(c->csv_blk.ensure((size_t)(nb + 1) * 8 + 32 + (size_t)nbc * 4));
     SKY_TRY(c->csv_scr.ensure(scan_scratch_words((size_t)std::max<int64_t>(nb, 1)) * 4));
     SKY_TRY(c->csv_counts.ensure(64 + 256 * 8));
-    uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1),
-             *cnt1k = d_nl + 4;
+    uint32_t *blk = c->csv_blk.as<uint32_t>(), *blk_off = blk + (nb + 1), *d_nl = blk_off + (nb + 1);
+    uint32_t *cnt1k = reinterpret_cast<uint32_t *>(((uintptr_t)(d_nl + 4) + 15) & ~(uintptr_t)15);   // 16-byte stores
     uint32_t h_nl = 0;
     uint8_t last = '\n';
     unsigned long long *d_cnt = c->csv_counts.as<unsigned long long>();

@@ -966,7 +966,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             p.sfs_pairs_upper = (int64_t)mbr_pairs[0];  // pair tests the pruned pass executed
             p.mbr_tiles = (int64_t)mbr_pairs[1];        // (y tile, x tile) pairs it tested
             if (mbr_pairs[3])                             // SKY_MBR_DBG bit 4: the scan's funnel
-                fprintf(stderr, "[mbr] reps %u groups %llu box %llu listed %llu tested %llu pairs %llu\n", p.mr,
+                fprintf(stderr, "[mbr] reps %u groups %llu box %llu pre %llu tested %llu pairs %llu\n", p.mr,
                         mbr_pairs[2], mbr_pairs[3], mbr_pairs[4], mbr_pairs[1], mbr_pairs[0]);
             uint32_t alive_sum = 0;
             for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];

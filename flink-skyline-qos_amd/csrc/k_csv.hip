@@ -81,12 +81,13 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__r
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o, 64); cm += __shfl_xor(cm, o, 64); }
     if ((threadIdx.x & 63) == 0) {
-        cnt1k[(int64_t)blockIdx.x * (kCsvChunk / kCsvCountBlk) + (threadIdx.x >> 6)] = c;   // per 1 KB (unscanned)
         s_w[threadIdx.x >> 6] = c;
         s_c[threadIdx.x >> 6] = cm;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        static_assert(kCsvChunk / kCsvCountBlk == 4, "one 16-byte store of the four 1 KB counts");
+        reinterpret_cast<uint4 *>(cnt1k)[blockIdx.x] = make_uint4(s_w[0], s_w[1], s_w[2], s_w[3]);   // unscanned
         blk_cnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
         const uint32_t t = s_c[0] + s_c[1] + s_c[2] + s_c[3];
         if (t) atomicAdd(&ncomma[blockIdx.x & (kCommaShards - 1)], (unsigned long long)t);   // sharded: no hot spot

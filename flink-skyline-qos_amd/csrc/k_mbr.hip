@@ -503,7 +503,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     constexpr int NW = R::NW;
     constexpr int S = mbr_subs<R>(), RS = kMbrT / S;
     uint64_t npairs = 0, ntested = 0;
-    uint32_t ngrp = 0, nbox = 0;
+    uint32_t ngrp = 0, nbox = 0, npre = 0;
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
     uint32_t witem, yt, part, parts;
     while (mbr_next_item(lpt, ys.ntiles, witem, yt, part, parts)) {
@@ -561,7 +561,30 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         }
         px = tpart[xi];
     };
-    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px) {
+    uint32_t tg[NW];                                // min corners of the group's tiles (lane = tile)
+    // the next tile of the group (bits tm) whose whole min corner is <= some live y (the corner
+    // came in with the tile scan: NW readlanes); *pm = those y.  Tiles that can dominate no live y
+    // are dropped here, before their rows are loaded and their sub-box corners read
+    auto next_tile = [&](uint64_t &tm, uint32_t g, uint32_t &xt, uint64_t &pm) -> bool {
+        while (tm) {
+            const int ti = (int)__builtin_ctzll(tm);
+            tm &= tm - 1;
+            uint32_t tc[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) tc[w] = (uint32_t)__builtin_amdgcn_readlane((int)tg[w], ti);
+            const uint64_t p = __ballot(R::le(tc, y)) & live;
+            if (p) {
+                xt = g + (uint32_t)ti;
+                pm = p;
+                return true;
+            }
+        }
+        return false;
+    };
+    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px, uint64_t pm) {
+        const uint64_t pre = pm & live;            // live may have shrunk since the tile was picked
+        if (!pre) return;
+        npre++;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
         // the S corners: wave-uniform, all loaded before the first test (scalar loads in flight
         // together); the tests are unconditional (a branch per box would wait per load) and a
@@ -579,7 +602,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
 #pragma unroll
         for (int b = 0; b < S; b++) {
             const uint64_t bal = __ballot(R::le(c[b], y));
-            ms[b] = bal & live & ((uint32_t)(b * RS) < nx ? ~0ull : 0ull);
+            ms[b] = bal & pre & ((uint32_t)(b * RS) < nx ? ~0ull : 0ull);
             E += (uint32_t)__popcll(ms[b]);
         }
         npairs += (uint64_t)RS * E;
@@ -647,7 +670,6 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             uint64_t tm;
             {
                 const uint32_t t = min(g + lane, ntiles - 1u);
-                uint32_t tg[NW];
 #pragma unroll
                 for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
                 const uint32_t tr = tprange[t];
@@ -659,24 +681,24 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             if (dbg & 2) tm = 0;
             nbox += (uint32_t)__popcll(tm);
             if (!tm) continue;
-            // the tiles of the group, the next one's rows in flight while one is tested (two
-            // register sets used alternately: no copy at the back-edge that would wait for them)
-            uint32_t xa = g + (uint32_t)__builtin_ctzll(tm), xb;
-            tm &= tm - 1;
+            // the group's tiles that pass the whole-tile test, the next one's rows in flight while
+            // one is tested (two register sets used alternately: no copy at the back-edge that would
+            // wait for them; past the last tile the current one is re-loaded, a cache hit)
+            uint32_t xa, xb;
+            uint64_t ma, mb;
+            if (!next_tile(tm, g, xa, ma)) continue;
             uint32_t va[NW], vb[NW], pa, pb;
             load_x(xa, va, pa);
             for (;;) {
-                const bool hb = tm != 0ull;
-                xb = hb ? g + (uint32_t)__builtin_ctzll(tm) : xa;
-                tm &= tm - 1;
+                const bool hb = next_tile(tm, g, xb, mb);
+                if (!hb) xb = xa;
                 load_x(xb, vb, pb);
-                test_tile(xa, va, pa);
+                test_tile(xa, va, pa, ma);
                 if (!hb || !live) break;
-                const bool ha = tm != 0ull;
-                xa = ha ? g + (uint32_t)__builtin_ctzll(tm) : xb;
-                tm &= tm - 1;
+                const bool ha = next_tile(tm, g, xa, ma);
+                if (!ha) xa = xb;
                 load_x(xa, va, pa);
-                test_tile(xb, vb, pb);
+                test_tile(xb, vb, pb, mb);
                 if (!ha || !live) break;
             }
         }
@@ -695,7 +717,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         if (dbg & 4) {
             atomicAdd(pairs + 2, (unsigned long long)ngrp);
             atomicAdd(pairs + 3, (unsigned long long)nbox);
-            atomicAdd(pairs + 4, (unsigned long long)ntested);
+            atomicAdd(pairs + 4, (unsigned long long)npre);
         }
     }
 }

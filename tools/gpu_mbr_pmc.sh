@@ -11,7 +11,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 TAG=${TAG:-r03}
 KRE=${KRE:-k_mbr_pairs}
 PMC_N=${PMC_N:-2000000}
-NS=${NS:-"2000000 10000000"}
+NS=${NS-"2000000 10000000"}
 if [ -z "$SKIP_PMC" ]; then
   i=0
   for CS in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR" \

@@ -38,6 +38,20 @@ if [[ $STEPS == *mtrace* ]]; then
   done
   done
 fi
+if [[ $STEPS == *mdbg* ]]; then
+  # measurement build, results invalid: SKY_MBR_DBG=1 stops each tile after its box tests
+  # (the scan + corner-test cost), =2 after the group / tile scans
+  for M in ${MBR_DBGS:-1 2}; do
+  for N in ${DOM_NS:-2000000 10000000}; do
+    SKYLINE_HIP_LIB=$R/flink-skyline-qos_amd/build_measure/libskyline_hip.so SKY_MBR_DBG=$M \
+      timeout -k 10 300 python -u tools/dom_bench.py $N 2 > $OUT/mdbg_${TAG}_${M}_$N.log 2>&1 || { tail -30 $OUT/mdbg_${TAG}_${M}_$N.log; exit 1; }
+    echo "dbg=$M $N $(tail -1 $OUT/mdbg_${TAG}_${M}_$N.log | cut -c1-160)"
+  done
+  done
+fi
+if [[ $STEPS == *mpmc* ]]; then
+  TAG=$TAG NS="" KRE=k_mbr_pairs PMC_N=${PMC_N:-2000000} bash tools/gpu_mbr_pmc.sh
+fi
 if [[ $STEPS == *csv* ]]; then
   for C in 1 0; do
     SKY_CSV_CHUNKS=$C timeout -k 10 240 python -u tools/csv_bench.py > $OUT/csv_${TAG}_$C.log 2>&1 || { tail -30 $OUT/csv_${TAG}_$C.log; exit 1; }
@@ -51,6 +65,15 @@ fi
 if [[ $STEPS == *bench* ]]; then
   timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { tail -30 $OUT/bench_$TAG.err; exit 1; }
   cut -c1-1500 $OUT/bench_$TAG.json
+fi
+if [[ $STEPS == *dtrace* ]]; then
+  export TMPDIR=/tmp
+  for N in ${DOM_NS:-2000000 10000000}; do
+    rm -rf $OUT/dtrace_${TAG}_$N
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/dtrace_${TAG}_$N -o run -- python3 -u $R/tools/dom_bench.py $N 2 > $OUT/dtrace_${TAG}_$N.log 2>&1 || { tail -30 $OUT/dtrace_${TAG}_$N.log; exit 1; }
+    python tools/prof_summary.py trace $OUT/dtrace_${TAG}_$N > $OUT/dtrace_${TAG}_${N}_summary.txt
+    head -16 $OUT/dtrace_${TAG}_${N}_summary.txt
+  done
 fi
 if [[ $STEPS == *ktrace* ]]; then
   export TMPDIR=/tmp
