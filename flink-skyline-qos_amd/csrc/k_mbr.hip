@@ -374,25 +374,27 @@ struct MbrYSet {
 template <class R>
 __global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restrict__ gmin, uint32_t ngroups,
                                                        MbrYSet ys, uint32_t *__restrict__ lpt) {
+    // lane = y tile: the groups' min corners are wave-uniform (scalar loads, read once per wave
+    // instead of once per y tile), one box test per (y tile, group)
     constexpr int NW = R::NW;
-    const uint32_t yt = __builtin_amdgcn_readfirstlane(blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6));
-    if (yt >= ys.ntiles) return;
-    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t yt = blockIdx.x * kThreads + threadIdx.x;
+    const bool valid = yt < ys.ntiles;
     uint32_t ymax[NW];
 #pragma unroll
-    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
+    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + min(yt, ys.ntiles - 1u)];
     uint32_t cnt = 0;
-    for (uint32_t g0 = 0; g0 < ngroups; g0 += 64) {
-        const uint32_t q = min(g0 + lane, ngroups - 1u);
+#pragma unroll 4
+    for (uint32_t g = 0; g < ngroups; g++) {
         uint32_t gc[NW];
 #pragma unroll
-        for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
-        cnt += (uint32_t)__popcll(__ballot(g0 + lane < ngroups && R::le(gc, ymax)));
+        for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + g];
+        cnt += R::le(gc, ymax) ? 1u : 0u;
     }
-    if (lane == 0) {
-        lpt[kMbrLptHead + yt] = cnt;
-        if (cnt) atomicAdd(reinterpret_cast<unsigned long long *>(lpt + 36), (unsigned long long)cnt);
-    }
+    if (valid) lpt[kMbrLptHead + yt] = cnt;
+    unsigned long long t = valid ? cnt : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+    if ((threadIdx.x & 63) == 0 && t) atomicAdd(reinterpret_cast<unsigned long long *>(lpt + 36), t);
 }
 
 // one workgroup: the split of every y tile, bucket counts of the items' costs (log2), offsets
@@ -488,7 +490,7 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 //    read back once per tile to retire the y's a rep of their own partition dominates.
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
 template <class R, bool FULL, bool GM>
-__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
                                                          const uint32_t *__restrict__ tprange,
@@ -788,7 +790,7 @@ static unsigned mbr_pair_waves(uint32_t ytiles) {
 // the work items of the pair pass, heaviest first (lpt: kMbrLptHead words zeroed by the caller)
 template <class R>
 static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, hipStream_t st) {
-    k_mbr_cost<typename R::Pair><<<(ys.ntiles + 3) / 4, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
+    k_mbr_cost<typename R::Pair><<<(ys.ntiles + kThreads - 1) / kThreads, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
     k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, lpt);
 }
 
