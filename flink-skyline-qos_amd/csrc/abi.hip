@@ -497,15 +497,15 @@ void launch_csv_parse_chunks(const uint8_t *text, int64_t nbytes, int chunk, int
                              longlong4 *spans, longlong3 *slow, unsigned long long *slow_n,
                              unsigned long long slow_cap, hipStream_t st);
 }
-// Byte chunks that find their own records and take their first record index from the count
-// pass's prefix (the default), or SKY_CSV_CHUNKS=0: the group pass (every R-th newline) + R
-// records per parse workgroup (route knob, read per call; the tests run both).  On the C4 text the
-// chunk parse takes 4.55-4.61 ms against 0.86 + 3.81 ms for groups + parse, 2 % less in all
-// (profiles/r03_csv_parse_ab.txt).  Texts of very short records (chunks under 512 bytes) take the
-// group route either way.
+// Parse route (knob read per call; every CSV test runs both).  Default: R records per parse
+// workgroup, the group boundaries found from the count pass's prefixes (k_csv_group_pos, ~1 KB of
+// text per group).  SKY_CSV_CHUNKS=1: byte chunks, each workgroup finds its records itself.  On the
+// C4 text (100M records): decode 4.27 ms for groups (count 0.78 + group ends 0.25 + parse 3.04)
+// against 4.77 ms for chunks (count 0.74 + parse 3.82) (profiles/r04_csv_parse_ab.txt).  Texts of
+// very short records (chunks under 512 bytes) take the group route either way.
 static bool csv_chunk_mode() {
     const char *e = SKY_ENV("SKY_CSV_CHUNKS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 // ServiceTuple.fromString (ServiceTuple.java:89-104) + filter(nonNull) (FlinkSkyline.java:103)
 // + Long.parseLong(id) (FlinkSkyline.java:276), over a whole device-resident buffer of records.
@@ -567,7 +567,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     if (chunk == 0) {
         SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / R + 2) * 8));
         c->ktimer_begin("csv_lines", c->st);
-        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, R, c->csv_lines.as<int64_t>(), c->st);
+        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, cnt1k, nl, R, c->csv_lines.as<int64_t>(), c->st);
         c->ktimer_end("csv_lines", c->st, nbytes);
     }
     direct = cap >= nrec && d_ids_out && d_values_out;
@@ -601,7 +601,7 @@ int sky_parse_csv_dev(sky_ctx *c, const char *d_text, int64_t nbytes, int64_t *d
     if (h_cnt[4] > slow_cap) {   // more exact conversions than the queue holds: re-parse every record exactly
         HIP_TRY(hipMemsetAsync(d_cnt, 0, 40, c->st));
         SKY_TRY(c->csv_lines.ensure((size_t)(std::max<int64_t>(nl, 1) / 256 + 2) * 8));   // unsized on the chunk path
-        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, 256, c->csv_lines.as<int64_t>(), c->st);
+        if (nl) launch_csv_nl_groups(text, nbytes, blk_off, cnt1k, nl, 256, c->csv_lines.as<int64_t>(), c->st);
         launch_csv_parse_exact(text, nbytes, c->csv_lines.as<int64_t>(), nl, nrec, D, pid, pval,
                                c->csv_status.as<uint8_t>(), d_cnt, c->st);
         HIP_TRY(hipGetLastError());

@@ -9,7 +9,7 @@
 // Passes (all HBM-streaming byte work, no MFMA):
 //   k_csv_nl_count  per 4 KB chunk: number of '\n' (16 B per lane, one vector load)
 //   scan            chunk offsets (k_scan.hip)
-//   k_csv_nl_groups positions of every R-th '\n' -> line_g[] (group boundaries, R records per
+//   k_csv_group_pos  positions of every R-th '\n' -> line_g[] (group boundaries, R records per
 //                   parse workgroup; the fallback finds a group's records itself)
 //   k_csv_parse     one lane per record; the workgroup's 256 records are first staged
 //                   into LDS with coalesced dword loads, then each lane walks its record:
@@ -95,46 +95,60 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_nl_count(const uint8_t *__r
 }
 
 
-// Only the group boundaries: the position of every newline whose index g (in the text) ends a
-// group of R records ((g + 1) % R == 0) -> line_g[(g + 1) / R - 1].  The parse workgroups need
-// only their group's first and last byte; a record-per-newline array (8 bytes per record,
-// 0.8 GB at 100M records) was written and read for nothing else.
-__global__ __launch_bounds__(kCsvThreads) void k_csv_nl_groups(const uint8_t *__restrict__ text, int64_t nbytes,
+// Only the group boundaries: line_g[g] = the position of newline (g + 1) R - 1 (0-based, in the
+// text), the last newline of group g (the parse workgroups need only their group's first and last
+// byte).  Found from the count pass's prefixes instead of a second pass over the text: one wave
+// per 4 KB block knows from two prefixes which group ends fall in it (usually none or one), picks
+// the 1 KB quarter holding each by the quarter counts, and reads that 1 KB (16 bytes per lane, a
+// popcount scan): ~1 KB of text per group instead of all of it.
+__global__ __launch_bounds__(kCsvThreads) void k_csv_group_pos(const uint8_t *__restrict__ text, int64_t nbytes,
                                                                bool aligned, const uint32_t *__restrict__ blk_off,
-                                                               uint32_t R, int64_t *__restrict__ line_g) {
-    __shared__ uint32_t s_w[kCsvThreads / 64];
-    const int64_t base = (int64_t)blockIdx.x * kCsvChunk + threadIdx.x * 16;
-    uint32_t w[4], m[4];
-    load16(text, nbytes, base, aligned, w);
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) { m[k] = nl_in_word(w[k]); c += __popc(m[k]); }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += t;
-    }
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    uint32_t g0 = blk_off[blockIdx.x] + inc - c;          // index of this thread's first newline
-    for (int i = 0; i < wv; i++) g0 += s_w[i];
-    if (!c) return;
-    // group ends q = (j + 1) R - 1 within [g0, g0 + c): one division per thread, at most
-    // two ends (c <= 16, R >= 8), each located by skipping q - g0 newlines
-    for (uint32_t q = (g0 / R + 1) * R - 1; q < g0 + c; q += R) {
-        uint32_t t = q - g0;
+                                                               const uint32_t *__restrict__ cnt1k, int64_t nb,
+                                                               uint32_t nl, uint32_t R, int64_t ngb,
+                                                               int64_t *__restrict__ line_g) {
+    const int64_t b = (int64_t)blockIdx.x * (kCsvThreads / 64) + (threadIdx.x >> 6);
+    if (b >= nb) return;                                   // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const uint32_t o0 = blk_off[b], o1 = b + 1 < nb ? blk_off[b + 1] : nl;
+    // group ends q = (g + 1) R - 1 with o0 <= q < o1
+    for (uint64_t q = ((uint64_t)o0 / R + 1) * R - 1; q < o1; q += R) {
+        const int64_t g = (int64_t)((q + 1) / R) - 1;
+        if (g >= ngb) break;
+        uint32_t r = (uint32_t)q - o0;                     // rank of the newline inside block b
+        int j = 0;
+        for (; j < 3; j++) {
+            const uint32_t c = cnt1k[b * (kCsvChunk / kCsvCountBlk) + j];
+            if (r < c) break;
+            r -= c;
+        }
+        const int64_t base = b * kCsvChunk + (int64_t)j * kCsvCountBlk + 16 * lane;
+        uint32_t w[4], m[4], c = 0;
+        load16(text, nbytes, base, aligned, w);
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint32_t ck = __popc(m[k]);
-            if (t < ck) {
-                uint32_t mk = m[k];
-                for (uint32_t u = 0; u < t; u++) mk &= mk - 1;
-                line_g[(q + 1) / R - 1] = base + k * 4 + ((__ffs(mk) - 1) >> 3);
-                break;
+            m[k] = nl_in_word(w[k]);
+            c += __popc(m[k]);
+        }
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        const uint32_t ex = inc - c;
+        if (r >= ex && r < inc) {                          // exactly one lane
+            uint32_t t = r - ex;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t ck = __popc(m[k]);
+                if (t < ck) {
+                    uint32_t mk = m[k];
+                    for (uint32_t u = 0; u < t; u++) mk &= mk - 1;
+                    line_g[g] = base + k * 4 + ((__ffs(mk) - 1) >> 3);
+                    break;
+                }
+                t -= ck;
             }
-            t -= ck;
         }
     }
 }
@@ -595,7 +609,7 @@ __device__ __forceinline__ bool swar_digits8(const uint32_t *__restrict__ buf, i
     return ((swar4_bad(w0) | swar4_bad(w1)) == 0u) & (len - 1u < 8u);   // no short circuit: no branch
 }
 
-// CHUNK = false: workgroup b parses records [b R, b R + R) (group boundaries from k_csv_nl_groups).
+// CHUNK = false: workgroup b parses records [b R, b R + R) (group boundaries from k_csv_group_pos).
 // CHUNK = true (no group pass): workgroup c parses the records that START in the byte chunk
 // [c C, c C + C): it stages the chunk plus a tail for its last record, finds its first record
 // start and its last record's end itself, and takes its first record's index from the count
@@ -672,7 +686,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_fields(const uint8_t *__res
         r0 = (int64_t)blockIdx.x * R;                       // R <= 256 records per workgroup (host-chosen)
         nr = (int)(nrec - r0 < R ? nrec - r0 : R);
         const int64_t rl = r0 + nr - 1;
-        // group boundaries (k_csv_nl_groups): the last group ends at the end of the text (its last
+        // group boundaries (k_csv_group_pos): the last group ends at the end of the text (its last
         // record has no '\n', or its '\n' is the last byte)
         const int64_t span_s = r0 == 0 ? 0 : line_g[blockIdx.x - 1] + 1;
         tail_open = rl >= nl;                               // last record has no '\n'
@@ -1055,7 +1069,7 @@ __global__ __launch_bounds__(kCsvThreads) void k_csv_slow(const uint8_t *__restr
 
 // ---- fallback: the workgroups k_csv_fields listed (very long records), lane per record from HBM.
 // The group's records are found here: the workgroup scans its span (group boundaries from
-// k_csv_nl_groups, or a listed chunk's span: its first record, and its end when known) 4 KB at
+// k_csv_group_pos, or a listed chunk's span: its first record, and its end when known) 4 KB at
 // a time for newlines, numbering them by a block scan; a chunk's records go in rounds of 256.
 __global__ __launch_bounds__(kCsvThreads) void k_csv_records(const uint8_t *__restrict__ text, int64_t nbytes,
                                                              const int64_t *__restrict__ line_g, int64_t nl,
@@ -1249,12 +1263,13 @@ void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt,
     const bool aligned = ((uintptr_t)text & 15) == 0;
     k_csv_nl_count<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_cnt, cnt1k, ncomma);
 }
-void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
-                          hipStream_t st) {
-    const int64_t nb = csv_chunks(nbytes);
-    if (nb == 0) return;
+void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, const uint32_t *cnt1k,
+                          int64_t nl, int R, int64_t *line_g, hipStream_t st) {
+    const int64_t nb = csv_chunks(nbytes), ngb = nl / R;
+    if (nb == 0 || ngb == 0) return;
     const bool aligned = ((uintptr_t)text & 15) == 0;
-    k_csv_nl_groups<<<(unsigned)nb, kCsvThreads, 0, st>>>(text, nbytes, aligned, blk_off, (uint32_t)R, line_g);
+    k_csv_group_pos<<<(unsigned)((nb + kCsvThreads / 64 - 1) / (kCsvThreads / 64)), kCsvThreads, 0, st>>>(
+        text, nbytes, aligned, blk_off, cnt1k, nb, (uint32_t)nl, (uint32_t)R, ngb, line_g);
 }
 static int csv_stop() {
     const char *e = SKY_MEASURE_ENV("SKY_CSV_STOP");

@@ -430,8 +430,8 @@ int64_t csv_chunks(int64_t nbytes);
 void launch_csv_nl_count(const uint8_t *text, int64_t nbytes, uint32_t *blk_cnt, uint32_t *cnt1k,
                          unsigned long long *ncomma, hipStream_t st);
 // positions of the newlines that end groups of R records: line_g[g] = end of group g
-void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, int R, int64_t *line_g,
-                          hipStream_t st);
+void launch_csv_nl_groups(const uint8_t *text, int64_t nbytes, const uint32_t *blk_off, const uint32_t *cnt1k,
+                          int64_t nl, int R, int64_t *line_g, hipStream_t st);
 void launch_csv_parse(const uint8_t *text, int64_t nbytes, const int64_t *line_g, int64_t nl, int64_t nrec, int D,
                       int64_t *ids, double *vals, uint8_t *status, unsigned long long *counts, uint32_t *spill,
                       longlong3 *slow, unsigned long long *slow_n, unsigned long long slow_cap, int R,

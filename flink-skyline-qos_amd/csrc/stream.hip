@@ -119,12 +119,11 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
                                                           uint32_t *__restrict__ ctr, uint32_t *__restrict__ newrep) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     const bool local = i < N && (rowf[R + i] & 1u);
-    uint32_t rep = 0xffffffffu;
-    if (local) {
-        const double *src = qrows + (size_t)(R + i) * D;
-        const int32_t k = qkey[R + i];
-        const uint32_t h = row_hash(src, D, k);
-        uint32_t mine = 0xffffffffu;                 // reserved rep slot (written before publishing)
+    const double *src = qrows + (size_t)(R + min(i, N - 1u)) * D;
+    const int32_t k = local ? qkey[R + i] : 0;
+    const uint32_t h = local ? row_hash(src, D, k) : 0u;
+    auto lookup = [&]() -> uint32_t {
+        uint32_t mine = 0xffffffffu, rep = 0xffffffffu;   // reserved rep slot (written before publishing)
         for (uint32_t s = h & hmask;; s = (s + 1) & hmask) {
             unsigned long long cur = table[s];
             if (cur == kHashEmpty) {
@@ -150,16 +149,42 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
             }
         }
         if (mine != 0xffffffffu && mine != rep) key2[mine] = -1;   // lost the race: an inert hole
-        newrep[i] = rep;
-    }
-    // tuple counts: one atomic per distinct rep of the wave
+        return rep;
+    };
+    // duplicates first resolved inside the wave: up to two leaders look their row up and every lane
+    // holding the same (key, row) takes the leader's rep, so a vector repeated across the stream (the
+    // zero vector of the reference streams) costs one table probe per wave, not one per tuple on
+    // the same table slot
+    const int lane = (int)(threadIdx.x & 63);
+    uint32_t rep = 0xffffffffu;
+    bool done = !local;
     uint64_t pend = __ballot(local);
-    while (pend) {
+    for (int round = 0; round < 2 && pend; round++) {
         const int leader = __ffsll((unsigned long long)pend) - 1;
+        bool same = !done && h == (uint32_t)__shfl((int)h, leader, 64) && k == __shfl(k, leader, 64);
+        for (int d = 0; d < D; d++) {
+            const long long x = __double_as_longlong(src[d]);   // bits: the table's notion of one vector
+            same &= __shfl(x, leader, 64) == x;
+        }
+        uint32_t r = 0;
+        if (lane == leader) r = lookup();
+        r = (uint32_t)__shfl((int)r, leader, 64);
+        if (same) {
+            rep = r;
+            done = true;
+        }
+        pend = __ballot(!done);
+    }
+    if (!done) rep = lookup();
+    if (local) newrep[i] = rep;
+    // tuple counts: one atomic per distinct rep of the wave
+    uint64_t pw = __ballot(local);
+    while (pw) {
+        const int leader = __ffsll((unsigned long long)pw) - 1;
         const uint32_t r0 = __shfl(rep, leader, 64);
         const uint64_t same = __ballot(local && rep == r0);
-        if ((int)(threadIdx.x & 63) == leader) atomicAdd(&w2[r0], (unsigned long long)__popcll(same));
-        pend &= ~same;
+        if (lane == leader) atomicAdd(&w2[r0], (unsigned long long)__popcll(same));
+        pw &= ~same;
     }
 }
 // the next state's tuples: resident tuples of kept reps (rep renumbered), then the new local

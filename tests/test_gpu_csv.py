@@ -84,7 +84,7 @@ def _check(eng, oracle, text, D, offset=0):
 @pytest.mark.parametrize("route", ["chunks", "groups"])
 @pytest.mark.parametrize("D", [1, 2, 4, 8])
 def test_csv_fuzz_matches_oracle(gpu_engine_factory, oracle, monkeypatch, D, route):
-    """Both parse routes: byte chunks (the default) and the group pass (SKY_CSV_CHUNKS=0)."""
+    """Both parse routes: the group route (the default, SKY_CSV_CHUNKS=0) and byte chunks (=1)."""
     monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
     rng = random.Random(100 + D)
     text = ("\n".join(_record(rng, D) for _ in range(20000))).encode()
@@ -211,7 +211,7 @@ print("ok")
 
 
 def test_csv_chunks_listed_spans(gpu_engine_factory, oracle, monkeypatch):
-    """Byte-chunk parse (the default; SKY_CSV_CHUNKS=0 is the group route): chunks sized from the text's average record, each
+    """Byte-chunk parse (SKY_CSV_CHUNKS=1; the default is the group route): chunks sized from the text's average record, each
     workgroup finding its own records; chunks that do not fit go to the fallback as spans: > 256
     record starts (tiny records), a record running past the staged tail (mid-text and the text's
     last, with and without a newline), > 2048 fields.  Same results as the group-pass parse."""

@@ -52,6 +52,28 @@ fi
 if [[ $STEPS == *mpmc* ]]; then
   TAG=$TAG NS="" KRE=k_mbr_pairs PMC_N=${PMC_N:-2000000} bash tools/gpu_mbr_pmc.sh
 fi
+if [[ $STEPS == *cpmc* ]]; then
+  # k_csv_fields (chunk route) on the C4 stream as producer text: instruction mix + HBM bytes
+  export TMPDIR=/tmp
+  i=0
+  for CS in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_WR" \
+            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAIT_INST_LDS" \
+            "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+    i=$((i+1))
+    rm -rf $OUT/pmc_csv_${TAG}_$i
+    timeout -s KILL 120 rocprofv3 --pmc $CS --kernel-include-regex "k_csv_fields" -f csv -d $OUT/pmc_csv_${TAG}_$i -o run -- \
+        python3 -u $R/tools/csv_bench.py 20000000 > $OUT/pmc_csv_${TAG}_$i.log 2>&1 || { tail -20 $OUT/pmc_csv_${TAG}_$i.log; exit 1; }
+    python tools/prof_summary.py pmcshow $OUT/pmc_csv_${TAG}_$i "k_csv_fields" | tee -a $OUT/pmc_csv_${TAG}.txt
+  done
+fi
+if [[ $STEPS == *fpmc* ]]; then
+  bash tools/gpu_pmc.sh $TAG
+fi
+if [[ $STEPS == *rehearse* ]]; then
+  # two ranks on the one GPU over gloo (bench.py starts its own ranks): the per-step phase split
+  timeout -k 10 400 python -u bench.py --gpus 2 --steps 5 --warmup 2 > $OUT/rehearsal_$TAG.json 2> $OUT/rehearsal_$TAG.err || { tail -30 $OUT/rehearsal_$TAG.err; exit 1; }
+  cut -c1-600 $OUT/rehearsal_$TAG.json
+fi
 if [[ $STEPS == *csv* ]]; then
   for C in 1 0; do
     SKY_CSV_CHUNKS=$C timeout -k 10 240 python -u tools/csv_bench.py > $OUT/csv_${TAG}_$C.log 2>&1 || { tail -30 $OUT/csv_${TAG}_$C.log; exit 1; }
