@@ -108,7 +108,11 @@ __global__ void k_ls_set_ctr(const uint32_t *__restrict__ kept, uint32_t *__rest
 }
 // new rows in L_k: the rep of their (key, row), created when absent.  A row that loses the race
 // to publish a new vector keeps its reserved slot as an inert hole (key -1: dropped by the next
-// query, weight 0).  Tuple counts are added per wave for lanes that share a rep.
+// query, weight 0).  Reps below *kept were published by an earlier kernel (plain loads see them);
+// reps created by this kernel are read past the CU's L1.  Tuple counts: per wave for lanes that
+// share a rep, then per workgroup in an LDS table over its grid-stride rows, one global atomic per
+// (workgroup, rep) — the reference streams put most new local tuples on one vector.
+constexpr int kLsSlots = 64;
 __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uint32_t R,
                                                           const uint8_t *__restrict__ rowf,
                                                           const double *__restrict__ qrows,
@@ -116,8 +120,19 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
                                                           double *__restrict__ rows2, int32_t *__restrict__ key2,
                                                           unsigned long long *__restrict__ w2,
                                                           unsigned long long *__restrict__ table, uint32_t hmask,
+                                                          const uint32_t *__restrict__ kept,
                                                           uint32_t *__restrict__ ctr, uint32_t *__restrict__ newrep) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    __shared__ uint32_t s_rep[kLsSlots];
+    __shared__ unsigned long long s_cnt[kLsSlots];
+    if (threadIdx.x < kLsSlots) {
+        s_rep[threadIdx.x] = 0xffffffffu;
+        s_cnt[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint32_t base = __builtin_amdgcn_readfirstlane(kept[0]);
+    const int lane = (int)(threadIdx.x & 63);
+    for (uint32_t i0 = blockIdx.x * kThreads; i0 < N; i0 += gridDim.x * kThreads) {   // block-uniform
+    const uint32_t i = i0 + threadIdx.x;
     const bool local = i < N && (rowf[R + i] & 1u);
     const double *src = qrows + (size_t)(R + min(i, N - 1u)) * D;
     const int32_t k = local ? qkey[R + i] : 0;
@@ -141,8 +156,16 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
             }
             if ((uint32_t)(cur >> 32) == h) {
                 const uint32_t r2 = (uint32_t)cur;
-                if (__hip_atomic_load(key2 + r2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k &&
-                    same_row(rows2 + (size_t)r2 * D, src, D)) {
+                bool eq;
+                if (r2 < base) {                           // an earlier kernel's rep
+                    eq = key2[r2] == k;
+                    for (int d = 0; d < D; d++)
+                        eq &= __double_as_longlong(rows2[(size_t)r2 * D + d]) == __double_as_longlong(src[d]);
+                } else {
+                    eq = __hip_atomic_load(key2 + r2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k &&
+                         same_row(rows2 + (size_t)r2 * D, src, D);
+                }
+                if (eq) {
                     rep = r2;
                     break;
                 }
@@ -155,7 +178,6 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
     // holding the same (key, row) takes the leader's rep, so a vector repeated across the stream (the
     // zero vector of the reference streams) costs one table probe per wave, not one per tuple on
     // the same table slot
-    const int lane = (int)(threadIdx.x & 63);
     uint32_t rep = 0xffffffffu;
     bool done = !local;
     uint64_t pend = __ballot(local);
@@ -177,15 +199,25 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
     }
     if (!done) rep = lookup();
     if (local) newrep[i] = rep;
-    // tuple counts: one atomic per distinct rep of the wave
+    // tuple counts: per group of lanes sharing a rep, into the workgroup's table (or global)
     uint64_t pw = __ballot(local);
     while (pw) {
         const int leader = __ffsll((unsigned long long)pw) - 1;
         const uint32_t r0 = __shfl(rep, leader, 64);
         const uint64_t same = __ballot(local && rep == r0);
-        if (lane == leader) atomicAdd(&w2[r0], (unsigned long long)__popcll(same));
+        if (lane == leader) {
+            const uint32_t sl = r0 & (kLsSlots - 1);
+            uint32_t cur = s_rep[sl];
+            if (cur == 0xffffffffu) cur = atomicCAS(&s_rep[sl], 0xffffffffu, r0) == 0xffffffffu ? r0 : s_rep[sl];
+            if (cur == r0) atomicAdd(&s_cnt[sl], (unsigned long long)__popcll(same));
+            else atomicAdd(&w2[r0], (unsigned long long)__popcll(same));
+        }
         pw &= ~same;
     }
+    }                                                      // next rows of this workgroup
+    __syncthreads();
+    if (threadIdx.x < kLsSlots && s_rep[threadIdx.x] != 0xffffffffu)
+        atomicAdd(&w2[s_rep[threadIdx.x]], s_cnt[threadIdx.x]);
 }
 // the next state's tuples: resident tuples of kept reps (rep renumbered), then the new local
 // tuples with their reps, arrival order kept
@@ -461,10 +493,10 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     }
     sky::k_ls_set_ctr<<<1, 64, 0, st>>>(w + 1, w + 2);
     if (N)
-        sky::k_ls_new_reps<<<sky::nblk(N), sky::kThreads, 0, st>>>(
+        sky::k_ls_new_reps<<<std::min<unsigned>(sky::nblk(N), 1024u), sky::kThreads, 0, st>>>(
             D, N, R, L.rowf.as<uint8_t>(), L.qrows.as<double>(), L.qkey.as<int32_t>(), L.rows2.as<double>(),
-            L.key2.as<int32_t>(), L.w2.as<unsigned long long>(), L.table.as<unsigned long long>(), hcap - 1, w + 2,
-            L.newrep.as<uint32_t>());
+            L.key2.as<int32_t>(), L.w2.as<unsigned long long>(), L.table.as<unsigned long long>(), hcap - 1, w + 1,
+            w + 2, L.newrep.as<uint32_t>());
     if (TN) {
         sky::k_ls_select<<<sky::nblk(TN), sky::kThreads, 0, st>>>(T, N, R, L.trep.as<uint32_t>(), L.rowf.as<uint8_t>(),
                                                                   1u, L.flag.as<uint32_t>());
