@@ -24,6 +24,10 @@
 #include <cstdlib>
 #include <vector>
 
+namespace sky {
+size_t mbr_group_slots(uint32_t mr);   // k_mbr.hip: gmin / gprange entries (groups + super-groups)
+}
+
 namespace {
 
 // pair tests below which the own-vs-union fates run as one pair kernel over the blocks
@@ -133,8 +137,8 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     SKY_TRY(p.mbr_max.ensure((xt + yt) * NW * 4));
     SKY_TRY(p.mbr_pr.ensure((xt + yt) * 4));
     SKY_TRY(p.mbr_sub.ensure((xt + yt) * kMbrSubMax * NW * 4));
-    SKY_TRY(p.mbr_gmin.ensure(mbr_groups(n_union) * NW * 4));
-    SKY_TRY(p.mbr_gpr.ensure(mbr_groups(n_union) * 4));
+    SKY_TRY(p.mbr_gmin.ensure(mbr_group_slots(n_union) * NW * 4));
+    SKY_TRY(p.mbr_gpr.ensure(mbr_group_slots(n_union) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)n_own * 4));
     SKY_TRY(p.mbr_pairs.ensure(16));
     SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(yt) * 4));

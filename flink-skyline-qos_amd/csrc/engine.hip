@@ -19,6 +19,8 @@
 
 namespace sky {
 
+size_t mbr_group_slots(uint32_t mr);   // k_mbr.hip: gmin / gprange entries (groups + super-groups)
+
 #define HIP_TRY(expr)                                                                     \
     do {                                                                                  \
         hipError_t e_ = (expr);                                                           \
@@ -678,8 +680,8 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_max.ensure(ntiles * NW * 4));
     SKY_TRY(p.mbr_pr.ensure(ntiles * 4));
     SKY_TRY(p.mbr_sub.ensure(ntiles * kMbrSubMax * NW * 4));
-    SKY_TRY(p.mbr_gmin.ensure(mbr_groups(mr) * NW * 4));
-    SKY_TRY(p.mbr_gpr.ensure(mbr_groups(mr) * 4));
+    SKY_TRY(p.mbr_gmin.ensure(mbr_group_slots(mr) * NW * 4));
+    SKY_TRY(p.mbr_gpr.ensure(mbr_group_slots(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
     SKY_TRY(p.mbr_pairs.ensure(64));
     SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(ntiles) * 4));

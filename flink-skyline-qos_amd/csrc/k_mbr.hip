@@ -651,7 +651,22 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
         __builtin_amdgcn_wave_barrier();
     };
 
-    for (uint32_t s0 = gs_lo; s0 < gs_hi && live; s0 += 64) {
+    // super-groups of 64 groups first (their min corners follow the groups' in gmin): a super-group
+    // whose corner is not <= the y tile's max corner holds no reachable group, and is skipped whole
+    const uint32_t nsup = (ngroups + kMbrG - 1) / kMbrG;
+    const uint32_t *sgmin = gmin + (size_t)NW * ngroups;
+    for (uint32_t u0 = 0; u0 < nsup && live; u0 += 64) {
+    uint64_t sm;
+    {
+        const uint32_t q = min(u0 + lane, nsup - 1u);
+        uint32_t sc[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) sc[w] = sgmin[(size_t)w * nsup + q];
+        sm = __ballot(u0 + lane < nsup && R::le(sc, ymax));
+    }
+    while (sm && live) {
+        const uint32_t s0 = (u0 + (uint32_t)__builtin_ctzll(sm)) * 64;
+        sm &= sm - 1;
         uint64_t gm;
         {
             const uint32_t q = min(s0 + lane, ngroups - 1u);
@@ -705,6 +720,7 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
             }
         }
     }
+    }                                               // the next reachable super-group
     if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
     if (trace && lane == 0) {
         trace[4 * (size_t)witem] = t_start;
@@ -755,6 +771,11 @@ static int mbr_bits(int D) {
 
 size_t mbr_tiles(uint32_t mr) { return (mr + kMbrT - 1) / kMbrT; }
 size_t mbr_groups(uint32_t mr) { return (mbr_tiles(mr) + kMbrG - 1) / kMbrG; }
+// words per row-word of gmin (and entries of gprange): the groups, then their super-groups of 64
+size_t mbr_group_slots(uint32_t mr) {
+    const size_t g = mbr_groups(mr);
+    return g + (g + kMbrG - 1) / kMbrG;
+}
 
 // Hilbert order + 64-row tiles (+ groups of 64 tiles) of one row set; returns the sorted order
 template <class R, int D>
@@ -777,6 +798,9 @@ static const uint32_t *mbr_build(const uint32_t *rows, const uint64_t *rep_key, 
     if (gmin) {
         const uint32_t ngroups = (uint32_t)mbr_groups(mr);
         k_mbr_groups<R><<<(ngroups + 3) / 4, kThreads, 0, st>>>(tmin, tprange, ntiles, ngroups, gmin, gprange);
+        const uint32_t nsup = (ngroups + kMbrG - 1) / kMbrG;   // the same reduction over the groups
+        k_mbr_groups<R><<<(nsup + 3) / 4, kThreads, 0, st>>>(gmin, gprange, ngroups, nsup,
+                                                             gmin + (size_t)R::NW * ngroups, gprange + ngroups);
     }
     return perm;
 }
