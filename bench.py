@@ -395,7 +395,7 @@ def csv_ingest_run(eng, ids, vals, n, D, steps, out_ids, out_org):
     k_ms = sum(kt[k][0] / max(kt[k][1], 1) for k in kt)
     del text, pi, pv
     achieved = alg / (p_ms / 1e3) / 1e9
-    return {"bound": "hbm", "kernel": "k_csv_fields (+ k_csv_nl_count, its scan, k_csv_nl_groups)",
+    return {"bound": "hbm", "kernel": "k_csv_fields (+ k_csv_nl_count, its scan, k_csv_group_pos)",
             "workload": f"C4 stream as producer CSV text, {n} records, {nb} bytes",
             "text_bytes": nb, "records": m,
             "decode_ms": dt_parse * 1e3, "kernels_ms": k_ms,
