@@ -144,6 +144,20 @@ def test_csv_producer_shape_mixed(gpu_engine_factory, oracle, monkeypatch, D, ra
 
 
 @pytest.mark.parametrize("route", ["chunks", "groups"])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 256, 257, 20000, 65537])
+def test_csv_block_aligned_records(gpu_engine_factory, oracle, monkeypatch, route, n):
+    """16-byte records: every '\n' is the last byte of a 16-byte unit, so group ends fall exactly on
+    1 KB / 4 KB count-block boundaries (k_csv_group_pos picks the quarter by its count), and the
+    record counts straddle the group size."""
+    monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
+    text = "".join("%08d,%06d\n" % (i, (i * 7919) % 1000000) for i in range(n)).encode()
+    assert len(text) == 16 * n
+    eng = gpu_engine_factory(1, 8)
+    assert _check(eng, oracle, text, 1) == n
+    eng.close()
+
+
+@pytest.mark.parametrize("route", ["chunks", "groups"])
 @pytest.mark.parametrize("offset", [1, 2, 3, 5])
 def test_csv_unaligned_buffer(gpu_engine_factory, oracle, monkeypatch, offset, route):
     monkeypatch.setenv("SKY_CSV_CHUNKS", "1" if route == "chunks" else "0")
