@@ -490,7 +490,7 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 //    read back once per tile to retire the y's a rep of their own partition dominates.
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
 template <class R, bool FULL, bool GM>
-__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
                                                          const uint32_t *__restrict__ tprange,
@@ -530,6 +530,11 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
     }
 #pragma unroll
     for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
+    // the tile's static max corner: what decides which split item owns which group (mbr_share),
+    // whatever the items' live lanes do; ymax itself shrinks with the live y's (refresh_ymax)
+    uint32_t ymax0[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) ymax0[w] = ymax[w];
     const uint32_t yr = ys.tprange[yt];
     const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
     const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
@@ -562,6 +567,28 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
             xv[4 * q + 3] = v.w;
         }
         px = tpart[xi];
+    };
+    // the live y's max corner: as y's are retired (a rep of their own partition dominates them) the
+    // box the x scan tests against shrinks; recomputed (wave max) when live changed since
+    uint64_t live_ymax = live;
+    auto refresh_ymax = [&]() {
+        if (live == live_ymax) return;
+        live_ymax = live;
+        uint32_t m[NW];
+        R::ident_max(m);
+        if ((live >> lane) & 1ull) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) m[w] = y[w];
+        }
+#pragma unroll
+        for (int o = 1; o <= 32; o <<= 1) {
+            uint32_t b[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) b[w] = (uint32_t)__shfl_xor((int)m[w], o, 64);
+            R::cmax(m, b);
+        }
+#pragma unroll
+        for (int w = 0; w < NW; w++) ymax[w] = (uint32_t)__builtin_amdgcn_readfirstlane((int)m[w]);
     };
     uint32_t tg[NW];                                // min corners of the group's tiles (lane = tile)
     // the next tile of the group (bits tm) whose whole min corner is <= some live y (the corner
@@ -662,11 +689,12 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
         uint32_t sc[NW];
 #pragma unroll
         for (int w = 0; w < NW; w++) sc[w] = sgmin[(size_t)w * nsup + q];
-        sm = __ballot(u0 + lane < nsup && R::le(sc, ymax));
+        sm = __ballot(u0 + lane < nsup && R::le(sc, parts == 1 ? ymax : ymax0));   // shares count static groups
     }
     while (sm && live) {
         const uint32_t s0 = (u0 + (uint32_t)__builtin_ctzll(sm)) * 64;
         sm &= sm - 1;
+        refresh_ymax();
         uint64_t gm;
         {
             const uint32_t q = min(s0 + lane, ngroups - 1u);
@@ -675,8 +703,8 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
             for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
             const uint32_t gr = gprange[q];
             const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax);
-            bool cand = reach;
+            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax0);
+            bool cand = reach && R::le(gc, ymax);
             if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
             gm = __ballot(cand) & mbr_share(__ballot(reach), gord, part, parts);
         }
@@ -684,6 +712,7 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
         while (gm && live) {
             const uint32_t g = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
             gm &= gm - 1;
+            refresh_ymax();
             uint64_t tm;
             {
                 const uint32_t t = min(g + lane, ntiles - 1u);
