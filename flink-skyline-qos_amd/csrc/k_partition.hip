@@ -1515,7 +1515,10 @@ void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
         return (unsigned)std::max(1, std::min(v, 64));
     }();
     const unsigned spans = nblk(a.n, kTile * kFilterFT);
-    const unsigned g = (spans + tpb - 1) / tpb;
+    // several tiles per workgroup only while the grid still holds >= 1024 workgroups (4 per CU): a
+    // 1M-tuple query (C1, a C5 trigger) has 489 tiles, which at 4 per workgroup left half the CUs idle
+    const unsigned tpe = std::max(1u, std::min(tpb, spans / 1024u));
+    const unsigned g = (spans + tpe - 1) / tpe;
     if (!g) return;
     if (a.given_keys) { SKY_DISPATCH_D(D, (k_filter<DD, true><<<g, kThreads, lds, st>>>(a))); }
     else { SKY_DISPATCH_D(D, (k_filter<DD, false><<<g, kThreads, lds, st>>>(a))); }
