@@ -1606,7 +1606,8 @@ static void out_count_t(const OutArgs &a, hipStream_t st) {
 void launch_out_count(const OutArgs &a, hipStream_t st) {
     if (!a.n) return;
     const int t = out_tpb();
-    if (t == 8) out_count_t<8>(a, st);
+    if (nblk(a.n, kTile) < 4u * 1024u) out_count_t<1>(a, st);   // < 1024 workgroups at 4 tiles: fill the GPU
+    else if (t == 8) out_count_t<8>(a, st);
     else if (t == 16) out_count_t<16>(a, st);
     else out_count_t<4>(a, st);
 }
