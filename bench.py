@@ -10,8 +10,9 @@ partition keys -> local skylines of the P partitions -> global merge -> stream-o
 skyline ids, inputs already resident in HBM.  With N GPUs (one process per GPU, launched
 by torch.distributed.run) every rank owns a shard; the ranks exchange their local
 skylines' distinct vectors with one RCCL all-gather and each rank filters ITS OWN
-vectors against the union (skyline/dist.py).  --scaling weak (default): N x 100M tuples;
---scaling strong: 100M tuples in total, split over the ranks.
+vectors against the union (skyline/dist.py).  --scaling strong (default, as BASELINE states
+C4: 100M tuples on 8 GPUs): 100M tuples in total, split over the ranks; --scaling weak: N x
+100M tuples.  With N > 1 the other mode is measured as well ("<mode>_scaling_companion").
 
 --config C1..C5 runs one BASELINE configuration as the headline line instead:
   C1 MR-Dim 2D uniform 1M P=8 | C2 MR-Grid 4D correlated 10M P=8 | C3 MR-Angle 4D anti 50M P=8
@@ -423,7 +424,7 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     eng.warmup()                                  # first launches / allocations, before the stream starts
     st = skyline.SkylineStream(eng, window)
     st.reserve(window if window else n)          # result buffers pinned once, before the stream starts
-    lat, sizes = [], []
+    lat_int, lat_ids, copy_ms, sizes = [], [], [], []
     eng.profile(1)                                # light timers only (the k_filter roofline)
     eng.profile_reset()
     t_start = time.perf_counter()
@@ -431,10 +432,18 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
         base = t * per_trigger
         for b0 in range(base, base + per_trigger, batch):
             st.append(ids[b0:b0 + batch], vals[b0:b0 + batch])
+            if b0 == base and t:
+                # the last trigger's ids reached host memory while this micro-batch went in
+                cm = st.wait()
+                copy_ms.append(cm)
+                lat_ids.append(lat_int[-1] + cm)
         tq = time.perf_counter()
-        g = st.query_host_view()
-        lat.append((time.perf_counter() - tq) * 1e3)
+        g = st.query_async_host_view()            # returns with the integers (skyline size, stats)
+        lat_int.append((time.perf_counter() - tq) * 1e3)
         sizes.append(g)
+    cm = st.wait()
+    copy_ms.append(cm)
+    lat_ids.append(lat_int[-1] + cm)
     total = time.perf_counter() - t_start
     eng.profile(False)
     roof = filter_roofline(eng, D)
@@ -443,13 +452,23 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     st.close()
     eng.close()
     rate = n / total
+    lat = lat_ids
     return {"workload": (f"C5: 6D mixed stream, MR-Angle P={P}, {batch}-tuple micro-batches from pinned host "
                          f"memory, query_trigger every {per_trigger} tuples, {triggers} triggers, "
                          + ("landmark window (reference semantics)" if window == 0
                             else f"count-based sliding window W={window} (extension)")),
             "ingest_tuples_per_s": rate, "sustains_10M_per_s": rate >= 1e7,
-            "p50_query_latency_ms": statistics.median(lat), "p90_query_latency_ms": sorted(lat)[int(0.9 * len(lat))],
-            "max_query_latency_ms": max(lat), "latencies_ms": [round(x, 3) for x in lat],
+            "latency_note": ("p50_query_latency_ms = trigger -> the reference's result integers (skyline_size, "
+                             "|L_k|, survivors_k: FlinkSkyline.java:593-608) on the host "
+                             "(sky_stream_query_async returns); ids_* = trigger -> every skyline id + origin in "
+                             "host memory = the integers' latency + the D2H copy's device time, the copy "
+                             "overlapping the next micro-batch's append"),
+            "p50_query_latency_ms": statistics.median(lat_int),
+            "p90_query_latency_ms": sorted(lat_int)[int(0.9 * len(lat_int))],
+            "max_query_latency_ms": max(lat_int), "latencies_ms": [round(x, 3) for x in lat_int],
+            "ids_p50_latency_ms": statistics.median(lat), "ids_p90_latency_ms": sorted(lat)[int(0.9 * len(lat))],
+            "ids_max_latency_ms": max(lat), "ids_latencies_ms": [round(x, 3) for x in lat],
+            "copy_ms": [round(x, 3) for x in copy_ms],
             "skyline_size_last": sizes[-1], "resident_tuples_last": resident,
             "resident_vectors_last": vectors,
             "resident_note": ("landmark: the local-skyline tuples kept (ids, arrival order) and the distinct "
@@ -691,8 +710,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C4", choices=["C1", "C2", "C3", "C4", "C5"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: --tuples per rank; strong: --tuples in total, split over the ranks")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default: BASELINE states each configuration's tuples in total, e.g. C4 = "
+                         "100M tuples on 8 GPUs): --tuples in total, split over the ranks; weak: --tuples per "
+                         "rank.  With N > 1 the other one is measured too, as a labelled companion key")
+    ap.add_argument("--no-companion-scaling", action="store_true",
+                    help="N > 1: skip the companion measurement of the other scaling mode")
     ap.add_argument("--tuples", type=int, default=None, help="override the config's tuple count")
     ap.add_argument("--dist", default=None, help="override the config's distribution (e.g. std_anti)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -757,41 +780,64 @@ def main():
         cfg["dist"] = args.dist
     D, P = cfg["dims"], cfg["partitions"]
     n_cfg = args.tuples or cfg["tuples"]
-    if args.scaling == "strong":
-        lo, hi = rank * n_cfg // world, (rank + 1) * n_cfg // world
-        n, id0, total = hi - lo, lo, n_cfg
-    else:
-        n, id0, total = n_cfg, rank * n_cfg, n_cfg * world
     seed = 1234 + D
     eng = skyline.SkylineEngine(D, P, cfg["algo"], 1000.0, dev_index)
-    vals, ids = make_stream(eng, cfg["dist"], n, seed, id0, dev)
-    out_ids = torch.empty(n, dtype=torch.int64, device=dev)
-    out_org = torch.empty(n, dtype=torch.int32, device=dev)
 
-    dist_phase_log = []
+    def shard(mode):
+        """(tuples on this rank, first id, tuples in the whole job) of a scaling mode."""
+        if mode == "strong":
+            lo, hi = rank * n_cfg // world, (rank + 1) * n_cfg // world
+            return hi - lo, lo, n_cfg
+        return n_cfg, rank * n_cfg, n_cfg * world
 
-    def step():
+    def measure(mode):
+        """W + K steps of one scaling mode; every rank's elapsed / p50 reduced by MAX."""
+        n, id0, total = shard(mode)
+        vals, ids = make_stream(eng, cfg["dist"], n, seed, id0, dev)
+        out_ids = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        out_org = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        dist_phase_log = []
+
+        def step():
+            if distributed:
+                g = distributed_query(eng, ids, vals, out_ids, out_org, n)
+                dist_phase_log.append(eng.last_dist_phases)     # export / all-gather / merge / finish split
+                return g
+            return eng.query_dev(ids, vals, out_ids, out_org, n)
+
+        elapsed, step_ms, g, kt = time_steps(step, eng, args.steps, args.warmup, distributed)
+        p50 = statistics.median(step_ms)
         if distributed:
-            g = distributed_query(eng, ids, vals, out_ids, out_org, n)
-            dist_phase_log.append(eng.last_dist_phases)     # export / all-gather / merge / finish split
-            return g
-        return eng.query_dev(ids, vals, out_ids, out_org, n)
+            t = torch.tensor([elapsed, p50], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed, p50 = float(t[0].item()), float(t[1].item())
+            gt = torch.tensor([g], dtype=torch.int64, device=red_dev)
+            dist.all_reduce(gt)
+            g = int(gt.item())
+        dist_stats = getattr(eng, "last_dist_stats", None) if distributed else None
+        if dist_stats is not None:
+            # the timed steps' phase split (warm-up steps come first, the profiled step last), with
+            # the own-vs-union pass's kernel time on its own (union_pass_kernel_ms)
+            dist_stats = dict(dist_stats, phases_per_step=dist_phase_log[args.warmup:args.warmup + args.steps])
+        return dict(n=n, total=total, elapsed=elapsed, step_ms=step_ms, p50=p50, g=g, kt=kt, dist_stats=dist_stats,
+                    vals=vals, ids=ids, out_ids=out_ids, out_org=out_org)
 
-    elapsed, step_ms, g, kt = time_steps(step, eng, args.steps, args.warmup, distributed)
-    p50 = statistics.median(step_ms)
-    if distributed:
-        t = torch.tensor([elapsed, p50], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, p50 = float(t[0].item()), float(t[1].item())
-        gt = torch.tensor([g], dtype=torch.int64, device=red_dev)
-        dist.all_reduce(gt)
-        g = int(gt.item())
+    companion = None
+    if distributed and not args.no_companion_scaling:
+        other = "weak" if args.scaling == "strong" else "strong"
+        c = measure(other)
+        ms_c = c["elapsed"] * 1e3 / args.steps
+        companion = {"scaling": other, "value": c["total"] / (ms_c / 1e3), "unit": "tuples/s",
+                     "ms_per_step": ms_c, "p50_query_latency_ms": c["p50"], "tuples_per_gpu": c["n"],
+                     "tuples_total": c["total"], "skyline_size": c["g"], "dist_exchange": c["dist_stats"]}
+        del c
+        torch.cuda.empty_cache()
+    m = measure(args.scaling)
+    n, total, elapsed, step_ms, p50, g, kt = (m[k] for k in ("n", "total", "elapsed", "step_ms", "p50", "g", "kt"))
+    vals, ids, out_ids, out_org = m["vals"], m["ids"], m["out_ids"], m["out_org"]
+    dist_stats = m["dist_stats"]
     phases, counters = eng.phases()
     roof = filter_roofline(eng, D, kt)
-    dist_stats = getattr(eng, "last_dist_stats", None) if distributed else None
-    if dist_stats is not None:
-        # the timed steps' phase split (warm-up steps come first, the profiled step last)
-        dist_stats = dict(dist_stats, phases_per_step=dist_phase_log[args.warmup:args.warmup + args.steps])
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -855,6 +901,8 @@ def main():
             "dist_exchange": dist_stats,
             "cpu_baseline": cpu,
         }
+        if companion is not None:
+            line[f"{companion['scaling']}_scaling_companion"] = companion
         line.update(extra)
         print(json.dumps(line), flush=True)
     eng.close()

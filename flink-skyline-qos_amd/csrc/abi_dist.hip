@@ -427,7 +427,7 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
     // all-reduced words), so every rank returns the same one
     const int64_t route_miss = st[2 * K], merge_err = st[2 * K + 1];
     if ((any & kDistError) || merge_err > 0) {
-        set_error("a look-back exceeded its spin bound on some rank");
+        set_error("a look-back exceeded its spin bound, or the bounding-box pass's work queue overflowed, on some rank");
         return SKY_E_HIP;
     }
     if (any & kDistNaN) {

@@ -242,6 +242,11 @@ struct sky_stream {
     int64_t appended = 0;
     sky::DevBuf out_ids, out_org, nanflag;
     void *nan_host = nullptr;   // pinned word: the append's NaN admission flag
+    // sky_stream_query_async: the result copy to host memory on its own stream (overlaps the
+    // next appends on the context's stream); ev_ready / ev_done bracket it
+    hipStream_t cst = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    bool copy_pending = false;
     sky_stream() = default;
     sky_stream(const sky_stream &) = delete;
     sky_stream &operator=(const sky_stream &) = delete;

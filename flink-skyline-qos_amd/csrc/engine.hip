@@ -978,6 +978,10 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             set_error("a look-back (radix sort / output) exceeded its spin bound");
             return SKY_E_HIP;
         }
+        if (flags3 & kFlagMbrQueue) {
+            set_error("the bounding-box pass's work items outgrew their queue (k_mbr_order): no pass ran");
+            return SKY_E_HIP;
+        }
     }
     pick_dom_group(p, KM);
     p.dom_w = 0;

@@ -29,7 +29,7 @@ __global__ void k_plan_verdict(const uint32_t *__restrict__ tot, const uint32_t 
     const uint32_t f = *flags;
     uint32_t v = 0;
     if (f & kFlagNaN) v |= kDistNaN;
-    if (f & kFlagRadixSpin) v |= kDistError;
+    if (f & (kFlagRadixSpin | kFlagMbrQueue)) v |= kDistError;
     if (pc.planned) {
         const uint32_t m = tot[0], nps = tot[5];
         bool ok = (uint64_t)m + nps <= pc.cap;
@@ -367,9 +367,10 @@ void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, u
 }
 
 // merge-time errors into the all-reduced stat words: a look-back that exceeded its spin bound in
-// the union pass (flags, kFlagRadixSpin) -> err = 1 (every rank then returns SKY_E_HIP)
+// the union pass (flags, kFlagRadixSpin), or its work queue's overflow (kFlagMbrQueue) -> err = 1
+// (every rank then returns SKY_E_HIP)
 __global__ void k_dist_merge_err(const uint32_t *__restrict__ flags, unsigned long long *__restrict__ err) {
-    if (threadIdx.x == 0) *err = (flags[0] & kFlagRadixSpin) ? 1ull : 0ull;
+    if (threadIdx.x == 0) *err = (flags[0] & (kFlagRadixSpin | kFlagMbrQueue)) ? 1ull : 0ull;
 }
 void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st) {
     k_dist_merge_err<<<1, 64, 0, st>>>(flags, err);

@@ -398,9 +398,14 @@ __global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restric
 }
 
 // one workgroup: the split of every y tile, bucket counts of the items' costs (log2), offsets
-// heaviest bucket first, then every item to its slot; lpt[33] = the number of items
-__global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__restrict__ lpt) {
-    __shared__ uint32_t s_cnt[32], s_off[32];
+// heaviest bucket first, then every item to its slot; lpt[33] = the number of items.  qcap: the
+// items the queue holds (the host's mbr_items_max).  The split rule keeps the items within it;
+// should a rule change ever break that bound, nothing is written past the queue: the kernel
+// raises kFlagMbrQueue in *err, leaves the queue empty (the pair pass then does nothing) and the
+// host returns SKY_E_HIP for the query
+__global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t qcap, uint32_t *__restrict__ lpt,
+                                                    uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_cnt[32], s_off[32], s_over;
     if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     // the cost per item: total / max(nyt, 4096), rounded UP, so that the items
@@ -419,20 +424,23 @@ __global__ __launch_bounds__(1024) void k_mbr_order(uint32_t nyt, uint32_t *__re
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t o = 0;
+        unsigned long long o = 0;
         for (int b = 31; b >= 0; b--) {
-            s_off[b] = o;
+            s_off[b] = (uint32_t)min(o, 0xffffffffull);
             o += s_cnt[b];
         }
-        lpt[33] = o;
+        s_over = o > qcap ? 1u : 0u;
+        lpt[33] = o > qcap ? 0u : (uint32_t)o;
+        if (o > qcap) atomicOr(err, kFlagMbrQueue);
     }
     __syncthreads();
+    if (s_over) return;                            // nothing past the queue; no items at all
     uint32_t *items = lpt + kMbrLptHead + nyt;
     for (uint32_t yt = threadIdx.x; yt < nyt; yt += 1024) {
         const uint32_t c = cost[yt], s = split(c);
         if (!s) continue;                          // no reachable group: nothing dominates its rows
         const uint32_t o = atomicAdd(&s_off[31 - __clz((c + s - 1) / s)], s);
-        for (uint32_t i = 0; i < s; i++) {
+        for (uint32_t i = 0; i < s && o + i < qcap; i++) {   // o + s <= total <= qcap here
             items[2 * (o + i)] = yt;
             items[2 * (o + i) + 1] = i | (s << 16);
         }
@@ -841,10 +849,19 @@ static unsigned mbr_pair_waves(uint32_t ytiles) {
 }
 
 // the work items of the pair pass, heaviest first (lpt: kMbrLptHead words zeroed by the caller)
+// the queue's capacity in items: what mbr_lpt_words sized (SKY_MBR_QCAP, measurement builds only,
+// shrinks it: the overflow test)
+static uint32_t mbr_qcap(uint32_t ytiles) {
+    const size_t cap = mbr_items_max(ytiles);
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_QCAP");
+    return (uint32_t)(e ? std::min<size_t>(cap, strtoull(e, nullptr, 10)) : cap);
+}
+
 template <class R>
-static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, hipStream_t st) {
+static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, uint32_t *err,
+                      hipStream_t st) {
     k_mbr_cost<typename R::Pair><<<(ys.ntiles + kThreads - 1) / kThreads, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
-    k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, lpt);
+    k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, mbr_qcap(ys.ntiles), lpt, err);
 }
 
 template <class R, int D>
@@ -857,7 +874,7 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
                                            a.tprange, a.tsub, a.gmin, a.gprange, st, lerr);
     const unsigned gp = mbr_pair_waves(ntiles);
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
-    mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, st);
+    mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, a.err, st);
 #define SKY_MBR_PAIRS(F, G)                                                                                  \
     k_mbr_pairs<typename R::Pair, F, G><<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
                                                   a.gprange, mr, ntiles, ys, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
@@ -906,7 +923,7 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     const uint32_t nyt = (uint32_t)mbr_tiles(y.mr);
     const unsigned gp = mbr_pair_waves(nyt);
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
-    mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, st);
+    mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, y.err, st);
     k_mbr_pairs<typename R::Pair, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, x.dbg,
                                                         y.domf, x.pairs, y.lpt, nullptr);

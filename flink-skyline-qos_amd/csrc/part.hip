@@ -687,10 +687,17 @@ int sky_global_merge_reps(sky_ctx *c, int nlists, const int32_t *part_ids, const
     for (int g = 0; g < nlists; g++) {
         R[g] = (uint32_t)nreps[g];
         T[g] = (uint32_t)counts[g];
+        // the reps' tuple counts are the pipeline's weights (|L_k| = counts[g], survivors_k = the
+        // weight of the surviving reps): each >= 1 and together exactly the list's tuples, or
+        // sky_global_stats could report survivors above the local size
+        int64_t wsum = 0;
         for (uint32_t r = 0; r < R[g]; r++) {
+            ARG_CHECK(rep_counts[g][r] >= 1, "rep_counts: a distinct vector must carry at least one tuple");
+            wsum += rep_counts[g][r];
             w[roff + r] = rep_counts[g][r];
             org[roff + r] = g;
         }
+        ARG_CHECK(wsum == counts[g], "rep_counts of a list must sum to its tuple count");
         if (R[g]) HIP_TRY(hipMemcpyAsync(c->h_vals.as<double>() + roff * D, reps[g], (size_t)R[g] * D * 8,
                                          hipMemcpyHostToDevice, st));
         int64_t *d_ids = c->pgm_up.as<int64_t>() + toff;

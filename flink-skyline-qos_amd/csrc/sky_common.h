@@ -25,6 +25,7 @@ constexpr uint32_t kFlagNaN = 2u;             // a NaN was seen
 constexpr uint32_t kFlagScoreTies = 4u;       // score key is not strictly monotone
 constexpr uint32_t kFlagRadixSpin = 16u;      // a radix look-back hit its spin bound (result invalid)
 constexpr uint32_t kFlagNotU16 = 8u;          // some candidate value is not an integer in [0, 65535]
+constexpr uint32_t kFlagMbrQueue = 32u;       // the pair pass's work items outgrew their queue (no pass ran: invalid)
 
 // padded row width in elements so every row starts 16-byte aligned
 template <typename T>

@@ -102,9 +102,12 @@ __global__ __launch_bounds__(kThreads) void k_ls_rep_keep(int D, uint32_t R, con
     for (uint32_t s = h & hmask;; s = (s + 1) & hmask)
         if (atomicCAS(&table[s], kHashEmpty, v) == kHashEmpty) break;
 }
-// the next rep count starts at the kept reps' count
+// the next rep count starts at the kept reps' count; the hole count (ctr[2]) at zero
 __global__ void k_ls_set_ctr(const uint32_t *__restrict__ kept, uint32_t *__restrict__ ctr) {
-    if (threadIdx.x == 0) ctr[0] = kept[0];
+    if (threadIdx.x == 0) {
+        ctr[0] = kept[0];
+        ctr[2] = 0u;
+    }
 }
 // new rows in L_k: the rep of their (key, row), created when absent.  A row that loses the race
 // to publish a new vector keeps its reserved slot as an inert hole (key -1: dropped by the next
@@ -121,7 +124,8 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
                                                           unsigned long long *__restrict__ w2,
                                                           unsigned long long *__restrict__ table, uint32_t hmask,
                                                           const uint32_t *__restrict__ kept,
-                                                          uint32_t *__restrict__ ctr, uint32_t *__restrict__ newrep) {
+                                                          uint32_t *__restrict__ ctr, uint32_t *__restrict__ holes,
+                                                          uint32_t *__restrict__ newrep) {
     __shared__ uint32_t s_rep[kLsSlots];
     __shared__ unsigned long long s_cnt[kLsSlots];
     if (threadIdx.x < kLsSlots) {
@@ -171,7 +175,10 @@ __global__ __launch_bounds__(kThreads) void k_ls_new_reps(int D, uint32_t N, uin
                 }
             }
         }
-        if (mine != 0xffffffffu && mine != rep) key2[mine] = -1;   // lost the race: an inert hole
+        if (mine != 0xffffffffu && mine != rep) {   // lost the race: an inert hole, counted
+            key2[mine] = -1;
+            atomicAdd(holes, 1u);
+        }
         return rep;
     };
     // duplicates first resolved inside the wave: up to two leaders look their row up and every lane
@@ -496,7 +503,7 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
         sky::k_ls_new_reps<<<std::min<unsigned>(sky::nblk(N), 1024u), sky::kThreads, 0, st>>>(
             D, N, R, L.rowf.as<uint8_t>(), L.qrows.as<double>(), L.qkey.as<int32_t>(), L.rows2.as<double>(),
             L.key2.as<int32_t>(), L.w2.as<unsigned long long>(), L.table.as<unsigned long long>(), hcap - 1, w + 1,
-            w + 2, L.newrep.as<uint32_t>());
+            w + 2, w + 4, L.newrep.as<uint32_t>());
     if (TN) {
         sky::k_ls_select<<<sky::nblk(TN), sky::kThreads, 0, st>>>(T, N, R, L.trep.as<uint32_t>(), L.rowf.as<uint8_t>(),
                                                                   1u, L.flag.as<uint32_t>());
@@ -509,18 +516,18 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
         HIP_TRY(hipMemsetAsync(w + 3, 0, 4, st));
     }
     HIP_TRY(hipGetLastError());
-    uint32_t h[4] = {};
+    uint32_t h[8] = {};
     c->host_syncs++;
-    HIP_TRY(hipMemcpyAsync(h, w, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h, w, 32, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    // swap in the next state: reps (with holes) [0, h[2]), tuples [0, h[3]), no new rows
+    // swap in the next state: reps (with h[4] holes) [0, h[2]), tuples [0, h[3]), no new rows
     std::swap(L.qrows, L.rows2);
     std::swap(L.qkey, L.key2);
     std::swap(L.qw, L.w2);
     std::swap(L.tid, L.tid2);
     std::swap(L.trep, L.trep2);
     L.R = h[2];
-    L.holes = (int64_t)h[2] - (int64_t)h[1];
+    L.holes = N ? (int64_t)h[4] : 0;        // the race losers of k_ls_new_reps (w[4] is zeroed with w[2])
     L.N = 0;
     L.T = h[3];
     s->n = L.T;
@@ -558,9 +565,28 @@ int stream_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64
     return SKY_OK;
 }
 
+// a result copy still in flight (sky_stream_query_async): wait for it on the host
+int stream_drain(sky_stream *s, double *copy_ms) {
+    if (copy_ms) *copy_ms = 0.0;
+    if (!s->copy_pending) return SKY_OK;
+    s->copy_pending = false;
+    HIP_TRY(hipEventSynchronize(s->ev_done));
+    if (copy_ms) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev_ready, s->ev_done));
+        *copy_ms = ms;
+    }
+    return SKY_OK;
+}
+
 }  // namespace
 
-sky_stream::~sky_stream() { delete lm; }
+sky_stream::~sky_stream() {
+    delete lm;
+    if (ev_ready) hipEventDestroy(ev_ready);
+    if (ev_done) hipEventDestroy(ev_done);
+    if (cst) hipStreamDestroy(cst);
+}
 
 extern "C" {
 
@@ -580,6 +606,7 @@ int sky_stream_destroy(sky_stream *s) {
     if (!s) return SKY_OK;
     hipSetDevice(s->ctx->dev);
     hipStreamSynchronize(s->ctx->st);
+    stream_drain(s, nullptr);
     if (s->nan_host) hipHostFree(s->nan_host);
     delete s;
     return SKY_OK;
@@ -596,6 +623,7 @@ int sky_stream_reserve(sky_stream *s, int64_t tuples) {
     ARG_CHECK(tuples >= 0 && tuples < (int64_t)0x3fffffffLL, "tuples out of range");
     sky_ctx *c = s->ctx;
     SKY_TRY(bind(c));
+    SKY_TRY(stream_drain(s, nullptr));      // a result copy in flight reads out_ids / out_org
     const size_t m = (size_t)std::max<int64_t>(tuples, 1);
     if (s->window == 0) {
         // rows: at most every appended tuple between two queries plus the reps; tuples: all of them
@@ -629,6 +657,7 @@ int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_ou
     GUARD_BEGIN
     ARG_CHECK(s && n_out, "null argument");
     SKY_TRY(bind(s->ctx));
+    SKY_TRY(stream_drain(s, nullptr));
     SKY_TRY(stream_query(s, d_ids_out, d_origin_out, cap, n_out));
     HIP_TRY(hipStreamSynchronize(s->ctx->st));
     if (*n_out > cap && (d_ids_out || d_origin_out)) {
@@ -643,6 +672,7 @@ int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64
     ARG_CHECK(s && n_out, "null argument");
     sky_ctx *c = s->ctx;
     SKY_TRY(bind(c));
+    SKY_TRY(stream_drain(s, nullptr));
     const size_t m = (size_t)std::max<int64_t>(s->n, 1);
     SKY_TRY(s->out_ids.ensure(m * 8));
     SKY_TRY(s->out_org.ensure(m * 4));
@@ -658,6 +688,50 @@ int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64
     if (g && origin_out)
         HIP_TRY(hipMemcpyAsync(origin_out, s->out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_stream_query_async(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out) {
+    GUARD_BEGIN
+    ARG_CHECK(s && n_out, "null argument");
+    sky_ctx *c = s->ctx;
+    SKY_TRY(bind(c));
+    SKY_TRY(stream_drain(s, nullptr));      // the last result copy reads the staging buffers
+    if (!s->cst) {
+        HIP_TRY(hipStreamCreateWithFlags(&s->cst, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreate(&s->ev_ready));
+        HIP_TRY(hipEventCreate(&s->ev_done));
+    }
+    const size_t m = (size_t)std::max<int64_t>(s->n, 1);
+    SKY_TRY(s->out_ids.ensure(m * 8));
+    SKY_TRY(s->out_org.ensure(m * 4));
+    int64_t g = 0;
+    // the query ends with its own read (the integers, the next state's counts): when it returns,
+    // *n_out and sky_global_stats hold the reference's result (FlinkSkyline.java:593-608)
+    SKY_TRY(stream_query(s, s->out_ids.as<int64_t>(), s->out_org.as<int32_t>(), (int64_t)m, &g));
+    *n_out = g;
+    if (g > cap && (ids_out || origin_out)) {
+        HIP_TRY(hipStreamSynchronize(c->st));
+        set_error("output capacity too small");
+        return SKY_E_CAPACITY;
+    }
+    HIP_TRY(hipEventRecord(s->ev_ready, c->st));
+    HIP_TRY(hipStreamWaitEvent(s->cst, s->ev_ready, 0));
+    if (g && ids_out) HIP_TRY(hipMemcpyAsync(ids_out, s->out_ids.p, (size_t)g * 8, hipMemcpyDeviceToHost, s->cst));
+    if (g && origin_out)
+        HIP_TRY(hipMemcpyAsync(origin_out, s->out_org.p, (size_t)g * 4, hipMemcpyDeviceToHost, s->cst));
+    HIP_TRY(hipEventRecord(s->ev_done, s->cst));
+    s->copy_pending = true;
+    return SKY_OK;
+    GUARD_END
+}
+
+int sky_stream_wait(sky_stream *s, double *copy_ms) {
+    GUARD_BEGIN
+    ARG_CHECK(s, "null stream");
+    SKY_TRY(bind(s->ctx));
+    SKY_TRY(stream_drain(s, copy_ms));
     return SKY_OK;
     GUARD_END
 }

@@ -95,6 +95,8 @@ SIGNATURES = {
     "sky_stream_reserve": [c_p, c_i64],
     "sky_stream_query": [c_p, c_p, c_p, c_i64, P_i64],
     "sky_stream_query_dev": [c_p, c_p, c_p, c_i64, P_i64],
+    "sky_stream_query_async": [c_p, c_p, c_p, c_i64, P_i64],
+    "sky_stream_wait": [c_p, P_dbl],
     "sky_synth_dev": [c_p, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_synth": [c_int, c_int, c_int, c_int, ctypes.c_uint64, c_i64, c_i64, c_p, c_p],
     "sky_dev_alloc": [c_p, c_i64, ctypes.POINTER(c_p)],

@@ -167,6 +167,10 @@ def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, out_cap, g
     h0 = engine.host_syncs()
     export = True
     clock = _PhaseClock(d_vals.is_cuda)
+    # the own-vs-union pass's kernels alone (HIP events around them inside sky_dist_merge_dev;
+    # on at engine.profile(1) and above): separates the merge kernels from whatever else shares
+    # the GPU in a rehearsal with several ranks on one device
+    u0 = engine.kernel_time("union_fate")[0] if d_vals.is_cuda else 0.0
     for attempt in range(max_attempts):
         clock.mark("start")
         if export:
@@ -183,6 +187,8 @@ def distributed_query(engine, d_ids, d_vals, d_ids_out, d_origin_out, out_cap, g
         rc, g, need = engine.dist_finish(ex.stats, out_cap)
         clock.mark("finish")
         engine.last_dist_phases = clock.split(attempt + 1)
+        if d_vals.is_cuda:
+            engine.last_dist_phases["union_pass_kernel_ms"] = round(engine.kernel_time("union_fate")[0] - u0, 4)
         if rc == _SKY_OK:
             _, cnt = engine.phases()
             engine.last_dist_stats = {

@@ -393,6 +393,24 @@ class SkylineStream:
         check(lib().sky_stream_query(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
         return g.value
 
+    def query_async_host_view(self):
+        """sky_stream_query_async into the reusable page-locked buffers: returns g as soon as the
+        integers are known (skyline size, engine.stats()); the ids / origins land in view()[:g]
+        while the caller goes on appending -- valid after wait()."""
+        r, _ = self.size()
+        cap = max(r, 1)
+        ids, org = self._out(cap)
+        g = ctypes.c_int64(0)
+        check(lib().sky_stream_query_async(self.h, _ptr(ids), _ptr(org), cap, ctypes.byref(g)))
+        return g.value
+
+    def wait(self):
+        """Waits for the result copy of the last query_async_host_view; returns its device time
+        (ms, from the end of the query's kernels to the last byte in host memory), 0 if none."""
+        ms = ctypes.c_double(0)
+        check(lib().sky_stream_wait(self.h, ctypes.byref(ms)))
+        return ms.value
+
     def view(self):
         return self._ids, self._org
 

@@ -218,6 +218,16 @@ int sky_stream_vectors(sky_stream *s, int64_t *vectors);
 int sky_stream_query(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
 int sky_stream_query_dev(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t cap,
                          int64_t *n_out);
+/* The reference's query result is its integers (skyline_size, |L_k|, survivors_k:
+ * FlinkSkyline.java:593-608, the JSON of :631-648).  sky_stream_query_async returns as soon as
+ * they are known (*n_out, sky_global_stats) and leaves the copy of the ids / origins into
+ * ids_out / origin_out in flight on a copy stream of its own, where it overlaps the next
+ * appends (give page-locked host memory for an asynchronous copy).  The host arrays are valid
+ * after sky_stream_wait (every later query and sky_stream_destroy wait too); *copy_ms
+ * (optional): the copy's device time, from the end of the query's kernels to the last byte in
+ * host memory. */
+int sky_stream_query_async(sky_stream *s, int64_t *ids_out, int32_t *origin_out, int64_t cap, int64_t *n_out);
+int sky_stream_wait(sky_stream *s, double *copy_ms);
 
 /* ---- multi-GPU step with one host read (one process per GPU) --------------------
  * The reference scales out by Flink's keyBy shuffle and one global reducer per query

@@ -387,10 +387,14 @@ public final class HipSkylineOperators {
             long[] gids = new long[Math.max(total, 1)];
             int[] gorg = new int[Math.max(total, 1)];
             final int g = SkylineHip.globalMergeReps(ctx, partIds, ids, repIdx, reps, repCounts, gids, gorg);
-            long[] lsz = new long[np], surv = new long[np];
-            SkylineHip.globalStats(ctx, lsz, surv);           // indexed by list, like partIds
+            // the integers are indexed by list, like partIds; their count K comes from the library
+            final int K = SkylineHip.globalStats(ctx, null, null);
+            long[] lsz = new long[Math.max(K, 1)], surv = new long[Math.max(K, 1)];
+            final int k2 = SkylineHip.globalStats(ctx, lsz, surv);
+            if (K < 0 || k2 != K)
+                throw new IllegalStateException("globalStats returned " + k2 + " (expected " + K + ")");
             double sum = 0.0;
-            for (int k = 0; k < np; k++)
+            for (int k = 0; k < Math.min(np, K); k++)
                 if (partIds[k] < totalPartitions && lsz[k] > 0) sum += (double) surv[k] / lsz[k];
             final double optimality = sum / totalPartitions;
             final long finish = System.currentTimeMillis();

@@ -66,6 +66,10 @@ public final class SkylineHip {
     /** globalMerge over partSnapshotReps messages: same ids, order, origins and stats. */
     public static native int globalMergeReps(long ctx, int[] partIds, long[][] ids, int[][] repIdx, double[][] reps,
                                              int[][] repCounts, long[] idsOut, int[] originOut);
+    /** The optimality integers of the last merge / query (FlinkSkyline.java:593-608), indexed like
+     *  its lists.  Returns K; with null arrays only K (size the arrays from it).  Arrays shorter
+     *  than K are left untouched and -K is returned: callers must treat a negative return as an
+     *  error. */
     public static native int globalStats(long ctx, long[] localSizes, long[] survivors);
 
     public static native int query(long ctx, long[] ids, double[] values, int n, long[] idsOut, int[] originOut);

@@ -478,12 +478,14 @@ out:
     return g;
 }
 
-/* the optimality integers (:593-608): returns K, fills |L_k| and survivors_k for k < K */
+/* the optimality integers (:593-608): returns K, fills |L_k| and survivors_k for k < K; with both
+ * arrays null it only returns K; arrays shorter than K: -K, nothing written */
 JNIEXPORT jint JNICALL Java_org_main_SkylineHip_globalStats(JNIEnv *env, jclass cls, jlong ctx,
                                                              jlongArray local_sizes, jlongArray survivors) {
     int32_t K = 0;
     if (fail(env, sky_global_stats(CTX(ctx), NULL, NULL, &K))) return 0;
-    if (!local_sizes || !survivors) { throw_arg(env, "globalStats: null array"); return 0; }
+    if (!local_sizes && !survivors) return K;
+    if (!local_sizes || !survivors) { throw_arg(env, "globalStats: one array null"); return 0; }
     if ((*env)->GetArrayLength(env, local_sizes) < K || (*env)->GetArrayLength(env, survivors) < K) return -K;
     jlong *ls = (*env)->GetLongArrayElements(env, local_sizes, NULL);
     jlong *sv = (*env)->GetLongArrayElements(env, survivors, NULL);

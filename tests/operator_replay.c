@@ -26,6 +26,8 @@
  *             then continues, and the answer must not change
  *
  * usage: operator_replay <csv file> <dims> <parallelism> <algo 0|1|2> [domain] [checkpoint C | -1] [G] [proto]
+ *        proto 0: distinct-vector messages; 1: ids + values messages; 2: as 0, plus empty messages of
+ *        the keys >= P the trigger does not reach (a merge whose stats K differs from P)
  * stdout: the JSON line, then "ids" and the sorted global skyline ids, then "lsz" / "surv";
  * stderr: "calls" -- the sky_parts_insert calls and their part counts (the call sequence).
  */
@@ -264,13 +266,23 @@ int main(int argc, char **argv) {
     }
     /* trigger "1,N" after the last tuple, broadcast to keys 0..P-1 (:145-157) */
     const int64_t dispatch = now_ms();
-    int32_t *part_ids = (int32_t *)malloc((size_t)P * 4);
-    int64_t **lid = (int64_t **)malloc((size_t)P * sizeof(int64_t *));
-    double **lval = (double **)malloc((size_t)P * sizeof(double *));
-    int32_t **lrep = (int32_t **)malloc((size_t)P * sizeof(int32_t *));
-    int32_t **lrc = (int32_t **)malloc((size_t)P * sizeof(int32_t *));
-    int64_t *lcnt = (int64_t *)malloc((size_t)P * 8), *lnr = (int64_t *)malloc((size_t)P * 8);
+    /* proto 2: the aggregator also receives empty messages of the keys the trigger does not reach
+     * (MR-Grid keys >= P): a merge over nl > P lists, whose sky_global_stats K is not P */
+    const int nl = proto == 2 ? kmax : P;
+    int32_t *part_ids = (int32_t *)malloc((size_t)nl * 4);
+    int64_t **lid = (int64_t **)calloc((size_t)nl, sizeof(int64_t *));
+    double **lval = (double **)calloc((size_t)nl, sizeof(double *));
+    int32_t **lrep = (int32_t **)calloc((size_t)nl, sizeof(int32_t *));
+    int32_t **lrc = (int32_t **)calloc((size_t)nl, sizeof(int32_t *));
+    int64_t *lcnt = (int64_t *)calloc((size_t)nl, 8), *lnr = (int64_t *)calloc((size_t)nl, 8);
     int64_t total = 0;
+    for (int k = P; k < nl; k++) {   /* the untriggered keys' empty messages */
+        part_ids[k] = k;
+        lid[k] = (int64_t *)malloc(8);
+        lrep[k] = (int32_t *)malloc(4);
+        lval[k] = (double *)malloc((size_t)D * 8);
+        lrc[k] = (int32_t *)malloc(4);
+    }
     for (int k = 0; k < P; k++) {   /* processQuery: flush (drainFull first), then the local skyline message */
         keyed_state *s = &ks[k];
         drain_full(ks);
@@ -279,7 +291,7 @@ int main(int argc, char **argv) {
             s->n = 0;
         }
         int64_t m = 0, r = 0;
-        if (proto == 0) {
+        if (proto != 1) {
             CHECK(sky_part_sizes(s->part, &m, &r));
             lid[k] = (int64_t *)malloc((size_t)(m > 0 ? m : 1) * 8);
             lrep[k] = (int32_t *)malloc((size_t)(m > 0 ? m : 1) * 4);
@@ -303,20 +315,26 @@ int main(int argc, char **argv) {
     int64_t *gids = (int64_t *)malloc((size_t)(total > 0 ? total : 1) * 8);
     int32_t *gorg = (int32_t *)malloc((size_t)(total > 0 ? total : 1) * 4);
     int64_t g = 0;
-    if (proto == 0)
-        CHECK(sky_global_merge_reps(ctx, P, part_ids, (const int64_t *const *)lid, (const int32_t *const *)lrep, lcnt,
+    if (proto != 1)
+        CHECK(sky_global_merge_reps(ctx, nl, part_ids, (const int64_t *const *)lid, (const int32_t *const *)lrep, lcnt,
                                     (const double *const *)lval, (const int32_t *const *)lrc, lnr, gids, gorg, total,
                                     &g));
     else
         CHECK(sky_global_merge(ctx, P, part_ids, (const int64_t *const *)lid, (const double *const *)lval, lcnt, gids,
                                gorg, total, &g));
-    int64_t *lsz = (int64_t *)malloc((size_t)P * 8), *surv = (int64_t *)malloc((size_t)P * 8);
-    int32_t K = 0;
-    CHECK(sky_global_stats(ctx, lsz, surv, &K));
+    /* the integers' count K from the library (as HipSkylineOperators sizes its arrays), then the
+     * integers; indexed by list, like part_ids */
+    int32_t K = 0, K2 = 0;
+    CHECK(sky_global_stats(ctx, NULL, NULL, &K));
+    if (K < 0 || K < P) { fprintf(stderr, "sky_global_stats: K = %d\n", K); return 5; }
+    int64_t *lsz = (int64_t *)malloc((size_t)K * 8 + 8), *surv = (int64_t *)malloc((size_t)K * 8 + 8);
+    CHECK(sky_global_stats(ctx, lsz, surv, &K2));
+    if (K2 != K) { fprintf(stderr, "sky_global_stats: K changed %d -> %d\n", K, K2); return 5; }
+    fprintf(stderr, "stats K %d lists %d\n", K, nl);
     const int64_t finish = now_ms();
     double opt = 0.0;
-    for (int k = 0; k < P; k++)
-        if (lsz[k] > 0) opt += (double)surv[k] / (double)lsz[k];
+    for (int k = 0; k < (K < nl ? K : nl); k++)
+        if (part_ids[k] < P && lsz[k] > 0) opt += (double)surv[k] / (double)lsz[k];
     opt /= P;
     char ostr[64];
     java_format_4f(opt, ostr, sizeof ostr);
@@ -340,7 +358,7 @@ int main(int argc, char **argv) {
         free(ks[k].ids);
         free(ks[k].vals);
     }
-    for (int k = 0; k < P; k++) { free(lid[k]); free(lval[k]); free(lrep[k]); free(lrc[k]); }
+    for (int k = 0; k < nl; k++) { free(lid[k]); free(lval[k]); free(lrep[k]); free(lrc[k]); }
     CHECK(sky_ctx_destroy(ctx));
     free(ks); free(lid); free(lval); free(lrep); free(lrc); free(lcnt); free(lnr); free(part_ids); free(g_full); free(gids); free(gorg); free(lsz); free(surv);
     free(keys); free(ids); free(vals); free(text);

@@ -111,3 +111,39 @@ def test_mbr_equals_sfs_at_scale(dist, D, n, gpu_engine_factory, oracle, monkeyp
         res.append((ids, org, ls, sv))
     for a, b in zip(res[0], res[1]):
         np.testing.assert_array_equal(a, b)
+
+
+MEASURE_LIB = __import__("os").path.join(__import__("conftest").PKG, "build_measure", "libskyline_hip.so")
+_QCAP_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import skyline
+from skyline._abi import SkylineError
+n, D = 60000, 8
+vals, ids = skyline.synth_host("std_anti", D, n, seed=3)
+eng = skyline.SkylineEngine(D, 16, "mr-angle", 1000.0, 0)
+try:
+    eng.query(vals, ids)
+    print("NO-ERROR")
+except SkylineError as e:
+    print("CODE", e.code, str(e))
+"""
+
+
+def test_mbr_queue_overflow_is_an_error_not_a_fault():
+    """k_mbr_order guards its work queue on the device: with the queue's capacity forced tiny
+    (SKY_MBR_QCAP, a knob of the measurement build only) the query must come back as SKY_E_HIP
+    with a message -- no item written past the queue, no pair pass over a partial queue."""
+    import os
+    import subprocess
+    import sys
+    from conftest import PKG
+    if not os.path.exists(MEASURE_LIB):
+        pytest.fail("build_measure/libskyline_hip.so missing: __graft_entry__.build() builds it")
+    env = dict(os.environ, SKYLINE_HIP_LIB=MEASURE_LIB, SKY_MBR_QCAP="8", SKY_MBR="1", SKY_MBR_MIN="1",
+               SKY_BRUTE="0", SKY_PLAN="0")
+    r = subprocess.run([sys.executable, "-c", _QCAP_CHILD, PKG], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout.strip().splitlines()[-1]
+    assert out.startswith("CODE -2") and "work items outgrew their queue" in out, out

@@ -289,6 +289,22 @@ def test_parts_global_merge_edge_cases(gpu_engine_factory, oracle):
     with pytest.raises(SkylineError) as e:
         eng.global_merge_reps([0], [(r.ids, bad, r.reps, r.rep_counts)])
     assert e.value.code == -1
+    # malformed tuple counts per rep (the merge's weights): a zero / negative count, or counts
+    # that do not sum to the list's tuples, are argument errors (else survivors_k > |L_k|)
+    assert len(r.reps) >= 2
+    for mutate in ("zero", "negative", "sum"):
+        rc = r.rep_counts.copy()
+        if mutate == "zero":
+            rc[0] = 0
+        elif mutate == "negative":
+            rc[0], rc[1] = -rc[1], rc[0] + 2 * rc[1]        # the sum stays right
+        else:
+            rc[0] += 1
+        with pytest.raises(SkylineError) as e:
+            eng.global_merge_reps([0], [(r.ids, r.rep_idx, r.reps, rc)])
+        assert e.value.code == -1 and "rep_counts" in str(e.value), (mutate, str(e.value))
+    ok_ids, _ = eng.global_merge_reps([0], [(r.ids, r.rep_idx, r.reps, r.rep_counts)])   # still usable
+    assert len(ok_ids) > 0
     for p in (a, b, c):
         p.close()
     eng.close()

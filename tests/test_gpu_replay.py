@@ -118,3 +118,40 @@ def test_c_caller_java_sequence_large(dist, D, algo, proto, tmp_path, oracle):
     keys = oracle.keys(algo, vals, P)
     assert (int(calls[1]), int(calls[3])) == _drain_model(keys, P, 8)
     assert int(calls[1]) > 0
+
+
+@pytest.mark.parametrize("path", [p for p in golden_streams() if "_4d" in p or "_8d" in p],
+                         ids=lambda p: os.path.basename(p)[7:-4])
+def test_c_caller_stats_count_differs_from_partitions(path, tmp_path):
+    """proto 2: the aggregator merges the P triggered keys' messages plus empty messages of the
+    MR-Grid keys >= P that hold state but never receive the trigger, so sky_global_stats' K (one
+    entry per list) is not P.  The caller sizes its arrays from the K the library returns (as
+    HipSkylineOperators does), sums only partitions < P, and the answer is unchanged."""
+    assert os.path.exists(BIN), "build/operator_replay missing: run __graft_entry__.build()"
+    g = load_golden(path)
+    vals, ids = g["values"], g["ids"]
+    D = vals.shape[1]
+    csv = tmp_path / "stream.csv"
+    with open(csv, "w") as f:
+        for i, row in zip(ids, vals):
+            f.write(f"{int(i)}," + ",".join(str(int(x)) for x in row) + "\n")
+    seen_k_ne_p = False
+    for P in (4, 8):
+        r = subprocess.run([BIN, str(csv), str(D), str(P // 2), str(ALGO["grid"]), "1000.0", "-1", "8", "2"],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        lines = r.stdout.strip().split("\n")
+        got_ids = np.array([int(x) for x in lines[1].split()[1:]], np.int64)
+        lsz = np.array([int(x) for x in lines[2].split()[1:]], np.int64)
+        surv = np.array([int(x) for x in lines[3].split()[1:]], np.int64)
+        np.testing.assert_array_equal(got_ids, np.sort(ids[g[f"gsky_grid_{P}"]]))
+        np.testing.assert_array_equal(lsz, g[f"lsz_grid_{P}"])
+        np.testing.assert_array_equal(surv, g[f"surv_grid_{P}"])
+        opt = sum(surv[i] / lsz[i] for i in range(P) if lsz[i] > 0) / P
+        assert lines[0].split('"optimality": ')[1].split(",")[0] == java_format_4f(opt)
+        k_line = [ln for ln in r.stderr.split("\n") if ln.startswith("stats K ")][-1].split()
+        K, nl = int(k_line[2]), int(k_line[4])
+        kmax = int(max(P, int(g[f"keys_grid_{P}"].max()) + 1))
+        assert K == nl == kmax
+        seen_k_ne_p |= K != P
+    assert seen_k_ne_p, "no merge with K != P on this stream"

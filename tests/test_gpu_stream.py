@@ -126,3 +126,69 @@ def test_stream_reserve_then_queries(gpu_engine_factory, oracle, W):
         _check(oracle, "angle", vals[lo:pos], ids[lo:pos], 8, got_ids[:k].copy(), eng)
     st.close()
     eng.close()
+
+
+@pytest.mark.parametrize("path", [p for p in golden_streams() if "anti_correlated_4d" in p or "uniform_6d" in p
+                                  or "uniform_2d" in p], ids=lambda p: p.split("stream_")[-1][:-4])
+def test_landmark_vectors_count_distinct_local_skyline_vectors(gpu_engine_factory, oracle, path):
+    """sky_stream_vectors after a query = the distinct (key, row) vectors of the local skylines L_k
+    over every tuple so far (the state the next query starts from), and + the rows appended since
+    before the next query.  The inert holes of k_ls_new_reps' publishing races are not counted."""
+    import skyline
+    g = load_golden(path)
+    vals, ids = g["values"], g["ids"].astype(np.int64)
+    n, D = vals.shape
+    P_ = 8
+    eng = gpu_engine_factory(D, P_, "mr-angle")
+    st = skyline.SkylineStream(eng, 0)
+    cuts = sorted({n // 5, n // 2, (4 * n) // 5, n})
+    pos = 0
+    for cut in cuts:
+        st.append(ids[pos:cut], vals[pos:cut])
+        assert st.vectors() >= cut - pos
+        pos = cut
+        st.query()
+        _, keys, _, _, inl = oracle.query_sfs_chunked("angle", vals[:pos], P_)
+        loc = np.nonzero(inl)[0]
+        distinct = len({(int(keys[i]),) + tuple(vals[i].view(np.int64).tolist()) for i in loc})
+        assert st.vectors() == distinct, (pos, st.vectors(), distinct)
+    st.append(ids[:7], vals[:7])                   # appended rows count until the next query
+    assert st.vectors() == distinct + 7
+    st.close()
+    eng.close()
+
+
+@pytest.mark.parametrize("W", [0, 5000])
+def test_stream_query_async_then_wait(gpu_engine_factory, oracle, W):
+    """sky_stream_query_async returns the integers (skyline size, sky_global_stats) and leaves the
+    id copy in flight; appends go on meanwhile; after sky_stream_wait the host view holds the same
+    ids as the oracle's answer for that trigger (the copy did not see the later appends)."""
+    import skyline
+    g = load_golden([p for p in golden_streams() if "anti_correlated_6d" in p][0])
+    vals, ids = g["values"], g["ids"].astype(np.int64)
+    n, D = vals.shape
+    eng = gpu_engine_factory(D, 8, "mr-angle")
+    st = skyline.SkylineStream(eng, W)
+    st.reserve(n)
+    pos, step = 0, max(1, n // 6)
+    while pos < n:
+        b = min(step, n - pos)
+        st.append(ids[pos:pos + b], vals[pos:pos + b])
+        pos += b
+        k = st.query_async_host_view()
+        ls, sv = eng.stats()
+        lo = max(0, pos - W) if W else 0
+        exp, _, els, esv = oracle.query_bnl("angle", vals[lo:pos], ids[lo:pos], 8)
+        assert k == len(exp) and (ls == els).all() and (sv == esv).all()
+        if pos < n:                                 # the next micro-batch while the copy runs
+            b2 = min(step, n - pos)
+            st.append(ids[pos:pos + b2], vals[pos:pos + b2])
+        ms = st.wait()
+        assert ms >= 0.0
+        got, _ = st.view()
+        assert sorted(got[:k].tolist()) == sorted(exp.tolist())
+        if pos < n:
+            pos += b2
+    assert st.wait() == 0.0                         # nothing pending
+    st.close()
+    eng.close()
