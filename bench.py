@@ -868,9 +868,9 @@ def main():
                     extra["configs"]["C5"] = {"landmark": stream_run(dev_index, 1234 + 6),
                                               "sliding_10M": stream_run(dev_index, 1234 + 6, window=10_000_000)}
             if not args.no_dominance:
-                extra["dominance_roofline"] = dominance_run(dev, D, P, args.dom_n, seed, 2, 1)
+                extra["dominance_roofline"] = dominance_run(dev, D, P, args.dom_n, seed, 3, 2)
                 if args.dom_n_large:
-                    extra["dominance_roofline_large"] = dominance_run(dev, D, P, args.dom_n_large, seed, 2, 1)
+                    extra["dominance_roofline_large"] = dominance_run(dev, D, P, args.dom_n_large, seed, 3, 2)
         line = {
             "metric": METRIC,
             "value": value,

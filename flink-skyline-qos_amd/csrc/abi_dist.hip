@@ -140,7 +140,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     SKY_TRY(p.mbr_gmin.ensure(mbr_group_slots(n_union) * NW * 4));
     SKY_TRY(p.mbr_gpr.ensure(mbr_group_slots(n_union) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)n_own * 4));
-    SKY_TRY(p.mbr_pairs.ensure(16));
+    SKY_TRY(p.mbr_pairs.ensure(128));
     SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(yt) * 4));
     // one radix scratch for both sorts (they run one after the other on the stream)
     SKY_TRY(p.scratch.ensure(radix_scratch_words(std::max(n_union, n_own)) * 4 + 64));
@@ -149,7 +149,7 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
     fill.add(p.mbr_mm.as<uint32_t>() + 2 * D, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + 3 * D, (size_t)D * 4, 0);
-    fill.add(p.mbr_pairs.p, 16, 0);
+    fill.add(p.mbr_pairs.p, 128, 0);
     fill.add(p.mbr_lpt.p, kMbrLptHead * 4, 0);
     fill.add(p.mbr_domf.p, (size_t)n_own * 4, 0);
     HIP_TRY(fill.launch(st));

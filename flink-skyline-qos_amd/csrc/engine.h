@@ -111,6 +111,12 @@ struct Pipe {
         bool single = false, global = false;
     } plan;
     int64_t plan_runs = 0, plan_misses = 0;
+    // candidate prefilter learning: when its first round cut fewer than 3 % of the slots (large
+    // anti-correlated skylines: the second-level pruners dominate almost nothing) the next queries
+    // skip it -- it is exact, so the result does not change -- and every 16th query probes again
+    bool pf_skip = false;
+    uint32_t pf_since_probe = 0;
+    int64_t pf_skipped = 0;
     bool last_planned = false, last_plan_miss = false;   // the last query's route (counters[7] bits 3, 4)
     bool fused = false;
     const int64_t *fused_ids = nullptr;

@@ -37,13 +37,14 @@ size_t mbr_group_slots(uint32_t mr);   // k_mbr.hip: gmin / gprange entries (gro
 
 int DevBuf::ensure(size_t bytes) {
     if (bytes <= cap && p) return SKY_OK;
-    // a buffer that has to grow again gets 1.5x headroom: query-to-query size changes (candidate
-    // counts, rep counts) then reallocate rarely (each hipFree synchronises the device and landed
-    // inside a query's latency)
+    // a buffer that has to grow again gets 1.5x headroom, a first one 1/8: query-to-query size
+    // changes (candidate counts, rep counts) then reallocate rarely (each hipFree synchronises the
+    // device and landed inside a query's latency: the learned prefilter skip grew every rep-sized
+    // buffer by 0.3 % in the first skipping query, +4.6 ms at std-anti 8D 2M)
     const bool regrow = cap != 0;
     release();
     size_t want = std::max<size_t>(bytes, 256);
-    if (regrow) want = std::max(want, bytes + bytes / 2);
+    want = regrow ? std::max(want, bytes + bytes / 2) : want + want / 8;
     want = (want + 4095) & ~size_t(4095);
     static const bool trace_alloc = SKY_MEASURE_ENV("SKY_TRACE_ALLOC") != nullptr;   // measurement only
     auto t0 = std::chrono::steady_clock::now();
@@ -161,6 +162,7 @@ static size_t slot_min() {
     const char *e = SKY_ENV("SKY_SLOT_MIN");
     return e ? (size_t)std::max(1, atoi(e)) : (size_t(1) << 20);
 }
+constexpr uint32_t kPrefilterProbe = 16;  // a skipped prefilter is probed again every 16 queries
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = SKY_ENV("SKY_FUSED_OUT");
@@ -683,14 +685,14 @@ static int mbr_run(Ctx &c, Pipe &p, const PipeIn &in, uint32_t mr, bool gmerge) 
     SKY_TRY(p.mbr_gmin.ensure(mbr_group_slots(mr) * NW * 4));
     SKY_TRY(p.mbr_gpr.ensure(mbr_group_slots(mr) * 4));
     SKY_TRY(p.mbr_domf.ensure((size_t)mr * 4));
-    SKY_TRY(p.mbr_pairs.ensure(64));
+    SKY_TRY(p.mbr_pairs.ensure(128));
     SKY_TRY(p.mbr_lpt.ensure(mbr_lpt_words(ntiles) * 4));
     SKY_TRY(p.scratch.ensure(std::max(radix_scratch_words(mr), scan_scratch_words(mr + 1)) * 4 + 64));
     FillSet fill;
     fill.add(p.mbr_lpt.p, kMbrLptHead * 4, 0);
     fill.add(p.mbr_mm.p, (size_t)D * 4, 0xff);
     fill.add(p.mbr_mm.as<uint32_t>() + D, (size_t)D * 4, 0);
-    fill.add(p.mbr_pairs.p, 64, 0);
+    fill.add(p.mbr_pairs.p, 128, 0);
     fill.add(p.mbr_domf.p, (size_t)mr * 4, 0);
     HIP_TRY(fill.launch(st));
     MbrArgs a;
@@ -918,6 +920,14 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
                                   {p.flags.p, 4}, {p.dup_cnt.p, (size_t)KM * 4}},
                           {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}));
         nout = tot[3];
+#ifdef SKY_MEASURE
+        if (SKY_MEASURE_ENV("SKY_FILTER_COUNT")) {   // k_filter's stores (tools/: the write itemisation)
+            uint32_t fw[16] = {};
+            HIP_TRY(hipMemcpy(fw, p.flags.p, 64, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[filter-count] n %u candidates %u deferred %u status_stored %u planes %d hist %d dom_kj %d\n",
+                    n, tot[0], tot[6], fw[8], p.planes_on ? 1 : 0, p.hist_count ? 1 : 0, p.dom_kj);
+        }
+#endif
         if (flags2 & kFlagRadixSpin) {
             set_error("a look-back (output) exceeded its spin bound");
             return SKY_E_HIP;
@@ -970,6 +980,15 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             if (mbr_pairs[3])                             // SKY_MBR_DBG bit 4: the scan's funnel
                 fprintf(stderr, "[mbr] reps %u groups %llu box %llu pre %llu tested %llu pairs %llu\n", p.mr,
                         mbr_pairs[2], mbr_pairs[3], mbr_pairs[4], mbr_pairs[1], mbr_pairs[0]);
+#ifdef SKY_MEASURE
+            {
+                unsigned long long tk[6] = {};
+                HIP_TRY(hipMemcpy(tk, p.mbr_pairs.as<unsigned long long>() + 8, 48, hipMemcpyDeviceToHost));
+                if (tk[0] | tk[1] | tk[2] | tk[3] | tk[4] | tk[5])   // SKY_MBR_DBG bit 16: region clocks
+                    fprintf(stderr, "[mbr-clock] setup %llu scans %llu pretest %llu loads %llu subbox %llu rows %llu\n",
+                            tk[0], tk[1], tk[2], tk[3], tk[4], tk[5]);
+            }
+#endif
             uint32_t alive_sum = 0;
             for (int k = 0; k < p.Kp; k++) alive_sum += p.h_seg_s[k];
             p.mg = in.global && !in.single ? alive_sum : 0;
@@ -1334,7 +1353,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // survivors are still too many for the brute path and the last round cut them by > 30 %
     int plan_rounds = 0;
     uint32_t plan_live[kPrefilterRounds] = {};
-    for (int round = 0; round < kPrefilterRounds && p.mt >= kPrefilterMin && !prefilter_disabled(); round++) {
+    const bool pf_probe = !p.pf_skip || ++p.pf_since_probe >= kPrefilterProbe;
+    if (!pf_probe && p.mt >= kPrefilterMin) p.pf_skipped++;
+    for (int round = 0; round < kPrefilterRounds && p.mt >= kPrefilterMin && !prefilter_disabled() && pf_probe;
+         round++) {
         const uint32_t mt0 = p.mt;
         const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
         const int KM2 = p.Kp * M2;
@@ -1380,6 +1402,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         plan_live[plan_rounds++] = live_n;
         if (debug_level() >= 3)
             fprintf(stderr, "[sky] prefilter round %d: %u -> %u slots (M2=%d)\n", round, mt0, live_n, M2);
+        if (round == 0) {                          // learn whether the next queries should run it
+            p.pf_skip = (uint64_t)live_n * 100 > (uint64_t)mt0 * 97 && live_n > brute_max();
+            p.pf_since_probe = 0;
+        }
         if (live_n <= brute_max() || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
     }
     const uint32_t mt = p.mt;

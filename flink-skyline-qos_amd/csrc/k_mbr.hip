@@ -47,6 +47,13 @@ __device__ __forceinline__ uint32_t pk_max(uint32_t x, uint32_t y) {
     return __builtin_bit_cast(uint32_t,
                               __builtin_elementwise_max(__builtin_bit_cast(mbr_u16x2, x), __builtin_bit_cast(mbr_u16x2, y)));
 }
+// (an LDS-DMA variant of the pair pass's x-tile prefetch measured slower: profiles/r05_dominance_ab.txt)
+__device__ __forceinline__ uint64_t wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// set bits of m below this lane (two VALU: mbcnt)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ uint32_t ord_f32(float f) {       // order-preserving image (no NaN here)
     const uint32_t u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -246,6 +253,8 @@ constexpr int kMbrT = 64;   // rows per tile (= one wave)
 // sub-boxes per tile whose min corners the pair pass tests each y against before comparing rows:
 // 8 boxes of 8 rows for packed u16 rows (the corners of a tile are 32 words: one pair of scalar
 // loads), 4 of 16 rows for f32 / f64 rows (32 / 64 words).  tsub holds kMbrSubMax corners per tile.
+// (4-row boxes for packed u16 rows, 16 per tile: 3.7x fewer pair tests at std-anti 8D 10M but twice
+// the sub-box passes; the pass took 21.1 vs 19.6 ms, profiles/r05_dominance_ab.txt)
 template <class R>
 constexpr int mbr_subs() { return R::NW <= 4 ? 8 : 4; }
 
@@ -371,17 +380,26 @@ struct MbrYSet {
 // is split into up to kMbrSplitMax items that take every s-th reachable group (the reachable
 // groups cluster, so interleaving balances the parts), and every wave of the pair pass takes
 // items from a ticket counter until none is left.
-template <class R>
+template <class R, int YT>
 __global__ __launch_bounds__(kThreads) void k_mbr_cost(const uint32_t *__restrict__ gmin, uint32_t ngroups,
                                                        MbrYSet ys, uint32_t *__restrict__ lpt) {
-    // lane = y tile: the groups' min corners are wave-uniform (scalar loads, read once per wave
-    // instead of once per y tile), one box test per (y tile, group)
+    // lane = y unit (YT consecutive y tiles, k_mbr_pairs' work item): the groups' min corners are
+    // wave-uniform (scalar loads, read once per wave instead of once per unit), one box test per
+    // (unit, group) against the unit's max corner
     constexpr int NW = R::NW;
+    const uint32_t nyu = (ys.ntiles + YT - 1) / YT;
     const uint32_t yt = blockIdx.x * kThreads + threadIdx.x;
-    const bool valid = yt < ys.ntiles;
+    const bool valid = yt < nyu;
     uint32_t ymax[NW];
+    R::ident_max(ymax);
 #pragma unroll
-    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + min(yt, ys.ntiles - 1u)];
+    for (int t = 0; t < YT; t++) {
+        const uint32_t tt = min(min(yt, nyu - 1u) * YT + t, ys.ntiles - 1u);
+        uint32_t tm[NW];
+#pragma unroll
+        for (int w = 0; w < NW; w++) tm[w] = ys.tmax[(size_t)w * ys.ntiles + tt];
+        R::cmax(ymax, tm);
+    }
     uint32_t cnt = 0;
 #pragma unroll 4
     for (uint32_t g = 0; g < ngroups; g++) {
@@ -486,19 +504,26 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 // The y tiles (ys) may be another set than the x tiles (the multi-GPU merge: own vectors against
 // the union, FULL only); for one set they are the same arrays.
 //
-// Per y tile (one wave, lane = y), for every x tile whose min corner is <= the y tile's max
-// corner (found 64 tiles at a time per reachable group, as above):
-//  * the tile's S sub-box min corners are wave-uniform loads (SGPRs), each tested against
-//    every live y at once: S ballots give the (y, sub-box) entries -- no per-tile listing pass
-//    in LDS and no readlane of corners;
-//  * the tile's rows (loaded one tile ahead, two register sets used alternately) are staged in
-//    LDS, the entries packed into an LDS list, and compared S entries per wave instruction
-//    (RS = 64 / S lanes per entry: lane r of entry g compares row r of its sub-box with its y);
-//  * a hit is one LDS atomic OR into the y's fate word (no per-group scalar loop); the fates are
-//    read back once per tile to retire the y's a rep of their own partition dominates.
+// A work item is a y UNIT: YT consecutive y tiles (64 YT y's, Hilbert neighbours), one wave,
+// lane = y of each tile.  The units' x work overlaps strongly (tools: per y tile the x tiles
+// that pass the whole-corner test drop from 283 to 177 at YT = 2 on std-anti 8D 2M), so the
+// per-x-tile costs -- group and tile scans, row and corner loads, the LDS staging, the fate
+// read-back -- are paid once for YT tiles.  For every x tile whose min corner is <= the unit's
+// max corner (found 64 tiles at a time per reachable group):
+//  * the whole tile's min corner against every live y (NW readlanes, one ballot per y tile);
+//  * sub-box stage, lane = (pre y, sub-box): the y's that passed are listed in LDS, each pass
+//    tests 64 / S of them against all S sub-box corners at once (the corner of box lane % S came
+//    in with the tile's rows), and the passing (y, box) entries are appended to an LDS list;
+//  * row stage, lane = (entry, row): the tile's rows (loaded one tile ahead, two register sets
+//    used alternately) are staged in LDS and S entries are compared per wave instruction (lane r
+//    of entry g: row r of its sub-box against its y);
+//  * a hit is one LDS atomic OR into the y's fate word; the fates are read back once per tile to
+//    retire the y's a rep of their own partition dominates.
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
-template <class R, bool FULL, bool GM>
-__global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+// packed-u16 rows: the register budget capped for 6 waves per SIMD (79 VGPRs at YT = 2, no spill;
+// the 5 waves the 82-VGPR default allows: 19.1 vs 18.8 ms at std-anti 8D 10M)
+template <class R, bool FULL, bool GM, int YT>
+__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(R::NW <= 4 ? 6 : 1))) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
                                                          const uint32_t *__restrict__ tprange,
@@ -512,60 +537,110 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
                                                          unsigned long long *__restrict__ trace) {
     constexpr int NW = R::NW;
     constexpr int S = mbr_subs<R>(), RS = kMbrT / S;
+    constexpr int NY = 64 * YT;                    // y's per work item
+    static_assert(NY <= 256 && S <= 16, "entries are (y << 4 | box) in 16 bits, pre y's in 8");
     uint64_t npairs = 0, ntested = 0;
     uint32_t ngrp = 0, nbox = 0, npre = 0;
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
-    uint32_t witem, yt, part, parts;
-    while (mbr_next_item(lpt, ys.ntiles, witem, yt, part, parts)) {
+    const uint32_t nyu = (ys.ntiles + YT - 1) / YT;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
+    __shared__ uint4 s_y[NY * NW / 4];            // this item's y rows (compare operands)
+    __shared__ uint32_t s_py[NY], s_hit[NY];       // y partitions; y fate words (bit 1 any, bit 0 same)
+    __shared__ uint4 s_x[64 * NW / 4];            // the x tile under test
+    __shared__ uint32_t s_px[64];
+    __shared__ uint16_t s_e[NY * S];              // (y << 4 | sub-box) entries
+    __shared__ uint8_t s_pl[NY];                  // the y's that passed the tile's whole-corner test
+    uint32_t *sy = reinterpret_cast<uint32_t *>(s_y), *sx = reinterpret_cast<uint32_t *>(s_x);
+#ifdef SKY_MEASURE
+    // SKY_MBR_DBG & 16 (measurement builds): shader-clock time per region of the pass, charged to
+    // the region running when the next one starts: 0 item setup / super-groups, 1 group and tile
+    // scans, 2 whole-corner pretests, 3 row / corner loads issued, 4 sub-box stage, 5 row stage
+    uint64_t t_acc[6] = {0, 0, 0, 0, 0, 0}, t_last = 0;
+    int t_cur = 0;
+    const bool timing = (dbg & 16) != 0;
+    if (timing) t_last = __builtin_amdgcn_s_memtime();
+    auto tick = [&](int k) {
+        if (!timing) return;
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            if (i == t_cur) t_acc[i] += t - t_last;
+        t_last = t;
+        t_cur = k;
+    };
+#else
+    auto tick = [](int) {};
+#endif
+    uint32_t witem, yu, part, parts;
+    while (mbr_next_item(lpt, nyu, witem, yu, part, parts)) {
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    tick(0);
     const uint64_t np0 = npairs, nt0 = ntested;
     uint32_t gord = 0;
-    const uint32_t gs_lo = 0, gs_hi = ngroups;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t j = yt * kMbrT + lane;
-    const bool valid = j < ys.mr;
-    uint32_t y[NW], ymax[NW];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(ys.trows + (size_t)min(j, ys.mr - 1u) * NW);
+    const uint32_t yt0 = yu * YT;
+    uint32_t y[YT][NW], ymax[NW];
+    uint64_t live[YT];
+    uint32_t f[YT];
+    uint32_t ypl = 0xffffffffu, yph = 0u;
+    R::ident_max(ymax);
+#pragma unroll
+    for (int t = 0; t < YT; t++) {
+        const uint32_t jt = (yt0 + t) * kMbrT + lane;
+        const bool valid = jt < ys.mr;
+        const uint4 *src = reinterpret_cast<const uint4 *>(ys.trows + (size_t)min(jt, ys.mr - 1u) * NW);
 #pragma unroll
         for (int q = 0; q < NW / 4; q++) {
             const uint4 v = src[q];
-            y[4 * q] = v.x;
-            y[4 * q + 1] = v.y;
-            y[4 * q + 2] = v.z;
-            y[4 * q + 3] = v.w;
+            y[t][4 * q] = v.x;
+            y[t][4 * q + 1] = v.y;
+            y[t][4 * q + 2] = v.z;
+            y[t][4 * q + 3] = v.w;
         }
-    }
+        if (yt0 + t < ys.ntiles) {                 // wave-uniform
+            uint32_t tm[NW];
 #pragma unroll
-    for (int w = 0; w < NW; w++) ymax[w] = ys.tmax[(size_t)w * ys.ntiles + yt];
-    // the tile's static max corner: what decides which split item owns which group (mbr_share),
+            for (int w = 0; w < NW; w++) tm[w] = ys.tmax[(size_t)w * ys.ntiles + yt0 + t];
+            R::cmax(ymax, tm);
+            const uint32_t yr = ys.tprange[yt0 + t];
+            ypl = min(ypl, yr & 0xffffu);
+            yph = max(yph, yr >> 16);
+        }
+#pragma unroll
+        for (int w = 0; w < NW; w++) sy[(t * 64 + lane) * NW + w] = y[t][w];
+        s_py[t * 64 + lane] = valid ? ys.tpart[min(jt, ys.mr - 1u)] : 0xffffffffu;
+        s_hit[t * 64 + lane] = 0u;
+        live[t] = __ballot(valid);
+        f[t] = 0u;
+    }
+    // the unit's static max corner: what decides which split item owns which group (mbr_share),
     // whatever the items' live lanes do; ymax itself shrinks with the live y's (refresh_ymax)
     uint32_t ymax0[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) ymax0[w] = ymax[w];
-    const uint32_t yr = ys.tprange[yt];
-    const uint32_t ypl = yr & 0xffffu, yph = yr >> 16;
-    const uint32_t py = valid ? ys.tpart[min(j, ys.mr - 1u)] : 0xffffffffu;
-    __shared__ uint4 s_y[64 * NW / 4];            // this wave's y rows (compare operands)
-    __shared__ uint32_t s_py[64], s_hit[64];       // y partitions; y fate words (bit 1 any, bit 0 same)
-    __shared__ uint4 s_x[64 * NW / 4];            // the x tile under test
-    __shared__ uint32_t s_px[64];
-    __shared__ uint16_t s_e[64 * S];              // (y << 3 | sub-box) entries
-    uint32_t *sy = reinterpret_cast<uint32_t *>(s_y), *sx = reinterpret_cast<uint32_t *>(s_x);
-#pragma unroll
-    for (int w = 0; w < NW; w++) sy[lane * NW + w] = y[w];
-    s_py[lane] = py;
-    s_hit[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
-    uint32_t f = 0;
-    uint64_t live = __ballot(valid);
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
+    auto any_live = [&]() -> bool {
+        uint64_t a = 0;
+#pragma unroll
+        for (int t = 0; t < YT; t++) a |= live[t];
+        return a != 0ull;
+    };
+    // some live y still lacks a dominator of any partition (GM: the scans cannot restrict
+    // themselves to the unit's partitions yet)
+    auto need_any = [&]() -> bool {
+        uint64_t a = 0;
+#pragma unroll
+        for (int t = 0; t < YT; t++) a |= live[t] & __ballot(!(f[t] & 2u));
+        return a != 0ull;
+    };
 
-    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx)
-    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t &px) {
+    // the rows + partition of x tile xt, one row per lane (clamped: past mr masked by nx), and the
+    // min corner of its sub-box (lane % S): the sub-box stage's operand
+    auto load_x = [&](uint32_t xt, uint32_t (&xv)[NW], uint32_t (&cv)[NW], uint32_t &px) {
+        tick(3);
         const uint32_t xi = min(xt * kMbrT + lane, mr - 1u);
         const uint4 *src = reinterpret_cast<const uint4 *>(trows + (size_t)xi * NW);
+        const uint4 *csrc = reinterpret_cast<const uint4 *>(tsub + ((size_t)xt * S + (lane % S)) * NW);
 #pragma unroll
         for (int q = 0; q < NW / 4; q++) {
             const uint4 v = src[q];
@@ -573,20 +648,30 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             xv[4 * q + 1] = v.y;
             xv[4 * q + 2] = v.z;
             xv[4 * q + 3] = v.w;
+            const uint4 c = csrc[q];
+            cv[4 * q] = c.x;
+            cv[4 * q + 1] = c.y;
+            cv[4 * q + 2] = c.z;
+            cv[4 * q + 3] = c.w;
         }
         px = tpart[xi];
     };
     // the live y's max corner: as y's are retired (a rep of their own partition dominates them) the
     // box the x scan tests against shrinks; recomputed (wave max) when live changed since
-    uint64_t live_ymax = live;
+    uint64_t live_ymax[YT];
+#pragma unroll
+    for (int t = 0; t < YT; t++) live_ymax[t] = live[t];
     auto refresh_ymax = [&]() {
-        if (live == live_ymax) return;
-        live_ymax = live;
+        bool same = true;
+#pragma unroll
+        for (int t = 0; t < YT; t++) same &= live[t] == live_ymax[t];
+        if (same) return;
         uint32_t m[NW];
         R::ident_max(m);
-        if ((live >> lane) & 1ull) {
 #pragma unroll
-            for (int w = 0; w < NW; w++) m[w] = y[w];
+        for (int t = 0; t < YT; t++) {
+            live_ymax[t] = live[t];
+            if ((live[t] >> lane) & 1ull) R::cmax(m, y[t]);
         }
 #pragma unroll
         for (int o = 1; o <= 32; o <<= 1) {
@@ -600,68 +685,75 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
     };
     uint32_t tg[NW];                                // min corners of the group's tiles (lane = tile)
     // the next tile of the group (bits tm) whose whole min corner is <= some live y (the corner
-    // came in with the tile scan: NW readlanes); *pm = those y.  Tiles that can dominate no live y
-    // are dropped here, before their rows are loaded and their sub-box corners read
-    auto next_tile = [&](uint64_t &tm, uint32_t g, uint32_t &xt, uint64_t &pm) -> bool {
+    // came in with the tile scan: NW readlanes); pm[t] = those y of y tile t.  Tiles that can
+    // dominate no live y are dropped here, before their rows are loaded and their corners read
+    auto next_tile = [&](uint64_t &tm, uint32_t g, uint32_t &xt, uint64_t (&pm)[YT]) -> bool {
+        tick(2);
         while (tm) {
             const int ti = (int)__builtin_ctzll(tm);
             tm &= tm - 1;
             uint32_t tc[NW];
 #pragma unroll
             for (int w = 0; w < NW; w++) tc[w] = (uint32_t)__builtin_amdgcn_readlane((int)tg[w], ti);
-            const uint64_t p = __ballot(R::le(tc, y)) & live;
-            if (p) {
+            uint64_t a = 0;
+#pragma unroll
+            for (int t = 0; t < YT; t++) {
+                pm[t] = __ballot(R::le(tc, y[t])) & live[t];
+                a |= pm[t];
+            }
+            if (a) {
                 xt = g + (uint32_t)ti;
-                pm = p;
                 return true;
             }
         }
         return false;
     };
-    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], uint32_t px, uint64_t pm) {
-        const uint64_t pre = pm & live;            // live may have shrunk since the tile was picked
-        if (!pre) return;
+    // One x tile against the y's that passed its whole-tile test (pre, P of them): the sub-box
+    // stage, the row stage and the fate read-back described above the kernel
+    auto test_tile = [&](uint32_t xt, const uint32_t (&xv)[NW], const uint32_t (&cv)[NW], uint32_t px,
+                         const uint64_t (&pm)[YT]) {
+        tick(4);
+        uint32_t P = 0;
+#pragma unroll
+        for (int t = 0; t < YT; t++) {             // live may have shrunk since the tile was picked
+            const uint64_t pre = pm[t] & live[t];
+            if ((pre >> lane) & 1ull) s_pl[P + lanes_below(pre)] = (uint8_t)(t * 64 + lane);
+            P += (uint32_t)__popcll(pre);
+        }
+        if (!P) return;
         npre++;
         const uint32_t nx = mr - xt * kMbrT < (uint32_t)kMbrT ? mr - xt * kMbrT : (uint32_t)kMbrT;
-        // the S corners: wave-uniform, all loaded before the first test (scalar loads in flight
-        // together); the tests are unconditional (a branch per box would wait per load) and a
-        // box past the last row is masked afterwards
-        const uint32_t *cs = tsub + (size_t)xt * S * NW;
-        uint32_t c[S][NW];
-#pragma unroll
-        for (int b = 0; b < S; b++)
-#pragma unroll
-            for (int w = 0; w < NW; w++) {
-                c[b][w] = cs[b * NW + w];
-            }
-        uint64_t ms[S];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t bl = lane % S;
+        const bool bvalid = bl * RS < nx;          // a box past the tile's last row holds no row
         uint32_t E = 0;
+        for (uint32_t j0 = 0; j0 < P; j0 += 64 / S) {
+            const uint32_t jj = j0 + lane / S;
+            const uint32_t yi = s_pl[min(jj, P - 1u)];
+            uint32_t yw[NW];
 #pragma unroll
-        for (int b = 0; b < S; b++) {
-            const uint64_t bal = __ballot(R::le(c[b], y));
-            ms[b] = bal & pre & ((uint32_t)(b * RS) < nx ? ~0ull : 0ull);
-            E += (uint32_t)__popcll(ms[b]);
+            for (int q = 0; q < NW / 4; q++) {
+                const uint4 b = s_y[yi * (NW / 4) + q];
+                yw[4 * q] = b.x; yw[4 * q + 1] = b.y; yw[4 * q + 2] = b.z; yw[4 * q + 3] = b.w;
+            }
+            const bool pass = (jj < P) & bvalid & R::le(cv, yw);
+            const uint64_t bal = wballot(pass);
+            if (pass) s_e[E + lanes_below(bal)] = (uint16_t)((yi << 4) | bl);
+            E += (uint32_t)__popcll(bal);
         }
         npairs += (uint64_t)RS * E;
         if ((dbg & 1) || !E) return;
         ntested++;
+        tick(5);
 #pragma unroll
         for (int w = 0; w < NW; w++) sx[lane * NW + w] = xv[w];
         s_px[lane] = px;
-        {
-            uint32_t eb = 0;
-#pragma unroll
-            for (int b = 0; b < S; b++) {
-                if ((ms[b] >> lane) & 1ull) s_e[eb + (uint32_t)__popcll(ms[b] & lt)] = (uint16_t)((lane << 3) | b);
-                eb += (uint32_t)__popcll(ms[b]);
-            }
-        }
         __builtin_amdgcn_wave_barrier();
         bool any = false;
         for (uint32_t e0 = 0; e0 < E; e0 += S) {
             const bool ev = e0 + eg < E;
             const uint32_t ent = s_e[min(e0 + eg, E - 1u)];
-            const uint32_t yb = ent >> 3, xr = (ent & 7u) * RS + er;
+            const uint32_t yb = ent >> 4, xr = (ent & 15u) * RS + er;
             uint32_t xw[NW], yw[NW];
 #pragma unroll
             for (int q = 0; q < NW / 4; q++) {
@@ -672,7 +764,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             // bitwise, not short-circuit: no exec-masked branches per test
             bool dom = ev & (xr < nx) & R::le(xw, yw);
             if constexpr (FULL) dom = dom & !R::le(yw, xw);
-            else dom = dom & !(xt == yt && xr == yb);
+            else dom = dom & !(xt == yt0 + (yb >> 6) && xr == (yb & 63u));
             if (dom) {
                 atomicOr(&s_hit[yb], s_px[xr] == s_py[yb] ? 3u : 2u);
                 any = true;
@@ -680,17 +772,20 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         }
         if (__ballot(any)) {
             __builtin_amdgcn_wave_barrier();
-            f |= s_hit[lane];
-            live &= __ballot(!(f & 1u));
+#pragma unroll
+            for (int t = 0; t < YT; t++) {
+                f[t] |= s_hit[t * 64 + lane];
+                live[t] &= __ballot(!(f[t] & 1u));
+            }
         }
         __builtin_amdgcn_wave_barrier();
     };
 
     // super-groups of 64 groups first (their min corners follow the groups' in gmin): a super-group
-    // whose corner is not <= the y tile's max corner holds no reachable group, and is skipped whole
+    // whose corner is not <= the unit's max corner holds no reachable group, and is skipped whole
     const uint32_t nsup = (ngroups + kMbrG - 1) / kMbrG;
     const uint32_t *sgmin = gmin + (size_t)NW * ngroups;
-    for (uint32_t u0 = 0; u0 < nsup && live; u0 += 64) {
+    for (uint32_t u0 = 0; u0 < nsup && any_live(); u0 += 64) {
     uint64_t sm;
     {
         const uint32_t q = min(u0 + lane, nsup - 1u);
@@ -699,7 +794,7 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
         for (int w = 0; w < NW; w++) sc[w] = sgmin[(size_t)w * nsup + q];
         sm = __ballot(u0 + lane < nsup && R::le(sc, parts == 1 ? ymax : ymax0));   // shares count static groups
     }
-    while (sm && live) {
+    while (sm && any_live()) {
         const uint32_t s0 = (u0 + (uint32_t)__builtin_ctzll(sm)) * 64;
         sm &= sm - 1;
         refresh_ymax();
@@ -710,16 +805,17 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
 #pragma unroll
             for (int w = 0; w < NW; w++) gc[w] = gmin[(size_t)w * ngroups + q];
             const uint32_t gr = gprange[q];
-            const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
-            const bool reach = s0 + lane < gs_hi && R::le(gc, ymax0);
+            const bool na = GM && need_any();
+            const bool reach = s0 + lane < ngroups && R::le(gc, ymax0);
             bool cand = reach && R::le(gc, ymax);
-            if (cand && !need_any) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
+            if (cand && !na) cand = (gr & 0xffffu) <= yph && (gr >> 16) >= ypl;
             gm = __ballot(cand) & mbr_share(__ballot(reach), gord, part, parts);
         }
         ngrp += (uint32_t)__popcll(gm);
-        while (gm && live) {
+        while (gm && any_live()) {
             const uint32_t g = (s0 + (uint32_t)__builtin_ctzll(gm)) * kMbrG;
             gm &= gm - 1;
+            tick(1);
             refresh_ymax();
             uint64_t tm;
             {
@@ -727,9 +823,9 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
 #pragma unroll
                 for (int w = 0; w < NW; w++) tg[w] = tmin[(size_t)w * ntiles + t];
                 const uint32_t tr = tprange[t];
-                const uint64_t need_any = GM ? (live & __ballot(!(f & 2u))) : 0ull;
+                const bool na = GM && need_any();
                 bool cand = g + lane < ntiles && R::le(tg, ymax);
-                if (cand && !need_any) cand = (tr & 0xffffu) <= yph && (tr >> 16) >= ypl;
+                if (cand && !na) cand = (tr & 0xffffu) <= yph && (tr >> 16) >= ypl;
                 tm = __ballot(cand);
             }
             if (dbg & 2) tm = 0;
@@ -739,32 +835,38 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             // one is tested (two register sets used alternately: no copy at the back-edge that would
             // wait for them; past the last tile the current one is re-loaded, a cache hit)
             uint32_t xa, xb;
-            uint64_t ma, mb;
+            uint64_t ma[YT], mb[YT];
             if (!next_tile(tm, g, xa, ma)) continue;
-            uint32_t va[NW], vb[NW], pa, pb;
-            load_x(xa, va, pa);
+            uint32_t va[NW], vb[NW], ca[NW], cb[NW], pa, pb;
+            load_x(xa, va, ca, pa);
             for (;;) {
                 const bool hb = next_tile(tm, g, xb, mb);
                 if (!hb) xb = xa;
-                load_x(xb, vb, pb);
-                test_tile(xa, va, pa, ma);
-                if (!hb || !live) break;
+                load_x(xb, vb, cb, pb);
+                test_tile(xa, va, ca, pa, ma);
+                if (!hb || !any_live()) break;
                 const bool ha = next_tile(tm, g, xa, ma);
                 if (!ha) xa = xb;
-                load_x(xa, va, pa);
-                test_tile(xb, vb, pb, mb);
-                if (!ha || !live) break;
+                load_x(xa, va, ca, pa);
+                test_tile(xb, vb, cb, pb, mb);
+                if (!ha || !any_live()) break;
             }
         }
     }
     }                                               // the next reachable super-group
-    if (valid && f) atomicOr(&domf[j], f);          // domf zeroed by the caller
+    tick(0);
+#pragma unroll
+    for (int t = 0; t < YT; t++) {
+        const uint32_t jt = (yt0 + t) * kMbrT + lane;
+        if (jt < ys.mr && f[t]) atomicOr(&domf[jt], f[t]);   // domf zeroed by the caller
+    }
     if (trace && lane == 0) {
         trace[4 * (size_t)witem] = t_start;
         trace[4 * (size_t)witem + 1] = __builtin_amdgcn_s_memrealtime();
         trace[4 * (size_t)witem + 2] = ntested - nt0;
         trace[4 * (size_t)witem + 3] = npairs - np0;
     }
+    __builtin_amdgcn_wave_barrier();               // the next item rewrites s_y / s_py / s_hit
     }                                               // the next work item
     if ((threadIdx.x & 63) == 0 && pairs) {
         atomicAdd(pairs, (unsigned long long)npairs);
@@ -774,6 +876,10 @@ __global__ __launch_bounds__(kMbrPairThreads) void k_mbr_pairs(const uint32_t *_
             atomicAdd(pairs + 3, (unsigned long long)nbox);
             atomicAdd(pairs + 4, (unsigned long long)npre);
         }
+#ifdef SKY_MEASURE
+        if (timing)
+            for (int i = 0; i < 6; i++) atomicAdd(pairs + 8 + i, (unsigned long long)t_acc[i]);
+#endif
     }
 }
 
@@ -857,11 +963,18 @@ static uint32_t mbr_qcap(uint32_t ytiles) {
     return (uint32_t)(e ? std::min<size_t>(cap, strtoull(e, nullptr, 10)) : cap);
 }
 
-template <class R>
+// y tiles per work item of the pair pass (k_mbr_pairs: the x-side work of Hilbert neighbours is
+// shared).  Two pay once the y tiles are many: std-anti 8D 10M (156k tiles) 18.8 vs 19.9 ms; at
+// 2M (31k tiles, 2.5 units per wave) one is faster (3.49 vs 3.61 ms)
+static int mbr_yt(uint32_t ytiles) { return ytiles >= 65536 ? 2 : 1; }
+
+template <class R, int YT>
 static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, uint32_t *err,
                       hipStream_t st) {
-    k_mbr_cost<typename R::Pair><<<(ys.ntiles + kThreads - 1) / kThreads, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
-    k_mbr_order<<<1, 1024, 0, st>>>(ys.ntiles, mbr_qcap(ys.ntiles), lpt, err);
+    const uint32_t nyu = (ys.ntiles + YT - 1) / YT;
+    k_mbr_cost<typename R::Pair, YT><<<(nyu + kThreads - 1) / kThreads, kThreads, 0, st>>>(gmin, ngroups, ys, lpt);
+    // the queue sized for ys.ntiles units holds the fewer units' items too
+    k_mbr_order<<<1, 1024, 0, st>>>(nyu, mbr_qcap(ys.ntiles), lpt, err);
 }
 
 template <class R, int D>
@@ -874,17 +987,24 @@ static void mbr_launch_t(const MbrArgs &a, hipStream_t st, hipError_t *lerr) {
                                            a.tprange, a.tsub, a.gmin, a.gprange, st, lerr);
     const unsigned gp = mbr_pair_waves(ntiles);
     const MbrYSet ys{a.trows, a.tpart, a.tmax, a.tprange, mr, ntiles};
-    mbr_order<R>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, a.err, st);
-#define SKY_MBR_PAIRS(F, G)                                                                                  \
-    k_mbr_pairs<typename R::Pair, F, G><<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange, a.tsub, a.gmin,                          \
-                                                  a.gprange, mr, ntiles, ys, a.dbg, a.domf, a.pairs, a.lpt, a.trace)
-    if (a.full) {
-        if (a.gmerge) SKY_MBR_PAIRS(true, true);
-        else SKY_MBR_PAIRS(true, false);
-    } else {
-        if (a.gmerge) SKY_MBR_PAIRS(false, true);
-        else SKY_MBR_PAIRS(false, false);
-    }
+#define SKY_MBR_PAIRS(F, G, Y)                                                                               \
+    k_mbr_pairs<typename R::Pair, F, G, Y><<<gp, kMbrPairThreads, 0, st>>>(a.trows, a.tpart, a.tmin, a.tprange,   \
+                                                                         a.tsub, a.gmin, a.gprange, mr, ntiles, ys, \
+                                                                         a.dbg, a.domf, a.pairs, a.lpt, a.trace)
+#define SKY_MBR_RUN(Y)                                                                                        \
+    do {                                                                                                      \
+        mbr_order<R, Y>(a.gmin, (uint32_t)mbr_groups(mr), ys, a.lpt, a.err, st);                              \
+        if (a.full) {                                                                                         \
+            if (a.gmerge) SKY_MBR_PAIRS(true, true, Y);                                                       \
+            else SKY_MBR_PAIRS(true, false, Y);                                                               \
+        } else {                                                                                              \
+            if (a.gmerge) SKY_MBR_PAIRS(false, true, Y);                                                      \
+            else SKY_MBR_PAIRS(false, false, Y);                                                              \
+        }                                                                                                     \
+    } while (0)
+    if (mbr_yt(ntiles) == 2) SKY_MBR_RUN(2);
+    else SKY_MBR_RUN(1);
+#undef SKY_MBR_RUN
 #undef SKY_MBR_PAIRS
     k_mbr_finish<<<gb, kThreads, 0, st>>>(perm, a.domf, mr, a.gmerge ? 1 : 0, a.alive_l, a.alive_g);
 }
@@ -923,10 +1043,17 @@ static void mbr_union_t(const MbrUnionArgs &a, hipStream_t st, hipError_t *lerr)
     const uint32_t nyt = (uint32_t)mbr_tiles(y.mr);
     const unsigned gp = mbr_pair_waves(nyt);
     const MbrYSet ys{y.trows, y.tpart, y.tmax, y.tprange, y.mr, nyt};
-    mbr_order<R>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, y.err, st);
-    k_mbr_pairs<typename R::Pair, true, true><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
+    if (mbr_yt(nyt) == 2) {
+        mbr_order<R, 2>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, y.err, st);
+        k_mbr_pairs<typename R::Pair, true, true, 2><<<gp, kMbrPairThreads, 0, st>>>(
+            x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin, x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, x.dbg,
+            y.domf, x.pairs, y.lpt, nullptr);
+    } else {
+    mbr_order<R, 1>(x.gmin, (uint32_t)mbr_groups(x.mr), ys, y.lpt, y.err, st);
+    k_mbr_pairs<typename R::Pair, true, true, 1><<<gp, kMbrPairThreads, 0, st>>>(x.trows, x.tpart, x.tmin, x.tprange, x.tsub, x.gmin,
                                                         x.gprange, x.mr, (uint32_t)mbr_tiles(x.mr), ys, x.dbg,
                                                         y.domf, x.pairs, y.lpt, nullptr);
+    }
     k_mbr_union_finish<<<(y.mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(perm, y.domf, y.mr, y.rep_key, a.ymult,
                                                                              a.K, a.flags, a.lsz, a.surv);
 }

@@ -437,6 +437,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
     const uint32_t sg = a.dom_kj >= 0 ? ((uint32_t)(a.dom_kj / a.M) << 8) | (uint32_t)(1 + a.dom_kj % a.M) : 0x10000u;
     double vn[D];                                                // the row of item r+1, in flight
     int32_t kn = 0;
+#ifdef SKY_MEASURE
+    uint32_t n_stored = 0;                                       // status words stored (planes on)
+#endif
 #define SKY_FILTER_FETCH_TO(I, VN, KN)                                                     \
     do {                                                                                   \
         const uint32_t i_ = min((uint32_t)(I), nl);                                        \
@@ -479,6 +482,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
                 const bool dg = vp && (uint32_t)st_prev == sg, ex = vp && (st_prev & 0xffu) != kCodeDropped && !dg;
                 const uint64_t bm = __ballot(dg), em = __ballot(ex);
                 if (ex) a.status[i - kThreads] = st_prev;
+#ifdef SKY_MEASURE
+                n_stored += (uint32_t)__popcll(em);
+#endif
                 if (lane == 0)
                     reinterpret_cast<ulonglong2 *>(a.planes)[((size_t)span * FT + (r - 1) / kItems) * 32 +
                                                              ((r - 1) % kItems) * (kThreads / 64) + wave] =
@@ -542,6 +548,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
             const bool dg = vp && (uint32_t)st_prev == sg, ex = vp && (st_prev & 0xffu) != kCodeDropped && !dg;
             const uint64_t bm = __ballot(dg), em = __ballot(ex);
             if (ex) a.status[il] = st_prev;
+#ifdef SKY_MEASURE
+            n_stored += (uint32_t)__popcll(em);
+#endif
             if (lane == 0)
                 reinterpret_cast<ulonglong2 *>(a.planes)[((size_t)span * FT + FT - 1) * 32 +
                                                          (kItems - 1) * (kThreads / 64) + wave] =
@@ -618,6 +627,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         atomicAnd(a.orand + 1, (unsigned long long)an);
     }
     if (lflags) atomicOr(a.flags, lflags);
+#ifdef SKY_MEASURE
+    if (lane == 0 && n_stored) atomicAdd(a.flags + 8, n_stored);   // measurement builds: flags[8]
+#endif
 }
 
 // The deferred MR-Angle tuples: exact fdlibm key, then the same classification;
@@ -896,25 +908,35 @@ __global__ __launch_bounds__(64) void k_cand_pick(const double *__restrict__ row
     if (j == 0) npr2[k] = __popcll(b);
 }
 
-// live[j] = candidate j is not dominated by a second-level pruner of its partition
-template <int D>
+// live[j] = candidate j is not dominated by a second-level pruner of its partition.  The pruners
+// (Kp x M2 rows, <= 2048) are staged in LDS once per workgroup: each lane's partition picks its
+// own rows, so global reads would be per-lane gathers (one 8-byte load per pruner and dimension)
+template <int D, bool STAGED>
 __global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restrict__ rows,
                                                           const uint64_t *__restrict__ key, uint32_t mt,
-                                                          const uint32_t *__restrict__ d_mt, int M2,
+                                                          const uint32_t *__restrict__ d_mt, int Kp, int M2,
                                                           const double *__restrict__ pr2,
                                                           const int32_t *__restrict__ npr2,
                                                           uint32_t *__restrict__ live) {
     constexpr int DP = padded_dims<double>(D);
-    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) double s_pr2[];   // [Kp * M2][D]
+    __shared__ int32_t s_np[kMaxK];
     if (d_mt) mt = min(mt, *d_mt);
+    const uint32_t j0 = blockIdx.x * kThreads;
+    if (j0 >= mt) return;                          // block-uniform
+    if constexpr (STAGED)
+        for (int q = threadIdx.x; q < Kp * M2 * D; q += kThreads) s_pr2[q] = pr2[q];
+    for (int q = threadIdx.x; q < Kp; q += kThreads) s_np[q] = npr2[q];
+    __syncthreads();
+    const uint32_t j = j0 + threadIdx.x;
     if (j >= mt) return;
     const int k = (int)(key[j] >> 56);
     double v[D];
     load_trow<double, D>(rows + (size_t)j * DP, v);
-    const int np = npr2[k];
-    const double *pr = pr2 + (size_t)k * M2 * D;
+    const int np = s_np[k];
+    const double *pr = (STAGED ? s_pr2 : pr2) + (size_t)k * M2 * D;
     bool dom = false;
-    for (int q = 0; q < np && !dom; q++) {
+    for (int q = 0; q < np; q++) {
         bool le = true, lt = false;
 #pragma unroll
         for (int d = 0; d < D; d++) {
@@ -922,14 +944,15 @@ __global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restri
             le &= x <= v[d];
             lt |= x < v[d];
         }
-        dom = le && lt;
+        dom |= le & lt;
     }
     live[j] = dom ? 0u : 1u;
 }
 
 // order-preserving compaction of the live slots (rows, keys, sources); the appended
 // pruner slots' indices are remapped (a dropped one: its duplicate group's fate is 0)
-__global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, const uint32_t *__restrict__ d_mt, int DP,
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, const uint32_t *__restrict__ d_mt,
                                                            const uint32_t *__restrict__ live,
                                                            const uint32_t *__restrict__ pos,
                                                            const double *__restrict__ rows,
@@ -937,11 +960,18 @@ __global__ __launch_bounds__(kThreads) void k_cand_compact(uint32_t mt, const ui
                                                            const uint32_t *__restrict__ src, double *__restrict__ rows2,
                                                            uint64_t *__restrict__ key2, uint32_t *__restrict__ src2,
                                                            int32_t *__restrict__ pruner_slot, int KM) {
+    constexpr int DP = padded_dims<double>(D);     // even: rows move as 16-byte pieces
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
     if (d_mt) mt = min(mt, *d_mt);
     if (j < mt && live[j]) {
         const uint32_t o = pos[j];
-        for (int d = 0; d < DP; d++) rows2[(size_t)o * DP + d] = rows[(size_t)j * DP + d];
+        const double2 *s2 = reinterpret_cast<const double2 *>(rows + (size_t)j * DP);
+        double2 *d2 = reinterpret_cast<double2 *>(rows2 + (size_t)o * DP);
+        double2 t[DP / 2];
+#pragma unroll
+        for (int q = 0; q < DP / 2; q++) t[q] = s2[q];
+#pragma unroll
+        for (int q = 0; q < DP / 2; q++) d2[q] = t[q];
         key2[o] = key[j];
         src2[o] = src[j];
     }
@@ -1543,16 +1573,25 @@ void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st) {
     const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 256u);
     SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.cmin)));
     SKY_DISPATCH_D(D, (k_cand_pick<DD><<<a.Kp, 64, 0, st>>>(a.rows, a.cmin, a.M2, a.pr2, a.npr2)));
-    SKY_DISPATCH_D(D, (k_cand_filter<DD><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(a.rows, a.key, a.mt, a.d_mt, a.M2, a.pr2,
-                                                                                   a.npr2, a.live)));
+    // the pruner image in LDS up to 32 KB (Kp x M2 x D doubles: 16 KB for C4's 16 x 16 x 8); beyond
+    // that (hundreds of partitions at high D) the rows are read from global memory
+    const size_t lds = (size_t)a.Kp * a.M2 * D * sizeof(double);
+    if (lds <= 32768) {
+        SKY_DISPATCH_D(D, (k_cand_filter<DD, true><<<nblk(a.mt, kThreads), kThreads, lds, st>>>(
+                              a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.pr2, a.npr2, a.live)));
+    } else {
+        SKY_DISPATCH_D(D, (k_cand_filter<DD, false><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(
+                              a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.pr2, a.npr2, a.live)));
+    }
 }
 
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
                          int32_t *pruner_slot, int KM, hipStream_t st) {
     const uint32_t n = std::max<uint32_t>(a.mt, (uint32_t)KM);
     if (!n) return;
-    k_cand_compact<<<nblk(n, kThreads), kThreads, 0, st>>>(a.mt, a.d_mt, padded_dims<double>(D), a.live, pos, a.rows, a.key,
-                                                           a.src, rows2, key2, src2, pruner_slot, KM);
+    SKY_DISPATCH_D(D, (k_cand_compact<DD><<<nblk(n, kThreads), kThreads, 0, st>>>(a.mt, a.d_mt, a.live, pos, a.rows, a.key,
+                                                                                 a.src, rows2, key2, src2, pruner_slot,
+                                                                                 KM)));
 }
 
 void launch_fate_tables(const FateArgs &a, hipStream_t st) {

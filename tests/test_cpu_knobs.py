@@ -15,7 +15,7 @@ MEASURE_ONLY = {"SKY_FILTER_DBG", "SKY_MBR_DBG", "SKY_CSV_STOP", "SKY_CSV_CHUNK_
                 "SKY_TRACE_ALLOC", "SKY_PLANES", "SKY_HIST_COUNT", "SKY_BRUTE_MAX", "SKY_MBR_ORDER",
                 "SKY_STAGE_THREADS", "SKY_PART_HOSTPROF", "SKY_DOM_PPT", "SKY_DOM_TX", "SKY_DOM_R",
                 "SKY_RADIX_ITEMS", "SKY_RADIX_COMPRESS", "SKY_SAMPLE_WG", "SKY_FILTER_TPB", "SKY_DEFER_WG",
-                "SKY_OUT_TPB", "SKY_PREFILTER_M2", "SKY_MBR_QCAP"}
+                "SKY_OUT_TPB", "SKY_PREFILTER_M2", "SKY_MBR_QCAP", "SKY_FILTER_COUNT"}
 NOT_KNOBS = {"SKY_DIST_STATS_WORDS"}   # a header macro named in an error message
 
 

@@ -13,6 +13,6 @@ import bench  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2_000_000
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 D = int(os.environ.get("DOM_D", "8"))
-r = bench.dominance_run(torch.device("cuda", 0), D, 16, n, 1234 + D, steps, 1)
+r = bench.dominance_run(torch.device("cuda", 0), D, 16, n, 1234 + D, steps, 2)
 print(json.dumps({k: r.get(k) for k in ("ms_per_query", "dominance_ms", "pair_tests_executed", "pair_tests_W", "frac",
                                         "W_rate", "path", "skyline_size", "tile_pairs_tested")}), flush=True)

@@ -70,11 +70,22 @@ def pmc(d, sub, meta):
         print("no dispatches matched", sub)
         return None
     names = sorted({c for v in per.values() for c in v})
-    avg = {c: sum(v.get(c, 0.0) for v in per.values()) / len(per) for c in names}
-    print(f"{len(per)} dispatches of *{sub}*")
+
+    def _key(k):
+        try:
+            return int(k)
+        except ValueError:
+            return 0
+    order = sorted(per, key=_key)
+    # the first dispatch of a run is cold (k_filter: no designated duplicate group yet, so every
+    # kept status word is stored); the steady state is every later one
+    warm = order[1:] if len(order) > 1 else order
+    avg = {c: sum(per[k].get(c, 0.0) for k in warm) / len(warm) for c in names}
+    print(f"{len(per)} dispatches of *{sub}* (averaging the {len(warm)} warm ones)")
     for c in names:
-        print(f"  {c:28s} {avg[c]:.6g}")
-    res = {"kernel_substr": sub, "dispatches": len(per), "avg": avg}
+        print(f"  {c:28s} {avg[c]:.6g}   per dispatch: " + " ".join(f"{per[k].get(c, 0.0):.6g}" for k in order))
+    res = {"kernel_substr": sub, "dispatches": len(per), "warm_dispatches": len(warm), "avg": avg,
+           "per_dispatch": {c: [per[k].get(c, 0.0) for k in order] for c in names}}
     res.update(meta)
     return res
 
@@ -115,7 +126,11 @@ def main():
         return
     out = os.path.join(REPO, "profiles", "traffic_filter.json")
     old = json.load(open(out)) if os.path.exists(out) else {}
-    old.update({k: v for k, v in res.items() if k != "avg"})
+    old.update({k: v for k, v in res.items() if k not in ("avg", "per_dispatch")})
+    old.setdefault("counters_per_dispatch", {}).update(res["per_dispatch"])
+    old["note"] = ("counters averaged over the warm dispatches (every one after a run's first, which runs "
+                   "before the designated duplicate group is known); per dispatch values in "
+                   "counters_per_dispatch, in dispatch order")
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from src_hash import kernel_src_sha
     old["kernel_src_sha"] = kernel_src_sha("k_filter")     # bench.py reports it for this build only
