@@ -544,7 +544,10 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
     const uint32_t ngroups = (ntiles + kMbrG - 1) / kMbrG;
     const uint32_t nyu = (ys.ntiles + YT - 1) / YT;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t eg = lane / RS, er = lane % RS;   // this lane's entry slot and row within it
+    // row stage: RL lanes per entry, each comparing two rows of the entry's sub-box (er and
+    // er + RL) with the entry's y: 64 / RL entries per wave instruction
+    constexpr int RL = RS / 2;
+    const uint32_t eg = lane / RL, er = lane % RL;   // this lane's entry slot and first row within it
     __shared__ uint4 s_y[NY * NW / 4];            // this item's y rows (compare operands)
     __shared__ uint32_t s_py[NY], s_hit[NY];       // y partitions; y fate words (bit 1 any, bit 0 same)
     __shared__ uint4 s_x[64 * NW / 4];            // the x tile under test
@@ -726,20 +729,25 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
         __builtin_amdgcn_wave_barrier();
         const uint32_t bl = lane % S;
         const bool bvalid = bl * RS < nx;          // a box past the tile's last row holds no row
+        // each lane tests two pre y's (j and j + 64 / S) against its box: 2 * 64 / S y's per pass
+        constexpr uint32_t YP = 64 / S;
         uint32_t E = 0;
-        for (uint32_t j0 = 0; j0 < P; j0 += 64 / S) {
-            const uint32_t jj = j0 + lane / S;
-            const uint32_t yi = s_pl[min(jj, P - 1u)];
-            uint32_t yw[NW];
+        for (uint32_t j0 = 0; j0 < P; j0 += 2 * YP) {
+            const uint32_t ja = j0 + lane / S, jb = ja + YP;
+            const uint32_t yia = s_pl[min(ja, P - 1u)], yib = s_pl[min(jb, P - 1u)];
+            uint32_t ya[NW], yb[NW];
 #pragma unroll
             for (int q = 0; q < NW / 4; q++) {
-                const uint4 b = s_y[yi * (NW / 4) + q];
-                yw[4 * q] = b.x; yw[4 * q + 1] = b.y; yw[4 * q + 2] = b.z; yw[4 * q + 3] = b.w;
+                const uint4 a = s_y[yia * (NW / 4) + q], b = s_y[yib * (NW / 4) + q];
+                ya[4 * q] = a.x; ya[4 * q + 1] = a.y; ya[4 * q + 2] = a.z; ya[4 * q + 3] = a.w;
+                yb[4 * q] = b.x; yb[4 * q + 1] = b.y; yb[4 * q + 2] = b.z; yb[4 * q + 3] = b.w;
             }
-            const bool pass = (jj < P) & bvalid & R::le(cv, yw);
-            const uint64_t bal = wballot(pass);
-            if (pass) s_e[E + lanes_below(bal)] = (uint16_t)((yi << 4) | bl);
-            E += (uint32_t)__popcll(bal);
+            const bool pa = (ja < P) & bvalid & R::le(cv, ya), pb = (jb < P) & bvalid & R::le(cv, yb);
+            const uint64_t ba = wballot(pa), bb = wballot(pb);
+            const uint32_t na = (uint32_t)__popcll(ba);
+            if (pa) s_e[E + lanes_below(ba)] = (uint16_t)((yia << 4) | bl);
+            if (pb) s_e[E + na + lanes_below(bb)] = (uint16_t)((yib << 4) | bl);
+            E += na + (uint32_t)__popcll(bb);
         }
         npairs += (uint64_t)RS * E;
         if ((dbg & 1) || !E) return;
@@ -750,23 +758,32 @@ __global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu
         s_px[lane] = px;
         __builtin_amdgcn_wave_barrier();
         bool any = false;
-        for (uint32_t e0 = 0; e0 < E; e0 += S) {
+        for (uint32_t e0 = 0; e0 < E; e0 += 64 / RL) {
             const bool ev = e0 + eg < E;
             const uint32_t ent = s_e[min(e0 + eg, E - 1u)];
-            const uint32_t yb = ent >> 4, xr = (ent & 15u) * RS + er;
-            uint32_t xw[NW], yw[NW];
+            const uint32_t yb = ent >> 4, xr0 = (ent & 15u) * RS + er, xr1 = xr0 + RL;
+            uint32_t xa[NW], xb[NW], yw[NW];
 #pragma unroll
             for (int q = 0; q < NW / 4; q++) {
-                const uint4 a = s_x[xr * (NW / 4) + q], b = s_y[yb * (NW / 4) + q];
-                xw[4 * q] = a.x; xw[4 * q + 1] = a.y; xw[4 * q + 2] = a.z; xw[4 * q + 3] = a.w;
+                const uint4 a = s_x[xr0 * (NW / 4) + q], c = s_x[xr1 * (NW / 4) + q], b = s_y[yb * (NW / 4) + q];
+                xa[4 * q] = a.x; xa[4 * q + 1] = a.y; xa[4 * q + 2] = a.z; xa[4 * q + 3] = a.w;
+                xb[4 * q] = c.x; xb[4 * q + 1] = c.y; xb[4 * q + 2] = c.z; xb[4 * q + 3] = c.w;
                 yw[4 * q] = b.x; yw[4 * q + 1] = b.y; yw[4 * q + 2] = b.z; yw[4 * q + 3] = b.w;
             }
             // bitwise, not short-circuit: no exec-masked branches per test
-            bool dom = ev & (xr < nx) & R::le(xw, yw);
-            if constexpr (FULL) dom = dom & !R::le(yw, xw);
-            else dom = dom & !(xt == yt0 + (yb >> 6) && xr == (yb & 63u));
-            if (dom) {
-                atomicOr(&s_hit[yb], s_px[xr] == s_py[yb] ? 3u : 2u);
+            bool d0 = ev & (xr0 < nx) & R::le(xa, yw), d1 = ev & (xr1 < nx) & R::le(xb, yw);
+            if constexpr (FULL) {
+                d0 = d0 & !R::le(yw, xa);
+                d1 = d1 & !R::le(yw, xb);
+            } else {
+                const bool own = xt == yt0 + (yb >> 6);
+                d0 = d0 & !(own && xr0 == (yb & 63u));
+                d1 = d1 & !(own && xr1 == (yb & 63u));
+            }
+            if (d0 | d1) {
+                const uint32_t py = s_py[yb];
+                const uint32_t h0 = d0 ? (s_px[xr0] == py ? 3u : 2u) : 0u, h1 = d1 ? (s_px[xr1] == py ? 3u : 2u) : 0u;
+                atomicOr(&s_hit[yb], h0 | h1);
                 any = true;
             }
         }
