@@ -60,7 +60,7 @@ static inline void store_stats(sky_ctx *c, const Pipe &p) {
     c->counters[5] = p.sfs_rounds;
     c->counters[6] = p.sfs_pairs_upper;
     c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0) | (p.u16 ? 4 : 0) | (p.last_planned ? 8 : 0) |
-                     (p.last_plan_miss ? 16 : 0) | (p.mbr_tiles << 8);
+                     (p.last_plan_miss ? 16 : 0) | (p.last_tiny ? 32 : 0) | (p.mbr_tiles << 8);
     c->dom_w = p.dom_w;
 }
 

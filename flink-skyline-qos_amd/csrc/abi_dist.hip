@@ -461,7 +461,7 @@ int sky_dist_finish(sky_ctx *c, const int64_t *d_stats_sum, int64_t out_cap, int
     c->counters[5] = (int64_t)sum[3];       // union vectors
     c->counters[6] = c->dist_last_route;
     c->counters[7] = (p.f64 ? 1 : 0) | (p.ties ? 2 : 0) | (p.u16 ? 4 : 0) | (p.last_planned ? 8 : 0) |
-                     (p.last_plan_miss ? 16 : 0);
+                     (p.last_plan_miss ? 16 : 0) | (p.last_tiny ? 32 : 0);
     if (g > out_cap) {
         set_error("output capacity " + std::to_string(out_cap) + " < this rank's skyline share " + std::to_string(g));
         return SKY_E_CAPACITY;

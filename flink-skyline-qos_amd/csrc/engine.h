@@ -109,15 +109,20 @@ struct Pipe {
         bool f64 = false, ints = false;
         int D = 0, Kp = 0, M = 0;
         bool single = false, global = false;
+        bool tiny = false;                     // its final slots were few: the one-workgroup tail
     } plan;
     int64_t plan_runs = 0, plan_misses = 0;
     // candidate prefilter learning: when its first round cut fewer than 3 % of the slots (large
     // anti-correlated skylines: the second-level pruners dominate almost nothing) the next queries
     // skip it -- it is exact, so the result does not change -- and every 16th query probes again
     bool pf_skip = false;
-    uint32_t pf_since_probe = 0;
+    uint32_t pf_since_probe = 0, pf_mt = 0;    // pf_mt: the slot count the skip was learned on
     int64_t pf_skipped = 0;
     bool last_planned = false, last_plan_miss = false;   // the last query's route (counters[7] bits 3, 4)
+    bool last_tiny = false;                              // ... its tail in one workgroup (bit 5)
+    int64_t tiny_runs = 0;
+    uint32_t tiny_block = 0;
+    DevBuf dbg_clk;                                      // measurement builds: the tail's phase clocks                             // plans learned without trying the tail (after a miss)
     bool fused = false;
     const int64_t *fused_ids = nullptr;
     const int32_t *fused_org = nullptr;

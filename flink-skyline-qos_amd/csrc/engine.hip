@@ -163,6 +163,7 @@ static size_t slot_min() {
     return e ? (size_t)std::max(1, atoi(e)) : (size_t(1) << 20);
 }
 constexpr uint32_t kPrefilterProbe = 16;  // a skipped prefilter is probed again every 16 queries
+constexpr uint32_t kTinyBlock = 16;       // plans learned without the one-workgroup tail after it missed
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = SKY_ENV("SKY_FUSED_OUT");
@@ -214,6 +215,10 @@ static bool brute_disabled() {
     return e && atoi(e) == 0;
 }
 // SKY_BRUTE16=0: the small-set pair pass compares f32 even for integer rows (A/B knob)
+static bool tiny_disabled() {    // SKY_TINY=0: the planned tail as one launch per stage (A/B knob)
+    const char *e = SKY_ENV("SKY_TINY");
+    return e && e[0] == '0';
+}
 static bool brute16_disabled() {
     const char *e = SKY_ENV("SKY_BRUTE16");
     return e && atoi(e) == 0;
@@ -756,6 +761,7 @@ struct PlanRun {
     size_t cap = 0, cap_full = 0;     // slots allocated / needed at most
     const uint32_t *d_cnt = nullptr;  // slots entering the brute pass (device)
     bool k_u16 = false, k_f32 = false;   // the brute pass's compare type
+    bool tiny = false;                    // k_tiny_tail ran the tail (fates, counts, scan, stats)
 };
 // the next run's designated duplicate group (status planes): the largest group of this run
 void pick_dom_group(Pipe &p, int KM) {
@@ -827,7 +833,8 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
     fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
     fta.tile_cand = p.hist_count ? p.tile_cand.as<uint32_t>() : nullptr;
-    launch_fate_tables(fta, st);
+    const bool tiny = pr && pr->tiny;
+    if (!tiny) launch_fate_tables(fta, st);
     if (tm) tm->mark(7, st);
     if (!in.fate) {                  // multi-GPU export: the shard's fates come after the union
         p.nout = 0;
@@ -875,15 +882,18 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     } else if (p.fused) {
         // count pass -> tile scan -> write pass, chained on the device (no host read in
         // between; positions >= out_cap are not written, the final read reports the total)
-        c.ktimer_begin("outc", st);
-        if (p.hist_count)
-            launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
-                                  KM, tiles, p.out_cnt.as<uint32_t>(), st);
-        else
-            launch_out_count(oa, st);
-        c.ktimer_end("outc", st, n);
-        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                      p.scratch.as<uint32_t>(), st);
+        // (the one-workgroup tail wrote the counts, their offsets and the total)
+        if (!tiny) {
+            c.ktimer_begin("outc", st);
+            if (p.hist_count)
+                launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(),
+                                      p.pruner_fate.as<uint8_t>(), KM, tiles, p.out_cnt.as<uint32_t>(), st);
+            else
+                launch_out_count(oa, st);
+            c.ktimer_end("outc", st, n);
+            scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                          p.scratch.as<uint32_t>(), st);
+        }
         OutArgs ow = oa;
         ow.out_off = p.out_off.as<uint32_t>();
         ow.ids = in.ids;
@@ -906,8 +916,9 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     STAGE(st, "fate");
     uint32_t nout = 0;
     SKY_TRY(p.statk.ensure((size_t)p.K * 16));
-    launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
-                       p.statk.as<unsigned long long>(), st);
+    if (!tiny)
+        launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
+                           p.statk.as<unsigned long long>(), st);
     std::vector<unsigned long long> sk2((size_t)p.K * 2);
     const bool have_seg = mt && (brute || !p.h_seg_n.empty());
     p.h_seg_s.assign(have_seg ? p.Kp : 0, 0u);
@@ -939,6 +950,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
                 set_error("a tuple value is NaN: the reference BNL result is order-dependent for NaN; rejected");
                 return SKY_E_NAN;
             }
+            if (flags2 & kFlagTinyMiss) {     // the final slots outgrew the one-workgroup tail
+                p.plan.tiny = false;
+                p.tiny_block = kTinyBlock;
+                return kPlanMiss;
+            }
             const uint32_t m = tot[0], nps = tot[5];
             if ((size_t)m + nps > pr->cap) {
                 p.slot_hint = std::min(pr->cap_full, ((size_t)m + nps) * 5 / 4 + (size_t)KM);
@@ -947,7 +963,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             }
             bool ok = tot[10] <= p.plan.bound[0];
             for (int r = 0; r < p.plan.rounds; r++) ok &= tot[11 + r] <= p.plan.bound[r + 1];
-            const uint32_t fin = p.plan.rounds ? tot[10 + p.plan.rounds] : tot[10];
+            const uint32_t fin = pr->tiny ? tot[14] : (p.plan.rounds ? tot[10 + p.plan.rounds] : tot[10]);
             ok &= fin <= brute_max();
             const bool f64 = (flags2 & kFlagNotF32) != 0, ints = !f64 && (flags2 & kFlagNotU16) == 0;
             ok &= pr->k_u16 ? ints : (pr->k_f32 ? !f64 : true);
@@ -956,6 +972,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             p.nps = nps;
             p.mt_pre = tot[10];
             p.mt = fin;
+            p.plan.tiny = fin <= tiny_brute_rows(c.D) * 3 / 4;
             p.f64 = f64;
             p.ints = ints;
             p.ties = (flags2 & kFlagScoreTies) != 0;
@@ -1034,31 +1051,193 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
 // The planned route's zero / all-ones initialisations, added to the run's first fill launch:
 // the criterion minima of every prefilter round (a slice each), the brute pass's domination
 // bits (its bound) and per-partition counts.
-static int plan_prepare(Pipe &p, int D, FillSet &fill) {
+static int plan_prepare(Pipe &p, int D, bool tiny, FillSet &fill) {
     const Pipe::Plan &pl = p.plan;
     const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
     const size_t KM2 = (size_t)p.Kp * M2;
     uint32_t fin = pl.bound[0];
     for (int r = 0; r < pl.rounds; r++) fin = std::min(pl.bound[r + 1], fin);
-    if (pl.rounds) {
+    if (pl.rounds && !tiny) {           // (the one-workgroup tail keeps its minima in LDS)
         SKY_TRY(p.cmin.ensure(KM2 * pl.rounds * 8));
         fill.add(p.cmin.p, KM2 * pl.rounds * 8, 0xff);
     }
     SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
     SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
-    SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(fin, 1) * 4));
     fill.add(p.segalive.p, (size_t)p.Kp * 4);
     fill.add(p.seg_begin.p, (size_t)p.Kp * 4);
-    fill.add(p.keep.p, (size_t)std::max<uint32_t>(fin, 1) * 4);
+    if (!tiny) {
+        SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(fin, 1) * 4));
+        fill.add(p.keep.p, (size_t)std::max<uint32_t>(fin, 1) * 4);
+    }
     (void)D;
     return SKY_OK;
+}
+
+// the planned route's final read; a miss re-runs the query on the synchronised route
+static int plan_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSet &fill, uint32_t bound,
+                       uint32_t tiles, const PlanRun &pr) {
+    const int r = pipe_finish(c, p, in, tm, fill, true, bound, tiles, &pr);
+    if (r != kPlanMiss) {
+        p.last_planned = r == SKY_OK;
+        p.last_tiny = pr.tiny && r == SKY_OK;
+        return r;
+    }
+    p.plan.valid = false;                      // re-run on the synchronised route (learns a new plan)
+    p.plan_misses++;
+    const int r2 = pipe_run(c, p, in, tm);
+    p.last_plan_miss = true;
+    return r2;
+}
+
+// The planned route's tail in ONE launch (k_tiny_tail, sky_internal.h): the pruner slots, the
+// prefilter rounds, the brute pass, the fate tables, the output counts + offsets and the stats;
+// pipe_finish then runs only the output write pass and the final read.
+static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size_t cap, size_t cap_full,
+                         uint32_t tiles, FillSet &fill, const AppendArgs &ap) {
+    hipStream_t st = c.st;
+    const int D = c.D;
+    const Pipe::Plan pl = p.plan;
+    const int KM = p.Kp * p.M;
+    const size_t rb64 = row_bytes(true, D);
+    TinyArgs ta{};
+    ta.ap = ap;
+    ta.rounds = pl.rounds;
+    ta.M2 = std::min(prefilter_m2(), 2048 / p.Kp);
+    uint32_t bound = pl.bound[0];
+    ta.bound[0] = bound;
+    SKY_TRY(p.live.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
+    SKY_TRY(p.livepos.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
+    ta.live = p.live.as<uint32_t>();
+    ta.livepos = p.livepos.as<uint32_t>();
+    p.s_rows = &p.rows;
+    p.s_key = &p.sortkey;
+    p.s_src = &p.slot_src;
+    // survivors of round r: at most its input bound (a plan without rounds: the round the tail
+    // runs itself above kTinyForce slots, bound = the slots' bound)
+    const int nr = std::max(pl.rounds, 1);
+    for (int r = 0; r < nr; r++) {
+        DevBuf *dr = r & 1 ? &p.rows3 : &p.rows2, *dk = r & 1 ? &p.sortkey3 : &p.sortkey2,
+               *ds = r & 1 ? &p.slot_src3 : &p.slot_src2;
+        SKY_TRY(dr->ensure((size_t)bound * rb64));
+        SKY_TRY(dk->ensure((size_t)bound * 8));
+        SKY_TRY(ds->ensure((size_t)bound * 4));
+        ta.rows_r[r] = dr->as<double>();
+        ta.key_r[r] = dk->as<uint64_t>();
+        ta.src_r[r] = ds->as<uint32_t>();
+        if (r < pl.rounds) {                   // (after a tail-chosen round the final slots' arrays
+            p.s_rows = dr;                     // are known on the device only; nothing reads them)
+            p.s_key = dk;
+            p.s_src = ds;
+            bound = std::min(pl.bound[r + 1], bound);
+        }
+        ta.bound[r + 1] = bound;
+    }
+    SKY_TRY(p.slot_rep.ensure((size_t)std::max<uint32_t>(bound, 1) * 4));
+    SKY_TRY(p.alive_l.ensure(std::max<uint32_t>(bound, 1)));
+    SKY_TRY(p.alive_g.ensure(std::max<uint32_t>(bound, 1)));
+    SKY_TRY(p.pruner_fate.ensure(std::max<size_t>(KM, 1)));
+    SKY_TRY(p.out_cnt.ensure((size_t)tiles * 4));
+    SKY_TRY(p.out_off.ensure((size_t)tiles * 4));
+    SKY_TRY(p.statk.ensure((size_t)p.K * 16));
+    ta.totals = p.totals.as<uint32_t>();
+    ta.gmerge = in.global && !in.single;
+    ta.alive_l = p.alive_l.as<uint8_t>();
+    ta.alive_g = p.alive_g.as<uint8_t>();
+    ta.segalive = p.segalive.as<uint32_t>();   // zeroed by plan_prepare
+    ta.segn = p.seg_begin.as<uint32_t>();
+    ta.slot_rep = p.slot_rep.as<uint32_t>();
+    ta.status = p.status.as<uint16_t>();
+    ta.pruner_fate = p.pruner_fate.as<uint8_t>();
+    ta.K = p.K;
+    ta.tile_hist = p.tile_hist.as<uint32_t>();
+    ta.ntiles = tiles;
+    ta.out_cnt = p.out_cnt.as<uint32_t>();
+    ta.out_off = p.out_off.as<uint32_t>();
+    ta.statk = p.statk.as<unsigned long long>();
+#ifdef SKY_MEASURE
+    static const bool tchk = SKY_MEASURE_ENV("SKY_TINY_CHK") != nullptr;
+    if (tchk) {                                 // bounds-checked tail: every global index vs its capacity
+        {
+            const hipError_t e0 = hipStreamSynchronize(st);   // the launches before the tail
+            fprintf(stderr, "[tiny-chk] before the tail: %s\n", hipGetErrorString(e0));
+            if (e0 != hipSuccess) return SKY_E_HIP;
+        }
+        fprintf(stderr, "[tiny-chk] ptrs pr %p dup %p ent %p ps %p rows %p key %p src %p orand %p live %p lp %p "
+                        "r0 %p k0 %p s0 %p tot %p al %p ag %p sa %p sn %p rep %p st %p pf %p th %p oc %p oo %p sk %p\n",
+                (void *)ta.ap.pruners, (void *)ta.ap.dup_cnt, (void *)ta.ap.entries, (void *)ta.ap.pruner_slot,
+                ta.ap.rows, (void *)ta.ap.sortkey, (void *)ta.ap.slot_src, (void *)ta.ap.orand, (void *)ta.live,
+                (void *)ta.livepos, (void *)ta.rows_r[0], (void *)ta.key_r[0], (void *)ta.src_r[0], (void *)ta.totals,
+                (void *)ta.alive_l, (void *)ta.alive_g, (void *)ta.segalive, (void *)ta.segn, (void *)ta.slot_rep,
+                (void *)ta.status, (void *)ta.pruner_fate, (void *)ta.tile_hist, (void *)ta.out_cnt,
+                (void *)ta.out_off, (void *)ta.statk);
+        fprintf(stderr, "[tiny-chk] Kp %d M %d M2 %d K %d ntiles %u slot_cap %u D %d\n", ta.ap.Kp, ta.ap.M, ta.M2, ta.K,
+                ta.ntiles, ta.ap.slot_cap, D);
+        ta.chk = p.flags.as<uint32_t>() + 13;
+        ta.cap[0] = (uint32_t)cap;
+        ta.cap[1] = (uint32_t)(p.live.cap / 4);
+        ta.cap[2] = (uint32_t)(p.rows2.cap / rb64);
+        ta.cap[3] = (uint32_t)(p.rows3.cap / rb64);
+        ta.cap[4] = (uint32_t)(p.rows2.cap / rb64);
+        ta.cap[5] = (uint32_t)p.alive_l.cap;
+        ta.cap[6] = (uint32_t)(p.status.cap / 2);
+        ta.cap[7] = (uint32_t)(p.pr_entries.cap / 4);
+    }
+#endif
+#ifdef SKY_MEASURE
+    static const bool tclk = SKY_MEASURE_ENV("SKY_TINY_CLK") != nullptr;
+    if (tclk) {
+        SKY_TRY(p.dbg_clk.ensure(128));
+        HIP_TRY(hipMemsetAsync(p.dbg_clk.p, 0, 128, st));
+        ta.clk = p.dbg_clk.as<unsigned long long>();
+    }
+#endif
+    c.ktimer_begin("tiny", st);
+    launch_tiny_tail(D, ta, st);
+#ifdef SKY_MEASURE
+    if (tclk) {
+        unsigned long long t[10] = {};
+        HIP_TRY(hipMemcpyAsync(t, ta.clk, 80, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "[tiny-clk] us:");
+        for (int i = 1; i < 10; i++) fprintf(stderr, " %d:%.2f", i, t[i] && t[i - 1] ? (t[i] - t[i - 1]) / 100.0 : -1.0);
+        fprintf(stderr, " total %.2f\n", t[9] && t[0] ? (t[9] - t[0]) / 100.0 : -1.0);
+    }
+#endif
+    c.ktimer_end("tiny", st, bound);
+#ifdef SKY_MEASURE
+    if (tchk) {
+        uint32_t w = 0;
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(&w, ta.chk, 4, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[tiny-chk] bits 0x%x caps %u %u %u %u %u %u %u %u bounds %u %u rounds %d\n", w, ta.cap[0],
+                ta.cap[1], ta.cap[2], ta.cap[3], ta.cap[4], ta.cap[5], ta.cap[6], ta.cap[7], ta.bound[0], ta.bound[1],
+                ta.rounds);
+    }
+#endif
+    STAGE(st, "tiny tail");
+    p.plan_runs++;
+    p.tiny_runs++;
+    p.f64 = pl.f64;
+    p.ints = pl.ints;
+    if (tm) {
+        tm->mark(3, st);
+        tm->mark(4, st);
+        tm->mark(5, st);
+        tm->mark(6, st);
+    }
+    PlanRun pr;
+    pr.cap = cap;
+    pr.cap_full = cap_full;
+    pr.d_cnt = p.totals.as<uint32_t>() + 14;
+    pr.tiny = true;                            // exact f64 tests: no compare-type assumption
+    return plan_finish(c, p, in, tm, fill, bound, tiles, pr);
 }
 
 // The planned route (see pipe_run): the prefilter rounds and the brute pass of the last
 // query's small-set route, every launch sized by the plan's bounds and reading its count
 // from the device; no host synchronisation before pipe_finish's final read.
 static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size_t cap, size_t cap_full,
-                            uint32_t tiles, FillSet &fill) {
+                            uint32_t tiles, FillSet &fill, const AppendArgs *tiny_ap) {
     hipStream_t st = c.st;
     const int D = c.D;
     const Pipe::Plan pl = p.plan;
@@ -1073,6 +1252,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     p.s_src = &p.slot_src;
     const uint32_t *d_cnt = p.totals.as<uint32_t>() + 10;   // min(m + nps, cap), by k_append_pruners
     uint32_t bound = pl.bound[0];
+    if (tiny_ap) return pipe_run_tiny(c, p, in, tm, cap, cap_full, tiles, fill, *tiny_ap);
     for (int round = 0; round < pl.rounds; round++) {
         const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
         const int KM2 = p.Kp * M2;
@@ -1132,16 +1312,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     c.ktimer_end("brute", st, (int64_t)bound * bound);
     STAGE(st, "brute");
     if (tm) tm->mark(6, st);
-    const int r = pipe_finish(c, p, in, tm, fill, true, bound, tiles, &pr);
-    if (r != kPlanMiss) {
-        p.last_planned = r == SKY_OK;
-        return r;
-    }
-    p.plan.valid = false;                      // re-run on the synchronised route (learns a new plan)
-    p.plan_misses++;
-    const int r2 = pipe_run(c, p, in, tm);
-    p.last_plan_miss = true;
-    return r2;
+    return plan_finish(c, p, in, tm, fill, bound, tiles, pr);
 }
 
 // every buffer of a whole-stream run whose size follows the tuple count, sized for n tuples
@@ -1168,7 +1339,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     const uint32_t n = in.n;
     p.n = n;
     p.K = in.K;
-    p.last_planned = p.last_plan_miss = false;
+    p.last_planned = p.last_plan_miss = p.last_tiny = false;
     p.Kp = in.single ? 1 : c.Kq();
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;
@@ -1251,7 +1422,22 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     if (p.dom_km != KM) p.dom_kj = -1;
     // the planned route's counters and flags go out with this launch too: one criterion-minima
     // slice per prefilter round, the brute pass's domination bits and partition counts
-    if (planned) SKY_TRY(plan_prepare(p, D, fill));
+    // the planned route's tail in one workgroup (k_tiny_tail): the last query's final slots
+    // few, its first bound small, the output from the duplicate histograms, the shape within
+    // the kernel's LDS arena (SKY_TINY=0: the launch-per-stage tail, A/B knob)
+    // (a plan without prefilter rounds also tries it: the tail runs a round of its own, which may
+    // cut the slots to what it holds; not for kTinyBlock queries after such a try missed)
+    const bool tiny_try = p.plan.tiny || (p.plan.rounds == 0 && p.tiny_block == 0);
+    if (planned && p.tiny_block) p.tiny_block--;
+    const bool tiny = planned && tiny_try && !in.dist && p.hist_count &&
+                      (size_t)p.plan.bound[0] * rb64 <= kTinyCandBytes &&
+                      !tiny_disabled() &&
+                      tiny_fits(D, p.Kp, std::min(prefilter_m2(), 2048 / p.Kp), KM, in.K, tiles);
+    if (debug_level() >= 2 && p.plan.valid)
+        fprintf(stderr, "[sky] plan: planned %d tiny %d (plan.tiny %d hist %d bound0 %u rounds %d fits %d)\n",
+                (int)planned, (int)tiny, (int)p.plan.tiny, (int)p.hist_count, p.plan.bound[0], p.plan.rounds,
+                (int)tiny_fits(D, p.Kp, std::min(prefilter_m2(), 2048 / p.Kp), KM, in.K, tiles));
+    if (planned) SKY_TRY(plan_prepare(p, D, tiny, fill));
     HIP_TRY(fill.launch(st));
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
                           p.pruners.as<double>(), p.npr.as<int32_t>(), st);
@@ -1317,9 +1503,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     aa.orand = p.orand.as<unsigned long long>();
     aa.slot_cap = (uint32_t)cap;
     aa.mt_total = p.totals.as<uint32_t>() + 10;
-    launch_append_pruners(D, aa, st);
+    if (!tiny) launch_append_pruners(D, aa, st);
     STAGE(st, "compact");
-    if (planned) return pipe_run_planned(c, p, in, tm, cap, cap_full, tiles, fill);
+    if (planned) return pipe_run_planned(c, p, in, tm, cap, cap_full, tiles, fill, tiny ? &aa : nullptr);
     uint32_t m = 0, nps = 0, flags = 0;
     unsigned long long orand[2] = {0ull, 0ull};
     SKY_TRY(sync_read(p, st, {{p.totals.p, 4}, {p.totals.as<uint32_t>() + 5, 4}, {p.flags.p, 4}, {p.orand.p, 16}},
@@ -1353,7 +1539,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     // survivors are still too many for the brute path and the last round cut them by > 30 %
     int plan_rounds = 0;
     uint32_t plan_live[kPrefilterRounds] = {};
-    const bool pf_probe = !p.pf_skip || ++p.pf_since_probe >= kPrefilterProbe;
+    // (probed again every kPrefilterProbe queries, and as soon as the slot count moved more than
+    // 1/16 from the one it was learned on: a sliding window's candidates change under it)
+    const bool pf_moved = p.mt > p.pf_mt + p.pf_mt / 16 || p.mt + p.pf_mt / 16 < p.pf_mt;
+    const bool pf_probe = !p.pf_skip || pf_moved || ++p.pf_since_probe >= kPrefilterProbe;
     if (!pf_probe && p.mt >= kPrefilterMin) p.pf_skipped++;
     for (int round = 0; round < kPrefilterRounds && p.mt >= kPrefilterMin && !prefilter_disabled() && pf_probe;
          round++) {
@@ -1404,6 +1593,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             fprintf(stderr, "[sky] prefilter round %d: %u -> %u slots (M2=%d)\n", round, mt0, live_n, M2);
         if (round == 0) {                          // learn whether the next queries should run it
             p.pf_skip = (uint64_t)live_n * 100 > (uint64_t)mt0 * 97 && live_n > brute_max();
+            p.pf_mt = mt0;
             p.pf_since_probe = 0;
         }
         if (live_n <= brute_max() || (uint64_t)live_n * 10 > (uint64_t)mt0 * 7) break;
@@ -1425,6 +1615,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         p.plan.M = p.M;
         p.plan.single = in.single;
         p.plan.global = in.global;
+        p.plan.tiny = mt <= tiny_brute_rows(D) * 3 / 4;   // the final slots fit the one-workgroup tail
     }
     const size_t rb = row_bytes(p.f64, D);
     SKY_TRY(p.slot_rep.ensure(std::max<size_t>(mt, 1) * 4));

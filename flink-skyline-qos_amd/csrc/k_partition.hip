@@ -1563,6 +1563,375 @@ void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st) {
     SKY_DISPATCH_D(D, (k_filter_deferred<DD><<<dgrid, kThreads, lds, st>>>(a)));
 }
 
+
+// ---- the small planned route's tail in one workgroup (sky_internal.h TinyArgs) -------------
+// Phase for phase the kernels it replaces, restated over one workgroup: k_append_pruners,
+// per prefilter round k_cand_min / k_cand_pick / k_cand_filter / the scan / k_cand_compact,
+// the brute pair pass + k_brute_finish (exact f64 dominance tests instead of the packed / f32
+// compare types: the same answer for every row type), k_fate_tables (slot stats), and
+// k_out_hist_count + the tile scan + k_stat_reduce.  Data that the next phase reads stays in LDS
+// (minima, second-level pruners, the final slots, fates, tile counts, stats); the slot arrays
+// the output pass and the host read are written as those kernels write them.
+__device__ __forceinline__ uint32_t tiny_scan_excl(uint32_t v, uint32_t *s_w, uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kTinyThreads / 64; i++) {
+        const uint32_t c = s_w[i];
+        wb += i < w ? c : 0u;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return wb + inc - v;
+}
+
+
+#ifdef SKY_MEASURE
+#define TINY_OK(i, c, bit) \
+    ((uint64_t)(i) < (uint64_t)(c) ? true : (a.chk ? (atomicOr(a.chk, 1u << (bit)), false) : true))
+#define TINY_CLK(i) \
+    if (a.clk && threadIdx.x == 0) a.clk[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define TINY_OK(i, c, bit) true
+#define TINY_CLK(i)
+#endif
+
+template <int D>
+__global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
+    constexpr int DP = padded_dims<double>(D);
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_arena[];
+    __shared__ uint32_t s_w[kTinyThreads / 64];
+    __shared__ int32_t s_np[kMaxK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int NT = kTinyThreads, NW = kTinyThreads / 64;
+    const AppendArgs &ap = a.ap;
+    const int Kp = ap.Kp, M = ap.M, KM = Kp * M;
+    uint32_t lflags = 0;
+    TINY_CLK(0);
+
+    // ---- 1. one slot per duplicated pruner (k_append_pruners)
+    const uint32_t m = *ap.m_total;
+    uint32_t run = 0;
+    uint64_t o = 0, an = ~0ull;
+    for (int q0 = 0; q0 < KM; q0 += NT) {
+        const int q = q0 + tid;
+        const bool has = q < KM && ap.dup_cnt[q] > 0;
+        uint32_t tot;
+        const uint32_t e = run + tiny_scan_excl(has ? 1u : 0u, s_w, tot);
+        if (has) {
+            const uint32_t slot = m + e;
+            if (TINY_OK(e, a.cap[7], 0)) ap.entries[e] = q;
+            ap.pruner_slot[q] = (int32_t)slot;
+            if (slot < ap.slot_cap && TINY_OK(slot, a.cap[0], 0)) {
+                ap.slot_src[slot] = 0x80000000u | e;
+                const uint64_t key = emit_pruner<double, D>(ap.pruners + (size_t)q * D, q / M, (double *)ap.rows, slot,
+                                                            ap.sortkey, lflags);
+                o |= key;
+                an &= key;
+            }
+        } else if (q < KM) {
+            ap.pruner_slot[q] = -1;
+        }
+        run += tot;
+    }
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        o |= __shfl_xor(o, sh, 64);
+        an &= __shfl_xor(an, sh, 64);
+    }
+    if (lane == 0 && run) {
+        atomicOr(&ap.orand[0], (unsigned long long)o);
+        atomicAnd(&ap.orand[1], (unsigned long long)an);
+    }
+    uint32_t cnt = min(m + run, ap.slot_cap);            // slots written (the launches' device count)
+    if (tid == 0) {
+        *ap.nps_total = run;
+        a.totals[10] = cnt;
+    }
+    __syncthreads();
+    TINY_CLK(1);
+
+    // ---- 2. the prefilter rounds
+    const double *rows = reinterpret_cast<const double *>(ap.rows);
+    const uint64_t *keys = ap.sortkey;
+    const uint32_t *src = ap.slot_src;
+    const int M2 = a.M2, KM2 = Kp * M2;
+    uint32_t rcap = a.cap[0];                                     // (SKY_TINY_CHK) the current slot arrays
+    // a plan without prefilter rounds gets one here when its slots are more than a few: in LDS it
+    // costs a few microseconds and keeps the brute pass below (exact either way) small
+    const int rounds = a.rounds ? a.rounds : (cnt > kTinyForce ? 1 : 0);
+    for (int r = 0; r < rounds; r++) {
+        const uint32_t wcap = r == 0 ? a.cap[2] : (r == 1 ? a.cap[3] : a.cap[4]);
+        const uint32_t mt = min(a.bound[r], cnt);
+        unsigned long long *s_min = reinterpret_cast<unsigned long long *>(s_arena);        // [KM2]
+        float *s_wt = reinterpret_cast<float *>(s_min + KM2);                               // [M2][D]
+        double *s_pr = reinterpret_cast<double *>(s_wt + ((M2 * D + 3) & ~3));             // [KM2][D]
+        for (int q = tid; q < KM2; q += NT) s_min[q] = ~0ull;
+        for (int q = tid; q < M2 * D; q += NT) s_wt[q] = cand_weight(q / D, q % D, D);
+        __syncthreads();
+        // k_cand_min: per (partition, criterion) the minimising slot
+        for (uint32_t j = tid; j < mt; j += NT) {
+            if (!TINY_OK(j, rcap, 1)) continue;
+            const int k = (int)(keys[j] >> 56);
+            if (!TINY_OK(k, Kp, 12)) continue;
+            double v[D];
+            load_trow<double, D>(rows + (size_t)j * DP, v);
+            float f[D];
+#pragma unroll
+            for (int d = 0; d < D; d++) f[d] = (float)v[d];
+            for (int c = 0; c < M2; c++) {
+                float cv = 0.0f;
+#pragma unroll
+                for (int d = 0; d < D; d++) cv += s_wt[c * D + d] * f[d];
+                if (cv != cv) continue;
+                const unsigned long long e = ((unsigned long long)f32_order_key(cv) << 32) | j;
+                unsigned long long *mp = &s_min[k * M2 + c];
+                if (e < *mp) atomicMin(mp, e);
+            }
+        }
+        __syncthreads();
+        TINY_CLK(2);
+        // k_cand_pick: one wave per partition, winners deduplicated and mutually non-dominated
+        for (int k = wave; k < Kp; k += NW) {
+            const unsigned long long w = lane < M2 ? s_min[k * M2 + lane] : ~0ull;
+            const bool has = w != ~0ull && TINY_OK((uint32_t)(w & 0xffffffffu), rcap, 2);
+            double c[D];
+            if (has) {
+                load_trow<double, D>(rows + (size_t)(uint32_t)(w & 0xffffffffu) * DP, c);
+            } else {
+#pragma unroll
+                for (int d = 0; d < D; d++) c[d] = 0.0;
+            }
+            const uint64_t hm = __ballot(has);
+            bool ok = has;
+            for (int q = 0; q < M2; q++) {
+                bool le = true, lt = false, eq = true;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    const double x = __shfl(c[d], q, 64);
+                    le &= x <= c[d];
+                    lt |= x < c[d];
+                    eq &= x == c[d];
+                }
+                if (q != lane && ((hm >> q) & 1ull) && ((le && lt) || (eq && q < lane))) ok = false;
+            }
+            const uint64_t b = __ballot(ok);
+            if (ok) {
+                const int pos = (int)lanes_below(b);
+#pragma unroll
+                for (int d = 0; d < D; d++) s_pr[((size_t)k * M2 + pos) * D + d] = c[d];
+            }
+            if (lane == 0) s_np[k] = __popcll(b);
+        }
+        __syncthreads();
+        TINY_CLK(3);
+        // k_cand_filter + scan + k_cand_compact: the live slots in slot order
+        double *rows2 = a.rows_r[r];
+        uint64_t *key2 = a.key_r[r];
+        uint32_t *src2 = a.src_r[r];
+        uint32_t base = 0;
+        for (uint32_t j0 = 0; j0 < mt; j0 += NT) {                 // block-uniform
+            const uint32_t j = j0 + tid;
+            bool liv = false;
+            double v[D];
+            if (j < mt && TINY_OK(j, rcap, 3)) {
+                const int k = (int)(keys[j] >> 56);
+                load_trow<double, D>(rows + (size_t)j * DP, v);
+                const double *pr = s_pr + (size_t)k * M2 * D;
+                bool dom = false;
+                for (int q = 0; q < s_np[k]; q++) {
+                    bool le = true, lt = false;
+#pragma unroll
+                    for (int d = 0; d < D; d++) {
+                        const double x = pr[q * D + d];
+                        le &= x <= v[d];
+                        lt |= x < v[d];
+                    }
+                    dom |= le & lt;
+                }
+                liv = !dom;
+            }
+            uint32_t tot;
+            const uint32_t pos = base + tiny_scan_excl(liv ? 1u : 0u, s_w, tot);
+            if (j < mt && TINY_OK(j, a.cap[1], 4)) {
+                a.live[j] = liv ? 1u : 0u;
+                a.livepos[j] = pos;
+                if (liv && TINY_OK(pos, wcap, 5) && TINY_OK(j, rcap, 3)) {
+                    const double2 *s2 = reinterpret_cast<const double2 *>(rows + (size_t)j * DP);
+                    double2 *d2 = reinterpret_cast<double2 *>(rows2 + (size_t)pos * DP);
+#pragma unroll
+                    for (int q = 0; q < DP / 2; q++) d2[q] = s2[q];
+                    key2[pos] = keys[j];
+                    src2[pos] = src[j];
+                }
+            }
+            base += tot;
+        }
+        __syncthreads();
+        TINY_CLK(4);
+        for (int q = tid; q < KM; q += NT) {
+            const int32_t ps = ap.pruner_slot[q];
+            if (ps >= 0 && TINY_OK((uint32_t)ps < mt ? ps : 0, a.cap[1], 6))
+                ap.pruner_slot[q] = (uint32_t)ps < mt && a.live[ps] ? (int32_t)a.livepos[ps] : -1;
+        }
+        if (tid == 0) a.totals[11 + r] = base;
+        cnt = base;
+        rows = rows2;
+        keys = key2;
+        src = src2;
+        rcap = wcap;
+        __syncthreads();
+        TINY_CLK(5);
+    }
+
+    // ---- 3. the brute pair pass over the final slots (exact f64 tests) + k_brute_finish
+    const uint32_t fin = min(a.bound[rounds], cnt);
+    if (tid == 0) a.totals[14] = fin;
+    constexpr uint32_t BR = tiny_brute_rows(D);
+    if (fin > BR) {                                                // block-uniform
+        if (tid == 0) atomicOr(ap.flags, kFlagTinyMiss);
+        return;
+    }
+    double *s_row = reinterpret_cast<double *>(s_arena);                          // [BR][D]
+    uint32_t *s_part = reinterpret_cast<uint32_t *>(s_row + (size_t)BR * D);       // [BR]
+    uint32_t *s_dom = s_part + BR;                                                 // [BR]
+    unsigned long long *s_l = reinterpret_cast<unsigned long long *>(s_dom + BR);   // [kMaxK]
+    unsigned long long *s_s = s_l + kMaxK;                                         // [kMaxK]
+    uint32_t *s_tc = reinterpret_cast<uint32_t *>(s_s + kMaxK);                   // [kTinyTiles]
+    uint32_t *s_sn = s_tc + kTinyTiles, *s_sa = s_sn + kMaxK;                       // [kMaxK] x 2
+    uint8_t *s_pf = reinterpret_cast<uint8_t *>(s_sa + kMaxK);                     // [kHistMaxKM]
+    for (uint32_t q = tid; q < fin * D; q += NT)
+        s_row[q] = TINY_OK(q / D, rcap, 7) ? rows[(size_t)(q / D) * DP + q % D] : 0.0;
+    for (uint32_t q = tid; q < fin; q += NT) {
+        s_part[q] = TINY_OK(q, rcap, 7) ? (uint32_t)(keys[q] >> 56) : 0u;
+        if (!TINY_OK(s_part[q], Kp, 13)) s_part[q] = 0;
+        s_dom[q] = 0u;
+    }
+    for (int q = tid; q < kMaxK; q += NT) {
+        s_l[q] = 0;
+        s_s[q] = 0;
+        s_sn[q] = 0;
+        s_sa[q] = 0;
+    }
+    for (uint32_t q = tid; q < a.ntiles; q += NT) s_tc[q] = 0u;
+    __syncthreads();
+    TINY_CLK(6);
+    for (uint32_t pq = tid; pq < fin * fin; pq += NT) {
+        const uint32_t y = pq / fin, x = pq - y * fin;
+        if (x == y) continue;
+        bool le = true, lt = false;
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const double xv = s_row[x * D + d], yv = s_row[y * D + d];
+            le &= xv <= yv;
+            lt |= xv < yv;
+        }
+        if (le & lt) atomicOr(&s_dom[y], s_part[x] == s_part[y] ? 3u : 2u);
+    }
+    __syncthreads();
+    TINY_CLK(7);
+    for (uint32_t j = tid; j < fin; j += NT) {
+        const uint32_t f = s_dom[j];
+        const bool in_l = !(f & 1u);
+        const bool in_g = a.gmerge ? !(f & 2u) : in_l;
+        if (TINY_OK(j, a.cap[5], 8)) {
+            a.alive_l[j] = in_l ? 1 : 0;
+            a.alive_g[j] = in_g ? 1 : 0;
+            a.slot_rep[j] = j;
+        }
+        s_dom[j] = (in_l ? 1u : 0u) | (in_g ? 2u : 0u);           // from here on: the slot's fate
+        atomicAdd(&s_sn[s_part[j]], 1u);
+        if (in_l) atomicAdd(&s_sa[s_part[j]], 1u);
+    }
+    __syncthreads();
+    for (int q = tid; q < Kp; q += NT) {
+        if (s_sn[q]) atomicAdd(&a.segn[q], s_sn[q]);
+        if (s_sa[q]) atomicAdd(&a.segalive[q], s_sa[q]);
+    }
+
+    // ---- 4. the fate tables (k_fate_tables, slot stats)
+    for (uint32_t j = tid; j < fin; j += NT) {
+        if (!TINY_OK(j, rcap, 9)) continue;
+        const uint32_t sj = src[j];
+        if (sj & 0x80000000u) continue;                            // appended pruner slots: below
+        if (!TINY_OK(sj, a.cap[6], 10)) continue;
+        const uint32_t f = s_dom[j];
+        const uint16_t s0 = a.status[sj];
+        a.status[sj] = (uint16_t)((s0 & 0xff00u) | (kCodeFate0 + f));
+        if ((f & 2u) && TINY_OK(sj / kTile, a.ntiles, 11)) atomicAdd(&s_tc[sj / kTile], 1u);
+        const int k = s0 >> 8;
+        if (!TINY_OK(k, a.K, 14)) continue;
+        if (f & 1u) {
+            atomicAdd(&s_l[k], 1ull);
+            if (f & 2u) atomicAdd(&s_s[k], 1ull);
+        }
+    }
+    for (int q = tid; q < KM; q += NT) {
+        const int32_t ps = ap.pruner_slot[q];
+        uint32_t f = 0;
+        if (ps >= 0 && (uint32_t)ps < fin) {
+            f = s_dom[ps];
+            const unsigned long long w = ap.dup_cnt[q];
+            const int k = q / M;
+            if (f & 1u) {
+                atomicAdd(&s_l[k], w);
+                if (f & 2u) atomicAdd(&s_s[k], w);
+            }
+        }
+        a.pruner_fate[q] = (uint8_t)f;
+        s_pf[q] = (uint8_t)f;
+    }
+    __syncthreads();
+    TINY_CLK(8);
+    for (int q = tid; q < a.K; q += NT) {                          // k_stat_reduce
+        a.statk[q] = s_l[q];
+        a.statk[a.K + q] = s_s[q];
+    }
+
+    // ---- 5. per-tile output counts (k_out_hist_count) and their exclusive scan
+    uint32_t base = 0;
+    for (uint32_t t0 = 0; t0 < a.ntiles; t0 += NT) {                // block-uniform
+        const uint32_t t = t0 + tid;
+        uint32_t c = 0;
+        if (t < a.ntiles) {
+            const uint32_t *h = a.tile_hist + (size_t)t * KM;
+            for (int q = 0; q < KM; q++) c += (s_pf[q] & 2u) ? h[q] : 0u;
+            c += s_tc[t];
+        }
+        uint32_t tot;
+        const uint32_t off = base + tiny_scan_excl(c, s_w, tot);
+        if (t < a.ntiles) {
+            a.out_cnt[t] = c;
+            a.out_off[t] = off;
+        }
+        base += tot;
+    }
+    if (tid == 0) a.totals[3] = base;
+    if (lflags) atomicOr(ap.flags, lflags);
+    TINY_CLK(9);
+}
+
+bool tiny_fits(int D, int Kp, int M2, int KM, int K, uint32_t tiles) {
+    const size_t KM2 = (size_t)Kp * M2;
+    const size_t pre = KM2 * 8 + (size_t)((M2 * D + 3) & ~3) * 4 + KM2 * D * 8;
+    const size_t brute = (size_t)tiny_brute_rows(D) * (D * 8 + 8) + kTinyFixed;
+    return M2 <= 64 && KM <= kHistMaxKM && K <= kMaxK && Kp <= kMaxK && tiles <= kTinyTiles &&
+           pre <= kTinyArena && brute <= kTinyArena;
+}
+
+void launch_tiny_tail(int D, const TinyArgs &a, hipStream_t st) {
+    SKY_DISPATCH_D(D, (k_tiny_tail<DD><<<1, kTinyThreads, kTinyArena, st>>>(a)));
+}
+
 void launch_append_pruners(int D, const AppendArgs &a, hipStream_t st) {
     SKY_DISPATCH_D(D, (k_append_pruners<DD><<<1, kThreads, 0, st>>>(a)));
 }

@@ -450,3 +450,62 @@ void launch_csv_fmt_write(const int64_t *ids, const double *vals, int64_t n, int
                           uint8_t *text, hipStream_t st);
 
 }  // namespace sky
+
+namespace sky {
+
+// ---- the small planned route's tail in ONE workgroup (k_partition.hip k_tiny_tail) ----
+// Everything between the filter and the output write pass of a planned query whose candidate
+// slot rows are few (bound[0] rows of f64 <= kTinyCandBytes: the prefilter passes read them from
+// one CU) and whose last query ended with <= 3/4 of tiny_brute_rows(D) slots:
+// append the duplicated pruners, the prefilter rounds, the brute pair pass (exact f64 tests),
+// the fate tables, the per-tile output counts + their scan and the stats -- one launch instead
+// of ~12 dependent launches of 2-6 us each, its phases' data kept in LDS.  If the final slots
+// exceed tiny_brute_rows(D) the kernel raises kFlagTinyMiss and writes no fate: the host re-runs the
+// query on the synchronised route.
+constexpr size_t kTinyCandBytes = 512 * 1024;
+constexpr uint32_t kTinyTiles = 4096;
+// LDS arena of the tail (bytes): the prefilter phase (minima, weights, second-level pruners) and
+// the brute / fate phase (final rows + partition + fate per slot, then per-partition stats and
+// counts, per-tile counts, pruner fates) reuse it; the final slots it holds follow from D
+constexpr size_t kTinyArena = 56 * 1024;
+constexpr size_t kTinyFixed = (size_t)kMaxK * 24 + (size_t)kTinyTiles * 4 + kHistMaxKM;
+constexpr uint32_t tiny_brute_rows(int D) {
+    return (kTinyArena - kTinyFixed) / (D * 8 + 8) < 512 ? (uint32_t)((kTinyArena - kTinyFixed) / (D * 8 + 8)) : 512u;
+}
+constexpr int kTinyThreads = 1024;
+constexpr uint32_t kTinyForce = 192;      // a plan without rounds: the tail runs one above this many slots
+constexpr uint32_t kFlagTinyMiss = 64u;
+struct TinyArgs {
+    AppendArgs ap;                        // rows / sortkey / slot_src: the filter's slots
+    int rounds = 0, M2 = 0;
+    uint32_t bound[4] = {};               // plan bounds (slots entering round r; [rounds]: the brute)
+    double *pr2 = nullptr;                // [Kp*M2][D] second-level pruners (scratch)
+    uint32_t *live = nullptr, *livepos = nullptr;        // [bound0] scratch
+    double *rows_r[3] = {};               // the rounds' compaction targets (f64 slot rows)
+    uint64_t *key_r[3] = {};
+    uint32_t *src_r[3] = {};
+    // [10] slots, [11 + r] survivors of round r, [14] the final slots, [3] output total
+    uint32_t *totals = nullptr;
+    bool gmerge = false;
+    uint8_t *alive_l = nullptr, *alive_g = nullptr;
+    uint32_t *segalive = nullptr, *segn = nullptr, *slot_rep = nullptr;
+    // fate tables (FateArgs semantics, slot stats), output counts
+    uint16_t *status = nullptr;
+    uint8_t *pruner_fate = nullptr;
+    int K = 1;
+    const uint32_t *tile_hist = nullptr;
+    uint32_t ntiles = 0;
+    uint32_t *out_cnt = nullptr, *out_off = nullptr;
+    unsigned long long *statk = nullptr;  // [2K]: |L_k|, survivors_k
+    // measurement builds (SKY_TINY_CHK): every global index checked against its buffer's
+    // capacity, an out-of-range access skipped and reported as a bit of *chk.  cap: slots,
+    // live, rows_r[0..2] (slots), final slots, status words, Kp*M
+    uint32_t *chk = nullptr;
+    uint32_t cap[8] = {};
+    unsigned long long *clk = nullptr;    // (SKY_TINY_CLK) s_memrealtime at the phase ends, [10]
+};
+void launch_tiny_tail(int D, const TinyArgs &a, hipStream_t st);
+// the tail's LDS arena holds both phases' data for this shape (host check before the launch)
+bool tiny_fits(int D, int Kp, int M2, int KM, int K, uint32_t tiles);
+
+}  // namespace sky

@@ -131,3 +131,56 @@ def test_plan_disabled_equals(gpu_engine_factory, oracle):
         eng.close()
     finally:
         del os.environ["SKY_PLAN"]
+
+
+TINY = 32
+
+
+@pytest.mark.parametrize("algo,dist,D,n,P", [("mr-dim", 0, 2, 1000000, 8), ("mr-angle", 1, 2, 100000, 8),
+                                             ("mr-grid", 0, 2, 200000, 16), ("mr-grid", 1, 3, 100000, 8)])
+def test_tiny_tail_equals_oracle(gpu_engine_factory, oracle, algo, dist, D, n, P):
+    """Few final slots: the planned replay runs its whole tail (pruner slots, prefilter rounds,
+    brute pass, fate tables, output counts, stats) as ONE workgroup (k_tiny_tail, counters[7]
+    bit 5); every answer equals the oracle's, and equals SKY_TINY=0's launch-per-stage tail."""
+    short = algo.split("-")[1]
+    eng = gpu_engine_factory(D, P, algo)
+    check(eng, oracle, oracle.synth(dist, D, n, seed=81), P, short)
+    tiny = 0
+    for seed in (82, 83, 84):
+        r, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=seed), P, short)
+        tiny += bool(r & TINY)
+        assert not (r & TINY) or r & PLANNED
+    assert tiny >= 2, "the one-workgroup tail did not run"
+    os.environ["SKY_TINY"] = "0"
+    try:
+        r, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=85), P, short)
+        assert not r & TINY
+    finally:
+        del os.environ["SKY_TINY"]
+    eng.close()
+
+
+def test_tiny_tail_prefilter_round(gpu_engine_factory, oracle):
+    """C1's shape: >= 4096 candidate slots (kPrefilterMin), so the learned route has a prefilter
+    round that the one-workgroup tail replays (in-LDS criterion minima, pick, compaction)."""
+    eng = gpu_engine_factory(2, 8, "mr-dim")
+    check(eng, oracle, oracle.synth(0, 2, 1000000, seed=91), 8, "dim")
+    for seed in (92, 93):
+        r, m = check(eng, oracle, oracle.synth(0, 2, 1000000, seed=seed), 8, "dim")
+        assert m >= 4096 and r & TINY, (r, m)
+    eng.close()
+
+
+def test_tiny_tail_miss(gpu_engine_factory, oracle):
+    """A stream whose final slots outgrow the tail's LDS even after the prefilter round it runs
+    itself (3D independent, 20k tuples, ~600 slots): the tail raises its miss flag, nothing it
+    wrote is used, the query re-runs synchronised with the oracle's answer, and the next queries
+    (kTinyBlock) do not try the tail."""
+    eng = gpu_engine_factory(3, 8, "mr-angle")
+    check(eng, oracle, oracle.synth(0, 3, 20000, seed=81), 8)
+    r, m = check(eng, oracle, oracle.synth(0, 3, 20000, seed=82), 8)
+    assert r & MISSED and not r & TINY, (r, m)
+    for seed in (83, 84):
+        r, _ = check(eng, oracle, oracle.synth(0, 3, 20000, seed=seed), 8)
+        assert r & PLANNED and not r & TINY, r
+    eng.close()
