@@ -167,8 +167,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm);
 int pipe_reserve(Ctx &c, Pipe &p, uint32_t n);
 // SKY_MBR_LPT=0 turns the bounding-box pass's cost-ordered work queue off (A/B knob)
 // read device ranges into host memory in one synchronisation (one gather launch when they are small)
+// prewritten: a kernel of the run already wrote the words into p.pin (this layout); only the
+// synchronisation and the unpacking remain
 int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
-              std::vector<void *> dsts);
+              std::vector<void *> dsts, bool prewritten = false);
 // the designated duplicate group of the next run's status planes, from p.h_dup
 void pick_dom_group(Pipe &p, int KM);
 // stream-ordered output of the tuples selected by the last run

@@ -571,8 +571,18 @@ static int sfs_run16(Ctx &c, Pipe &p, const uint32_t *rows16, uint32_t nrep, std
 }
 
 int sync_read(Pipe &p, hipStream_t st, const std::vector<std::pair<const void *, size_t>> &srcs,
-              std::vector<void *> dsts) {
+              std::vector<void *> dsts, bool prewritten) {
     p.host_syncs++;
+    if (prewritten) {                   // a kernel of the run wrote the words into p.pin itself
+        HIP_TRY(hipStreamSynchronize(st));
+        p.up_used = 0;
+        size_t off = 0;
+        for (size_t i = 0; i < srcs.size(); i++) {
+            if (srcs[i].second) memcpy(dsts[i], (char *)p.pin + off, srcs[i].second);
+            off += (srcs[i].second + 15) & ~size_t(15);
+        }
+        return SKY_OK;
+    }
     size_t tot = 0;
     for (auto &s : srcs) tot += (s.second + 15) & ~size_t(15);
     SKY_TRY(p.pinned(tot));
@@ -926,10 +936,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         uint32_t flags2 = 0, tot[16] = {};
         p.h_seg_n.assign(p.Kp, 0u);
         p.h_dup.assign(KM, 0u);
+        // (the one-workgroup tail wrote these words into p.pin in this layout: tiny_pin_layout)
         SKY_TRY(sync_read(p, st, {{p.totals.p, 64}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
                                   {p.flags.p, 4}, {p.dup_cnt.p, (size_t)KM * 4}},
-                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}));
+                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}, tiny));
         nout = tot[3];
 #ifdef SKY_MEASURE
         if (SKY_MEASURE_ENV("SKY_FILTER_COUNT")) {   // k_filter's stores (tools/: the write itemisation)
@@ -1154,6 +1165,8 @@ static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size
     ta.out_cnt = p.out_cnt.as<uint32_t>();
     ta.out_off = p.out_off.as<uint32_t>();
     ta.statk = p.statk.as<unsigned long long>();
+    SKY_TRY(p.pinned(tiny_pin_layout(p.K, p.Kp, KM, ta.pin_off)));   // the final read, written by the tail
+    ta.pin = reinterpret_cast<uint32_t *>(p.pin);
 #ifdef SKY_MEASURE
     static const bool tchk = SKY_MEASURE_ENV("SKY_TINY_CHK") != nullptr;
     if (tchk) {                                 // bounds-checked tail: every global index vs its capacity
@@ -1185,6 +1198,10 @@ static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size
 #endif
 #ifdef SKY_MEASURE
     static const bool tclk = SKY_MEASURE_ENV("SKY_TINY_CLK") != nullptr;
+    {
+        const char *e = SKY_MEASURE_ENV("SKY_TINY_DBG");
+        ta.dbg = e ? atoi(e) : 0;
+    }
     if (tclk) {
         SKY_TRY(p.dbg_clk.ensure(128));
         HIP_TRY(hipMemsetAsync(p.dbg_clk.p, 0, 128, st));
@@ -1439,8 +1456,9 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 (int)tiny_fits(D, p.Kp, std::min(prefilter_m2(), 2048 / p.Kp), KM, in.K, tiles));
     if (planned) SKY_TRY(plan_prepare(p, D, tiny, fill));
     HIP_TRY(fill.launch(st));
+    // the sample minima only: the filter's workgroups pick the pruners from them (one launch less)
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
-                          p.pruners.as<double>(), p.npr.as<int32_t>(), st);
+                          p.pruners.as<double>(), p.npr.as<int32_t>(), st, false);
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
@@ -1469,6 +1487,10 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.tile_hist = p.hist_count ? p.tile_hist.as<uint32_t>() : nullptr;
     fa.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
     fa.dom_kj = p.dom_kj;
+    fa.pick_gmin = p.pmin.as<unsigned long long>();
+    fa.pick_S = S;
+    fa.pruners_w = p.pruners.as<double>();
+    fa.npr_w = p.npr.as<int32_t>();
     {
         static const int fdbg = [] { const char *e = SKY_MEASURE_ENV("SKY_FILTER_DBG"); return e ? atoi(e) : 0; }();
         fa.dbg = fdbg;
@@ -1482,7 +1504,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     c.ktimer_begin("filter", st);
     launch_filter(D, fa, st);
     c.ktimer_end("filter", st, n);
-    if (angle_keys) launch_filter_deferred(D, fa, st);
+    if (angle_keys) {
+        FilterArgs fd = fa;                    // the pruners are in place by now (filter workgroup 0)
+        fd.pick_gmin = nullptr;
+        launch_filter_deferred(D, fd, st);
+    }
     STAGE(st, "filter");
     if (tm) tm->mark(2, st);
 

@@ -370,6 +370,53 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
                                                  int ndup_arrays = 1) {
     const int nprw = a.Kp * a.M;
     const int MD = a.M * D;
+    if (a.pick_gmin) {
+        // k_pick_pruners per workgroup: one wave per partition, lane j = criterion j's sample
+        // winner; duplicates keep the first, winners another winner dominates are dropped
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        for (int k = wave; k < a.Kp; k += kThreads / 64) {
+            const unsigned long long w = lane < a.M ? a.pick_gmin[k * a.M + lane] : ~0ull;
+            const bool has = w != ~0ull;
+            double c[D];
+            if (has) {
+                const uint32_t i = (uint32_t)(((uint64_t)(uint32_t)(w & 0xffffffffu) * a.n) / a.pick_S);
+#pragma unroll
+                for (int d = 0; d < D; d++) c[d] = a.vals[(size_t)i * D + d];
+            } else {
+#pragma unroll
+                for (int d = 0; d < D; d++) c[d] = 0.0;
+            }
+            const uint64_t hm = __ballot(has);
+            bool ok = has;
+            for (int q = 0; q < a.M; q++) {
+                bool le = true, lt = false, eq = true;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    const double x = __shfl(c[d], q, 64);
+                    le &= x <= c[d];
+                    lt |= x < c[d];
+                    eq &= x == c[d];
+                }
+                if (q != lane && ((hm >> q) & 1ull) && ((le && lt) || (eq && q < lane))) ok = false;
+            }
+            const uint64_t b = __ballot(ok);
+            if (ok) {
+                const int pos = (int)lanes_below(b);
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    s_pr[k * pr_stride<D>(a.M) + pr_off<D>(k, pos, d)] = c[d];
+                    if (blockIdx.x == 0) a.pruners_w[((size_t)k * a.M + pos) * D + d] = c[d];
+                }
+            }
+            if (lane == 0) {
+                s_npr[k] = __popcll(b);
+                if (blockIdx.x == 0) a.npr_w[k] = __popcll(b);
+            }
+        }
+        for (int q = threadIdx.x; q < nprw * ndup_arrays; q += kThreads) s_dup[q] = 0;
+        __syncthreads();
+        return;
+    }
     for (int q = threadIdx.x; q < nprw * D; q += kThreads) {
         const int k = q / MD, r = q - k * MD;
         s_pr[k * pr_stride<D>(a.M) + pr_off<D>(k, r / D, r % D)] = a.pruners[q];
@@ -1525,7 +1572,7 @@ void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int
 
 void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
-                           double *pruners, int32_t *npr, hipStream_t st) {
+                           double *pruners, int32_t *npr, hipStream_t st, bool pick) {
     if (S == 0) return;                               // gmin: all-ones on entry (the caller's fill)
     static const unsigned sgrid = [] {        // SKY_SAMPLE_WG: workgroups of the sample pass (A/B knob)
         const char *e = SKY_MEASURE_ENV("SKY_SAMPLE_WG");
@@ -1533,7 +1580,7 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
     }();
     const unsigned g = std::min<unsigned>(nblk(S, kThreads), sgrid);
     SKY_DISPATCH_D(D, (k_sample_min<DD><<<g, kThreads, 0, st>>>(vals, n, S, kp, given_keys, single, Kp, M, gmin)));
-    SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
+    if (pick) SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
@@ -1611,10 +1658,18 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_arena[];
     __shared__ uint32_t s_w[kTinyThreads / 64];
     __shared__ int32_t s_np[kMaxK];
+    __shared__ uint32_t s_fl;
+    // the pruner slot table, the entry -> pruner map and the duplicate counts stay in LDS for the
+    // whole tail (no dependent global round trips for them: one workgroup is latency-bound)
+    __shared__ int32_t s_ps[kHistMaxKM], s_ps2[kHistMaxKM];
+    __shared__ uint16_t s_ent[kHistMaxKM];
+    __shared__ uint32_t s_dupc[kHistMaxKM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_fl = 0u;
     constexpr int NT = kTinyThreads, NW = kTinyThreads / 64;
     const AppendArgs &ap = a.ap;
     const int Kp = ap.Kp, M = ap.M, KM = Kp * M;
+    constexpr int TU = 16 / DP > 0 ? 16 / DP : 1;                 // slot rows per thread and batch
     uint32_t lflags = 0;
     TINY_CLK(0);
 
@@ -1624,13 +1679,16 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     uint64_t o = 0, an = ~0ull;
     for (int q0 = 0; q0 < KM; q0 += NT) {
         const int q = q0 + tid;
-        const bool has = q < KM && ap.dup_cnt[q] > 0;
+        const uint32_t dc = q < KM ? ap.dup_cnt[q] : 0u;
+        const bool has = dc > 0;
+        if (q < KM) s_dupc[q] = dc;
         uint32_t tot;
         const uint32_t e = run + tiny_scan_excl(has ? 1u : 0u, s_w, tot);
         if (has) {
             const uint32_t slot = m + e;
             if (TINY_OK(e, a.cap[7], 0)) ap.entries[e] = q;
-            ap.pruner_slot[q] = (int32_t)slot;
+            s_ent[e] = (uint16_t)q;
+            s_ps[q] = (int32_t)slot;
             if (slot < ap.slot_cap && TINY_OK(slot, a.cap[0], 0)) {
                 ap.slot_src[slot] = 0x80000000u | e;
                 const uint64_t key = emit_pruner<double, D>(ap.pruners + (size_t)q * D, q / M, (double *)ap.rows, slot,
@@ -1639,7 +1697,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
                 an &= key;
             }
         } else if (q < KM) {
-            ap.pruner_slot[q] = -1;
+            s_ps[q] = -1;
         }
         run += tot;
     }
@@ -1664,45 +1722,80 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     const double *rows = reinterpret_cast<const double *>(ap.rows);
     const uint64_t *keys = ap.sortkey;
     const uint32_t *src = ap.slot_src;
-    const int M2 = a.M2, KM2 = Kp * M2;
-    uint32_t rcap = a.cap[0];                                     // (SKY_TINY_CHK) the current slot arrays
+    constexpr int M2 = kTinyM2;                                    // (tiny_fits: a.M2 == kTinyM2)
+    [[maybe_unused]] uint32_t rcap = a.cap[0];                                     // (SKY_TINY_CHK) the current slot arrays
     // a plan without prefilter rounds gets one here when its slots are more than a few: in LDS it
     // costs a few microseconds and keeps the brute pass below (exact either way) small
     const int rounds = a.rounds ? a.rounds : (cnt > kTinyForce ? 1 : 0);
     for (int r = 0; r < rounds; r++) {
         const uint32_t wcap = r == 0 ? a.cap[2] : (r == 1 ? a.cap[3] : a.cap[4]);
         const uint32_t mt = min(a.bound[r], cnt);
-        unsigned long long *s_min = reinterpret_cast<unsigned long long *>(s_arena);        // [KM2]
-        float *s_wt = reinterpret_cast<float *>(s_min + KM2);                               // [M2][D]
-        double *s_pr = reinterpret_cast<double *>(s_wt + ((M2 * D + 3) & ~3));             // [KM2][D]
-        for (int q = tid; q < KM2; q += NT) s_min[q] = ~0ull;
+        // per-partition strides padded by one element: lanes of different partitions read
+        // different banks (unpadded, every partition's row started on the same bank)
+        const int MS = M2 + 1, PS = M2 * D + 1;
+        unsigned long long *s_min = reinterpret_cast<unsigned long long *>(s_arena);        // [Kp][MS]
+        float *s_wt = reinterpret_cast<float *>(s_min + Kp * MS);                           // [M2][D]
+        double *s_pr = reinterpret_cast<double *>(s_wt + ((M2 * D + 3) & ~3));             // [Kp][PS]
+        for (int q = tid; q < Kp * MS; q += NT) s_min[q] = ~0ull;
         for (int q = tid; q < M2 * D; q += NT) s_wt[q] = cand_weight(q / D, q % D, D);
         __syncthreads();
-        // k_cand_min: per (partition, criterion) the minimising slot
-        for (uint32_t j = tid; j < mt; j += NT) {
-            if (!TINY_OK(j, rcap, 1)) continue;
-            const int k = (int)(keys[j] >> 56);
-            if (!TINY_OK(k, Kp, 12)) continue;
-            double v[D];
-            load_trow<double, D>(rows + (size_t)j * DP, v);
-            float f[D];
+        // k_cand_min: per (partition, criterion) the minimising slot; TU rows per thread and
+        // batch, all their loads issued before the first is used: one workgroup is bound by
+        // dependent global round trips (1.5-3 us each, measured), not by its arithmetic
+        auto cand_min_rows = [&](uint32_t j0, uint32_t stride) {
+            double v[TU][D];
+            int kk[TU];
 #pragma unroll
-            for (int d = 0; d < D; d++) f[d] = (float)v[d];
-            for (int c = 0; c < M2; c++) {
-                float cv = 0.0f;
-#pragma unroll
-                for (int d = 0; d < D; d++) cv += s_wt[c * D + d] * f[d];
-                if (cv != cv) continue;
-                const unsigned long long e = ((unsigned long long)f32_order_key(cv) << 32) | j;
-                unsigned long long *mp = &s_min[k * M2 + c];
-                if (e < *mp) atomicMin(mp, e);
+            for (int u = 0; u < TU; u++) {               // (row addresses independent of the keys)
+                const uint32_t jc = min(j0 + u * stride, mt - 1u);
+                const bool okc = TINY_OK(jc, rcap, 1);
+                const uint32_t jr = okc ? jc : 0u;
+                kk[u] = okc ? (int)(reinterpret_cast<const uint32_t *>(keys)[2 * (size_t)jr + 1] >> 24) : -1;
+                load_trow<double, D>(rows + (size_t)jr * DP, v[u]);
             }
-        }
+#pragma unroll
+            for (int u = 0; u < TU; u++) {
+                const uint32_t j = j0 + u * stride;
+                if (j >= mt || !TINY_OK(kk[u], Kp, 12) || kk[u] < 0) continue;
+#ifdef SKY_MEASURE
+                if (a.dbg & 2) {                                   // loads only
+                    if (v[u][0] == -12345.0) atomicMin(&s_min[0], 0ull);
+                    continue;
+                }
+#endif
+                float f[D];
+#pragma unroll
+                for (int d = 0; d < D; d++) f[d] = (float)v[u][d];
+                // all M2 criteria first, then all M2 current minima read together (one LDS
+                // round trip per row, not two per criterion), then the winning atomics
+                unsigned long long ev[M2], cur[M2];
+                unsigned long long *mrow = s_min + kk[u] * MS;
+#pragma unroll
+                for (int c = 0; c < M2; c++) {
+                    float cv = 0.0f;
+#pragma unroll
+                    for (int d = 0; d < D; d++) cv += s_wt[c * D + d] * f[d];
+                    ev[c] = cv != cv ? ~0ull : ((unsigned long long)f32_order_key(cv) << 32) | j;
+                }
+#pragma unroll
+                for (int c = 0; c < M2; c++) cur[c] = mrow[c];
+#ifdef SKY_MEASURE
+                if (a.dbg & 1) {                                   // no atomics
+                    if (ev[0] < cur[1] && ev[2] == 7ull) atomicMin(&mrow[0], ev[0]);
+                    continue;
+                }
+#endif
+#pragma unroll
+                for (int c = 0; c < M2; c++)
+                    if (ev[c] < cur[c]) atomicMin(&mrow[c], ev[c]);
+            }
+        };
+        for (uint32_t j0 = tid; j0 < mt; j0 += TU * NT) cand_min_rows(j0, NT);
         __syncthreads();
         TINY_CLK(2);
         // k_cand_pick: one wave per partition, winners deduplicated and mutually non-dominated
         for (int k = wave; k < Kp; k += NW) {
-            const unsigned long long w = lane < M2 ? s_min[k * M2 + lane] : ~0ull;
+            const unsigned long long w = lane < M2 ? s_min[k * MS + lane] : ~0ull;
             const bool has = w != ~0ull && TINY_OK((uint32_t)(w & 0xffffffffu), rcap, 2);
             double c[D];
             if (has) {
@@ -1728,61 +1821,89 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
             if (ok) {
                 const int pos = (int)lanes_below(b);
 #pragma unroll
-                for (int d = 0; d < D; d++) s_pr[((size_t)k * M2 + pos) * D + d] = c[d];
+                for (int d = 0; d < D; d++) s_pr[(size_t)k * PS + pos * D + d] = c[d];
             }
             if (lane == 0) s_np[k] = __popcll(b);
         }
         __syncthreads();
         TINY_CLK(3);
-        // k_cand_filter + scan + k_cand_compact: the live slots in slot order
+        // k_cand_filter + scan + k_cand_compact: the live slots, TU per thread and batch (loads
+        // first), one block scan per batch, the survivors written from registers.  The compacted
+        // order is the batch order, not the slot order: nothing downstream depends on slot order
+        // (the brute pass, the fates and the counts are per slot; pruner_slot follows livepos)
         double *rows2 = a.rows_r[r];
         uint64_t *key2 = a.key_r[r];
         uint32_t *src2 = a.src_r[r];
         uint32_t base = 0;
-        for (uint32_t j0 = 0; j0 < mt; j0 += NT) {                 // block-uniform
-            const uint32_t j = j0 + tid;
-            bool liv = false;
-            double v[D];
-            if (j < mt && TINY_OK(j, rcap, 3)) {
-                const int k = (int)(keys[j] >> 56);
-                load_trow<double, D>(rows + (size_t)j * DP, v);
-                const double *pr = s_pr + (size_t)k * M2 * D;
-                bool dom = false;
-                for (int q = 0; q < s_np[k]; q++) {
-                    bool le = true, lt = false;
+        for (int q = tid; q < KM; q += NT) s_ps2[q] = -1;          // (a pruner slot past mt: dropped)
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < mt; j0 += TU * NT) {            // block-uniform
+            double v[TU][D];
+            uint64_t kv[TU];
+            uint32_t sv[TU];
+            bool liv[TU];
 #pragma unroll
-                    for (int d = 0; d < D; d++) {
-                        const double x = pr[q * D + d];
-                        le &= x <= v[d];
-                        lt |= x < v[d];
+            for (int u = 0; u < TU; u++) {
+                const uint32_t jc = min(j0 + u * NT + tid, mt - 1u);
+                const bool okc = TINY_OK(jc, rcap, 3);
+                kv[u] = okc ? keys[jc] : 0ull;
+                sv[u] = okc ? src[jc] : 0u;
+                load_trow<double, D>(rows + (size_t)(okc ? jc : 0u) * DP, v[u]);
+            }
+            uint32_t c = 0;
+#pragma unroll
+            for (int u = 0; u < TU; u++) {
+                const uint32_t j = j0 + u * NT + tid;
+                liv[u] = false;
+                if (j < mt) {
+                    const int k = (int)(kv[u] >> 56);
+                    const double *pr = s_pr + (size_t)k * PS;
+                    const int np = s_np[k];
+                    bool dom = false;
+                    // four pruners' rows read together per step (LDS latency, not bandwidth, bound)
+                    for (int q0 = 0; q0 < np; q0 += 4) {
+                        double x[4][D];
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+#pragma unroll
+                            for (int d = 0; d < D; d++) x[i][d] = pr[min(q0 + i, M2 - 1) * D + d];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            bool le = true, lt = false;
+#pragma unroll
+                            for (int d = 0; d < D; d++) {
+                                le &= x[i][d] <= v[u][d];
+                                lt |= x[i][d] < v[u][d];
+                            }
+                            dom |= le & lt & (q0 + i < np);
+                        }
                     }
-                    dom |= le & lt;
+                    liv[u] = !dom;
+                    c += liv[u] ? 1u : 0u;
                 }
-                liv = !dom;
             }
             uint32_t tot;
-            const uint32_t pos = base + tiny_scan_excl(liv ? 1u : 0u, s_w, tot);
-            if (j < mt && TINY_OK(j, a.cap[1], 4)) {
-                a.live[j] = liv ? 1u : 0u;
-                a.livepos[j] = pos;
-                if (liv && TINY_OK(pos, wcap, 5) && TINY_OK(j, rcap, 3)) {
-                    const double2 *s2 = reinterpret_cast<const double2 *>(rows + (size_t)j * DP);
-                    double2 *d2 = reinterpret_cast<double2 *>(rows2 + (size_t)pos * DP);
+            uint32_t pos = base + tiny_scan_excl(c, s_w, tot);
 #pragma unroll
-                    for (int q = 0; q < DP / 2; q++) d2[q] = s2[q];
-                    key2[pos] = keys[j];
-                    src2[pos] = src[j];
+            for (int u = 0; u < TU; u++) {
+                const uint32_t j = j0 + u * NT + tid;
+                if (j < mt) {
+                    if (liv[u] && TINY_OK(pos, wcap, 5)) {
+                        store_row<double, D>(rows2 + (size_t)pos * DP, v[u]);
+                        key2[pos] = kv[u];
+                        src2[pos] = sv[u];
+                    }
+                    if (sv[u] & 0x80000000u)                        // a pruner slot: its new index
+                        s_ps2[s_ent[sv[u] & 0x7fffffffu]] = liv[u] ? (int32_t)pos : -1;
+                    pos += liv[u] ? 1u : 0u;
                 }
             }
             base += tot;
         }
         __syncthreads();
         TINY_CLK(4);
-        for (int q = tid; q < KM; q += NT) {
-            const int32_t ps = ap.pruner_slot[q];
-            if (ps >= 0 && TINY_OK((uint32_t)ps < mt ? ps : 0, a.cap[1], 6))
-                ap.pruner_slot[q] = (uint32_t)ps < mt && a.live[ps] ? (int32_t)a.livepos[ps] : -1;
-        }
+        __syncthreads();
+        for (int q = tid; q < KM; q += NT) s_ps[q] = s_ps2[q];
         if (tid == 0) a.totals[11 + r] = base;
         cnt = base;
         rows = rows2;
@@ -1798,21 +1919,45 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     if (tid == 0) a.totals[14] = fin;
     constexpr uint32_t BR = tiny_brute_rows(D);
     if (fin > BR) {                                                // block-uniform
-        if (tid == 0) atomicOr(ap.flags, kFlagTinyMiss);
+        if (lflags) atomicOr(&s_fl, lflags);
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t f = s_fl | kFlagTinyMiss;
+            const uint32_t old = atomicOr(ap.flags, f);
+            if (a.pin) {
+                for (int i = 0; i < 16; i++) a.pin[i] = a.totals[i];
+                a.pin[a.pin_off[3]] = old | f;
+            }
+        }
         return;
     }
     double *s_row = reinterpret_cast<double *>(s_arena);                          // [BR][D]
     uint32_t *s_part = reinterpret_cast<uint32_t *>(s_row + (size_t)BR * D);       // [BR]
     uint32_t *s_dom = s_part + BR;                                                 // [BR]
-    unsigned long long *s_l = reinterpret_cast<unsigned long long *>(s_dom + BR);   // [kMaxK]
+    uint32_t *s_src = s_dom + BR;                                                  // [BR]
+    unsigned long long *s_l = reinterpret_cast<unsigned long long *>(s_src + BR + (BR & 1u));   // [kMaxK]
     unsigned long long *s_s = s_l + kMaxK;                                         // [kMaxK]
     uint32_t *s_tc = reinterpret_cast<uint32_t *>(s_s + kMaxK);                   // [kTinyTiles]
     uint32_t *s_sn = s_tc + kTinyTiles, *s_sa = s_sn + kMaxK;                       // [kMaxK] x 2
     uint8_t *s_pf = reinterpret_cast<uint8_t *>(s_sa + kMaxK);                     // [kHistMaxKM]
-    for (uint32_t q = tid; q < fin * D; q += NT)
-        s_row[q] = TINY_OK(q / D, rcap, 7) ? rows[(size_t)(q / D) * DP + q % D] : 0.0;
+    uint8_t *s_gq = s_pf + kHistMaxKM;                         // [kHistMaxKM] pruner groups in G
+    uint32_t *s_ng = reinterpret_cast<uint32_t *>(s_gq + kHistMaxKM);              // [1]
+    {                                                              // <= BR * D / NT values per thread
+        constexpr int LU = (BR * D + NT - 1) / NT;
+        double tv[LU];
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const uint32_t q = tid + u * NT;
+            tv[u] = q < fin * D && TINY_OK(q / D, rcap, 7) ? rows[(size_t)(q / D) * DP + q % D] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < LU; u++)
+            if (tid + u * NT < fin * D) s_row[tid + u * NT] = tv[u];
+    }
     for (uint32_t q = tid; q < fin; q += NT) {
-        s_part[q] = TINY_OK(q, rcap, 7) ? (uint32_t)(keys[q] >> 56) : 0u;
+        const bool okq = TINY_OK(q, rcap, 7);
+        s_part[q] = okq ? (uint32_t)(keys[q] >> 56) : 0u;
+        s_src[q] = okq ? src[q] : 0x80000000u;
         if (!TINY_OK(s_part[q], Kp, 13)) s_part[q] = 0;
         s_dom[q] = 0u;
     }
@@ -1860,8 +2005,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
 
     // ---- 4. the fate tables (k_fate_tables, slot stats)
     for (uint32_t j = tid; j < fin; j += NT) {
-        if (!TINY_OK(j, rcap, 9)) continue;
-        const uint32_t sj = src[j];
+        const uint32_t sj = s_src[j];
         if (sj & 0x80000000u) continue;                            // appended pruner slots: below
         if (!TINY_OK(sj, a.cap[6], 10)) continue;
         const uint32_t f = s_dom[j];
@@ -1876,11 +2020,12 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         }
     }
     for (int q = tid; q < KM; q += NT) {
-        const int32_t ps = ap.pruner_slot[q];
+        const int32_t ps = s_ps[q];
+        ap.pruner_slot[q] = ps;                                    // (the final slots' index, as the chain leaves it)
         uint32_t f = 0;
         if (ps >= 0 && (uint32_t)ps < fin) {
             f = s_dom[ps];
-            const unsigned long long w = ap.dup_cnt[q];
+            const unsigned long long w = s_dupc[q];
             const int k = q / M;
             if (f & 1u) {
                 atomicAdd(&s_l[k], w);
@@ -1897,14 +2042,28 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         a.statk[a.K + q] = s_s[q];
     }
 
-    // ---- 5. per-tile output counts (k_out_hist_count) and their exclusive scan
+    // ---- 5. per-tile output counts (k_out_hist_count) and their exclusive scan: only the
+    // duplicate groups whose pruner is in G count, listed first (usually a handful)
+    if (wave == 0) {
+        uint32_t ng = 0;
+        for (int q0 = 0; q0 < KM; q0 += 64) {
+            const bool g = q0 + lane < KM && (s_pf[q0 + lane] & 2u);
+            const uint64_t b = __ballot(g);
+            if (g) s_gq[ng + lanes_below(b)] = (uint8_t)(q0 + lane);
+            ng += (uint32_t)__popcll(b);
+        }
+        if (lane == 0) *s_ng = ng;
+    }
+    __syncthreads();
+    const uint32_t ng = *s_ng;
     uint32_t base = 0;
     for (uint32_t t0 = 0; t0 < a.ntiles; t0 += NT) {                // block-uniform
         const uint32_t t = t0 + tid;
         uint32_t c = 0;
         if (t < a.ntiles) {
             const uint32_t *h = a.tile_hist + (size_t)t * KM;
-            for (int q = 0; q < KM; q++) c += (s_pf[q] & 2u) ? h[q] : 0u;
+#pragma unroll 8
+            for (uint32_t i = 0; i < ng; i++) c += h[s_gq[i]];
             c += s_tc[t];
         }
         uint32_t tot;
@@ -1916,15 +2075,36 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         base += tot;
     }
     if (tid == 0) a.totals[3] = base;
-    if (lflags) atomicOr(ap.flags, lflags);
+    if (lflags) atomicOr(&s_fl, lflags);
+    __syncthreads();
+    // ---- 6. the flags, and the final read's words into the host-mapped buffer
+    if (tid == 0) {
+        const uint32_t old = s_fl ? atomicOr(ap.flags, s_fl) : *ap.flags;
+        if (a.pin) {
+            for (int i = 0; i < 16; i++) a.pin[i] = a.totals[i];     // (this thread's own writes)
+            a.pin[a.pin_off[3]] = old | s_fl;
+        }
+    }
+    if (a.pin) {
+        for (int q = tid; q < a.K; q += NT) {
+            a.pin[a.pin_off[0] + 2 * q] = (uint32_t)s_l[q];
+            a.pin[a.pin_off[0] + 2 * q + 1] = (uint32_t)(s_l[q] >> 32);
+            a.pin[a.pin_off[0] + 2 * (a.K + q)] = (uint32_t)s_s[q];
+            a.pin[a.pin_off[0] + 2 * (a.K + q) + 1] = (uint32_t)(s_s[q] >> 32);
+        }
+        for (int q = tid; q < Kp; q += NT) {
+            a.pin[a.pin_off[1] + q] = s_sa[q];
+            a.pin[a.pin_off[2] + q] = s_sn[q];
+        }
+        for (int q = tid; q < KM; q += NT) a.pin[a.pin_off[4] + q] = s_dupc[q];
+    }
     TINY_CLK(9);
 }
 
 bool tiny_fits(int D, int Kp, int M2, int KM, int K, uint32_t tiles) {
-    const size_t KM2 = (size_t)Kp * M2;
-    const size_t pre = KM2 * 8 + (size_t)((M2 * D + 3) & ~3) * 4 + KM2 * D * 8;
-    const size_t brute = (size_t)tiny_brute_rows(D) * (D * 8 + 8) + kTinyFixed;
-    return M2 <= 64 && KM <= kHistMaxKM && K <= kMaxK && Kp <= kMaxK && tiles <= kTinyTiles &&
+    const size_t pre = (size_t)Kp * (M2 + 1) * 8 + (size_t)((M2 * D + 3) & ~3) * 4 + (size_t)Kp * (M2 * D + 1) * 8;
+    const size_t brute = (size_t)tiny_brute_rows(D) * (D * 8 + 12) + kTinyFixed;
+    return M2 == kTinyM2 && KM <= kHistMaxKM && K <= kMaxK && Kp <= kMaxK && tiles <= kTinyTiles &&
            pre <= kTinyArena && brute <= kTinyArena;
 }
 

@@ -82,13 +82,21 @@ struct FilterArgs {
     // word is stored (candidates, other duplicate groups, deferred keys); else dropped
     uint64_t *planes = nullptr;
     int32_t dom_kj = -1;
+    // the pruner pick inside the filter (k_pick_pruners' work, redone by every workgroup from
+    // the sample minima; workgroup 0 also writes pruners / npr for the later kernels):
+    // pick_gmin non-null replaces reading pruners / npr
+    const unsigned long long *pick_gmin = nullptr;
+    uint32_t pick_S = 0;
+    double *pruners_w = nullptr;
+    int32_t *npr_w = nullptr;
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
 // pruners: per partition up to M (<= 64) distinct, mutually non-dominated sample tuples
+// (pick = false: only the sample minima; the filter picks them itself, FilterArgs.pick_gmin)
 void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
-                           double *pruners, int32_t *npr, hipStream_t st);
+                           double *pruners, int32_t *npr, hipStream_t st, bool pick = true);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
 struct AppendArgs {
@@ -213,7 +221,7 @@ void launch_iota(uint32_t *a, uint32_t n, hipStream_t st);
 void launch_nan_any(const double *v, size_t count, uint32_t *flag, hipStream_t st);
 // up to kFillMax byte ranges (4-byte aligned starts, < 4 GiB each): the kernel argument of
 // one k_fill_multi / k_gather_words launch
-constexpr int kFillMax = 8;
+constexpr int kFillMax = 16;
 struct FillRanges {
     uint8_t *p[kFillMax] = {};
     uint32_t bytes[kFillMax] = {};
@@ -468,11 +476,12 @@ constexpr uint32_t kTinyTiles = 4096;
 // the brute / fate phase (final rows + partition + fate per slot, then per-partition stats and
 // counts, per-tile counts, pruner fates) reuse it; the final slots it holds follow from D
 constexpr size_t kTinyArena = 56 * 1024;
-constexpr size_t kTinyFixed = (size_t)kMaxK * 24 + (size_t)kTinyTiles * 4 + kHistMaxKM;
-constexpr uint32_t tiny_brute_rows(int D) {
-    return (kTinyArena - kTinyFixed) / (D * 8 + 8) < 512 ? (uint32_t)((kTinyArena - kTinyFixed) / (D * 8 + 8)) : 512u;
+constexpr size_t kTinyFixed = (size_t)kMaxK * 24 + (size_t)kTinyTiles * 4 + 2 * kHistMaxKM + 16 + 8;
+constexpr uint32_t tiny_brute_rows(int D) {     // per final slot: the row, partition, fate, source
+    return (kTinyArena - kTinyFixed) / (D * 8 + 12) < 512 ? (uint32_t)((kTinyArena - kTinyFixed) / (D * 8 + 12)) : 512u;
 }
 constexpr int kTinyThreads = 1024;
+constexpr int kTinyM2 = 16;             // second-level pruners per partition in the tail (compile-time)
 constexpr uint32_t kTinyForce = 192;      // a plan without rounds: the tail runs one above this many slots
 constexpr uint32_t kFlagTinyMiss = 64u;
 struct TinyArgs {
@@ -503,7 +512,24 @@ struct TinyArgs {
     uint32_t *chk = nullptr;
     uint32_t cap[8] = {};
     unsigned long long *clk = nullptr;    // (SKY_TINY_CLK) s_memrealtime at the phase ends, [10]
+    int dbg = 0;                          // (SKY_TINY_DBG, measurement only, results invalid): 1 no atomics, 2 no criteria
+    // the final read's words written straight into the host-mapped buffer (no gather launch):
+    // totals at word 0, then (word offsets) statk, segalive, segn, flags, dup_cnt -- the layout of
+    // pipe_finish's read list (tiny_pin_layout)
+    uint32_t *pin = nullptr;
+    uint32_t pin_off[5] = {};
 };
+// word offsets of statk / segalive / segn / flags / dup_cnt after the 16 totals words, each range
+// rounded up to 16 bytes as sync_read lays them out; returns the bytes in all
+inline size_t tiny_pin_layout(int K, int Kp, int KM, uint32_t off[5]) {
+    const size_t sz[6] = {64, (size_t)K * 16, (size_t)Kp * 4, (size_t)Kp * 4, 4, (size_t)KM * 4};
+    size_t o = 0;
+    for (int i = 0; i < 6; i++) {
+        if (i) off[i - 1] = (uint32_t)(o / 4);
+        o += (sz[i] + 15) & ~size_t(15);
+    }
+    return o;
+}
 void launch_tiny_tail(int D, const TinyArgs &a, hipStream_t st);
 // the tail's LDS arena holds both phases' data for this shape (host check before the launch)
 bool tiny_fits(int D, int Kp, int M2, int KM, int K, uint32_t tiles);
