@@ -122,6 +122,7 @@ struct Pipe {
     bool last_tiny = false;                              // ... its tail in one workgroup (bit 5)
     int64_t tiny_runs = 0;
     uint32_t tiny_block = 0;
+    DevBuf cand_lb;                                      // the fused prefilter pass's look-back words
     DevBuf dbg_clk;                                      // measurement builds: the tail's phase clocks                             // plans learned without trying the tail (after a miss)
     bool fused = false;
     const int64_t *fused_ids = nullptr;

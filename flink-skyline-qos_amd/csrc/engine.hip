@@ -215,6 +215,12 @@ static bool brute_disabled() {
     return e && atoi(e) == 0;
 }
 // SKY_BRUTE16=0: the small-set pair pass compares f32 even for integer rows (A/B knob)
+static bool cand_fused_disabled() {   // SKY_CAND_FUSED=0: pick / filter / scan / compact launches (A/B knob)
+    const char *e = SKY_ENV("SKY_CAND_FUSED");
+    return e && e[0] == '0';
+}
+// the fused prefilter pass's look-back words of each planned round: [tiles][u64] + a ticket word
+static size_t cand_lb_bytes(uint32_t bound) { return (size_t)cand_fused_tiles(bound) * 8 + 64; }
 static bool tiny_disabled() {    // SKY_TINY=0: the planned tail as one launch per stage (A/B knob)
     const char *e = SKY_ENV("SKY_TINY");
     return e && e[0] == '0';
@@ -1068,9 +1074,23 @@ static int plan_prepare(Pipe &p, int D, bool tiny, FillSet &fill) {
     const size_t KM2 = (size_t)p.Kp * M2;
     uint32_t fin = pl.bound[0];
     for (int r = 0; r < pl.rounds; r++) fin = std::min(pl.bound[r + 1], fin);
+    if (pl.rounds && tiny) {            // round 0's minima: k_cand_min on the whole GPU before the tail
+        SKY_TRY(p.cmin.ensure(KM2 * 8));
+        fill.add(p.cmin.p, KM2 * 8, 0xff);
+    }
     if (pl.rounds && !tiny) {           // (the one-workgroup tail keeps its minima in LDS)
         SKY_TRY(p.cmin.ensure(KM2 * pl.rounds * 8));
         fill.add(p.cmin.p, KM2 * pl.rounds * 8, 0xff);
+        if (cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled()) {   // the fused pass's look-back words
+            size_t lb = 0;
+            uint32_t b = pl.bound[0];
+            for (int r = 0; r < pl.rounds; r++) {
+                lb += cand_lb_bytes(b);
+                b = std::min(pl.bound[r + 1], b);
+            }
+            SKY_TRY(p.cand_lb.ensure(lb));
+            fill.add(p.cand_lb.p, lb);
+        }
     }
     SKY_TRY(p.segalive.ensure((size_t)p.Kp * 4));
     SKY_TRY(p.seg_begin.ensure((size_t)p.Kp * 4));
@@ -1080,7 +1100,6 @@ static int plan_prepare(Pipe &p, int D, bool tiny, FillSet &fill) {
         SKY_TRY(p.keep.ensure((size_t)std::max<uint32_t>(fin, 1) * 4));
         fill.add(p.keep.p, (size_t)std::max<uint32_t>(fin, 1) * 4);
     }
-    (void)D;
     return SKY_OK;
 }
 
@@ -1208,6 +1227,18 @@ static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size
         ta.clk = p.dbg_clk.as<unsigned long long>();
     }
 #endif
+    if (pl.rounds) {                    // round 0's criterion minima over the candidate slots
+        CandArgs ca{};
+        ca.mt = pl.bound[0];
+        ca.d_mt = p.totals.as<uint32_t>();     // the filter's candidates (the pruner slots follow them)
+        ca.rows = p.rows.as<double>();
+        ca.key = p.sortkey.as<uint64_t>();
+        ca.Kp = p.Kp;
+        ca.M2 = ta.M2;
+        ca.cmin = p.cmin.as<unsigned long long>();   // filled by plan_prepare
+        launch_cand_min(D, ca, st);
+        ta.cmin0 = ca.cmin;
+    }
     c.ktimer_begin("tiny", st);
     launch_tiny_tail(D, ta, st);
 #ifdef SKY_MEASURE
@@ -1270,6 +1301,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     const uint32_t *d_cnt = p.totals.as<uint32_t>() + 10;   // min(m + nps, cap), by k_append_pruners
     uint32_t bound = pl.bound[0];
     if (tiny_ap) return pipe_run_tiny(c, p, in, tm, cap, cap_full, tiles, fill, *tiny_ap);
+    size_t lb_off = 0;                         // this round's look-back words (fused prefilter pass)
     for (int round = 0; round < pl.rounds; round++) {
         const int M2 = std::min(prefilter_m2(), 2048 / p.Kp);
         const int KM2 = p.Kp * M2;
@@ -1297,10 +1329,25 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         ca.live = p.live.as<uint32_t>();
         uint32_t *d_live = p.totals.as<uint32_t>() + 11 + round;
         c.ktimer_begin("prefilter", st);
-        launch_cand_prefilter(D, ca, st);
-        scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), bound, d_live, p.scratch.as<uint32_t>(), st, d_cnt);
-        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(), ds->as<uint32_t>(),
-                            p.pruner_slot.as<int32_t>(), KM, st);
+        if (cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled()) {   // (plan_prepare zeroed its words)
+            ca.rows2 = dr->as<double>();
+            ca.key2 = dk->as<uint64_t>();
+            ca.src2 = ds->as<uint32_t>();
+            ca.d_live = d_live;
+            ca.pruner_slot = p.pruner_slot.as<int32_t>();
+            ca.entries = p.pr_entries.as<int32_t>();
+            ca.lb = reinterpret_cast<unsigned long long *>(p.cand_lb.as<char>() + lb_off);
+            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + lb_off + (size_t)cand_fused_tiles(bound) * 8);
+            ca.err = p.flags.as<uint32_t>();
+            launch_cand_min(D, ca, st);
+            launch_cand_fused(D, ca, st);
+            lb_off += cand_lb_bytes(bound);
+        } else {
+            launch_cand_prefilter(D, ca, st);
+            scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), bound, d_live, p.scratch.as<uint32_t>(), st, d_cnt);
+            launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(),
+                                ds->as<uint32_t>(), p.pruner_slot.as<int32_t>(), KM, st);
+        }
         c.ktimer_end("prefilter", st, bound);
         STAGE(st, "prefilter");
         p.s_rows = dr;
@@ -1587,6 +1634,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(dk->ensure((size_t)mt0 * 8));
         SKY_TRY(ds->ensure((size_t)mt0 * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(mt0 + 1) * 4 + 64));
+        const bool fused = cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled();
+        if (fused) {
+            SKY_TRY(p.cand_lb.ensure(cand_lb_bytes(mt0)));
+            fill.add(p.cand_lb.p, cand_lb_bytes(mt0));
+        }
         fill.add(p.cmin.p, (size_t)KM2 * 8, 0xff);
         HIP_TRY(fill.launch(st));
         CandArgs ca{};
@@ -1601,11 +1653,25 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         ca.npr2 = p.npr2.as<int32_t>();
         ca.live = p.live.as<uint32_t>();
         c.ktimer_begin("prefilter", st);
-        launch_cand_prefilter(D, ca, st);
-        scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), mt0, p.totals.as<uint32_t>() + 8, p.scratch.as<uint32_t>(),
-                      st);
-        launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(), ds->as<uint32_t>(),
-                            p.pruner_slot.as<int32_t>(), KM, st);
+        if (fused) {
+            ca.rows2 = dr->as<double>();
+            ca.key2 = dk->as<uint64_t>();
+            ca.src2 = ds->as<uint32_t>();
+            ca.d_live = p.totals.as<uint32_t>() + 8;
+            ca.pruner_slot = p.pruner_slot.as<int32_t>();
+            ca.entries = p.pr_entries.as<int32_t>();
+            ca.lb = p.cand_lb.as<unsigned long long>();
+            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + (size_t)cand_fused_tiles(mt0) * 8);
+            ca.err = p.flags.as<uint32_t>();
+            launch_cand_min(D, ca, st);
+            launch_cand_fused(D, ca, st);
+        } else {
+            launch_cand_prefilter(D, ca, st);
+            scan_excl_u32(ca.live, p.livepos.as<uint32_t>(), mt0, p.totals.as<uint32_t>() + 8, p.scratch.as<uint32_t>(),
+                          st);
+            launch_cand_compact(D, ca, p.livepos.as<uint32_t>(), dr->as<double>(), dk->as<uint64_t>(),
+                                ds->as<uint32_t>(), p.pruner_slot.as<int32_t>(), KM, st);
+        }
         c.ktimer_end("prefilter", st, mt0);
         STAGE(st, "prefilter");
         uint32_t live_n = 0;

@@ -996,6 +996,139 @@ __global__ __launch_bounds__(kThreads) void k_cand_filter(const double *__restri
     live[j] = dom ? 0u : 1u;
 }
 
+// decoupled look-back words: flag (aggregate / inclusive prefix) | count
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbCount = (1ull << 62) - 1;
+
+// The prefilter's pick, live test, scan and compaction in ONE launch (was: k_cand_pick,
+// k_cand_filter, one to three scan kernels, k_cand_compact -- four to six dependent launches of
+// 3-6 us each).  Every workgroup redoes the pick (k_cand_pick: one wave per partition, lane =
+// criterion winner, shuffles) into LDS; one slot per thread; the tile's exclusive prefix comes
+// from a decoupled look-back over the earlier tiles (tiles numbered in start order by a ticket, so a
+// tile only waits for tiles already running; bounded spin -> kFlagRadixSpin), which keeps the
+// compaction in slot order exactly as the scan + k_cand_compact did.  The appended pruner slots'
+// indices are remapped from their entries (a dropped one: -1).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
+    constexpr int DP = padded_dims<double>(D);
+    extern __shared__ __attribute__((aligned(16))) double s_pr2[];   // [Kp][M2 * D + 1]
+    __shared__ int32_t s_np[kMaxK];
+    __shared__ uint32_t s_w[kThreads / 64];
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_prefix;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int M2 = a.M2, PS = a.M2 * D + 1;
+    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+    const uint32_t mt = a.d_mt ? min(a.mt, *a.d_mt) : a.mt;
+    for (int k = wave; k < a.Kp; k += kThreads / 64) {
+        const unsigned long long w = lane < M2 ? a.cmin[k * M2 + lane] : ~0ull;
+        const bool has = w != ~0ull;
+        double c[D];
+        if (has) {
+            load_trow<double, D>(a.rows + (size_t)(uint32_t)(w & 0xffffffffu) * DP, c);
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; d++) c[d] = 0.0;
+        }
+        const uint64_t hm = __ballot(has);
+        bool ok = has;
+        for (int q = 0; q < M2; q++) {
+            bool le = true, lt = false, eq = true;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const double x = __shfl(c[d], q, 64);
+                le &= x <= c[d];
+                lt |= x < c[d];
+                eq &= x == c[d];
+            }
+            if (q != lane && ((hm >> q) & 1ull) && ((le && lt) || (eq && q < lane))) ok = false;
+        }
+        const uint64_t b = __ballot(ok);
+        if (ok) {
+            const int pos = (int)lanes_below(b);
+#pragma unroll
+            for (int d = 0; d < D; d++) s_pr2[k * PS + pos * D + d] = c[d];
+        }
+        if (lane == 0) s_np[k] = __popcll(b);
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t j = tile * kThreads + threadIdx.x;
+    bool liv = false;
+    double v[D];
+    uint64_t kv = 0;
+    uint32_t sv = 0;
+    if (j < mt) {
+        kv = a.key[j];
+        sv = a.src[j];
+        load_trow<double, D>(a.rows + (size_t)j * DP, v);
+        const int k = (int)(kv >> 56);
+        const double *pr = s_pr2 + (size_t)k * PS;
+        const int np = s_np[k];
+        bool dom = false;
+        for (int q = 0; q < np; q++) {
+            bool le = true, lt = false;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                const double x = pr[q * D + d];
+                le &= x <= v[d];
+                lt |= x < v[d];
+            }
+            dom |= le & lt;
+        }
+        liv = !dom;
+    }
+    uint32_t bt;
+    const uint32_t pl = block_scan_excl(liv ? 1u : 0u, s_w, bt);
+    if (threadIdx.x < 64) {
+        unsigned long long excl = 0;
+        if (lane == 0)
+            __hip_atomic_store(a.lb + tile, (tile == 0 ? kLbInc : kLbAgg) | bt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tile > 0) {
+            int64_t end = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t idx = end - lane;
+                const unsigned long long svv = idx >= 0 ? __hip_atomic_load(a.lb + idx, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT)
+                                                        : kLbInc;
+                const unsigned long long f = svv & ~kLbCount;
+                const uint64_t inc = __ballot(f == kLbInc), zero = __ballot(f == 0ull);
+                const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+                if (zero & upto) {
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0) atomicOr(a.err, kFlagRadixSpin);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long c = lane <= first ? (svv & kLbCount) : 0ull;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (first < 64) break;
+                end -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(a.lb + tile, kLbInc | (excl + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_prefix = excl;
+            if (tile == gridDim.x - 1) *a.d_live = (uint32_t)(excl + bt);
+        }
+    }
+    __syncthreads();
+    const uint32_t pos = (uint32_t)s_prefix + pl;
+    if (liv) {
+        store_row<double, D>(a.rows2 + (size_t)pos * DP, v);
+        a.key2[pos] = kv;
+        a.src2[pos] = sv;
+    }
+    if (j < mt && (sv & 0x80000000u)) a.pruner_slot[a.entries[sv & 0x7fffffffu]] = liv ? (int32_t)pos : -1;
+}
+
 // order-preserving compaction of the live slots (rows, keys, sources); the appended
 // pruner slots' indices are remapped (a dropped one: its duplicate group's fate is 0)
 template <int D>
@@ -1465,7 +1598,6 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
 // the ids / origins staged in LDS and written coalesced.  Replaces count pass + scan +
 // host read + write pass; positions >= cap are not written (the caller reports
 // SKY_E_CAPACITY from the total).
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbCount = (1ull << 62) - 1;
 __global__ __launch_bounds__(kThreads) void k_out_fused(OutArgs a, unsigned long long *__restrict__ lb,
                                                         uint32_t *__restrict__ ticket, uint32_t *__restrict__ d_total,
                                                         uint32_t *__restrict__ err, int64_t cap) {
@@ -1658,7 +1790,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_arena[];
     __shared__ uint32_t s_w[kTinyThreads / 64];
     __shared__ int32_t s_np[kMaxK];
-    __shared__ uint32_t s_fl;
+    __shared__ uint32_t s_fl, t_tot[16], f_start;
     // the pruner slot table, the entry -> pruner map and the duplicate counts stay in LDS for the
     // whole tail (no dependent global round trips for them: one workgroup is latency-bound)
     __shared__ int32_t s_ps[kHistMaxKM], s_ps2[kHistMaxKM];
@@ -1675,6 +1807,10 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
 
     // ---- 1. one slot per duplicated pruner (k_append_pruners)
     const uint32_t m = *ap.m_total;
+    // thread 0 mirrors the totals words and the flags word for the final read: the earlier kernels'
+    // values read here, in the first round trip, this kernel's own kept as it writes them
+    if (tid < 16) t_tot[tid] = a.totals[tid];
+    if (tid == 16) f_start = *ap.flags;
     uint32_t run = 0;
     uint64_t o = 0, an = ~0ull;
     for (int q0 = 0; q0 < KM; q0 += NT) {
@@ -1714,6 +1850,8 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     if (tid == 0) {
         *ap.nps_total = run;
         a.totals[10] = cnt;
+        t_tot[5] = run;
+        t_tot[10] = cnt;
     }
     __syncthreads();
     TINY_CLK(1);
@@ -1733,21 +1871,28 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         // per-partition strides padded by one element: lanes of different partitions read
         // different banks (unpadded, every partition's row started on the same bank)
         const int MS = M2 + 1, PS = M2 * D + 1;
-        unsigned long long *s_min = reinterpret_cast<unsigned long long *>(s_arena);        // [Kp][MS]
-        float *s_wt = reinterpret_cast<float *>(s_min + Kp * MS);                           // [M2][D]
+        // one minima copy per wave when they fit (LDS atomics then contend within a wave only),
+        // merged into copy 0 after the pass
+        const int ncopy = (size_t)NW * Kp * MS * 8 + (size_t)Kp * PS * 8 + M2 * D * 4 + 64 <= kTinyArena ? NW : 1;
+        unsigned long long *s_min = reinterpret_cast<unsigned long long *>(s_arena);        // [ncopy][Kp][MS]
+        float *s_wt = reinterpret_cast<float *>(s_min + ncopy * Kp * MS);                   // [M2][D]
         double *s_pr = reinterpret_cast<double *>(s_wt + ((M2 * D + 3) & ~3));             // [Kp][PS]
-        for (int q = tid; q < Kp * MS; q += NT) s_min[q] = ~0ull;
+        unsigned long long *s_minw = s_min + (ncopy > 1 ? wave * Kp * MS : 0);
+        for (int q = tid; q < ncopy * Kp * MS; q += NT) s_min[q] = ~0ull;
         for (int q = tid; q < M2 * D; q += NT) s_wt[q] = cand_weight(q / D, q % D, D);
         __syncthreads();
-        // k_cand_min: per (partition, criterion) the minimising slot; TU rows per thread and
-        // batch, all their loads issued before the first is used: one workgroup is bound by
-        // dependent global round trips (1.5-3 us each, measured), not by its arithmetic
+        // k_cand_min: per (partition, criterion) the minimising slot; TU rows per thread and batch,
+        // their loads issued before the first is used.  Round 0 of a planned route with rounds takes
+        // the minima k_cand_min computed over the candidate slots on the whole GPU (a.cmin0): on one
+        // CU this pass cost 15-27 us at C1's 10k slots (loads ~7, criteria ~7, atomics ~6, measured)
+        const uint32_t ns = (r == 0 && a.cmin0) ? 0u : mt;
+        auto slot_of = [&](uint32_t i) -> uint32_t { return i; };
         auto cand_min_rows = [&](uint32_t j0, uint32_t stride) {
             double v[TU][D];
             int kk[TU];
 #pragma unroll
             for (int u = 0; u < TU; u++) {               // (row addresses independent of the keys)
-                const uint32_t jc = min(j0 + u * stride, mt - 1u);
+                const uint32_t jc = slot_of(min(j0 + u * stride, ns - 1u));
                 const bool okc = TINY_OK(jc, rcap, 1);
                 const uint32_t jr = okc ? jc : 0u;
                 kk[u] = okc ? (int)(reinterpret_cast<const uint32_t *>(keys)[2 * (size_t)jr + 1] >> 24) : -1;
@@ -1755,8 +1900,8 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < TU; u++) {
-                const uint32_t j = j0 + u * stride;
-                if (j >= mt || !TINY_OK(kk[u], Kp, 12) || kk[u] < 0) continue;
+                if (j0 + u * stride >= ns || !TINY_OK(kk[u], Kp, 12) || kk[u] < 0) continue;
+                const uint32_t j = slot_of(j0 + u * stride);
 #ifdef SKY_MEASURE
                 if (a.dbg & 2) {                                   // loads only
                     if (v[u][0] == -12345.0) atomicMin(&s_min[0], 0ull);
@@ -1769,7 +1914,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
                 // all M2 criteria first, then all M2 current minima read together (one LDS
                 // round trip per row, not two per criterion), then the winning atomics
                 unsigned long long ev[M2], cur[M2];
-                unsigned long long *mrow = s_min + kk[u] * MS;
+                unsigned long long *mrow = s_minw + kk[u] * MS;
 #pragma unroll
                 for (int c = 0; c < M2; c++) {
                     float cv = 0.0f;
@@ -1790,8 +1935,17 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
                     if (ev[c] < cur[c]) atomicMin(&mrow[c], ev[c]);
             }
         };
-        for (uint32_t j0 = tid; j0 < mt; j0 += TU * NT) cand_min_rows(j0, NT);
+        for (uint32_t j0 = tid; j0 < ns; j0 += TU * NT) cand_min_rows(j0, NT);
         __syncthreads();
+        if (ncopy > 1 || (r == 0 && a.cmin0)) {
+            for (int q = tid; q < Kp * MS; q += NT) {
+                unsigned long long mn = s_min[q];
+                for (int w = 1; w < ncopy; w++) mn = min(mn, s_min[w * Kp * MS + q]);
+                if (r == 0 && a.cmin0 && q % MS < M2) mn = a.cmin0[(q / MS) * M2 + q % MS];
+                s_min[q] = mn;
+            }
+            __syncthreads();
+        }
         TINY_CLK(2);
         // k_cand_pick: one wave per partition, winners deduplicated and mutually non-dominated
         for (int k = wave; k < Kp; k += NW) {
@@ -1904,7 +2058,12 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         TINY_CLK(4);
         __syncthreads();
         for (int q = tid; q < KM; q += NT) s_ps[q] = s_ps2[q];
-        if (tid == 0) a.totals[11 + r] = base;
+        if (tid == 0) {
+            a.totals[11 + r] = base;
+            if (r == 0) t_tot[11] = base;
+            else if (r == 1) t_tot[12] = base;
+            else t_tot[13] = base;
+        }
         cnt = base;
         rows = rows2;
         keys = key2;
@@ -1916,17 +2075,21 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
 
     // ---- 3. the brute pair pass over the final slots (exact f64 tests) + k_brute_finish
     const uint32_t fin = min(a.bound[rounds], cnt);
-    if (tid == 0) a.totals[14] = fin;
+    if (tid == 0) {
+        a.totals[14] = fin;
+        t_tot[14] = fin;
+    }
     constexpr uint32_t BR = tiny_brute_rows(D);
     if (fin > BR) {                                                // block-uniform
         if (lflags) atomicOr(&s_fl, lflags);
         __syncthreads();
         if (tid == 0) {
             const uint32_t f = s_fl | kFlagTinyMiss;
-            const uint32_t old = atomicOr(ap.flags, f);
+            atomicOr(ap.flags, f);
             if (a.pin) {
-                for (int i = 0; i < 16; i++) a.pin[i] = a.totals[i];
-                a.pin[a.pin_off[3]] = old | f;
+#pragma unroll
+                for (int i = 0; i < 16; i++) a.pin[i] = t_tot[i];
+                a.pin[a.pin_off[3]] = f_start | f;
             }
         }
         return;
@@ -2074,15 +2237,20 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         }
         base += tot;
     }
-    if (tid == 0) a.totals[3] = base;
+    if (tid == 0) {
+        a.totals[3] = base;
+        t_tot[3] = base;
+    }
     if (lflags) atomicOr(&s_fl, lflags);
     __syncthreads();
-    // ---- 6. the flags, and the final read's words into the host-mapped buffer
+    // ---- 6. the flags, and the final read's words into the host-mapped buffer (the flags word as
+    // it stands after this kernel: the earlier kernels' bits, read at the start, and this one's)
     if (tid == 0) {
-        const uint32_t old = s_fl ? atomicOr(ap.flags, s_fl) : *ap.flags;
+        if (s_fl) atomicOr(ap.flags, s_fl);
         if (a.pin) {
-            for (int i = 0; i < 16; i++) a.pin[i] = a.totals[i];     // (this thread's own writes)
-            a.pin[a.pin_off[3]] = old | s_fl;
+#pragma unroll
+            for (int i = 0; i < 16; i++) a.pin[i] = t_tot[i];
+            a.pin[a.pin_off[3]] = f_start | s_fl;
         }
     }
     if (a.pin) {
@@ -2102,7 +2270,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
 }
 
 bool tiny_fits(int D, int Kp, int M2, int KM, int K, uint32_t tiles) {
-    const size_t pre = (size_t)Kp * (M2 + 1) * 8 + (size_t)((M2 * D + 3) & ~3) * 4 + (size_t)Kp * (M2 * D + 1) * 8;
+    const size_t pre = (size_t)Kp * (M2 + 1) * 8 + (size_t)((M2 * D + 3) & ~3) * 4 + (size_t)Kp * (M2 * D + 1) * 8 + 64;
     const size_t brute = (size_t)tiny_brute_rows(D) * (D * 8 + 12) + kTinyFixed;
     return M2 == kTinyM2 && KM <= kHistMaxKM && K <= kMaxK && Kp <= kMaxK && tiles <= kTinyTiles &&
            pre <= kTinyArena && brute <= kTinyArena;
@@ -2132,6 +2300,22 @@ void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st) {
         SKY_DISPATCH_D(D, (k_cand_filter<DD, false><<<nblk(a.mt, kThreads), kThreads, 0, st>>>(
                               a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.pr2, a.npr2, a.live)));
     }
+}
+
+void launch_cand_min(int D, const CandArgs &a, hipStream_t st) {
+    if (!a.mt) return;
+    const unsigned g = std::min<unsigned>(nblk(a.mt, kThreads), 256u);
+    SKY_DISPATCH_D(D, (k_cand_min<DD><<<g, kThreads, 0, st>>>(a.rows, a.key, a.mt, a.d_mt, a.Kp, a.M2, a.cmin)));
+}
+
+bool cand_fused_fits(int D, int Kp, int M2) {
+    return M2 <= 64 && (size_t)Kp * (M2 * D + 1) * sizeof(double) <= 32768;
+}
+
+void launch_cand_fused(int D, const CandArgs &a, hipStream_t st) {
+    if (!a.mt) return;
+    const size_t lds = (size_t)a.Kp * (a.M2 * D + 1) * sizeof(double);
+    SKY_DISPATCH_D(D, (k_cand_fused<DD><<<cand_fused_tiles(a.mt), kThreads, lds, st>>>(a)));
 }
 
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,

@@ -143,8 +143,25 @@ struct CandArgs {
     int32_t *npr2;                // [Kp]
     uint32_t *live;               // [mt] out
     const uint32_t *d_mt = nullptr;   // device slot count (mt is then its bound)
+    // the fused pass (k_cand_fused: pick + live test + scan + ordered compaction in one launch)
+    double *rows2 = nullptr;
+    uint64_t *key2 = nullptr;
+    uint32_t *src2 = nullptr;
+    uint32_t *d_live = nullptr;           // out: surviving slots
+    int32_t *pruner_slot = nullptr;       // remapped in place (appended pruner slots)
+    const int32_t *entries = nullptr;     // pruner slot entry -> k * M + j
+    unsigned long long *lb = nullptr;     // [cand_fused_tiles(mt)] look-back words, zeroed
+    uint32_t *ticket = nullptr;           // zeroed
+    uint32_t *err = nullptr;              // kFlagRadixSpin if a look-back ran out of spins
 };
 void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st);
+// the criterion minima alone (k_cand_min), for the fused pass after it
+void launch_cand_min(int D, const CandArgs &a, hipStream_t st);
+// the fused pass: false (nothing launched) when its pruner image does not fit LDS -- the caller
+// then runs k_cand_pick / k_cand_filter / the scan / k_cand_compact
+bool cand_fused_fits(int D, int Kp, int M2);
+inline uint32_t cand_fused_tiles(uint32_t mt) { return (mt + kThreads - 1) / kThreads; }
+void launch_cand_fused(int D, const CandArgs &a, hipStream_t st);
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
                          int32_t *pruner_slot, int KM, hipStream_t st);
 
@@ -489,6 +506,7 @@ struct TinyArgs {
     int rounds = 0, M2 = 0;
     uint32_t bound[4] = {};               // plan bounds (slots entering round r; [rounds]: the brute)
     double *pr2 = nullptr;                // [Kp*M2][D] second-level pruners (scratch)
+    const unsigned long long *cmin0 = nullptr;   // round 0's criterion minima from k_cand_min (or nullptr)
     uint32_t *live = nullptr, *livepos = nullptr;        // [bound0] scratch
     double *rows_r[3] = {};               // the rounds' compaction targets (f64 slot rows)
     uint64_t *key_r[3] = {};

@@ -184,3 +184,20 @@ def test_tiny_tail_miss(gpu_engine_factory, oracle):
         r, _ = check(eng, oracle, oracle.synth(0, 3, 20000, seed=seed), 8)
         assert r & PLANNED and not r & TINY, r
     eng.close()
+
+
+def test_cand_fused_pass_equals_launch_chain(gpu_engine_factory, oracle):
+    """The prefilter's pick / live test / scan / compaction as one launch with a decoupled look-back
+    (k_cand_fused, default) and as the launch chain (SKY_CAND_FUSED=0, read per query): both routes
+    (synchronised, planned) give the oracle's answer on a stream with prefilter rounds."""
+    for knob in ("1", "0"):
+        os.environ["SKY_CAND_FUSED"] = knob
+        try:
+            eng = gpu_engine_factory(8, 16, "mr-angle")
+            r0, m0 = check(eng, oracle, oracle.synth(2, 8, 2500000, seed=111), 16)
+            r1, m1 = check(eng, oracle, oracle.synth(2, 8, 2500000, seed=112), 16)
+            assert m0 >= 4096                       # learned with a prefilter round, replayed with it
+            assert r1 & PLANNED
+            eng.close()
+        finally:
+            del os.environ["SKY_CAND_FUSED"]
