@@ -164,6 +164,10 @@ static size_t slot_min() {
 }
 constexpr uint32_t kPrefilterProbe = 16;  // a skipped prefilter is probed again every 16 queries
 constexpr uint32_t kTinyBlock = 16;       // plans learned without the one-workgroup tail after it missed
+constexpr uint32_t kPickInFilterMax = 16u << 20;   // tuples up to which the filter picks its own pruners
+// slots up to which a prefilter round runs as the fused pass: beyond, its per-workgroup pick and the
+// look-back cost what the launches it saves cost (C4's 241k slots: 46 us fused vs 39 us + 5 launches)
+constexpr uint32_t kCandFusedMax = 65536;
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = SKY_ENV("SKY_FUSED_OUT");
@@ -1085,7 +1089,7 @@ static int plan_prepare(Pipe &p, int D, bool tiny, FillSet &fill) {
             size_t lb = 0;
             uint32_t b = pl.bound[0];
             for (int r = 0; r < pl.rounds; r++) {
-                lb += cand_lb_bytes(b);
+                if (b <= kCandFusedMax) lb += cand_lb_bytes(b);
                 b = std::min(pl.bound[r + 1], b);
             }
             SKY_TRY(p.cand_lb.ensure(lb));
@@ -1329,7 +1333,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         ca.live = p.live.as<uint32_t>();
         uint32_t *d_live = p.totals.as<uint32_t>() + 11 + round;
         c.ktimer_begin("prefilter", st);
-        if (cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled()) {   // (plan_prepare zeroed its words)
+        if (cand_fused_fits(D, p.Kp, M2) && bound <= kCandFusedMax && !cand_fused_disabled()) {   // (plan_prepare zeroed its words)
             ca.rows2 = dr->as<double>();
             ca.key2 = dk->as<uint64_t>();
             ca.src2 = ds->as<uint32_t>();
@@ -1503,9 +1507,12 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 (int)tiny_fits(D, p.Kp, std::min(prefilter_m2(), 2048 / p.Kp), KM, in.K, tiles));
     if (planned) SKY_TRY(plan_prepare(p, D, tiny, fill));
     HIP_TRY(fill.launch(st));
-    // the sample minima only: the filter's workgroups pick the pruners from them (one launch less)
+    // small streams: the sample minima only, the filter's workgroups pick the pruners from them (one
+    // dependent launch less, where launches are the query's cost); large ones keep k_pick_pruners
+    // (every filter workgroup's prologue would wait on two more dependent loads)
+    const bool pick_in_filter = n <= kPickInFilterMax;
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
-                          p.pruners.as<double>(), p.npr.as<int32_t>(), st, false);
+                          p.pruners.as<double>(), p.npr.as<int32_t>(), st, !pick_in_filter);
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
@@ -1534,7 +1541,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.tile_hist = p.hist_count ? p.tile_hist.as<uint32_t>() : nullptr;
     fa.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
     fa.dom_kj = p.dom_kj;
-    fa.pick_gmin = p.pmin.as<unsigned long long>();
+    fa.pick_gmin = pick_in_filter ? p.pmin.as<unsigned long long>() : nullptr;
     fa.pick_S = S;
     fa.pruners_w = p.pruners.as<double>();
     fa.npr_w = p.npr.as<int32_t>();
@@ -1634,7 +1641,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(dk->ensure((size_t)mt0 * 8));
         SKY_TRY(ds->ensure((size_t)mt0 * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(mt0 + 1) * 4 + 64));
-        const bool fused = cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled();
+        const bool fused = cand_fused_fits(D, p.Kp, M2) && mt0 <= kCandFusedMax && !cand_fused_disabled();
         if (fused) {
             SKY_TRY(p.cand_lb.ensure(cand_lb_bytes(mt0)));
             fill.add(p.cand_lb.p, cand_lb_bytes(mt0));

@@ -1007,6 +1007,7 @@ constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbCount 
 // tile only waits for tiles already running; bounded spin -> kFlagRadixSpin), which keeps the
 // compaction in slot order exactly as the scan + k_cand_compact did.  The appended pruner slots'
 // indices are remapped from their entries (a dropped one: -1).
+constexpr int kCandFI = 4;                 // slots per thread in k_cand_fused
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
     constexpr int DP = padded_dims<double>(D);
@@ -1052,33 +1053,45 @@ __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
     }
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint32_t j = tile * kThreads + threadIdx.x;
-    bool liv = false;
-    double v[D];
-    uint64_t kv = 0;
-    uint32_t sv = 0;
-    if (j < mt) {
-        kv = a.key[j];
-        sv = a.src[j];
-        load_trow<double, D>(a.rows + (size_t)j * DP, v);
-        const int k = (int)(kv >> 56);
-        const double *pr = s_pr2 + (size_t)k * PS;
-        const int np = s_np[k];
-        bool dom = false;
-        for (int q = 0; q < np; q++) {
-            bool le = true, lt = false;
+    // kCandFI consecutive slots per thread (the tile's order = slot order): the pick above is
+    // paid once per kCandFI * kThreads slots
+    const uint32_t j0 = (tile * kThreads + threadIdx.x) * kCandFI;
+    bool liv[kCandFI];
+    double v[kCandFI][D];
+    uint64_t kv[kCandFI];
+    uint32_t sv[kCandFI];
 #pragma unroll
-            for (int d = 0; d < D; d++) {
-                const double x = pr[q * D + d];
-                le &= x <= v[d];
-                lt |= x < v[d];
+    for (int u = 0; u < kCandFI; u++) {
+        const uint32_t jc = min(j0 + u, mt > 0 ? mt - 1u : 0u);
+        kv[u] = a.key[jc];
+        sv[u] = a.src[jc];
+        load_trow<double, D>(a.rows + (size_t)jc * DP, v[u]);
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kCandFI; u++) {
+        liv[u] = false;
+        if (j0 + u < mt) {
+            const int k = (int)(kv[u] >> 56);
+            const double *pr = s_pr2 + (size_t)k * PS;
+            const int np = s_np[k];
+            bool dom = false;
+            for (int q = 0; q < np; q++) {
+                bool le = true, lt = false;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    const double x = pr[q * D + d];
+                    le &= x <= v[u][d];
+                    lt |= x < v[u][d];
+                }
+                dom |= le & lt;
             }
-            dom |= le & lt;
+            liv[u] = !dom;
+            cnt += liv[u] ? 1u : 0u;
         }
-        liv = !dom;
     }
     uint32_t bt;
-    const uint32_t pl = block_scan_excl(liv ? 1u : 0u, s_w, bt);
+    const uint32_t pl = block_scan_excl(cnt, s_w, bt);
     if (threadIdx.x < 64) {
         unsigned long long excl = 0;
         if (lane == 0)
@@ -1120,13 +1133,18 @@ __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
         }
     }
     __syncthreads();
-    const uint32_t pos = (uint32_t)s_prefix + pl;
-    if (liv) {
-        store_row<double, D>(a.rows2 + (size_t)pos * DP, v);
-        a.key2[pos] = kv;
-        a.src2[pos] = sv;
+    uint32_t pos = (uint32_t)s_prefix + pl;
+#pragma unroll
+    for (int u = 0; u < kCandFI; u++) {
+        if (liv[u]) {
+            store_row<double, D>(a.rows2 + (size_t)pos * DP, v[u]);
+            a.key2[pos] = kv[u];
+            a.src2[pos] = sv[u];
+        }
+        if (j0 + u < mt && (sv[u] & 0x80000000u))
+            a.pruner_slot[a.entries[sv[u] & 0x7fffffffu]] = liv[u] ? (int32_t)pos : -1;
+        pos += liv[u] ? 1u : 0u;
     }
-    if (j < mt && (sv & 0x80000000u)) a.pruner_slot[a.entries[sv & 0x7fffffffu]] = liv ? (int32_t)pos : -1;
 }
 
 // order-preserving compaction of the live slots (rows, keys, sources); the appended

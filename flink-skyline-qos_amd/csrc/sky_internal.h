@@ -160,7 +160,7 @@ void launch_cand_min(int D, const CandArgs &a, hipStream_t st);
 // the fused pass: false (nothing launched) when its pruner image does not fit LDS -- the caller
 // then runs k_cand_pick / k_cand_filter / the scan / k_cand_compact
 bool cand_fused_fits(int D, int Kp, int M2);
-inline uint32_t cand_fused_tiles(uint32_t mt) { return (mt + kThreads - 1) / kThreads; }
+inline uint32_t cand_fused_tiles(uint32_t mt) { return (mt + 4 * kThreads - 1) / (4 * kThreads); }   // kCandFI = 4
 void launch_cand_fused(int D, const CandArgs &a, hipStream_t st);
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
                          int32_t *pruner_slot, int KM, hipStream_t st);

@@ -315,7 +315,8 @@ int sky_profile_enable(sky_ctx *ctx, int on);
 /* counters_out: n, candidates, reps (slots on the small-set route), global reps, output size,
  * SFS rounds, pair tests, and [7] = bit0 f64 compares, bit1 score ties, bit2 packed u16,
  * bit3 the planned (device-sized, no mid-query host read) route served the query, bit4 a
- * planned attempt missed and the query re-ran synchronised, bits 8.. bounding-box tiles */
+ * planned attempt missed and the query re-ran synchronised, bit5 the planned route's tail ran
+ * as one workgroup (k_tiny_tail), bits 8.. bounding-box tiles */
 int sky_profile_phases(sky_ctx *ctx, double *ms_out /* SKY_PHASES */, int64_t *counters_out /* 8 */);
 int sky_profile_kernel(sky_ctx *ctx, const char *name, double *total_ms, int64_t *launches,
                        int64_t *units);
