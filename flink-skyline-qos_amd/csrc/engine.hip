@@ -8,6 +8,7 @@
 // Host synchronisations happen only where the host must size the next launch
 // (candidate count, representative count, per-round SFS segment counts).
 #include "engine.h"
+#include "sky_tail.h"
 #include "knobs.h"
 #include "ctx.h"
 
@@ -168,6 +169,7 @@ constexpr uint32_t kPickInFilterMax = 16u << 20;   // tuples up to which the fil
 // slots up to which a prefilter round runs as the fused pass: beyond, its per-workgroup pick and the
 // look-back cost what the launches it saves cost (C4's 241k slots: 46 us fused vs 39 us + 5 launches)
 constexpr uint32_t kCandFusedMax = 65536;
+constexpr uint32_t kTailTilesMax = 1024;        // tiles up to which the brute route's counts run as k_tail_counts
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
     const char *e = SKY_ENV("SKY_FUSED_OUT");
@@ -225,6 +227,10 @@ static bool cand_fused_disabled() {   // SKY_CAND_FUSED=0: pick / filter / scan 
 }
 // the fused prefilter pass's look-back words of each planned round: [tiles][u64] + a ticket word
 static size_t cand_lb_bytes(uint32_t bound) { return (size_t)cand_fused_tiles(bound) * 8 + 64; }
+static bool tail_counts_disabled() {   // SKY_TAIL_COUNTS=0: hist counts / scan / stat reduce / gather launches (A/B knob)
+    const char *e = SKY_ENV("SKY_TAIL_COUNTS");
+    return e && e[0] == '0';
+}
 static bool tiny_disabled() {    // SKY_TINY=0: the planned tail as one launch per stage (A/B knob)
     const char *e = SKY_ENV("SKY_TINY");
     return e && e[0] == '0';
@@ -882,6 +888,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     oa.out_cnt = p.out_cnt.as<uint32_t>();
     oa.select_local = 0;
     p.fused = slot_stats && (in.out_ids || in.out_org) && !fused_disabled();
+    // the brute route's counts, scan, stats and final read in one workgroup (k_tail_counts)
+    // (up to kTailTilesMax tiles: one workgroup's pass over C2's 4883 tiles took 20 us, slower than
+    // the four launches it replaces; C1-sized runs take the one-workgroup tail anyway)
+    const bool tailk = !tiny && brute && p.fused && !fused_onepass() && p.hist_count && slot_stats &&
+                       tiles <= kTailTilesMax && (p.segalive.p && p.seg_begin.p) && !tail_counts_disabled();
     p.fused_ids = in.out_ids;
     p.fused_org = in.out_org;
     c.ktimer_begin("out", st);
@@ -902,8 +913,34 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     } else if (p.fused) {
         // count pass -> tile scan -> write pass, chained on the device (no host read in
         // between; positions >= out_cap are not written, the final read reports the total)
-        // (the one-workgroup tail wrote the counts, their offsets and the total)
-        if (!tiny) {
+        // (the one-workgroup tail wrote the counts, their offsets and the total; on the brute route
+        // k_tail_counts writes them, the stats and the final read in one launch)
+        if (tailk) {
+            SKY_TRY(p.statk.ensure((size_t)p.K * 16));
+            TailArgs ta{};
+            ta.tile_hist = p.tile_hist.as<uint32_t>();
+            ta.tile_cand = p.tile_cand.as<uint32_t>();
+            ta.pruner_fate = p.pruner_fate.as<uint8_t>();
+            ta.KM = KM;
+            ta.K = p.K;
+            ta.Kp = p.Kp;
+            ta.ntiles = tiles;
+            ta.out_cnt = p.out_cnt.as<uint32_t>();
+            ta.out_off = p.out_off.as<uint32_t>();
+            ta.totals = p.totals.as<uint32_t>();
+            ta.lsz = p.lsz.as<unsigned long long>();
+            ta.surv = p.surv.as<unsigned long long>();
+            ta.statk = p.statk.as<unsigned long long>();
+            ta.segalive = p.segalive.as<uint32_t>();
+            ta.segn = p.seg_begin.as<uint32_t>();
+            ta.flags = p.flags.as<uint32_t>();
+            ta.dup_cnt = p.dup_cnt.as<uint32_t>();
+            SKY_TRY(p.pinned(tiny_pin_layout(p.K, p.Kp, KM, ta.pin_off)));
+            ta.pin = reinterpret_cast<uint32_t *>(p.pin);
+            c.ktimer_begin("outc", st);
+            launch_tail_counts(ta, st);
+            c.ktimer_end("outc", st, n);
+        } else if (!tiny) {
             c.ktimer_begin("outc", st);
             if (p.hist_count)
                 launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(),
@@ -936,7 +973,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     STAGE(st, "fate");
     uint32_t nout = 0;
     SKY_TRY(p.statk.ensure((size_t)p.K * 16));
-    if (!tiny)
+    if (!tiny && !tailk)
         launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
                            p.statk.as<unsigned long long>(), st);
     std::vector<unsigned long long> sk2((size_t)p.K * 2);
@@ -950,7 +987,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         SKY_TRY(sync_read(p, st, {{p.totals.p, 64}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
                                   {p.flags.p, 4}, {p.dup_cnt.p, (size_t)KM * 4}},
-                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}, tiny));
+                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}, tiny || tailk));
         nout = tot[3];
 #ifdef SKY_MEASURE
         if (SKY_MEASURE_ENV("SKY_FILTER_COUNT")) {   // k_filter's stores (tools/: the write itemisation)

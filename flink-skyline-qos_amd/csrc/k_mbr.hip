@@ -522,8 +522,17 @@ __device__ __forceinline__ uint64_t mbr_share(uint64_t m, uint32_t &ord, uint32_
 // With 8-row sub-boxes (packed u16 rows) a y meets 2.6x fewer rows than with 16-row ones.
 // packed-u16 rows: the register budget capped for 6 waves per SIMD (79 VGPRs at YT = 2, no spill;
 // the 5 waves the 82-VGPR default allows: 19.1 vs 18.8 ms at std-anti 8D 10M)
+// waves per SIMD the pair pass's register budget is sized for: 7 for one-tile work items (2M: pass
+// 3.54 -> 3.40 ms), 6 for the two-tile items of >= 65536 y tiles (10M: 7 is 1.5 % slower;
+// profiles/r05_dominance_ab.txt)
+#ifndef SKY_MBR_WPE
+#define SKY_MBR_WPE 6
+#endif
+#ifndef SKY_MBR_WPE1
+#define SKY_MBR_WPE1 7
+#endif
 template <class R, bool FULL, bool GM, int YT>
-__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(R::NW <= 4 ? 6 : 1))) void k_mbr_pairs(const uint32_t *__restrict__ trows,
+__global__ __launch_bounds__(kMbrPairThreads) __attribute__((amdgpu_waves_per_eu(R::NW <= 4 ? (YT == 1 ? SKY_MBR_WPE1 : SKY_MBR_WPE) : 1))) void k_mbr_pairs(const uint32_t *__restrict__ trows,
                                                          const uint32_t *__restrict__ tpart,
                                                          const uint32_t *__restrict__ tmin,
                                                          const uint32_t *__restrict__ tprange,

@@ -13,6 +13,7 @@
 //   k_act_compact  order-preserving compaction of the survivors for the next round.
 // The work is Σ_rounds |R|·|X'| pair tests of D compares each.
 #include "sky_internal.h"
+#include "sky_tail.h"
 
 namespace sky {
 
@@ -440,6 +441,115 @@ __global__ __launch_bounds__(kThreads) void k_scatter_alive(const uint32_t *__re
 }
 
 // sum the [shard][K] stat accumulators into [K] (one workgroup per key)
+// The brute route's per-tile output counts (k_out_hist_count: the duplicate groups whose pruner is
+// in G, listed first, plus the tile's candidates in G), their exclusive scan, the stats reduce
+// (k_stat_reduce) and the final read's words into host-mapped memory (k_gather_words), in ONE
+// 1024-thread workgroup: four dependent launches of 4-6 us each before.  Tiles TT per thread and
+// batch, their loads issued together.
+constexpr int kTailThreads = 1024;
+__global__ __launch_bounds__(kTailThreads) void k_tail_counts(TailArgs a) {
+    constexpr int NT = kTailThreads, NW = kTailThreads / 64, TT = 4;
+    __shared__ uint16_t s_gq[kHistMaxKM];
+    __shared__ uint32_t s_ng, s_w[NW];
+    __shared__ unsigned long long s_st[2 * kMaxK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (wave == 0) {
+        uint32_t ng = 0;
+        for (int q0 = 0; q0 < a.KM; q0 += 64) {
+            const bool g = q0 + lane < a.KM && (a.pruner_fate[q0 + lane] & 2u);
+            const uint64_t b = __ballot(g);
+            if (g) s_gq[ng + __popcll(b & (lane ? (~0ull >> (64 - lane)) : 0ull))] = (uint16_t)(q0 + lane);
+            ng += (uint32_t)__popcll(b);
+        }
+        if (lane == 0) s_ng = ng;
+    }
+    // stats: wave w reduces partitions w, w + NW, ... over the shards
+    for (int k = wave; k < a.K; k += NW) {
+        unsigned long long l = 0, sv = 0;
+        for (int sh = lane; sh < kStatShards; sh += 64) {
+            l += a.lsz[(size_t)sh * a.K + k];
+            sv += a.surv[(size_t)sh * a.K + k];
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            l += __shfl_xor(l, o, 64);
+            sv += __shfl_xor(sv, o, 64);
+        }
+        if (lane == 0) {
+            s_st[k] = l;
+            s_st[a.K + k] = sv;
+            a.statk[k] = l;
+            a.statk[a.K + k] = sv;
+        }
+    }
+    __syncthreads();
+    const uint32_t ng = s_ng;
+    uint32_t base = 0;
+    for (uint32_t t0 = 0; t0 < a.ntiles; t0 += TT * NT) {           // block-uniform
+        uint32_t c[TT], tot_t = 0;
+#pragma unroll
+        for (int u = 0; u < TT; u++) {
+            const uint32_t t = t0 + (uint32_t)tid * TT + u;          // consecutive tiles per thread
+            c[u] = 0;
+            if (t < a.ntiles) {
+                const uint32_t *h = a.tile_hist + (size_t)t * a.KM;
+                for (uint32_t i = 0; i < ng; i++) c[u] += h[s_gq[i]];
+                c[u] += a.tile_cand[t];
+            }
+            tot_t += c[u];
+        }
+        // block exclusive scan of the per-thread sums
+        uint32_t inc = tot_t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        uint32_t wb = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const uint32_t x = s_w[i];
+            wb += i < wave ? x : 0u;
+            tot += x;
+        }
+        __syncthreads();
+        uint32_t off = base + wb + inc - tot_t;
+#pragma unroll
+        for (int u = 0; u < TT; u++) {
+            const uint32_t t = t0 + (uint32_t)tid * TT + u;
+            if (t < a.ntiles) {
+                a.out_cnt[t] = c[u];
+                a.out_off[t] = off;
+            }
+            off += c[u];
+        }
+        base += tot;
+    }
+    if (tid == 0) a.totals[3] = base;
+    __syncthreads();
+    if (a.pin) {
+        if (tid < 16) a.pin[tid] = tid == 3 ? base : a.totals[tid];
+        for (int q = tid; q < a.K; q += NT) {
+            a.pin[a.pin_off[0] + 2 * q] = (uint32_t)s_st[q];
+            a.pin[a.pin_off[0] + 2 * q + 1] = (uint32_t)(s_st[q] >> 32);
+            a.pin[a.pin_off[0] + 2 * (a.K + q)] = (uint32_t)s_st[a.K + q];
+            a.pin[a.pin_off[0] + 2 * (a.K + q) + 1] = (uint32_t)(s_st[a.K + q] >> 32);
+        }
+        for (int q = tid; q < a.Kp; q += NT) {
+            a.pin[a.pin_off[1] + q] = a.segalive[q];
+            a.pin[a.pin_off[2] + q] = a.segn[q];
+        }
+        if (tid == 0) a.pin[a.pin_off[3]] = *a.flags;
+        for (int q = tid; q < a.KM; q += NT) a.pin[a.pin_off[4] + q] = a.dup_cnt[q];
+    }
+}
+
+void launch_tail_counts(const TailArgs &a, hipStream_t st) {
+    k_tail_counts<<<1, kTailThreads, 0, st>>>(a);
+}
+
 __global__ __launch_bounds__(kThreads) void k_stat_reduce(const unsigned long long *__restrict__ lsz,
                                                           const unsigned long long *__restrict__ surv, int K,
                                                           unsigned long long *__restrict__ out) {

@@ -201,3 +201,21 @@ def test_cand_fused_pass_equals_launch_chain(gpu_engine_factory, oracle):
             eng.close()
         finally:
             del os.environ["SKY_CAND_FUSED"]
+
+
+@pytest.mark.parametrize("algo,dist,D,n,P", [("mr-angle", 0, 5, 200000, 16), ("mr-grid", 1, 4, 1000000, 8)])
+def test_tail_counts_equals_launch_chain(gpu_engine_factory, oracle, algo, dist, D, n, P):
+    """The brute route's output counts, scan, stats and final read in one workgroup (k_tail_counts,
+    default) and as four launches (SKY_TAIL_COUNTS=0, read per query): the oracle's answer on the
+    synchronised and the planned brute route either way."""
+    short = algo.split("-")[1]
+    for knob in ("1", "0"):
+        os.environ["SKY_TAIL_COUNTS"] = knob
+        try:
+            eng = gpu_engine_factory(D, P, algo)
+            check(eng, oracle, oracle.synth(dist, D, n, seed=121), P, short)
+            r, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=122), P, short)
+            assert r & PLANNED
+            eng.close()
+        finally:
+            del os.environ["SKY_TAIL_COUNTS"]
