@@ -46,6 +46,7 @@ from skyline.dist import distributed_query  # noqa: E402
 
 METRIC = "skyline tuples/sec + p50 query latency, 8D anti-corr, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.29 measured copy)
+PCIE_PEAK_GBS = 64.0    # PCIe 5.0 x16, one direction (the host link the ingest-inclusive rate crosses)
 # VALU compare peaks: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T 32-bit lane-ops/s; k_dom16
 # compares packed u16 pairs (v_pk_sub_u16: 2 compares per lane-op) -> 157.3 T compares/s
 VALU_PEAK_32 = 256 * 4 * 32 * 2.4e9
@@ -207,15 +208,31 @@ def config_line(name, dev, dev_index, steps, warmup, with_cpu):
     vals, ids = make_stream(eng, cfg["dist"], n, seed, 0, dev)
     out_ids = torch.empty(n, dtype=torch.int64, device=dev)
     out_org = torch.empty(n, dtype=torch.int32, device=dev)
-    elapsed, step_ms, g, kt = time_steps(lambda: eng.query_dev(ids, vals, out_ids, out_org, n), eng, steps, warmup,
-                                         False)
+    step = lambda: eng.query_dev(ids, vals, out_ids, out_org, n)   # noqa: E731
+    elapsed, step_ms, g, kt = time_steps(step, eng, steps, warmup, False)
     phases, counters = eng.phases()
     roof = filter_roofline(eng, D, kt)
     if roof:
         roof["traffic"] = traffic_for(n, D, cfg["dist"])
-    ms = elapsed * 1e3 / steps
-    line = {"metric": METRIC, "value": n / (ms / 1e3), "unit": "tuples/s", "n_gpus": 1, "steps": steps,
-            "warmup": warmup, "ms_per_step": ms, "p50_query_latency_ms": statistics.median(step_ms),
+    # the same steps again with no profiler event in the stream: a HIP-event pair around k_filter
+    # puts ~10 us of gap into a query whose kernels take tens of microseconds (C1, C2); the
+    # roofline above comes from the timed steps with the events
+    eng.sync()
+    t0 = time.perf_counter()
+    bare_ms = []
+    for _ in range(max(steps, 20)):
+        ts = time.perf_counter()
+        step()
+        eng.sync()
+        bare_ms.append((time.perf_counter() - ts) * 1e3)
+    bare_elapsed = time.perf_counter() - t0
+    ms = bare_elapsed * 1e3 / len(bare_ms)
+    ms_timed = elapsed * 1e3 / steps
+    line = {"metric": METRIC, "value": n / (ms / 1e3), "unit": "tuples/s", "n_gpus": 1, "steps": len(bare_ms),
+            "warmup": warmup, "ms_per_step": ms, "p50_query_latency_ms": statistics.median(bare_ms),
+            "with_kernel_timers": {"steps": steps, "ms_per_step": ms_timed, "p50_query_latency_ms":
+                                   statistics.median(step_ms), "note": "HIP events around k_filter in every "
+                                   "step (the roofline's measurement)"},
             "dtype": "f64", "config": {"workload": cfg["workload"], "tuples": n, "dims": D, "partitions": P,
                                        "algo": cfg["algo"], "dist": cfg["dist"], "seed": seed, "skyline_size": g},
             "roofline": roof, "phases_ms_last_step": phases,
@@ -363,6 +380,43 @@ def dominance_run(dev, D, P, n, seed, steps, warmup):
             "tile_pairs_tested": int(counters[7]) >> 8 if mbr else None}
 
 
+def dominance_dense_run(dev, D, P, n, seed, steps=3):
+    """The dense all-pairs dominance kernel alone (sky_profile_pairs_dev: k_brute16_pairs, the
+    small-set route's pair pass, every row against every row -- the pairs of the BNL loops
+    FlinkSkyline.java:424-441 without any pruning) on n rows of the labelled std-anti generator
+    with their MR-Angle keys: D x n^2 compares / the kernel's HIP-event time, against the
+    packed-u16 compare peak.  n = 16384 is the brute route's slot ceiling."""
+    eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev.index or 0)
+    vals = torch.empty((n, D), dtype=torch.float64, device=dev)
+    ids = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.synth_dev("std_anti", n, vals, ids, seed=seed)
+    keys = torch.empty(n, dtype=torch.int32, device=dev)
+    eng.partition_keys_dev(vals, keys)
+    fates = torch.empty(n, dtype=torch.int32, device=dev)
+    eng.profile_pairs_dev(vals, keys, fates)              # warm-up
+    ms = []
+    kind = 0
+    for _ in range(steps):
+        kind, t = eng.profile_pairs_dev(vals, keys, fates)
+        ms.append(t)
+    eng.sync()
+    in_g = int(((fates & 2) == 0).sum().item())
+    eng.close()
+    t = statistics.median(ms)
+    pairs = n * n
+    achieved = D * pairs / (t / 1e3)
+    return {"bound": "valu", "kernel": "k_brute16_pairs (dense all-pairs, packed u16, HIP events)"
+            if kind == 0 else "k_brute_pairs (f32/f64)",
+            "workload": f"std_anti {D}D, {n} rows, MR-Angle P={P} keys, every row against every row",
+            "pair_tests": pairs, "compares": D * pairs, "kernel_ms": t, "achieved": achieved,
+            "peak": VALU_PEAK_PK16, "unit": "compares/s", "frac": achieved / VALU_PEAK_PK16,
+            "peak_32bit": VALU_PEAK_32, "frac_32bit": achieved / VALU_PEAK_32,
+            "rows_not_dominated": in_g,
+            "peak_note": "packed-u16 compare peak: 2 compares per v_pk_sub_u16 lane-op at 128 lanes/clk/CU; "
+                         "the kernel issues 4 v_pk_sub_u16 + 1 v_sub_u32 + 2 v_or3 + 1 v_min (+2 v_mov per 4 "
+                         "rows) per 8D pair test, so issue-bound it tops out near 8/8.5/2 = 0.47 of it"}
+
+
 def csv_ingest_run(eng, ids, vals, n, D, steps, out_ids, out_org):
     """Bulk CSV -> SoA decode (ServiceTuple.fromString, ServiceTuple.java:89-104)
     on the same stream, formatted as the producer's payload (unified_producer.py:174) in HBM.
@@ -422,34 +476,42 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     ids = torch.from_numpy(ids_np).pin_memory().numpy()
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
     eng.warmup()                                  # first launches / allocations, before the stream starts
-    st = skyline.SkylineStream(eng, window)
-    st.reserve(window if window else n)          # result buffers pinned once, before the stream starts
-    lat_int, lat_ids, copy_ms, sizes = [], [], [], []
-    eng.profile(1)                                # light timers only (the k_filter roofline)
-    eng.profile_reset()
-    t_start = time.perf_counter()
-    for t in range(triggers):
-        base = t * per_trigger
-        for b0 in range(base, base + per_trigger, batch):
-            st.append(ids[b0:b0 + batch], vals[b0:b0 + batch])
-            if b0 == base and t:
-                # the last trigger's ids reached host memory while this micro-batch went in
-                cm = st.wait()
-                copy_ms.append(cm)
-                lat_ids.append(lat_int[-1] + cm)
-        tq = time.perf_counter()
-        g = st.query_async_host_view()            # returns with the integers (skyline size, stats)
-        lat_int.append((time.perf_counter() - tq) * 1e3)
-        sizes.append(g)
-    cm = st.wait()
-    copy_ms.append(cm)
-    lat_ids.append(lat_int[-1] + cm)
-    total = time.perf_counter() - t_start
-    eng.profile(False)
+
+    def run_stream(timers):
+        st = skyline.SkylineStream(eng, window)
+        st.reserve(window if window else n)      # result buffers pinned once, before the stream starts
+        lat_int, lat_ids, copy_ms, sizes = [], [], [], []
+        eng.profile(1 if timers else 0)          # light timers only (the k_filter roofline)
+        eng.profile_reset()
+        t_start = time.perf_counter()
+        for t in range(triggers):
+            base = t * per_trigger
+            for b0 in range(base, base + per_trigger, batch):
+                st.append(ids[b0:b0 + batch], vals[b0:b0 + batch])
+                if b0 == base and t:
+                    # the last trigger's ids reached host memory while this micro-batch went in
+                    cm = st.wait()
+                    copy_ms.append(cm)
+                    lat_ids.append(lat_int[-1] + cm)
+            tq = time.perf_counter()
+            g = st.query_async_host_view()        # returns with the integers (skyline size, stats)
+            lat_int.append((time.perf_counter() - tq) * 1e3)
+            sizes.append(g)
+        cm = st.wait()
+        copy_ms.append(cm)
+        lat_ids.append(lat_int[-1] + cm)
+        total = time.perf_counter() - t_start
+        eng.profile(False)
+        resident, _ = st.size()
+        vectors = st.vectors()
+        st.close()
+        return lat_int, lat_ids, copy_ms, sizes, total, resident, vectors
+
+    # the stream as measured: no profiler event in it (an event pair around k_filter adds ~10 us
+    # to a trigger of ~0.3 ms); then the same stream again with the light timers, for the roofline
+    lat_int, lat_ids, copy_ms, sizes, total, resident, vectors = run_stream(False)
+    t_lat = run_stream(True)[0]
     roof = filter_roofline(eng, D)
-    resident, _ = st.size()
-    vectors = st.vectors()
-    st.close()
     eng.close()
     rate = n / total
     lat = lat_ids
@@ -469,6 +531,7 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
             "ids_p50_latency_ms": statistics.median(lat), "ids_p90_latency_ms": sorted(lat)[int(0.9 * len(lat))],
             "ids_max_latency_ms": max(lat), "ids_latencies_ms": [round(x, 3) for x in lat],
             "copy_ms": [round(x, 3) for x in copy_ms],
+            "with_kernel_timers_p50_query_latency_ms": statistics.median(t_lat),
             "skyline_size_last": sizes[-1], "resident_tuples_last": resident,
             "resident_vectors_last": vectors,
             "resident_note": ("landmark: the local-skyline tuples kept (ids, arrival order) and the distinct "
@@ -722,6 +785,8 @@ def main():
     ap.add_argument("--dom-n", type=int, default=2_000_000, help="tuples of the dominance-bound companion run")
     ap.add_argument("--dom-n-large", type=int, default=10_000_000,
                     help="tuples of the second dominance-bound companion run (0: skip)")
+    ap.add_argument("--dom-n-huge", type=int, default=100_000_000,
+                    help="tuples of the north_star-size dominance run (std-anti 8D; 0: skip)")
     ap.add_argument("--no-dominance", action="store_true")
     ap.add_argument("--no-csv", action="store_true", help="skip the CSV-ingest companion measurement")
     ap.add_argument("--no-stream", action="store_true", help="skip the C5 continuous-query companion measurement")
@@ -871,6 +936,12 @@ def main():
                 extra["dominance_roofline"] = dominance_run(dev, D, P, args.dom_n, seed, 3, 2)
                 if args.dom_n_large:
                     extra["dominance_roofline_large"] = dominance_run(dev, D, P, args.dom_n_large, seed, 3, 2)
+                extra["dominance_dense_roofline"] = dominance_dense_run(dev, D, P, 16384, seed)
+                extra["dominance_dense_roofline_64k"] = dominance_dense_run(dev, D, P, 65536, seed)
+                if args.dom_n_huge:
+                    # north_star's size: the std-anti 8D stream at 100M tuples through the whole query
+                    extra[f"dominance_roofline_{args.dom_n_huge // 1_000_000}M"] = dominance_run(
+                        dev, D, P, args.dom_n_huge, seed, 1, 1)
         line = {
             "metric": METRIC,
             "value": value,
@@ -903,6 +974,16 @@ def main():
         }
         if companion is not None:
             line[f"{companion['scaling']}_scaling_companion"] = companion
+        e2e = extra.get("end_to_end")
+        if e2e:
+            # tuples INGESTED and reflected per second -- with the host->device copy inside
+            # the step (never `value`, which is the HBM-resident re-query rate); bound: PCIe 5.0 x16
+            rh = e2e["rows_h2d"]
+            line["value_end_to_end"] = {
+                "value": rh["tuples_per_s"], "unit": "tuples/s", "bound": "pcie",
+                "workload": rh["workload"], "ms_per_step": rh["ms_per_step"],
+                "h2d_GBs": rh["h2d_GBs"], "peak_GBs": PCIE_PEAK_GBS, "frac_of_pcie": rh["h2d_GBs"] / PCIE_PEAK_GBS,
+                "csv_text_tuples_per_s": e2e["csv_h2d"]["tuples_per_s"]}
         line.update(extra)
         print(json.dumps(line), flush=True)
     eng.close()

@@ -759,3 +759,41 @@ int sky_profile_sort_dev(sky_ctx *c, uint64_t *d_keys, uint32_t *d_vals, int64_t
     return SKY_OK;
     GUARD_END
 }
+
+int sky_profile_pairs_dev(sky_ctx *c, const double *d_values, const int32_t *d_keys, int64_t n, uint32_t *d_fates_out,
+                          int32_t *kind_out, double *ms_out) {
+    GUARD_BEGIN
+    ARG_CHECK(c && d_values && d_keys && d_fates_out && n >= 0 && n < (int64_t)0x7fffffffLL, "bad arguments");
+    SKY_TRY(bind(c));
+    const int D = c->D;
+    const uint32_t m = (uint32_t)n;
+    const size_t DP = (size_t)padded_dims<double>(D);
+    SKY_TRY(c->prof_v.ensure((size_t)std::max<int64_t>(n, 1) * DP * 8));
+    SKY_TRY(c->prof_k.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    SKY_TRY(c->prof_scr.ensure(64));
+    uint32_t *d_flags = c->prof_scr.as<uint32_t>();
+    HIP_TRY(hipMemsetAsync(d_flags, 0, 4, c->st));
+    launch_prof_slots(D, d_values, d_keys, m, c->prof_v.as<double>(), c->prof_k.as<uint64_t>(), d_flags, c->st);
+    uint32_t fl = 0;
+    HIP_TRY(hipMemcpyAsync(&fl, d_flags, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    // the compare type the query's brute pass would take: packed u16 for integer rows with a
+    // tie-free score, f32 when every value is an f32, else f64
+    const bool f64 = (fl & kFlagNotF32) != 0;
+    const bool u16 = !f64 && !(fl & kFlagNotU16) && !(fl & kFlagScoreTies);
+    HIP_TRY(hipMemsetAsync(d_fates_out, 0, (size_t)std::max<int64_t>(n, 1) * 4, c->st));
+    hipEvent_t a = c->take_event(), b = c->take_event();
+    HIP_TRY(hipEventRecord(a, c->st));
+    launch_brute_pairs(D, !f64, u16, c->prof_v.p, c->prof_k.as<uint64_t>(), m, d_fates_out, c->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(b, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, a, b));
+    c->event_pool.push_back(a);
+    c->event_pool.push_back(b);
+    if (kind_out) *kind_out = u16 ? 0 : (f64 ? 2 : 1);
+    if (ms_out) *ms_out = ms;
+    return SKY_OK;
+    GUARD_END
+}

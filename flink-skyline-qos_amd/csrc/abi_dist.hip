@@ -37,6 +37,16 @@ uint64_t dist_brute_pairs() {
     return e ? strtoull(e, nullptr, 10) : (1ull << 28);
 }
 
+// the wide pair pass's per-own-row bits: zeroed when (re)allocated, cleared by its finish kernel
+int dist_dom_ready(Pipe &p, int64_t cap, hipStream_t st) {
+    const size_t bytes = (size_t)std::max<int64_t>(cap, 1) * 4;
+    const void *before = p.dist_dom.p;
+    const size_t cap_before = p.dist_dom.cap;
+    SKY_TRY(p.dist_dom.ensure(bytes));
+    if (p.dist_dom.p != before || p.dist_dom.cap != cap_before) HIP_TRY(hipMemsetAsync(p.dist_dom.p, 0, p.dist_dom.cap, st));
+    return SKY_OK;
+}
+
 int dist_write_block(sky_ctx *c, int64_t *d_block, int64_t cap) {
     Pipe &p = c->main;
     hipStream_t st = c->st;
@@ -112,8 +122,9 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     *union_out = h[7];
     if (!n_own || h[0] > (unsigned long long)cap) return SKY_OK;   // overflow: sky_dist_finish re-runs
     if ((uint64_t)n_own * n_union <= dist_brute_pairs()) {
-        launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, c->main.dist_own.as<uint8_t>(), lsz, surv,
-                               sum, ~0ull, nullptr, st);
+        SKY_TRY(dist_dom_ready(c->main, cap, st));
+        launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, c->main.dist_own.as<uint8_t>(),
+                               c->main.dist_dom.as<uint32_t>(), lsz, surv, sum, ~0ull, nullptr, st);
         return SKY_OK;
     }
     const uint32_t fl = (uint32_t)h[5];
@@ -191,9 +202,24 @@ int dist_union_mbr(sky_ctx *c, const int64_t *d_blocks, int world, int rank, int
     a.flags = c->main.dist_own.as<uint8_t>();
     a.lsz = lsz;
     a.surv = surv;
+#ifdef SKY_MEASURE
+    {
+        const char *e = SKY_MEASURE_ENV("SKY_MBR_DBG");
+        a.x.dbg = e ? atoi(e) : 0;
+    }
+#endif
     c->ktimer_begin("union_fate", st);
     HIP_TRY(launch_mbr_union(a, st));
     c->ktimer_end("union_fate", st, (int64_t)n_own * n_union);
+#ifdef SKY_MEASURE
+    if (a.x.dbg & 4) {        // the scan's funnel (measurement builds): as engine.hip prints it for a query
+        unsigned long long f[5] = {};
+        HIP_TRY(hipMemcpyAsync(f, p.mbr_pairs.p, 40, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "[mbr-union] own %u union %u groups %llu box %llu pre %llu tested %llu pairs %llu\n", n_own,
+                n_union, f[2], f[3], f[4], f[1], f[0]);
+    }
+#endif
     return SKY_OK;
 }
 
@@ -304,8 +330,9 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
             const unsigned __int128 worst = (unsigned __int128)(uint64_t)cap * (uint64_t)cap * (uint64_t)world;
             const unsigned long long limit = worst <= bp ? ~0ull : (unsigned long long)bp;
             c->ktimer_begin("union_fate", st);
-            launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, p.dist_own.as<uint8_t>(), lsz, surv, sum,
-                                   limit, w_miss, st);
+            SKY_TRY(dist_dom_ready(p, cap, st));
+            launch_dist_union_fate(D, d_blocks, world, rank, (uint32_t)cap, K, p.dist_own.as<uint8_t>(),
+                                   p.dist_dom.as<uint32_t>(), lsz, surv, sum, limit, w_miss, st);
             c->ktimer_end("union_fate", st, 0);
             c->dist_last_route = 0;
         } else {

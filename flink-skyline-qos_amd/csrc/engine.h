@@ -121,15 +121,16 @@ struct Pipe {
     bool last_planned = false, last_plan_miss = false;   // the last query's route (counters[7] bits 3, 4)
     bool last_tiny = false;                              // ... its tail in one workgroup (bit 5)
     int64_t tiny_runs = 0;
-    uint32_t tiny_block = 0;
+    uint32_t tiny_block = 0;                             // plans learned without trying the tail (after a miss)
     DevBuf cand_lb;                                      // the fused prefilter pass's look-back words
-    DevBuf dbg_clk;                                      // measurement builds: the tail's phase clocks                             // plans learned without trying the tail (after a miss)
+    DevBuf dbg_clk;                                      // measurement builds: the tail's phase clocks
     bool fused = false;
     const int64_t *fused_ids = nullptr;
     const int32_t *fused_org = nullptr;
     // multi-GPU step (sky_dist_*): what the export left for the merge
     DevBuf dverd;                         // u64 words: [0] the run's verdict, [8..15] the merge's summary
     DevBuf dist_flag, dist_pos, dist_own; // per unit: alive (u32), export position; per own row: fates
+    DevBuf dist_dom;                      // per own row: dominated bits of the wide pair pass (u32, kept zero)
     bool dist_slots = false;              // units = candidate slots (small-set route) or representatives
     uint32_t dist_n = 0;                  // units (their bound on the planned route)
     const uint32_t *dist_d_n = nullptr;   // the unit count on the device (planned route)

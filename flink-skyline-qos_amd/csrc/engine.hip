@@ -959,6 +959,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         ow.out_cap = in.out_cap;
         ow.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
         ow.dom_kj = p.dom_kj;
+        ow.skip_flags = tiny ? p.flags.as<uint32_t>() : nullptr;
         c.ktimer_begin("outw", st);
         launch_out_write(ow, st);
         c.ktimer_end("outw", st, n);
@@ -999,6 +1000,10 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
 #endif
         if (flags2 & kFlagRadixSpin) {
             set_error("a look-back (output) exceeded its spin bound");
+            return SKY_E_HIP;
+        }
+        if (flags2 & kFlagTinyOob) {
+            set_error("the one-workgroup tail computed an index past a buffer's capacity (device guard): no result");
             return SKY_E_HIP;
         }
         if (pr) {
@@ -1227,7 +1232,25 @@ static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size
     ta.statk = p.statk.as<unsigned long long>();
     SKY_TRY(p.pinned(tiny_pin_layout(p.K, p.Kp, KM, ta.pin_off)));   // the final read, written by the tail
     ta.pin = reinterpret_cast<uint32_t *>(p.pin);
+    // the capacities every global index of the tail is checked against on the device (an index
+    // past one skips its access and raises kFlagTinyOob: SKY_E_HIP, not a fault)
+    ta.cap[0] = (uint32_t)std::min<size_t>(cap, 0xffffffffu);
+    ta.cap[1] = (uint32_t)(p.live.cap / 4);
+    ta.cap[2] = (uint32_t)(p.rows2.cap / rb64);
+    ta.cap[3] = (uint32_t)(p.rows3.cap / rb64);
+    ta.cap[4] = (uint32_t)(p.rows2.cap / rb64);
+    ta.cap[5] = (uint32_t)p.alive_l.cap;
+    ta.cap[6] = (uint32_t)(p.status.cap / 2);
+    ta.cap[7] = (uint32_t)(p.pr_entries.cap / 4);
 #ifdef SKY_MEASURE
+    {   // SKY_TINY_CAP=i:c (measurement builds): capacity i forced to c -- the guard's test
+        const char *e = SKY_MEASURE_ENV("SKY_TINY_CAP");
+        if (e) {
+            const int i = atoi(e);
+            const char *c2 = strchr(e, ':');
+            if (i >= 0 && i < 8 && c2) ta.cap[i] = (uint32_t)strtoul(c2 + 1, nullptr, 10);
+        }
+    }
     static const bool tchk = SKY_MEASURE_ENV("SKY_TINY_CHK") != nullptr;
     if (tchk) {                                 // bounds-checked tail: every global index vs its capacity
         {
@@ -1246,14 +1269,6 @@ static int pipe_run_tiny(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, size
         fprintf(stderr, "[tiny-chk] Kp %d M %d M2 %d K %d ntiles %u slot_cap %u D %d\n", ta.ap.Kp, ta.ap.M, ta.M2, ta.K,
                 ta.ntiles, ta.ap.slot_cap, D);
         ta.chk = p.flags.as<uint32_t>() + 13;
-        ta.cap[0] = (uint32_t)cap;
-        ta.cap[1] = (uint32_t)(p.live.cap / 4);
-        ta.cap[2] = (uint32_t)(p.rows2.cap / rb64);
-        ta.cap[3] = (uint32_t)(p.rows3.cap / rb64);
-        ta.cap[4] = (uint32_t)(p.rows2.cap / rb64);
-        ta.cap[5] = (uint32_t)p.alive_l.cap;
-        ta.cap[6] = (uint32_t)(p.status.cap / 2);
-        ta.cap[7] = (uint32_t)(p.pr_entries.cap / 4);
     }
 #endif
 #ifdef SKY_MEASURE
@@ -1377,6 +1392,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
             ca.d_live = d_live;
             ca.pruner_slot = p.pruner_slot.as<int32_t>();
             ca.entries = p.pr_entries.as<int32_t>();
+            ca.KM = KM;
             ca.lb = reinterpret_cast<unsigned long long *>(p.cand_lb.as<char>() + lb_off);
             ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + lb_off + (size_t)cand_fused_tiles(bound) * 8);
             ca.err = p.flags.as<uint32_t>();
@@ -1704,6 +1720,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             ca.d_live = p.totals.as<uint32_t>() + 8;
             ca.pruner_slot = p.pruner_slot.as<int32_t>();
             ca.entries = p.pr_entries.as<int32_t>();
+            ca.KM = KM;
             ca.lb = p.cand_lb.as<unsigned long long>();
             ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + (size_t)cand_fused_tiles(mt0) * 8);
             ca.err = p.flags.as<uint32_t>();

@@ -29,7 +29,7 @@ __global__ void k_plan_verdict(const uint32_t *__restrict__ tot, const uint32_t 
     const uint32_t f = *flags;
     uint32_t v = 0;
     if (f & kFlagNaN) v |= kDistNaN;
-    if (f & (kFlagRadixSpin | kFlagMbrQueue)) v |= kDistError;
+    if (f & (kFlagRadixSpin | kFlagMbrQueue | kFlagTinyOob)) v |= kDistError;
     if (pc.planned) {
         const uint32_t m = tot[0], nps = tot[5];
         bool ok = (uint64_t)m + nps <= pc.cap;
@@ -218,82 +218,189 @@ __global__ __launch_bounds__(kThreads) void k_dist_pack(const double *__restrict
 // (the union of every rank's local skylines holds a dominator of every dominated tuple).  Full
 // dominance test (equal vectors never dominate: the same vector can come from several ranks);
 // x dominates y => sum(x) <= sum(y) (rounding is monotone; values clamped to +-1e300 so that
-// infinities never meet): larger sums skip the compare.  Per-rank stat shares: multiplicities of the own vectors
-// in L_k / G (FlinkSkyline.java:593-608), summed over the ranks by the caller's all-reduce.
-constexpr int kDistTile = 256;
-template <int D>
+// infinities never meet): a union row whose sum exceeds every live own vector's is skipped.
+//
+// A 2D work space walked grid-stride by a fixed grid: item = (64 own vectors, kUnionX union
+// rows).  The union rows of an item are staged in LDS once (f64 row, key, sum); the four waves
+// of the workgroup hold the same 64 own vectors (lane = own vector) and take a quarter of the
+// rows each (every lane reads the same LDS address: a broadcast); the dominated bits are
+// OR-reduced in LDS and leave as one global atomic per own vector and item.  Consecutive
+// workgroups take consecutive own tiles of the same union rows (the rows stay in L2).
+// k_dist_union_finish turns the bits into fates and per-rank stat shares (FlinkSkyline.java:
+// 593-608), and clears them for the next step.
+//
 // limit: the route was chosen from the previous step's sizes; if this step's |own| x |union|
 // (k_dist_summary's sum[4] x sum[3]) exceeds it, no fate is written and *miss = 1 (the caller's
 // all-reduce carries it: every rank returns SKY_E_RETRY and this rank re-runs on the sized route).
-__global__ __launch_bounds__(kThreads) void k_dist_union_fate(const int64_t *__restrict__ blocks, int world, int rank,
-                                                              uint32_t cap, int K, uint8_t *__restrict__ flags,
-                                                              unsigned long long *__restrict__ lsz,
-                                                              unsigned long long *__restrict__ surv,
-                                                              const unsigned long long *__restrict__ sum,
-                                                              unsigned long long limit,
-                                                              unsigned long long *__restrict__ miss) {
+constexpr int kUnionY = 64;
+constexpr int kUnionOffLds = 256;       // block offsets staged in LDS up to this world size
+template <int D>
+constexpr int union_rows() { return D <= 8 ? 512 : 256; }
+
+__device__ __forceinline__ uint32_t union_block_of(uint32_t u, int world, const uint32_t *s_off,
+                                                   const unsigned long long *sum) {
+    // the last block whose compacted start is <= u (empty blocks share their successor's start)
+    int lo = 0, hi = world - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const uint32_t o = world <= kUnionOffLds ? s_off[mid] : (uint32_t)sum[16 + mid];
+        if (o <= u) lo = mid;
+        else hi = mid - 1;
+    }
+    return (uint32_t)lo;
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_dist_union_pairs(const int64_t *__restrict__ blocks, int world, int rank,
+                                                               uint32_t cap, const unsigned long long *__restrict__ sum,
+                                                               unsigned long long limit,
+                                                               unsigned long long *__restrict__ miss,
+                                                               uint32_t *__restrict__ dom) {
     constexpr int RW = D + 2;
-    if (sum[4] * sum[3] > limit) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) *miss = 1ull;
+    constexpr int CH = union_rows<D>();
+    const unsigned long long n_own = sum[4], n_union = sum[3];
+    if (n_own * n_union > limit) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && miss) *miss = 1ull;
         return;
     }
-    __shared__ double s_x[kDistTile * D];
-    __shared__ double s_s[kDistTile];
-    __shared__ int32_t s_k[kDistTile];
+    if (!n_own || !n_union) return;
+    __shared__ double s_x[CH * D];
+    __shared__ int32_t s_k[CH];
+    __shared__ uint32_t s_off[kUnionOffLds];
+    __shared__ uint32_t s_bits[kUnionY];
+    __shared__ uint32_t s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int b = tid; b < world && b < kUnionOffLds; b += kThreads) s_off[b] = (uint32_t)sum[16 + b];
     const size_t bstride = (size_t)(cap + 1) * RW;
     const int64_t *own = blocks + (size_t)rank * bstride;
-    const uint32_t n_own = (uint32_t)min((unsigned long long)max(own[0], (int64_t)0), (unsigned long long)cap);
-    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    const bool valid = j < n_own;
-    double y[D];
-#pragma unroll
-    for (int d = 0; d < D; d++) y[d] = valid ? __longlong_as_double(own[(size_t)(j + 1) * RW + d]) : 0.0;
-    const int32_t ky = valid ? (int32_t)own[(size_t)(j + 1) * RW + D] : -1;
+    const uint32_t ytiles = (uint32_t)((n_own + kUnionY - 1) / kUnionY);
+    // union rows per item: enough items to spread over the grid (>= 2 per workgroup), at least
+    // 16 rows per wave, at most what LDS holds
+    const unsigned long long want = (n_union * ytiles + 2ull * gridDim.x - 1) / (2ull * gridDim.x);
+    const uint32_t per = (uint32_t)min((unsigned long long)CH, max(64ull, (want + 63) & ~63ull));
+    const uint32_t xch = (uint32_t)((n_union + per - 1) / per);
+    const uint64_t items = (uint64_t)ytiles * xch;
     auto score = [](const double *v) {
         double s = 0.0;
 #pragma unroll
         for (int d = 0; d < D; d++) s += v[d] > 1e300 ? 1e300 : (v[d] < -1e300 ? -1e300 : v[d]);
         return s;
     };
-    const double sy = score(y);
-    bool dom_l = false, dom_g = false;
-    if (!__syncthreads_or(valid)) return;
-    for (int b = 0; b < world; b++) {
-        const int64_t *blk = blocks + (size_t)b * bstride;
-        const uint32_t nb = (uint32_t)min((unsigned long long)max(blk[0], (int64_t)0), (unsigned long long)cap);
-        bool go = true;
-        for (uint32_t t0 = 0; t0 < nb && go; t0 += kDistTile) {
-            const uint32_t cn = nb - t0 < (uint32_t)kDistTile ? nb - t0 : (uint32_t)kDistTile;
-            __syncthreads();
-            for (uint32_t q = threadIdx.x; q < cn * D; q += kThreads) {
-                const uint32_t row = q / D, d = q - row * D;
-                s_x[q] = __longlong_as_double(blk[(size_t)(t0 + row + 1) * RW + d]);
+    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t yt = (uint32_t)(it % ytiles), xc = (uint32_t)(it / ytiles);
+        // this lane's own vector (the four waves hold the same 64)
+        const uint32_t j = yt * kUnionY + lane;
+        const bool valid = j < n_own;
+        double y[D];
+#pragma unroll
+        for (int d = 0; d < D; d++) y[d] = valid ? __longlong_as_double(own[(size_t)(j + 1) * RW + d]) : 0.0;
+        const int32_t ky = valid ? (int32_t)own[(size_t)(j + 1) * RW + D] : -1;
+        double smax = valid ? score(y) : -INFINITY;
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) smax = fmax(smax, __shfl_xor(smax, s, 64));
+        // stage the item's union rows that can dominate one of the 64 (sum <= their largest)
+        __syncthreads();                                  // the previous item's readers are done
+        if (tid == 0) s_cnt = 0;
+        if (tid < kUnionY) s_bits[tid] = 0;
+        __syncthreads();
+        const uint32_t u0 = xc * per;
+        const uint32_t cn = (uint32_t)min((unsigned long long)per, n_union - u0);
+        for (uint32_t r0 = 0; r0 < cn; r0 += kThreads) {
+            const uint32_t r = r0 + tid;
+            double v[D];
+            int32_t kx = 0;
+            bool take = false;
+            if (r < cn) {
+                const uint32_t u = u0 + r;
+                const uint32_t b = union_block_of(u, world, s_off, sum);
+                const uint32_t ob = world <= kUnionOffLds ? s_off[b] : (uint32_t)sum[16 + b];
+                const int64_t *row = blocks + (size_t)b * bstride + (size_t)(u - ob + 1) * RW;
+#pragma unroll
+                for (int d = 0; d < D; d++) v[d] = __longlong_as_double(row[d]);
+                kx = (int32_t)row[D];
+                take = score(v) <= smax;
             }
-            for (uint32_t q = threadIdx.x; q < cn; q += kThreads) s_k[q] = (int32_t)blk[(size_t)(t0 + q + 1) * RW + D];
-            __syncthreads();
-            for (uint32_t q = threadIdx.x; q < cn; q += kThreads) s_s[q] = score(s_x + (size_t)q * D);
-            __syncthreads();
-            if (valid && !dom_l) {
-                for (uint32_t i = 0; i < cn; i++) {
-                    if (s_s[i] <= sy && dominates_full<D, double>(s_x + (size_t)i * D, y)) {
-                        dom_g = true;
-                        if (s_k[i] == ky) {
-                            dom_l = true;
-                            break;
-                        }
-                    }
-                }
+            const unsigned long long m = __ballot(take);
+            uint32_t base = 0;
+            if (lane == 0 && m) base = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+            base = __shfl(base, 0, 64);
+            if (take) {
+                const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+#pragma unroll
+                for (int d = 0; d < D; d++) s_x[q * D + d] = v[d];
+                s_k[q] = kx;
             }
-            go = __syncthreads_or(valid && !dom_l) != 0;
         }
-        if (!go) break;
+        __syncthreads();
+        // rows wave, wave + 4, ... against the 64 own vectors (broadcast LDS reads)
+        const uint32_t nr = s_cnt;
+        bool dl = false, dg = false;
+        for (uint32_t i0 = wave; i0 < nr; i0 += 4 * 16) {
+            if (__ballot(valid && !dl) == 0ull) break;      // every own vector settled
+            const uint32_t ie = min(nr, i0 + 4 * 16);
+#pragma unroll 2
+            for (uint32_t i = i0; i < ie; i += 4) {
+                const double *x = s_x + i * D;
+                bool gt = false, lt = false;
+#pragma unroll
+                for (int d = 0; d < D; d++) {
+                    gt |= x[d] > y[d];
+                    lt |= x[d] < y[d];
+                }
+                const bool dm = !gt & lt;
+                dg |= dm;
+                dl |= dm & (s_k[i] == ky);
+            }
+        }
+        const uint32_t bits = (dl ? 1u : 0u) | (dg ? 2u : 0u);
+        if (valid && bits) atomicOr(&s_bits[lane], bits);
+        __syncthreads();
+        if (tid < kUnionY) {
+            const uint32_t w = s_bits[tid], jj = yt * kUnionY + tid;
+            if (w && jj < n_own) atomicOr(&dom[jj], w);
+        }
     }
-    if (!valid) return;
-    flags[j] = (uint8_t)((dom_l ? 0u : 1u) | (dom_g ? 0u : 2u));
-    if (ky >= 0 && ky < K) {
-        const unsigned long long m = (unsigned long long)own[(size_t)(j + 1) * RW + D + 1];
-        if (!dom_l) atomicAdd(&lsz[ky], m);
-        if (!dom_g) atomicAdd(&surv[ky], m);
+}
+
+// the own vectors' fates from the pair bits (bit 0: a union row of its key dominates it, bit
+// 1: some union row does) -> flags (bit 0: in L_k, bit 1: in G) and this rank's stat shares;
+// the bits are cleared for the next step
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_dist_union_finish(const int64_t *__restrict__ blocks, int rank, uint32_t cap,
+                                                                int K, const unsigned long long *__restrict__ sum,
+                                                                unsigned long long limit, uint32_t *__restrict__ dom,
+                                                                uint8_t *__restrict__ flags,
+                                                                unsigned long long *__restrict__ lsz,
+                                                                unsigned long long *__restrict__ surv) {
+    constexpr int RW = D + 2;
+    const unsigned long long n_own = sum[4];
+    if (n_own * sum[3] > limit) return;
+    __shared__ unsigned long long s_l[kMaxK], s_g[kMaxK];
+    const bool lds = K <= kMaxK;
+    for (int k = threadIdx.x; lds && k < K; k += kThreads) { s_l[k] = 0; s_g[k] = 0; }
+    __syncthreads();
+    const int64_t *own = blocks + (size_t)rank * (size_t)(cap + 1) * RW;
+    for (uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x; j < n_own; j += (uint64_t)gridDim.x * kThreads) {
+        const uint32_t w = dom[j];
+        if (w) dom[j] = 0;
+        const bool dl = w & 1u, dg = (w & 2u) != 0;
+        flags[j] = (uint8_t)((dl ? 0u : 1u) | (dg ? 0u : 2u));
+        const int32_t ky = (int32_t)own[(j + 1) * RW + D];
+        if (ky >= 0 && ky < K && !dl) {
+            const unsigned long long m = (unsigned long long)own[(j + 1) * RW + D + 1];
+            if (lds) {
+                atomicAdd(&s_l[ky], m);
+                if (!dg) atomicAdd(&s_g[ky], m);
+            } else {
+                atomicAdd(&lsz[ky], m);
+                if (!dg) atomicAdd(&surv[ky], m);
+            }
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; lds && k < K; k += kThreads) {
+        if (s_l[k]) atomicAdd(&lsz[k], s_l[k]);
+        if (s_g[k]) atomicAdd(&surv[k], s_g[k]);
     }
 }
 
@@ -359,18 +466,25 @@ void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *
 }
 
 void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
-                            unsigned long long *lsz, unsigned long long *surv, const unsigned long long *sum,
-                            unsigned long long limit, unsigned long long *miss, hipStream_t st) {
+                            uint32_t *dom, unsigned long long *lsz, unsigned long long *surv,
+                            const unsigned long long *sum, unsigned long long limit, unsigned long long *miss,
+                            hipStream_t st) {
     if (!cap) return;
-    SKY_DISPATCH_D(D, (k_dist_union_fate<DD><<<nblk_d(cap, kThreads), kThreads, 0, st>>>(
-                          blocks, world, rank, cap, K, flags, lsz, surv, sum, limit, miss)));
+    // the grid walks the (own tile, union rows) items; its size bounds them from the capacity
+    const uint64_t ytiles = (cap + kUnionY - 1) / kUnionY;
+    const uint64_t items = ytiles * (((uint64_t)world * cap + 63) / 64);
+    const unsigned g = (unsigned)std::min<uint64_t>(items, 1024);
+    const unsigned gf = (unsigned)std::min<uint64_t>(((uint64_t)cap + kThreads - 1) / kThreads, 256);
+    SKY_DISPATCH_D(D, (k_dist_union_pairs<DD><<<g, kThreads, 0, st>>>(blocks, world, rank, cap, sum, limit, miss, dom)));
+    SKY_DISPATCH_D(D, (k_dist_union_finish<DD><<<gf, kThreads, 0, st>>>(blocks, rank, cap, K, sum, limit, dom, flags,
+                                                                         lsz, surv)));
 }
 
 // merge-time errors into the all-reduced stat words: a look-back that exceeded its spin bound in
 // the union pass (flags, kFlagRadixSpin), or its work queue's overflow (kFlagMbrQueue) -> err = 1
 // (every rank then returns SKY_E_HIP)
 __global__ void k_dist_merge_err(const uint32_t *__restrict__ flags, unsigned long long *__restrict__ err) {
-    if (threadIdx.x == 0) *err = (flags[0] & (kFlagRadixSpin | kFlagMbrQueue)) ? 1ull : 0ull;
+    if (threadIdx.x == 0) *err = (flags[0] & (kFlagRadixSpin | kFlagMbrQueue | kFlagTinyOob)) ? 1ull : 0ull;
 }
 void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st) {
     k_dist_merge_err<<<1, 64, 0, st>>>(flags, err);

@@ -992,7 +992,12 @@ static uint32_t mbr_qcap(uint32_t ytiles) {
 // y tiles per work item of the pair pass (k_mbr_pairs: the x-side work of Hilbert neighbours is
 // shared).  Two pay once the y tiles are many: std-anti 8D 10M (156k tiles) 18.8 vs 19.9 ms; at
 // 2M (31k tiles, 2.5 units per wave) one is faster (3.49 vs 3.61 ms)
-static int mbr_yt(uint32_t ytiles) { return ytiles >= 65536 ? 2 : 1; }
+// SKY_MBR_YT=1|2 (measurement builds): the item size forced at any size (the two-tile items' test)
+static int mbr_yt(uint32_t ytiles) {
+    const char *e = SKY_MEASURE_ENV("SKY_MBR_YT");
+    if (e) return atoi(e) == 2 ? 2 : 1;
+    return ytiles >= 65536 ? 2 : 1;
+}
 
 template <class R, int YT>
 static void mbr_order(const uint32_t *gmin, uint32_t ngroups, const MbrYSet &ys, uint32_t *lpt, uint32_t *err,
@@ -1044,16 +1049,28 @@ __global__ __launch_bounds__(kThreads) void k_mbr_union_finish(const uint32_t *_
                                                                uint8_t *__restrict__ flags,
                                                                unsigned long long *__restrict__ lsz,
                                                                unsigned long long *__restrict__ surv) {
+    // the stat shares summed per workgroup in LDS first: one global atomic per (workgroup, key)
+    // (a global atomic per own row onto K words serialised: 11.8 ms for 1.2M rows, 16 keys)
+    __shared__ unsigned long long s_l[kMaxK], s_g[kMaxK];
+    const int Ke = K < kMaxK ? K : kMaxK;          // keys are the sort key's top byte
+    for (int q = threadIdx.x; q < Ke; q += kThreads) { s_l[q] = 0; s_g[q] = 0; }
+    __syncthreads();
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
-    if (j >= mr) return;
-    const uint32_t f = domf[j], r = perm[j];
-    const bool in_l = !(f & 1u), in_g = !(f & 2u);
-    flags[r] = (uint8_t)((in_l ? 1u : 0u) | (in_g ? 2u : 0u));
-    const int k = (int)(ykey[r] >> 56);
-    if (k < K) {
-        const unsigned long long m = (unsigned long long)ymult[r];
-        if (in_l) atomicAdd(&lsz[k], m);
-        if (in_g) atomicAdd(&surv[k], m);
+    if (j < mr) {
+        const uint32_t f = domf[j], r = perm[j];
+        const bool in_l = !(f & 1u), in_g = !(f & 2u);
+        flags[r] = (uint8_t)((in_l ? 1u : 0u) | (in_g ? 2u : 0u));
+        const int k = (int)(ykey[r] >> 56);
+        if (k < Ke) {
+            const unsigned long long m = (unsigned long long)ymult[r];
+            if (in_l) atomicAdd(&s_l[k], m);
+            if (in_g) atomicAdd(&s_g[k], m);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < Ke; q += kThreads) {
+        if (s_l[q]) atomicAdd(&lsz[q], s_l[q]);
+        if (s_g[q]) atomicAdd(&surv[q], s_g[q]);
     }
 }
 

@@ -1053,6 +1053,14 @@ __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
     }
     __syncthreads();
     const uint32_t tile = s_tile;
+    // the invariant k_cand_compact keeps: a pruner slot at or past mt (slots truncated) is no slot
+    // of this round's index space.  Race-free: no tile rewrites an entry whose slot is >= mt, and
+    // an entry below mt stays below it when remapped
+    if (tile == 0)
+        for (int q = threadIdx.x; q < a.KM; q += kThreads) {
+            const int32_t ps = a.pruner_slot[q];
+            if (ps >= 0 && (uint32_t)ps >= mt) a.pruner_slot[q] = -1;
+        }
     // kCandFI consecutive slots per thread (the tile's order = slot order): the pick above is
     // paid once per kCandFI * kThreads slots
     const uint32_t j0 = (tile * kThreads + threadIdx.x) * kCandFI;
@@ -1515,6 +1523,9 @@ __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
 // is (k, wave, lane): a selected tuple's output position is the count of the (k, wave)
 // groups before it (32 per tile, scanned in LDS) plus its rank in its wave's ballot.
 __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
+    // after a one-workgroup tail that missed (or tripped its guard) no fate / offset is valid:
+    // the caller's buffers are left untouched (the host re-runs the query or returns the error)
+    if (a.skip_flags && (*a.skip_flags & (kFlagTinyMiss | kFlagTinyOob))) return;
     __shared__ uint8_t s_pf[2048];
     __shared__ uint32_t s_cnt[kItems * (kThreads / 64)];
     __shared__ uint32_t s_tot;
@@ -1793,12 +1804,15 @@ __device__ __forceinline__ uint32_t tiny_scan_excl(uint32_t v, uint32_t *s_w, ui
 
 
 #ifdef SKY_MEASURE
-#define TINY_OK(i, c, bit) \
-    ((uint64_t)(i) < (uint64_t)(c) ? true : (a.chk ? (atomicOr(a.chk, 1u << (bit)), false) : true))
+#define TINY_OK(i, c, bit)                                                                          \
+    ((uint64_t)(i) < (uint64_t)(c) ? true                                                         \
+                                   : ((lflags |= kFlagTinyOob), (a.chk ? (atomicOr(a.chk, 1u << (bit)), false) : false)))
 #define TINY_CLK(i) \
     if (a.clk && threadIdx.x == 0) a.clk[i] = __builtin_amdgcn_s_memrealtime()
 #else
-#define TINY_OK(i, c, bit) true
+// product build: the same capacity check on every global index the tail computes; an index out
+// of range skips its access and raises kFlagTinyOob (the run fails with SKY_E_HIP, no fault)
+#define TINY_OK(i, c, bit) ((uint64_t)(i) < (uint64_t)(c) ? true : ((lflags |= kFlagTinyOob), false))
 #define TINY_CLK(i)
 #endif
 
@@ -2416,4 +2430,37 @@ void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, cons
 void launch_out_write(const OutArgs &a, hipStream_t st) {
     if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
 }
+// sky_profile_pairs_dev: caller rows -> the slot format of the brute pass (f64 rows padded to
+// 16 B, sort key = partition | f32 score | hash, as k_filter appends candidates)
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_prof_slots(const double *__restrict__ vals,
+                                                        const int32_t *__restrict__ keys, uint32_t n,
+                                                        double *__restrict__ rows, uint64_t *__restrict__ key,
+                                                        uint32_t *__restrict__ flags) {
+    constexpr int DP = padded_dims<double>(D);
+    const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
+    uint32_t lf = 0;
+    if (j < n) {
+        double v[D];
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            v[d] = vals[(size_t)j * D + d];
+            if ((double)(float)v[d] != v[d]) lf |= kFlagNotF32;
+        }
+#pragma unroll
+        for (int d = 0; d < DP; d++) rows[(size_t)j * DP + d] = d < D ? v[d] : 0.0;
+        key[j] = make_sortkey<double, D>(v, (uint32_t)keys[j], lf);
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) lf |= (uint32_t)__shfl_xor((int)lf, s, 64);
+    if ((threadIdx.x & 63) == 0 && lf) atomicOr(flags, lf);
+}
+
+void launch_prof_slots(int D, const double *vals, const int32_t *keys, uint32_t n, double *rows, uint64_t *key,
+                       uint32_t *flags, hipStream_t st) {
+    if (!n) return;
+    SKY_DISPATCH_D(D, (k_prof_slots<DD><<<(n + kThreads - 1) / kThreads, kThreads, 0, st>>>(vals, keys, n, rows, key,
+                                                                                           flags)));
+}
+
 }  // namespace sky

@@ -440,7 +440,6 @@ __global__ __launch_bounds__(kThreads) void k_scatter_alive(const uint32_t *__re
     if (j < mg) alive_g[gval[j]] = galive[j];
 }
 
-// sum the [shard][K] stat accumulators into [K] (one workgroup per key)
 // The brute route's per-tile output counts (k_out_hist_count: the duplicate groups whose pruner is
 // in G, listed first, plus the tile's candidates in G), their exclusive scan, the stats reduce
 // (k_stat_reduce) and the final read's words into host-mapped memory (k_gather_words), in ONE
@@ -550,6 +549,7 @@ void launch_tail_counts(const TailArgs &a, hipStream_t st) {
     k_tail_counts<<<1, kTailThreads, 0, st>>>(a);
 }
 
+// sum the [shard][K] stat accumulators into [K] (one workgroup per key)
 __global__ __launch_bounds__(kThreads) void k_stat_reduce(const unsigned long long *__restrict__ lsz,
                                                           const unsigned long long *__restrict__ surv, int K,
                                                           unsigned long long *__restrict__ out) {
@@ -676,10 +676,13 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restric
 //     x dominates y  <=>  x <= y everywhere and sum(x) < sum(y)
 // (x <= y with x != y makes the sum strictly smaller; equal vectors have equal sums), i.e.
 //     OR_w sat_u16(x_w - y_w)  |  sat_u32(sum(x) + 1 - sum(y))  == 0.
-// Each lane keeps the minimum of that word over the x chunk (any partition) and of it OR
-// (px ^ py) (same partition): 10 + 3 VALU ops per pair and no per-pair VALU -> SGPR mask
-// traffic.  A workgroup: 256 y (one per lane) against kB16X x rows packed into LDS once.
-constexpr int kB16Y = 256, kB16X = 128;
+// A dense all-pairs tile: a workgroup holds 256 y (one per lane) and stages kB16X x rows in LDS
+// once, ordered by partition (a counting sort of the chunk), so that every x row costs the
+// compare words and ONE running minimum: per partition run the lane keeps min_x(word); at the
+// run's end the any-partition minimum takes it, and the same-partition minimum too where the
+// run's partition is the lane's.  8D: 4 v_pk_sub_u16 (clamp) + 1 saturating u32 subtract + 2
+// v_or3 + 1 v_min per pair test (8 compares), no per-pair VALU -> SGPR mask traffic.
+constexpr int kB16Y = 256, kB16X = 512;
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t sat_sub_u16x2(uint32_t x, uint32_t y) {
@@ -700,36 +703,39 @@ __device__ __forceinline__ uint32_t pack_row16(const double *r, uint32_t (&w)[W]
     return s;
 }
 
+template <int W>
+__device__ __forceinline__ uint32_t dom16_word(const uint4 (&xw)[W / 4], uint32_t xs, const uint32_t (&y)[W],
+                                               uint32_t sy) {
+    uint32_t r = __builtin_elementwise_sub_sat(xs, sy);
+#pragma unroll
+    for (int q = 0; q < W / 4; q++)
+        r |= sat_sub_u16x2(xw[q].x, y[4 * q]) | sat_sub_u16x2(xw[q].y, y[4 * q + 1]) |
+             sat_sub_u16x2(xw[q].z, y[4 * q + 2]) | sat_sub_u16x2(xw[q].w, y[4 * q + 3]);
+    return r;
+}
+
 template <int D, int W>
 __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
                                                          const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
+    constexpr int RPT = kB16X / kB16Y;                          // x rows staged per thread
     if (d_mr) mr = min(mr, *d_mr);
     if (blockIdx.x * kB16Y >= mr || blockIdx.y * kB16X >= mr) return;
     __shared__ uint4 s_x[kB16X][W / 4];
-    __shared__ uint2 s_sp[kB16X];                              // (sum + 1, partition)
+    __shared__ uint32_t s_s[kB16X];                             // sum + 1 of each staged row
+    __shared__ uint32_t s_h[kMaxK];                             // rows per partition -> run start
+    __shared__ uint32_t s_rb[kMaxK + 1], s_rp[kMaxK];            // runs: start, partition
+    __shared__ uint32_t s_w[kB16Y / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t y0 = blockIdx.x * kB16Y, x0 = blockIdx.y * kB16X;
     const uint32_t cn = mr - x0 < (uint32_t)kB16X ? mr - x0 : (uint32_t)kB16X;
-    if (threadIdx.x < kB16X) {
-        uint32_t w[W];
-        uint2 sp;
-        if (threadIdx.x < cn) {
-            sp.x = pack_row16<D, W>(rows + (size_t)(x0 + threadIdx.x) * DP, w) + 1u;
-            sp.y = (uint32_t)(key[x0 + threadIdx.x] >> 56);
-        } else {                                               // padding: dominates nothing
-#pragma unroll
-            for (int q = 0; q < W; q++) w[q] = 0xffffffffu;
-            sp = make_uint2(0xffffffffu, 0u);
-        }
-#pragma unroll
-        for (int q = 0; q < W / 4; q++) s_x[threadIdx.x][q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-        s_sp[threadIdx.x] = sp;
-    }
-    const uint32_t j = y0 + threadIdx.x;
+    for (int q = tid; q < kMaxK; q += kB16Y) s_h[q] = 0;
+    // this lane's y
+    const uint32_t j = y0 + tid;
     const bool valid = j < mr;
-    uint32_t y[W], sy = 0, py = 0;
+    uint32_t y[W], sy = 0, py = 0xffffffffu;
     if (valid) {
         sy = pack_row16<D, W>(rows + (size_t)j * DP, y);
         py = (uint32_t)(key[j] >> 56);
@@ -737,20 +743,94 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
 #pragma unroll
         for (int q = 0; q < W; q++) y[q] = 0u;
     }
-    __syncthreads();
-    const uint32_t cn4 = (cn + 3u) & ~3u;                      // rows cn..cn4-1 are padding
-    uint32_t acc_a = 0xffffffffu, acc_s = 0xffffffffu;
-#pragma unroll 4
-    for (uint32_t i = 0; i < cn4; i++) {
-        uint32_t r = __builtin_elementwise_sub_sat(s_sp[i].x, sy);
+    // the chunk's rows, ranked within their partition
+    uint32_t xw[RPT][W], xs[RPT], xp[RPT], xr[RPT];
 #pragma unroll
-        for (int q = 0; q < W / 4; q++) {
-            const uint4 xw = s_x[i][q];
-            r |= sat_sub_u16x2(xw.x, y[4 * q]) | sat_sub_u16x2(xw.y, y[4 * q + 1]) |
-                 sat_sub_u16x2(xw.z, y[4 * q + 2]) | sat_sub_u16x2(xw.w, y[4 * q + 3]);
+    for (int u = 0; u < RPT; u++) {
+        const uint32_t r = u * kB16Y + tid;
+        xp[u] = 0xffffffffu;
+        if (r < cn) {
+            xs[u] = pack_row16<D, W>(rows + (size_t)(x0 + r) * DP, xw[u]) + 1u;
+            xp[u] = (uint32_t)(key[x0 + r] >> 56);
         }
-        acc_a = min(acc_a, r);
-        acc_s = min(acc_s, r | (s_sp[i].y ^ py));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < RPT; u++)
+        if (xp[u] != 0xffffffffu) xr[u] = atomicAdd(&s_h[xp[u]], 1u);
+    __syncthreads();
+    // exclusive scan of the partition counts (kMaxK = 256 = one per thread) and the run list
+    {
+        const uint32_t c = tid < kMaxK ? s_h[tid] : 0u;
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        const uint64_t nz = __ballot(c != 0u);
+        if (lane == 63) s_w[wave] = inc | ((uint32_t)__popcll(nz) << 16);
+        __syncthreads();
+        uint32_t base = 0, rbase = 0, tot_r = 0;
+#pragma unroll
+        for (int w = 0; w < kB16Y / 64; w++) {
+            const uint32_t v = s_w[w];
+            if (w < wave) { base += v & 0xffffu; rbase += v >> 16; }
+            tot_r += v >> 16;
+        }
+        const uint32_t start = base + inc - c;
+        __syncthreads();
+        if (tid < kMaxK) s_h[tid] = start;
+        if (c) {
+            const uint32_t ri = rbase + (uint32_t)__popcll(nz & ((1ull << lane) - 1ull));
+            s_rb[ri] = start;
+            s_rp[ri] = (uint32_t)tid;
+        }
+        if (tid == 0) s_rb[tot_r] = cn;                         // the end of the last run
+        if (tid == 0) s_w[0] = tot_r;
+    }
+    __syncthreads();
+    const uint32_t nruns = __builtin_amdgcn_readfirstlane((int)s_w[0]);
+#pragma unroll
+    for (int u = 0; u < RPT; u++) {
+        if (xp[u] == 0xffffffffu) continue;
+        const uint32_t pos = s_h[xp[u]] + xr[u];
+#pragma unroll
+        for (int q = 0; q < W / 4; q++) s_x[pos][q] = make_uint4(xw[u][4 * q], xw[u][4 * q + 1], xw[u][4 * q + 2], xw[u][4 * q + 3]);
+        s_s[pos] = xs[u];
+    }
+    __syncthreads();
+    uint32_t acc_a = 0xffffffffu, acc_s = 0xffffffffu;
+    for (uint32_t rr = 0; rr < nruns; rr++) {
+        const uint32_t b = __builtin_amdgcn_readfirstlane((int)s_rb[rr]);
+        const uint32_t e = __builtin_amdgcn_readfirstlane((int)s_rb[rr + 1]);
+        const uint32_t px = __builtin_amdgcn_readfirstlane((int)s_rp[rr]);
+        constexpr int U = 4;                                    // rows in flight
+        uint32_t acc_u[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) acc_u[u] = 0xffffffffu;
+        uint32_t i = b;
+        for (; i + U <= e; i += U) {
+            uint4 xa[U][W / 4];
+            uint32_t sa[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+#pragma unroll
+                for (int q = 0; q < W / 4; q++) xa[u][q] = s_x[i + u][q];
+                sa[u] = s_s[i + u];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) acc_u[u] = min(acc_u[u], dom16_word<W>(xa[u], sa[u], y, sy));
+        }
+        for (; i < e; i++) {
+            uint4 xa[W / 4];
+#pragma unroll
+            for (int q = 0; q < W / 4; q++) xa[q] = s_x[i][q];
+            acc_u[0] = min(acc_u[0], dom16_word<W>(xa, s_s[i], y, sy));
+        }
+        const uint32_t acc = min(min(acc_u[0], acc_u[1]), min(acc_u[2], acc_u[3]));
+        acc_a = min(acc_a, acc);
+        if (px == py) acc_s = min(acc_s, acc);
     }
     const uint32_t f = (acc_s == 0u ? 3u : 0u) | (acc_a == 0u ? 2u : 0u);
     if (valid && f) atomicOr(&domf[j], f);
@@ -784,9 +864,8 @@ __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__res
     }
 }
 
-void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
-                        uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
-                        uint32_t *slot_rep, hipStream_t st, const uint32_t *d_mr) {
+void launch_brute_pairs(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, uint32_t *domf,
+                        hipStream_t st, const uint32_t *d_mr) {
     if (!mr) return;
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
     if (u16) {
@@ -798,6 +877,13 @@ void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint6
     } else {
         SKY_DISPATCH_D(D, (k_brute_pairs<double, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, d_mr, domf)));
     }
+}
+
+void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
+                        uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
+                        uint32_t *slot_rep, hipStream_t st, const uint32_t *d_mr) {
+    if (!mr) return;
+    launch_brute_pairs(D, f32, u16, rows, key, mr, domf, st, d_mr);
     k_brute_finish<<<(mr + kThreads - 1) / kThreads, kThreads, 0, st>>>(key, mr, d_mr, gmerge ? 1 : 0, domf, alive_l,
                                                                          alive_g, segalive, segn, slot_rep);
 }

@@ -150,6 +150,7 @@ struct CandArgs {
     uint32_t *d_live = nullptr;           // out: surviving slots
     int32_t *pruner_slot = nullptr;       // remapped in place (appended pruner slots)
     const int32_t *entries = nullptr;     // pruner slot entry -> k * M + j
+    int KM = 0;                           // pruner_slot entries (k * M + j)
     unsigned long long *lb = nullptr;     // [cand_fused_tiles(mt)] look-back words, zeroed
     uint32_t *ticket = nullptr;           // zeroed
     uint32_t *err = nullptr;              // kFlagRadixSpin if a look-back ran out of spins
@@ -209,6 +210,7 @@ struct OutArgs {
     int select_local;             // output tuples in L instead of G
     const uint64_t *planes = nullptr;   // the filter's status planes (k_out_write only)
     int32_t dom_kj = -1;
+    const uint32_t *skip_flags = nullptr;   // write pass: nothing is written if this word has a tail miss / guard bit
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);
 // per-tile counts of the global level from the filter's duplicate histograms + k_fate_tables'
@@ -274,6 +276,13 @@ uint32_t brute_max();
 // f32: compare in f32 (every candidate value exactly an f32), else f64; u16: every candidate
 // value an integer in [0, 65535]: packed u16 compares (k_brute16_pairs)
 // d_mr (optional): the slot count on the device, mr its bound
+// the pair kernel of launch_brute_fates alone (domf zeroed by the caller)
+void launch_brute_pairs(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, uint32_t *domf,
+                        hipStream_t st, const uint32_t *d_mr = nullptr);
+// rows n x D (f64, row-major) + partition keys -> slot rows (f64, padded) + sort keys as the
+// filter writes them; *flags |= kFlagNotF32 / kFlagNotU16 / kFlagScoreTies
+void launch_prof_slots(int D, const double *vals, const int32_t *keys, uint32_t n, double *rows, uint64_t *key,
+                       uint32_t *flags, hipStream_t st);
 void launch_brute_fates(int D, bool f32, bool u16, const void *rows, const uint64_t *key, uint32_t mr, bool gmerge,
                         uint32_t *domf, uint8_t *alive_l, uint8_t *alive_g, uint32_t *segalive, uint32_t *segn,
                         uint32_t *slot_rep, hipStream_t st, const uint32_t *d_mr = nullptr);
@@ -438,7 +447,7 @@ void launch_dist_compact(int D, const int64_t *blocks, int world, uint32_t cap, 
                          uint64_t *ukey, int64_t *umult, hipStream_t st);
 void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *out, hipStream_t st);
 void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
-                            unsigned long long *lsz, unsigned long long *surv, const unsigned long long *sum,
+                            uint32_t *dom, unsigned long long *lsz, unsigned long long *surv, const unsigned long long *sum,
                             unsigned long long limit, unsigned long long *miss, hipStream_t st);
 void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st);
 void launch_dist_alive_g(const uint32_t *flag, const uint32_t *pos, uint32_t n, const uint8_t *own_flags, uint32_t cap,
@@ -501,6 +510,9 @@ constexpr int kTinyThreads = 1024;
 constexpr int kTinyM2 = 16;             // second-level pruners per partition in the tail (compile-time)
 constexpr uint32_t kTinyForce = 192;      // a plan without rounds: the tail runs one above this many slots
 constexpr uint32_t kFlagTinyMiss = 64u;
+// an index of the one-workgroup tail fell outside the capacity the host passed for its array: the
+// access was skipped and the run is invalid (SKY_E_HIP; the product build's device guard)
+constexpr uint32_t kFlagTinyOob = 128u;
 struct TinyArgs {
     AppendArgs ap;                        // rows / sortkey / slot_src: the filter's slots
     int rounds = 0, M2 = 0;

@@ -109,6 +109,7 @@ SIGNATURES = {
     "sky_profile_dominance": [c_p, P_i64],
     "sky_profile_reset": [c_p],
     "sky_profile_sort_dev": [c_p, c_p, c_p, c_i64, P_i32, P_dbl],
+    "sky_profile_pairs_dev": [c_p, c_p, c_p, c_i64, c_p, P_i32, P_dbl],
     "sky_last_error": [],
     "sky_version": [],
     "sky_device_count": [P_i32],

@@ -261,6 +261,18 @@ class SkylineEngine:
                                              ctypes.byref(ms)))
         return p.value, ms.value
 
+    def profile_pairs_dev(self, d_values, d_keys, d_fates_out):
+        """The small-set route's dense all-pairs kernel alone on device rows with given
+        partition keys (int32): fates (bit0 dominated within its partition, bit1 by any row)
+        into d_fates_out (int32 view of u32); returns (kind 0 u16 / 1 f32 / 2 f64, kernel ms)."""
+        n = d_values.numel() // self.dims
+        kind = ctypes.c_int32(0)
+        ms = ctypes.c_double(0)
+        with _Ordered(self.h, self.device):
+            check(lib().sky_profile_pairs_dev(self.h, _tptr(d_values), _tptr(d_keys), n, _tptr(d_fates_out),
+                                              ctypes.byref(kind), ctypes.byref(ms)))
+        return kind.value, ms.value
+
     def set_stream(self, stream_ptr):
         check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 

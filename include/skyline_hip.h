@@ -333,6 +333,14 @@ int sky_profile_host_syncs(sky_ctx *ctx, int64_t *n_out);
  * roofline at scale; *passes_out = digit passes, *ms_out = HIP-event time of the sort */
 int sky_profile_sort_dev(sky_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, int64_t n, int32_t *passes_out,
                          double *ms_out);
+/* the small-set route's dense all-pairs kernel (k_brute16_pairs for integer rows, k_brute_pairs
+ * f32 / f64 otherwise: every row against every row, ServiceTuple.dominates over the pairs of
+ * FlinkSkyline.java:424-441) run alone on n device rows (n x dims f64) with the given partition
+ * keys, for the dense dominance roofline: d_fates_out[i] bit0 = some row of i's partition
+ * dominates row i, bit1 = some row does; *kind_out = 0 packed u16, 1 f32, 2 f64 compares;
+ * *ms_out = HIP-event time of the pair kernel */
+int sky_profile_pairs_dev(sky_ctx *ctx, const double *d_values, const int32_t *d_keys, int64_t n,
+                          uint32_t *d_fates_out, int32_t *kind_out, double *ms_out);
 
 #ifdef __cplusplus
 }

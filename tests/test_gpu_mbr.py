@@ -147,3 +147,78 @@ def test_mbr_queue_overflow_is_an_error_not_a_fault():
     assert r.returncode == 0, r.stderr[-2000:]
     out = r.stdout.strip().splitlines()[-1]
     assert out.startswith("CODE -2") and "work items outgrew their queue" in out, out
+
+
+_YT_CHILD = r"""
+import os, sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[2])
+import skyline
+from conftest import dist_emulate
+out = {}
+def one(tag, dist, D, n, seed, P):
+    vals, ids = skyline.synth_host(dist, D, n, seed=seed)
+    for yt in ("1", "2"):
+        os.environ["SKY_MBR_YT"] = yt
+        eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, 0)
+        gi, go = eng.query(vals, ids)
+        ls, sv = eng.stats()
+        reps = int(eng.phases()[1][2])
+        eng.close()
+        out[f"{tag}_{yt}_ids"], out[f"{tag}_{yt}_org"] = gi, go
+        out[f"{tag}_{yt}_ls"], out[f"{tag}_{yt}_sv"] = ls, sv
+        out[f"{tag}_{yt}_reps"] = np.array([reps])
+one("small", "std_anti", 8, 60000, 360, 16)
+one("big", "std_anti", 8, 300000, 708, 16)
+one("uni", "uniform", 6, 400000, 706, 16)
+one("odd", "std_anti", 5, 150001, 505, 8)
+# the multi-GPU union route (own tiles vs union tiles, the full test): 2 emulated ranks
+os.environ["SKY_DIST_BRUTE_PAIRS"] = "0"
+D, n = 8, 80000
+vals, ids = skyline.synth_host("std_anti", D, n, seed=77)
+dv, di = torch.from_numpy(vals).cuda(), torch.from_numpy(ids).cuda()
+for yt in ("1", "2"):
+    os.environ["SKY_MBR_YT"] = yt
+    engs = [skyline.SkylineEngine(D, 16, "mr-angle", 1000.0, 0) for _ in range(2)]
+    r = dist_emulate(engs, [di[:n // 2], di[n // 2:]], [dv[:n // 2], dv[n // 2:]], steps=2)[-1]
+    route = int(engs[0].phases()[1][6])
+    for e in engs:
+        e.close()
+    out[f"dist_{yt}_ids"], out[f"dist_{yt}_org"], out[f"dist_{yt}_ls"], out[f"dist_{yt}_sv"] = r["ids"], r["org"], r["ls"], r["sv"]
+    out[f"dist_{yt}_route"] = np.array([route])
+np.savez(sys.argv[3], **out)
+print("DONE", flush=True)
+"""
+
+
+def test_mbr_two_tile_items_equal_one_tile_items(tmp_path, oracle):
+    """The pair pass's two-y-tile work items (YT = 2, the default above 65536 y tiles, i.e. ~4.2M
+    reps) forced at test sizes through the measurement build's SKY_MBR_YT: the ids, origins,
+    |L_k| and survivors_k equal the one-tile items on std-anti 8D 60k / 300k, uniform 6D 400k,
+    a stream with an odd y-tile count (the last unit holds one tile), and the multi-GPU union
+    route (own tiles vs union tiles, the full test, gmerge); the 60k case also equals the oracle."""
+    import os
+    import subprocess
+    import sys
+    from conftest import PKG, REPO
+    if not os.path.exists(MEASURE_LIB):
+        pytest.fail("build_measure/libskyline_hip.so missing: __graft_entry__.build() builds it")
+    npz = str(tmp_path / "yt.npz")
+    env = dict(os.environ, SKYLINE_HIP_LIB=MEASURE_LIB, SKY_MBR="1", SKY_MBR_MIN="1", SKY_BRUTE="0")
+    r = subprocess.run([sys.executable, "-c", _YT_CHILD, PKG, os.path.join(REPO, "tests"), npz], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "DONE" in r.stdout, r.stderr[-3000:]
+    z = np.load(npz)
+    for tag in ("small", "big", "uni", "odd", "dist"):
+        for f in ("ids", "org", "ls", "sv"):
+            np.testing.assert_array_equal(z[f"{tag}_1_{f}"], z[f"{tag}_2_{f}"], err_msg=f"{tag} {f}")
+    tiles = [(int(z[f"{t}_1_reps"][0]) + 63) // 64 for t in ("small", "big", "uni", "odd")]
+    assert any(t % 2 == 1 for t in tiles), tiles              # a unit with one tile in it
+    assert int(z["dist_1_route"][0]) == 1                      # the bounding-box union route ran
+    import skyline
+    vals, _ = skyline.synth_host("std_anti", 8, 60000, seed=360)
+    exp, keys, els, esv = oracle.query_sfs("angle", vals, 16)
+    np.testing.assert_array_equal(z["small_2_ids"], exp)
+    np.testing.assert_array_equal(z["small_2_org"], keys[exp])
+    np.testing.assert_array_equal(z["small_2_ls"], els)
+    np.testing.assert_array_equal(z["small_2_sv"], esv)

@@ -219,3 +219,46 @@ def test_tail_counts_equals_launch_chain(gpu_engine_factory, oracle, algo, dist,
             eng.close()
         finally:
             del os.environ["SKY_TAIL_COUNTS"]
+
+
+MEASURE_LIB = os.path.join(__import__("conftest").PKG, "build_measure", "libskyline_hip.so")
+_TINY_CAP_CHILD = r"""
+import os, sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import skyline
+from skyline._abi import SkylineError
+vals, ids = skyline.synth_host("uniform", 2, 200000, seed=5)
+eng = skyline.SkylineEngine(2, 8, "mr-dim", 1000.0, 0)
+ref = eng.query(vals, ids)[0]                  # synchronised: learns the small-set plan
+os.environ["SKY_TINY_CAP"] = sys.argv[2]       # the replay's tail gets a capacity far too small
+try:
+    eng.query(vals, ids)
+    print("NO-ERROR", flush=True)
+except SkylineError as e:
+    print("CODE", e.code, str(e), flush=True)
+del os.environ["SKY_TINY_CAP"]
+os.environ["SKY_TINY"] = "0"                   # the same context still answers afterwards
+got = eng.query(vals, ids)[0]
+print("AFTER", int(np.array_equal(got, ref)), flush=True)
+"""
+
+
+@pytest.mark.parametrize("capspec", ["0:4", "6:16"])
+def test_tiny_tail_guard_is_an_error_not_a_fault(capspec):
+    """k_tiny_tail checks every global index it computes against the capacity the host passed
+    for that array (the product build too): with the slot capacity (0:4) or the status words'
+    capacity (6:16) forced tiny through the measurement build's SKY_TINY_CAP, the planned query
+    must come back as SKY_E_HIP with a message -- no access past the capacity, no fault, nothing
+    written into the caller's buffers -- and the context answers the next query correctly."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    if not os.path.exists(MEASURE_LIB):
+        pytest.fail("build_measure/libskyline_hip.so missing: __graft_entry__.build() builds it")
+    env = dict(os.environ, SKYLINE_HIP_LIB=MEASURE_LIB)
+    r = subprocess.run([sys.executable, "-c", _TINY_CAP_CHILD, PKG, capspec], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert lines[-2].startswith("CODE -2") and "device guard" in lines[-2], lines
+    assert lines[-1] == "AFTER 1", lines
