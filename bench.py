@@ -205,6 +205,7 @@ def config_line(name, dev, dev_index, steps, warmup, with_cpu):
     D, P, n = cfg["dims"], cfg["partitions"], cfg["tuples"]
     seed = 1234 + D
     eng = skyline.SkylineEngine(D, P, cfg["algo"], 1000.0, dev_index)
+    eng.use_torch_stream()
     vals, ids = make_stream(eng, cfg["dist"], n, seed, 0, dev)
     out_ids = torch.empty(n, dtype=torch.int64, device=dev)
     out_org = torch.empty(n, dtype=torch.int32, device=dev)
@@ -475,6 +476,7 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     vals = torch.from_numpy(vals_np).pin_memory().numpy()
     ids = torch.from_numpy(ids_np).pin_memory().numpy()
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
+    eng.use_torch_stream()
     eng.warmup()                                  # first launches / allocations, before the stream starts
 
     def run_stream(timers):
@@ -815,6 +817,9 @@ def main():
     dev_index = local_rank % n_dev   # > 1 rank per GPU only when rehearsing with gloo
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
+    # one non-default stream for everything this process issues; the engines run ON it
+    # (use_torch_stream: no cross-stream events per call), and the collectives order after it
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -847,6 +852,7 @@ def main():
     n_cfg = args.tuples or cfg["tuples"]
     seed = 1234 + D
     eng = skyline.SkylineEngine(D, P, cfg["algo"], 1000.0, dev_index)
+    eng.use_torch_stream()
 
     def shard(mode):
         """(tuples on this rank, first id, tuples in the whole job) of a scaling mode."""

@@ -56,6 +56,18 @@ int dist_write_block(sky_ctx *c, int64_t *d_block, int64_t cap) {
     SKY_TRY(p.dist_pos.ensure(((size_t)units + 1) * 4));
     SKY_TRY(p.scratch.ensure(scan_scratch_words((size_t)units + 1) * 4 + 64));
     uint32_t *d_count = p.totals.as<uint32_t>() + 4;
+    if (units && p.dist_slots && units <= dist_export_one_max()) {
+        // verdict, flags, scan, rows and header in one workgroup
+        launch_dist_export_one(D, p.totals.as<uint32_t>(), p.flags.as<uint32_t>(), p.dist_pc, p.dverd.as<uint32_t>(),
+                               p.alive_l.as<uint8_t>(), units, p.dist_d_n, p.dist_flag.as<uint32_t>(),
+                               p.dist_pos.as<uint32_t>(), d_count, p.s_rows->as<double>(), p.s_key->as<uint64_t>(),
+                               p.s_src->as<uint32_t>(), p.dup_cnt.as<uint32_t>(), p.pr_entries.as<int32_t>(), d_block,
+                               (uint32_t)cap, p.n, st);
+        HIP_TRY(hipGetLastError());
+        return SKY_OK;
+    }
+    if (p.dist_verdict_pending)
+        launch_plan_verdict(p.totals.as<uint32_t>(), p.flags.as<uint32_t>(), p.dist_pc, p.dverd.as<uint32_t>(), st);
     if (units) {
         launch_dist_flags(p.alive_l.as<uint8_t>(), units, p.dist_d_n, p.dist_flag.as<uint32_t>(), st);
         scan_excl_u32(p.dist_flag.as<uint32_t>(), p.dist_pos.as<uint32_t>(), units, d_count, p.scratch.as<uint32_t>(),
@@ -255,6 +267,7 @@ int sky_dist_export_dev(sky_ctx *c, const int64_t *d_ids, const double *d_values
         p.dist_n = 0;
         p.dist_d_n = nullptr;
         p.dist_slots = false;
+        p.dist_verdict_pending = false;
         HIP_TRY(hipMemsetAsync(p.dverd.p, 0, 4, c->st));
     } else {
         const int r = pipe_run(*c, p, in, c->profile >= 2 ? &c->pt : nullptr);
@@ -377,13 +390,16 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
         oa.K = p.K;
         oa.out_cnt = p.out_cnt.as<uint32_t>();
         c->ktimer_begin("out", st);
-        if (p.hist_count)
-            launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
-                                  KM, tiles, p.out_cnt.as<uint32_t>(), st);
-        else
+        if (p.hist_count) {                   // counts + scan in one launch
+            SKY_TRY(out_hist_scan_words(p, tiles, st));
+            launch_out_hist_scan(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(), KM,
+                                 tiles, p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), p.totals.as<uint32_t>() + 3,
+                                 p.out_lb.as<unsigned long long>(), ++p.out_epoch, p.flags.as<uint32_t>(), st);
+        } else {
             launch_out_count(oa, st);
-        scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                      p.scratch.as<uint32_t>(), st);
+            scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                          p.scratch.as<uint32_t>(), st);
+        }
         if (d_ids_out || d_origin_out) {
             OutArgs ow = oa;
             ow.out_off = p.out_off.as<uint32_t>();

@@ -131,10 +131,13 @@ struct Pipe {
     DevBuf dverd;                         // u64 words: [0] the run's verdict, [8..15] the merge's summary
     DevBuf dist_flag, dist_pos, dist_own; // per unit: alive (u32), export position; per own row: fates
     DevBuf dist_dom;                      // per own row: dominated bits of the wide pair pass (u32, kept zero)
+    DevBuf out_lb;                        // k_out_hist_scan's look-back words (zeroed when allocated)
+    uint32_t out_epoch = 0;               // ... and the epoch its last launch tagged them with
     bool dist_slots = false;              // units = candidate slots (small-set route) or representatives
     uint32_t dist_n = 0;                  // units (their bound on the planned route)
     const uint32_t *dist_d_n = nullptr;   // the unit count on the device (planned route)
     PlanCheck dist_pc;
+    bool dist_verdict_pending = false;    // the verdict is computed by the one-workgroup export tail
     int64_t host_syncs = 0;               // host synchronisations (read-backs) of this pipeline
     // host-visible pinned staging
     void *pin = nullptr;

@@ -818,7 +818,10 @@ static int dist_finish_run(Ctx &c, Pipe &p, PhaseTimer *tm, bool brute, uint32_t
         pc.k_u16 = pr->k_u16 ? 1 : 0;
         pc.k_f32 = pr->k_f32 ? 1 : 0;
     }
-    launch_plan_verdict(p.totals.as<uint32_t>(), p.flags.as<uint32_t>(), pc, p.dverd.as<uint32_t>(), st);
+    // a slot-mode export of few units computes the verdict in its one-workgroup tail (dist_write_block)
+    p.dist_verdict_pending = brute && mt > 0 && mt <= dist_export_one_max();
+    if (!p.dist_verdict_pending)
+        launch_plan_verdict(p.totals.as<uint32_t>(), p.flags.as<uint32_t>(), pc, p.dverd.as<uint32_t>(), st);
     p.dist_pc = pc;
     p.dist_slots = brute;
     p.dist_n = brute ? mt : p.mr;
@@ -831,6 +834,20 @@ static int dist_finish_run(Ctx &c, Pipe &p, PhaseTimer *tm, bool brute, uint32_t
         tm->mark(8, st);
     }
     return stage_check(st, "dist export");
+}
+
+// k_out_hist_scan's look-back words: zeroed when (re)allocated; every launch tags them with a new
+// epoch, so they need no zeroing per query
+int out_hist_scan_words(Pipe &p, uint32_t tiles, hipStream_t st) {
+    const size_t bytes = (size_t)std::max<uint32_t>(out_hist_scan_blocks(tiles), 1) * 8;
+    const void *before = p.out_lb.p;
+    const size_t cap_before = p.out_lb.cap;
+    SKY_TRY(p.out_lb.ensure(bytes));
+    if (p.out_lb.p != before || p.out_lb.cap != cap_before) {
+        HIP_TRY(hipMemsetAsync(p.out_lb.p, 0, p.out_lb.cap, st));
+        p.out_epoch = 0;
+    }
+    return SKY_OK;
 }
 
 static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSet &fill, bool brute, uint32_t mt,
@@ -942,14 +959,18 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             c.ktimer_end("outc", st, n);
         } else if (!tiny) {
             c.ktimer_begin("outc", st);
-            if (p.hist_count)
-                launch_out_hist_count(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(),
-                                      p.pruner_fate.as<uint8_t>(), KM, tiles, p.out_cnt.as<uint32_t>(), st);
-            else
+            if (p.hist_count) {             // counts + scan in one launch
+                SKY_TRY(out_hist_scan_words(p, tiles, st));
+                launch_out_hist_scan(p.tile_hist.as<uint32_t>(), p.tile_cand.as<uint32_t>(), p.pruner_fate.as<uint8_t>(),
+                                     KM, tiles, p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(),
+                                     p.totals.as<uint32_t>() + 3, p.out_lb.as<unsigned long long>(), ++p.out_epoch,
+                                     p.flags.as<uint32_t>(), st);
+            } else {
                 launch_out_count(oa, st);
+                scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
+                              p.scratch.as<uint32_t>(), st);
+            }
             c.ktimer_end("outc", st, n);
-            scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
-                          p.scratch.as<uint32_t>(), st);
         }
         OutArgs ow = oa;
         ow.out_off = p.out_off.as<uint32_t>();

@@ -23,9 +23,8 @@ static inline unsigned nblk_d(size_t n, int per) { return (unsigned)((n + per - 
 // overflow, every count within the bound its launches were sized for, the small-set size, the
 // compare type), evaluated where the data is: the verdict travels in the block header, so every
 // rank learns after the all-gather whether some rank has to re-run its local phase.
-__global__ void k_plan_verdict(const uint32_t *__restrict__ tot, const uint32_t *__restrict__ flags, PlanCheck pc,
-                               uint32_t *__restrict__ verdict) {
-    if (threadIdx.x != 0) return;
+__device__ __forceinline__ uint32_t plan_verdict_value(const uint32_t *__restrict__ tot,
+                                                       const uint32_t *__restrict__ flags, const PlanCheck &pc) {
     const uint32_t f = *flags;
     uint32_t v = 0;
     if (f & kFlagNaN) v |= kDistNaN;
@@ -41,7 +40,12 @@ __global__ void k_plan_verdict(const uint32_t *__restrict__ tot, const uint32_t 
         ok &= pc.k_u16 ? ints : (pc.k_f32 ? !f64 : true);
         if (!ok) v |= kDistReplan;
     }
-    *verdict = v;
+    return v;
+}
+
+__global__ void k_plan_verdict(const uint32_t *__restrict__ tot, const uint32_t *__restrict__ flags, PlanCheck pc,
+                               uint32_t *__restrict__ verdict) {
+    if (threadIdx.x == 0) *verdict = plan_verdict_value(tot, flags, pc);
 }
 
 // alive u8 -> u32 over a device-sized unit range (units >= *d_n count 0)
@@ -97,6 +101,86 @@ __global__ void k_dist_header(const uint32_t *__restrict__ d_count, const uint32
         block[t] = v;
     }
 }
+
+// The slot-mode export tail in ONE workgroup (the planned small-set route's shards: a few
+// thousand units): the run's verdict (k_plan_verdict), the alive flags (k_dist_flags), their
+// exclusive scan, the exported rows (k_dist_rows) and the header (k_dist_header) -- five dependent
+// launches of 4-6 us each before.  flag / pos stay written for the merge's k_dist_alive_g.
+constexpr int kDistExportThreads = 1024;
+constexpr uint32_t kDistExportOneMax = 32768;        // units the one-workgroup tail takes
+template <int D>
+__global__ __launch_bounds__(kDistExportThreads) void k_dist_export_one(
+    const uint32_t *__restrict__ tot, const uint32_t *__restrict__ flags, PlanCheck pc, uint32_t *__restrict__ verdict,
+    const uint8_t *__restrict__ alive, uint32_t n_units, const uint32_t *__restrict__ d_n, uint32_t *__restrict__ flag,
+    uint32_t *__restrict__ pos, uint32_t *__restrict__ d_count, const double *__restrict__ rows,
+    const uint64_t *__restrict__ key, const uint32_t *__restrict__ slot_src, const uint32_t *__restrict__ dup_cnt,
+    const int32_t *__restrict__ pr_entries, int64_t *__restrict__ block, uint32_t cap, uint32_t n_tuples) {
+    constexpr int DP = padded_dims<double>(D);
+    constexpr int RW = D + 2;
+    constexpr int NW = kDistExportThreads / 64;
+    __shared__ uint32_t s_w[NW], s_v;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_v = plan_verdict_value(tot, flags, pc);
+    const uint32_t nd = d_n ? min(n_units, *d_n) : n_units;
+    uint32_t base = 0;
+    for (uint32_t j0 = 0; j0 < n_units; j0 += kDistExportThreads) {     // block-uniform
+        const uint32_t j = j0 + tid;
+        const uint32_t f = j < nd && alive[j] ? 1u : 0u;
+        uint32_t inc = f;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) s_w[wave] = inc;
+        __syncthreads();
+        uint32_t wb = 0, bt = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint32_t c = s_w[w];
+            wb += w < wave ? c : 0u;
+            bt += c;
+        }
+        __syncthreads();
+        const uint32_t e = base + wb + inc - f;
+        if (j < n_units) {
+            flag[j] = f;
+            pos[j] = e;
+        }
+        if (f && e < cap) {                   // counted past cap: the exchange re-runs larger
+            int64_t *o = block + (size_t)(e + 1) * RW;
+            const double *r = rows + (size_t)j * DP;
+#pragma unroll
+            for (int d = 0; d < D; d++) o[d] = __double_as_longlong(r[d]);
+            o[D] = (int64_t)(key[j] >> 56);
+            const uint32_t src = slot_src[j];
+            o[D + 1] = (src & 0x80000000u) ? (int64_t)dup_cnt[pr_entries[src & 0x7fffffffu]] : 1ll;
+        }
+        base += bt;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        *verdict = s_v;
+        *d_count = base;
+        pos[n_units] = base;                  // (the scan's total slot, as scan_excl_u32 leaves it)
+        block[0] = (int64_t)base;
+        block[1] = (int64_t)s_v;
+        block[2] = (int64_t)n_tuples;
+        if (D + 2 > 3) block[3] = D;
+    }
+    if (tid >= 4 && tid < D + 2) block[tid] = 0;
+}
+
+void launch_dist_export_one(int D, const uint32_t *tot, const uint32_t *flags, const PlanCheck &pc, uint32_t *verdict,
+                            const uint8_t *alive, uint32_t n_units, const uint32_t *d_n, uint32_t *flag, uint32_t *pos,
+                            uint32_t *d_count, const double *rows, const uint64_t *key, const uint32_t *slot_src,
+                            const uint32_t *dup_cnt, const int32_t *pr_entries, int64_t *block, uint32_t cap,
+                            uint32_t n_tuples, hipStream_t st) {
+    SKY_DISPATCH_D(D, (k_dist_export_one<DD><<<1, kDistExportThreads, 0, st>>>(
+                          tot, flags, pc, verdict, alive, n_units, d_n, flag, pos, d_count, rows, key, slot_src, dup_cnt,
+                          pr_entries, block, cap, n_tuples)));
+}
+uint32_t dist_export_one_max() { return kDistExportOneMax; }
 
 // ---- the merge -------------------------------------------------------------------------
 // sum[0] = largest count of any block, [1] = OR of the verdicts, [2] = this rank's verdict,

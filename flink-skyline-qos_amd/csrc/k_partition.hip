@@ -1376,6 +1376,97 @@ __global__ __launch_bounds__(kThreads) void k_out_hist_count(const uint32_t *__r
     if (lane == 0) out_cnt[tile] = c + tile_cand[tile];
 }
 
+// The same per-tile counts AND their exclusive scan in ONE launch (k_out_hist_count + the
+// three-kernel scan before: four dependent launches): a workgroup takes 256 consecutive tiles
+// (one per thread; the duplicate groups whose pruner is in G listed once in LDS, usually a
+// handful), scans them in the block and takes its prefix from a decoupled look-back over the
+// earlier workgroups (blockIdx order: every earlier workgroup was dispatched first).  The
+// look-back words carry the launch's epoch in their high half, so the words of an earlier
+// launch never read as this launch's (no zeroing launch): bits 63..34 epoch, 33..32 state
+// (1 aggregate, 2 inclusive prefix), 31..0 count.  A spin past its bound -> kFlagRadixSpin.
+__global__ __launch_bounds__(kThreads) void k_out_hist_scan(const uint32_t *__restrict__ hist,
+                                                            const uint32_t *__restrict__ tile_cand,
+                                                            const uint8_t *__restrict__ pruner_fate, int KM,
+                                                            uint32_t ntiles, uint32_t *__restrict__ out_cnt,
+                                                            uint32_t *__restrict__ out_off, uint32_t *__restrict__ d_total,
+                                                            unsigned long long *__restrict__ lb, uint32_t epoch,
+                                                            uint32_t *__restrict__ err) {
+    __shared__ uint8_t s_gq[kHistMaxKM];
+    __shared__ uint32_t s_ng, s_w[kThreads / 64];
+    __shared__ uint32_t s_prefix;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave == 0) {
+        uint32_t ng = 0;
+        for (int q0 = 0; q0 < KM; q0 += 64) {
+            const bool g = q0 + lane < KM && (pruner_fate[q0 + lane] & 2u);
+            const uint64_t b = __ballot(g);
+            if (g) s_gq[ng + lanes_below(b)] = (uint8_t)(q0 + lane);
+            ng += (uint32_t)__popcll(b);
+        }
+        if (lane == 0) s_ng = ng;
+    }
+    const uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t tc = t < ntiles ? tile_cand[t] : 0u;
+    __syncthreads();
+    const uint32_t ng = s_ng;
+    uint32_t c = tc;
+    if (t < ntiles) {
+        const uint32_t *h = hist + (size_t)t * KM;
+        for (uint32_t i = 0; i < ng; i++) c += h[s_gq[i]];
+    }
+    uint32_t bt;
+    const uint32_t pl = block_scan_excl(c, s_w, bt);
+    const unsigned long long tag = (unsigned long long)epoch << 34;
+    const unsigned long long kAgg = 1ull << 32, kInc = 2ull << 32, kState = 3ull << 32;
+    if (wave == 0) {
+        uint32_t excl = 0;
+        const uint32_t b = blockIdx.x;
+        if (lane == 0)
+            __hip_atomic_store(lb + b, tag | (b == 0 ? kInc : kAgg) | bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (b > 0) {
+            int64_t end = (int64_t)b - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t idx = end - lane;
+                const unsigned long long w = idx >= 0 ? __hip_atomic_load(lb + idx, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                                      : (tag | kInc);
+                const bool cur = (w >> 34) == (unsigned long long)epoch;
+                const unsigned long long st = cur ? (w & kState) : 0ull;
+                const uint64_t inc = __ballot(st == kInc), none = __ballot(st == 0ull);
+                const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+                if (none & upto) {
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0) atomicOr(err, kFlagRadixSpin);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t v = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                excl += v;
+                if (first < 64) break;
+                end -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(lb + b, tag | kInc | (unsigned long long)(excl + bt), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_prefix = excl;
+            if (b == gridDim.x - 1) *d_total = excl + bt;
+        }
+    }
+    __syncthreads();
+    if (t < ntiles) {
+        out_cnt[t] = c;
+        out_off[t] = s_prefix + pl;
+    }
+}
+
 // Count pass: kOutTPB tiles per workgroup, every tile's status words loaded up front
 // (the pass is latency-bound per workgroup otherwise); per-tile selected counts by
 // ballot + popcount.  Stats (|L_k|, survivors_k): unit weights by wave ballots per
@@ -2419,6 +2510,16 @@ void launch_out_fused(const OutArgs &a, unsigned long long *lb, uint32_t *ticket
                       int64_t cap, hipStream_t st) {
     const uint32_t tiles = (a.n + kTile - 1) / kTile;
     if (tiles) k_out_fused<<<tiles, kThreads, 0, st>>>(a, lb, ticket, d_total, err, cap);
+}
+
+uint32_t out_hist_scan_blocks(uint32_t ntiles) { return (ntiles + kThreads - 1) / kThreads; }
+
+void launch_out_hist_scan(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,
+                          uint32_t ntiles, uint32_t *out_cnt, uint32_t *out_off, uint32_t *d_total,
+                          unsigned long long *lb, uint32_t epoch, uint32_t *err, hipStream_t st) {
+    if (!ntiles) return;
+    k_out_hist_scan<<<out_hist_scan_blocks(ntiles), kThreads, 0, st>>>(hist, tile_cand, pruner_fate, KM, ntiles, out_cnt,
+                                                                       out_off, d_total, lb, epoch & 0x3fffffffu, err);
 }
 
 void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,

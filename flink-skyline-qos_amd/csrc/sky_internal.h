@@ -218,6 +218,14 @@ void launch_out_count(const OutArgs &a, hipStream_t st);
 constexpr int kHistMaxKM = 256;
 void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,
                            uint32_t ntiles, uint32_t *out_cnt, hipStream_t st);
+// the same counts + their exclusive scan (out_off, *d_total) in one launch: lb holds
+// out_hist_scan_blocks(ntiles) look-back words, zeroed when allocated; epoch != the last launch's
+uint32_t out_hist_scan_blocks(uint32_t ntiles);
+struct Pipe;
+int out_hist_scan_words(Pipe &p, uint32_t tiles, hipStream_t st);   // engine.hip: sizes / zeroes the words
+void launch_out_hist_scan(const uint32_t *hist, const uint32_t *tile_cand, const uint8_t *pruner_fate, int KM,
+                          uint32_t ntiles, uint32_t *out_cnt, uint32_t *out_off, uint32_t *d_total,
+                          unsigned long long *lb, uint32_t epoch, uint32_t *err, hipStream_t st);
 void launch_out_write(const OutArgs &a, hipStream_t st);
 // count + prefix + write in one pass (decoupled look-back over tiles): lb [tiles] u64 and
 // *ticket zeroed by the caller; *d_total = selected tuples; writes positions < cap only
@@ -436,6 +444,14 @@ struct PlanCheck {                      // pipe_finish's planned-route checks, a
 void launch_plan_verdict(const uint32_t *totals, const uint32_t *flags, const PlanCheck &pc, uint32_t *verdict,
                          hipStream_t st);
 void launch_dist_flags(const uint8_t *alive, uint32_t n, const uint32_t *d_n, uint32_t *out, hipStream_t st);
+// the slot-mode export tail (verdict, flags, scan, rows, header) in one workgroup, for up to
+// dist_export_one_max() units; pos has n_units + 1 entries
+uint32_t dist_export_one_max();
+void launch_dist_export_one(int D, const uint32_t *tot, const uint32_t *flags, const PlanCheck &pc, uint32_t *verdict,
+                            const uint8_t *alive, uint32_t n_units, const uint32_t *d_n, uint32_t *flag, uint32_t *pos,
+                            uint32_t *d_count, const double *rows, const uint64_t *key, const uint32_t *slot_src,
+                            const uint32_t *dup_cnt, const int32_t *pr_entries, int64_t *block, uint32_t cap,
+                            uint32_t n_tuples, hipStream_t st);
 void launch_dist_rows(int D, bool f64, const void *rows, const uint64_t *key, const uint32_t *flag, const uint32_t *pos,
                       uint32_t n, const uint32_t *slot_src, const uint32_t *dup_cnt, const int32_t *pr_entries,
                       const unsigned long long *mult, int64_t *block, uint32_t cap, hipStream_t st);

@@ -22,11 +22,14 @@ def _tptr(t):
 class _Ordered:
     """Brackets a *_dev call: the library's stream first waits for the caller's current
     torch stream (which produced the inputs), and the torch stream then waits for the
-    library (which wrote the outputs).  GPU-side events only."""
+    library (which wrote the outputs).  GPU-side events only.  An engine bound to a torch
+    stream (SkylineEngine.use_torch_stream) runs ON that stream: no events, no stream lookup."""
 
-    def __init__(self, h, device):
+    def __init__(self, h, device, bound=None):
         self.h = h
         self.s = None
+        if bound is not None:
+            return
         t = _abi.torch
         if t is not None and t.cuda.is_available():
             self.s = ctypes.c_void_p(t.cuda.current_stream(device).cuda_stream)
@@ -66,6 +69,7 @@ class SkylineEngine:
             check(lib().sky_ctx_set_semantics(self.h, _abi.SEM_COMPLETE))
         if grid_filter:   # GridDominanceFilter (FlinkSkyline.java:716-733)
             check(lib().sky_ctx_set_grid_filter(self.h, 1))
+        self._bound = None               # use_torch_stream: the torch stream the library runs on
         self.last_dist_stats = None      # set by skyline.dist.distributed_query
         self.K = self.P if not (self.algo == _abi.ALGO_GRID and semantics == "complete") else max(self.P, 1 << self.dims)
 
@@ -93,7 +97,7 @@ class SkylineEngine:
 
     def partition_keys_dev(self, d_values, d_keys_out):
         n = d_values.numel() // self.dims
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_partition_keys_dev(self.h, _tptr(d_values), n, _tptr(d_keys_out)))
 
     # ---- fused query ---------------------------------------------------------------
@@ -113,7 +117,7 @@ class SkylineEngine:
     def query_dev(self, d_ids, d_values, d_ids_out, d_origin_out, cap):
         n = d_values.numel() // self.dims
         cnt = ctypes.c_int64(0)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_query_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_ids_out),
                                       _tptr(d_origin_out), cap, ctypes.byref(cnt)))
         return cnt.value
@@ -180,17 +184,17 @@ class SkylineEngine:
     def dist_export_dev(self, d_ids, d_values, d_block, cap):
         """Local skylines of this rank's shard -> its fixed-size exchange block (no host read)."""
         n = d_values.numel() // self.dims
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_dist_export_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_block), cap))
 
     def dist_reblock_dev(self, d_block, cap):
         """Rewrite this rank's block with a larger capacity (after SKY_E_CAPACITY with need_cap)."""
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_dist_reblock_dev(self.h, _tptr(d_block), cap))
 
     def dist_merge_dev(self, d_blocks, world, rank, cap, d_ids_out, d_origin_out, out_cap, d_stats):
         """Own vectors vs the gathered union; output ids and this rank's stat shares (no host read)."""
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_dist_merge_dev(self.h, _tptr(d_blocks), world, rank, cap, _tptr(d_ids_out),
                                            _tptr(d_origin_out), out_cap, _tptr(d_stats)))
 
@@ -199,7 +203,7 @@ class SkylineEngine:
         status is SKY_OK or SKY_E_RETRY / SKY_E_CAPACITY (the caller re-runs), other codes raise."""
         n = ctypes.c_int64(0)
         need = ctypes.c_int64(0)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             rc = lib().sky_dist_finish(self.h, _tptr(d_stats_sum), out_cap, ctypes.byref(n), ctypes.byref(need))
         if rc not in (_abi.SKY_OK, _abi.SKY_E_RETRY, _abi.SKY_E_CAPACITY) or \
                 (rc == _abi.SKY_E_CAPACITY and need.value == 0):
@@ -216,7 +220,7 @@ class SkylineEngine:
     def synth_dev(self, dist, n, d_values, d_ids=None, seed=1234, id0=0, dmin=0, dmax=1000):
         if isinstance(dist, str):
             dist = _abi.DISTS[dist]
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_synth_dev(self.h, dist, dmin, dmax, seed, id0, n, _tptr(d_values), _tptr(d_ids)))
 
     # ---- bulk CSV ingest (ServiceTuple.fromString over raw records, ServiceTuple.java:89-104)
@@ -237,7 +241,7 @@ class SkylineEngine:
         """Device bytes -> device rows; returns (accepted, counts int64[4])."""
         n = ctypes.c_int64(0)
         cnt = np.zeros(4, np.int64)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_parse_csv_dev(self.h, _tptr(d_text), nbytes, _tptr(d_ids_out), _tptr(d_values_out), cap,
                                           ctypes.byref(n), cnt.ctypes.data_as(_abi.P_i64), _tptr(d_status_out)))
         return n.value, cnt
@@ -246,7 +250,7 @@ class SkylineEngine:
         """The producers' "id,v1,...,vD\n" payload of a device stream; returns its byte count
         (call with d_text=None first to size the buffer)."""
         nb = ctypes.c_int64(0)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_format_csv_dev(self.h, _tptr(d_ids), _tptr(d_values), n, _tptr(d_text), cap,
                                            ctypes.byref(nb)))
         return nb.value
@@ -256,7 +260,7 @@ class SkylineEngine:
         in place; returns (passes, ms)."""
         p = ctypes.c_int32(0)
         ms = ctypes.c_double(0)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_profile_sort_dev(self.h, _tptr(d_keys), _tptr(d_vals), d_keys.numel(), ctypes.byref(p),
                                              ctypes.byref(ms)))
         return p.value, ms.value
@@ -268,13 +272,24 @@ class SkylineEngine:
         n = d_values.numel() // self.dims
         kind = ctypes.c_int32(0)
         ms = ctypes.c_double(0)
-        with _Ordered(self.h, self.device):
+        with _Ordered(self.h, self.device, self._bound):
             check(lib().sky_profile_pairs_dev(self.h, _tptr(d_values), _tptr(d_keys), n, _tptr(d_fates_out),
                                               ctypes.byref(kind), ctypes.byref(ms)))
         return kind.value, ms.value
 
     def set_stream(self, stream_ptr):
         check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+        self._bound = None
+
+    def use_torch_stream(self, stream=None):
+        """Run the library on a torch stream (default: the current one) instead of its own:
+        the *_dev calls then need no cross-stream events (two HIP event operations and a
+        stream lookup per call).  The caller keeps issuing the tensors it passes on that
+        stream (or calls use_torch_stream again / set_stream(None) to go back)."""
+        t = _abi.torch
+        st = stream if stream is not None else t.cuda.current_stream(self.device)
+        check(lib().sky_ctx_set_stream(self.h, ctypes.c_void_p(st.cuda_stream)))
+        self._bound = st
 
     def sync(self):
         check(lib().sky_ctx_sync(self.h))
@@ -351,7 +366,7 @@ class SkylineStream:
 
     def append_dev(self, d_ids, d_values, n=None):
         n = d_values.shape[0] if n is None else n
-        with _Ordered(self.engine.h, self.engine.device):
+        with _Ordered(self.engine.h, self.engine.device, self.engine._bound):
             check(lib().sky_stream_append_dev(self.h, _tptr(d_ids), _tptr(d_values), n))
 
     def size(self):
@@ -428,6 +443,6 @@ class SkylineStream:
 
     def query_dev(self, d_ids_out, d_origin_out, cap):
         g = ctypes.c_int64(0)
-        with _Ordered(self.engine.h, self.engine.device):
+        with _Ordered(self.engine.h, self.engine.device, self.engine._bound):
             check(lib().sky_stream_query_dev(self.h, _tptr(d_ids_out), _tptr(d_origin_out), cap, ctypes.byref(g)))
         return g.value

@@ -406,3 +406,34 @@ def test_packed_u16_brute_pass(D, gpu_engine_factory, oracle, monkeypatch):
             monkeypatch.setenv("SKY_BRUTE16", flag)
             check_vs_oracle(gpu_engine_factory, oracle, vals, P, algo)
     monkeypatch.setenv("SKY_BRUTE16", "1")
+
+
+def test_use_torch_stream_equals_own_stream(gpu_engine_factory, oracle):
+    """SkylineEngine.use_torch_stream(): the library runs on the caller's torch stream (a side
+    stream here), so the *_dev calls skip the cross-stream events.  The tensors are produced and
+    consumed on that stream with no extra synchronisation; every query -- the synchronised route
+    and the planned replays, whose one-workgroup tail writes the final read into host-mapped
+    memory -- equals the oracle, as on the library's own stream."""
+    D, P, n = 2, 8, 200000
+    vals = oracle.synth(0, D, n, seed=55)
+    exp, keys, els, esv = oracle.query_sfs("dim", vals, P)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        eng = gpu_engine_factory(D, P, "mr-dim")
+        eng.use_torch_stream()
+        for rep in range(4):
+            dv = torch.from_numpy(vals).cuda()
+            di = torch.arange(n, dtype=torch.int64, device="cuda")
+            oi = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+            oo = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            g = eng.query_dev(di, dv, oi, oo, n)
+            got = oi[:g].cpu().numpy()                      # ordered after the query on `side`
+            np.testing.assert_array_equal(got, exp)
+            np.testing.assert_array_equal(oo[:g].cpu().numpy(), keys[exp])
+            ls, sv = eng.stats()
+            np.testing.assert_array_equal(ls, els)
+            np.testing.assert_array_equal(sv, esv)
+        eng.set_stream(None)                                 # back on the library's own stream
+        g = eng.query_dev(di, dv, oi, oo, n)
+        np.testing.assert_array_equal(oi[:g].cpu().numpy(), exp)
+        eng.close()
