@@ -676,13 +676,14 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restric
 //     x dominates y  <=>  x <= y everywhere and sum(x) < sum(y)
 // (x <= y with x != y makes the sum strictly smaller; equal vectors have equal sums), i.e.
 //     OR_w sat_u16(x_w - y_w)  |  sat_u32(sum(x) + 1 - sum(y))  == 0.
-// A dense all-pairs tile: a workgroup holds 256 y (one per lane) and stages kB16X x rows in LDS
+// A dense all-pairs tile: a workgroup holds 512 y (two per lane) and stages kB16X x rows in LDS
 // once, ordered by partition (a counting sort of the chunk), so that every x row costs the
-// compare words and ONE running minimum: per partition run the lane keeps min_x(word); at the
-// run's end the any-partition minimum takes it, and the same-partition minimum too where the
-// run's partition is the lane's.  8D: 4 v_pk_sub_u16 (clamp) + 1 saturating u32 subtract + 2
-// v_or3 + 1 v_min per pair test (8 compares), no per-pair VALU -> SGPR mask traffic.
-constexpr int kB16Y = 256, kB16X = 512;
+// compare words and ONE running minimum per y: per partition run the lane keeps min_x(word); at
+// the run's end the any-partition minimum takes it, and the same-partition minimum too where the
+// run's partition is the y's.  8D: 4 v_pk_sub_u16 (clamp) + 1 saturating u32 subtract + 2 v_or3 +
+// 1 v_min per pair test (8 compares), no per-pair VALU -> SGPR mask traffic; every x row read
+// from LDS serves both of a lane's y (half the LDS reads per pair test of one y per lane).
+constexpr int kB16T = 256, kB16YL = 2, kB16Y = kB16T * kB16YL, kB16X = 512;
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t sat_sub_u16x2(uint32_t x, uint32_t y) {
@@ -715,39 +716,45 @@ __device__ __forceinline__ uint32_t dom16_word(const uint4 (&xw)[W / 4], uint32_
 }
 
 template <int D, int W>
-__global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restrict__ rows,
+__global__ __launch_bounds__(kB16T) void k_brute16_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
                                                          const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
-    constexpr int RPT = kB16X / kB16Y;                          // x rows staged per thread
+    constexpr int RPT = kB16X / kB16T;                          // x rows staged per thread
+    constexpr int YL = kB16YL;
     if (d_mr) mr = min(mr, *d_mr);
     if (blockIdx.x * kB16Y >= mr || blockIdx.y * kB16X >= mr) return;
     __shared__ uint4 s_x[kB16X][W / 4];
     __shared__ uint32_t s_s[kB16X];                             // sum + 1 of each staged row
     __shared__ uint32_t s_h[kMaxK];                             // rows per partition -> run start
     __shared__ uint32_t s_rb[kMaxK + 1], s_rp[kMaxK];            // runs: start, partition
-    __shared__ uint32_t s_w[kB16Y / 64];
+    __shared__ uint32_t s_w[kB16T / 64];
+    static_assert(kMaxK == kB16T, "the partition scan takes one partition per thread");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t y0 = blockIdx.x * kB16Y, x0 = blockIdx.y * kB16X;
     const uint32_t cn = mr - x0 < (uint32_t)kB16X ? mr - x0 : (uint32_t)kB16X;
-    for (int q = tid; q < kMaxK; q += kB16Y) s_h[q] = 0;
-    // this lane's y
-    const uint32_t j = y0 + tid;
-    const bool valid = j < mr;
-    uint32_t y[W], sy = 0, py = 0xffffffffu;
-    if (valid) {
-        sy = pack_row16<D, W>(rows + (size_t)j * DP, y);
-        py = (uint32_t)(key[j] >> 56);
-    } else {
+    for (int q = tid; q < kMaxK; q += kB16T) s_h[q] = 0;
+    // this lane's y's
+    uint32_t y[YL][W], sy[YL], py[YL];
 #pragma unroll
-        for (int q = 0; q < W; q++) y[q] = 0u;
+    for (int v = 0; v < YL; v++) {
+        const uint32_t j = y0 + v * kB16T + tid;
+        sy[v] = 0;
+        py[v] = 0xffffffffu;
+        if (j < mr) {
+            sy[v] = pack_row16<D, W>(rows + (size_t)j * DP, y[v]);
+            py[v] = (uint32_t)(key[j] >> 56);
+        } else {
+#pragma unroll
+            for (int q = 0; q < W; q++) y[v][q] = 0u;
+        }
     }
     // the chunk's rows, ranked within their partition
     uint32_t xw[RPT][W], xs[RPT], xp[RPT], xr[RPT];
 #pragma unroll
     for (int u = 0; u < RPT; u++) {
-        const uint32_t r = u * kB16Y + tid;
+        const uint32_t r = u * kB16T + tid;
         xp[u] = 0xffffffffu;
         if (r < cn) {
             xs[u] = pack_row16<D, W>(rows + (size_t)(x0 + r) * DP, xw[u]) + 1u;
@@ -759,9 +766,9 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
     for (int u = 0; u < RPT; u++)
         if (xp[u] != 0xffffffffu) xr[u] = atomicAdd(&s_h[xp[u]], 1u);
     __syncthreads();
-    // exclusive scan of the partition counts (kMaxK = 256 = one per thread) and the run list
+    // exclusive scan of the partition counts (one per thread) and the run list
     {
-        const uint32_t c = tid < kMaxK ? s_h[tid] : 0u;
+        const uint32_t c = s_h[tid];
         uint32_t inc = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -773,14 +780,14 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
         __syncthreads();
         uint32_t base = 0, rbase = 0, tot_r = 0;
 #pragma unroll
-        for (int w = 0; w < kB16Y / 64; w++) {
+        for (int w = 0; w < kB16T / 64; w++) {
             const uint32_t v = s_w[w];
             if (w < wave) { base += v & 0xffffu; rbase += v >> 16; }
             tot_r += v >> 16;
         }
         const uint32_t start = base + inc - c;
         __syncthreads();
-        if (tid < kMaxK) s_h[tid] = start;
+        s_h[tid] = start;
         if (c) {
             const uint32_t ri = rbase + (uint32_t)__popcll(nz & ((1ull << lane) - 1ull));
             s_rb[ri] = start;
@@ -800,15 +807,19 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
         s_s[pos] = xs[u];
     }
     __syncthreads();
-    uint32_t acc_a = 0xffffffffu, acc_s = 0xffffffffu;
+    uint32_t acc_a[YL], acc_s[YL];
+#pragma unroll
+    for (int v = 0; v < YL; v++) acc_a[v] = acc_s[v] = 0xffffffffu;
     for (uint32_t rr = 0; rr < nruns; rr++) {
         const uint32_t b = __builtin_amdgcn_readfirstlane((int)s_rb[rr]);
         const uint32_t e = __builtin_amdgcn_readfirstlane((int)s_rb[rr + 1]);
         const uint32_t px = __builtin_amdgcn_readfirstlane((int)s_rp[rr]);
         constexpr int U = 4;                                    // rows in flight
-        uint32_t acc_u[U];
+        uint32_t acc_u[YL][U];
 #pragma unroll
-        for (int u = 0; u < U; u++) acc_u[u] = 0xffffffffu;
+        for (int v = 0; v < YL; v++)
+#pragma unroll
+            for (int u = 0; u < U; u++) acc_u[v][u] = 0xffffffffu;
         uint32_t i = b;
         for (; i + U <= e; i += U) {
             uint4 xa[U][W / 4];
@@ -820,20 +831,31 @@ __global__ __launch_bounds__(kB16Y) void k_brute16_pairs(const double *__restric
                 sa[u] = s_s[i + u];
             }
 #pragma unroll
-            for (int u = 0; u < U; u++) acc_u[u] = min(acc_u[u], dom16_word<W>(xa[u], sa[u], y, sy));
+            for (int v = 0; v < YL; v++)
+#pragma unroll
+                for (int u = 0; u < U; u++) acc_u[v][u] = min(acc_u[v][u], dom16_word<W>(xa[u], sa[u], y[v], sy[v]));
         }
         for (; i < e; i++) {
             uint4 xa[W / 4];
 #pragma unroll
             for (int q = 0; q < W / 4; q++) xa[q] = s_x[i][q];
-            acc_u[0] = min(acc_u[0], dom16_word<W>(xa, s_s[i], y, sy));
+            const uint32_t sa = s_s[i];
+#pragma unroll
+            for (int v = 0; v < YL; v++) acc_u[v][0] = min(acc_u[v][0], dom16_word<W>(xa, sa, y[v], sy[v]));
         }
-        const uint32_t acc = min(min(acc_u[0], acc_u[1]), min(acc_u[2], acc_u[3]));
-        acc_a = min(acc_a, acc);
-        if (px == py) acc_s = min(acc_s, acc);
+#pragma unroll
+        for (int v = 0; v < YL; v++) {
+            const uint32_t acc = min(min(acc_u[v][0], acc_u[v][1]), min(acc_u[v][2], acc_u[v][3]));
+            acc_a[v] = min(acc_a[v], acc);
+            if (px == py[v]) acc_s[v] = min(acc_s[v], acc);
+        }
     }
-    const uint32_t f = (acc_s == 0u ? 3u : 0u) | (acc_a == 0u ? 2u : 0u);
-    if (valid && f) atomicOr(&domf[j], f);
+#pragma unroll
+    for (int v = 0; v < YL; v++) {
+        const uint32_t j = y0 + v * kB16T + tid;
+        const uint32_t f = (acc_s[v] == 0u ? 3u : 0u) | (acc_a[v] == 0u ? 2u : 0u);
+        if (j < mr && f) atomicOr(&domf[j], f);
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_brute_finish(const uint64_t *__restrict__ key, uint32_t mr,
@@ -870,8 +892,8 @@ void launch_brute_pairs(int D, bool f32, bool u16, const void *rows, const uint6
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
     if (u16) {
         const dim3 g16((mr + kB16Y - 1) / kB16Y, (mr + kB16X - 1) / kB16X);
-        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
-        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16Y, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
+        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
+        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
     } else if (f32) {
         SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, d_mr, domf)));
     } else {

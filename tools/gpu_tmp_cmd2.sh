@@ -5,6 +5,12 @@ export PYTHONUNBUFFERED=1
 cd ${GRAFT_REPO_ROOT:-.}
 O=gpurun_out
 ML=flink-skyline-qos_amd/build_measure/libskyline_hip.so
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_dist_step.py tests/test_gpu_dist.py \
+   "tests/test_gpu_configs.py::test_c4_8way_decomposition" "tests/test_gpu_configs.py::test_c3_angle_4d_anti_50m_one_gpu_and_sharded" \
+   tests/test_gpu_operators.py > $O/disttests_g.log 2>&1 || { tail -40 $O/disttests_g.log; exit 1; }
+tail -2 $O/disttests_g.log
+timeout -k 10 600 python -u tools/dist_phases.py --only c4_8way,c3_8way --out $O/r06_dist_phases_g.json > $O/distphases_g.log 2>&1 || { tail -30 $O/distphases_g.log; exit 1; }
+grep '^{' $O/distphases_g.log | cut -c1-600
 : > $O/sq_g.log
 for c in C1 C2 C5T C4R; do
   CFG=$c timeout -k 10 120 python -u tools/small_query_ab.py >> $O/sq_g.log 2>&1 || { tail -20 $O/sq_g.log; exit 1; }
