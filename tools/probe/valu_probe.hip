@@ -25,6 +25,28 @@ __global__ __launch_bounds__(256) void k_fadd(float *out, float seed) {
     if (s == 12345.f) out[0] = s;
 }
 
+// independent v_pk_sub_u16 (clamp) chains: the packed 16-bit lane-op rate (2 compares per op is the
+// packed-u16 compare peak's definition)
+__global__ __launch_bounds__(256) void k_pksub(uint32_t *out, const uint32_t *__restrict__ subs, uint32_t seed) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    u16x2 a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        a[i] = __builtin_bit_cast(u16x2, seed + threadIdx.x * 65537u + i);
+        b[i] = __builtin_bit_cast(u16x2, subs[i]);            // runtime operands: no folding of the chain
+    }
+    for (int it = 0; it < kIters; it += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) a[i] = __builtin_elementwise_sub_sat(a[i], b[(i + j) & 7]);
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s ^= __builtin_bit_cast(uint32_t, a[i]);
+    if (s == 12345u) out[0] = s;
+}
+
 template <int PPT>
 __global__ __launch_bounds__(256) void k_cmp_f32(const float *__restrict__ xs, int nx, float *out) {
     float y[PPT][8];
@@ -123,6 +145,11 @@ int main() {
     double ms = time_ms([&] { k_fadd<<<blocks, 256>>>(out, 1.0f); });
     double ops = (double)blocks * 256 * kIters * 8;
     printf(", \"fadd_lane_ops_per_s\": %.4g", ops / (ms * 1e-3));
+    uint32_t *subs;
+    CK(hipMalloc(&subs, 64));
+    CK(hipMemset(subs, 0, 64));                               // x - 0: the chain keeps its values
+    ms = time_ms([&] { k_pksub<<<blocks, 256>>>((uint32_t *)out, subs, 0x03e803e8u); });
+    printf(", \"pk_sub_u16_lane_ops_per_s\": %.4g", ops / (ms * 1e-3));
     const int nx = 512;
     std::vector<float> hx(nx * 8);
     std::vector<uint32_t> hu(nx * 4);

@@ -19,7 +19,9 @@ import skyline  # noqa: E402
 
 CFGS = {"C1": ("mr-dim", 2, 8, "uniform", 1_000_000), "C2": ("mr-grid", 4, 8, "correlated", 10_000_000),
         "C5T": ("mr-angle", 6, 8, "mixed", 1_000_000),
-        "C4R": ("mr-angle", 8, 16, "anti_correlated", 12_500_000)}   # one rank's shard of C4 on 8 GPUs
+        "C4R": ("mr-angle", 8, 16, "anti_correlated", 12_500_000),   # one rank's shard of C4 on 8 GPUs
+        "C3": ("mr-angle", 4, 8, "anti_correlated", 50_000_000), "C3R": ("mr-angle", 4, 8, "anti_correlated", 6_250_000),
+        "C4H": ("mr-angle", 8, 16, "anti_correlated", 25_000_000)}
 name = os.environ.get("CFG", "C1")
 algo, D, P, dist, n = CFGS[name]
 dev = torch.device("cuda", 0)
@@ -62,7 +64,7 @@ for k in ("filter", "prefilter", "brute", "out", "outc", "outw", "mbr", "sfs_sma
 phases, counters = eng.phases()
 eng.close()
 print(json.dumps({"config": name, "filter_dbg": os.environ.get("SKY_FILTER_DBG"),
-                  "filter_tpb": os.environ.get("SKY_FILTER_TPB"),
+                  "filter_tpb": os.environ.get("SKY_FILTER_TPB"), "filter_pf": os.environ.get("SKY_FILTER_PF"),
                   "lib": os.path.basename(os.path.dirname(skyline._abi.LIB_PATH)),
                   "wall_p50_ms": statistics.median(wall), "wall_min_ms": min(wall),
                   "c_entry_p50_ms": statistics.median(raw), "c_entry_min_ms": min(raw),
