@@ -476,7 +476,8 @@ def stream_run(dev_index, seed, triggers=20, per_trigger=1_000_000, batch=50_000
     vals = torch.from_numpy(vals_np).pin_memory().numpy()
     ids = torch.from_numpy(ids_np).pin_memory().numpy()
     eng = skyline.SkylineEngine(D, P, "mr-angle", 1000.0, dev_index)
-    eng.use_torch_stream()
+    if not os.environ.get("BENCH_OWN_STREAM"):   # (A/B: the library on its own stream)
+        eng.use_torch_stream()
     eng.warmup()                                  # first launches / allocations, before the stream starts
 
     def run_stream(timers):

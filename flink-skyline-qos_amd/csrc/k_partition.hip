@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #pragma unroll
         for (int d = 0; d < D; d++) v[d] = vn[d];
         const int32_t kg = kn;
-        if (r > 0 && a.dbg < 2) {                                       // item r-1, beside the prefetch
+        if (r > 0 && !(a.dbg & 2)) {                                    // item r-1, beside the prefetch
             const bool vp = i - kThreads < a.n;
             if (!planes) {
                 if (vp) a.status[i - kThreads] = st_prev;
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
 #else
         SKY_FILTER_FETCH(r + 1 < kSpanItems ? i + kThreads : i);       // past the span: a cache hit
 #endif
-        if (a.dbg) {                 // measurement only (SKY_FILTER_DBG=1): the stream without the work
+        if (a.dbg & 3) {             // measurement only (SKY_FILTER_DBG=1): the stream without the work
             double acc = 0;
 #pragma unroll
             for (int d = 0; d < D; d++) acc += v[d];
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         wcnt += (uint32_t)__popcll(cm);
         st_prev = st;
     }
-    if (a.dbg < 2) {
+    if (!(a.dbg & 2)) {
         const uint32_t il = base + (kSpanItems - 1) * kThreads + threadIdx.x;
         const bool vp = il < a.n;
         if (!planes) {
@@ -624,9 +624,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(D <= 8
         const uint32_t c = s_dup[fq];
         const uint32_t tile = span * FT + f;
         if (a.tile_hist && tile < ntiles) a.tile_hist[(size_t)tile * KM + q] = c;
-        if (c) { atomicAdd(&a.dup_cnt[q], c); s_dup[fq] = 0; }
+        if (c) {
+            if (!(a.dbg & 4)) atomicAdd(&a.dup_cnt[q], c);      // (SKY_FILTER_DBG & 4: no global atomics)
+            s_dup[fq] = 0;
+        }
     }
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(a.m_total, total) : 0u;
+    if (threadIdx.x == 0) s_base = total && !(a.dbg & 4) ? atomicAdd(a.m_total, total) : 0u;
     if (threadIdx.x == 64 && dtotal) s_dbase = atomicAdd(a.defer_cnt, dtotal);
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < dtotal; q += kThreads) {

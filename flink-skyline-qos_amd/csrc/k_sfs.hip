@@ -676,14 +676,18 @@ __global__ __launch_bounds__(kBruteY) void k_brute_pairs(const double *__restric
 //     x dominates y  <=>  x <= y everywhere and sum(x) < sum(y)
 // (x <= y with x != y makes the sum strictly smaller; equal vectors have equal sums), i.e.
 //     OR_w sat_u16(x_w - y_w)  |  sat_u32(sum(x) + 1 - sum(y))  == 0.
-// A dense all-pairs tile: a workgroup holds 512 y (two per lane) and stages kB16X x rows in LDS
+// A dense all-pairs tile: a workgroup holds 256 YL y (YL per lane) and stages X x rows in LDS
 // once, ordered by partition (a counting sort of the chunk), so that every x row costs the
 // compare words and ONE running minimum per y: per partition run the lane keeps min_x(word); at
 // the run's end the any-partition minimum takes it, and the same-partition minimum too where the
 // run's partition is the y's.  8D: 4 v_pk_sub_u16 (clamp) + 1 saturating u32 subtract + 2 v_or3 +
 // 1 v_min per pair test (8 compares), no per-pair VALU -> SGPR mask traffic; every x row read
 // from LDS serves both of a lane's y (half the LDS reads per pair test of one y per lane).
-constexpr int kB16T = 256, kB16YL = 2, kB16Y = kB16T * kB16YL, kB16X = 512;
+// Tile shape by size: YL y per lane and X rows per chunk.  Large sets (the 64k dense line): two y
+// per lane, 512-row chunks; the query's slot sets (C4: 7.9k slots) keep one y per lane and 128-row
+// chunks, so that the grid still holds ~2k workgroups (16 x 16 of the large shape was one wave
+// per SIMD: 41 us against 24 us for C4's slots)
+constexpr int kB16T = 256;
 
 typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t sat_sub_u16x2(uint32_t x, uint32_t y) {
@@ -715,25 +719,25 @@ __device__ __forceinline__ uint32_t dom16_word(const uint4 (&xw)[W / 4], uint32_
     return r;
 }
 
-template <int D, int W>
+template <int D, int W, int YL, int X>
 __global__ __launch_bounds__(kB16T) void k_brute16_pairs(const double *__restrict__ rows,
                                                          const uint64_t *__restrict__ key, uint32_t mr,
                                                          const uint32_t *__restrict__ d_mr,
                                                          uint32_t *__restrict__ domf) {
     constexpr int DP = padded_dims<double>(D);
-    constexpr int RPT = kB16X / kB16T;                          // x rows staged per thread
-    constexpr int YL = kB16YL;
+    constexpr int RPT = (X + kB16T - 1) / kB16T;                // x rows staged per thread (at most)
+    constexpr int YB = kB16T * YL;                              // y per workgroup
     if (d_mr) mr = min(mr, *d_mr);
-    if (blockIdx.x * kB16Y >= mr || blockIdx.y * kB16X >= mr) return;
-    __shared__ uint4 s_x[kB16X][W / 4];
-    __shared__ uint32_t s_s[kB16X];                             // sum + 1 of each staged row
+    if (blockIdx.x * YB >= mr || blockIdx.y * X >= mr) return;
+    __shared__ uint4 s_x[X][W / 4];
+    __shared__ uint32_t s_s[X];                                 // sum + 1 of each staged row
     __shared__ uint32_t s_h[kMaxK];                             // rows per partition -> run start
     __shared__ uint32_t s_rb[kMaxK + 1], s_rp[kMaxK];            // runs: start, partition
     __shared__ uint32_t s_w[kB16T / 64];
     static_assert(kMaxK == kB16T, "the partition scan takes one partition per thread");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t y0 = blockIdx.x * kB16Y, x0 = blockIdx.y * kB16X;
-    const uint32_t cn = mr - x0 < (uint32_t)kB16X ? mr - x0 : (uint32_t)kB16X;
+    const uint32_t y0 = blockIdx.x * YB, x0 = blockIdx.y * X;
+    const uint32_t cn = mr - x0 < (uint32_t)X ? mr - x0 : (uint32_t)X;
     for (int q = tid; q < kMaxK; q += kB16T) s_h[q] = 0;
     // this lane's y's
     uint32_t y[YL][W], sy[YL], py[YL];
@@ -756,7 +760,7 @@ __global__ __launch_bounds__(kB16T) void k_brute16_pairs(const double *__restric
     for (int u = 0; u < RPT; u++) {
         const uint32_t r = u * kB16T + tid;
         xp[u] = 0xffffffffu;
-        if (r < cn) {
+        if (r < cn) {                                           // (cn <= X)
             xs[u] = pack_row16<D, W>(rows + (size_t)(x0 + r) * DP, xw[u]) + 1u;
             xp[u] = (uint32_t)(key[x0 + r] >> 56);
         }
@@ -891,9 +895,17 @@ void launch_brute_pairs(int D, bool f32, bool u16, const void *rows, const uint6
     if (!mr) return;
     const dim3 g((mr + kBruteY - 1) / kBruteY, (mr + kBruteX - 1) / kBruteX);
     if (u16) {
-        const dim3 g16((mr + kB16Y - 1) / kB16Y, (mr + kB16X - 1) / kB16X);
-        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
-        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }
+        // the large shape once it still fills the chip with >= 4096 workgroups (mr >= ~46k)
+        const bool big = (uint64_t)((mr + 511) / 512) * ((mr + 511) / 512) >= 4096;
+#define SKY_B16(YL, X)                                                                                       \
+    do {                                                                                                     \
+        const dim3 g16((mr + kB16T * YL - 1) / (kB16T * YL), (mr + X - 1) / X);                              \
+        if (D <= 8) { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 4, YL, X><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); } \
+        else { SKY_DISPATCH_D(D, (k_brute16_pairs<DD, 8, YL, X><<<g16, kB16T, 0, st>>>((const double *)rows, key, mr, d_mr, domf))); }     \
+    } while (0)
+        if (big) SKY_B16(2, 512);
+        else SKY_B16(1, 128);
+#undef SKY_B16
     } else if (f32) {
         SKY_DISPATCH_D(D, (k_brute_pairs<float, DD><<<g, kBruteY, 0, st>>>((const double *)rows, key, mr, d_mr, domf)));
     } else {

@@ -76,7 +76,7 @@ struct FilterArgs {
     uint32_t *defer_cnt;
     uint32_t slot_cap;            // slots allocated: appends past it are counted, not written
     uint32_t *tile_hist;          // [tiles][Kp*M] duplicates per tile (nullptr: not kept; Kp*M <= kHistMaxKM)
-    int dbg;                      // SKY_FILTER_DBG (measurement only, results invalid): 1 = loads + status only
+    int dbg;                      // SKY_FILTER_DBG (measurement only, results invalid): 1 = loads + status only, 2 = loads only, 4 = no global atomics
     // status planes (nullptr: every status word is stored): per tile 32 (item, wave) pairs of
     // 64-bit words, B = duplicate of the designated group dom_kj (k * M + j), E = the status
     // word is stored (candidates, other duplicate groups, deferred keys); else dropped

@@ -4,10 +4,23 @@ set -e
 export PYTHONUNBUFFERED=1
 cd ${GRAFT_REPO_ROOT:-.}
 O=gpurun_out
-timeout -k 10 120 tools/probe/valu_probe > $O/valu_probe_i.json 2>&1 || { cat $O/valu_probe_i.json; exit 1; }
-cat $O/valu_probe_i.json
-timeout -k 10 900 python -u bench.py > $O/bench_i.json 2> $O/bench_i.err || { tail -30 $O/bench_i.err; exit 1; }
-cut -c1-1200 $O/bench_i.json
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-   --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --dist-backend gloo > $O/rehearsal2_i.json 2> $O/rehearsal2_i.err || { tail -30 $O/rehearsal2_i.err; exit 1; }
-grep '^{' $O/rehearsal2_i.json | cut -c1-300
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_dense.py tests/test_gpu_plan.py \
+    tests/test_gpu_configs.py tests/test_gpu_mbr.py > $O/tests_k.log 2>&1 || { tail -40 $O/tests_k.log; exit 1; }
+tail -2 $O/tests_k.log
+timeout -k 10 200 python -u tools/dense_bench.py 16384 65536 > $O/dense_k.log 2>&1 || { tail -20 $O/dense_k.log; exit 1; }
+grep '^{' $O/dense_k.log | cut -c1-400
+timeout -k 10 300 python -u tools/c5_ab.py > $O/c5ab_k.log 2>&1 || { tail -20 $O/c5ab_k.log; exit 1; }
+grep '^{' $O/c5ab_k.log
+ML=flink-skyline-qos_amd/build_measure/libskyline_hip.so
+: > $O/atom_k.log
+for c in C1 C2 C4R C3; do
+  for m in 0 4 1; do
+    CFG=$c SKYLINE_HIP_LIB=$ML SKY_FILTER_DBG=$m timeout -k 10 120 python -u tools/small_query_ab.py >> $O/atom_k.log 2>&1 || { tail -20 $O/atom_k.log; exit 1; }
+  done
+done
+grep '^{' $O/atom_k.log | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); k = d['kernel_mean_ms_profiled']
+    print(d['config'], 'dbg', d['filter_dbg'], 'filter_ms', round(k.get('filter', 0), 4))
+"
