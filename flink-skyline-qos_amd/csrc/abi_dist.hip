@@ -26,6 +26,8 @@
 
 namespace sky {
 size_t mbr_group_slots(uint32_t mr);   // k_mbr.hip: gmin / gprange entries (groups + super-groups)
+uint32_t dist_export_one_max();        // k_dist.hip
+bool dist_summary_fused(int world);    // k_dist.hip: the pair pass computes k_dist_summary's words
 }
 
 namespace {
@@ -327,7 +329,11 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
     fill.add(c->dist_sum.p, 128);
     if (p.hist_count && c->dist_state == 1 && tiles) fill.add(p.tile_cand.p, (size_t)tiles * 4);
     HIP_TRY(fill.launch(st));
-    launch_dist_summary(d_blocks, world, rank, (uint32_t)cap, D, sum, st);
+    const uint64_t bp0 = dist_brute_pairs();
+    const bool brute_route = c->dist_state == 1 && p.n && c->dist_hist_pairs >= 0 &&
+                             (uint64_t)c->dist_hist_pairs <= bp0;
+    // the pair-kernel route computes the summary words itself (one launch less)
+    if (!(brute_route && dist_summary_fused(world))) launch_dist_summary(d_blocks, world, rank, (uint32_t)cap, D, sum, st);
     if (c->dist_state == 2 || p.n == 0)        // NaN (finish reports it) or an empty shard: no fates
         HIP_TRY(hipMemsetAsync(p.totals.as<uint32_t>() + 3, 0, 4, st));
     if (c->dist_state == 1 && p.n) {
@@ -337,8 +343,8 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
         //      kernel checks this step's sizes on the device and, when they are too large, writes
         //      no fate and raises the route-miss word: every rank returns SKY_E_RETRY, this one
         //      then takes the sized route)
-        const uint64_t bp = dist_brute_pairs();
-        const bool brute = c->dist_hist_pairs >= 0 && (uint64_t)c->dist_hist_pairs <= bp;
+        const uint64_t bp = bp0;
+        const bool brute = brute_route;
         if (brute) {
             const unsigned __int128 worst = (unsigned __int128)(uint64_t)cap * (uint64_t)cap * (uint64_t)world;
             const unsigned long long limit = worst <= bp ? ~0ull : (unsigned long long)bp;
@@ -415,8 +421,7 @@ int sky_dist_merge_dev(sky_ctx *c, const int64_t *d_blocks, int32_t world, int32
     }
     // merge-time errors (the union pass's look-backs) into the summed words, then this rank's
     // shares for the caller's all-reduce
-    launch_dist_merge_err(p.flags.as<uint32_t>(), w_err, st);
-    HIP_TRY(hipMemcpyAsync(d_stats, p.statk.p, (size_t)SKY_DIST_STATS_WORDS(K) * 8, hipMemcpyDeviceToDevice, st));
+    launch_dist_merge_err(p.flags.as<uint32_t>(), lsz, (int)(w_err - lsz), (int)SKY_DIST_STATS_WORDS(K), d_stats, st);
     HIP_TRY(hipGetLastError());
     c->dist_world = world;
     c->dist_merged = true;

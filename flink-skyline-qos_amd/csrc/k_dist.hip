@@ -336,26 +336,61 @@ __device__ __forceinline__ uint32_t union_block_of(uint32_t u, int world, const 
 
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_dist_union_pairs(const int64_t *__restrict__ blocks, int world, int rank,
-                                                               uint32_t cap, const unsigned long long *__restrict__ sum,
+                                                               uint32_t cap, unsigned long long *__restrict__ sum,
                                                                unsigned long long limit,
                                                                unsigned long long *__restrict__ miss,
-                                                               uint32_t *__restrict__ dom) {
+                                                               uint32_t *__restrict__ dom, int fused_summary) {
     constexpr int RW = D + 2;
     constexpr int CH = union_rows<D>();
-    const unsigned long long n_own = sum[4], n_union = sum[3];
-    if (n_own * n_union > limit) {
-        if (blockIdx.x == 0 && threadIdx.x == 0 && miss) *miss = 1ull;
-        return;
-    }
-    if (!n_own || !n_union) return;
     __shared__ double s_x[CH * D];
     __shared__ int32_t s_k[CH];
     __shared__ uint32_t s_off[kUnionOffLds];
     __shared__ uint32_t s_bits[kUnionY];
     __shared__ uint32_t s_cnt;
+    __shared__ unsigned long long s_sum[2];                  // this launch's |union|, |own|
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int b = tid; b < world && b < kUnionOffLds; b += kThreads) s_off[b] = (uint32_t)sum[16 + b];
     const size_t bstride = (size_t)(cap + 1) * RW;
+    if (fused_summary) {
+        // k_dist_summary's words from the gathered headers (world <= kUnionOffLds), in every
+        // workgroup; workgroup 0 also stores them for the later kernels and the host's finish
+        if (tid == 0) {
+            unsigned long long mx = 0, vor = 0, tot = 0, all = 0, mine = 0, mine_all = 0, mine_v = 0, off_own = 0;
+            for (int b = 0; b < world; b++) {
+                const int64_t c = blocks[(size_t)b * bstride], v = blocks[(size_t)b * bstride + 1];
+                const unsigned long long cu = c < 0 ? 0ull : (unsigned long long)c;
+                const unsigned long long held = cu < cap ? cu : (unsigned long long)cap;
+                s_off[b] = (uint32_t)tot;
+                if (b == rank) { mine = held; mine_all = cu; mine_v = (unsigned long long)v; off_own = tot; }
+                mx = cu > mx ? cu : mx;
+                vor |= (unsigned long long)v;
+                tot += held;
+                all += cu;
+            }
+            s_sum[0] = tot;
+            s_sum[1] = mine;
+            if (blockIdx.x == 0) {
+                sum[0] = mx;
+                sum[1] = vor;
+                sum[2] = mine_v;
+                sum[3] = tot;
+                sum[4] = mine;
+                sum[6] = off_own;
+                sum[7] = all;
+                sum[8] = mine_all;
+                for (int b = 0; b < world; b++) sum[16 + b] = s_off[b];
+            }
+        }
+    } else {
+        for (int b = tid; b < world && b < kUnionOffLds; b += kThreads) s_off[b] = (uint32_t)sum[16 + b];
+        if (tid == 0) { s_sum[0] = sum[3]; s_sum[1] = sum[4]; }
+    }
+    __syncthreads();
+    const unsigned long long n_own = s_sum[1], n_union = s_sum[0];
+    if (n_own * n_union > limit) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && miss) *miss = 1ull;
+        return;
+    }
+    if (!n_own || !n_union) return;
     const int64_t *own = blocks + (size_t)rank * bstride;
     const uint32_t ytiles = (uint32_t)((n_own + kUnionY - 1) / kUnionY);
     // union rows per item: enough items to spread over the grid (>= 2 per workgroup), at least
@@ -549,9 +584,11 @@ void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *
     }
 }
 
+bool dist_summary_fused(int world) { return world <= kUnionOffLds; }
+
 void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
                             uint32_t *dom, unsigned long long *lsz, unsigned long long *surv,
-                            const unsigned long long *sum, unsigned long long limit, unsigned long long *miss,
+                            unsigned long long *sum, unsigned long long limit, unsigned long long *miss,
                             hipStream_t st) {
     if (!cap) return;
     // the grid walks the (own tile, union rows) items; its size bounds them from the capacity
@@ -559,7 +596,11 @@ void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, u
     const uint64_t items = ytiles * (((uint64_t)world * cap + 63) / 64);
     const unsigned g = (unsigned)std::min<uint64_t>(items, 1024);
     const unsigned gf = (unsigned)std::min<uint64_t>(((uint64_t)cap + kThreads - 1) / kThreads, 256);
-    SKY_DISPATCH_D(D, (k_dist_union_pairs<DD><<<g, kThreads, 0, st>>>(blocks, world, rank, cap, sum, limit, miss, dom)));
+    // the summary words are computed inside the pair pass while the block offsets fit its LDS
+    // (the caller then launched no k_dist_summary: dist_summary_fused)
+    const int fused = world <= kUnionOffLds ? 1 : 0;
+    SKY_DISPATCH_D(D, (k_dist_union_pairs<DD><<<g, kThreads, 0, st>>>(blocks, world, rank, cap, sum, limit, miss, dom,
+                                                                      fused)));
     SKY_DISPATCH_D(D, (k_dist_union_finish<DD><<<gf, kThreads, 0, st>>>(blocks, rank, cap, K, sum, limit, dom, flags,
                                                                          lsz, surv)));
 }
@@ -567,11 +608,20 @@ void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, u
 // merge-time errors into the all-reduced stat words: a look-back that exceeded its spin bound in
 // the union pass (flags, kFlagRadixSpin), or its work queue's overflow (kFlagMbrQueue) -> err = 1
 // (every rank then returns SKY_E_HIP)
-__global__ void k_dist_merge_err(const uint32_t *__restrict__ flags, unsigned long long *__restrict__ err) {
-    if (threadIdx.x == 0) *err = (flags[0] & (kFlagRadixSpin | kFlagMbrQueue | kFlagTinyOob)) ? 1ull : 0ull;
+// ... and this rank's share words (statk, err included) into the caller's buffer: one launch
+// instead of the error word's kernel and a device-to-device copy
+__global__ void k_dist_merge_err(const uint32_t *__restrict__ flags, unsigned long long *__restrict__ statk,
+                                 int err_word, int words, int64_t *__restrict__ out) {
+    const unsigned long long e = (flags[0] & (kFlagRadixSpin | kFlagMbrQueue | kFlagTinyOob)) ? 1ull : 0ull;
+    for (int t = threadIdx.x; t < words; t += blockDim.x) {
+        const unsigned long long v = t == err_word ? e : statk[t];
+        if (t == err_word) statk[t] = e;
+        out[t] = (int64_t)v;
+    }
 }
-void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st) {
-    k_dist_merge_err<<<1, 64, 0, st>>>(flags, err);
+void launch_dist_merge_err(const uint32_t *flags, unsigned long long *statk, int err_word, int words, int64_t *out,
+                           hipStream_t st) {
+    k_dist_merge_err<<<1, 256, 0, st>>>(flags, statk, err_word, words, out);
 }
 
 void launch_dist_alive_g(const uint32_t *flag, const uint32_t *pos, uint32_t n, const uint8_t *own_flags, uint32_t cap,

@@ -463,9 +463,10 @@ void launch_dist_compact(int D, const int64_t *blocks, int world, uint32_t cap, 
                          uint64_t *ukey, int64_t *umult, hipStream_t st);
 void launch_dist_pack(int D, const double *rows, uint32_t m, int fmt, uint32_t *out, hipStream_t st);
 void launch_dist_union_fate(int D, const int64_t *blocks, int world, int rank, uint32_t cap, int K, uint8_t *flags,
-                            uint32_t *dom, unsigned long long *lsz, unsigned long long *surv, const unsigned long long *sum,
+                            uint32_t *dom, unsigned long long *lsz, unsigned long long *surv, unsigned long long *sum,
                             unsigned long long limit, unsigned long long *miss, hipStream_t st);
-void launch_dist_merge_err(const uint32_t *flags, unsigned long long *err, hipStream_t st);
+void launch_dist_merge_err(const uint32_t *flags, unsigned long long *statk, int err_word, int words, int64_t *out,
+                           hipStream_t st);
 void launch_dist_alive_g(const uint32_t *flag, const uint32_t *pos, uint32_t n, const uint8_t *own_flags, uint32_t cap,
                          uint8_t *alive_g, hipStream_t st);
 
