@@ -166,8 +166,9 @@ static size_t slot_min() {
 constexpr uint32_t kPrefilterProbe = 16;  // a skipped prefilter is probed again every 16 queries
 constexpr uint32_t kTinyBlock = 16;       // plans learned without the one-workgroup tail after it missed
 constexpr uint32_t kPickInFilterMax = 16u << 20;   // tuples up to which the filter picks its own pruners
-// slots up to which a prefilter round runs as the fused pass: beyond, its per-workgroup pick and the
-// look-back cost what the launches it saves cost (C4's 241k slots: 46 us fused vs 39 us + 5 launches)
+// slots up to which a prefilter round's fused pass redoes the pick in every workgroup (four slots per
+// thread); beyond, one k_cand_pick launch and one slot per thread (C4's 241k slots: 236 four-slot
+// workgroups, one per CU, took 46 us against 39 us + 5 launches for the chain)
 constexpr uint32_t kCandFusedMax = 65536;
 constexpr uint32_t kTailTilesMax = 1024;        // tiles up to which the brute route's counts run as k_tail_counts
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
@@ -226,9 +227,18 @@ static bool cand_fused_disabled() {   // SKY_CAND_FUSED=0: pick / filter / scan 
     return e && e[0] == '0';
 }
 // the fused prefilter pass's look-back words of each planned round: [tiles][u64] + a ticket word
-static size_t cand_lb_bytes(uint32_t bound) { return (size_t)cand_fused_tiles(bound) * 8 + 64; }
+// above kCandFusedMax slots (or SKY_CAND_FUSED=2) the fused pass runs after one k_cand_pick
+static bool cand_picked(uint32_t bound) {
+    const char *e = SKY_ENV("SKY_CAND_FUSED");
+    return bound > kCandFusedMax || (e && e[0] == '2');
+}
+static size_t cand_lb_bytes(uint32_t bound) { return (size_t)cand_fused_tiles(bound, cand_picked(bound)) * 8 + 64; }
 static bool tail_counts_disabled() {   // SKY_TAIL_COUNTS=0: hist counts / scan / stat reduce / gather launches (A/B knob)
     const char *e = SKY_ENV("SKY_TAIL_COUNTS");
+    return e && e[0] == '0';
+}
+static bool epilogue_disabled() {   // SKY_OUT_EPILOGUE=0: k_stat_reduce + k_gather_words launches (A/B knob)
+    const char *e = SKY_ENV("SKY_OUT_EPILOGUE");
     return e && e[0] == '0';
 }
 static bool tiny_disabled() {    // SKY_TINY=0: the planned tail as one launch per stage (A/B knob)
@@ -910,6 +920,9 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     // the four launches it replaces; C1-sized runs take the one-workgroup tail anyway)
     const bool tailk = !tiny && brute && p.fused && !fused_onepass() && p.hist_count && slot_stats &&
                        tiles <= kTailTilesMax && (p.segalive.p && p.seg_begin.p) && !tail_counts_disabled();
+    // the brute route's stat reduce and final read as the write pass's epilogue workgroups
+    const bool ep = !tiny && !tailk && brute && p.fused && !fused_onepass() && slot_stats && p.segalive.p &&
+                    p.seg_begin.p && p.K <= 65536 && !epilogue_disabled();
     p.fused_ids = in.out_ids;
     p.fused_org = in.out_org;
     c.ktimer_begin("out", st);
@@ -981,6 +994,20 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         ow.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
         ow.dom_kj = p.dom_kj;
         ow.skip_flags = tiny ? p.flags.as<uint32_t>() : nullptr;
+        if (ep) {
+            SKY_TRY(p.statk.ensure((size_t)p.K * 16));
+            SKY_TRY(p.pinned(tiny_pin_layout(p.K, p.Kp, KM, ow.ep_off)));
+            ow.ep_pin = reinterpret_cast<uint32_t *>(p.pin);
+            ow.ep_lsz = p.lsz.as<unsigned long long>();
+            ow.ep_surv = p.surv.as<unsigned long long>();
+            ow.ep_statk = p.statk.as<unsigned long long>();
+            ow.ep_totals = p.totals.as<uint32_t>();
+            ow.ep_segalive = p.segalive.as<uint32_t>();
+            ow.ep_segn = p.seg_begin.as<uint32_t>();
+            ow.ep_flags = p.flags.as<uint32_t>();
+            ow.ep_dup = p.dup_cnt.as<uint32_t>();
+            ow.ep_Kp = p.Kp;
+        }
         c.ktimer_begin("outw", st);
         launch_out_write(ow, st);
         c.ktimer_end("outw", st, n);
@@ -995,7 +1022,7 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     STAGE(st, "fate");
     uint32_t nout = 0;
     SKY_TRY(p.statk.ensure((size_t)p.K * 16));
-    if (!tiny && !tailk)
+    if (!tiny && !tailk && !ep)
         launch_stat_reduce(p.lsz.as<unsigned long long>(), p.surv.as<unsigned long long>(), p.K,
                            p.statk.as<unsigned long long>(), st);
     std::vector<unsigned long long> sk2((size_t)p.K * 2);
@@ -1009,7 +1036,8 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         SKY_TRY(sync_read(p, st, {{p.totals.p, 64}, {p.statk.p, (size_t)p.K * 16},
                                   {p.segalive.p, (size_t)p.Kp * 4}, {p.seg_begin.p, (size_t)p.Kp * 4},
                                   {p.flags.p, 4}, {p.dup_cnt.p, (size_t)KM * 4}},
-                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()}, tiny || tailk));
+                          {tot, sk2.data(), p.h_seg_s.data(), p.h_seg_n.data(), &flags2, p.h_dup.data()},
+                          tiny || tailk || ep));
         nout = tot[3];
 #ifdef SKY_MEASURE
         if (SKY_MEASURE_ENV("SKY_FILTER_COUNT")) {   // k_filter's stores (tools/: the write itemisation)
@@ -1152,7 +1180,7 @@ static int plan_prepare(Pipe &p, int D, bool tiny, FillSet &fill) {
             size_t lb = 0;
             uint32_t b = pl.bound[0];
             for (int r = 0; r < pl.rounds; r++) {
-                if (b <= kCandFusedMax) lb += cand_lb_bytes(b);
+                lb += cand_lb_bytes(b);
                 b = std::min(pl.bound[r + 1], b);
             }
             SKY_TRY(p.cand_lb.ensure(lb));
@@ -1406,7 +1434,7 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
         ca.live = p.live.as<uint32_t>();
         uint32_t *d_live = p.totals.as<uint32_t>() + 11 + round;
         c.ktimer_begin("prefilter", st);
-        if (cand_fused_fits(D, p.Kp, M2) && bound <= kCandFusedMax && !cand_fused_disabled()) {   // (plan_prepare zeroed its words)
+        if (cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled()) {   // (plan_prepare zeroed its words)
             ca.rows2 = dr->as<double>();
             ca.key2 = dk->as<uint64_t>();
             ca.src2 = ds->as<uint32_t>();
@@ -1415,7 +1443,9 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
             ca.entries = p.pr_entries.as<int32_t>();
             ca.KM = KM;
             ca.lb = reinterpret_cast<unsigned long long *>(p.cand_lb.as<char>() + lb_off);
-            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + lb_off + (size_t)cand_fused_tiles(bound) * 8);
+            ca.picked = cand_picked(bound);
+            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + lb_off +
+                                                     (size_t)cand_fused_tiles(bound, ca.picked) * 8);
             ca.err = p.flags.as<uint32_t>();
             launch_cand_min(D, ca, st);
             launch_cand_fused(D, ca, st);
@@ -1715,7 +1745,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
         SKY_TRY(dk->ensure((size_t)mt0 * 8));
         SKY_TRY(ds->ensure((size_t)mt0 * 4));
         SKY_TRY(p.scratch.ensure(scan_scratch_words(mt0 + 1) * 4 + 64));
-        const bool fused = cand_fused_fits(D, p.Kp, M2) && mt0 <= kCandFusedMax && !cand_fused_disabled();
+        const bool fused = cand_fused_fits(D, p.Kp, M2) && !cand_fused_disabled();
         if (fused) {
             SKY_TRY(p.cand_lb.ensure(cand_lb_bytes(mt0)));
             fill.add(p.cand_lb.p, cand_lb_bytes(mt0));
@@ -1743,7 +1773,8 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
             ca.entries = p.pr_entries.as<int32_t>();
             ca.KM = KM;
             ca.lb = p.cand_lb.as<unsigned long long>();
-            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + (size_t)cand_fused_tiles(mt0) * 8);
+            ca.picked = cand_picked(mt0);
+            ca.ticket = reinterpret_cast<uint32_t *>(p.cand_lb.as<char>() + (size_t)cand_fused_tiles(mt0, ca.picked) * 8);
             ca.err = p.flags.as<uint32_t>();
             launch_cand_min(D, ca, st);
             launch_cand_fused(D, ca, st);

@@ -1010,10 +1010,13 @@ constexpr unsigned long long kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbCount 
 // tile only waits for tiles already running; bounded spin -> kFlagRadixSpin), which keeps the
 // compaction in slot order exactly as the scan + k_cand_compact did.  The appended pruner slots'
 // indices are remapped from their entries (a dropped one: -1).
-constexpr int kCandFI = 4;                 // slots per thread in k_cand_fused
-template <int D>
+// PICKED (CandArgs::picked, large slot counts): k_cand_pick ran once before and its pr2 / npr2 are
+// staged instead, one slot per thread -- at C4's 241k slots the per-workgroup pick over 236
+// workgroups of four slots per thread (one per CU) was slower than the launch chain it replaced
+template <int D, int FI, bool PICKED>
 __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
     constexpr int DP = padded_dims<double>(D);
+    constexpr int kCandFI = FI;
     extern __shared__ __attribute__((aligned(16))) double s_pr2[];   // [Kp][M2 * D + 1]
     __shared__ int32_t s_np[kMaxK];
     __shared__ uint32_t s_w[kThreads / 64];
@@ -1021,9 +1024,20 @@ __global__ __launch_bounds__(kThreads) void k_cand_fused(CandArgs a) {
     __shared__ unsigned long long s_prefix;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int M2 = a.M2, PS = a.M2 * D + 1;
-    if (threadIdx.x == 0) s_tile = atomicAdd(a.ticket, 1u);
+    // tiles in blockIdx order, as k_out_hist_scan: each XCD dispatches its workgroups in order, so a
+    // tile only waits for tiles dispatched before it.  (A ticket -- an atomic per workgroup on one
+    // address, serialised at one L2 channel ahead of every workgroup's loads -- cost C4's 943-tile
+    // pass 11 us of its 29.)
+    if (threadIdx.x == 0) s_tile = blockIdx.x;
     const uint32_t mt = a.d_mt ? min(a.mt, *a.d_mt) : a.mt;
-    for (int k = wave; k < a.Kp; k += kThreads / 64) {
+    if constexpr (PICKED) {
+        for (int q = threadIdx.x; q < a.Kp * M2 * D; q += kThreads) {
+            const int k = q / (M2 * D), r = q - k * (M2 * D);
+            s_pr2[k * PS + r] = a.pr2[q];
+        }
+        for (int k = threadIdx.x; k < a.Kp; k += kThreads) s_np[k] = a.npr2[k];
+    }
+    for (int k = wave; k < (PICKED ? 0 : a.Kp); k += kThreads / 64) {
         const unsigned long long w = lane < M2 ? a.cmin[k * M2 + lane] : ~0ull;
         const bool has = w != ~0ull;
         double c[D];
@@ -1616,10 +1630,57 @@ __global__ __launch_bounds__(kThreads) void k_out_count(OutArgs a) {
 // layout of the count pass made the id loads 64-byte strided).  Index order within the tile
 // is (k, wave, lane): a selected tuple's output position is the count of the (k, wave)
 // groups before it (32 per tile, scanned in LDS) plus its rank in its wave's ballot.
+// The write pass's epilogue workgroups (OutArgs::ep_pin): workgroup e < K sums stat key e over the
+// shards (k_stat_reduce), workgroup K copies the final read's other words (k_gather_words); every
+// word they read was final before this launch, and the write pass changes none of them
+__device__ __forceinline__ void out_epilogue(const OutArgs &a, uint32_t e) {
+    __shared__ unsigned long long s_l[kThreads / 64], s_s[kThreads / 64];
+    const int K = a.K;
+    if (e < (uint32_t)K) {
+        unsigned long long l = 0, sv = 0;
+        for (int sh = threadIdx.x; sh < kStatShards; sh += kThreads) {
+            l += a.ep_lsz[(size_t)sh * K + e];
+            sv += a.ep_surv[(size_t)sh * K + e];
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            l += __shfl_xor(l, o, 64);
+            sv += __shfl_xor(sv, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) { s_l[threadIdx.x >> 6] = l; s_s[threadIdx.x >> 6] = sv; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            l = 0;
+            sv = 0;
+            for (int q = 0; q < kThreads / 64; q++) { l += s_l[q]; sv += s_s[q]; }
+            a.ep_statk[e] = l;
+            a.ep_statk[K + e] = sv;
+            unsigned long long *pk = reinterpret_cast<unsigned long long *>(a.ep_pin + a.ep_off[0]);
+            pk[e] = l;
+            pk[K + e] = sv;
+        }
+        return;
+    }
+    for (int q = threadIdx.x; q < 16; q += kThreads) a.ep_pin[q] = a.ep_totals[q];
+    for (int q = threadIdx.x; q < a.ep_Kp; q += kThreads) {
+        a.ep_pin[a.ep_off[1] + q] = a.ep_segalive[q];
+        a.ep_pin[a.ep_off[2] + q] = a.ep_segn[q];
+    }
+    if (threadIdx.x == 0) a.ep_pin[a.ep_off[3]] = a.ep_flags[0];
+    for (int q = threadIdx.x; q < a.KM; q += kThreads) a.ep_pin[a.ep_off[4] + q] = a.ep_dup[q];
+}
+
 __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     // after a one-workgroup tail that missed (or tripped its guard) no fate / offset is valid:
     // the caller's buffers are left untouched (the host re-runs the query or returns the error)
     if (a.skip_flags && (*a.skip_flags & (kFlagTinyMiss | kFlagTinyOob))) return;
+    {
+        const uint32_t ntile = (a.n + kTile - 1) / kTile;
+        if (blockIdx.x >= ntile) {                     // (block-uniform) the final read's words
+            out_epilogue(a, blockIdx.x - ntile);
+            return;
+        }
+    }
     __shared__ uint8_t s_pf[2048];
     __shared__ uint32_t s_cnt[kItems * (kThreads / 64)];
     __shared__ uint32_t s_tot;
@@ -2441,7 +2502,12 @@ bool cand_fused_fits(int D, int Kp, int M2) {
 void launch_cand_fused(int D, const CandArgs &a, hipStream_t st) {
     if (!a.mt) return;
     const size_t lds = (size_t)a.Kp * (a.M2 * D + 1) * sizeof(double);
-    SKY_DISPATCH_D(D, (k_cand_fused<DD><<<cand_fused_tiles(a.mt), kThreads, lds, st>>>(a)));
+    if (a.picked) {
+        SKY_DISPATCH_D(D, (k_cand_pick<DD><<<a.Kp, 64, 0, st>>>(a.rows, a.cmin, a.M2, a.pr2, a.npr2)));
+        SKY_DISPATCH_D(D, (k_cand_fused<DD, 1, true><<<cand_fused_tiles(a.mt, true), kThreads, lds, st>>>(a)));
+    } else {
+        SKY_DISPATCH_D(D, (k_cand_fused<DD, 4, false><<<cand_fused_tiles(a.mt, false), kThreads, lds, st>>>(a)));
+    }
 }
 
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
@@ -2532,7 +2598,7 @@ void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, cons
 }
 
 void launch_out_write(const OutArgs &a, hipStream_t st) {
-    if (a.n) k_out_write<<<nblk(a.n, kTile), kThreads, 0, st>>>(a);
+    if (a.n) k_out_write<<<nblk(a.n, kTile) + (a.ep_pin ? (uint32_t)a.K + 1u : 0u), kThreads, 0, st>>>(a);
 }
 // sky_profile_pairs_dev: caller rows -> the slot format of the brute pass (f64 rows padded to
 // 16 B, sort key = partition | f32 score | hash, as k_filter appends candidates)

@@ -154,6 +154,7 @@ struct CandArgs {
     unsigned long long *lb = nullptr;     // [cand_fused_tiles(mt)] look-back words, zeroed
     uint32_t *ticket = nullptr;           // zeroed
     uint32_t *err = nullptr;              // kFlagRadixSpin if a look-back ran out of spins
+    bool picked = false;                  // k_cand_pick first (pr2 / npr2), then one slot per thread
 };
 void launch_cand_prefilter(int D, const CandArgs &a, hipStream_t st);
 // the criterion minima alone (k_cand_min), for the fused pass after it
@@ -161,7 +162,11 @@ void launch_cand_min(int D, const CandArgs &a, hipStream_t st);
 // the fused pass: false (nothing launched) when its pruner image does not fit LDS -- the caller
 // then runs k_cand_pick / k_cand_filter / the scan / k_cand_compact
 bool cand_fused_fits(int D, int Kp, int M2);
-inline uint32_t cand_fused_tiles(uint32_t mt) { return (mt + 4 * kThreads - 1) / (4 * kThreads); }   // kCandFI = 4
+// (four slots per thread, or one after k_cand_pick)
+inline uint32_t cand_fused_tiles(uint32_t mt, bool picked) {
+    const uint32_t per = picked ? kThreads : 4 * kThreads;
+    return (mt + per - 1) / per;
+}
 void launch_cand_fused(int D, const CandArgs &a, hipStream_t st);
 void launch_cand_compact(int D, const CandArgs &a, const uint32_t *pos, double *rows2, uint64_t *key2, uint32_t *src2,
                          int32_t *pruner_slot, int KM, hipStream_t st);
@@ -211,6 +216,16 @@ struct OutArgs {
     const uint64_t *planes = nullptr;   // the filter's status planes (k_out_write only)
     int32_t dom_kj = -1;
     const uint32_t *skip_flags = nullptr;   // write pass: nothing is written if this word has a tail miss / guard bit
+    // write pass: the brute route's final read folded in (k_stat_reduce + k_gather_words): K more
+    // workgroups past the tiles reduce one stat key each, one more copies the other words, all into
+    // host-mapped memory in tiny_pin_layout (ep_pin nullptr: no epilogue)
+    uint32_t *ep_pin = nullptr;
+    uint32_t ep_off[5] = {};
+    const unsigned long long *ep_lsz = nullptr, *ep_surv = nullptr;   // [kStatShards][K]
+    unsigned long long *ep_statk = nullptr;                          // [2K]
+    const uint32_t *ep_totals = nullptr, *ep_segalive = nullptr, *ep_segn = nullptr, *ep_flags = nullptr,
+                   *ep_dup = nullptr;
+    int ep_Kp = 0;
 };
 void launch_out_count(const OutArgs &a, hipStream_t st);
 // per-tile counts of the global level from the filter's duplicate histograms + k_fate_tables'

@@ -188,9 +188,10 @@ def test_tiny_tail_miss(gpu_engine_factory, oracle):
 
 def test_cand_fused_pass_equals_launch_chain(gpu_engine_factory, oracle):
     """The prefilter's pick / live test / scan / compaction as one launch with a decoupled look-back
-    (k_cand_fused, default) and as the launch chain (SKY_CAND_FUSED=0, read per query): both routes
+    (k_cand_fused, default), after one k_cand_pick with one slot per thread (SKY_CAND_FUSED=2, the
+    form above 64k slots) and as the launch chain (SKY_CAND_FUSED=0, read per query): both routes
     (synchronised, planned) give the oracle's answer on a stream with prefilter rounds."""
-    for knob in ("1", "0"):
+    for knob in ("1", "2", "0"):
         os.environ["SKY_CAND_FUSED"] = knob
         try:
             eng = gpu_engine_factory(8, 16, "mr-angle")
@@ -219,6 +220,25 @@ def test_tail_counts_equals_launch_chain(gpu_engine_factory, oracle, algo, dist,
             eng.close()
         finally:
             del os.environ["SKY_TAIL_COUNTS"]
+
+
+@pytest.mark.parametrize("algo,dist,D,n,P,planned", [("mr-grid", 1, 4, 2500000, 8, True),
+                                                      ("mr-angle", 1, 5, 2200000, 16, False)])
+def test_out_epilogue_equals_launches(gpu_engine_factory, oracle, algo, dist, D, n, P, planned):
+    """Past k_tail_counts' 1024 tiles, the brute route's stat reduce and final read run as the write
+    pass's epilogue workgroups (default) or as k_stat_reduce + k_gather_words (SKY_OUT_EPILOGUE=0):
+    the oracle's ids, origins and stats on the synchronised and the planned route either way."""
+    short = algo.split("-")[1]
+    for knob in ("1", "0"):
+        os.environ["SKY_OUT_EPILOGUE"] = knob
+        try:
+            eng = gpu_engine_factory(D, P, algo)
+            check(eng, oracle, oracle.synth(dist, D, n, seed=131), P, short)
+            r, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=132), P, short)
+            assert bool(r & PLANNED) or not planned
+            eng.close()
+        finally:
+            del os.environ["SKY_OUT_EPILOGUE"]
 
 
 MEASURE_LIB = os.path.join(__import__("conftest").PKG, "build_measure", "libskyline_hip.so")
