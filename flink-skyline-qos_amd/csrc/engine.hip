@@ -241,6 +241,14 @@ static bool epilogue_disabled() {   // SKY_OUT_EPILOGUE=0: k_stat_reduce + k_gat
     const char *e = SKY_ENV("SKY_OUT_EPILOGUE");
     return e && e[0] == '0';
 }
+static bool fill_embed_disabled() {   // SKY_FILL_EMBED=0: the query's fills as their own launch (A/B knob)
+    const char *e = SKY_ENV("SKY_FILL_EMBED");
+    return e && e[0] == '0';
+}
+static bool finish_fold_disabled() {   // SKY_FINISH_FOLD=0: k_brute_finish as its own launch (A/B knob)
+    const char *e = SKY_ENV("SKY_FINISH_FOLD");
+    return e && e[0] == '0';
+}
 static bool tiny_disabled() {    // SKY_TINY=0: the planned tail as one launch per stage (A/B knob)
     const char *e = SKY_ENV("SKY_TINY");
     return e && e[0] == '0';
@@ -798,6 +806,8 @@ struct PlanRun {
     const uint32_t *d_cnt = nullptr;  // slots entering the brute pass (device)
     bool k_u16 = false, k_f32 = false;   // the brute pass's compare type
     bool tiny = false;                    // k_tiny_tail ran the tail (fates, counts, scan, stats)
+    const uint32_t *domf = nullptr;       // k_brute_finish left to k_fate_tables: the pass's bits
+    bool gmerge = false;
 };
 // the next run's designated duplicate group (status planes): the largest group of this run
 void pick_dom_group(Pipe &p, int KM) {
@@ -886,6 +896,16 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
     fta.lsz = slot_stats ? p.lsz.as<unsigned long long>() : nullptr;
     fta.surv = slot_stats ? p.surv.as<unsigned long long>() : nullptr;
     fta.tile_cand = p.hist_count ? p.tile_cand.as<uint32_t>() : nullptr;
+    if (pr && pr->domf) {                       // the brute pass's finish, folded in
+        fta.domf = pr->domf;
+        fta.key = p.s_key->as<uint64_t>();
+        fta.gmerge = pr->gmerge ? 1 : 0;
+        fta.alive_l_w = p.alive_l.as<uint8_t>();
+        fta.alive_g_w = p.alive_g.as<uint8_t>();
+        fta.slot_rep_w = p.slot_rep.as<uint32_t>();
+        fta.segalive = p.segalive.as<uint32_t>();
+        fta.segn = p.seg_begin.as<uint32_t>();
+    }
     const bool tiny = pr && pr->tiny;
     if (!tiny) launch_fate_tables(fta, st);
     if (tm) tm->mark(7, st);
@@ -1079,6 +1099,11 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
             ok &= fin <= brute_max();
             const bool f64 = (flags2 & kFlagNotF32) != 0, ints = !f64 && (flags2 & kFlagNotU16) == 0;
             ok &= pr->k_u16 ? ints : (pr->k_f32 ? !f64 : true);
+            if (!ok && debug_level() >= 1)
+                fprintf(stderr, "[sky] plan miss: slots %u/%u rounds %d live %u/%u fin %u tiny %d u16 %d/%d f32 %d/%d\n",
+                        tot[10], p.plan.bound[0], p.plan.rounds, p.plan.rounds ? tot[11] : 0u,
+                        p.plan.rounds ? p.plan.bound[1] : 0u, fin, (int)pr->tiny, (int)pr->k_u16, (int)ints,
+                        (int)pr->k_f32, (int)!f64);
             if (!ok) return kPlanMiss;
             p.m = m;
             p.nps = nps;
@@ -1478,9 +1503,19 @@ static int pipe_run_planned(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, s
     pr.k_u16 = p.ints && !brute16_disabled();
     pr.k_f32 = !p.f64;
     c.ktimer_begin("brute", st);
-    launch_brute_fates(D, pr.k_f32, pr.k_u16, p.s_rows->p, p.s_key->as<uint64_t>(), bound, in.global && !in.single,
-                       p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
-                       p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st, d_cnt);
+    // the finish (alive flags, per-partition counts) runs inside k_fate_tables unless this run
+    // writes no fates (multi-GPU export; SKY_FINISH_FOLD=0: the separate k_brute_finish, A/B knob)
+    const bool fold = !in.dist && in.fate && !finish_fold_disabled();
+    if (fold) {
+        launch_brute_pairs(D, pr.k_f32, pr.k_u16, p.s_rows->p, p.s_key->as<uint64_t>(), bound, p.keep.as<uint32_t>(), st,
+                           d_cnt);
+        pr.domf = p.keep.as<uint32_t>();
+        pr.gmerge = in.global && !in.single;
+    } else {
+        launch_brute_fates(D, pr.k_f32, pr.k_u16, p.s_rows->p, p.s_key->as<uint64_t>(), bound, in.global && !in.single,
+                           p.keep.as<uint32_t>(), p.alive_l.as<uint8_t>(), p.alive_g.as<uint8_t>(),
+                           p.segalive.as<uint32_t>(), p.seg_begin.as<uint32_t>(), p.slot_rep.as<uint32_t>(), st, d_cnt);
+    }
     c.ktimer_end("brute", st, (int64_t)bound * bound);
     STAGE(st, "brute");
     if (tm) tm->mark(6, st);
@@ -1567,7 +1602,19 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.pmin.ensure((size_t)p.Kp * p.M * 8));
     SKY_TRY(p.pruners.ensure((size_t)p.Kp * p.M * D * 8));
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
-    fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);   // per-slot sample minima start all-ones
+    // the sample minima are tagged per query (launch_select_pruners): all-ones only for a new buffer
+    // and when the 16-bit query count wraps
+    const bool pmin_reset = p.pmin.p != p.pmin_at || ((p.pmin_epoch + 1) & 0xffffu) == 0;
+    if (pmin_reset) {
+        fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);
+        p.pmin_at = p.pmin.p;
+        p.pmin_epoch = 0;
+#ifdef SKY_MEASURE
+        if (const char *e = SKY_MEASURE_ENV("SKY_PMIN_EPOCH0")) p.pmin_epoch = (uint32_t)atoi(e) & 0xffffu;   // the wrap's test
+#endif
+    }
+    p.pmin_epoch++;
+    const uint32_t ptag = 0xffffu - (p.pmin_epoch & 0xffffu);
     // output counts from per-tile duplicate histograms (unit weights, stats over slots, the
     // single-pass output's buffers): the filter keeps them, the fate pass counts candidates
     p.hist_count = ((in.fate && (in.out_ids || in.out_org)) || in.dist) && !in.origin && !in.weights &&
@@ -1610,13 +1657,17 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
                 (int)planned, (int)tiny, (int)p.plan.tiny, (int)p.hist_count, p.plan.bound[0], p.plan.rounds,
                 (int)tiny_fits(D, p.Kp, std::min(prefilter_m2(), 2048 / p.Kp), KM, in.K, tiles));
     if (planned) SKY_TRY(plan_prepare(p, D, tiny, fill));
-    HIP_TRY(fill.launch(st));
+    // the fills go with the sample pass (one launch less) unless pmin itself is among them
+    FillRanges pre{};
+    const bool pre_taken = !pmin_reset && !fill_embed_disabled() && fill.take(pre);
+    if (!pre_taken) HIP_TRY(fill.launch(st));
     // small streams: the sample minima only, the filter's workgroups pick the pruners from them (one
     // dependent launch less, where launches are the query's cost); large ones keep k_pick_pruners
     // (every filter workgroup's prologue would wait on two more dependent loads)
     const bool pick_in_filter = n <= kPickInFilterMax;
     launch_select_pruners(D, in.vals, n, S, kp, in.keys, in.single, p.Kp, p.M, p.pmin.as<unsigned long long>(),
-                          p.pruners.as<double>(), p.npr.as<int32_t>(), st, !pick_in_filter);
+                          p.pruners.as<double>(), p.npr.as<int32_t>(), st, !pick_in_filter, ptag,
+                          pre_taken ? &pre : nullptr);
     STAGE(st, "pruners");
     if (tm) tm->mark(1, st);
 
@@ -1647,6 +1698,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     fa.dom_kj = p.dom_kj;
     fa.pick_gmin = pick_in_filter ? p.pmin.as<unsigned long long>() : nullptr;
     fa.pick_S = S;
+    fa.pick_tag = ptag;
     fa.pruners_w = p.pruners.as<double>();
     fa.npr_w = p.npr.as<int32_t>();
     {

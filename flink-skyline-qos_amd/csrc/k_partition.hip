@@ -147,9 +147,12 @@ template <int D>
 __global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restrict__ vals, uint32_t n, uint32_t S,
                                                          KeyParams kp, const int32_t *__restrict__ given_keys,
                                                          int single, int Kp, int M,
-                                                         unsigned long long *__restrict__ gmin) {
+                                                         unsigned long long *__restrict__ gmin, uint32_t tag,
+                                                         FillRanges pre) {
     __shared__ unsigned long long s_min[2048];
     const int KM = Kp * M;
+    fill_ranges_grid(pre);                   // the query's fills (read by the later kernels only)
+    const unsigned long long tg = (unsigned long long)tag << 48;
     for (int q = threadIdx.x; q < KM; q += kThreads) s_min[q] = ~0ull;
     __syncthreads();
     // grid-stride over the sample (few workgroups: each adds its KM minima to the same KM
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restric
                 if (j >= M) break;
                 const float c = j == 0 ? sum : sum + 3.0f * f[(j - 1) % D];
                 if (c != c) continue;
-                atomicMin(&s_min[k * M + j], ((unsigned long long)f32_order_key(c) << 32) | s);
+                atomicMin(&s_min[k * M + j], tg | ((unsigned long long)f32_order_key(c) << 16) | s);
             }
         }
     }
@@ -189,14 +192,15 @@ __global__ __launch_bounds__(kThreads) void k_sample_min(const double *__restric
 template <int D>
 __global__ __launch_bounds__(64) void k_pick_pruners(const double *__restrict__ vals, uint32_t n, uint32_t S,
                                                      const unsigned long long *__restrict__ gmin, int M,
-                                                     double *__restrict__ pruners, int32_t *__restrict__ npr) {
+                                                     double *__restrict__ pruners, int32_t *__restrict__ npr,
+                                                     uint32_t tag) {
     __shared__ double s_c[64][D];
     __shared__ int s_ok[64];
     const int k = blockIdx.x, j = threadIdx.x;
     const unsigned long long w = j < M ? gmin[k * M + j] : ~0ull;
-    const bool has = w != ~0ull;
+    const bool has = (uint32_t)(w >> 48) == tag;       // (a word of an earlier query: empty)
     if (has) {
-        const uint32_t s = (uint32_t)(w & 0xffffffffu);
+        const uint32_t s = (uint32_t)(w & 0xffffu);
         const uint32_t i = (uint32_t)(((uint64_t)s * n) / S);
 #pragma unroll
         for (int d = 0; d < D; d++) s_c[j][d] = vals[(size_t)i * D + d];
@@ -376,10 +380,10 @@ __device__ __forceinline__ void load_pruners_lds(const FilterArgs &a, double *s_
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
         for (int k = wave; k < a.Kp; k += kThreads / 64) {
             const unsigned long long w = lane < a.M ? a.pick_gmin[k * a.M + lane] : ~0ull;
-            const bool has = w != ~0ull;
+            const bool has = (uint32_t)(w >> 48) == a.pick_tag;
             double c[D];
             if (has) {
-                const uint32_t i = (uint32_t)(((uint64_t)(uint32_t)(w & 0xffffffffu) * a.n) / a.pick_S);
+                const uint32_t i = (uint32_t)(((uint64_t)(uint32_t)(w & 0xffffu) * a.n) / a.pick_S);
 #pragma unroll
                 for (int d = 0; d < D; d++) c[d] = a.vals[(size_t)i * D + d];
             } else {
@@ -1300,11 +1304,21 @@ __global__ __launch_bounds__(kThreads) void k_rep_mult(uint32_t mt, const uint32
 // Stats (|L_k|, survivors_k) for unit weights and computed origins: every stream
 // tuple in L_k is a candidate (one slot, weight 1) or a duplicate of a pruner
 // (weight dup_cnt), so they are summed over slots here instead of over tuples.
+__device__ __forceinline__ uint32_t fate_from_domf(const FateArgs &a, uint32_t r) {
+    const uint32_t df = a.domf[r];
+    const bool in_l = !(df & 1u), in_g = a.gmerge ? !(df & 2u) : in_l;
+    return (in_l ? 1u : 0u) | (in_g ? 2u : 0u);
+}
+
 __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
     __shared__ unsigned long long s_l[kMaxK], s_s[kMaxK];
-    const bool stats = a.lsz != nullptr;
-    if (stats) {
-        for (int q = threadIdx.x; q < a.K; q += kThreads) { s_l[q] = 0; s_s[q] = 0; }
+    __shared__ uint32_t s_n[kMaxK], s_a[kMaxK];
+    const bool stats = a.lsz != nullptr, fin = a.domf != nullptr;
+    if (stats || fin) {
+        if (stats)
+            for (int q = threadIdx.x; q < a.K; q += kThreads) { s_l[q] = 0; s_s[q] = 0; }
+        if (fin)
+            for (int q = threadIdx.x; q < kMaxK; q += kThreads) { s_n[q] = 0; s_a[q] = 0; }
         __syncthreads();
     }
     const uint32_t j = blockIdx.x * kThreads + threadIdx.x;
@@ -1314,10 +1328,23 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
     unsigned long long w = 0;
     uint32_t f = 0;
     if (j < a.mt) {
+        if (fin && j < mtd) {                          // k_brute_finish's outputs for slot j
+            const uint32_t fj = fate_from_domf(a, j);
+            const uint32_t kk = (uint32_t)(a.key[j] >> 56);
+            a.alive_l_w[j] = (uint8_t)(fj & 1u);
+            a.alive_g_w[j] = (uint8_t)(fj >> 1);
+            a.slot_rep_w[j] = j;
+            atomicAdd(&s_n[kk], 1u);
+            if (fj & 1u) atomicAdd(&s_a[kk], 1u);
+        }
         const uint32_t src = j < mtd ? a.slot_src[j] : 0x80000000u;
         if (!(src & 0x80000000u)) {                    // (appended pruner slots: below)
-            const uint32_t r = a.slot_rep[j];
-            f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            if (fin) {
+                f = fate_from_domf(a, j);
+            } else {
+                const uint32_t r = a.slot_rep[j];
+                f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            }
             const uint16_t s0 = a.status[src];
             a.status[src] = (uint16_t)((s0 & 0xff00u) | (kCodeFate0 + f));
             cand_tile = (f & 2u) ? src / kTile : 0xffffffffu;
@@ -1328,8 +1355,12 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
         const uint32_t q = j - a.mt;
         const int32_t ps = a.pruner_slot[q];
         if (ps >= 0 && (uint32_t)ps < mtd) {
-            const uint32_t r = a.slot_rep[ps];
-            f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            if (fin) {
+                f = fate_from_domf(a, (uint32_t)ps);
+            } else {
+                const uint32_t r = a.slot_rep[ps];
+                f = (a.alive_l[r] ? 1u : 0u) | (a.alive_g[r] ? 2u : 0u);
+            }
             k = (int)(q / (uint32_t)a.M);
             w = stats ? a.dup_cnt[q] : 0u;
         }
@@ -1347,18 +1378,23 @@ __global__ __launch_bounds__(kThreads) void k_fate_tables(FateArgs a) {
             pend &= ~same;
         }
     }
+    if (stats && k >= 0 && (f & 1u)) {
+        atomicAdd(&s_l[k], w);
+        if (f & 2u) atomicAdd(&s_s[k], w);
+    }
+    if (stats || fin) __syncthreads();
     if (stats) {
-        if (k >= 0 && (f & 1u)) {
-            atomicAdd(&s_l[k], w);
-            if (f & 2u) atomicAdd(&s_s[k], w);
-        }
-        __syncthreads();
         const size_t sh = (size_t)(blockIdx.x % kStatShards) * a.K;
         for (int q = threadIdx.x; q < a.K; q += kThreads) {
             if (s_l[q]) atomicAdd(&a.lsz[sh + q], s_l[q]);
             if (s_s[q]) atomicAdd(&a.surv[sh + q], s_s[q]);
         }
     }
+    if (fin)
+        for (int q = threadIdx.x; q < kMaxK; q += kThreads) {
+            if (s_n[q]) atomicAdd(&a.segn[q], s_n[q]);
+            if (s_a[q]) atomicAdd(&a.segalive[q], s_a[q]);
+        }
 }
 
 // fate of one tuple from its status word (candidates: after k_fate_tables), branch
@@ -1888,15 +1924,18 @@ void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int
 
 void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
-                           double *pruners, int32_t *npr, hipStream_t st, bool pick) {
-    if (S == 0) return;                               // gmin: all-ones on entry (the caller's fill)
+                           double *pruners, int32_t *npr, hipStream_t st, bool pick, uint32_t tag,
+                           const FillRanges *pre) {
+    if (S == 0) return;                               // (S <= 65536: 16-bit sample ids)
     static const unsigned sgrid = [] {        // SKY_SAMPLE_WG: workgroups of the sample pass (A/B knob)
         const char *e = SKY_MEASURE_ENV("SKY_SAMPLE_WG");
         return e ? (unsigned)std::max(1, atoi(e)) : 256u;   // 32: +20 us, 64: +2 us (latency-bound per row)
     }();
     const unsigned g = std::min<unsigned>(nblk(S, kThreads), sgrid);
-    SKY_DISPATCH_D(D, (k_sample_min<DD><<<g, kThreads, 0, st>>>(vals, n, S, kp, given_keys, single, Kp, M, gmin)));
-    if (pick) SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr)));
+    const FillRanges none{};
+    const FillRanges &f = pre ? *pre : none;
+    SKY_DISPATCH_D(D, (k_sample_min<DD><<<g, kThreads, 0, st>>>(vals, n, S, kp, given_keys, single, Kp, M, gmin, tag, f)));
+    if (pick) SKY_DISPATCH_D(D, (k_pick_pruners<DD><<<Kp, 64, 0, st>>>(vals, n, S, gmin, M, pruners, npr, tag)));
 }
 
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
@@ -1991,6 +2030,11 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     constexpr int TU = 16 / DP > 0 ? 16 / DP : 1;                 // slot rows per thread and batch
     uint32_t lflags = 0;
     TINY_CLK(0);
+    // round 0's criterion minima (k_cand_min over the whole GPU), fetched with the first round trip
+    constexpr int MS0 = kTinyM2 + 1;
+    const bool cm0_pre = a.cmin0 && Kp * MS0 <= NT;
+    const unsigned long long cm0 = cm0_pre && tid < Kp * MS0 && tid % MS0 < kTinyM2
+                                       ? a.cmin0[(tid / MS0) * kTinyM2 + tid % MS0] : ~0ull;
 
     // ---- 1. one slot per duplicated pruner (k_append_pruners)
     const uint32_t m = *ap.m_total;
@@ -2003,6 +2047,8 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
     for (int q0 = 0; q0 < KM; q0 += NT) {
         const int q = q0 + tid;
         const uint32_t dc = q < KM ? ap.dup_cnt[q] : 0u;
+        double prow[D];                          // the pruner's row, loaded with its count
+        load_row<D>(ap.pruners + (size_t)min(q, KM - 1) * D, prow);
         const bool has = dc > 0;
         if (q < KM) s_dupc[q] = dc;
         uint32_t tot;
@@ -2014,8 +2060,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
             s_ps[q] = (int32_t)slot;
             if (slot < ap.slot_cap && TINY_OK(slot, a.cap[0], 0)) {
                 ap.slot_src[slot] = 0x80000000u | e;
-                const uint64_t key = emit_pruner<double, D>(ap.pruners + (size_t)q * D, q / M, (double *)ap.rows, slot,
-                                                            ap.sortkey, lflags);
+                const uint64_t key = emit_pruner<double, D>(prow, q / M, (double *)ap.rows, slot, ap.sortkey, lflags);
                 o |= key;
                 an &= key;
             }
@@ -2065,6 +2110,10 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
         float *s_wt = reinterpret_cast<float *>(s_min + ncopy * Kp * MS);                   // [M2][D]
         double *s_pr = reinterpret_cast<double *>(s_wt + ((M2 * D + 3) & ~3));             // [Kp][PS]
         unsigned long long *s_minw = s_min + (ncopy > 1 ? wave * Kp * MS : 0);
+        if (r == 0 && cm0_pre) {                 // the minima prefetched above: no pass, no merge
+            for (int q = tid; q < Kp * MS; q += NT) s_min[q] = cm0;
+            __syncthreads();
+        } else {
         for (int q = tid; q < ncopy * Kp * MS; q += NT) s_min[q] = ~0ull;
         for (int q = tid; q < M2 * D; q += NT) s_wt[q] = cand_weight(q / D, q % D, D);
         __syncthreads();
@@ -2132,6 +2181,7 @@ __global__ __launch_bounds__(kTinyThreads) void k_tiny_tail(TinyArgs a) {
                 s_min[q] = mn;
             }
             __syncthreads();
+        }
         }
         TINY_CLK(2);
         // k_cand_pick: one wave per partition, winners deduplicated and mutually non-dominated

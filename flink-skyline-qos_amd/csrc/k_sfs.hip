@@ -350,6 +350,13 @@ static void launch_fill_ranges(const FillRanges &f, hipStream_t st) {
     k_fill_multi<<<dim3(gx, (unsigned)f.n), kThreads, 0, st>>>(f);
 }
 
+bool FillSet::take(FillRanges &out) {
+    if (!full.empty() || !plain.empty()) return false;
+    out = static_cast<const FillRanges &>(*this);
+    n = 0;
+    return true;
+}
+
 hipError_t FillSet::launch(hipStream_t st) {
     hipError_t e = hipSuccess;
     for (const FillRanges &f : full) launch_fill_ranges(f, st);

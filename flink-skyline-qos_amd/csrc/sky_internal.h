@@ -87,16 +87,24 @@ struct FilterArgs {
     // pick_gmin non-null replaces reading pruners / npr
     const unsigned long long *pick_gmin = nullptr;
     uint32_t pick_S = 0;
+    uint32_t pick_tag = 0;            // this query's sample-minima tag (k_sample_min)
     double *pruners_w = nullptr;
     int32_t *npr_w = nullptr;
 };
 void launch_filter_deferred(int D, const FilterArgs &a, hipStream_t st);
 void launch_keys(int D, const double *vals, uint32_t n, const KeyParams &kp, int32_t *keys, hipStream_t st);
 // pruners: per partition up to M (<= 64) distinct, mutually non-dominated sample tuples
-// (pick = false: only the sample minima; the filter picks them itself, FilterArgs.pick_gmin)
+// (pick = false: only the sample minima; the filter picks them itself, FilterArgs.pick_gmin).
+// The minima words are tagged, (tag << 48) | order-key(c) << 16 | sample id (S <= 65536): a
+// word of an earlier query (a larger tag) loses to any of this one and reads as empty, so the
+// words need no fill between queries (the caller fills them all-ones when the buffer is new and
+// when its 16-bit query count wraps).  pre: the query's other fills, done by the sample pass's
+// threads before their samples (one launch less; nullptr: the caller launched them)
+struct FillRanges;
 void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, const KeyParams &kp,
                            const int32_t *given_keys, int single, int Kp, int M, unsigned long long *gmin,
-                           double *pruners, int32_t *npr, hipStream_t st, bool pick = true);
+                           double *pruners, int32_t *npr, hipStream_t st, bool pick, uint32_t tag,
+                           const FillRanges *pre);
 void launch_filter(int D, const FilterArgs &a, hipStream_t st);
 
 struct AppendArgs {
@@ -128,6 +136,15 @@ struct FateArgs {
     unsigned long long *lsz, *surv;       // [kStatShards][K] stat shards, or nullptr: no stats
     uint32_t *tile_cand;                  // [tiles] zeroed: += candidates in G per tile (nullptr: not counted)
     const uint32_t *d_mt = nullptr;       // device slot count (mt is then its bound)
+    // the brute route's k_brute_finish folded in: fates from the pair pass's domination bits per
+    // slot (every slot its own representative), and the finish's outputs written here -- alive_l /
+    // alive_g / slot_rep per slot, per-partition slot / local-skyline counts (zeroed); nullptr: the
+    // finish ran and the fates come from alive_l / alive_g / slot_rep
+    const uint32_t *domf = nullptr;
+    const uint64_t *key = nullptr;        // slot sort keys (partition in bits 63..56)
+    int gmerge = 0;
+    uint8_t *alive_l_w = nullptr, *alive_g_w = nullptr;
+    uint32_t *slot_rep_w = nullptr, *segalive = nullptr, *segn = nullptr;
 };
 void launch_fate_tables(const FateArgs &a, hipStream_t st);
 
@@ -277,7 +294,25 @@ struct FillSet : FillRanges {
     std::vector<std::pair<std::pair<void *, size_t>, int>> plain;   // unaligned: hipMemsetAsync
     void add(void *ptr, size_t nbytes, int value = 0);
     hipError_t launch(hipStream_t st);
+    // the pending ranges as ONE kernel argument for another kernel to fill (cleared here, nothing
+    // launched); false (nothing taken) when they need more than one batch or a hipMemsetAsync
+    bool take(FillRanges &out);
 };
+// a kernel's grid-wide share of k_fill_multi's work (every thread of the grid calls it)
+__device__ inline void fill_ranges_grid(const FillRanges &f) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, T = gridDim.x * blockDim.x;
+#pragma unroll
+    for (int j = 0; j < kFillMax; j++) {           // (compile-time indices into the argument)
+        if (j >= f.n) break;
+        uint8_t *p = f.p[j];
+        const uint32_t bytes = f.bytes[j], val = f.val[j];
+        const uint32_t words = bytes >> 2, w4 = val * 0x01010101u;
+        uint32_t *p4 = reinterpret_cast<uint32_t *>(p);
+        for (uint32_t q = t; q < words; q += T) p4[q] = w4;
+        if (t < (bytes & 3u)) p[words * 4 + t] = (uint8_t)val;
+    }
+}
+
 // ranges g.p[j] (g.bytes[j] bytes, 4-aligned) copied to pinned_dst + g.val[j] in one launch
 hipError_t launch_gather_words(const FillRanges &g, void *pinned_dst, hipStream_t st);
 void launch_global_keys(const uint64_t *rep_key, const uint8_t *alive_l, const uint32_t *alive_scan, uint32_t mr,

@@ -241,6 +241,26 @@ def test_out_epilogue_equals_launches(gpu_engine_factory, oracle, algo, dist, D,
             del os.environ["SKY_OUT_EPILOGUE"]
 
 
+@pytest.mark.parametrize("algo,dist,D,n,P", [("mr-angle", 0, 5, 200000, 16), ("mr-grid", 1, 4, 2500000, 8)])
+def test_finish_fold_equals_launch(gpu_engine_factory, oracle, algo, dist, D, n, P):
+    """The planned brute route's finish (alive flags, per-partition counts) inside k_fate_tables
+    (default) and as its own k_brute_finish launch (SKY_FINISH_FOLD=0): the oracle's ids, origins and
+    stats either way, on the planned route."""
+    short = algo.split("-")[1]
+    for knob in ("1", "0"):
+        os.environ["SKY_FINISH_FOLD"] = knob
+        try:
+            eng = gpu_engine_factory(D, P, algo)
+            # (seed 141 -> 142 is a genuine plan miss at this shape: 34 % more slots than learned)
+            check(eng, oracle, oracle.synth(dist, D, n, seed=131), P, short)
+            r, _ = check(eng, oracle, oracle.synth(dist, D, n, seed=132), P, short)
+            assert r & PLANNED
+            check(eng, oracle, oracle.synth(dist, D, n, seed=142), P, short)   # (planned or a miss)
+            eng.close()
+        finally:
+            del os.environ["SKY_FINISH_FOLD"]
+
+
 MEASURE_LIB = os.path.join(__import__("conftest").PKG, "build_measure", "libskyline_hip.so")
 _TINY_CAP_CHILD = r"""
 import os, sys, numpy as np
@@ -261,6 +281,59 @@ os.environ["SKY_TINY"] = "0"                   # the same context still answers 
 got = eng.query(vals, ids)[0]
 print("AFTER", int(np.array_equal(got, ref)), flush=True)
 """
+
+
+_EPOCH_CHILD = r"""
+import hashlib, os, sys
+sys.path.insert(0, sys.argv[1])
+import skyline
+eng = skyline.SkylineEngine(2, 8, "mr-dim", 1000.0, 0)
+for dist, n, seed in [("uniform", 200000, 1), ("anti_correlated", 200000, 2), ("uniform", 17000000, 3),
+                      ("correlated", 200000, 4), ("uniform", 200000, 5), ("uniform", 17000000, 6), ("uniform", 300000, 7)]:
+    vals, ids = skyline.synth_host(dist, 2, n, seed=seed)
+    got = eng.query(vals, ids)[0]
+    print(hashlib.sha1(got.tobytes()).hexdigest(), flush=True)
+"""
+
+
+def test_sample_minima_tags_across_the_wrap():
+    """The sample minima are tagged per query instead of filled (launch_select_pruners): a word of an
+    earlier query must read as empty.  The measurement build starts the 16-bit query count at 65533
+    (SKY_PMIN_EPOCH0), so the tags run 1, 0, then wrap (a fill) every two queries, over streams that pick
+    their pruners in the filter (200k) and in k_pick_pruners (17M); every answer must equal the product
+    build's with no wrap in sight."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    if not os.path.exists(MEASURE_LIB):
+        pytest.fail("build_measure/libskyline_hip.so missing: __graft_entry__.build() builds it")
+    outs = []
+    for lib, extra in ((MEASURE_LIB, {"SKY_PMIN_EPOCH0": "65533"}), (None, {})):
+        env = dict(os.environ, **extra)
+        if lib:
+            env["SKYLINE_HIP_LIB"] = lib
+        r = subprocess.run([sys.executable, "-c", _EPOCH_CHILD, PKG], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout.split())
+    assert len(outs[0]) == 7 and outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("algo,dist,D,n,P", [("mr-dim", 0, 2, 1000000, 8), ("mr-angle", 2, 8, 2500000, 16)])
+def test_fill_embed_equals_fill_launch(gpu_engine_factory, oracle, algo, dist, D, n, P):
+    """The query's zero / all-ones fills done by the sample pass's threads (default) or as their own
+    k_fill_multi launch (SKY_FILL_EMBED=0): the oracle's ids, origins and stats on the synchronised and
+    the planned route either way."""
+    short = algo.split("-")[1]
+    for knob in ("1", "0"):
+        os.environ["SKY_FILL_EMBED"] = knob
+        try:
+            eng = gpu_engine_factory(D, P, algo)
+            for seed in (151, 152, 153):
+                check(eng, oracle, oracle.synth(dist, D, n, seed=seed), P, short)
+            eng.close()
+        finally:
+            del os.environ["SKY_FILL_EMBED"]
 
 
 @pytest.mark.parametrize("capspec", ["0:4", "6:16"])

@@ -1,20 +1,11 @@
 #!/bin/bash
-# round-6 scratch GPU call 2: k_filter rows in flight per lane (PF 1 / 2) by stream size (measurement build)
-set -e
-export PYTHONUNBUFFERED=1
-cd ${GRAFT_REPO_ROOT:-.}
-O=gpurun_out
-ML=flink-skyline-qos_amd/build_measure/libskyline_hip.so
-timeout -k 10 60 tools/probe/valu_probe > $O/valu_probe_j.json 2>&1 && cat $O/valu_probe_j.json
-: > $O/pf_j.log
-for c in C1 C5T C3R C2 C4R C4H C3; do
-  for pf in 1 2; do
-    CFG=$c SKYLINE_HIP_LIB=$ML SKY_FILTER_PF=$pf timeout -k 10 120 python -u tools/small_query_ab.py >> $O/pf_j.log 2>&1 || { tail -20 $O/pf_j.log; exit 1; }
-  done
-done
-grep '^{' $O/pf_j.log | python3 -c "
-import sys, json
-for l in sys.stdin:
-    d = json.loads(l); k = d['kernel_mean_ms_profiled']
-    print(d['config'], 'pf', d['filter_pf'], 'wall', round(d['wall_p50_ms'], 4), 'c_entry', round(d['c_entry_p50_ms'], 4), 'filter_ms', round(k.get('filter', 0), 4))
-"
+# scratch GPU command (not part of the record)
+set -o pipefail
+OUT=gpurun_out; mkdir -p $OUT
+TAG=$1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_plan.py tests/test_gpu_configs.py tests/test_gpu_engine.py tests/test_gpu_stream.py -m gpu > $OUT/plan_$TAG.log 2>&1 || { tail -40 $OUT/plan_$TAG.log; exit 1; }
+tail -2 $OUT/plan_$TAG.log
+for i in 1 2; do CFG=C1 timeout -k 10 120 python -u tools/small_query_ab.py > $OUT/c1_${TAG}_$i.log 2>&1 || { tail -20 $OUT/c1_${TAG}_$i.log; exit 1; }
+grep '^{' $OUT/c1_${TAG}_$i.log | cut -c1-260; done
+timeout -k 10 500 python -u bench.py --no-cpu-baseline --no-dominance --no-csv --no-sort --no-e2e --no-operator > $OUT/bcfg_$TAG.json 2> $OUT/bcfg_$TAG.err || { tail -30 $OUT/bcfg_$TAG.err; exit 1; }
+python3 tools/bsum.py $OUT/bcfg_$TAG.json
