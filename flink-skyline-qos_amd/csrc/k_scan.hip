@@ -144,6 +144,86 @@ __global__ __launch_bounds__(kScanOneThreads) void k_scan_one(const uint32_t *__
     if (threadIdx.x == 0 && total_out) *total_out = tot;
 }
 
+// One tile per workgroup as k_scan_tile, its prefix from a decoupled look-back (wave 0 reads 64
+// earlier tiles' words per step; blockIdx order: every earlier workgroup was dispatched first on
+// its XCD).  Words: bits 63..34 epoch, 33..32 state (1 aggregate, 2 inclusive prefix), 31..0 count.
+__global__ __launch_bounds__(kScanThreads) void k_scan_lb(const uint32_t *__restrict__ in, size_t n,
+                                                          uint32_t *__restrict__ out, uint32_t *__restrict__ total_out,
+                                                          unsigned long long *__restrict__ lb, uint32_t epoch,
+                                                          uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_prefix;
+    const uint32_t b = blockIdx.x;
+    const size_t base = (size_t)b * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) { v[i] = base + i < n ? in[base + i] : 0u; s += v[i]; }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, s_w, total);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x & 63;
+        const unsigned long long tag = (unsigned long long)epoch << 34;
+        uint32_t excl = 0;
+        if (lane == 0)
+            __hip_atomic_store(lb + b, tag | ((b == 0 ? 2ull : 1ull) << 32) | total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (b > 0) {
+            int64_t end = (int64_t)b - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t idx = end - lane;
+                const unsigned long long w = idx >= 0 ? __hip_atomic_load(lb + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                      : (tag | (2ull << 32));
+                const uint32_t state = (w >> 34) == (unsigned long long)epoch ? (uint32_t)(w >> 32) & 3u : 0u;
+                const uint64_t inc = __ballot(state == 2u), zero = __ballot(state == 0u);
+                const int first = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1ull);
+                if (zero & upto) {
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0 && err) *err = 1u;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t c = lane <= first ? (uint32_t)w : 0u;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+                excl += c;
+                if (first < 64) break;
+                end -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(lb + b, tag | (2ull << 32) | (uint32_t)(excl + total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_prefix = excl;
+            if (b == gridDim.x - 1 && total_out) *total_out = excl + total;
+        }
+    }
+    __syncthreads();
+    run += s_prefix;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+}
+
+size_t scan_lb_words(size_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+void scan_excl_u32_lb(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, unsigned long long *lb,
+                      uint32_t epoch, uint32_t *err, hipStream_t st) {
+    const size_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (n == 0 || tiles == 1 || n <= kScanOneMax) {       // one workgroup: no look-back words needed
+        scan_excl_u32(in, out, n, d_total, nullptr, st);
+        return;
+    }
+    k_scan_lb<<<(unsigned)tiles, kScanThreads, 0, st>>>(in, n, out, d_total, lb, epoch, err);
+}
+
 // out[i] = sum(in[0..i)), *d_total = sum(in) ; `scratch` needs scan_scratch_words(n) words
 size_t scan_scratch_words(size_t n) {
     size_t tiles = (n + kScanTile - 1) / kScanTile;

@@ -38,6 +38,13 @@ size_t scan_scratch_words(size_t n);
 // d_n (optional): the item count on the device, n its bound
 void scan_excl_u32(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, uint32_t *scratch,
                    hipStream_t st, const uint32_t *d_n = nullptr);
+// the same in ONE launch above one workgroup's size (decoupled look-back over the earlier tiles
+// in blockIdx order, instead of reduce + partials + tiles): lb holds scan_lb_words(n) u64 words,
+// zeroed when allocated; epoch in [1, 2^30), larger than every earlier launch's on the same words
+// (their words then read as not yet published); a look-back past its spin bound sets *err = 1
+size_t scan_lb_words(size_t n);
+void scan_excl_u32_lb(const uint32_t *in, uint32_t *out, size_t n, uint32_t *d_total, unsigned long long *lb,
+                      uint32_t epoch, uint32_t *err, hipStream_t st);
 
 // ---- k_radix.hip ----
 size_t radix_scratch_words(size_t m);

@@ -264,6 +264,9 @@ struct sky_stream_landmark {
     sky::DevBuf tid, trep;                  // resident tuples (arrival order): capacity tcap
     sky::DevBuf rows2, key2, w2, tid2, trep2;   // the next state, swapped in after a query
     sky::DevBuf rowf, flag, pos, rflag, rpos, newrep, table, words, scratch;
+    sky::DevBuf lb;                         // the query's one-pass scans' look-back words (scan_excl_u32_lb)
+    const void *lb_at = nullptr;            // ... the buffer zeroed last, and the last scan's epoch
+    uint32_t lb_epoch = 0;
     int64_t R = 0, N = 0, T = 0, holes = 0;
     int64_t qcap = 0, tcap = 0;
 };
@@ -334,6 +337,24 @@ int lm_reserve(sky_stream *s, int64_t rows, int64_t tuples) {
     SKY_TRY(L.pos.ensure(tn * 4 + 64));
     SKY_TRY(L.scratch.ensure(sky::scan_scratch_words(tn + 1) * 4 + 64));
     SKY_TRY(L.words.ensure(256));
+    SKY_TRY(L.lb.ensure(sky::scan_lb_words(tn + 1) * 8));
+    if (L.lb.p != L.lb_at) {                  // new words: zeroed (no epoch yet), the error word too
+        HIP_TRY(hipMemsetAsync(L.lb.p, 0, L.lb.cap, c->st));
+        HIP_TRY(hipMemsetAsync(L.words.as<uint32_t>() + 6, 0, 4, c->st));
+        L.lb_at = L.lb.p;
+        L.lb_epoch = 0;
+    }
+    return SKY_OK;
+}
+
+// the next one-pass scan's epoch on the landmark's look-back words (re-zeroed at the 30-bit wrap)
+int lm_scan_epoch(sky_stream *s, uint32_t *epoch) {
+    sky_stream_landmark &L = *s->lm;
+    if (++L.lb_epoch >= (1u << 30)) {
+        HIP_TRY(hipMemsetAsync(L.lb.p, 0, L.lb.cap, s->ctx->st));
+        L.lb_epoch = 1;
+    }
+    *epoch = L.lb_epoch;
     return SKY_OK;
 }
 
@@ -475,7 +496,10 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     if (TN && (d_ids_out || d_origin_out)) {
         sky::k_ls_select<<<sky::nblk(TN), sky::kThreads, 0, st>>>(T, N, R, L.trep.as<uint32_t>(), L.rowf.as<uint8_t>(),
                                                                   2u, L.flag.as<uint32_t>());
-        sky::scan_excl_u32(L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), TN, w, L.scratch.as<uint32_t>(), st);
+        uint32_t ep = 0;
+        SKY_TRY(lm_scan_epoch(s, &ep));
+        sky::scan_excl_u32_lb(L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), TN, w, L.lb.as<unsigned long long>(), ep,
+                              w + 6, st);
         sky::k_ls_write_out<<<sky::nblk(TN), sky::kThreads, 0, st>>>(
             T, N, R, L.tid.as<int64_t>(), L.trep.as<uint32_t>(), L.qids.as<int64_t>(), L.qkey.as<int32_t>(),
             L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), cap, d_ids_out, d_origin_out);
@@ -490,7 +514,10 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     HIP_TRY(hipMemsetAsync(L.w2.p, 0, (size_t)(R + N) * 8, st));
     if (R) {
         sky::k_ls_rep_flag<<<sky::nblk(R), sky::kThreads, 0, st>>>(R, L.rowf.as<uint8_t>(), L.rflag.as<uint32_t>());
-        sky::scan_excl_u32(L.rflag.as<uint32_t>(), L.rpos.as<uint32_t>(), R, w + 1, L.scratch.as<uint32_t>(), st);
+        uint32_t ep = 0;
+        SKY_TRY(lm_scan_epoch(s, &ep));
+        sky::scan_excl_u32_lb(L.rflag.as<uint32_t>(), L.rpos.as<uint32_t>(), R, w + 1, L.lb.as<unsigned long long>(), ep,
+                              w + 6, st);
         sky::k_ls_rep_keep<<<sky::nblk(R), sky::kThreads, 0, st>>>(
             D, R, L.rflag.as<uint32_t>(), L.rpos.as<uint32_t>(), L.qrows.as<double>(), L.qkey.as<int32_t>(),
             L.qw.as<int64_t>(), L.rows2.as<double>(), L.key2.as<int32_t>(), L.w2.as<int64_t>(),
@@ -507,7 +534,10 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     if (TN) {
         sky::k_ls_select<<<sky::nblk(TN), sky::kThreads, 0, st>>>(T, N, R, L.trep.as<uint32_t>(), L.rowf.as<uint8_t>(),
                                                                   1u, L.flag.as<uint32_t>());
-        sky::scan_excl_u32(L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), TN, w + 3, L.scratch.as<uint32_t>(), st);
+        uint32_t ep = 0;
+        SKY_TRY(lm_scan_epoch(s, &ep));
+        sky::scan_excl_u32_lb(L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), TN, w + 3, L.lb.as<unsigned long long>(), ep,
+                              w + 6, st);
         sky::k_ls_tuples<<<sky::nblk(TN), sky::kThreads, 0, st>>>(
             T, N, R, L.tid.as<int64_t>(), L.trep.as<uint32_t>(), L.qids.as<int64_t>(), L.rpos.as<uint32_t>(),
             L.newrep.as<uint32_t>(), L.flag.as<uint32_t>(), L.pos.as<uint32_t>(), L.tid2.as<int64_t>(),
@@ -520,6 +550,11 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     c->host_syncs++;
     HIP_TRY(hipMemcpyAsync(h, w, 32, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (h[6]) {                             // a one-pass scan's look-back ran out of spins: no result
+        HIP_TRY(hipMemsetAsync(w + 6, 0, 4, st));
+        set_error("a look-back (stream scan) exceeded its spin bound");
+        return SKY_E_HIP;
+    }
     // swap in the next state: reps (with h[4] holes) [0, h[2]), tuples [0, h[3]), no new rows
     std::swap(L.qrows, L.rows2);
     std::swap(L.qkey, L.key2);
