@@ -54,6 +54,9 @@ struct PipeIn {
     int64_t *out_ids = nullptr;
     int32_t *out_org = nullptr;
     int64_t out_cap = 0;
+    // optional: per tuple its fate (bit 0 in L_k, bit 1 in G), written by the run's count pass when
+    // it has one (given origins / weights: the landmark stream's state update), else left untouched
+    uint8_t *row_flags = nullptr;
 };
 
 struct PhaseTimer;
@@ -96,6 +99,7 @@ struct Pipe {
     DevBuf lbuf;
     DevBuf tile_hist, tile_cand;      // per-tile duplicate histograms / surviving candidates (output counts)
     bool hist_count = false;
+    bool row_flags_done = false;      // the last run's count pass wrote PipeIn::row_flags
     // status planes (k_filter): B / E words per tile instead of a status word per tuple; the
     // designated duplicate group (B) is the largest group of the last run with the same shape
     DevBuf planes;

@@ -1033,11 +1033,14 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         c.ktimer_end("outw", st, n);
     } else {
         c.ktimer_begin("outc", st);
+        oa.row_flags = in.row_flags;           // (the same pass: no second one over the status words)
         launch_out_count(oa, st);
+        oa.row_flags = nullptr;
         c.ktimer_end("outc", st, n);
         scan_excl_u32(p.out_cnt.as<uint32_t>(), p.out_off.as<uint32_t>(), tiles, p.totals.as<uint32_t>() + 3,
                       p.scratch.as<uint32_t>(), st);
     }
+    p.row_flags_done = in.row_flags && !p.fused && in.fate;
     c.ktimer_end("out", st, n);
     STAGE(st, "fate");
     uint32_t nout = 0;
@@ -1547,6 +1550,7 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     p.n = n;
     p.K = in.K;
     p.last_planned = p.last_plan_miss = p.last_tiny = false;
+    p.row_flags_done = false;
     p.Kp = in.single ? 1 : c.Kq();
     p.M = std::max(1, std::min(8, 49152 / (p.Kp * D * 8)));
     p.m = p.nps = p.mt = p.mr = p.mg = p.nout = 0;

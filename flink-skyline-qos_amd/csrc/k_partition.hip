@@ -1941,15 +1941,20 @@ void launch_select_pruners(int D, const double *vals, uint32_t n, uint32_t S, co
 void launch_filter(int D, const FilterArgs &a, hipStream_t st) {
     const size_t lds = (D == 8 ? pruner_lds_bytes<8>(a.Kp, a.M) : (size_t)a.Kp * a.M * D * sizeof(double) + (size_t)a.Kp * a.M * 4) +
                        (size_t)(kFilterFT - 1) * a.Kp * a.M * 4;   // one duplicate-count array per output tile of a span
-    static const unsigned tpb = [] {           // tiles per workgroup (SKY_FILTER_TPB, A/B knob)
-        const char *e = SKY_MEASURE_ENV("SKY_FILTER_TPB");   // 4: -4 % filter time vs 1 (2: -3 %, 8: -3 %)
-        const int v = e ? atoi(e) : 4;
-        return (unsigned)std::max(1, std::min(v, 64));
+    static const int tpb_env = [] {            // tiles per workgroup (SKY_FILTER_TPB, A/B knob)
+        const char *e = SKY_MEASURE_ENV("SKY_FILTER_TPB");
+        return e ? std::max(1, std::min(atoi(e), 64)) : 0;
     }();
+    // 8D (C4): 4 tiles -4 % filter time vs 1 (2: -3 %, 8: -3 %); up to 4D (C3's 50M): 8 tiles -2.5 % vs 4
+    const unsigned tpb = tpb_env ? (unsigned)tpb_env : (D <= 4 ? 8u : 4u);
     const unsigned spans = nblk(a.n, kTile * kFilterFT);
+    static const unsigned minwg = [] {         // SKY_FILTER_MINWG: the grid's floor (A/B knob; 512 / 256
+        const char *e = SKY_MEASURE_ENV("SKY_FILTER_MINWG");   // measured no faster at C2-C4 sizes)
+        return e ? (unsigned)std::max(1, atoi(e)) : 1024u;
+    }();
     // several tiles per workgroup only while the grid still holds >= 1024 workgroups (4 per CU): a
     // 1M-tuple query (C1, a C5 trigger) has 489 tiles, which at 4 per workgroup left half the CUs idle
-    const unsigned tpe = std::max(1u, std::min(tpb, spans / 1024u));
+    const unsigned tpe = std::max(1u, std::min(tpb, spans / minwg));
     const unsigned g = (spans + tpe - 1) / tpe;
     if (!g) return;
     if (a.given_keys) { SKY_DISPATCH_D(D, (k_filter<DD, true><<<g, kThreads, lds, st>>>(a))); }

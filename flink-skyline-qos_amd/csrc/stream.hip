@@ -475,6 +475,7 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     in.weights = L.qw.as<int64_t>();
     in.global = true;
     in.K = c->Kq();
+    in.row_flags = L.rowf.as<uint8_t>();    // the per-row fates from the run's own count pass
     c->shard_valid = false;
     if (c->profile >= 2) {
         if (!c->pt.ok) c->pt.init();
@@ -487,7 +488,7 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
     *n_out = g;
     // the per-row fates (bit 0: in L_k, bit 1: in G)
     int64_t sel = 0;
-    if (R + N) {
+    if (R + N && !c->main.row_flags_done) {   // (the run's count pass wrote them: no pass of its own)
         SKY_TRY(pipe_output(*c, c->main, in, false, nullptr, nullptr, nullptr, 0, &sel, L.rowf.as<uint8_t>()));
     }
     uint32_t *w = L.words.as<uint32_t>();
