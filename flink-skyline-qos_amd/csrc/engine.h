@@ -151,6 +151,7 @@ struct Pipe {
 
     // results of the last run
     uint32_t n = 0, m = 0, nps = 0, mt = 0, mr = 0, mg = 0, nout = 0, mt_pre = 0;
+    uint32_t n_prev = 0, nout_prev = 0;   // the last completed run's tuples / output (the write pass's form)
     int M = 1, Kp = 1, K = 1;
     bool f64 = false, ties = false, u16 = false, ints = false;   // ints: every candidate value an integer in [0, 65535]
     std::vector<uint32_t> h_dup;

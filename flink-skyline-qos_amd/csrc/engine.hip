@@ -241,6 +241,10 @@ static bool epilogue_disabled() {   // SKY_OUT_EPILOGUE=0: k_stat_reduce + k_gat
     const char *e = SKY_ENV("SKY_OUT_EPILOGUE");
     return e && e[0] == '0';
 }
+static bool sparse_out_disabled() {   // SKY_SPARSE_OUT=0: the write pass always loads every id first (A/B knob)
+    const char *e = SKY_ENV("SKY_SPARSE_OUT");
+    return e && e[0] == '0';
+}
 static bool fill_embed_disabled() {   // SKY_FILL_EMBED=0: the query's fills as their own launch (A/B knob)
     const char *e = SKY_ENV("SKY_FILL_EMBED");
     return e && e[0] == '0';
@@ -1014,6 +1018,8 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         ow.planes = p.planes_on ? p.planes.as<uint64_t>() : nullptr;
         ow.dom_kj = p.dom_kj;
         ow.skip_flags = tiny ? p.flags.as<uint32_t>() : nullptr;
+        // a shape whose last run selected < 1/32 of its tuples: ids loaded by the selected lanes only
+        ow.sparse_ids = p.n_prev == n && (uint64_t)p.nout_prev * 32 < n && !sparse_out_disabled();
         if (ep) {
             SKY_TRY(p.statk.ensure((size_t)p.K * 16));
             SKY_TRY(p.pinned(tiny_pin_layout(p.K, p.Kp, KM, ow.ep_off)));
@@ -1175,6 +1181,8 @@ static int pipe_finish(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm, FillSe
         p.h_surv[k] = sk2[(size_t)p.K + k];
     }
     p.nout = nout;
+    p.n_prev = n;
+    p.nout_prev = nout;
     if (debug_level() >= 3) {
         fprintf(stderr, "[sky] run n=%u m=%u nps=%u mr=%u mg=%u nout=%u u16=%d seg_n:", n, p.m, p.nps, p.mr, p.mg,
                 nout, (int)p.u16);

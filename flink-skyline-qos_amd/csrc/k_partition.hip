@@ -1706,6 +1706,9 @@ __device__ __forceinline__ void out_epilogue(const OutArgs &a, uint32_t e) {
     for (int q = threadIdx.x; q < a.KM; q += kThreads) a.ep_pin[a.ep_off[4] + q] = a.ep_dup[q];
 }
 
+// SPARSE (OutArgs::sparse_ids: the last run selected < 1/32 of its tuples): the ids are loaded
+// after the selection, only by the selected lanes (C2 selects 0.13 %: the dense form read every id)
+template <bool SPARSE>
 __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     // after a one-workgroup tail that missed (or tripped its guard) no fate / offset is valid:
     // the caller's buffers are left untouched (the host re-runs the query or returns the error)
@@ -1732,12 +1735,14 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
     int64_t idv[kItems];
     // the id loads first: the status words are widened / packed as soon as they arrive, and
     // vmcnt waits in issue order, so ids issued after them would wait behind that
-    if (a.ids) {
+    if constexpr (!SPARSE) {
+        if (a.ids) {
 #pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];
-    } else {
+            for (int k = 0; k < kItems; k++) idv[k] = a.ids[min(i0 + k * kThreads, nl)];
+        } else {
 #pragma unroll
-        for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k * kThreads);
+            for (int k = 0; k < kItems; k++) idv[k] = (int64_t)(i0 + k * kThreads);
+        }
     }
     // status planes: the (item, wave) words are wave-uniform (scalar loads); a status word is
     // loaded only where the E bit says the filter stored one, the B bit stands for the
@@ -1779,6 +1784,13 @@ __global__ __launch_bounds__(kThreads) void k_out_write(OutArgs a) {
         const uint32_t f = in ? tuple_fate(st[k], s_pf, a.M) : 0u;
         msk[k] = __ballot((f >> shift) & 1u);
         if (lane == 0) s_cnt[k * (kThreads / 64) + wave] = (uint32_t)__popcll(msk[k]);
+    }
+    if constexpr (SPARSE) {
+#pragma unroll
+        for (int k = 0; k < kItems; k++) {
+            const uint32_t i = i0 + k * kThreads;             // (selected: i < n)
+            idv[k] = (msk[k] >> lane) & 1ull ? (a.ids ? a.ids[i] : (int64_t)i) : 0;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {                            // exclusive offsets of the 32 (k, wave) groups
@@ -2653,7 +2665,10 @@ void launch_out_hist_count(const uint32_t *hist, const uint32_t *tile_cand, cons
 }
 
 void launch_out_write(const OutArgs &a, hipStream_t st) {
-    if (a.n) k_out_write<<<nblk(a.n, kTile) + (a.ep_pin ? (uint32_t)a.K + 1u : 0u), kThreads, 0, st>>>(a);
+    if (!a.n) return;
+    const unsigned g = nblk(a.n, kTile) + (a.ep_pin ? (uint32_t)a.K + 1u : 0u);
+    if (a.sparse_ids) k_out_write<true><<<g, kThreads, 0, st>>>(a);
+    else k_out_write<false><<<g, kThreads, 0, st>>>(a);
 }
 // sky_profile_pairs_dev: caller rows -> the slot format of the brute pass (f64 rows padded to
 // 16 B, sort key = partition | f32 score | hash, as k_filter appends candidates)

@@ -240,6 +240,7 @@ struct OutArgs {
     const uint64_t *planes = nullptr;   // the filter's status planes (k_out_write only)
     int32_t dom_kj = -1;
     const uint32_t *skip_flags = nullptr;   // write pass: nothing is written if this word has a tail miss / guard bit
+    bool sparse_ids = false;                 // write pass: ids loaded after the selection, by selected lanes only
     // write pass: the brute route's final read folded in (k_stat_reduce + k_gather_words): K more
     // workgroups past the tiles reduce one stat key each, one more copies the other words, all into
     // host-mapped memory in tiny_pin_layout (ep_pin nullptr: no epilogue)

@@ -283,6 +283,32 @@ print("AFTER", int(np.array_equal(got, ref)), flush=True)
 """
 
 
+@pytest.mark.parametrize("algo,dist,D,n,P", [("mr-grid", 1, 4, 2500000, 8), ("mr-dim", 0, 2, 1000000, 8)])
+def test_sparse_write_pass_equals_dense(gpu_engine_factory, oracle, algo, dist, D, n, P):
+    """After a run that selected < 1/32 of its tuples, the next run of the shape loads ids only in the
+    selected lanes of the write pass (default) or every id first (SKY_SPARSE_OUT=0): the oracle's ids,
+    origins and stats either way (the caller's ids here are not the tuple indices)."""
+    short = algo.split("-")[1]
+    for knob in ("1", "0"):
+        os.environ["SKY_SPARSE_OUT"] = knob
+        try:
+            eng = gpu_engine_factory(D, P, algo)
+            for seed in (131, 132, 133):
+                vals = oracle.synth(dist, D, n, seed=seed)
+                ids = np.arange(n, dtype=np.int64) * 7 + 1000
+                got, org = eng.query(vals, ids)
+                exp, keys, els, esv = oracle.query_sfs(short, vals, P)
+                np.testing.assert_array_equal(got, ids[exp])
+                np.testing.assert_array_equal(org, keys[exp])
+                ls, sv = eng.stats()
+                np.testing.assert_array_equal(ls, els)
+                np.testing.assert_array_equal(sv, esv)
+                assert len(exp) * 32 < n
+            eng.close()
+        finally:
+            del os.environ["SKY_SPARSE_OUT"]
+
+
 _EPOCH_CHILD = r"""
 import hashlib, os, sys
 sys.path.insert(0, sys.argv[1])
