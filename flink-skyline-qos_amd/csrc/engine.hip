@@ -166,10 +166,6 @@ static size_t slot_min() {
 constexpr uint32_t kPrefilterProbe = 16;  // a skipped prefilter is probed again every 16 queries
 constexpr uint32_t kTinyBlock = 16;       // plans learned without the one-workgroup tail after it missed
 constexpr uint32_t kPickInFilterMax = 16u << 20;   // tuples up to which the filter picks its own pruners
-// slots up to which a prefilter round's fused pass redoes the pick in every workgroup (four slots per
-// thread); beyond, one k_cand_pick launch and one slot per thread (C4's 241k slots: 236 four-slot
-// workgroups, one per CU, took 46 us against 39 us + 5 launches for the chain)
-constexpr uint32_t kCandFusedMax = 65536;
 constexpr uint32_t kTailTilesMax = 1024;        // tiles up to which the brute route's counts run as k_tail_counts
 constexpr int kPrefilterRounds = 3;   // fewer slots: the SFS runs in one small pass anyway
 static bool fused_disabled() {   // SKY_FUSED_OUT=0: count pass + scan + write pass (A/B knob)
@@ -227,10 +223,13 @@ static bool cand_fused_disabled() {   // SKY_CAND_FUSED=0: pick / filter / scan 
     return e && e[0] == '0';
 }
 // the fused prefilter pass's look-back words of each planned round: [tiles][u64] + a ticket word
-// above kCandFusedMax slots (or SKY_CAND_FUSED=2) the fused pass runs after one k_cand_pick
-static bool cand_picked(uint32_t bound) {
+// the fused pass after one k_cand_pick, one slot per thread (default), or redoing the pick in every
+// workgroup with four slots per thread (SKY_CAND_FUSED=1, A/B knob): the per-workgroup pick measured
+// slower at every size tried -- C4's 241k slots 46 vs 27 us, C2's 40k 28.5 vs 24.6, a 1M 6D trigger's
+// 29.7 vs 23.1 (with k_cand_min)
+static bool cand_picked(uint32_t) {
     const char *e = SKY_ENV("SKY_CAND_FUSED");
-    return bound > kCandFusedMax || (e && e[0] == '2');
+    return !(e && e[0] == '1');
 }
 static size_t cand_lb_bytes(uint32_t bound) { return (size_t)cand_fused_tiles(bound, cand_picked(bound)) * 8 + 64; }
 static bool tail_counts_disabled() {   // SKY_TAIL_COUNTS=0: hist counts / scan / stat reduce / gather launches (A/B knob)

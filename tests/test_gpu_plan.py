@@ -188,8 +188,9 @@ def test_tiny_tail_miss(gpu_engine_factory, oracle):
 
 def test_cand_fused_pass_equals_launch_chain(gpu_engine_factory, oracle):
     """The prefilter's pick / live test / scan / compaction as one launch with a decoupled look-back
-    (k_cand_fused, default), after one k_cand_pick with one slot per thread (SKY_CAND_FUSED=2, the
-    form above 64k slots) and as the launch chain (SKY_CAND_FUSED=0, read per query): both routes
+    (k_cand_fused) after one k_cand_pick with one slot per thread (default, SKY_CAND_FUSED=2), with the
+    pick redone in every workgroup (SKY_CAND_FUSED=1) and as the launch chain (SKY_CAND_FUSED=0, read per
+    query): both routes
     (synchronised, planned) give the oracle's answer on a stream with prefilter rounds."""
     for knob in ("1", "2", "0"):
         os.environ["SKY_CAND_FUSED"] = knob
