@@ -3,13 +3,27 @@
 set -o pipefail
 OUT=gpurun_out; mkdir -p $OUT
 TAG=$1
-timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_plan.py tests/test_gpu_engine.py tests/test_gpu_configs.py -m gpu > $OUT/st_$TAG.log 2>&1 || { tail -40 $OUT/st_$TAG.log; exit 1; }
-tail -2 $OUT/st_$TAG.log
-for C in C2 C1; do for k in 1 0; do SKY_SPARSE_OUT=$k CFG=$C timeout -k 10 120 python -u tools/small_query_ab.py > $OUT/sp_${TAG}_${C}_$k.log 2>&1 || exit 1
-python3 -c "
-import json
-d=json.loads([l for l in open('$OUT/sp_${TAG}_${C}_$k.log') if l.startswith('{')][-1])
-print('$C sparse=$k', 'entry_p50', round(d['c_entry_p50_ms'],4), {a: round(b,4) for a,b in d['kernel_mean_ms_profiled'].items()})"
-done; done
-timeout -k 10 500 python -u bench.py --no-cpu-baseline --no-dominance --no-csv --no-sort --no-e2e --no-operator --no-stream > $OUT/bcfg_$TAG.json 2> $OUT/bcfg_$TAG.err || { tail -30 $OUT/bcfg_$TAG.err; exit 1; }
-python3 tools/bsum.py $OUT/bcfg_$TAG.json
+export TMPDIR=/tmp
+rm -rf $OUT/c5tl_$TAG
+timeout -k 10 300 rocprofv3 --kernel-trace -f csv -d $OUT/c5tl_$TAG -o run -- python3 -u -c "
+import sys, time; sys.path.insert(0, 'flink-skyline-qos_amd')
+import numpy as np, skyline
+from skyline import _abi
+D, P, per, batch, trig = 6, 8, 1000000, 50000, 6
+vals, ids = skyline.synth_host(_abi.DISTS['mixed'], D, per * trig, seed=1240)
+eng = skyline.SkylineEngine(D, P, 'mr-angle', 1000.0, 0)
+eng.warmup()
+st = skyline.SkylineStream(eng, 0)
+st.reserve(per * trig)
+lat = []
+for t in range(trig):
+    for b0 in range(t * per, (t + 1) * per, batch):
+        st.append(ids[b0:b0 + batch], vals[b0:b0 + batch])
+    t0 = time.perf_counter(); st.query_async_host_view(); lat.append((time.perf_counter() - t0) * 1e3)
+    st.wait()
+print('latencies_ms', [round(x, 3) for x in lat])
+st.close(); eng.close()
+" > $OUT/c5tl_$TAG.log 2>&1 || { tail -30 $OUT/c5tl_$TAG.log; exit 1; }
+python3 tools/prof_summary.py timeline $OUT/c5tl_$TAG 60 > $OUT/c5tl_${TAG}.txt
+rm -rf $OUT/c5tl_$TAG
+grep latencies $OUT/c5tl_$TAG.log; tail -34 $OUT/c5tl_${TAG}.txt
