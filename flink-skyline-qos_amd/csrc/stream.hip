@@ -511,8 +511,12 @@ int lm_query(sky_stream *s, int64_t *d_ids_out, int32_t *d_origin_out, int64_t c
         while (h < 2u * (R + N)) h <<= 1;
         return h;
     }();
-    HIP_TRY(hipMemsetAsync(L.table.p, 0xff, (size_t)hcap * 8, st));
-    HIP_TRY(hipMemsetAsync(L.w2.p, 0, (size_t)(R + N) * 8, st));
+    {                                       // the hash table all-ones, the next weights zero: one launch
+        sky::FillSet fs;
+        fs.add(L.table.p, (size_t)hcap * 8, 0xff);
+        fs.add(L.w2.p, (size_t)(R + N) * 8, 0);
+        HIP_TRY(fs.launch(st));
+    }
     if (R) {
         sky::k_ls_rep_flag<<<sky::nblk(R), sky::kThreads, 0, st>>>(R, L.rowf.as<uint8_t>(), L.rflag.as<uint32_t>());
         uint32_t ep = 0;
