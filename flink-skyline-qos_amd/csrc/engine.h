@@ -69,7 +69,8 @@ struct Pipe {
     // pruners
     DevBuf pmin, pruners, npr, dup_cnt, pr_entries, pruner_slot;
     uint32_t pmin_epoch = 0;          // queries since pmin was filled all-ones (its words' tags)
-    const void *pmin_at = nullptr;    // ... and the buffer that fill was for
+    const void *pmin_at = nullptr;    // ... and the buffer that fill was for (address and capacity:
+    size_t pmin_cap = 0;              //     a regrown buffer may come back at the same address)
     // candidates (slot order) and sort
     DevBuf rows, sortkey, slot_src, perm, key_alt, val_alt, rows_sorted;
     DevBuf runflag, runscan, run_first, repof, repflag, repscan, rep_rows, rep_key, rep_of_sorted, slot_rep;

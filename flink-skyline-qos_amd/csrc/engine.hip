@@ -1615,10 +1615,11 @@ int pipe_run(Ctx &c, Pipe &p, const PipeIn &in, PhaseTimer *tm) {
     SKY_TRY(p.npr.ensure((size_t)p.Kp * 4));
     // the sample minima are tagged per query (launch_select_pruners): all-ones only for a new buffer
     // and when the 16-bit query count wraps
-    const bool pmin_reset = p.pmin.p != p.pmin_at || ((p.pmin_epoch + 1) & 0xffffu) == 0;
+    const bool pmin_reset = p.pmin.p != p.pmin_at || p.pmin.cap != p.pmin_cap || ((p.pmin_epoch + 1) & 0xffffu) == 0;
     if (pmin_reset) {
-        fill.add(p.pmin.p, (size_t)p.Kp * p.M * 8, 0xff);
+        fill.add(p.pmin.p, p.pmin.cap, 0xff);     // (the whole buffer: no word of an earlier use survives)
         p.pmin_at = p.pmin.p;
+        p.pmin_cap = p.pmin.cap;
         p.pmin_epoch = 0;
 #ifdef SKY_MEASURE
         if (const char *e = SKY_MEASURE_ENV("SKY_PMIN_EPOCH0")) p.pmin_epoch = (uint32_t)atoi(e) & 0xffffu;   // the wrap's test
